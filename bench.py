@@ -1,0 +1,173 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-3 1.3B pre-training tokens/sec under fleet data parallelism
+(BASELINE.json: "samples/sec/GPU ResNet-50 bf16 + tokens/sec GPT-3-1.3B fleet DP at 1/2/4/8 MI355X").
+
+    python bench.py --gpus N --steps K --warmup W            # N=1 runs in-process
+    torchrun --nproc-per-node N bench.py --gpus N ...         # driver launch for N>1
+
+Each step = forward + backward + AdamW update (fp32 master weights) of the full
+24-layer GPT-3 1.3B (hidden 2048, 16 heads, ffn 8192, vocab 50304, seq 2048) in
+bf16 on synthetic token ids; weak scaling (micro-batch per GPU fixed).
+``--model resnet50`` measures the ResNet-50 bf16 samples/sec config instead.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+BASELINE_METRIC = "samples/sec/GPU ResNet-50 bf16 + tokens/sec GPT-3-1.3B fleet DP at 1/2/4/8 MI355X"
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="gpt3-1.3b")
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = _args()
+    import torch
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd import distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_parallel_env()
+    rank = dist.get_rank()
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    paddle.set_device(f"gpu:{torch.cuda.current_device()}")
+    paddle.seed(1234 + rank)
+
+    if a.model.startswith("resnet"):
+        return bench_resnet(a, paddle, dist, world, rank)
+
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    cfg = gpt_config(a.model, max_position_embeddings=max(2048, a.seq_len), recompute=a.recompute)
+    model = GPTForPretraining(cfg)
+    model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, beta1=0.9, beta2=0.95, weight_decay=0.1,
+                                 parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0),
+                                 multi_precision=True)
+    if world > 1:
+        strategy = dist.fleet.DistributedStrategy() if hasattr(dist, "fleet") else None
+        if strategy is not None:
+            strategy.hybrid_configs = {"dp_degree": world, "mp_degree": 1, "pp_degree": 1}
+            dist.fleet.init(is_collective=True, strategy=strategy)
+            model = dist.fleet.distributed_model(model)
+            opt = dist.fleet.distributed_optimizer(opt)
+        else:
+            model = paddle.DataParallel(model)
+    B, S = a.micro_batch, a.seq_len
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(rank)
+    ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (B, S + 1), device="cuda", generator=gen))
+    inp, lab = ids[:, :-1], ids[:, 1:]
+    inp = paddle.Tensor(inp._t.contiguous())
+    lab = paddle.Tensor(lab._t.contiguous())
+
+    def step():
+        loss = model(inp, lab)
+        loss.backward()
+        opt.step()
+        opt.clear_grad(set_to_zero=False)
+        return loss
+
+    for _ in range(a.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / a.steps * 1000.0
+    tokens = B * S * world * a.steps
+    value = tokens / elapsed
+    if rank == 0:
+        n_params = sum(p._t.numel() for p in (model._layers if hasattr(model, "_layers") else model).parameters())
+        out = {
+            "metric": "tokens/sec GPT-3-1.3B fleet DP (bf16, whole job)",
+            "baseline_metric": BASELINE_METRIC,
+            "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (random token ids), random-init weights",
+            "config": {"model": "GPT-3-1.3B" if a.model == "gpt3-1.3b" else a.model, "global_batch": B * world,
+                       "seq_len": S, "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "n_params": n_params,
+                       "optimizer": "AdamW fp32-master", "final_loss": round(float(loss.item()), 4)},
+        }
+        print(json.dumps(out), flush=True)
+
+
+def bench_resnet(a, paddle, dist, world, rank):
+    import torch
+    from paddle_hackathon_amd.vision.models import resnet50
+    model = resnet50(data_format="NHWC")
+    model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
+    opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
+                                    weight_decay=paddle.regularizer.L2Decay(1e-4), multi_precision=True)
+    if world > 1:
+        model = paddle.DataParallel(model)
+    B = a.micro_batch if a.micro_batch != 8 else 256
+    x = paddle.to_tensor(torch.randn(B, 224, 224, 3, device="cuda").to(torch.bfloat16))
+    y = paddle.to_tensor(torch.randint(0, 1000, (B,), device="cuda"))
+
+    def step():
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            out = model(x)
+        loss = paddle.nn.functional.cross_entropy(out, y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad(set_to_zero=False)
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = B * world * a.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "samples/sec ResNet-50 bf16 (whole job)", "baseline_metric": BASELINE_METRIC,
+            "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic ImageNet-shaped, random-init weights",
+            "config": {"model": "ResNet-50", "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
+                       "layout": "NHWC", "samples_per_sec_per_gpu": round(value / world, 2)}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

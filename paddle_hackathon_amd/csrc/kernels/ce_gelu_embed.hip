@@ -1,0 +1,214 @@
+// Softmax-cross-entropy (hard labels), bias+GELU, and embedding gather for gfx950.
+//
+// softmax_ce: one 256-thread block per row, single pass with an online
+//   (max, sum-exp) pair per thread merged across the block — the logits row is
+//   read once in forward; backward re-reads it once and writes dlogits once.
+//   Reference: paddle/phi/kernels/gpu/cross_entropy_kernel.cu (hard-label path).
+// bias_gelu: 8-wide vectorised elementwise, exact erf GELU (or tanh approx).
+//   Reference: phi/kernels/gpu/gelu_kernel.cu, operators/fused/fused_dropout_act_bias.h.
+// embedding: one wave per output row, 16-byte vector row copies.
+//   Reference: phi/kernels/gpu/embedding_kernel.cu.
+#include "common.h"
+
+using namespace pha;
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                             float* __restrict__ loss, float* __restrict__ lse_out,
+                                                             int V, int ignore_index) {
+  const long row = blockIdx.x;
+  const T* xr = logits + row * (long)V;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    float v[8];
+    Vec8<T>::ld(xr + c, v);
+    float vm = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) vm = fmaxf(vm, v[i]);
+    const float nm = fmaxf(m, vm);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += __expf(v[i] - nm);
+    m = nm;
+    s = acc;
+  }
+  // merge (m, s) pairs across the wave, then across waves
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, om);
+    s = (nm == -INFINITY) ? 0.f : s * __expf(m - nm) + os * __expf(om - nm);
+    m = nm;
+  }
+  __shared__ float sm[4], ss[4];
+  if (lane == 0) { sm[wid] = m; ss[wid] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int i = 1; i < 4; ++i) {
+      const float nm = fmaxf(M, sm[i]);
+      S = S * __expf(M - nm) + ss[i] * __expf(sm[i] - nm);
+      M = nm;
+    }
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const long lab = labels[row];
+    if (lab == ignore_index || lab < 0 || lab >= V) {
+      loss[row] = 0.f;
+    } else {
+      loss[row] = lse - Cvt<T>::ld(xr, lab);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_ce_bwd_kernel(const float* __restrict__ gloss, const T* __restrict__ logits,
+                                                             const int64_t* __restrict__ labels, const float* __restrict__ lse,
+                                                             T* __restrict__ dx, int V, int ignore_index) {
+  const long row = blockIdx.x;
+  const long lab = labels[row];
+  const bool ign = (lab == ignore_index || lab < 0 || lab >= V);
+  const float g = ign ? 0.f : gloss[row];
+  const float l = lse[row];
+  const T* xr = logits + row * (long)V;
+  T* dr = dx + row * (long)V;
+  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+    float v[8], o[8];
+    Vec8<T>::ld(xr + c, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float p = __expf(v[i] - l);
+      o[i] = g * (p - ((c + i) == lab ? 1.f : 0.f));
+    }
+    Vec8<T>::st(dr + c, o);
+  }
+}
+
+__device__ __forceinline__ float gelu_f(float x, bool approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;  // sqrt(2/pi)
+    const float u = k * (x + 0.044715f * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+
+__device__ __forceinline__ float gelu_grad(float x, bool approx) {
+  if (approx) {
+    const float k = 0.7978845608028654f;
+    const float x2 = x * x;
+    const float u = k * (x + 0.044715f * x2 * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x2);
+  }
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ b, T* __restrict__ y,
+                                                            long n8, int H, bool approx) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8], o[8];
+    Vec8<T>::ld(x + i * 8, v);
+    if (b) {
+      float bv[8];
+      Vec8<T>::ld(b + (i * 8) % H, bv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += bv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = gelu_f(v[k], approx);
+    Vec8<T>::st(y + i * 8, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict__ gy, const T* __restrict__ x, const T* __restrict__ b,
+                                                            T* __restrict__ gx, long n8, int H, bool approx) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float v[8], g[8], o[8];
+    Vec8<T>::ld(x + i * 8, v);
+    Vec8<T>::ld(gy + i * 8, g);
+    if (b) {
+      float bv[8];
+      Vec8<T>::ld(b + (i * 8) % H, bv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += bv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = g[k] * gelu_grad(v[k], approx);
+    Vec8<T>::st(gx + i * 8, o);
+  }
+}
+
+// one wave per output row; row bytes multiple of 16
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const uint4* __restrict__ w,
+                                                            uint4* __restrict__ out, long rows, int row_vecs, long vocab) {
+  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  long id = ids[r];
+  uint4* dst = out + r * row_vecs;
+  if (id < 0 || id >= vocab) {
+    for (int c = lane; c < row_vecs; c += 64) dst[c] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const uint4* src = w + id * row_vecs;
+  for (int c = lane; c < row_vecs; c += 64) dst[c] = src[c];
+}
+
+inline int grid_for(long n, int per_block) {
+  long g = (n + per_block - 1) / per_block;
+  if (g > 256L * 16) g = 256L * 16;   // grid-stride beyond ~16 blocks per CU
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+PHA_API int pha_softmax_ce_fwd(int dt, const void* logits, const int64_t* labels, float* loss, float* lse,
+                               long rows, int V, int ignore_index, hipStream_t stream) {
+  if (V % 8) return (int)hipErrorInvalidValue;
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((softmax_ce_fwd_kernel<T>), dim3(rows), dim3(256), 0, stream, (const T*)logits, labels, loss, lse, V, ignore_index);
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_softmax_ce_bwd(int dt, const float* gloss, const void* logits, const int64_t* labels, const float* lse,
+                               void* dx, long rows, int V, int ignore_index, hipStream_t stream) {
+  if (V % 8) return (int)hipErrorInvalidValue;
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((softmax_ce_bwd_kernel<T>), dim3(rows), dim3(256), 0, stream, gloss, (const T*)logits, labels, lse, (T*)dx, V, ignore_index);
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_bias_gelu_fwd(int dt, const void* x, const void* b, void* y, long n, int H, int approx, hipStream_t stream) {
+  if (n % 8 || (b && H % 8)) return (int)hipErrorInvalidValue;
+  const long n8 = n / 8;
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((bias_gelu_fwd_kernel<T>), dim3(grid_for(n8, 256)), dim3(256), 0, stream, (const T*)x, (const T*)b, (T*)y, n8, H, approx != 0);
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_bias_gelu_bwd(int dt, const void* gy, const void* x, const void* b, void* gx, long n, int H, int approx, hipStream_t stream) {
+  if (n % 8 || (b && H % 8)) return (int)hipErrorInvalidValue;
+  const long n8 = n / 8;
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(grid_for(n8, 256)), dim3(256), 0, stream, (const T*)gy, (const T*)x, (const T*)b, (T*)gx, n8, H, approx != 0);
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_embedding_fwd(const int64_t* ids, const void* w, void* out, long rows, int row_bytes, long vocab, hipStream_t stream) {
+  if (row_bytes % 16) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, ids, (const uint4*)w, (uint4*)out, rows, row_bytes / 16, vocab);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,340 @@
+// LayerNorm (fwd/bwd) and row softmax (fwd/bwd) for gfx950.
+//
+// Design: one wave64 per row. A row of H elements is split into NCH chunks of
+// 512 (64 lanes x 8 elements, one 16-byte vector per lane per chunk), held in
+// registers between the statistics pass and the output pass, so every element
+// is read from HBM exactly once and written once (memory-bound ops: the roof is
+// HBM bandwidth, Appendix B of the CDNA guide). 4 waves (4 rows) per 256-thread
+// block. Statistics in fp32, two-pass (exact) mean/variance from registers.
+//
+// Reference behaviour: paddle/phi/kernels/gpu/layer_norm_kernel.cu,
+// layer_norm_grad_kernel.cu, softmax_kernel.cu / gpudnn/softmax_gpudnn.h.
+#include "common.h"
+
+using namespace pha;
+
+namespace {
+
+constexpr int kWaves = 4;
+
+template <typename T, typename W, int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                     const W* __restrict__ b, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + (long)row * H;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      Vec8<T>::ld(xr + col, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = 0.f;
+    }
+  }
+  const float mu = wave_sum(s) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { float d = v[c][i] - mu; ss += d * d; }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / H + eps);
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+  T* yr = y + (long)row * H;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      float wv[8], bv[8], o[8];
+      Vec8<W>::ld(w + col, wv);
+      if (b) Vec8<W>::ld(b + col, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * rs * wv[i] + (b ? bv[i] : 0.f);
+      Vec8<T>::st(yr + col, o);
+    }
+  }
+}
+
+// dx per row + per-block partial column sums of dy*xhat (dw) and dy (db).
+template <typename T, typename W, int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const W* __restrict__ w, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, T* __restrict__ dx,
+                                                     float* __restrict__ part_w, float* __restrict__ part_b,
+                                                     int rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float aw[NCH][8], ab[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; }
+
+  for (int row = blockIdx.x * kWaves + wid; row < rows; row += gridDim.x * kWaves) {
+    const float mu = mean[row], rs = rstd[row];
+    const T* xr = x + (long)row * H;
+    const T* gr = dy + (long)row * H;
+    // pass 1: row statistics of g = dy*w (re-read in pass 2 from L1/L2 instead of
+    // holding x and g in registers: keeps VGPRs for the dw/db accumulators)
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        float xv[8], gv[8], wv[8];
+        Vec8<T>::ld(xr + col, xv);
+        Vec8<T>::ld(gr + col, gv);
+        Vec8<W>::ld(w + col, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float g = gv[i] * wv[i];
+          s1 += g * (xv[i] - mu) * rs;
+          s2 += g;
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / H, c2 = wave_sum(s2) / H;
+    T* dr = dx + (long)row * H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        float xv[8], gv[8], wv[8], o[8];
+        Vec8<T>::ld(xr + col, xv);
+        Vec8<T>::ld(gr + col, gv);
+        Vec8<W>::ld(w + col, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xh = (xv[i] - mu) * rs;
+          o[i] = rs * (gv[i] * wv[i] - xh * c1 - c2);
+          aw[c][i] += gv[i] * xh;
+          ab[c][i] += gv[i];
+        }
+        Vec8<T>::st(dr + col, o);
+      }
+    }
+  }
+  // block reduction of the 4 waves' partial column sums through LDS, one column chunk at a time
+  __shared__ float red[kWaves][512];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = pass == 0 ? aw[c][i] : ab[c][i];
+      __syncthreads();
+      // 256 threads reduce 512 columns: 2 columns per thread
+      for (int k = threadIdx.x; k < 512; k += 256) {
+        const int cc = c * 512 + k;
+        if (cc < H) {
+          float t = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+          float* dst = pass == 0 ? part_w : part_b;
+          dst[(long)blockIdx.x * H + cc] = t;
+        }
+      }
+      __syncthreads();
+      (void)col;
+    }
+  }
+}
+
+// sum partials [P, H] over P -> out [H] (cast to W)
+template <typename W>
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, W* __restrict__ out, int P, int H) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= H) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(long)p * H + col];
+  Cvt<W>::st(out, col, s);
+}
+
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + (long)row * H;
+  float v[NCH][8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      Vec8<T>::ld(xr + col, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m = fmaxf(m, v[c][i]);
+    }
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { v[c][i] = __expf(v[c][i] - m); s += v[c][i]; }
+    }
+  }
+  const float inv = 1.f / wave_sum(s);
+  T* yr = y + (long)row * H;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * inv;
+      Vec8<T>::st(yr + col, o);
+    }
+  }
+}
+
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx, int rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float yv[NCH][8], gv[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      Vec8<T>::ld(y + (long)row * H + col, yv[c]);
+      Vec8<T>::ld(dy + (long)row * H + col, gv[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += yv[c][i] * gv[c][i];
+    }
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 512 + lane * 8;
+    if (col < H) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = yv[c][i] * (gv[c][i] - s);
+      Vec8<T>::st(dx + (long)row * H + col, o);
+    }
+  }
+}
+
+template <typename F>
+int dispatch_nch_small(int H, F&& f) {
+  const int n = (H + 511) / 512;
+  switch (n) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: case 8: f(std::integral_constant<int, 8>{}); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename F>
+int dispatch_nch(int H, F&& f) {
+  const int n = (H + 511) / 512;
+  switch (n) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: case 10: case 11: case 12: f(std::integral_constant<int, 12>{}); break;
+    case 13: case 14: case 15: case 16: f(std::integral_constant<int, 16>{}); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
+                               float* mean, float* rstd, int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    if (wdt == kF32) {
+      rc = dispatch_nch(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_fwd_kernel<T, float, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)x, (const float*)w, (const float*)b, (T*)y, mean, rstd, rows, H, eps);
+      });
+    } else {
+      rc = dispatch_nch(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_fwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, H, eps);
+      });
+    }
+  });
+  return rc;
+}
+
+// part_w / part_b: workspace [nblocks, H] fp32 each; dw/db outputs (may be null db).
+PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, const void* w, const float* mean,
+                               const float* rstd, void* dx, void* dw, void* db, float* part_w, float* part_b,
+                               int nblocks, int rows, int H, hipStream_t stream) {
+  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid(nblocks), block(256);
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    if (wdt == kF32) {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
+      });
+      if (rc) return rc;
+      hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 255) / 256), dim3(256), 0, stream, part_w, (float*)dw, nblocks, H);
+      if (db) hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 255) / 256), dim3(256), 0, stream, part_b, (float*)db, nblocks, H);
+    } else {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
+      });
+      if (rc) return rc;
+      hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, stream, part_w, (T*)dw, nblocks, H);
+      if (db) hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, stream, part_b, (T*)db, nblocks, H);
+    }
+  });
+  return rc ? rc : (int)hipGetLastError();
+}
+
+PHA_API int pha_softmax_fwd(int dt, const void* x, void* y, int rows, int H, hipStream_t stream) {
+  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    rc = dispatch_nch(H, [&](auto nch) {
+      hipLaunchKernelGGL((softmax_fwd_kernel<T, decltype(nch)::value>), grid, block, 0, stream, (const T*)x, (T*)y, rows, H);
+    });
+  });
+  return rc;
+}
+
+PHA_API int pha_softmax_bwd(int dt, const void* dy, const void* y, void* dx, int rows, int H, hipStream_t stream) {
+  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    rc = dispatch_nch(H, [&](auto nch) {
+      hipLaunchKernelGGL((softmax_bwd_kernel<T, decltype(nch)::value>), grid, block, 0, stream, (const T*)dy, (const T*)y, (T*)dx, rows, H);
+    });
+  });
+  return rc;
+}

@@ -1,0 +1,180 @@
+// Multi-tensor optimizer kernels (Adam/AdamW, Momentum) and multi-tensor L2 norm.
+//
+// One launch updates every parameter of the model: the host packs a table of
+// TensorMeta records plus a chunk list (tensor index, chunk index); each
+// 256-thread block processes one CHUNK of one tensor. Master weights are fp32;
+// bf16/f16 params are re-materialised from the master in the same pass, so the
+// whole update is one read of (g, m, v, master) and one write of (m, v, master, p).
+// Reference: paddle/phi/kernels/gpu/adam_kernel.cu, adamw_kernel.cu,
+// merged_momentum_kernel.cu, fluid/operators/optimizers/*.
+#include "common.h"
+
+using namespace pha;
+
+namespace {
+
+constexpr int kChunk = 16384;
+constexpr int kILP = 4;
+
+struct TensorMeta {
+  void* p;        // param (dtype P)
+  const void* g;  // grad (dtype G)
+  float* m;       // first moment / velocity
+  float* v;       // second moment (adam)
+  float* master;  // fp32 master or null
+  long n;
+  float lr_ratio;
+  float wd;       // per-tensor weight decay coefficient
+};
+
+struct AdamArgs {
+  float lr, beta1, beta2, eps, bc1, bc2, grad_scale;
+  int decoupled;
+};
+
+template <typename P, typename G>
+__global__ __launch_bounds__(256) void adam_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks, AdamArgs a) {
+  const int2 ch = chunks[blockIdx.x];
+  const TensorMeta mt = metas[ch.x];
+  const long start = (long)ch.y * kChunk;
+  const long end = min(start + (long)kChunk, mt.n);
+  const float lr = a.lr * mt.lr_ratio;
+  const float sbc2 = sqrtf(a.bc2);
+  const float step = lr * sbc2 / a.bc1;
+  const float eps_hat = a.eps * sbc2;
+  P* p = (P*)mt.p;
+  const G* g = (const G*)mt.g;
+  float* master = mt.master;
+  for (long base = start + threadIdx.x; base < end; base += 256L * kILP) {
+    float gv[kILP], pv[kILP], mv[kILP], vv[kILP];
+#pragma unroll
+    for (int k = 0; k < kILP; ++k) {
+      const long i = base + (long)k * 256;
+      if (i < end) {
+        gv[k] = Cvt<G>::ld(g, i) * a.grad_scale;
+        pv[k] = master ? master[i] : Cvt<P>::ld(p, i);
+        mv[k] = mt.m[i];
+        vv[k] = mt.v[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kILP; ++k) {
+      const long i = base + (long)k * 256;
+      if (i < end) {
+        float gr = gv[k];
+        float pr = pv[k];
+        if (mt.wd != 0.f) {
+          if (a.decoupled) pr *= (1.f - lr * mt.wd);
+          else gr += mt.wd * pr;
+        }
+        const float m1 = a.beta1 * mv[k] + (1.f - a.beta1) * gr;
+        const float v1 = a.beta2 * vv[k] + (1.f - a.beta2) * gr * gr;
+        pr -= step * m1 / (sqrtf(v1) + eps_hat);
+        mt.m[i] = m1;
+        mt.v[i] = v1;
+        if (master) master[i] = pr;
+        Cvt<P>::st(p, i, pr);
+      }
+    }
+  }
+}
+
+struct MomArgs {
+  float lr, mu, grad_scale;
+  int nesterov;
+};
+
+template <typename P, typename G>
+__global__ __launch_bounds__(256) void momentum_kernel(const TensorMeta* __restrict__ metas, const int2* __restrict__ chunks, MomArgs a) {
+  const int2 ch = chunks[blockIdx.x];
+  const TensorMeta mt = metas[ch.x];
+  const long start = (long)ch.y * kChunk;
+  const long end = min(start + (long)kChunk, mt.n);
+  const float lr = a.lr * mt.lr_ratio;
+  P* p = (P*)mt.p;
+  const G* g = (const G*)mt.g;
+  for (long i = start + threadIdx.x; i < end; i += 256) {
+    float gr = Cvt<G>::ld(g, i) * a.grad_scale;
+    float pr = mt.master ? mt.master[i] : Cvt<P>::ld(p, i);
+    if (mt.wd != 0.f) gr += mt.wd * pr;
+    const float v1 = a.mu * mt.m[i] + gr;
+    mt.m[i] = v1;
+    pr -= a.nesterov ? lr * (gr + a.mu * v1) : lr * v1;
+    if (mt.master) mt.master[i] = pr;
+    Cvt<P>::st(p, i, pr);
+  }
+}
+
+struct NormMeta {
+  const void* x;
+  long n;
+  int dtype;
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void l2sq_partial_kernel(const NormMeta* __restrict__ metas, const int2* __restrict__ chunks, float* __restrict__ partial) {
+  const int2 ch = chunks[blockIdx.x];
+  const NormMeta mt = metas[ch.x];
+  const long start = (long)ch.y * kChunk;
+  const long end = min(start + (long)kChunk, mt.n);
+  float s = 0.f;
+  if (mt.dtype == kF32) {
+    const float* x = (const float*)mt.x;
+    for (long i = start + threadIdx.x; i < end; i += 256) { float v = x[i]; s += v * v; }
+  } else if (mt.dtype == kBF16) {
+    const bf16_t* x = (const bf16_t*)mt.x;
+    for (long i = start + threadIdx.x; i < end; i += 256) { float v = Cvt<bf16_t>::ld(x, i); s += v * v; }
+  } else {
+    const half_t* x = (const half_t*)mt.x;
+    for (long i = start + threadIdx.x; i < end; i += 256) { float v = Cvt<half_t>::ld(x, i); s += v * v; }
+  }
+  __shared__ float red[4];
+  s = block_reduce<false>(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int n, float* __restrict__ out) {
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += partial[i];
+  __shared__ float red[4];
+  s = block_reduce<false>(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+}  // namespace
+
+PHA_API int pha_chunk_size() { return kChunk; }
+PHA_API int pha_tensor_meta_size() { return (int)sizeof(TensorMeta); }
+
+PHA_API int pha_multi_tensor_adam(int pdt, int gdt, const void* metas, const void* chunks, int nchunks, float lr,
+                                  float beta1, float beta2, float eps, float bc1, float bc2, float grad_scale,
+                                  int decoupled, hipStream_t stream) {
+  if (nchunks <= 0) return 0;
+  AdamArgs a{lr, beta1, beta2, eps, bc1, bc2, grad_scale, decoupled};
+  PHA_DISPATCH_T(pdt, P, {
+    PHA_DISPATCH_T(gdt, G, {
+      hipLaunchKernelGGL((adam_kernel<P, G>), dim3(nchunks), dim3(256), 0, stream, (const TensorMeta*)metas, (const int2*)chunks, a);
+    });
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_multi_tensor_momentum(int pdt, int gdt, const void* metas, const void* chunks, int nchunks, float lr,
+                                      float mu, float grad_scale, int nesterov, hipStream_t stream) {
+  if (nchunks <= 0) return 0;
+  MomArgs a{lr, mu, grad_scale, nesterov};
+  PHA_DISPATCH_T(pdt, P, {
+    PHA_DISPATCH_T(gdt, G, {
+      hipLaunchKernelGGL((momentum_kernel<P, G>), dim3(nchunks), dim3(256), 0, stream, (const TensorMeta*)metas, (const int2*)chunks, a);
+    });
+  });
+  return (int)hipGetLastError();
+}
+
+// partial: workspace of nchunks floats; out: 1 float
+PHA_API int pha_multi_tensor_l2sq(const void* metas, const void* chunks, int nchunks, float* partial, float* out, hipStream_t stream) {
+  if (nchunks <= 0) return (int)hipMemsetAsync(out, 0, sizeof(float), stream);
+  hipLaunchKernelGGL(l2sq_partial_kernel, dim3(nchunks), dim3(256), 0, stream, (const NormMeta*)metas, (const int2*)chunks, partial);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, partial, nchunks, out);
+  return (int)hipGetLastError();
+}

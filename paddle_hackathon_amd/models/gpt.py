@@ -1,0 +1,216 @@
+"""GPT (GPT-3 family) for fleet training — the model behind the headline
+"tokens/sec GPT-3 1.3B" benchmark (reference usage: the fleet hybrid-parallel GPT
+tests, python/paddle/fluid/tests/unittests/hybrid_parallel_pp_transformer.py,
+and PaddleNLP/fleetx GPT whose parameter layout this follows).
+
+MI355X-first choices:
+  * pre-LN decoder; fused QKV projection (one [h, 3h] GEMM on hipBLASLt);
+  * attention = our MFMA flash-attention kernel on [B, S, H, D] (no S×S tensor);
+  * FFN = GEMM + fused bias-GELU HIP kernel + GEMM;
+  * LayerNorm = HIP wave-per-row kernel; loss = fused one-pass softmax-CE kernel
+    over the (tied-embedding) vocab logits;
+  * tensor parallel: QKV/FFN1 column-parallel, out/FFN2 row-parallel, vocab-parallel
+    embedding + parallel cross-entropy when ``tensor_parallel_degree > 1``;
+  * optional activation recompute per layer (``recompute=True``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from ..framework.core import Tensor, _wrap
+from .. import nn
+from ..nn import functional as F
+from ..nn import initializer as I
+from .. import ops as _ops
+
+
+@dataclass
+class GPTConfig:
+    vocab_size: int = 50304
+    hidden_size: int = 2048
+    num_layers: int = 24
+    num_heads: int = 16
+    ffn_hidden_size: int = 8192
+    max_position_embeddings: int = 2048
+    hidden_dropout: float = 0.0
+    attention_dropout: float = 0.0
+    initializer_range: float = 0.02
+    layer_norm_eps: float = 1e-5
+    tensor_parallel_degree: int = 1
+    recompute: bool = False
+    fuse_qkv: bool = True
+    tie_word_embeddings: bool = True
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_heads
+
+
+GPT_CONFIGS = {
+    "gpt3-125m": dict(hidden_size=768, num_layers=12, num_heads=12, ffn_hidden_size=3072),
+    "gpt3-350m": dict(hidden_size=1024, num_layers=24, num_heads=16, ffn_hidden_size=4096),
+    "gpt3-1.3b": dict(hidden_size=2048, num_layers=24, num_heads=16, ffn_hidden_size=8192),
+    "gpt3-2.7b": dict(hidden_size=2560, num_layers=32, num_heads=32, ffn_hidden_size=10240),
+    "gpt3-6.7b": dict(hidden_size=4096, num_layers=32, num_heads=32, ffn_hidden_size=16384),
+    "gpt3-13b": dict(hidden_size=5120, num_layers=40, num_heads=40, ffn_hidden_size=20480),
+    "gpt-tiny": dict(hidden_size=64, num_layers=2, num_heads=4, ffn_hidden_size=256, vocab_size=512,
+                     max_position_embeddings=128),
+}
+
+
+def gpt_config(name, **overrides):
+    d = dict(GPT_CONFIGS[name])
+    d.update(overrides)
+    return GPTConfig(**d)
+
+
+def _w_attr(cfg, scale=1.0):
+    return nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range * scale))
+
+
+class GPTAttention(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.cfg = cfg
+        h = cfg.hidden_size
+        tp = cfg.tensor_parallel_degree
+        self.num_heads = cfg.num_heads // tp
+        self.head_dim = cfg.head_dim
+        out_scale = 1.0 / math.sqrt(2.0 * cfg.num_layers)
+        if tp > 1:
+            from ..parallel.mp_layers import ColumnParallelLinear, RowParallelLinear
+            self.qkv_proj = ColumnParallelLinear(h, 3 * h, weight_attr=_w_attr(cfg), has_bias=True, gather_output=False)
+            self.out_proj = RowParallelLinear(h, h, weight_attr=_w_attr(cfg, out_scale), has_bias=True, input_is_parallel=True)
+        else:
+            self.qkv_proj = nn.Linear(h, 3 * h, weight_attr=_w_attr(cfg))
+            self.out_proj = nn.Linear(h, h, weight_attr=_w_attr(cfg, out_scale))
+
+    def forward(self, x):
+        B, S = x._t.shape[0], x._t.shape[1]
+        qkv = self.qkv_proj(x)._t.reshape(B, S, self.num_heads, 3 * self.head_dim)
+        q, k, v = qkv.split(self.head_dim, dim=-1)
+        drop = self.cfg.attention_dropout if self.training else 0.0
+        o = _ops.flash_attention(q, k, v, causal=True, dropout_p=drop, training=self.training)
+        o = o.reshape(B, S, self.num_heads * self.head_dim)
+        return self.out_proj(_wrap(o))
+
+
+class GPTMLP(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        h, f = cfg.hidden_size, cfg.ffn_hidden_size
+        out_scale = 1.0 / math.sqrt(2.0 * cfg.num_layers)
+        if cfg.tensor_parallel_degree > 1:
+            from ..parallel.mp_layers import ColumnParallelLinear, RowParallelLinear
+            self.linear1 = ColumnParallelLinear(h, f, weight_attr=_w_attr(cfg), has_bias=True, gather_output=False)
+            self.linear2 = RowParallelLinear(f, h, weight_attr=_w_attr(cfg, out_scale), has_bias=True, input_is_parallel=True)
+        else:
+            self.linear1 = nn.Linear(h, f, weight_attr=_w_attr(cfg))
+            self.linear2 = nn.Linear(f, h, weight_attr=_w_attr(cfg, out_scale))
+
+    def forward(self, x):
+        h = torch.matmul(x._t, self.linear1.weight._t)
+        h = _ops.bias_gelu(h, self.linear1.bias._t, approximate=True)
+        return self.linear2(_wrap(h))
+
+
+class GPTDecoderLayer(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.norm1 = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+        self.self_attn = GPTAttention(cfg)
+        self.norm2 = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+        self.mlp = GPTMLP(cfg)
+        self.dropout = cfg.hidden_dropout
+
+    def _drop(self, t):
+        return F.dropout(t, self.dropout, training=self.training) if self.dropout and self.training else t
+
+    def forward(self, x):
+        x = x + self._drop(self.self_attn(self.norm1(x)))
+        x = x + self._drop(self.mlp(self.norm2(x)))
+        return x
+
+
+class GPTEmbeddings(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        if cfg.tensor_parallel_degree > 1:
+            from ..parallel.mp_layers import VocabParallelEmbedding
+            self.word_embeddings = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, weight_attr=_w_attr(cfg))
+        else:
+            self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden_size, weight_attr=_w_attr(cfg))
+        self.position_embeddings = nn.Embedding(cfg.max_position_embeddings, cfg.hidden_size, weight_attr=_w_attr(cfg))
+        self.dropout = cfg.hidden_dropout
+
+    def forward(self, input_ids, position_ids=None):
+        S = input_ids._t.shape[-1]
+        if position_ids is None:
+            position_ids = _wrap(torch.arange(S, device=input_ids._t.device).unsqueeze(0))
+        x = self.word_embeddings(input_ids) + self.position_embeddings(position_ids)
+        if self.dropout and self.training:
+            x = F.dropout(x, self.dropout, training=True)
+        return x
+
+
+class GPTModel(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embeddings = GPTEmbeddings(cfg)
+        self.layers = nn.LayerList([GPTDecoderLayer(cfg) for _ in range(cfg.num_layers)])
+        self.final_norm = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+
+    def forward(self, input_ids, position_ids=None):
+        x = self.embeddings(input_ids, position_ids)
+        for layer in self.layers:
+            if self.cfg.recompute and self.training:
+                from ..parallel.recompute import recompute
+                x = recompute(layer, x)
+            else:
+                x = layer(x)
+        return self.final_norm(x)
+
+
+class GPTForPretraining(nn.Layer):
+    """Returns per-token logits (or the loss when labels are given)."""
+
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.gpt = GPTModel(cfg)
+
+    def logits(self, h):
+        w = self.gpt.embeddings.word_embeddings.weight
+        if self.cfg.tensor_parallel_degree > 1:
+            from ..parallel.mp_layers import _c_identity
+            h = _c_identity(h)
+        return _wrap(torch.matmul(h._t, w._t.t()))
+
+    def forward(self, input_ids, labels=None, loss_mask=None, position_ids=None):
+        h = self.gpt(input_ids, position_ids)
+        logits = self.logits(h)
+        if labels is None:
+            return logits
+        return gpt_pretraining_loss(logits, labels, loss_mask, self.cfg.tensor_parallel_degree)
+
+
+def gpt_pretraining_loss(logits, labels, loss_mask=None, tp_degree=1):
+    """GPTPretrainingCriterion: mean CE over masked tokens (fused one-pass HIP CE kernel)."""
+    if tp_degree > 1:
+        from ..parallel.mp_layers import parallel_cross_entropy
+        per_tok = parallel_cross_entropy(logits._t, labels._t)
+    else:
+        per_tok = _ops.softmax_cross_entropy(logits._t, labels._t)
+    if loss_mask is not None:
+        m = loss_mask._t.reshape(per_tok.shape).float()
+        return _wrap((per_tok * m).sum() / m.sum().clamp_min(1.0))
+    return _wrap(per_tok.mean())
+
+
+def gpt_1_3b(**kw):
+    return GPTForPretraining(gpt_config("gpt3-1.3b", **kw))

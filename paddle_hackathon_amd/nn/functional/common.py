@@ -1,0 +1,285 @@
+"""Common functional ops (reference: python/paddle/nn/functional/{common,input,extension,vision}.py)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as TF
+
+from ...framework.core import Tensor, _wrap, convert_dtype
+from ...framework.dispatch import register_ops
+from ...tensor._helpers import _int_list
+from ... import ops as _ops
+
+_w = _wrap
+
+__all__ = ["linear", "dropout", "dropout2d", "dropout3d", "alpha_dropout", "pad", "zeropad2d",
+           "interpolate", "upsample", "bilinear", "cosine_similarity", "unfold", "fold", "label_smooth",
+           "embedding", "one_hot", "class_center_sample", "diag_embed", "sequence_mask", "gather_tree",
+           "temporal_shift", "pixel_shuffle", "pixel_unshuffle", "channel_shuffle", "affine_grid",
+           "grid_sample", "normalize", "fused_matmul_bias", "linear_bias_gelu"]
+
+
+def _t(x):
+    return x._t if isinstance(x, Tensor) else x
+
+
+def linear(x, weight, bias=None, name=None):
+    """y = x @ W + b with Paddle's [in, out] weight layout (hipBLASLt GEMM + fused bias epilogue)."""
+    xt, wt = x._t, weight._t
+    if bias is not None and xt.dim() >= 2:
+        b = bias._t
+        out = torch.addmm(b, xt.reshape(-1, xt.shape[-1]), wt)
+        return _w(out.reshape(list(xt.shape[:-1]) + [wt.shape[-1]]))
+    out = torch.matmul(xt, wt)
+    if bias is not None:
+        out = out + bias._t
+    return _w(out)
+
+
+def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, name=None):
+    a, b = _t(x), _t(y)
+    if transpose_x:
+        a = a.transpose(-1, -2)
+    if transpose_y:
+        b = b.transpose(-1, -2)
+    out = torch.matmul(a, b)
+    if bias is not None:
+        out = out + _t(bias)
+    return _w(out)
+
+
+def linear_bias_gelu(x, weight, bias, approximate=False):
+    """gelu(x @ W + b): GEMM on hipBLASLt, bias+GELU fused in one HIP pass."""
+    xt = x._t
+    h = torch.matmul(xt, weight._t)
+    return _w(_ops.bias_gelu(h, bias._t, approximate))
+
+
+def dropout(x, p=0.5, axis=None, training=True, mode="upscale_in_train", name=None):
+    t = _t(x)
+    if isinstance(p, Tensor):
+        p = float(p._t.item())
+    if not training or p == 0.0:
+        if mode == "downscale_in_infer" and not training:
+            return _w(t * (1.0 - p))
+        return _w(t)
+    if p == 1.0:
+        return _w(torch.zeros_like(t))
+    if axis is not None:
+        axes = _int_list(axis)
+        shape = [t.shape[i] if i in [a % t.dim() for a in axes] else 1 for i in range(t.dim())]
+        mask = torch.empty(shape, device=t.device, dtype=t.dtype).bernoulli_(1 - p)
+        if mode == "upscale_in_train":
+            return _w(t * mask / (1 - p))
+        return _w(t * mask)
+    if mode == "upscale_in_train":
+        return _w(TF.dropout(t, p, True))
+    mask = torch.empty_like(t).bernoulli_(1 - p)
+    return _w(t * mask)
+
+
+def dropout2d(x, p=0.5, training=True, data_format="NCHW", name=None):
+    t = _t(x)
+    if data_format == "NHWC":
+        return _w(TF.dropout2d(t.permute(0, 3, 1, 2), p, training).permute(0, 2, 3, 1))
+    return _w(TF.dropout2d(t, p, training))
+
+
+def dropout3d(x, p=0.5, training=True, data_format="NCDHW", name=None):
+    t = _t(x)
+    if data_format == "NDHWC":
+        return _w(TF.dropout3d(t.permute(0, 4, 1, 2, 3), p, training).permute(0, 2, 3, 4, 1))
+    return _w(TF.dropout3d(t, p, training))
+
+
+def alpha_dropout(x, p=0.5, training=True, name=None):
+    return _w(TF.alpha_dropout(_t(x), p, training))
+
+
+def pad(x, pad, mode="constant", value=0.0, data_format="NCHW", name=None):
+    t = _t(x)
+    pads = _int_list(pad)
+    nd = t.dim()
+    if len(pads) == 2 * nd:
+        # paddle full-rank pad: [d0_before, d0_after, d1_before, ...]
+        tp = []
+        for i in reversed(range(nd)):
+            tp += [pads[2 * i], pads[2 * i + 1]]
+        return _w(TF.pad(t, tp, mode=mode, value=value) if mode == "constant" else TF.pad(t, tp, mode=mode))
+    channels_last = data_format in ("NHWC", "NLC", "NDHWC")
+    if channels_last:
+        t = t.movedim(-1, 1)
+    # paddle spatial pad order: [left, right, top, bottom, front, back] (last spatial dim first) — same as torch
+    if mode == "constant":
+        out = TF.pad(t, pads, mode="constant", value=value)
+    else:
+        out = TF.pad(t, pads, mode={"reflect": "reflect", "replicate": "replicate", "circular": "circular"}[mode])
+    if channels_last:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def zeropad2d(x, padding, data_format="NCHW", name=None):
+    return pad(x, padding, "constant", 0.0, data_format)
+
+
+def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=False, align_mode=0,
+                data_format="NCHW", name=None):
+    t = _t(x)
+    channels_last = data_format in ("NHWC", "NLC", "NDHWC")
+    if channels_last:
+        t = t.movedim(-1, 1)
+    if size is not None:
+        size = _int_list(size)
+    if isinstance(scale_factor, Tensor):
+        scale_factor = scale_factor._t.tolist()
+    m = mode.lower()
+    kw = {}
+    if m in ("linear", "bilinear", "bicubic", "trilinear"):
+        kw["align_corners"] = align_corners
+    out = TF.interpolate(t, size=size, scale_factor=scale_factor, mode=m, **kw)
+    if channels_last:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+upsample = interpolate
+
+
+def bilinear(x1, x2, weight, bias=None, name=None):
+    out = TF.bilinear(_t(x1), _t(x2), _t(weight), None if bias is None else _t(bias).reshape(-1))
+    return _w(out)
+
+
+def cosine_similarity(x1, x2, axis=1, eps=1e-8):
+    return _w(TF.cosine_similarity(_t(x1), _t(x2), axis, eps))
+
+
+def unfold(x, kernel_sizes, strides=1, paddings=0, dilations=1, name=None):
+    p = paddings
+    if isinstance(p, (list, tuple)) and len(p) == 4:
+        t = TF.pad(_t(x), [p[1], p[3], p[0], p[2]])
+        p = 0
+    else:
+        t = _t(x)
+    return _w(TF.unfold(t, kernel_sizes, dilations, p, strides))
+
+
+def fold(x, output_sizes, kernel_sizes, strides=1, paddings=0, dilations=1, name=None):
+    return _w(TF.fold(_t(x), output_sizes, kernel_sizes, dilations, paddings, strides))
+
+
+def label_smooth(label, prior_dist=None, epsilon=0.1, name=None):
+    t = _t(label)
+    k = t.shape[-1]
+    if prior_dist is not None:
+        return _w((1 - epsilon) * t + epsilon * _t(prior_dist))
+    return _w((1 - epsilon) * t + epsilon / k)
+
+
+def embedding(x, weight, padding_idx=None, sparse=False, name=None):
+    w = weight._t
+    if padding_idx is not None and padding_idx < 0:
+        padding_idx += w.shape[0]
+    return _w(_ops.embedding(_t(x), w, padding_idx, sparse))
+
+
+def one_hot(x, num_classes, name=None):
+    return _w(TF.one_hot(_t(x).long(), num_classes).float())
+
+
+def class_center_sample(label, num_classes, num_samples, group=None):
+    lab = _t(label)
+    pos = torch.unique(lab)
+    if pos.numel() < num_samples:
+        neg_mask = torch.ones(num_classes, dtype=torch.bool, device=lab.device)
+        neg_mask[pos] = False
+        neg = torch.nonzero(neg_mask).reshape(-1)
+        neg = neg[torch.randperm(neg.numel(), device=lab.device)[: num_samples - pos.numel()]]
+        sampled = torch.sort(torch.cat([pos, neg])).values
+    else:
+        sampled = pos
+    remap = torch.full((num_classes,), -1, dtype=torch.int64, device=lab.device)
+    remap[sampled] = torch.arange(sampled.numel(), device=lab.device)
+    return _w(remap[lab]), _w(sampled)
+
+
+def diag_embed(input, offset=0, dim1=-2, dim2=-1):
+    return _w(torch.diag_embed(_t(input), offset, dim1, dim2))
+
+
+def sequence_mask(x, maxlen=None, dtype="int64", name=None):
+    t = _t(x)
+    if maxlen is None:
+        maxlen = int(t.max().item())
+    elif isinstance(maxlen, Tensor):
+        maxlen = int(maxlen._t.item())
+    r = torch.arange(maxlen, device=t.device)
+    return _w((r < t.unsqueeze(-1)).to(convert_dtype(dtype)))
+
+
+def gather_tree(ids, parents):
+    i, p = _t(ids), _t(parents)
+    T = i.shape[0]
+    out = torch.empty_like(i)
+    out[T - 1] = i[T - 1]
+    par = p[T - 1]
+    for t in range(T - 2, -1, -1):
+        out[t] = torch.gather(i[t], 1, par)
+        par = torch.gather(p[t], 1, par)
+    return _w(out)
+
+
+def temporal_shift(x, seg_num, shift_ratio=0.25, name=None, data_format="NCHW"):
+    t = _t(x)
+    if data_format == "NHWC":
+        t = t.permute(0, 3, 1, 2)
+    nt, c, h, w = t.shape
+    n = nt // seg_num
+    t5 = t.reshape(n, seg_num, c, h, w)
+    fold_ = int(c * shift_ratio)
+    out = torch.zeros_like(t5)
+    out[:, :-1, :fold_] = t5[:, 1:, :fold_]
+    out[:, 1:, fold_:2 * fold_] = t5[:, :-1, fold_:2 * fold_]
+    out[:, :, 2 * fold_:] = t5[:, :, 2 * fold_:]
+    out = out.reshape(nt, c, h, w)
+    if data_format == "NHWC":
+        out = out.permute(0, 2, 3, 1)
+    return _w(out)
+
+
+def pixel_shuffle(x, upscale_factor, data_format="NCHW", name=None):
+    t = _t(x)
+    if data_format == "NHWC":
+        return _w(TF.pixel_shuffle(t.permute(0, 3, 1, 2), upscale_factor).permute(0, 2, 3, 1))
+    return _w(TF.pixel_shuffle(t, upscale_factor))
+
+
+def pixel_unshuffle(x, downscale_factor, data_format="NCHW", name=None):
+    t = _t(x)
+    if data_format == "NHWC":
+        return _w(TF.pixel_unshuffle(t.permute(0, 3, 1, 2), downscale_factor).permute(0, 2, 3, 1))
+    return _w(TF.pixel_unshuffle(t, downscale_factor))
+
+
+def channel_shuffle(x, groups, data_format="NCHW", name=None):
+    t = _t(x)
+    if data_format == "NHWC":
+        n, h, w, c = t.shape
+        return _w(t.reshape(n, h, w, groups, c // groups).transpose(3, 4).reshape(n, h, w, c))
+    return _w(TF.channel_shuffle(t, groups))
+
+
+def affine_grid(theta, out_shape, align_corners=True, name=None):
+    return _w(TF.affine_grid(_t(theta), _int_list(out_shape), align_corners=align_corners))
+
+
+def grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True, name=None):
+    return _w(TF.grid_sample(_t(x), _t(grid), mode=mode, padding_mode=padding_mode, align_corners=align_corners))
+
+
+def normalize(x, p=2, axis=1, epsilon=1e-12, name=None):
+    return _w(TF.normalize(_t(x), p, axis, epsilon))
+
+
+register_ops(globals(), __all__)

@@ -1,0 +1,142 @@
+"""Convolutions (reference: python/paddle/nn/functional/conv.py, phi/kernels/gpu/conv_*).
+
+Paddle layouts: weight [C_out, C_in/groups, *k] (transpose conv: [C_in, C_out/groups, *k]);
+``data_format`` NCHW or NHWC. NHWC inputs are viewed as NCHW tensors in
+channels-last memory format (no copies), which is the layout gfx950 conv
+kernels want.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as TF
+
+from ...framework.core import Tensor, _wrap
+from ...framework.dispatch import register_ops
+
+_w = _wrap
+
+__all__ = ["conv1d", "conv2d", "conv3d", "conv1d_transpose", "conv2d_transpose", "conv3d_transpose"]
+
+
+def _tup(v, n):
+    if isinstance(v, (list, tuple)):
+        v = [int(a) for a in v]
+        if len(v) == 1:
+            return v * n
+        return v
+    return [int(v)] * n
+
+
+def _padding(padding, n, k, stride, dilation, x_spatial):
+    """Paddle padding forms -> (torch_padding, pre_pad list or None)."""
+    if isinstance(padding, str):
+        p = padding.upper()
+        if p == "VALID":
+            return [0] * n, None
+        if p == "SAME":
+            pads = []
+            for i in range(n):
+                out = (x_spatial[i] + stride[i] - 1) // stride[i]
+                tot = max((out - 1) * stride[i] + (k[i] - 1) * dilation[i] + 1 - x_spatial[i], 0)
+                pads.append((tot // 2, tot - tot // 2))
+            if all(a == b for a, b in pads):
+                return [a for a, _ in pads], None
+            return [0] * n, pads
+        raise ValueError(padding)
+    if isinstance(padding, (list, tuple)):
+        padding = list(padding)
+        if len(padding) == n and all(isinstance(p, int) for p in padding):
+            return padding, None
+        if len(padding) == 2 * n and all(isinstance(p, int) for p in padding):
+            pads = [(padding[2 * i], padding[2 * i + 1]) for i in range(n)]
+            if all(a == b for a, b in pads):
+                return [a for a, _ in pads], None
+            return [0] * n, pads
+        if len(padding) == n + 2:  # [[0,0],[0,0],[a,b],...] forms
+            sp = [p for p in padding if list(p) != [0, 0]] if len(padding) else []
+            flat = [tuple(p) for p in padding]
+            spatial = flat[2:] if flat[1] == (0, 0) else flat[1:-1]
+            return _padding([v for pr in spatial for v in pr], n, k, stride, dilation, x_spatial)
+    return [int(padding)] * n, None
+
+
+def _to_ncx(t, data_format):
+    if data_format[-1] == "C" and len(data_format) > 2:
+        return t.movedim(-1, 1), True
+    return t, False
+
+
+def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
+    t = x._t
+    w = weight._t
+    t, cl = _to_ncx(t, data_format)
+    stride = _tup(stride, n)
+    dilation = _tup(dilation, n)
+    k = list(w.shape[2:])
+    pad, pre = _padding(padding, n, k, stride, dilation, list(t.shape[2:]))
+    if pre is not None:
+        fl = []
+        for a, b in reversed(pre):
+            fl += [a, b]
+        t = TF.pad(t, fl)
+    if cl and n == 2:
+        t = t.contiguous(memory_format=torch.channels_last) if not t.is_contiguous(memory_format=torch.channels_last) else t
+    f = {1: TF.conv1d, 2: TF.conv2d, 3: TF.conv3d}[n]
+    out = f(t, w, None if bias is None else bias._t, stride, pad, dilation, groups)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCL", name=None):
+    return _convnd(1, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
+    return _convnd(2, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
+    return _convnd(3, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def _convnd_t(n, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format):
+    t = x._t
+    w = weight._t
+    t, cl = _to_ncx(t, data_format)
+    stride = _tup(stride, n)
+    dilation = _tup(dilation, n)
+    k = list(w.shape[2:])
+    if isinstance(padding, str):
+        pad = [0] * n if padding.upper() == "VALID" else [((k[i] - 1) * dilation[i]) // 2 for i in range(n)]
+    else:
+        pad, pre = _padding(padding, n, k, stride, dilation, list(t.shape[2:]))
+    opad = _tup(output_padding, n)
+    if output_size is not None:
+        osz = _tup(output_size if not isinstance(output_size, Tensor) else output_size._t.tolist(), n)
+        for i in range(n):
+            base = (t.shape[2 + i] - 1) * stride[i] - 2 * pad[i] + dilation[i] * (k[i] - 1) + 1
+            opad[i] = osz[i] - base
+    f = {1: TF.conv_transpose1d, 2: TF.conv_transpose2d, 3: TF.conv_transpose3d}[n]
+    out = f(t, w, None if bias is None else bias._t, stride, pad, opad, groups, dilation)
+    if cl:
+        out = out.movedim(1, -1)
+    return _w(out)
+
+
+def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format="NCL", name=None):
+    return _convnd_t(1, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format)
+
+
+def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, dilation=1, groups=1,
+                     output_size=None, data_format="NCHW", name=None):
+    return _convnd_t(2, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format)
+
+
+def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format="NCDHW", name=None):
+    return _convnd_t(3, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format)
+
+
+register_ops(globals(), __all__)

@@ -1,0 +1,291 @@
+"""Fused hot ops: HIP kernels on gfx950, PyTorch reference path on CPU.
+
+Reference parity (what each op replaces in the reference):
+  * layer_norm       — phi/kernels/gpu/layer_norm_kernel.cu, layer_norm_grad_kernel.cu
+  * softmax          — phi/kernels/gpu/softmax_kernel.cu (gpudnn/softmax_gpudnn.h)
+  * softmax_cross_entropy — phi/kernels/gpu/cross_entropy_kernel.cu (softmax_with_cross_entropy)
+  * gelu / bias_gelu — phi/kernels/gpu/gelu_kernel.cu, operators/fused/fused_dropout_act_bias.h
+  * fused_adam_      — phi/kernels/gpu/adam_kernel.cu (+ multi_tensor_adam in fluid/operators/optimizers)
+  * fused_momentum_  — phi/kernels/gpu/merged_momentum_kernel.cu
+  * flash_attention  — operators/fused/fused_attention_op.cu, fmha_ref.h
+  * embedding        — phi/kernels/gpu/embedding_kernel.cu
+  * bias_dropout_residual_layer_norm — operators/fused/fused_bias_dropout_residual_layer_norm_op.cu
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as TF
+
+from . import _lib
+from . import hip as _hip
+
+_native = None
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    global _native
+    if not t.is_cuda:
+        return False
+    if _native is None:
+        _native = _lib.require_native()
+    return _native
+
+
+# ----------------------------------------------------------------------------
+# GELU / bias-GELU
+# ----------------------------------------------------------------------------
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b, approximate):
+        ctx.save_for_backward(x, b)
+        ctx.approximate = approximate
+        return _hip.bias_gelu_fwd(x, b, approximate)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, b = ctx.saved_tensors
+        gx, gb = _hip.bias_gelu_bwd(gy.contiguous(), x, b, ctx.approximate)
+        return gx, gb, None
+
+
+def gelu(x, approximate=False):
+    if _use_hip(x) and x.dtype in (torch.bfloat16, torch.float32, torch.float16) and x.is_contiguous():
+        return _BiasGelu.apply(x, None, bool(approximate))
+    return TF.gelu(x, approximate="tanh" if approximate else "none")
+
+
+def bias_gelu(x, b, approximate=False):
+    """gelu(x + b) with b broadcast over the last dim."""
+    if _use_hip(x) and x.dtype in (torch.bfloat16, torch.float32, torch.float16) and x.is_contiguous() and b.dim() == 1 and b.dtype == x.dtype:
+        return _BiasGelu.apply(x, b, bool(approximate))
+    return TF.gelu(x + b, approximate="tanh" if approximate else "none")
+
+
+def add_relu(x, y):
+    return torch.relu(x + y)
+
+
+# ----------------------------------------------------------------------------
+# softmax
+# ----------------------------------------------------------------------------
+class _Softmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = _hip.softmax_fwd(x)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        return _hip.softmax_bwd(gy.contiguous(), y)
+
+
+def softmax(x, axis=-1):
+    if axis in (-1, x.dim() - 1) and _use_hip(x) and x.dtype in (torch.bfloat16, torch.float32, torch.float16) and x.is_contiguous() and x.shape[-1] <= 16384:
+        return _Softmax.apply(x)
+    return torch.softmax(x, axis)
+
+
+# ----------------------------------------------------------------------------
+# LayerNorm / RMSNorm
+# ----------------------------------------------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y, mean, rstd = _hip.layer_norm_fwd(x, w, b, eps)
+        ctx.save_for_backward(x, w, b, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, b, mean, rstd = ctx.saved_tensors
+        gx, gw, gb = _hip.layer_norm_bwd(gy.contiguous(), x, w, mean, rstd, b is not None)
+        return gx, gw, gb, None
+
+
+def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
+    H = 1
+    for s in normalized_shape:
+        H *= s
+    if (_use_hip(x) and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float32, torch.float16)
+            and weight is not None and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 16384
+            and (bias is None or bias.dtype == weight.dtype)):
+        return _LayerNorm.apply(x, weight.reshape(-1), None if bias is None else bias.reshape(-1), float(eps))
+    return TF.layer_norm(x, list(normalized_shape), weight, bias, eps)
+
+
+def rms_norm(x, weight, eps=1e-6):
+    v = x.float().pow(2).mean(-1, keepdim=True)
+    y = (x.float() * torch.rsqrt(v + eps)).to(x.dtype)
+    return y * weight if weight is not None else y
+
+
+def bias_dropout_residual_layer_norm(x, residual, bias, ln_w, ln_b, dropout_p, training, eps):
+    h = x + bias if bias is not None else x
+    if training and dropout_p > 0:
+        h = TF.dropout(h, dropout_p, True)
+    h = h + residual
+    return layer_norm(h, [h.shape[-1]], ln_w, ln_b, eps)
+
+
+# ----------------------------------------------------------------------------
+# softmax cross-entropy (hard labels)
+# ----------------------------------------------------------------------------
+class _SoftmaxCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        loss, lse = _hip.softmax_ce_fwd(logits, labels, ignore_index)
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.ignore_index = ignore_index
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        logits, labels, lse = ctx.saved_tensors
+        gx = _hip.softmax_ce_bwd(gloss.contiguous().float(), logits, labels, lse, ctx.ignore_index)
+        return gx, None, None
+
+
+def softmax_cross_entropy(logits, labels, ignore_index=-100):
+    """Per-row loss (fp32) of softmax CE with int labels; logits [..., V]."""
+    shp = logits.shape[:-1]
+    V = logits.shape[-1]
+    l2 = logits.reshape(-1, V)
+    lab = labels.reshape(-1)
+    if _use_hip(logits) and logits.dtype in (torch.bfloat16, torch.float32, torch.float16) and V % 8 == 0:
+        if not l2.is_contiguous():
+            l2 = l2.contiguous()
+        loss = _SoftmaxCE.apply(l2, lab.to(torch.int64).contiguous(), int(ignore_index))
+    else:
+        loss = TF.cross_entropy(l2.float(), lab.long(), reduction="none", ignore_index=ignore_index)
+    return loss.reshape(shp)
+
+
+# ----------------------------------------------------------------------------
+# embedding
+# ----------------------------------------------------------------------------
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w, padding_idx):
+        ctx.save_for_backward(ids)
+        ctx.num = w.shape[0]
+        ctx.padding_idx = padding_idx
+        return _hip.embedding_fwd(ids, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (ids,) = ctx.saved_tensors
+        gw = torch.ops.aten.embedding_dense_backward(gy, ids, ctx.num, ctx.padding_idx if ctx.padding_idx is not None else -1, False)
+        return None, gw, None
+
+
+def embedding(ids, weight, padding_idx=None, sparse=False):
+    if _use_hip(weight) and weight.is_contiguous() and (weight.shape[1] * weight.element_size()) % 16 == 0 and weight.dtype in (torch.bfloat16, torch.float32, torch.float16):
+        return _Embedding.apply(ids.contiguous(), weight, padding_idx)
+    return TF.embedding(ids, weight, padding_idx)
+
+
+# ----------------------------------------------------------------------------
+# attention
+# ----------------------------------------------------------------------------
+def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=True):
+    """q, k, v: [B, S, H, D] (Paddle's fused-attention layout). Returns [B, S, H, D]."""
+    if _use_hip(q) and _hip.flash_attn_supported(q, k, v, dropout_p if training else 0.0):
+        return _hip.FlashAttention.apply(q, k, v, bool(causal), scale)
+    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+    o = TF.scaled_dot_product_attention(qt, kt, vt, dropout_p=dropout_p if training else 0.0,
+                                        is_causal=causal, scale=scale)
+    return o.transpose(1, 2)
+
+
+# ----------------------------------------------------------------------------
+# optimizers / AMP helpers (multi-tensor)
+# ----------------------------------------------------------------------------
+def fused_adam_(params, grads, exp_avgs, exp_avg_sqs, masters, lr, beta1, beta2, eps, step,
+                weight_decay=0.0, decoupled=True, lr_ratios=None, grad_scale=1.0):
+    """In-place Adam/AdamW over lists. ``masters`` (fp32) may be None entries
+    (params then fp32 themselves). ``step`` is the 1-based step count."""
+    if params and _use_hip(params[0]):
+        return _hip.multi_tensor_adam(params, grads, exp_avgs, exp_avg_sqs, masters, lr, beta1, beta2,
+                                      eps, step, weight_decay, decoupled, lr_ratios, grad_scale)
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    with torch.no_grad():
+        for i, (p, g, m, v) in enumerate(zip(params, grads, exp_avgs, exp_avg_sqs)):
+            if g is None:
+                continue
+            mp = masters[i] if masters is not None and masters[i] is not None else p
+            lr_i = lr * (lr_ratios[i] if lr_ratios is not None else 1.0)
+            gf = g.float() * grad_scale if grad_scale != 1.0 else g.float()
+            if weight_decay and not decoupled:
+                gf = gf + weight_decay * mp.float()
+            m.mul_(beta1).add_(gf, alpha=1 - beta1)
+            v.mul_(beta2).addcmul_(gf, gf, value=1 - beta2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+            upd = (m / bc1) / denom
+            newp = mp.float()
+            if weight_decay and decoupled:
+                newp = newp * (1 - lr_i * weight_decay)
+            newp = newp - lr_i * upd
+            mp.copy_(newp)
+            if mp is not p:
+                p.copy_(newp)
+
+
+def fused_momentum_(params, grads, velocities, masters, lr, mu, use_nesterov=False, weight_decay=0.0,
+                    lr_ratios=None, grad_scale=1.0):
+    if params and _use_hip(params[0]):
+        return _hip.multi_tensor_momentum(params, grads, velocities, masters, lr, mu, use_nesterov,
+                                          weight_decay, lr_ratios, grad_scale)
+    with torch.no_grad():
+        for i, (p, g, vel) in enumerate(zip(params, grads, velocities)):
+            if g is None:
+                continue
+            mp = masters[i] if masters is not None and masters[i] is not None else p
+            lr_i = lr * (lr_ratios[i] if lr_ratios is not None else 1.0)
+            gf = g.float() * grad_scale
+            if weight_decay:
+                gf = gf + weight_decay * mp.float()
+            vel.mul_(mu).add_(gf)
+            if use_nesterov:
+                newp = mp.float() - lr_i * (gf + mu * vel)
+            else:
+                newp = mp.float() - lr_i * vel
+            mp.copy_(newp)
+            if mp is not p:
+                p.copy_(newp)
+
+
+def global_norm_sq(tensors):
+    """Sum of squares over a list of tensors (fp32 scalar tensor)."""
+    tensors = [t for t in tensors if t is not None]
+    if not tensors:
+        return torch.zeros((), dtype=torch.float32)
+    if _use_hip(tensors[0]):
+        return _hip.multi_tensor_l2norm_sq(tensors)
+    return sum(t.float().pow(2).sum() for t in tensors)
+
+
+def scale_grads_(tensors, scale):
+    with torch.no_grad():
+        torch._foreach_mul_([t for t in tensors if t is not None], scale)
+
+
+def check_finite_and_unscale_(tensors, inv_scale):
+    """Unscale in place; return a bool tensor ``found_inf`` (reference: operators/amp/check_finite_and_unscale_op.cu)."""
+    tensors = [t for t in tensors if t is not None]
+    if not tensors:
+        return torch.zeros((), dtype=torch.bool)
+    found = torch.zeros(1, dtype=torch.float32, device=tensors[0].device)
+    torch._amp_foreach_non_finite_check_and_unscale_(tensors, found, torch.tensor([inv_scale], dtype=torch.float32, device=tensors[0].device))
+    return found[0] > 0
+
+
+# ----------------------------------------------------------------------------
+# batch norm (training stats) — NHWC channel reduction
+# ----------------------------------------------------------------------------
+def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, channel_axis):
+    return TF.batch_norm(x, running_mean, running_var, weight, bias, True, 1 - momentum, eps)

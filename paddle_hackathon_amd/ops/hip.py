@@ -1,0 +1,356 @@
+"""ctypes bindings to ``libpha_kernels.so`` (torch tensors in, torch tensors out).
+
+Each call passes raw device pointers and the *current* torch HIP stream, so the
+kernels order correctly with PyTorch-ROCm's own work and are capturable in HIP
+graphs. Shape preconditions are checked here on the host before any launch
+(a kernel reading out of bounds can take the whole GPU node down).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_int, c_long, c_float, c_void_p
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+_sigs_done = False
+
+
+def _L():
+    global _sigs_done
+    L = _lib.lib
+    if L is None:
+        raise RuntimeError("libpha_kernels.so not loaded")
+    if not _sigs_done:
+        P, I, F, LG = c_void_p, c_int, c_float, c_long
+        sig = {
+            "pha_layer_norm_fwd": [I, I, P, P, P, P, P, P, I, I, F, P],
+            "pha_layer_norm_bwd": [I, I, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+            "pha_softmax_fwd": [I, P, P, I, I, P],
+            "pha_softmax_bwd": [I, P, P, P, I, I, P],
+            "pha_softmax_ce_fwd": [I, P, P, P, P, LG, I, I, P],
+            "pha_softmax_ce_bwd": [I, P, P, P, P, P, LG, I, I, P],
+            "pha_bias_gelu_fwd": [I, P, P, P, LG, I, I, P],
+            "pha_bias_gelu_bwd": [I, P, P, P, P, LG, I, I, P],
+            "pha_embedding_fwd": [P, P, P, LG, I, LG, P],
+            "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P],
+            "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
+            "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
+            "pha_chunk_size": [],
+            "pha_tensor_meta_size": [],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name, None)
+            if f is None:
+                continue
+            f.argtypes = args
+            f.restype = c_int
+        for name in ("pha_flash_attn_fwd", "pha_flash_attn_bwd", "pha_flash_attn_bwd_preprocess"):
+            if hasattr(L, name):
+                getattr(L, name).restype = c_int
+        _sigs_done = True
+    return L
+
+
+def _stream(t):
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hipError {rc}")
+
+
+# ----------------------------------------------------------------------------
+# layer norm / softmax
+# ----------------------------------------------------------------------------
+def layer_norm_fwd(x, w, b, eps):
+    H = w.numel()
+    rows = x.numel() // H
+    assert x.numel() == rows * H and H % 8 == 0 and H <= 4096
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    _check(_L().pha_layer_norm_fwd(_DT[x.dtype], _DT[w.dtype], _ptr(x), _ptr(w.contiguous()), _ptr(None if b is None else b.contiguous()),
+                                   _ptr(y), _ptr(mean), _ptr(rstd), rows, H, float(eps), _stream(x)), "layer_norm_fwd")
+    return y, mean, rstd
+
+
+def layer_norm_bwd(dy, x, w, mean, rstd, has_bias):
+    H = w.numel()
+    rows = x.numel() // H
+    nblocks = max(1, min((rows + 3) // 4, 1024))
+    dx = torch.empty_like(x)
+    dw = torch.empty_like(w)
+    db = torch.empty_like(w) if has_bias else None
+    part = torch.empty((2, nblocks, H), dtype=torch.float32, device=x.device)
+    _check(_L().pha_layer_norm_bwd(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx),
+                                   _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H, _stream(x)), "layer_norm_bwd")
+    return dx, dw, db
+
+
+def softmax_fwd(x):
+    H = x.shape[-1]
+    rows = x.numel() // H
+    assert H % 8 == 0 and H <= 4096
+    y = torch.empty_like(x)
+    _check(_L().pha_softmax_fwd(_DT[x.dtype], _ptr(x), _ptr(y), rows, H, _stream(x)), "softmax_fwd")
+    return y
+
+
+def softmax_bwd(dy, y):
+    H = y.shape[-1]
+    rows = y.numel() // H
+    dx = torch.empty_like(y)
+    _check(_L().pha_softmax_bwd(_DT[y.dtype], _ptr(dy), _ptr(y), _ptr(dx), rows, H, _stream(y)), "softmax_bwd")
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# cross entropy / gelu / embedding
+# ----------------------------------------------------------------------------
+def softmax_ce_fwd(logits, labels, ignore_index):
+    rows, V = logits.shape
+    assert labels.numel() == rows and V % 8 == 0
+    loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    _check(_L().pha_softmax_ce_fwd(_DT[logits.dtype], _ptr(logits), _ptr(labels), _ptr(loss), _ptr(lse), rows, V,
+                                   int(ignore_index), _stream(logits)), "softmax_ce_fwd")
+    return loss, lse
+
+
+def softmax_ce_bwd(gloss, logits, labels, lse, ignore_index):
+    rows, V = logits.shape
+    dx = torch.empty_like(logits)
+    _check(_L().pha_softmax_ce_bwd(_DT[logits.dtype], _ptr(gloss), _ptr(logits), _ptr(labels), _ptr(lse), _ptr(dx), rows, V,
+                                   int(ignore_index), _stream(logits)), "softmax_ce_bwd")
+    return dx
+
+
+def bias_gelu_fwd(x, b, approximate):
+    n = x.numel()
+    H = x.shape[-1]
+    if n % 8 or (b is not None and (H % 8 or b.numel() != H)):
+        import torch.nn.functional as TF
+        return TF.gelu(x + b if b is not None else x, approximate="tanh" if approximate else "none")
+    y = torch.empty_like(x)
+    _check(_L().pha_bias_gelu_fwd(_DT[x.dtype], _ptr(x), _ptr(b), _ptr(y), n, H, int(approximate), _stream(x)), "bias_gelu_fwd")
+    return y
+
+
+def bias_gelu_bwd(gy, x, b, approximate):
+    n = x.numel()
+    H = x.shape[-1]
+    if n % 8 or (b is not None and H % 8):
+        xx = (x + b if b is not None else x).detach().float().requires_grad_(True)
+        import torch.nn.functional as TF
+        with torch.enable_grad():
+            y = TF.gelu(xx, approximate="tanh" if approximate else "none")
+            (gx,) = torch.autograd.grad(y, xx, gy.float())
+        gx = gx.to(x.dtype)
+    else:
+        gx = torch.empty_like(x)
+        _check(_L().pha_bias_gelu_bwd(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), n, H, int(approximate), _stream(x)), "bias_gelu_bwd")
+    gb = gx.reshape(-1, H).sum(0, dtype=torch.float32).to(b.dtype) if b is not None else None
+    return gx, gb
+
+
+def embedding_fwd(ids, w):
+    ids = ids.to(torch.int64)
+    rows = ids.numel()
+    D = w.shape[1]
+    out = torch.empty(list(ids.shape) + [D], dtype=w.dtype, device=w.device)
+    if rows == 0:
+        return out
+    _check(_L().pha_embedding_fwd(_ptr(ids), _ptr(w), _ptr(out), rows, D * w.element_size(), w.shape[0], _stream(w)), "embedding_fwd")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# multi-tensor optimizers
+# ----------------------------------------------------------------------------
+_META_DT = np.dtype([("p", "<u8"), ("g", "<u8"), ("m", "<u8"), ("v", "<u8"), ("master", "<u8"),
+                     ("n", "<i8"), ("lr", "<f4"), ("wd", "<f4")])
+_NORM_DT = np.dtype([("x", "<u8"), ("n", "<i8"), ("dt", "<i4"), ("pad", "<i4")])
+
+
+def _chunk():
+    return _L().pha_chunk_size()
+
+
+def _upload(arr, device):
+    host = torch.from_numpy(arr.view(np.uint8).copy()).pin_memory()
+    return host.to(device, non_blocking=True)
+
+
+def _group_by_dtype(items, key):
+    groups = {}
+    for it in items:
+        groups.setdefault(key(it), []).append(it)
+    return groups
+
+
+class _TablePlan:
+    """Cached (metas, chunks) device tables for a fixed list of tensors."""
+
+    def __init__(self):
+        self.key = None
+        self.tables = None
+
+
+_plans = {}
+
+
+def _build_tables(recs, device, chunk):
+    meta = np.zeros(len(recs), dtype=_META_DT)
+    chunks = []
+    for i, r in enumerate(recs):
+        meta[i] = r
+        n = int(r[5])
+        for c in range((n + chunk - 1) // chunk):
+            chunks.append((i, c))
+    ch = np.asarray(chunks, dtype=np.int32).reshape(-1, 2)
+    return _upload(meta, device), _upload(ch, device), len(chunks)
+
+
+def _tables_cached(tag, recs, device):
+    """Pointer tables are rebuilt only when any pointer/size changes (steady state: cached)."""
+    key = tuple(tuple(r[:6]) + (r[6], r[7]) for r in recs)
+    plan = _plans.get(tag)
+    if plan is not None and plan[0] == key:
+        return plan[1]
+    t = _build_tables(recs, device, _chunk())
+    _plans[tag] = (key, t)
+    return t
+
+
+def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, step, weight_decay, decoupled,
+                      lr_ratios, grad_scale, wds=None):
+    L = _L()
+    dev = params[0].device
+    items = []
+    for i, p in enumerate(params):
+        g = grads[i]
+        if g is None:
+            continue
+        mst = masters[i] if masters is not None else None
+        wd = wds[i] if wds is not None else weight_decay
+        rec = (p.data_ptr(), g.data_ptr(), ms[i].data_ptr(), vs[i].data_ptr(), 0 if mst is None else mst.data_ptr(),
+               p.numel(), float(lr_ratios[i]) if lr_ratios is not None else 1.0, float(wd))
+        items.append((p.dtype, g.dtype, rec))
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    stream = _stream(params[0])
+    for (pdt, gdt), its in _group_by_dtype(items, lambda t: (t[0], t[1])).items():
+        metas, chunks, n = _tables_cached(("adam", pdt, gdt), [t[2] for t in its], dev)
+        _check(L.pha_multi_tensor_adam(_DT[pdt], _DT[gdt], _ptr(metas), _ptr(chunks), n, float(lr), float(beta1), float(beta2),
+                                       float(eps), float(bc1), float(bc2), float(grad_scale), int(bool(decoupled)), stream),
+               "multi_tensor_adam")
+
+
+def multi_tensor_momentum(params, grads, vels, masters, lr, mu, nesterov, weight_decay, lr_ratios, grad_scale, wds=None):
+    L = _L()
+    dev = params[0].device
+    items = []
+    for i, p in enumerate(params):
+        g = grads[i]
+        if g is None:
+            continue
+        mst = masters[i] if masters is not None else None
+        wd = wds[i] if wds is not None else weight_decay
+        rec = (p.data_ptr(), g.data_ptr(), vels[i].data_ptr(), 0, 0 if mst is None else mst.data_ptr(), p.numel(),
+               float(lr_ratios[i]) if lr_ratios is not None else 1.0, float(wd))
+        items.append((p.dtype, g.dtype, rec))
+    stream = _stream(params[0])
+    for (pdt, gdt), its in _group_by_dtype(items, lambda t: (t[0], t[1])).items():
+        metas, chunks, n = _tables_cached(("mom", pdt, gdt), [t[2] for t in its], dev)
+        _check(L.pha_multi_tensor_momentum(_DT[pdt], _DT[gdt], _ptr(metas), _ptr(chunks), n, float(lr), float(mu),
+                                           float(grad_scale), int(bool(nesterov)), stream), "multi_tensor_momentum")
+
+
+def multi_tensor_l2norm_sq(tensors):
+    L = _L()
+    dev = tensors[0].device
+    chunk = _chunk()
+    meta = np.zeros(len(tensors), dtype=_NORM_DT)
+    chunks = []
+    for i, t in enumerate(tensors):
+        assert t.is_contiguous()
+        meta[i] = (t.data_ptr(), t.numel(), _DT[t.dtype], 0)
+        for c in range((t.numel() + chunk - 1) // chunk):
+            chunks.append((i, c))
+    ch = np.asarray(chunks, dtype=np.int32).reshape(-1, 2)
+    out = torch.empty(1, dtype=torch.float32, device=dev)
+    partial = torch.empty(max(1, len(chunks)), dtype=torch.float32, device=dev)
+    _check(L.pha_multi_tensor_l2sq(_ptr(_upload(meta, dev)), _ptr(_upload(ch, dev)), len(chunks), _ptr(partial), _ptr(out), _stream(tensors[0])),
+           "multi_tensor_l2sq")
+    return out[0]
+
+
+# ----------------------------------------------------------------------------
+# flash attention (csrc/kernels/flash_attn.hip)
+# ----------------------------------------------------------------------------
+def flash_attn_supported(q, k, v, dropout_p):
+    if dropout_p and dropout_p > 0:
+        return False
+    L = _lib.lib
+    if L is None or not hasattr(L, "pha_flash_attn_fwd"):
+        return False
+    if q.dtype not in (torch.bfloat16, torch.float16) or k.dtype != q.dtype or v.dtype != q.dtype:
+        return False
+    B, S, H, D = q.shape
+    if D not in (64, 128) or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
+        return False
+    if H % k.shape[2] != 0:
+        return False
+    return True
+
+
+class FlashAttention(torch.autograd.Function):
+    """Forward/backward on our MFMA flash-attention kernels. Layout [B, S, H, D]."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, S, H, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+        o = torch.empty_like(q)
+        lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        L = _L()
+        _check(L.pha_flash_attn_fwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), c_int(B), c_int(S), c_int(Sk),
+                                    c_int(H), c_int(Hk), c_int(D), c_float(sc), c_int(int(causal)), _stream(q)), "flash_attn_fwd")
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal = causal
+        ctx.scale = sc
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        B, S, H, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        L = _L()
+        delta = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        dq_acc = torch.zeros((B, S, H, D), dtype=torch.float32, device=q.device)
+        dk = torch.empty_like(k) if Hk == H else torch.empty((B, Sk, H, D), dtype=k.dtype, device=k.device)
+        dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
+        _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S), c_int(H), c_int(D),
+                                               _stream(q)), "flash_attn_bwd_preprocess")
+        _check(L.pha_flash_attn_bwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq_acc),
+                                    _ptr(dk), _ptr(dv), c_int(B), c_int(S), c_int(Sk), c_int(H), c_int(Hk), c_int(D),
+                                    c_float(ctx.scale), c_int(int(ctx.causal)), _stream(q)), "flash_attn_bwd")
+        dq = dq_acc.to(q.dtype)
+        if Hk != H:
+            g = H // Hk
+            dk = dk.view(B, Sk, Hk, g, D).sum(3)
+            dv = dv.view(B, Sk, Hk, g, D).sum(3)
+        return dq, dk, dv, None, None

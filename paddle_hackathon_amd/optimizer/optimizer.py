@@ -1,0 +1,464 @@
+"""Optimizers (reference: python/paddle/optimizer/{optimizer,sgd,momentum,adam,adamw,adamax,
+adagrad,adadelta,rmsprop,lamb}.py; kernels phi/kernels/gpu/{adam,adamw,momentum,...}_kernel.cu).
+
+Adam/AdamW/Momentum/SGD update *every* parameter with one multi-tensor HIP
+launch per (param dtype, grad dtype) group (ops.fused_adam_ / fused_momentum_),
+with fp32 master weights for bf16/fp16 parameters (``multi_precision``).
+Accumulator names follow the reference (``{param}_moment1_0`` …) so optimizer
+checkpoints (.pdopt) keep the same keys.
+"""
+from __future__ import annotations
+
+import collections
+import math
+
+import numpy as np
+import torch
+
+from ..framework.core import Tensor, Parameter, _wrap
+from ..framework import core as _core
+from ..regularizer import L1Decay, L2Decay, WeightDecayRegularizer
+from .. import ops as _ops
+from .lr import LRScheduler
+
+__all__ = ["Optimizer", "SGD", "Momentum", "Adam", "AdamW", "Adamax", "Adagrad", "Adadelta", "RMSProp", "Lamb"]
+
+
+class Optimizer:
+    def __init__(self, learning_rate=0.001, parameters=None, weight_decay=None, grad_clip=None, name=None,
+                 multi_precision=True):
+        if parameters is not None and isinstance(parameters, Tensor):
+            raise TypeError("parameters should be a list of Tensor / dict")
+        self._parameter_list = None
+        self._param_groups = []
+        if parameters is not None:
+            parameters = list(parameters)
+            if parameters and isinstance(parameters[0], dict):
+                for g in parameters:
+                    self._add_param_group(dict(g))
+            else:
+                self._add_param_group({"params": parameters})
+            self._parameter_list = [p for g in self._param_groups for p in g["params"]]
+        self._learning_rate = learning_rate
+        if isinstance(weight_decay, (int, float)):
+            self.regularization = L2Decay(float(weight_decay)) if weight_decay else None
+        else:
+            self.regularization = weight_decay
+        self._grad_clip = grad_clip
+        self._name = name
+        self._multi_precision = multi_precision
+        self._accumulators = collections.defaultdict(dict)   # acc_name -> {param.name: Tensor}
+        self._master_weights = {}
+        self._step_count = 0
+        self._state_loaded = {}
+
+    # -- groups ----------------------------------------------------------------------
+    def _add_param_group(self, group):
+        params = group["params"]
+        if isinstance(params, Tensor):
+            params = [params]
+        group["params"] = list(params)
+        self._param_groups.append(group)
+
+    @property
+    def _parameters(self):
+        return self._parameter_list
+
+    # -- lr -----------------------------------------------------------------------------
+    def get_lr(self):
+        lr = self._learning_rate
+        return float(lr()) if isinstance(lr, LRScheduler) else float(lr)
+
+    def set_lr(self, value):
+        if isinstance(self._learning_rate, LRScheduler):
+            raise RuntimeError("optimizer's learning rate can't be LRScheduler when invoke this API")
+        self._learning_rate = float(value)
+
+    def set_lr_scheduler(self, scheduler):
+        self._learning_rate = scheduler
+
+    # -- accumulators ---------------------------------------------------------------
+    def _acc(self, name, p, dtype=torch.float32, fill=0.0, shape=None):
+        d = self._accumulators[name]
+        t = d.get(p.name)
+        if t is None:
+            key = f"{p.name}_{name}_0"
+            if key in self._state_loaded:
+                src = self._state_loaded.pop(key)
+                src_t = src._t if isinstance(src, Tensor) else torch.as_tensor(np.asarray(src))
+                t = _wrap(src_t.to(device=p._t.device, dtype=dtype).clone())
+            else:
+                shp = p._t.shape if shape is None else shape
+                t = _wrap(torch.full(shp, fill, dtype=dtype, device=p._t.device))
+            t.name = key
+            d[p.name] = t
+        return t
+
+    def _master(self, p):
+        if not self._multi_precision or p._t.dtype not in (torch.float16, torch.bfloat16):
+            return None
+        m = self._master_weights.get(p.name)
+        if m is None:
+            mw = self._state_loaded.get("master_weights", {})
+            if p.name in mw:
+                src = mw[p.name]
+                src_t = src._t if isinstance(src, Tensor) else torch.as_tensor(np.asarray(src))
+                m = _wrap(src_t.to(device=p._t.device, dtype=torch.float32).clone())
+            else:
+                m = _wrap(p._t.detach().float().clone())
+            m.name = p.name + "_fp32_master_0"
+            self._master_weights[p.name] = m
+        return m
+
+    # -- step ---------------------------------------------------------------------------
+    def _collect(self):
+        out = []
+        for g in self._param_groups:
+            for p in g["params"]:
+                if p.stop_gradient or p._t.grad is None:
+                    continue
+                out.append((p, _wrap(p._t.grad), g))
+        return out
+
+    def _apply_clip(self, pgs):
+        if self._grad_clip is None:
+            return
+        self._grad_clip([(p, g) for p, g, _ in pgs])
+
+    def _wd_for(self, p, group):
+        reg = p.regularizer if getattr(p, "regularizer", None) is not None else group.get("weight_decay", self.regularization)
+        if isinstance(reg, (int, float)):
+            return float(reg), "l2"
+        if isinstance(reg, L2Decay):
+            return reg.coeff, "l2"
+        if isinstance(reg, L1Decay):
+            return reg.coeff, "l1"
+        return 0.0, None
+
+    def step(self):
+        if self._parameter_list is None:
+            raise ValueError("parameters must be given in dygraph mode")
+        pgs = self._collect()
+        self._apply_clip(pgs)
+        self._step_count += 1
+        with torch.no_grad():
+            self._update(pgs)
+
+    def _update(self, pgs):
+        raise NotImplementedError
+
+    def _lr_ratio(self, p, group):
+        r = p.optimize_attr.get("learning_rate", 1.0) if hasattr(p, "optimize_attr") else 1.0
+        if "learning_rate" in group:
+            r *= float(group["learning_rate"])
+        return r
+
+    def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        if not _core.in_dynamic_mode():
+            from ..static.program import minimize_static
+            return minimize_static(self, loss, parameters, no_grad_set)
+        if parameters is not None and self._parameter_list is None:
+            self._add_param_group({"params": list(parameters)})
+            self._parameter_list = list(parameters)
+        self.step()
+        return None, [(p, _wrap(p._t.grad)) for p in (self._parameter_list or []) if p._t.grad is not None]
+
+    def clear_grad(self, set_to_zero=True):
+        ps = [p for p in self._parameter_list or [] if p._t.grad is not None]
+        if set_to_zero:
+            if ps:
+                torch._foreach_zero_([p._t.grad for p in ps])
+        else:
+            for p in ps:
+                p._t.grad = None
+
+    clear_gradients = clear_grad
+
+    def backward(self, loss, startup_program=None, parameters=None, no_grad_set=None, callbacks=None):
+        loss.backward()
+        return [(p, _wrap(p._t.grad)) for p in (self._parameter_list or []) if p._t.grad is not None]
+
+    def apply_gradients(self, params_grads):
+        self.step()
+
+    # -- state -------------------------------------------------------------------------
+    def state_dict(self):
+        sd = {}
+        for name, d in self._accumulators.items():
+            for pname, t in d.items():
+                sd[t.name] = t
+        if self._master_weights:
+            sd["master_weights"] = dict(self._master_weights)
+        if isinstance(self._learning_rate, LRScheduler):
+            sd["LR_Scheduler"] = self._learning_rate.state_dict()
+        sd["@step_count@"] = self._step_count
+        return sd
+
+    def set_state_dict(self, state_dict):
+        state_dict = dict(state_dict)
+        if isinstance(self._learning_rate, LRScheduler) and "LR_Scheduler" in state_dict:
+            self._learning_rate.set_state_dict(state_dict.pop("LR_Scheduler"))
+        self._step_count = int(state_dict.pop("@step_count@", self._step_count))
+        # existing accumulators are overwritten now; the rest are loaded lazily on first use
+        for name, d in self._accumulators.items():
+            for pname, t in d.items():
+                if t.name in state_dict:
+                    v = state_dict.pop(t.name)
+                    src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+                    with torch.no_grad():
+                        t._t.copy_(src.to(t._t.device, t._t.dtype).reshape(t._t.shape))
+        mw = state_dict.get("master_weights")
+        if mw:
+            for pname, m in list(self._master_weights.items()):
+                if pname in mw:
+                    v = mw[pname]
+                    src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+                    with torch.no_grad():
+                        m._t.copy_(src.to(m._t.device, torch.float32))
+        self._state_loaded.update(state_dict)
+
+    set_dict = set_state_dict
+
+
+class SGD(Optimizer):
+    def __init__(self, learning_rate=0.001, parameters=None, weight_decay=None, grad_clip=None, multi_precision=False, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            gt = g._t.float()
+            m = self._master(p)
+            target = m._t if m is not None else p._t
+            if kind == "l2":
+                gt = gt + wd * target.float()
+            elif kind == "l1":
+                gt = gt + wd * torch.sign(target.float())
+            target.add_(gt.to(target.dtype), alpha=-lr * self._lr_ratio(p, group))
+            if m is not None:
+                p._t.copy_(m._t)
+
+
+class Momentum(Optimizer):
+    def __init__(self, learning_rate=0.001, momentum=0.9, parameters=None, use_nesterov=False, weight_decay=None,
+                 grad_clip=None, multi_precision=False, rescale_grad=1.0, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
+        self._momentum = momentum
+        self._use_nesterov = bool(use_nesterov)
+        self._rescale_grad = rescale_grad
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        params, grads, vels, masters, ratios, wds = [], [], [], [], [], []
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            if kind == "l1":
+                g._t.add_(torch.sign(p._t) * wd)
+                wd = 0.0
+            params.append(p._t)
+            grads.append(g._t)
+            vels.append(self._acc("velocity", p)._t)
+            m = self._master(p)
+            masters.append(None if m is None else m._t)
+            ratios.append(self._lr_ratio(p, group))
+            wds.append(wd)
+        if params:
+            if params[0].is_cuda:
+                from ..ops import hip
+                hip.multi_tensor_momentum(params, grads, vels, masters, lr, self._momentum, self._use_nesterov, 0.0,
+                                          ratios, self._rescale_grad, wds)
+            else:
+                for i in range(len(params)):
+                    _ops.fused_momentum_([params[i]], [grads[i]], [vels[i]], [masters[i]], lr, self._momentum,
+                                         self._use_nesterov, wds[i], [ratios[i]], self._rescale_grad)
+
+
+class Adam(Optimizer):
+    _decoupled = False
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-08, parameters=None, weight_decay=None,
+                 grad_clip=None, lazy_mode=False, multi_precision=True, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
+        self._beta1 = float(beta1._t.item()) if isinstance(beta1, Tensor) else float(beta1)
+        self._beta2 = float(beta2._t.item()) if isinstance(beta2, Tensor) else float(beta2)
+        self._epsilon = float(epsilon._t.item()) if isinstance(epsilon, Tensor) else float(epsilon)
+        self._lazy_mode = lazy_mode
+        self._grad_scale = 1.0
+
+    def _decay_for(self, p, group):
+        wd, kind = self._wd_for(p, group)
+        return wd, kind
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        params, grads, m1, m2, masters, ratios, wds = [], [], [], [], [], [], []
+        step_pows = []
+        for p, g, group in pgs:
+            wd, kind = self._decay_for(p, group)
+            if kind == "l1":
+                g._t.add_(torch.sign(p._t) * wd)
+                wd = 0.0
+            params.append(p._t)
+            grads.append(g._t)
+            m1.append(self._acc("moment1", p)._t)
+            m2.append(self._acc("moment2", p)._t)
+            b1p = self._acc("beta1_pow_acc", p, fill=self._beta1, shape=[1])
+            b2p = self._acc("beta2_pow_acc", p, fill=self._beta2, shape=[1])
+            step_pows.append((b1p, b2p))
+            m = self._master(p)
+            masters.append(None if m is None else m._t)
+            ratios.append(self._lr_ratio(p, group))
+            wds.append(wd)
+        if not params:
+            return
+        # bias correction uses the optimizer step count; the per-param beta-pow accumulators
+        # are still maintained (one foreach launch) so .pdopt checkpoints keep the reference keys
+        step = self._step_count
+        if params[0].is_cuda:
+            from ..ops import hip
+            hip.multi_tensor_adam(params, grads, m1, m2, masters, lr, self._beta1, self._beta2, self._epsilon, step, 0.0,
+                                  self._decoupled, ratios, self._grad_scale, wds)
+        else:
+            for i in range(len(params)):
+                _ops.fused_adam_([params[i]], [grads[i]], [m1[i]], [m2[i]], [masters[i]], lr, self._beta1, self._beta2,
+                                 self._epsilon, step, wds[i], self._decoupled, [ratios[i]], self._grad_scale)
+        torch._foreach_mul_([b[0]._t for b in step_pows], self._beta1)
+        torch._foreach_mul_([b[1]._t for b in step_pows], self._beta2)
+
+
+class AdamW(Adam):
+    _decoupled = True
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, parameters=None, weight_decay=0.01,
+                 lr_ratio=None, apply_decay_param_fun=None, grad_clip=None, lazy_mode=False, multi_precision=True, name=None):
+        super().__init__(learning_rate, beta1, beta2, epsilon, parameters, None, grad_clip, lazy_mode, multi_precision, name)
+        self._coeff = float(weight_decay) if not isinstance(weight_decay, WeightDecayRegularizer) else weight_decay.coeff
+        self._apply_decay_param_fun = apply_decay_param_fun
+        self._lr_ratio_fn = lr_ratio
+
+    def _decay_for(self, p, group):
+        coeff = group.get("weight_decay", self._coeff)
+        if isinstance(coeff, WeightDecayRegularizer):
+            coeff = coeff.coeff
+        if self._apply_decay_param_fun is not None and not self._apply_decay_param_fun(p.name):
+            return 0.0, None
+        return float(coeff), "decoupled"
+
+    def _lr_ratio(self, p, group):
+        r = super()._lr_ratio(p, group)
+        if self._lr_ratio_fn is not None:
+            r *= float(self._lr_ratio_fn(p))
+        return r
+
+
+class Adamax(Optimizer):
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-08, parameters=None, weight_decay=None,
+                 grad_clip=None, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, False)
+        self._beta1, self._beta2, self._epsilon = beta1, beta2, epsilon
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            gt = g._t.float() + (wd * p._t.float() if kind == "l2" else 0)
+            m = self._acc("moment", p)._t
+            u = self._acc("inf_norm", p)._t
+            b1p = self._acc("beta1_pow_acc", p, fill=self._beta1, shape=[1])._t
+            m.mul_(self._beta1).add_(gt, alpha=1 - self._beta1)
+            torch.maximum(u * self._beta2, gt.abs() + self._epsilon, out=u)
+            lr_t = lr * self._lr_ratio(p, group) / (1 - b1p)
+            p._t.sub_((lr_t * m / u).to(p._t.dtype))
+            b1p.mul_(self._beta1)
+
+
+class Adagrad(Optimizer):
+    def __init__(self, learning_rate, epsilon=1e-06, parameters=None, weight_decay=None, grad_clip=None, name=None,
+                 initial_accumulator_value=0.0):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, False)
+        self._epsilon, self._init_acc = epsilon, initial_accumulator_value
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            gt = g._t.float() + (wd * p._t.float() if kind == "l2" else 0)
+            m = self._acc("moment", p, fill=self._init_acc)._t
+            m.add_(gt * gt)
+            p._t.sub_((lr * self._lr_ratio(p, group) * gt / (m.sqrt() + self._epsilon)).to(p._t.dtype))
+
+
+class Adadelta(Optimizer):
+    def __init__(self, learning_rate=0.001, epsilon=1.0e-6, rho=0.95, parameters=None, weight_decay=None, grad_clip=None, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, False)
+        self._epsilon, self._rho = epsilon, rho
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            gt = g._t.float() + (wd * p._t.float() if kind == "l2" else 0)
+            sg = self._acc("_avg_squared_grad", p)._t
+            su = self._acc("_avg_squared_update", p)._t
+            sg.mul_(self._rho).add_(gt * gt, alpha=1 - self._rho)
+            upd = -torch.sqrt((su + self._epsilon) / (sg + self._epsilon)) * gt
+            su.mul_(self._rho).add_(upd * upd, alpha=1 - self._rho)
+            p._t.add_((lr * self._lr_ratio(p, group) * upd).to(p._t.dtype))
+
+
+class RMSProp(Optimizer):
+    def __init__(self, learning_rate, rho=0.95, epsilon=1.0e-6, momentum=0.0, centered=False, parameters=None,
+                 weight_decay=None, grad_clip=None, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, False)
+        self._rho, self._epsilon, self._momentum, self._centered = rho, epsilon, momentum, centered
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            wd, kind = self._wd_for(p, group)
+            gt = g._t.float() + (wd * p._t.float() if kind == "l2" else 0)
+            ms = self._acc("mean_square", p)._t
+            mom = self._acc("momentum", p)._t
+            ms.mul_(self._rho).add_(gt * gt, alpha=1 - self._rho)
+            if self._centered:
+                mg = self._acc("mean_grad", p)._t
+                mg.mul_(self._rho).add_(gt, alpha=1 - self._rho)
+                denom = ms - mg * mg + self._epsilon
+            else:
+                denom = ms + self._epsilon
+            mom.mul_(self._momentum).add_(lr * self._lr_ratio(p, group) * gt / denom.sqrt())
+            p._t.sub_(mom.to(p._t.dtype))
+
+
+class Lamb(Optimizer):
+    def __init__(self, learning_rate=0.001, lamb_weight_decay=0.01, beta1=0.9, beta2=0.999, epsilon=1e-6, parameters=None,
+                 grad_clip=None, exclude_from_weight_decay_fn=None, multi_precision=False, name=None):
+        super().__init__(learning_rate, parameters, None, grad_clip, name, multi_precision)
+        self._wd, self._beta1, self._beta2, self._epsilon = lamb_weight_decay, beta1, beta2, epsilon
+        self._exclude = exclude_from_weight_decay_fn
+
+    def _update(self, pgs):
+        lr = self.get_lr()
+        for p, g, group in pgs:
+            gt = g._t.float()
+            m = self._master(p)
+            w = (m._t if m is not None else p._t).float()
+            m1 = self._acc("moment1", p)._t
+            m2 = self._acc("moment2", p)._t
+            b1p = self._acc("beta1_pow_acc", p, fill=self._beta1, shape=[1])._t
+            b2p = self._acc("beta2_pow_acc", p, fill=self._beta2, shape=[1])._t
+            m1.mul_(self._beta1).add_(gt, alpha=1 - self._beta1)
+            m2.mul_(self._beta2).addcmul_(gt, gt, value=1 - self._beta2)
+            mhat = m1 / (1 - b1p)
+            vhat = m2 / (1 - b2p)
+            wd = 0.0 if (self._exclude is not None and self._exclude(p)) else self._wd
+            r = mhat / (vhat.sqrt() + self._epsilon) + wd * w
+            wn, rn = w.norm(), r.norm()
+            trust = torch.where((wn > 0) & (rn > 0), wn / rn, torch.ones_like(wn))
+            neww = w - lr * self._lr_ratio(p, group) * trust * r
+            if m is not None:
+                m._t.copy_(neww)
+            p._t.copy_(neww.to(p._t.dtype))
+            b1p.mul_(self._beta1)
+            b2p.mul_(self._beta2)
