@@ -84,8 +84,12 @@ def main():
         opt.clear_grad(set_to_zero=False)
         return loss
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
+        tw = time.perf_counter()
         loss = step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup {i} loss={float(loss.item()):.4f} {time.perf_counter() - tw:.3f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

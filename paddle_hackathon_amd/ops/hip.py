@@ -289,8 +289,13 @@ def multi_tensor_l2norm_sq(tensors):
     ch = np.asarray(chunks, dtype=np.int32).reshape(-1, 2)
     out = torch.empty(1, dtype=torch.float32, device=dev)
     partial = torch.empty(max(1, len(chunks)), dtype=torch.float32, device=dev)
-    _check(L.pha_multi_tensor_l2sq(_ptr(_upload(meta, dev)), _ptr(_upload(ch, dev)), len(chunks), _ptr(partial), _ptr(out), _stream(tensors[0])),
+    meta_d = _upload(meta, dev)   # keep the device tables alive until the launch is enqueued
+    ch_d = _upload(ch, dev)
+    _check(L.pha_multi_tensor_l2sq(_ptr(meta_d), _ptr(ch_d), len(chunks), _ptr(partial), _ptr(out), _stream(tensors[0])),
            "multi_tensor_l2sq")
+    # the caching allocator may hand these blocks out again once freed; tie them to the stream
+    meta_d.record_stream(torch.cuda.current_stream(dev))
+    ch_d.record_stream(torch.cuda.current_stream(dev))
     return out[0]
 
 
@@ -298,6 +303,9 @@ def multi_tensor_l2norm_sq(tensors):
 # flash attention (csrc/kernels/flash_attn.hip)
 # ----------------------------------------------------------------------------
 def flash_attn_supported(q, k, v, dropout_p):
+    import os
+    if os.environ.get("PHA_DISABLE_FLASH") == "1":
+        return False
     if dropout_p and dropout_p > 0:
         return False
     L = _lib.lib

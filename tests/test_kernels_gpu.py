@@ -166,3 +166,50 @@ def test_gpt_tiny_train_step_gpu():
         opt.clear_grad()
         losses.append(loss.item())
     assert losses[-1] < losses[0] - 1.0, losses
+
+
+def _ref_attn(q, k, v, causal, scale=None):
+    B, S, H, D = q.shape
+    Hk = k.shape[2]
+    if Hk != H:
+        k = k.repeat_interleave(H // Hk, dim=2)
+        v = v.repeat_interleave(H // Hk, dim=2)
+    qt, kt, vt = (t.float().transpose(1, 2) for t in (q, k, v))
+    o = TF.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale)
+    return o.transpose(1, 2)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("S", [128, 200, 512])
+def test_flash_attention_fwd_bwd(dt, D, causal, S):
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(0)
+    B, H = 2, 3
+    q = torch.randn(B, S, H, D, device="cuda").to(dt).requires_grad_(True)
+    k = torch.randn(B, S, H, D, device="cuda").to(dt).requires_grad_(True)
+    v = torch.randn(B, S, H, D, device="cuda").to(dt).requires_grad_(True)
+    assert hip.flash_attn_supported(q, k, v, 0.0)
+    o = hip.FlashAttention.apply(q, k, v, causal, None)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qr, kr, vr, causal)
+    assert (o.float() - ref).abs().max().item() < 2e-2, (o.float() - ref).abs().max().item()
+    g = torch.randn_like(ref)
+    o.backward(g.to(dt))
+    ref.backward(g)
+    for got, want, name in ((q.grad, qr.grad, "dq"), (k.grad, kr.grad, "dk"), (v.grad, vr.grad, "dv")):
+        err = (got.float() - want).abs().max().item()
+        scale = want.abs().max().item()
+        assert err < 3e-2 * max(1.0, scale), (name, err, scale)
+
+
+def test_flash_attention_gqa():
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(0)
+    q = torch.randn(1, 256, 8, 128, device="cuda").bfloat16()
+    k = torch.randn(1, 256, 2, 128, device="cuda").bfloat16()
+    v = torch.randn(1, 256, 2, 128, device="cuda").bfloat16()
+    o = hip.FlashAttention.apply(q, k, v, True, None)
+    ref = _ref_attn(q, k, v, True)
+    assert (o.float() - ref).abs().max().item() < 2e-2

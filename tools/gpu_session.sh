@@ -1,34 +1,38 @@
 #!/bin/bash
-# One GPU session: gpu tests, bench, rocprofv3 kernel stats. Stops at the first fault/timeout.
-# usage: tools/gpu_session.sh [tests|bench|prof ...]   (default: all)
+# One GPU session. Steps run in the order given; stops at the first fault/timeout.
+# usage: tools/gpu_session.sh smoke bench prof tests tests_fa ...
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p $OUT
 cd $ROOT
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONUNBUFFERED=1
 fatal() { case $1 in 124|137|134|139|135|136) return 0;; *) return 1;; esac; }
-steps=${@:-tests bench prof}
-for s in $steps; do
+for s in "$@"; do
+  echo "=== step $s $(date +%T)"
   case $s in
-    tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -x > $OUT/pytest_gpu.log 2>&1; rc=$?
-      echo "pytest gpu rc=$rc"; tail -5 $OUT/pytest_gpu.log
-      if fatal $rc; then echo "FATAL in tests"; exit $rc; fi ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
-      echo "smoke rc=$rc"; tail -3 $OUT/smoke.log
-      if fatal $rc; then exit $rc; fi ;;
+      tail -3 $OUT/smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
-      echo "bench rc=$rc"; tail -3 $OUT/bench.log
-      if fatal $rc; then exit $rc; fi ;;
+      timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
+      tail -3 $OUT/bench.log ;;
+    bench_resnet)
+      timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
+      tail -3 $OUT/bench_resnet.log ;;
     prof)
       export TMPDIR=/tmp
       rm -rf $OUT/prof
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $ROOT/bench.py --steps 3 --warmup 2 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; rc=$?
-      echo "prof rc=$rc"; tail -3 $OUT/prof.log
-      if fatal $rc; then exit $rc; fi ;;
-    *) echo "unknown step $s";;
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $ROOT/bench.py --steps 3 --warmup 2 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; rc=$?
+      tail -3 $OUT/prof.log ;;
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -v -x --timeout 240 -k "not flash" > $OUT/pytest_gpu.log 2>&1; rc=$?
+      tail -5 $OUT/pytest_gpu.log ;;
+    tests_fa)
+      timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 120 -k "flash" > $OUT/pytest_fa.log 2>&1; rc=$?
+      tail -5 $OUT/pytest_fa.log ;;
+    *) echo "unknown step $s"; rc=0 ;;
   esac
+  echo "=== step $s rc=$rc $(date +%T)"
+  if fatal $rc; then echo "FATAL rc=$rc in $s; stopping"; exit $rc; fi
 done
