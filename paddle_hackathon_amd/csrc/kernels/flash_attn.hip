@@ -16,10 +16,8 @@
 //    the query on the lane so the online-softmax rescale is lane-local.
 //  * exp2 with log2(e)*scale folded into one multiply; fp32 statistics; LSE saved for bwd.
 //
-// Backward (FA2-style, key-block parallel): workgroup = 4 waves = 128 keys; each wave keeps
-// its 32 keys' K and V fragments in registers and accumulates dK^T / dV^T over all query
-// tiles; dS goes through LDS once so each wave computes one 32-wide d block of the
-// workgroup's dQ contribution (all 128 keys), added with one fp32 atomic per element.
+// Backward: a key-parallel dK/dV kernel and a query-parallel dQ kernel (see below) — no
+// atomics and no cross-workgroup reduction; both prefetch their next tile into registers.
 #include "common.h"
 
 using namespace pha;
@@ -42,7 +40,10 @@ template <> struct MF<bf16_t> {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
-    return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+    // plain conversions: hipcc lowers the pair to one v_cvt_pk_bf16_f32 (RNE) on gfx950
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
   }
 };
 template <> struct MF<half_t> {
@@ -51,8 +52,9 @@ template <> struct MF<half_t> {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
   }
   static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
-    _Float16 l = (_Float16)lo, h = (_Float16)hi;
-    return (uint32_t)__builtin_bit_cast(uint16_t, l) | ((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+    const f16x2 v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, v);
   }
 };
 
@@ -123,26 +125,60 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
   if (CAUSAL) kend = min(Sk, q0 + BM);
   const int wave_qmax = q0 + wid * 32 + 31;
 
-  for (int k0 = 0; k0 < kend; k0 += BN) {
-    __syncthreads();  // previous tile fully consumed
-    // ---- stage K (swizzled rows) and V^T into LDS --------------------------------
+  // ---- register-staged K/V pipeline (T14): tile t+1 is loaded into VGPRs while tile t is
+  // computed, and written to LDS after the next barrier.
+  //   K: 4 x 16-B chunks per thread (row-major, swizzled into LDS).
+  //   V: thread owns 4 consecutive keys x one 8-wide d chunk, so the transposed V^T image is
+  //      written with 8 ds_write_b64 (4 keys each) instead of 32 ds_write_b16.
+  constexpr int KCH = (BN * CH) / 256;          // K chunks per thread
+  constexpr int VITEMS = (BN / 4) * CH;          // (4-key group, d chunk) items
+  u32x4 kreg[KCH];
+  u32x4 vreg[4];
+  const int v_item = tid;                        // valid when tid < VITEMS
+  const int v_kg = v_item / CH, v_ch = v_item % CH;
+  auto load_tile = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < (BN * CH) / 256; ++i) {
+    for (int i = 0; i < KCH; ++i) {
       const int c = tid + 256 * i;
       const int row = c / CH, ch = c % CH;
       const int key = k0 + row;
-      u32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
-      if (key < Sk) {
-        kv = *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8);
-        vv = *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + ch * 8);
-      }
-      *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(row, ch)) = kv;
-      const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        *reinterpret_cast<uint16_t*>(vt_lds + (ch * 8 + e) * VT_STRIDE + row * 2) = ve[e];
+      kreg[i] = (key < Sk) ? *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
     }
+    if (v_item < VITEMS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + v_kg * 4 + j;
+        vreg[j] = (key < Sk) ? *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + v_ch * 8) : u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(c / CH, c % CH)) = kreg[i];
+    }
+    if (v_item < VITEMS) {
+      const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&vreg[0]);
+      const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&vreg[1]);
+      const uint16_t* e2 = reinterpret_cast<const uint16_t*>(&vreg[2]);
+      const uint16_t* e3 = reinterpret_cast<const uint16_t*>(&vreg[3]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        u32x2 w;
+        w[0] = (uint32_t)e0[e] | ((uint32_t)e1[e] << 16);
+        w[1] = (uint32_t)e2[e] | ((uint32_t)e3[e] << 16);
+        *reinterpret_cast<u32x2*>(vt_lds + (v_ch * 8 + e) * VT_STRIDE + v_kg * 8) = w;
+      }
+    }
+  };
+
+  if (kend > 0) load_tile(0);
+  for (int k0 = 0; k0 < kend; k0 += BN) {
+    __syncthreads();  // previous tile fully consumed
+    store_tile();
     __syncthreads();
+    if (k0 + BN < kend) load_tile(k0 + BN);     // in flight during this tile's MFMAs
     if (CAUSAL && k0 > wave_qmax) continue;  // whole tile masked for this wave (barriers stay uniform)
 
     // ---- S^T = K . Q^T for two 32-key blocks ------------------------------------------
@@ -156,23 +192,46 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
         s[kb] = MF<T>::mma(as_frag<frag>(a), qf[kk], s[kb]);
       }
     }
-    // ---- masking + online softmax (query on the lane) ---------------------------------
+    // ---- masking (only on diagonal / ragged tiles) + online softmax (query on the lane) ----
+    const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
     float tmax = -INFINITY;
+    if (need_mask) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = k0 + kb * 32 + acc_row(r, h);
-        float v = s[kb][r] * scale_log2;
-        const bool masked = (key >= Sk) || (CAUSAL && key > q);
-        v = masked ? -INFINITY : v;
-        s[kb][r] = v;
-        tmax = fmaxf(tmax, v);
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kb * 32 + acc_row(r, h);
+          const bool masked = (key >= Sk) || (CAUSAL && key > q);
+          const float v = masked ? -INFINITY : s[kb][r] * scale_log2;
+          s[kb][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = s[kb][r] * scale_log2;
+          s[kb][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+    }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    // deferred rescale (CDNA guide T13): keep the running max unless some row grew by more
+    // than kThr (log2 units) — P is then bounded by 2^kThr, harmless for bf16 P and fp32 l/O.
+    constexpr float kThr = 8.f;
+    if (!__all(tmax <= m_run + kThr)) {
+      const float m_new = fmaxf(m_run, tmax);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      m_run = m_new;
+    }
+    const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
     float psum = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -183,12 +242,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
         psum += p;
       }
     psum += __shfl_xor(psum, 32, 64);
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-#pragma unroll
-    for (int i = 0; i < ND; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    l_run += psum;
 
     // ---- O^T += V^T . P^T ---------------------------------------------------------------
 #pragma unroll
@@ -260,41 +314,62 @@ __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const T* __restrict__ O
   }
 }
 
-// Backward. Workgroup = 4 waves = 128 keys (wave w: keys k0 + 32w .. +31, key on the lane).
-// Per query tile of 32 rows (all 4 waves share it through LDS):
-//   S  = Q K^T       C[q][key]  (A = Q rows from LDS, B = K^T from registers)
-//   P  = exp2(S*c - lse*log2e)
-//   dP = dO V^T      C[q][key]  (A = dO rows from LDS, B = V^T from registers)
-//   dS = P (dP - delta)
-//   dV^T += dO^T P   (A = dO^T from LDS (transposed image), B = P  accumulator-as-operand)
-//   dK^T += Q^T dS   (A = Q^T  from LDS (transposed image), B = dS accumulator-as-operand)
-//   dQ  += dS K      (dS through LDS [q][key], B = K^T... K[key][d] from LDS transposed)
+// ============================================================================================
+// Backward = two kernels (no atomics, no cross-workgroup reduction):
+//
+//  fa_bwd_dkdv_kernel — key-parallel. Workgroup = 4 waves = 128 keys, key on the MFMA lane;
+//    each wave keeps its 32 keys' K/V fragments in registers and accumulates dK^T, dV^T over
+//    all query tiles (32 rows each; Q/dO tile t+1 prefetched into registers during tile t):
+//      S  = Q K^T, dP = dO V^T           C[q][key]  (A = Q / dO rows from LDS)
+//      P  = exp2(S c - lse), dS = P (dP - delta)    (row constants broadcast from LDS)
+//      dV^T += dO^T P, dK^T += Q^T dS    accumulator-as-B-operand; A = transposed images
+//
+//  fa_bwd_dq_kernel — query-parallel (the forward's structure). Workgroup = 4 waves = 128
+//    queries, query on the lane, Q/dO fragments in registers; per 64-key tile:
+//      S^T = K Q^T, dP^T = V dO^T        A = K / V rows (swizzled LDS)
+//      dS^T lane-local (the lane's own lse/delta), dQ^T += K^T dS^T (A = K^T image)
+// ============================================================================================
+
+// transposed 4-row gather: 4 rows x one 8-wide chunk (4 x u32x4) -> 8 x u32x2 (4 rows each)
+__device__ __forceinline__ void write_t4(unsigned char* img, int row_stride_bytes, int chunk, int row0,
+                                         const u32x4 (&r)[4]) {
+  const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&r[0]);
+  const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&r[1]);
+  const uint16_t* e2 = reinterpret_cast<const uint16_t*>(&r[2]);
+  const uint16_t* e3 = reinterpret_cast<const uint16_t*>(&r[3]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    u32x2 w;
+    w[0] = (uint32_t)e0[e] | ((uint32_t)e1[e] << 16);
+    w[1] = (uint32_t)e2[e] | ((uint32_t)e3[e] << 16);
+    *reinterpret_cast<u32x2*>(img + (chunk * 8 + e) * row_stride_bytes + row0 * 2) = w;
+  }
+}
+
 template <typename T, int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void fa_bwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
-                                                     const T* __restrict__ V, const T* __restrict__ dO,
-                                                     const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                     float* __restrict__ dQ, T* __restrict__ dK, T* __restrict__ dV,
-                                                     int S, int Sk, int H, int Hk, float scale) {
+__global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                          const T* __restrict__ V, const T* __restrict__ dO,
+                                                          const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                          T* __restrict__ dK, T* __restrict__ dV,
+                                                          int S, int Sk, int H, int Hk, float scale) {
   typedef typename MF<T>::frag frag;
   constexpr int NK = D / 16;
   constexpr int ND = D / 32;
-  constexpr int BQ = 32;                      // query rows per iteration
-  constexpr int ROWB = D * 2 + 16;            // padded row bytes for Q/dO row images [q][d]
-  constexpr int TB = (BQ + 8) * 2;            // padded row bytes for transposed images [d][q]
-  constexpr int KTB = (128 + 8) * 2;          // K^T image rows [d][key] for the workgroup's 128 keys
-  constexpr int DSB = (128 + 8) * 2;          // dS image rows [q][key]
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BQ * ROWB + 2 * D * TB + D * KTB + BQ * DSB];
-  unsigned char* q_lds = smem;                       // [32][D] rows
-  unsigned char* do_lds = q_lds + BQ * ROWB;         // [32][D] rows
-  unsigned char* qt_lds = do_lds + BQ * ROWB;        // [D][32]
-  unsigned char* dot_lds = qt_lds + D * TB;          // [D][32]
-  unsigned char* kt_lds = dot_lds + D * TB;          // [D][128]
-  unsigned char* ds_lds = kt_lds + D * KTB;          // [32][128]
+  constexpr int CH = D / 8;
+  constexpr int BQ = 32;
+  constexpr int ROWB = D * 2 + 16;            // [q][d] row images (16-B pad)
+  constexpr int TB = (BQ + 4) * 2;            // [d][q] transposed images (row = 72 B)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BQ * ROWB + 2 * D * TB + 2 * BQ * 4];
+  unsigned char* q_lds = smem;
+  unsigned char* do_lds = q_lds + BQ * ROWB;
+  unsigned char* qt_lds = do_lds + BQ * ROWB;
+  unsigned char* dot_lds = qt_lds + D * TB;
+  float* lse_lds = reinterpret_cast<float*>(dot_lds + D * TB);
+  float* del_lds = lse_lds + BQ;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int head = blockIdx.y, b = blockIdx.z;
-  const int group = H / Hk;
-  const int hk = head / group;
+  const int hk = head / (H / Hk);
   const int k0 = blockIdx.x * 128;
   const int key = k0 + wid * 32 + lr;
   const long qstride = (long)H * D, kstride = (long)Hk * D;
@@ -306,7 +381,6 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const T* __restrict__ Q, co
   const float* del_b = DELTA + ((long)b * H + head) * S;
   const float scale_log2 = scale * kLog2e;
 
-  // K^T / V^T fragments for this wave's keys (B operands: B[k=d][col=key] = K[key][d])
   frag kf[NK], vf[NK];
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
@@ -318,126 +392,106 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const T* __restrict__ Q, co
     kf[kk] = as_frag<frag>(a);
     vf[kk] = as_frag<frag>(c);
   }
-  // K^T image of the workgroup's 128 keys for the dQ product (B[k=key][col=d] = K[key][d])
-  for (int c = tid; c < 128 * (D / 8); c += 256) {
-    const int row = c / (D / 8), ch = c % (D / 8);
-    const int kk = k0 + row;
-    u32x4 v = {0, 0, 0, 0};
-    if (kk < Sk) v = *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + ch * 8);
-    const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<uint16_t*>(kt_lds + (ch * 8 + i) * KTB + row * 2) = e[i];
-  }
-
   f32x16 dvt[ND], dkt[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
 
-  int qstart = 0;
-  if (CAUSAL) qstart = (k0 / BQ) * BQ;
-  for (int qt = qstart; qt < S; qt += BQ) {
-    __syncthreads();
-    // stage Q, dO rows and their transposed images
-    for (int c = tid; c < BQ * (D / 8); c += 256) {
-      const int row = c / (D / 8), ch = c % (D / 8);
-      const int qq = qt + row;
-      u32x4 a = {0, 0, 0, 0}, g = {0, 0, 0, 0};
-      if (qq < S) {
-        a = *reinterpret_cast<const u32x4*>(Qb + (long)qq * qstride + ch * 8);
-        g = *reinterpret_cast<const u32x4*>(dOb + (long)qq * qstride + ch * 8);
-      }
-      *reinterpret_cast<u32x4*>(q_lds + row * ROWB + ch * 16) = a;
-      *reinterpret_cast<u32x4*>(do_lds + row * ROWB + ch * 16) = g;
-      const uint16_t* ea = reinterpret_cast<const uint16_t*>(&a);
-      const uint16_t* eg = reinterpret_cast<const uint16_t*>(&g);
+  // staging item: threads [0, 8*CH) own (4-row group, chunk) of Q, the next 8*CH of dO
+  constexpr int ITEMS = (BQ / 4) * CH;        // per tensor (D=128: 128, D=64: 64)
+  const bool is_q = tid < ITEMS;
+  const bool is_do = tid >= ITEMS && tid < 2 * ITEMS;
+  const int it = is_q ? tid : tid - ITEMS;
+  const int rg = it / CH, ch = it % CH;
+  u32x4 sreg[4];
+  float srow = 0.f;
+  auto load_tile = [&](int qt) {
+    if (is_q || is_do) {
+      const T* src = is_q ? Qb : dOb;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        *reinterpret_cast<uint16_t*>(qt_lds + (ch * 8 + i) * TB + row * 2) = ea[i];
-        *reinterpret_cast<uint16_t*>(dot_lds + (ch * 8 + i) * TB + row * 2) = eg[i];
+      for (int j = 0; j < 4; ++j) {
+        const int qq = qt + rg * 4 + j;
+        sreg[j] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8) : u32x4{0, 0, 0, 0};
       }
     }
-    __syncthreads();
-
-    const bool active = !(CAUSAL && (k0 + wid * 32) > (qt + BQ - 1));
-    f32x16 sacc = zero16(), dpacc = zero16();
-    if (active) {
+    if (tid < 2 * BQ) {
+      const int qq = qt + (tid & (BQ - 1));
+      srow = (qq < S) ? (tid < BQ ? lse_b[qq] : del_b[qq]) : 0.f;
+    }
+  };
+  auto store_tile = [&]() {
+    if (is_q || is_do) {
+      unsigned char* rows = is_q ? q_lds : do_lds;
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const u32x4 qa = *reinterpret_cast<const u32x4*>(q_lds + lr * ROWB + (2 * kk + h) * 16);
-        const u32x4 ga = *reinterpret_cast<const u32x4*>(do_lds + lr * ROWB + (2 * kk + h) * 16);
-        sacc = MF<T>::mma(as_frag<frag>(qa), kf[kk], sacc);
-        dpacc = MF<T>::mma(as_frag<frag>(ga), vf[kk], dpacc);
-      }
-      // P and dS; rows = queries qt + acc_row(r,h), column = key (lane)
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(rows + (rg * 4 + j) * ROWB + ch * 16) = sreg[j];
+      write_t4(is_q ? qt_lds : dot_lds, TB, ch, rg * 4, sreg);
+    }
+    if (tid < 2 * BQ) (tid < BQ ? lse_lds : del_lds)[tid & (BQ - 1)] = srow;
+  };
+
+  const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
+  if (qstart < S) load_tile(qstart);
+  for (int qt = qstart; qt < S; qt += BQ) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (qt + BQ < S) load_tile(qt + BQ);
+    if (CAUSAL && (k0 + wid * 32) > (qt + BQ - 1)) continue;   // no query of this tile sees these keys
+
+    f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const u32x4 qa = *reinterpret_cast<const u32x4*>(q_lds + lr * ROWB + (2 * kk + h) * 16);
+      const u32x4 ga = *reinterpret_cast<const u32x4*>(do_lds + lr * ROWB + (2 * kk + h) * 16);
+      sacc = MF<T>::mma(as_frag<frag>(qa), kf[kk], sacc);
+      dpacc = MF<T>::mma(as_frag<frag>(ga), vf[kk], dpacc);
+    }
+    const bool need_mask = (qt + BQ > S) || (k0 + 128 > Sk) || (CAUSAL && k0 + wid * 32 + 31 > qt);
+    if (need_mask) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qq = qt + acc_row(r, h);
+        const int ql = acc_row(r, h);
+        const int qq = qt + ql;
         float p = 0.f, ds = 0.f;
         if (qq < S && key < Sk && !(CAUSAL && key > qq)) {
-          p = exp2f(sacc[r] * scale_log2 - lse_b[qq] * kLog2e);
-          ds = p * (dpacc[r] - del_b[qq]);
+          p = exp2f(sacc[r] * scale_log2 - lse_lds[ql] * kLog2e);
+          ds = p * (dpacc[r] - del_lds[ql]);
         }
         sacc[r] = p;
         dpacc[r] = ds;
       }
-      // dS image for dQ: ds_lds[q][key_local]
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        T* dst = reinterpret_cast<T*>(ds_lds + acc_row(r, h) * DSB + (wid * 32 + lr) * 2);
-        Cvt<T>::st(dst, 0, dpacc[r]);
-      }
-      // dV^T += dO^T P ; dK^T += Q^T dS  (sum over q = accumulator row index)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        u32x4 pw, dw;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pw[j] = MF<T>::pack(sacc[8 * s + 2 * j], sacc[8 * s + 2 * j + 1]);
-          dw[j] = MF<T>::pack(dpacc[8 * s + 2 * j], dpacc[8 * s + 2 * j + 1]);
-        }
-        const int qbase = 16 * s + 4 * h;
-#pragma unroll
-        for (int db = 0; db < ND; ++db) {
-          const unsigned char* r1 = dot_lds + (db * 32 + lr) * TB;
-          const unsigned char* r2 = qt_lds + (db * 32 + lr) * TB;
-          const u32x2 a0 = *reinterpret_cast<const u32x2*>(r1 + qbase * 2);
-          const u32x2 a1 = *reinterpret_cast<const u32x2*>(r1 + (qbase + 8) * 2);
-          const u32x2 b0 = *reinterpret_cast<const u32x2*>(r2 + qbase * 2);
-          const u32x2 b1 = *reinterpret_cast<const u32x2*>(r2 + (qbase + 8) * 2);
-          const u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
-          const u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
-          dvt[db] = MF<T>::mma(as_frag<frag>(av), as_frag<frag>(pw), dvt[db]);
-          dkt[db] = MF<T>::mma(as_frag<frag>(bv), as_frag<frag>(dw), dkt[db]);
-        }
-      }
     } else {
-      // inactive wave still publishes zeros for its dS columns
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        T* dst = reinterpret_cast<T*>(ds_lds + acc_row(r, h) * DSB + (wid * 32 + lr) * 2);
-        Cvt<T>::st(dst, 0, 0.f);
+        const int ql = acc_row(r, h);
+        const float p = exp2f(sacc[r] * scale_log2 - lse_lds[ql] * kLog2e);
+        sacc[r] = p;
+        dpacc[r] = p * (dpacc[r] - del_lds[ql]);
       }
     }
-    __syncthreads();
-    // dQ[32 q][D] += dS[32][128 keys] . K[128][D]: wave w computes d-block(s) w (and w+4 if D>128)
-    for (int db = wid; db < ND; db += 4) {
-      f32x16 acc = zero16();
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {  // 128 keys = 8 k-steps of 16
-        const u32x4 a = *reinterpret_cast<const u32x4*>(ds_lds + lr * DSB + (16 * ks + 8 * h) * 2);
-        const unsigned char* kr = kt_lds + (db * 32 + lr) * KTB + (16 * ks + 8 * h) * 2;
-        const u32x4 bb = *reinterpret_cast<const u32x4*>(kr);
-        acc = MF<T>::mma(as_frag<frag>(a), as_frag<frag>(bb), acc);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 pw, dw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pw[j] = MF<T>::pack(sacc[8 * s2 + 2 * j], sacc[8 * s2 + 2 * j + 1]);
+        dw[j] = MF<T>::pack(dpacc[8 * s2 + 2 * j], dpacc[8 * s2 + 2 * j + 1]);
       }
-      // acc: C[q][d] rows = q, col = d (lane)
+      const int qbase = 16 * s2 + 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qq = qt + acc_row(r, h);
-        if (qq < S) atomicAdd(dQ + (((long)b * S + qq) * H + head) * D + db * 32 + lr, acc[r] * scale);
+      for (int db = 0; db < ND; ++db) {
+        const unsigned char* r1 = dot_lds + (db * 32 + lr) * TB;
+        const unsigned char* r2 = qt_lds + (db * 32 + lr) * TB;
+        const u32x2 a0 = *reinterpret_cast<const u32x2*>(r1 + qbase * 2);
+        const u32x2 a1 = *reinterpret_cast<const u32x2*>(r1 + (qbase + 8) * 2);
+        const u32x2 b0 = *reinterpret_cast<const u32x2*>(r2 + qbase * 2);
+        const u32x2 b1 = *reinterpret_cast<const u32x2*>(r2 + (qbase + 8) * 2);
+        const u32x4 av = {a0[0], a0[1], a1[0], a1[1]};
+        const u32x4 bv = {b0[0], b0[1], b1[0], b1[1]};
+        dvt[db] = MF<T>::mma(as_frag<frag>(av), as_frag<frag>(pw), dvt[db]);
+        dkt[db] = MF<T>::mma(as_frag<frag>(bv), as_frag<frag>(dw), dkt[db]);
       }
     }
   }
-  // ---- store dK, dV (rows = d, col = key on the lane) ----------------------------------
   if (key < Sk) {
     T* dkr = dK + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;   // dK/dV are [B, Sk, H, D]
     T* dvr = dV + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;
@@ -448,6 +502,162 @@ __global__ __launch_bounds__(256) void fa_bwd_kernel(const T* __restrict__ Q, co
         const int d = db * 32 + acc_row(r, h);
         Cvt<T>::st(dkr, d, dkt[db][r] * scale);
         Cvt<T>::st(dvr, d, dvt[db][r]);
+      }
+  }
+}
+
+template <typename T, int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                        const T* __restrict__ V, const T* __restrict__ dO,
+                                                        const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                        T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale) {
+  typedef typename MF<T>::frag frag;
+  constexpr int CH = D / 8;
+  constexpr int ND = D / 32;
+  constexpr int NK = D / 16;
+  constexpr int KT_STRIDE = (BN + VT_PAD) * 2;  // K^T image row bytes
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BN * D * 2 + D * KT_STRIDE];
+  unsigned char* k_lds = smem;                  // K rows (swizzled)
+  unsigned char* v_lds = smem + BN * D * 2;     // V rows (swizzled)
+  unsigned char* kt_lds = v_lds + BN * D * 2;   // K^T [d][key]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
+  const int nqb = (S + BM - 1) / BM;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM;
+  const int q = q0 + wid * 32 + lr;
+  const long qstride = (long)H * D, kstride = (long)Hk * D;
+  const T* Qb = Q + (long)b * S * qstride + (long)head * D;
+  const T* dOb = dO + (long)b * S * qstride + (long)head * D;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * D;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * D;
+  const float scale_log2 = scale * kLog2e;
+  const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
+  const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
+
+  frag qf[NK], gf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, g = {0, 0, 0, 0};
+    if (q < S) {
+      a = *reinterpret_cast<const u32x4*>(Qb + (long)q * qstride + 16 * kk + 8 * h);
+      g = *reinterpret_cast<const u32x4*>(dOb + (long)q * qstride + 16 * kk + 8 * h);
+    }
+    qf[kk] = as_frag<frag>(a);
+    gf[kk] = as_frag<frag>(g);
+  }
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = zero16();
+
+  // staging: K as (4-key group, chunk) items -> K rows + K^T image; V as 16-B row chunks
+  constexpr int KITEMS = (BN / 4) * CH;
+  constexpr int VCH = (BN * CH) / 256;
+  const int kg = tid / CH, kch = tid % CH;
+  u32x4 kreg[4];
+  u32x4 vreg[VCH];
+  auto load_tile = [&](int k0) {
+    if (tid < KITEMS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k0 + kg * 4 + j;
+        kreg[j] = (kk < Sk) ? *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + kch * 8) : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + 256 * i;
+      const int kk = k0 + c / CH;
+      vreg[i] = (kk < Sk) ? *reinterpret_cast<const u32x4*>(Vb + (long)kk * kstride + (c % CH) * 8) : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_tile = [&]() {
+    if (tid < KITEMS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(kg * 4 + j, kch)) = kreg[j];
+      write_t4(kt_lds, KT_STRIDE, kch, kg * 4, kreg);
+    }
+#pragma unroll
+    for (int i = 0; i < VCH; ++i) {
+      const int c = tid + 256 * i;
+      *reinterpret_cast<u32x4*>(v_lds + k_lds_off<D>(c / CH, c % CH)) = vreg[i];
+    }
+  };
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM);
+  const int wave_qmax = q0 + wid * 32 + 31;
+  if (kend > 0) load_tile(0);
+  for (int k0 = 0; k0 < kend; k0 += BN) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (k0 + BN < kend) load_tile(k0 + BN);
+    if (CAUSAL && k0 > wave_qmax) continue;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s[kb] = zero16();
+      dp[kb] = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(k_lds + k_lds_off<D>(kb * 32 + lr, 2 * kk + h));
+        const u32x4 c = *reinterpret_cast<const u32x4*>(v_lds + k_lds_off<D>(kb * 32 + lr, 2 * kk + h));
+        s[kb] = MF<T>::mma(as_frag<frag>(a), qf[kk], s[kb]);
+        dp[kb] = MF<T>::mma(as_frag<frag>(c), gf[kk], dp[kb]);
+      }
+    }
+    const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kk = k0 + kb * 32 + acc_row(r, h);
+          const bool ok = (kk < Sk) && !(CAUSAL && kk > q);
+          const float p = ok ? exp2f(s[kb][r] * scale_log2 - lse2) : 0.f;
+          s[kb][r] = p * (dp[kb][r] - dlt);   // dS^T
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = exp2f(s[kb][r] * scale_log2 - lse2) * (dp[kb][r] - dlt);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const f32x16& sv = s[ks >> 1];
+      const int s8 = (ks & 1) * 8;
+      u32x4 pw;
+      pw[0] = MF<T>::pack(sv[s8 + 0], sv[s8 + 1]);
+      pw[1] = MF<T>::pack(sv[s8 + 2], sv[s8 + 3]);
+      pw[2] = MF<T>::pack(sv[s8 + 4], sv[s8 + 5]);
+      pw[3] = MF<T>::pack(sv[s8 + 6], sv[s8 + 7]);
+      const frag pf = as_frag<frag>(pw);
+      const int kbase = 16 * ks + 4 * h;
+#pragma unroll
+      for (int db = 0; db < ND; ++db) {
+        const unsigned char* row = kt_lds + (db * 32 + lr) * KT_STRIDE;
+        const u32x2 lo = *reinterpret_cast<const u32x2*>(row + kbase * 2);
+        const u32x2 hi = *reinterpret_cast<const u32x2*>(row + (kbase + 8) * 2);
+        const u32x4 a = {lo[0], lo[1], hi[0], hi[1]};
+        dq[db] = MF<T>::mma(as_frag<frag>(a), pf, dq[db]);
+      }
+    }
+  }
+  if (q < S) {
+    T* qrow = dQ + ((long)b * S + q) * qstride + (long)head * D;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = db * 32 + 8 * g + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(dq[db][4 * g + 0] * scale, dq[db][4 * g + 1] * scale);
+        w[1] = MF<T>::pack(dq[db][4 * g + 2] * scale, dq[db][4 * g + 3] * scale);
+        *reinterpret_cast<u32x2*>(qrow + d) = w;
       }
   }
 }
@@ -467,12 +677,16 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
 
 template <typename T>
 int launch_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
-               float* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
+               void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
                hipStream_t st) {
-  const dim3 grid((Sk + 127) / 128, H, B), block(256);
-#define FB_L(DD, CC) hipLaunchKernelGGL((fa_bwd_kernel<T, DD, CC>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta, dq, (T*)dk, (T*)dv, S, Sk, H, Hk, scale)
-  if (D == 128) { if (causal) FB_L(128, true); else FB_L(128, false); }
-  else if (D == 64) { if (causal) FB_L(64, true); else FB_L(64, false); }
+  const dim3 gkv((Sk + 127) / 128, H, B), gq((S + BM - 1) / BM, H, B), block(256);
+#define FB_L(DD, CC)                                                                                               \
+  hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, DD, CC>), gkv, block, 0, st, (const T*)q, (const T*)k, (const T*)v,   \
+                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale);                              \
+  hipLaunchKernelGGL((fa_bwd_dq_kernel<T, DD, CC>), gq, block, 0, st, (const T*)q, (const T*)k, (const T*)v,       \
+                     (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale)
+  if (D == 128) { if (causal) { FB_L(128, true); } else { FB_L(128, false); } }
+  else if (D == 64) { if (causal) { FB_L(64, true); } else { FB_L(64, false); } }
   else return (int)hipErrorInvalidValue;
 #undef FB_L
   return (int)hipGetLastError();
@@ -504,10 +718,10 @@ PHA_API int pha_flash_attn_bwd_preprocess(int dt, const void* o, const void* dou
   return (int)hipGetLastError();
 }
 
-// dq: fp32 [B, S, H, D] zero-initialised by the caller; dk/dv: [B, Sk, H, D] (per query head;
-// the caller sums head groups for GQA).
+// dq: [B, S, H, D] (same dtype as q); dk/dv: [B, Sk, H, D] (per query head; the caller sums
+// head groups for GQA).
 PHA_API int pha_flash_attn_bwd(int dt, const void* q, const void* k, const void* v, const void* dout, const float* lse,
-                               const float* delta, float* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
+                               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
                                int D, float scale, int causal, hipStream_t stream) {
   if (H % Hk || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_bwd<bf16_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);

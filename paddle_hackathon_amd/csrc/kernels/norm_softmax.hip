@@ -150,14 +150,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
-// sum partials [P, H] over P -> out [H] (cast to W)
+// sum partials [P, H] over P -> out [H] (cast to W). 64 columns per block (one per lane, so
+// every row read is a coalesced 256-B segment), the 4 waves split the P rows.
 template <typename W>
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, W* __restrict__ out, int P, int H) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= H) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * H + col];
-  Cvt<W>::st(out, col, s);
+  if (col < H)
+    for (int p = w; p < P; p += 4) s += part[(long)p * H + col];
+  __shared__ float red[4][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < H) Cvt<W>::st(out, col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
 template <typename T, int NCH>
@@ -300,16 +305,16 @@ PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, c
                            (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
       });
       if (rc) return rc;
-      hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 255) / 256), dim3(256), 0, stream, part_w, (float*)dw, nblocks, H);
-      if (db) hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 255) / 256), dim3(256), 0, stream, part_b, (float*)db, nblocks, H);
+      hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (float*)dw, nblocks, H);
+      if (db) hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_b, (float*)db, nblocks, H);
     } else {
       rc = dispatch_nch_small(H, [&](auto nch) {
         hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
                            (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
       });
       if (rc) return rc;
-      hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, stream, part_w, (T*)dw, nblocks, H);
-      if (db) hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 255) / 256), dim3(256), 0, stream, part_b, (T*)db, nblocks, H);
+      hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (T*)dw, nblocks, H);
+      if (db) hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, stream, part_b, (T*)db, nblocks, H);
     }
   });
   return rc ? rc : (int)hipGetLastError();

@@ -86,7 +86,7 @@ def layer_norm_fwd(x, w, b, eps):
 def layer_norm_bwd(dy, x, w, mean, rstd, has_bias):
     H = w.numel()
     rows = x.numel() // H
-    nblocks = max(1, min((rows + 3) // 4, 1024))
+    nblocks = max(1, min((rows + 3) // 4, 256))   # one block per CU; partials [256, H]
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     db = torch.empty_like(w) if has_bias else None
@@ -348,15 +348,14 @@ class FlashAttention(torch.autograd.Function):
         Sk, Hk = k.shape[1], k.shape[2]
         L = _L()
         delta = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
-        dq_acc = torch.zeros((B, S, H, D), dtype=torch.float32, device=q.device)
+        dq = torch.empty_like(q)
         dk = torch.empty_like(k) if Hk == H else torch.empty((B, Sk, H, D), dtype=k.dtype, device=k.device)
         dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S), c_int(H), c_int(D),
                                                _stream(q)), "flash_attn_bwd_preprocess")
-        _check(L.pha_flash_attn_bwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq_acc),
+        _check(L.pha_flash_attn_bwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq),
                                     _ptr(dk), _ptr(dv), c_int(B), c_int(S), c_int(Sk), c_int(H), c_int(Hk), c_int(D),
                                     c_float(ctx.scale), c_int(int(ctx.causal)), _stream(q)), "flash_attn_bwd")
-        dq = dq_acc.to(q.dtype)
         if Hk != H:
             g = H // Hk
             dk = dk.view(B, Sk, Hk, g, D).sum(3)

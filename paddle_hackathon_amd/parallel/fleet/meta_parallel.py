@@ -5,5 +5,7 @@ from ..pipeline import LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParall
 
 
 def __getattr__(name):
-    from . import TensorParallel, ShardingParallel
-    return {"TensorParallel": TensorParallel, "ShardingParallel": ShardingParallel}[name]
+    if name in ("TensorParallel", "ShardingParallel"):
+        from . import TensorParallel, ShardingParallel
+        return {"TensorParallel": TensorParallel, "ShardingParallel": ShardingParallel}[name]
+    raise AttributeError(name)
