@@ -61,7 +61,10 @@ _LAZY = {
 
 def __getattr__(name):
     if name in _LAZY:
-        mod = importlib.import_module(_LAZY[name], __name__)
+        try:
+            mod = importlib.import_module(_LAZY[name], __name__)
+        except ImportError as e:
+            raise AttributeError(f"paddle_hackathon_amd.{name} unavailable: {e}") from e
         if name in ("Model", "summary", "flops", "enable_static", "disable_static", "batch"):
             return getattr(mod, name)
         globals()[name] = mod

@@ -1,0 +1,800 @@
+"""Static graph: Program / Block / Variable, recording and the replay Executor
+(reference: python/paddle/fluid/framework.py, executor.py, backward.py, compiler.py;
+paddle/fluid/framework/{program_desc,block_desc,op_desc,executor,new_executor/*}).
+
+Recording: in static mode every public op call whose arguments contain a ``Variable``
+appends an ``OpDesc`` (op type = qualified op name, bound arguments, output Variables)
+to the current block; output shapes/dtypes come from running the op on ``meta``
+tensors (our InferMeta). Parameters are real device tensors living in the global scope.
+
+Execution: ``Executor.run`` interprets the op list against a value environment —
+feeds bound to data Variables, parameters by reference — so autograd, the HIP kernels
+and the fused optimizers run exactly as in dynamic mode. ``CompiledProgram`` can freeze
+a forward-only program into a HIP graph (torch.cuda.CUDAGraph on ROCm) replayed per run.
+
+Serialisation: programs are lists of registered op names + JSON-able argument trees, so a
+program round-trips through ``serialize_program`` / ``save_inference_model``.
+"""
+from __future__ import annotations
+
+import contextlib
+import copy
+import inspect
+import itertools
+import json
+
+import numpy as np
+import torch
+
+from ..framework import core as _core
+from ..framework.core import Tensor, Parameter, _wrap, convert_dtype, dtype_to_str
+
+__all__ = ["Variable", "Program", "Block", "OpDesc", "record_op", "default_main_program", "default_startup_program",
+           "program_guard", "data", "Executor", "global_scope", "scope_guard", "append_backward", "gradients",
+           "minimize_static", "enable_static", "disable_static", "name_scope", "OP_REGISTRY", "CompiledProgram",
+           "BuildStrategy", "ExecutionStrategy", "InputSpec", "Scope"]
+
+OP_REGISTRY = {}
+_var_ids = itertools.count()
+
+
+class InputSpec:
+    """Shape/dtype/name of a program input (reference: python/paddle/static/input.py)."""
+
+    def __init__(self, shape, dtype="float32", name=None, stop_gradient=False):
+        self.shape = [(-1 if s is None else int(s)) for s in shape]
+        self.dtype = convert_dtype(dtype)
+        self.name = name
+        self.stop_gradient = stop_gradient
+
+    @classmethod
+    def from_tensor(cls, tensor, name=None):
+        return cls(tensor.shape, tensor.dtype, name or tensor.name)
+
+    @classmethod
+    def from_numpy(cls, ndarray, name=None):
+        return cls(ndarray.shape, ndarray.dtype, name)
+
+    def batch(self, batch_size):
+        return InputSpec([batch_size] + self.shape, self.dtype, self.name)
+
+    def unbatch(self):
+        return InputSpec(self.shape[1:], self.dtype, self.name)
+
+    def __repr__(self):
+        return f"InputSpec(shape={self.shape}, dtype={self.dtype}, name={self.name})"
+
+    def __eq__(self, other):
+        return isinstance(other, InputSpec) and (self.shape, self.dtype, self.name) == (other.shape, other.dtype, other.name)
+
+    def __hash__(self):
+        return hash((tuple(self.shape), self.dtype, self.name))
+
+
+class Variable(Tensor):
+    """A symbolic tensor of a static Program. ``_t`` is a meta tensor (shape/dtype only)."""
+
+    __slots__ = ()
+
+    def __init__(self, block, meta, name=None, declared_shape=None, is_data=False, persistable=False, stop_gradient=True):
+        self._t = meta
+        self._name = name or f"_generated_var_{next(_var_ids)}"
+        self._persistable = persistable
+        self.block = block
+        self.is_data = is_data
+        self.declared_shape = declared_shape
+        self.need_grad = not stop_gradient
+        self.op = None
+
+    @property
+    def shape(self):
+        if self.declared_shape is not None:
+            return list(self.declared_shape)
+        return list(self._t.shape)
+
+    @property
+    def stop_gradient(self):
+        return not self.need_grad
+
+    @stop_gradient.setter
+    def stop_gradient(self, v):
+        self.need_grad = not v
+
+    def numpy(self):
+        raise RuntimeError("a static Variable has no value; fetch it with Executor.run")
+
+    def __repr__(self):
+        return f"Variable(name={self.name}, shape={self.shape}, dtype={dtype_to_str(self._t.dtype)})"
+
+    def __bool__(self):
+        raise TypeError("a static Variable has no truth value; use paddle.static.nn.cond")
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __deepcopy__(self, memo):
+        return self
+
+    def to_string(self, throw_on_error=False, with_details=False):
+        return repr(self)
+
+
+class OpDesc:
+    __slots__ = ("type", "fn", "args", "kwargs", "outputs", "attrs")
+
+    def __init__(self, type, fn, args, kwargs, outputs, attrs=None):
+        self.type, self.fn, self.args, self.kwargs, self.outputs = type, fn, args, kwargs, outputs
+        self.attrs = attrs or {}
+
+    def input_arg_names(self):
+        return [v.name for v in _iter_vars((self.args, self.kwargs))]
+
+    def output_arg_names(self):
+        return [v.name for v in _iter_vars(self.outputs)]
+
+    def __repr__(self):
+        return f"{{{', '.join(self.output_arg_names())}}} = {self.type}({', '.join(self.input_arg_names())})"
+
+
+class Block:
+    def __init__(self, program, idx=0, parent_idx=-1):
+        self.program, self.idx, self.parent_idx = program, idx, parent_idx
+        self.ops = []
+        self.vars = {}
+
+    def var(self, name):
+        return self.vars[name]
+
+    def has_var(self, name):
+        return name in self.vars
+
+    def all_parameters(self):
+        return [v for v in self.vars.values() if isinstance(v, Parameter)]
+
+    def append_op(self, op):
+        self.ops.append(op)
+        return op
+
+    def create_var(self, name=None, shape=None, dtype="float32", persistable=False, **kw):
+        meta = torch.empty([1 if s in (None, -1) else s for s in (shape or [])], dtype=convert_dtype(dtype), device="meta")
+        v = Variable(self, meta, name, declared_shape=shape, persistable=persistable)
+        self.vars[v.name] = v
+        return v
+
+    def __repr__(self):
+        return "\n".join(repr(o) for o in self.ops)
+
+
+class Program:
+    _ids = itertools.count()
+
+    def __init__(self):
+        self.blocks = [Block(self)]
+        self.random_seed = 0
+        self._id = next(Program._ids)
+        self._is_test = False
+        self._hip_graph_cache = {}
+
+    def global_block(self):
+        return self.blocks[0]
+
+    def block(self, i):
+        return self.blocks[i]
+
+    def current_block(self):
+        return self.blocks[-1]
+
+    @property
+    def num_blocks(self):
+        return len(self.blocks)
+
+    def list_vars(self):
+        return list(self.global_block().vars.values())
+
+    def all_parameters(self):
+        seen, out = set(), []
+        for op in self.global_block().ops:
+            for a in _iter_tensors((op.args, op.kwargs)):
+                if isinstance(a, Parameter) and id(a) not in seen:
+                    seen.add(id(a))
+                    out.append(a)
+        return out
+
+    def clone(self, for_test=False):
+        p = Program()
+        p.random_seed = self.random_seed
+        blk = p.global_block()
+        blk.vars = dict(self.global_block().vars)
+        for op in self.global_block().ops:
+            if for_test and op.type.startswith("@"):
+                continue   # drop backward / optimizer ops
+            kwargs = dict(op.kwargs)
+            if for_test:
+                for k in ("training", "is_test"):
+                    if k in kwargs:
+                        kwargs[k] = (k == "is_test")
+                if "use_global_stats" in kwargs and "training" in op.kwargs:
+                    pass
+            blk.ops.append(OpDesc(op.type, op.fn, op.args, kwargs, op.outputs, dict(op.attrs)))
+        p._is_test = for_test
+        return p
+
+    def __repr__(self):
+        return f"Program(ops={len(self.global_block().ops)})\n" + repr(self.global_block())
+
+    to_string = lambda self, throw_on_error=False, with_details=False: repr(self)  # noqa: E731
+
+    def state_dict(self, mode="all", scope=None):
+        return {p.name: p for p in self.all_parameters()}
+
+    def set_state_dict(self, state_dict, scope=None):
+        own = {p.name: p for p in self.all_parameters()}
+        for k, v in state_dict.items():
+            if k in own:
+                own[k].set_value(v.numpy() if isinstance(v, Tensor) else np.asarray(v))
+
+    def _prune(self, targets):
+        p = self.clone()
+        targets = targets if isinstance(targets, (list, tuple)) else [targets]
+        p.global_block().ops = prune_ops(p.global_block().ops, [t for t in targets if isinstance(t, Variable)])
+        return p
+
+
+class _State:
+    main = None
+    startup = None
+
+
+_state = _State()
+_state.main = Program()
+_state.startup = Program()
+
+
+def default_main_program():
+    return _state.main
+
+
+def default_startup_program():
+    return _state.startup
+
+
+@contextlib.contextmanager
+def program_guard(main_program, startup_program=None):
+    old_main, old_startup = _state.main, _state.startup
+    _state.main = main_program
+    if startup_program is not None:
+        _state.startup = startup_program
+    try:
+        yield
+    finally:
+        _state.main, _state.startup = old_main, old_startup
+
+
+@contextlib.contextmanager
+def name_scope(prefix=None):
+    yield
+
+
+def enable_static():
+    _core._mode.static = True
+
+
+def disable_static(place=None):
+    _core._mode.static = False
+    if place is not None:
+        _core.set_device(place)
+
+
+# ----------------------------------------------------------------------------- data
+def data(name, shape, dtype=None, lod_level=0):
+    dt = convert_dtype(dtype) or _core._default_dtype
+    shape = [(-1 if s is None else int(s)) for s in shape]
+    meta = torch.empty([1 if s == -1 else s for s in shape], dtype=dt, device="meta")
+    blk = default_main_program().global_block()
+    v = Variable(blk, meta, name, declared_shape=shape, is_data=True)
+    blk.vars[name] = v
+    return v
+
+
+# ----------------------------------------------------------------------------- recording
+def _iter_vars(tree):
+    if isinstance(tree, Variable):
+        yield tree
+    elif isinstance(tree, (list, tuple)):
+        for t in tree:
+            yield from _iter_vars(t)
+    elif isinstance(tree, dict):
+        for t in tree.values():
+            yield from _iter_vars(t)
+
+
+def _iter_tensors(tree):
+    if isinstance(tree, Tensor):
+        yield tree
+    elif isinstance(tree, (list, tuple)):
+        for t in tree:
+            yield from _iter_tensors(t)
+    elif isinstance(tree, dict):
+        for t in tree.values():
+            yield from _iter_tensors(t)
+
+
+def _has_var(tree):
+    return next(_iter_vars(tree), None) is not None
+
+
+def _to_meta(tree):
+    if isinstance(tree, Variable):
+        return _wrap(tree._t)
+    if isinstance(tree, Tensor):
+        return _wrap(tree._t.to("meta"))
+    if isinstance(tree, torch.Tensor):
+        return tree.to("meta")
+    if isinstance(tree, list):
+        return [_to_meta(t) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_to_meta(t) for t in tree)
+    if isinstance(tree, dict):
+        return {k: _to_meta(v) for k, v in tree.items()}
+    return tree
+
+
+def _outputs_to_vars(tree, block):
+    if isinstance(tree, Tensor):
+        v = Variable(block, tree._t if tree._t.device.type == "meta" else tree._t.to("meta"))
+        block.vars[v.name] = v
+        return v
+    if isinstance(tree, list):
+        return [_outputs_to_vars(t, block) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_outputs_to_vars(t, block) for t in tree)
+    return tree
+
+
+def _bind(fn, args, kwargs):
+    """Bind positional args to names so ops can be re-parameterised (clone(for_test)) and serialised."""
+    try:
+        sig = inspect.signature(fn)
+    except (TypeError, ValueError):
+        return args, kwargs
+    if any(p.kind in (p.VAR_POSITIONAL, p.VAR_KEYWORD) for p in sig.parameters.values()):
+        return args, kwargs
+    try:
+        b = sig.bind(*args, **kwargs)
+    except TypeError:
+        return args, kwargs
+    return (), dict(b.arguments)
+
+
+def record_op(fn, name, args, kwargs):
+    """Called by every wrapped op in static mode (see framework/dispatch.py)."""
+    if not _has_var((args, kwargs)):
+        return fn(*args, **kwargs)
+    qual = f"{fn.__module__}.{name}"
+    OP_REGISTRY.setdefault(qual, fn)
+    bargs, bkw = _bind(fn, args, kwargs)
+    _core._mode.record_depth += 1
+    try:
+        meta_out = fn(*_to_meta(bargs), **_to_meta(bkw))
+    finally:
+        _core._mode.record_depth -= 1
+    blk = default_main_program().current_block()
+    outs = _outputs_to_vars(meta_out, blk)
+    op = OpDesc(qual, fn, bargs, bkw, outs)
+    for v in _iter_vars(outs):
+        v.op = op
+    blk.append_op(op)
+    return outs
+
+
+# ----------------------------------------------------------------------------- backward / optimize ops
+def _grad_var(block, like, name):
+    v = Variable(block, like._t.to("meta") if like._t.device.type != "meta" else like._t, name)
+    block.vars[name] = v
+    return v
+
+
+def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None, checkpoints=None,
+                    distop_context=None):
+    prog = default_main_program()
+    blk = prog.global_block()
+    params = parameter_list if parameter_list is not None else [p for p in prog.all_parameters() if p.trainable]
+    params = [blk.vars.get(p, p) if isinstance(p, str) else p for p in params]
+    nog = set(id(v) for v in (no_grad_set or []) if not isinstance(v, str))
+    params = [p for p in params if id(p) not in nog]
+    gvars = [_grad_var(blk, p, p.name + "@GRAD") for p in params]
+
+    def _backward(loss_t, *ps):
+        grads = torch.autograd.grad(loss_t._t, [p._t for p in ps], allow_unused=True, retain_graph=True)
+        return tuple(_wrap(g if g is not None else torch.zeros_like(p._t)) for g, p in zip(grads, ps))
+
+    op = OpDesc("@backward", _backward, (loss,) + tuple(params), {}, tuple(gvars))
+    blk.append_op(op)
+    return list(zip(params, gvars))
+
+
+def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
+    prog = default_main_program()
+    blk = prog.global_block()
+    targets = [targets] if isinstance(targets, Tensor) else list(targets)
+    inputs = [inputs] if isinstance(inputs, Tensor) else list(inputs)
+    for v in inputs:
+        if isinstance(v, Variable):
+            v.need_grad = True
+    tg = target_gradients if target_gradients is None or isinstance(target_gradients, (list, tuple)) else [target_gradients]
+    gvars = [_grad_var(blk, x, x.name + "@GRAD") for x in inputs]
+
+    def _grads(ts, xs, gts):
+        gs = torch.autograd.grad([t._t for t in ts], [x._t for x in xs], [g._t for g in gts] if gts else None,
+                                 allow_unused=True, retain_graph=True, create_graph=True)
+        return tuple(_wrap(g if g is not None else torch.zeros_like(x._t)) for g, x in zip(gs, xs))
+
+    op = OpDesc("@gradients", _grads, (tuple(targets), tuple(inputs), tuple(tg or ())), {}, tuple(gvars))
+    blk.append_op(op)
+    return gvars
+
+
+def minimize_static(optimizer, loss, parameters=None, no_grad_set=None):
+    prog = default_main_program()
+    blk = prog.global_block()
+    params = parameters if parameters is not None else [p for p in prog.all_parameters() if p.trainable]
+    nog = set(id(v) for v in (no_grad_set or []) if not isinstance(v, str))
+    params = [p for p in params if id(p) not in nog]
+    if optimizer._parameter_list is None:
+        optimizer._add_param_group({"params": list(params)})
+        optimizer._parameter_list = list(params)
+    gvars = [_grad_var(blk, p, p.name + "@GRAD") for p in params]
+
+    def _optimize(loss_t, *ps):
+        for p in ps:
+            p._t.grad = None
+        loss_t._t.backward()
+        grads = tuple(_wrap(p._t.grad if p._t.grad is not None else torch.zeros_like(p._t)) for p in ps)
+        with _core_dynamic():
+            optimizer.step()
+        optimizer.clear_grad(set_to_zero=False)
+        return grads
+
+    op = OpDesc("@optimize", _optimize, (loss,) + tuple(params), {}, tuple(gvars))
+    blk.append_op(op)
+    return [op], list(zip(params, gvars))
+
+
+@contextlib.contextmanager
+def _core_dynamic():
+    prev = _core._mode.static
+    _core._mode.static = False
+    try:
+        yield
+    finally:
+        _core._mode.static = prev
+
+
+# ----------------------------------------------------------------------------- scope / executor
+class Scope:
+    def __init__(self):
+        self.vars = {}
+
+    def var(self, name):
+        return self.vars.setdefault(name, _ScopeVar(name))
+
+    def find_var(self, name):
+        v = self.vars.get(name)
+        if v is None:
+            for p in default_main_program().all_parameters():
+                if p.name == name:
+                    return _ScopeVar(name, p)
+        return v
+
+
+class _ScopeVar:
+    def __init__(self, name, value=None):
+        self.name, self.value = name, value
+
+    def get_tensor(self):
+        return self.value
+
+    def set(self, value, place=None):
+        if self.value is not None and isinstance(self.value, Tensor):
+            self.value.set_value(value)
+        else:
+            self.value = _core.to_tensor(value)
+
+
+_global_scope = Scope()
+
+
+def global_scope():
+    return _global_scope
+
+
+@contextlib.contextmanager
+def scope_guard(scope):
+    global _global_scope
+    old = _global_scope
+    _global_scope = scope
+    try:
+        yield
+    finally:
+        _global_scope = old
+
+
+def _subst(tree, env):
+    if isinstance(tree, Variable):
+        try:
+            return env[id(tree)]
+        except KeyError:
+            raise RuntimeError(f"variable {tree.name} has no value (missing feed?)")
+    if isinstance(tree, list):
+        return [_subst(t, env) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_subst(t, env) for t in tree)
+    if isinstance(tree, dict):
+        return {k: _subst(v, env) for k, v in tree.items()}
+    return tree
+
+
+def _bind_outputs(outs, vals, env):
+    if isinstance(outs, Variable):
+        env[id(outs)] = vals
+    elif isinstance(outs, (list, tuple)):
+        for o, v in zip(outs, vals):
+            _bind_outputs(o, v, env)
+
+
+def run_program(program, feed, fetch_list):
+    """Interpret ``program`` with ``feed``; returns fetched Tensors (real)."""
+    blk = program.global_block()
+    env = {}
+    for name, val in (feed or {}).items():
+        v = blk.vars.get(name)
+        if v is None:
+            continue
+        t = val._t if isinstance(val, Tensor) else _core._to_torch(np.asarray(val) if not isinstance(val, torch.Tensor) else val,
+                                                                    dtype=v._t.dtype)
+        if t.dtype != v._t.dtype:
+            t = t.to(v._t.dtype)
+        if t.device != _core.default_device():
+            t = t.to(_core.default_device())
+        if v.need_grad and t.is_floating_point():
+            t = t.detach().requires_grad_(True)
+        env[id(v)] = _wrap(t)
+    prev_static = _core._mode.static
+    _core._mode.record_depth += 1
+    try:
+        for op in blk.ops:
+            out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
+            _bind_outputs(op.outputs, out, env)
+    finally:
+        _core._mode.record_depth -= 1
+        _core._mode.static = prev_static
+    res = []
+    for f in fetch_list or []:
+        if isinstance(f, str):
+            f = blk.vars[f]
+        if isinstance(f, Variable):
+            res.append(env[id(f)])
+        elif isinstance(f, Tensor):
+            res.append(f)
+        else:
+            raise TypeError(f"cannot fetch {f!r}")
+    return res
+
+
+class Executor:
+    def __init__(self, place=None):
+        self.place = place
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch",
+            scope=None, return_numpy=True, use_program_cache=False, return_merged=True, use_prune=False):
+        if program is None:
+            program = default_main_program()
+        if isinstance(program, CompiledProgram):
+            outs = program._run(feed, fetch_list)
+        else:
+            if not program.global_block().ops:
+                return []
+            outs = run_program(program, feed, fetch_list)
+        if return_numpy:
+            return [o.numpy() if isinstance(o, Tensor) else o for o in outs]
+        return outs
+
+    def close(self):
+        pass
+
+    def train_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        for batch in dataset:
+            self.run(program, feed=batch, fetch_list=fetch_list)
+
+    infer_from_dataset = train_from_dataset
+
+
+class BuildStrategy:
+    def __init__(self):
+        self.fuse_elewise_add_act_ops = False
+        self.fuse_bn_act_ops = False
+        self.fuse_all_reduce_ops = True
+        self.enable_inplace = True
+        self.enable_addto = False
+        self.memory_optimize = True
+        self.fuse_gemm_epilogue = True
+        self.use_hip_graph = False
+        self.build_cinn_pass = False
+        self.sync_batch_norm = False
+        self.reduce_strategy = 0
+        self.gradient_scale_strategy = 0
+        self.debug_graphviz_path = ""
+
+
+class ExecutionStrategy:
+    def __init__(self):
+        self.num_threads = 1
+        self.num_iteration_per_drop_scope = 100
+        self.use_thread_barrier = False
+
+
+class CompiledProgram:
+    """Program + build strategy. With ``build_strategy.use_hip_graph`` a forward-only program is
+    captured once per feed signature into a HIP graph and replayed (static input/output
+    buffers), removing per-op launch overhead."""
+
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._program = program_or_graph
+        self._build_strategy = build_strategy or BuildStrategy()
+        self._graphs = {}
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, share_vars_from=None,
+                           places=None):
+        if build_strategy is not None:
+            self._build_strategy = build_strategy
+        return self
+
+    def _run(self, feed, fetch_list):
+        has_opt = any(op.type.startswith("@") for op in self._program.global_block().ops)
+        if not self._build_strategy.use_hip_graph or has_opt or not torch.cuda.is_available():
+            return run_program(self._program, feed, fetch_list)
+        key = tuple((k, tuple(np.shape(v if not isinstance(v, Tensor) else v._t)), str(getattr(v, "dtype", "")))
+                    for k, v in sorted(feed.items()))
+        ent = self._graphs.get(key)
+        if ent is None:
+            static_in = {k: _wrap((v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))).to(_core.default_device()).clone())
+                         for k, v in feed.items()}
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s), torch.no_grad():
+                for _ in range(2):
+                    run_program(self._program, static_in, fetch_list)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                outs = run_program(self._program, static_in, fetch_list)
+            ent = (g, static_in, outs)
+            self._graphs[key] = ent
+        g, static_in, outs = ent
+        for k, v in feed.items():
+            src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+            static_in[k]._t.copy_(src)
+        g.replay()
+        return outs
+
+
+# ----------------------------------------------------------------------------- serialisation
+def _encode(x, consts):
+    if isinstance(x, Variable):
+        return {"@var": x.name}
+    if isinstance(x, Parameter):
+        consts[x.name] = x
+        return {"@param": x.name}
+    if isinstance(x, Tensor):
+        name = f"@const_{len(consts)}"
+        consts[name] = x
+        return {"@const": name}
+    if isinstance(x, torch.dtype):
+        return {"@dtype": dtype_to_str(x)}
+    if isinstance(x, np.ndarray):
+        return {"@ndarray": x.tolist(), "dtype": str(x.dtype)}
+    if isinstance(x, (np.integer,)):
+        return int(x)
+    if isinstance(x, (np.floating,)):
+        return float(x)
+    if isinstance(x, tuple):
+        return {"@tuple": [_encode(v, consts) for v in x]}
+    if isinstance(x, list):
+        return [_encode(v, consts) for v in x]
+    if isinstance(x, dict):
+        return {"@dict": {k: _encode(v, consts) for k, v in x.items()}}
+    if isinstance(x, (int, float, str, bool)) or x is None:
+        return x
+    if isinstance(x, slice):
+        return {"@slice": [x.start, x.stop, x.step]}
+    if x is Ellipsis:
+        return {"@ellipsis": True}
+    raise TypeError(f"cannot serialise op argument of type {type(x)}")
+
+
+def prune_ops(ops, fetch_vars):
+    """Keep only the ops the fetch targets depend on (reference: Program._prune)."""
+    if not fetch_vars:
+        return list(ops)
+    needed = {id(v) for v in fetch_vars}
+    kept = []
+    for op in reversed(ops):
+        if any(id(v) in needed for v in _iter_vars(op.outputs)):
+            kept.append(op)
+            needed.update(id(v) for v in _iter_vars((op.args, op.kwargs)))
+    return kept[::-1]
+
+
+def serialize_program_dict(program, feed_vars, fetch_vars):
+    consts = {}
+    ops = []
+    for op in prune_ops(program.global_block().ops, fetch_vars):
+        if op.type.startswith("@"):
+            continue
+        ops.append({"type": op.type, "args": _encode(list(op.args), consts), "kwargs": _encode(op.kwargs, consts),
+                    "outputs": _encode(op.outputs if isinstance(op.outputs, (list, tuple)) else op.outputs, consts)})
+    feeds = [{"name": v.name, "shape": v.shape, "dtype": dtype_to_str(v._t.dtype)} for v in feed_vars]
+    fetches = [v.name for v in fetch_vars]
+    return {"format": "paddle_hackathon_amd.program/1", "ops": ops, "feeds": feeds, "fetches": fetches}, consts
+
+
+def _resolve_fn(qual):
+    fn = OP_REGISTRY.get(qual)
+    if fn is not None:
+        return fn
+    import importlib
+    mod, _, name = qual.rpartition(".")
+    m = importlib.import_module(mod)
+    f = getattr(m, name)
+    return getattr(f, "__wrapped_op__", f)
+
+
+def deserialize_program_dict(d, params):
+    prog = Program()
+    blk = prog.global_block()
+    vars_ = {}
+
+    def var(name, meta=None):
+        if name not in vars_:
+            v = Variable(blk, meta if meta is not None else torch.empty(0, device="meta"), name)
+            vars_[name] = v
+            blk.vars[name] = v
+        return vars_[name]
+
+    for f in d["feeds"]:
+        meta = torch.empty([1 if s == -1 else s for s in f["shape"]], dtype=convert_dtype(f["dtype"]), device="meta")
+        v = var(f["name"], meta)
+        v.is_data, v.declared_shape = True, f["shape"]
+
+    def dec(x):
+        if isinstance(x, dict):
+            if "@var" in x:
+                return var(x["@var"])
+            if "@param" in x:
+                return params[x["@param"]]
+            if "@const" in x:
+                return params[x["@const"]]
+            if "@dtype" in x:
+                return convert_dtype(x["@dtype"])
+            if "@ndarray" in x:
+                return np.asarray(x["@ndarray"], dtype=x["dtype"])
+            if "@tuple" in x:
+                return tuple(dec(v) for v in x["@tuple"])
+            if "@dict" in x:
+                return {k: dec(v) for k, v in x["@dict"].items()}
+            if "@slice" in x:
+                return slice(*x["@slice"])
+            if "@ellipsis" in x:
+                return Ellipsis
+        if isinstance(x, list):
+            return [dec(v) for v in x]
+        return x
+
+    for o in d["ops"]:
+        fn = _resolve_fn(o["type"])
+        outs = dec(o["outputs"])
+        blk.append_op(OpDesc(o["type"], fn, tuple(dec(o["args"])), dec(o["kwargs"]), outs))
+    feeds = [vars_[f["name"]] for f in d["feeds"]]
+    fetches = [vars_[n] for n in d["fetches"]]
+    return prog, feeds, fetches
