@@ -113,5 +113,26 @@ def monkey_patch_variable():
     pass
 
 
+from .framework.core import set_printoptions  # noqa: E402,F401
+
+
+def check_shape(shape):
+    """Validate a shape argument: list/tuple of ints (>= -1) or Tensors, or an int Tensor
+    (reference: fluid/layers/utils.py:check_shape)."""
+    if isinstance(shape, Tensor):
+        if shape.dtype not in (int32, int64):
+            raise TypeError("shape Tensor must be int32 or int64")
+        return
+    if not isinstance(shape, (list, tuple)):
+        raise TypeError(f"shape must be list/tuple/Tensor, got {type(shape)}")
+    for e in shape:
+        if isinstance(e, Tensor):
+            continue
+        if not isinstance(e, int):
+            raise TypeError(f"All elements in ``shape`` must be integers, got {type(e)}")
+        if e < -1:
+            raise ValueError("All elements in ``shape`` must be positive when it's a list or tuple")
+
+
 def monkey_patch_math_varbase():
     pass

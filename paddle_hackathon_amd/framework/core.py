@@ -270,6 +270,7 @@ def place_of(t: torch.Tensor) -> Place:
 class _Mode:
     static = False
     record_depth = 0
+    trace = False  # op/layer host tracing on (paddle.profiler)
 
 
 _mode = _Mode()
@@ -287,6 +288,22 @@ _name_counter = itertools.count()
 
 def _unique_name(prefix):
     return f"{prefix}_{next(_name_counter)}"
+
+
+_PRINT_OPTS = {}
+
+
+def set_printoptions(precision=None, threshold=None, edgeitems=None, sci_mode=None, linewidth=None):
+    """paddle.set_printoptions (reference: python/paddle/tensor/to_string.py)."""
+    for k, v in (("precision", precision), ("threshold", threshold), ("edgeitems", edgeitems),
+                 ("max_line_width", linewidth)):
+        if v is not None:
+            _PRINT_OPTS[k] = int(v)
+    if sci_mode is not None:
+        _PRINT_OPTS["floatmode"] = "maxprec"
+        _PRINT_OPTS["suppress_small"] = not sci_mode
+    torch.set_printoptions(precision=precision, threshold=threshold, edgeitems=edgeitems, linewidth=linewidth,
+                           sci_mode=sci_mode)
 
 
 class Tensor:
@@ -378,6 +395,40 @@ class Tensor:
 
     def is_sparse_csr(self):
         return self._t.layout == torch.sparse_csr
+
+    # -- sparse accessors (reference: fluid/dygraph/varbase_patch_methods.py:898-990) -----
+    def values(self):
+        t = self._t
+        if t.layout == torch.sparse_coo:
+            return _wrap((t if t.is_coalesced() else t.coalesce()).values())
+        return _wrap(t.values() if t.layout == torch.sparse_csr else t)
+
+    def indices(self):
+        if not self._t.is_sparse:
+            raise ValueError("indices() is only defined for sparse COO tensors")
+        return _wrap(self._t.coalesce().indices() if not self._t.is_coalesced() else self._t.indices())
+
+    def crows(self):
+        return _wrap(self._t.crow_indices())
+
+    def cols(self):
+        return _wrap(self._t.col_indices())
+
+    def nnz(self):
+        return self._t._nnz()
+
+    def to_dense(self):
+        return _wrap(self._t.to_dense()) if self.is_sparse() else self
+
+    def to_sparse_coo(self, sparse_dim):
+        t = self._t.to_dense() if self._t.layout == torch.sparse_csr else self._t
+        return _wrap(t.to_sparse(sparse_dim))
+
+    def to_sparse_csr(self):
+        t = self._t
+        if t.is_sparse:
+            t = t.to_dense()
+        return _wrap(t.to_sparse_csr())
 
     # -- autograd ---------------------------------------------------------------
     @property
@@ -573,8 +624,7 @@ class Tensor:
     def __repr__(self):
         t = self._t.detach()
         body = np.array2string(self.numpy() if t.dtype != torch.bfloat16 else t.float().cpu().numpy(),
-                               separator=", ", prefix="       ")
-        grad = "True" if not self.stop_gradient else "True"
+                               separator=", ", prefix="       ", **_PRINT_OPTS)
         return (f"Tensor(shape={self.shape}, dtype={dtype_to_str(t.dtype)}, place={self.place}, "
                 f"stop_gradient={self.stop_gradient},\n       {body})")
 

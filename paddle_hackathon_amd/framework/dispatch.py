@@ -20,6 +20,12 @@ def _record_hook(fn, name, args, kwargs):
     return record_op(fn, name, args, kwargs)
 
 
+def _traced(fn, name, args, kwargs):
+    from ..profiler import _op_range
+    with _op_range(name, "Operator"):
+        return fn(*args, **kwargs)
+
+
 def static_op(fn, name=None):
     opname = name or fn.__name__
 
@@ -27,6 +33,8 @@ def static_op(fn, name=None):
     def wrapper(*args, **kwargs):
         if _mode.static and _mode.record_depth == 0:
             return _record_hook(fn, opname, args, kwargs)
+        if _mode.trace:
+            return _traced(fn, opname, args, kwargs)
         return fn(*args, **kwargs)
 
     wrapper.__wrapped_op__ = fn

@@ -1,0 +1,2 @@
+"""incubate.distributed (reference: python/paddle/incubate/distributed/)."""
+from . import models  # noqa: F401

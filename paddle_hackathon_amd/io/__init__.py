@@ -14,6 +14,7 @@ import itertools
 import math
 import multiprocessing as mp
 import queue
+import os
 import threading
 
 import numpy as np
@@ -268,7 +269,30 @@ def get_worker_info():
     return getattr(_worker_info, "info", None)
 
 
-def _worker_loop(dataset, index_q, out_q, collate_fn, worker_id, num_workers, init_fn, seed, iterable, batch_size, drop_last):
+_RING = "__pha_ring__"
+
+
+def _ring_put(ring, idx, data):
+    """Write a collated batch into a free shared-memory slot; False if it does not fit."""
+    from ..utils import native
+    while True:
+        slot = ring.acquire_write(timeout_ms=1000)
+        if slot == -2:
+            return True  # ring closed: trainer is shutting down
+        if slot >= 0:
+            break
+        if os.getppid() == 1:  # trainer died
+            return True
+    n = native.pack_into(data, ring.slot_view(slot))
+    if n < 0:
+        ring.abort(slot)
+        return False
+    ring.commit(slot, idx, n)
+    return True
+
+
+def _worker_loop(dataset, index_q, out_q, collate_fn, worker_id, num_workers, init_fn, seed, iterable, batch_size,
+                 drop_last, ring=None):
     _worker_info.info = _WorkerInfo(worker_id, num_workers, dataset, seed)
     np.random.seed((seed + worker_id) % (2 ** 32))
     torch.manual_seed(seed + worker_id)
@@ -294,8 +318,58 @@ def _worker_loop(dataset, index_q, out_q, collate_fn, worker_id, num_workers, in
         try:
             data = collate_fn([dataset[i] for i in indices])
         except Exception as e:  # propagate worker errors
-            data = RuntimeError(f"DataLoader worker {worker_id} failed: {e!r}")
-        out_q.put((idx, data))
+            out_q.put((idx, RuntimeError(f"DataLoader worker {worker_id} failed: {e!r}")))
+            continue
+        if ring is not None and _is_array_tree(data) and _ring_put(ring, idx, data):
+            out_q.put((idx, _RING))
+        else:
+            out_q.put((idx, data))
+
+
+def _is_array_tree(x):
+    if isinstance(x, np.ndarray):
+        return x.dtype != object
+    if isinstance(x, dict):
+        return all(_is_array_tree(v) for v in x.values())
+    if isinstance(x, (list, tuple)):
+        return all(_is_array_tree(v) for v in x)
+    return isinstance(x, (int, float, str, bytes, np.generic)) or x is None
+
+
+def _tree_nbytes(x):
+    if isinstance(x, np.ndarray):
+        return x.nbytes + 64
+    if isinstance(x, dict):
+        return sum(_tree_nbytes(v) for v in x.values())
+    if isinstance(x, (list, tuple)):
+        return sum(_tree_nbytes(v) for v in x)
+    return 64
+
+
+def _ring_take(ring, idx, pin):
+    """Read batch ``idx`` out of the ring into private (pinned, when feeding a GPU) memory."""
+    from ..utils import native
+    slot = ring.acquire_read(idx, timeout_ms=60000)
+    if slot < 0:
+        raise RuntimeError(f"DataLoader shared-memory ring lost batch {idx}")
+    try:
+        views = native.unpack_from(ring.slot_view(slot, ring.nbytes(slot)), copy=False)
+
+        def own(x):
+            if isinstance(x, np.ndarray):
+                if pin:
+                    t = torch.empty(x.shape, dtype=torch.from_numpy(x[:0].copy()).dtype, pin_memory=True)
+                    t.copy_(torch.from_numpy(x))
+                    return t
+                return x.copy()
+            if isinstance(x, dict):
+                return {k: own(v) for k, v in x.items()}
+            if isinstance(x, (list, tuple)):
+                return [own(v) for v in x]
+            return x
+        return own(views)
+    finally:
+        ring.release(slot)
 
 
 def _to_device_tree(x, dev, non_blocking):
@@ -335,6 +409,7 @@ class DataLoader:
         self.return_list = return_list
         self.num_workers = num_workers
         self.use_buffer_reader = use_buffer_reader
+        self.use_shared_memory = use_shared_memory
         self.worker_init_fn = worker_init_fn
         self.timeout = timeout
         self.prefetch_factor = max(2, prefetch_factor)
@@ -411,25 +486,33 @@ class DataLoader:
                         p.terminate()
             return
         index_qs = [ctx.Queue() for _ in range(self.num_workers)]
-        workers = [ctx.Process(target=_worker_loop, args=(self.dataset, index_qs[w], out_q, self.collate_fn, w, self.num_workers,
-                                                         self.worker_init_fn, seed, False, None, False), daemon=True)
+        batches = iter(self.batch_sampler)
+        first = next(batches, None)
+        if first is None:
+            return
+        ring = self._make_ring(first)
+        pin = ring is not None and self.device.type == "cuda"
+        workers = [ctx.Process(target=_worker_loop, args=(self.dataset, index_qs[w], out_q, self.collate_fn, w,
+                                                         self.num_workers, self.worker_init_fn, seed, False, None,
+                                                         False, ring), daemon=True)
                    for w in range(self.num_workers)]
         for p in workers:
             p.start()
+        cap = self.num_workers * self.prefetch_factor  # == ring slots: every in-flight batch has a slot
         try:
-            batches = iter(self.batch_sampler)
             sent = 0
-            for _ in range(self.num_workers * self.prefetch_factor):
-                b = next(batches, None)
-                if b is None:
-                    break
+            b = first
+            while b is not None:
                 index_qs[sent % self.num_workers].put((sent, b))
                 sent += 1
+                b = next(batches, None) if sent < cap else None
             pending = {}
             nxt = 0
             while nxt < sent:
                 while nxt not in pending:
-                    idx, data = out_q.get(timeout=self.timeout or None)
+                    idx, data = self._get(out_q, workers)
+                    if isinstance(data, str) and data == _RING:
+                        data = _ring_take(ring, idx, pin)
                     pending[idx] = data
                 data = pending.pop(nxt)
                 nxt += 1
@@ -441,12 +524,52 @@ class DataLoader:
                     raise data
                 yield data
         finally:
+            if ring is not None:
+                ring.close()
             for q in index_qs:
                 q.put(None)
             for p in workers:
                 p.join(timeout=1)
                 if p.is_alive():
                     p.terminate()
+            if ring is not None:
+                ring.destroy()
+
+    def _get(self, out_q, workers):
+        """out_q.get with a liveness watchdog: a dead worker raises instead of hanging."""
+        import queue as _queue
+        waited = 0.0
+        while True:
+            try:
+                return out_q.get(timeout=5.0)
+            except _queue.Empty:
+                waited += 5.0
+                dead = [p for p in workers if not p.is_alive() and p.exitcode not in (0, None)]
+                if dead:
+                    raise RuntimeError(f"DataLoader worker (pid {dead[0].pid}) exited unexpectedly "
+                                       f"with code {dead[0].exitcode}")
+                if self.timeout and waited >= self.timeout:
+                    raise RuntimeError(f"DataLoader timed out after {self.timeout}s")
+
+    def _make_ring(self, first_indices):
+        """Shared-memory batch ring sized from one probe batch (None: pickle through the queue)."""
+        if not self.use_shared_memory:
+            return None
+        from ..utils import native
+        if not native.available():
+            return None
+        try:
+            probe = self.collate_fn([self.dataset[i] for i in first_indices])
+        except Exception:
+            return None
+        if not _is_array_tree(probe):
+            return None
+        slot = max(1 << 16, 2 * _tree_nbytes(probe) + (1 << 16))
+        name = f"/pha_dl_{os.getpid()}_{id(self) & 0xffffff}_{np.random.randint(1 << 30)}"
+        try:
+            return native.ShmRing(name, self.num_workers * self.prefetch_factor, slot)
+        except OSError:
+            return None
 
     def __iter__(self):
         dev = self.device

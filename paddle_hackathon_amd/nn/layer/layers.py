@@ -247,6 +247,13 @@ class Layer:
         return h
 
     def __call__(self, *inputs, **kwargs):
+        if _core._mode.trace:
+            from ...profiler import _op_range
+            with _op_range(type(self).__name__, "Forward"):
+                return self._call_impl(*inputs, **kwargs)
+        return self._call_impl(*inputs, **kwargs)
+
+    def _call_impl(self, *inputs, **kwargs):
         if self._forward_pre_hooks:
             for hook in list(self._forward_pre_hooks.values()):
                 r = hook(self, inputs)

@@ -81,7 +81,7 @@ def build_runtime(force=False, verbose=True):
     if not force and not _newer(srcs + hdrs + [__file__], target):
         return target
     cxx = shutil.which("g++") or shutil.which("c++")
-    _run([cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", target + ".tmp"] + srcs)
+    _run([cxx, "-O3", "-std=c++17", "-Wall", "-shared", "-fPIC", "-pthread", "-o", target + ".tmp"] + srcs)
     os.replace(target + ".tmp", target)
     if verbose:
         print(f"[pha] built {target} from {len(srcs)} C++ sources")

@@ -50,6 +50,6 @@ class ShowClickEntry(_Entry):
 
 
 try:
-    from ..incubate.distributed_dataset import InMemoryDataset, QueueDataset  # noqa: E402,F401
+    from .fleet.dataset import InMemoryDataset, QueueDataset  # noqa: E402,F401
 except ImportError:  # pragma: no cover
     pass

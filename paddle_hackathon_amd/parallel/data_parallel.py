@@ -60,21 +60,19 @@ class _Reducer:
         self.avg_native = C.get_backend() == "nccl"
         self.buckets = []
         self.param_bucket = {}
-        # reverse order ≈ gradient-ready order
-        cur, cur_bytes, cur_dt = [], 0, None
-        limit = last_bucket_bytes
-        for p in reversed(self.params):
-            nb = p._t.numel() * p._t.element_size()
-            dt = p._t.dtype
-            if cur and (cur_bytes + nb > limit or dt != cur_dt):
-                self._add(cur, cur_dt)
-                cur, cur_bytes = [], 0
-                limit = bucket_bytes
-            cur.append(p)
-            cur_bytes += nb
-            cur_dt = dt
-        if cur:
-            self._add(cur, cur_dt)
+        # reverse order ≈ gradient-ready order; planning runs in the native runtime
+        # (csrc/runtime/bucket.cpp): first bucket small so RCCL starts early, then large ones
+        from ..utils import native
+        dts = {}
+        gids = native.plan_buckets([p._t.numel() * p._t.element_size() for p in self.params],
+                                   [dts.setdefault(p._t.dtype, len(dts)) for p in self.params],
+                                   [last_bucket_bytes, bucket_bytes],
+                                   order=list(range(len(self.params) - 1, -1, -1)))
+        groups = {}
+        for p, g in zip(reversed(self.params), reversed(gids)):
+            groups.setdefault(g, []).append(p)
+        for g in sorted(groups):
+            self._add(groups[g], groups[g][0]._t.dtype)
         self.handles = []
         self._callback_queued = False
         for p in self.params:
