@@ -607,10 +607,10 @@ class Tensor:
         return bool(self._t)
 
     def __float__(self):
-        return float(self._t)
+        return float(self._t.detach())
 
     def __int__(self):
-        return int(self._t)
+        return int(self._t.detach())
 
     def __index__(self):
         return int(self._t)
