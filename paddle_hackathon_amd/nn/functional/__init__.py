@@ -4,6 +4,7 @@ from .common import *  # noqa: F401,F403
 from .conv import *  # noqa: F401,F403
 from .pooling import *  # noqa: F401,F403
 from .norm import *  # noqa: F401,F403
+from .norm import batch_norm_act  # noqa: F401,E402
 from .loss import *  # noqa: F401,F403
 from .attention import *  # noqa: F401,F403
 from .vision_ops import *  # noqa: F401,F403

@@ -66,9 +66,35 @@ def _to_ncx(t, data_format):
     return t, False
 
 
+def _hip_conv2d(x, w, bias, stride, pad, dilation, groups):
+    """NHWC conv on the gfx950 implicit-GEMM MFMA kernels (ops/conv_gemm.py). Inputs whose
+    channel count is not a multiple of 8 (the RGB stem) are zero-padded to 8 channels."""
+    from ...ops import conv_gemm
+    if x.shape[-1] % 8 != 0:
+        c = x.shape[-1]
+        cp = (c + 7) // 8 * 8
+        x = TF.pad(x, [0, cp - c])
+        w = TF.pad(w, [0, 0, 0, 0, 0, cp - c])
+    return conv_gemm.conv2d_nhwc(x, w, bias, stride, pad, dilation)
+
+
+def _hip_conv_ok(t_nhwc, w, groups):
+    import os
+    if os.environ.get("PHA_CONV_IMPL", "hip") != "hip":
+        return False
+    from ...ops import conv_gemm, _lib
+    return (t_nhwc.is_cuda and t_nhwc.dim() == 4 and t_nhwc.dtype in (torch.bfloat16, torch.float16)
+            and w.dtype == t_nhwc.dtype and groups == 1 and w.shape[0] % 8 == 0 and _lib.require_native())
+
+
 def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     t = x._t
     w = weight._t
+    if n == 2 and data_format == "NHWC" and _hip_conv_ok(t, w, groups):
+        st, dl = _tup(stride, 2), _tup(dilation, 2)
+        pad, pre = _padding(padding, 2, list(w.shape[2:]), st, dl, list(t.shape[1:3]))
+        if pre is None and (st == [1, 1] or dl == [1, 1]):
+            return _w(_hip_conv2d(t.contiguous(), w, None if bias is None else bias._t, st, pad, dl, groups))
     t, cl = _to_ncx(t, data_format)
     stride = _tup(stride, n)
     dilation = _tup(dilation, n)

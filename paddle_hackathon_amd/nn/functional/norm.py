@@ -21,17 +21,36 @@ def _t(x):
 
 def batch_norm(x, running_mean, running_var, weight, bias, training=False, momentum=0.9, epsilon=1e-05,
                data_format="NCHW", use_global_stats=None, name=None):
+    """Channels-last inputs (NHWC/NLC/NDHWC) run the fused HIP BN kernels; channels-first
+    falls back to the library kernel (reference: nn/functional/norm.py:batch_norm)."""
+    return batch_norm_act(x, running_mean, running_var, weight, bias, training, momentum, epsilon, data_format,
+                          use_global_stats)
+
+
+def batch_norm_act(x, running_mean, running_var, weight, bias, training=False, momentum=0.9, epsilon=1e-05,
+                   data_format="NCHW", use_global_stats=None, residual=None, act=None):
+    """BN (+ residual add) (+ ReLU) in one pass — the fused_bn_add_activation op of the reference
+    (fluid/operators/fused/fused_bn_add_activation_op.cu), used by the ResNet blocks."""
+    if act not in (None, "relu"):
+        raise ValueError(f"unsupported fused activation {act}")
     t = x._t
-    cl = data_format in ("NHWC", "NLC", "NDHWC")
-    if cl:
-        t = t.movedim(-1, 1)
-        if t.dim() == 4:
-            t = t.contiguous(memory_format=torch.channels_last) if not t.is_contiguous(memory_format=torch.channels_last) else t
+    cl = data_format in ("NHWC", "NLC", "NDHWC") or (t.dim() == 2)
     use_batch = training and not use_global_stats
     rm, rv = _t(running_mean), _t(running_var)
-    out = TF.batch_norm(t, rm, rv, _t(weight), _t(bias), use_batch, 1.0 - momentum, epsilon)
+    res = _t(residual)
     if cl:
-        out = out.movedim(1, -1)
+        if use_batch:
+            out = _ops.fused.batch_norm_train(t.contiguous(), _t(weight), _t(bias), rm, rv, momentum, epsilon, -1,
+                                              residual=res, relu=act == "relu")
+        else:
+            out = _ops.fused.batch_norm_infer(t.contiguous(), _t(weight), _t(bias), rm, rv, epsilon, -1, residual=res,
+                                              relu=act == "relu")
+        return _w(out)
+    out = TF.batch_norm(t, rm, rv, _t(weight), _t(bias), use_batch, 1.0 - momentum, epsilon)
+    if res is not None:
+        out = out + res
+    if act == "relu":
+        out = torch.relu(out)
     return _w(out)
 
 

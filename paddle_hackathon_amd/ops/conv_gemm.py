@@ -1,0 +1,211 @@
+"""Host side of the gfx950 MFMA GEMM / implicit-GEMM convolution (csrc/kernels/gemm_conv.hip).
+
+``conv2d_nhwc`` is an autograd Function whose forward, data-gradient and weight-gradient
+are all the same MFMA kernel with different operand loaders:
+
+  * forward   : out[(n,oh,ow), co] = im2col(x)[m, (kh,kw,ci)] @ W^T          (A_CONV x B_ROW)
+  * grad data : stride 1 — the forward kernel on dY with the spatially flipped, channel-
+                transposed kernel; stride s — s*s sub-pixel convolutions (one per output
+                phase, each a stride-1 conv over dY with that phase's taps), interleaved.
+  * grad wgt  : dW[co, (kh,kw,ci)] = dY^T @ im2col(x), reduction over N*OH*OW output pixels,
+                split-K across blocks with an fp32 slab reduction             (A_COL x B_CONV)
+
+Layouts: activations NHWC (C contiguous), weights Paddle OIHW [Cout, Cin, KH, KW].
+Requires bf16/fp16, Cin % 8 == 0 and Cout % 8 == 0 (everything in ResNet after the stem);
+other shapes use the portable path in nn.functional.conv.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_int, c_long, c_void_p
+
+import torch
+
+from . import _lib
+
+A_ROW, A_COL, A_CONV = 0, 1, 2
+B_ROW, B_COL, B_CONV = 0, 1, 2
+EPI = {None: 0, "relu": 1, "gelu": 2}
+_DT = {torch.bfloat16: 1, torch.float16: 2}
+_sig = False
+_zero = {}
+
+
+def _L():
+    global _sig
+    L = _lib.lib
+    if L is None:
+        raise RuntimeError("libpha_kernels.so not loaded")
+    if not _sig:
+        P, I, LG = c_void_p, c_int, c_long
+        L.pha_gemm.argtypes = [I, I, I, I, P, LG, P, LG, P, LG, P, LG, LG, LG, I, P, P, P, P]
+        L.pha_gemm.restype = c_int
+        _sig = True
+    return L
+
+
+def _ptr(t):
+    return c_void_p(0 if t is None else t.data_ptr())
+
+
+def _zero_page(dev):
+    z = _zero.get(dev)
+    if z is None:
+        z = torch.zeros(256, dtype=torch.uint8, device=dev)
+        _zero[dev] = z
+    return z
+
+
+def _num_cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def _pick_splitk(M, N, K, dev, force=None):
+    if force is not None:
+        return max(1, int(force))
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    target = 2 * _num_cus(dev)
+    if tiles >= target or K < 2048:
+        return 1
+    s = min(target // max(tiles, 1), K // 1024, 64)
+    return max(1, s)
+
+
+def gemm_raw(amode, bmode, a, lda, b, ldb, c, ldc, M, N, K, bias=None, act=None, conv=None, splitk=None):
+    """Launch one GEMM; all tensors must already have the layouts the modes describe."""
+    dev = c.device
+    sk = _pick_splitk(M, N, K, dev, splitk)
+    ws = torch.empty(sk * M * N, dtype=torch.float32, device=dev) if sk > 1 else None
+    cv = None
+    if conv is not None:
+        cv = (ctypes.c_int * 14)(*conv)
+    stream = c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    rc = _L().pha_gemm(_DT[c.dtype], amode, bmode, EPI[act], _ptr(a), lda, _ptr(b), ldb, _ptr(c), ldc,
+                       _ptr(bias), M, N, K, sk, _ptr(ws), cv, _ptr(_zero_page(dev)), stream)
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm failed (hip error {rc}) M={M} N={N} K={K} modes=({amode},{bmode})")
+    return c
+
+
+# ----------------------------------------------------------------------------- dense matmul
+def matmul(a, b, trans_a=False, trans_b=False, bias=None, act=None):
+    """2-D bf16/fp16 matmul on the MFMA kernel: op(a) @ op(b) (+bias) (+act)."""
+    assert a.dim() == 2 and b.dim() == 2 and a.dtype == b.dtype and a.dtype in _DT
+    a, b = a.contiguous(), b.contiguous()
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    assert K == Kb and K % 8 == 0
+    out = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    am = A_COL if trans_a else A_ROW          # a^T stored [K][M]
+    bm = B_ROW if trans_b else B_COL          # b^T stored [N][K] is K-contiguous
+    lda = a.shape[1]
+    ldb = b.shape[1]
+    return gemm_raw(am, bm, a, lda, b, ldb, out, N, M, N, K, bias=bias, act=act)
+
+
+# ----------------------------------------------------------------------------- conv
+def _geo(N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, dh, dw):
+    return [N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, dh, dw]
+
+
+def supported(x, weight, groups):
+    return (x.is_cuda and x.dtype in _DT and weight.dtype == x.dtype and groups == 1 and x.dim() == 4
+            and x.shape[-1] % 8 == 0 and weight.shape[0] % 8 == 0 and _lib.native_available())
+
+
+def conv_fwd(x, weight, stride, padding, dilation, bias=None, act=None):
+    N, H, W, C = x.shape
+    Co, Ci, KH, KW = weight.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+    wt = weight.permute(0, 2, 3, 1).contiguous()  # [Co][KH][KW][Ci] = B^T, K-contiguous
+    out = torch.empty(N, OH, OW, Co, dtype=x.dtype, device=x.device)
+    K = KH * KW * Ci
+    gemm_raw(A_CONV, B_ROW, x.contiguous(), C, wt, K, out, Co, N * OH * OW, Co, K,
+             bias=bias, act=act, conv=_geo(N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, dh, dw))
+    return out
+
+
+def conv_bwd_data(dy, weight, x_shape, stride, padding, dilation):
+    N, H, W, Ci = x_shape
+    Co, _, KH, KW = weight.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    _, OH, OW, _ = dy.shape
+    dy = dy.contiguous()
+    if (sh, sw) == (1, 1):
+        # dX = conv(dY, flip(W)^T) with pad' = d*(K-1) - p, dilation d
+        wt = weight.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Ci][KH][KW][Co]
+        dx = torch.empty(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
+        K = KH * KW * Co
+        gemm_raw(A_CONV, B_ROW, dy, Co, wt, K, dx, Ci, N * H * W, Ci, K,
+                 conv=_geo(N, OH, OW, Co, H, W, KH, KW, 1, 1, dh * (KH - 1) - ph, dw * (KW - 1) - pw, dh, dw))
+        return dx
+    if (dh, dw) != (1, 1):
+        raise NotImplementedError("strided + dilated conv grad")
+    dx = torch.zeros(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
+    for rh in range(sh):
+        for rw in range(sw):
+            hs = list(range(rh, H, sh))
+            ws_ = list(range(rw, W, sw))
+            if not hs or not ws_:
+                continue
+            # taps contributing to this output phase: kh = (rh + ph) mod sh + j*sh
+            kh0, kw0 = (rh + ph) % sh, (rw + pw) % sw
+            khs = list(range(kh0, KH, sh))
+            kws = list(range(kw0, KW, sw))
+            if not khs or not kws:
+                continue
+            bh, bw = (rh + ph - kh0) // sh, (rw + pw - kw0) // sw
+            nh, nw = len(khs), len(kws)
+            # phase output i' reads dY row i' + bh - j for tap j  ==  stride-1 conv with taps
+            # reversed (t = nh-1-j) and pad = nh-1-bh
+            sub = weight[:, :, khs[::-1], :][:, :, :, kws[::-1]]  # [Co][Ci][nh][nw]
+            wt = sub.permute(1, 2, 3, 0).contiguous()  # [Ci][nh][nw][Co]
+            PH, PW = len(hs), len(ws_)
+            tmp = torch.empty(N, PH, PW, Ci, dtype=dy.dtype, device=dy.device)
+            K = nh * nw * Co
+            gemm_raw(A_CONV, B_ROW, dy, Co, wt, K, tmp, Ci, N * PH * PW, Ci, K,
+                     conv=_geo(N, OH, OW, Co, PH, PW, nh, nw, 1, 1, nh - 1 - bh, nw - 1 - bw, 1, 1))
+            dx[:, rh::sh, rw::sw, :] = tmp
+    return dx
+
+
+def conv_bwd_weight(dy, x, w_shape, stride, padding, dilation):
+    Co, Ci, KH, KW = w_shape
+    N, H, W, C = x.shape
+    _, OH, OW, _ = dy.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    M, Nn, K = Co, KH * KW * Ci, N * OH * OW
+    dwt = torch.empty(Co, KH, KW, Ci, dtype=dy.dtype, device=dy.device)
+    gemm_raw(A_COL, B_CONV, dy.contiguous(), Co, x.contiguous(), 0, dwt, Nn, M, Nn, K,
+             conv=_geo(N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw, dh, dw))
+    return dwt.permute(0, 3, 1, 2).contiguous()
+
+
+class Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation):
+        ctx.save_for_backward(x, weight)
+        ctx.conf = (stride, padding, dilation, bias is not None)
+        return conv_fwd(x, weight, stride, padding, dilation, bias=None if bias is None else bias.float())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, has_bias = ctx.conf
+        gy = gy.contiguous()
+        dx = conv_bwd_data(gy, weight, x.shape, stride, padding, dilation) if ctx.needs_input_grad[0] else None
+        dw = conv_bwd_weight(gy, x, weight.shape, stride, padding, dilation) if ctx.needs_input_grad[1] else None
+        db = gy.float().sum((0, 1, 2)).to(gy.dtype) if has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+def conv2d_nhwc(x, weight, bias, stride, padding, dilation):
+    return Conv2dNHWC.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))

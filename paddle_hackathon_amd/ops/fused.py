@@ -111,7 +111,7 @@ def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
     for s in normalized_shape:
         H *= s
     if (_use_hip(x) and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float32, torch.float16)
-            and weight is not None and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 16384
+            and weight is not None and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 4096
             and (bias is None or bias.dtype == weight.dtype)):
         return _LayerNorm.apply(x, weight.reshape(-1), None if bias is None else bias.reshape(-1), float(eps))
     return TF.layer_norm(x, list(normalized_shape), weight, bias, eps)
@@ -287,5 +287,73 @@ def check_finite_and_unscale_(tensors, inv_scale):
 # ----------------------------------------------------------------------------
 # batch norm (training stats) — NHWC channel reduction
 # ----------------------------------------------------------------------------
-def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, channel_axis):
-    return TF.batch_norm(x, running_mean, running_var, weight, bias, True, 1 - momentum, eps)
+class _BatchNormNHWC(torch.autograd.Function):
+    """Training batch norm over the last (channel) dim with optional fused residual add + ReLU
+    (HIP kernels in csrc/kernels/batch_norm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+        w32 = weight.float() if weight is not None else torch.ones(x.shape[-1], device=x.device)
+        b32 = bias.float() if bias is not None else None
+        y, mean, istd = _hip.bn_fwd_train(x, w32, b32, running_mean, running_var, eps, momentum, residual, relu)
+        ctx.save_for_backward(x, y if relu else None, w32, mean, istd)
+        ctx.relu, ctx.has_res = relu, residual is not None
+        ctx.wdt = None if weight is None else weight.dtype
+        ctx.bdt = None if bias is None else bias.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, w32, mean, istd = ctx.saved_tensors
+        dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res)
+        return (dx, None if ctx.wdt is None else dw.to(ctx.wdt), None if ctx.bdt is None else db.to(ctx.bdt),
+                None, None, dres, None, None, None)
+
+
+def _bn_hip_ok(x, channel_axis):
+    return (_use_hip(x) and channel_axis in (-1, x.dim() - 1) and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and x.is_contiguous() and x.shape[-1] % 8 == 0 and x.numel() > 0)
+
+
+def batch_norm_train(x, weight, bias, running_mean, running_var, momentum, eps, channel_axis, residual=None,
+                     relu=False):
+    """Training-mode BN (Paddle momentum semantics: running = running*m + batch*(1-m)).
+    Channels-last inputs use the fused HIP kernels; other layouts fall back to torch."""
+    if _bn_hip_ok(x, channel_axis) and (running_mean is None or running_mean.dtype == torch.float32) and \
+            (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape)):
+        res = residual.contiguous() if residual is not None else None
+        return _BatchNormNHWC.apply(x, weight, bias, running_mean, running_var, res, float(momentum), float(eps),
+                                    bool(relu))
+    if channel_axis in (-1, x.dim() - 1) and x.dim() > 2:
+        perm = [0, x.dim() - 1] + list(range(1, x.dim() - 1))
+        xt = x.permute(*perm)
+        y = TF.batch_norm(xt, running_mean, running_var, weight, bias, True, 1 - momentum, eps)
+        inv = [0] + list(range(2, x.dim())) + [1]
+        y = y.permute(*inv)
+    else:
+        y = TF.batch_norm(x, running_mean, running_var, weight, bias, True, 1 - momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
+def batch_norm_infer(x, weight, bias, running_mean, running_var, eps, channel_axis, residual=None, relu=False):
+    """Eval-mode BN (frozen statistics) as one fused affine (+add)(+relu) pass."""
+    if _bn_hip_ok(x, channel_axis) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape)):
+        istd = torch.rsqrt(running_var.float() + eps)
+        scale = istd * (weight.float() if weight is not None else 1.0)
+        shift = (bias.float() if bias is not None else 0.0) - running_mean.float() * scale
+        if not torch.is_grad_enabled() or not (x.requires_grad or (weight is not None and weight.requires_grad)):
+            return _hip.bn_apply(x, scale.contiguous(), shift.contiguous(),
+                                 residual.contiguous() if residual is not None else None, relu)
+    shape = [1] * (x.dim() - 1) + [-1] if channel_axis in (-1, x.dim() - 1) else [1, -1] + [1] * (x.dim() - 2)
+    istd = torch.rsqrt(running_var + eps)
+    y = (x - running_mean.reshape(shape)) * istd.reshape(shape)
+    if weight is not None:
+        y = y * weight.reshape(shape)
+    if bias is not None:
+        y = y + bias.reshape(shape)
+    y = y.to(x.dtype)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y

@@ -39,6 +39,10 @@ def _L():
             "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P],
             "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
             "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
+            "pha_bn_num_blocks": [LG, I],
+            "pha_bn_fwd_train": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, F, F, I, P],
+            "pha_bn_apply": [I, P, P, P, LG, I, P, P, I, P],
+            "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P],
             "pha_chunk_size": [],
             "pha_tensor_meta_size": [],
         }
@@ -94,6 +98,62 @@ def layer_norm_bwd(dy, x, w, mean, rstd, has_bias):
     _check(_L().pha_layer_norm_bwd(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx),
                                    _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H, _stream(x)), "layer_norm_bwd")
     return dx, dw, db
+
+
+# ----------------------------------------------------------------------------
+# batch norm (channels-last [M, C] view), optional fused residual-add + ReLU
+# ----------------------------------------------------------------------------
+def bn_supported(x, C):
+    return x.is_cuda and x.dtype in _DT and x.is_contiguous() and C % 8 == 0 and x.numel() > 0 and x.shape[-1] == C
+
+
+def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=None, relu=False):
+    """x: [..., C] contiguous (NHWC). Returns y, save_mean, save_istd. Updates running stats in place."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    assert bn_supported(x, C) and w.dtype == torch.float32 and w.numel() == C
+    assert residual is None or (residual.shape == x.shape and residual.dtype == x.dtype and residual.is_contiguous())
+    assert running_mean is None or (running_mean.dtype == torch.float32 and running_mean.is_contiguous())
+    L = _L()
+    nb = L.pha_bn_num_blocks(M, C)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    part = torch.empty(nb * 2 * C, **f32)
+    stats = torch.empty(4, C, **f32)  # save_mean, save_istd, scale, shift
+    y = torch.empty_like(x)
+    _check(L.pha_bn_fwd_train(_DT[x.dtype], _ptr(x), _ptr(residual), _ptr(y), M, C, _ptr(w), _ptr(b),
+                              _ptr(running_mean), _ptr(running_var), _ptr(stats[0]), _ptr(stats[1]), _ptr(stats[2]),
+                              _ptr(stats[3]), _ptr(part), float(eps), float(momentum), int(relu), _stream(x)),
+           "bn_fwd_train")
+    return y, stats[0], stats[1]
+
+
+def bn_apply(x, scale, shift, residual=None, relu=False):
+    C = x.shape[-1]
+    M = x.numel() // C
+    assert bn_supported(x, C) and scale.dtype == torch.float32 and scale.numel() == C and shift.numel() == C
+    y = torch.empty_like(x)
+    _check(_L().pha_bn_apply(_DT[x.dtype], _ptr(x), _ptr(residual), _ptr(y), M, C, _ptr(scale.contiguous()),
+                             _ptr(shift.contiguous()), int(relu), _stream(x)), "bn_apply")
+    return y
+
+
+def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False):
+    C = x.shape[-1]
+    M = x.numel() // C
+    assert bn_supported(x, C) and dy.shape == x.shape and dy.dtype == x.dtype and dy.is_contiguous()
+    assert not relu or (y is not None and y.shape == x.shape)
+    L = _L()
+    nb = L.pha_bn_num_blocks(M, C)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    part = torch.empty(nb * 2 * C, **f32)
+    coef = torch.empty(3 * C, **f32)
+    dwb = torch.empty(2, C, **f32)
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if want_dres else None
+    _check(L.pha_bn_bwd(_DT[x.dtype], _ptr(dy), _ptr(x), _ptr(y), M, C, _ptr(w), _ptr(save_mean), _ptr(save_istd),
+                        _ptr(dx), _ptr(dres), _ptr(dwb[0]), _ptr(dwb[1]), _ptr(part), _ptr(coef), int(relu), _stream(x)),
+           "bn_bwd")
+    return dx, dwb[0], dwb[1], dres
 
 
 def softmax_fwd(x):

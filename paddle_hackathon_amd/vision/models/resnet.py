@@ -8,7 +8,22 @@ every activation channels-last, the layout MI355X conv/BN kernels run fastest in
 from __future__ import annotations
 
 from ... import nn
+from ...nn import functional as F
+from ...nn.layer.conv_norm_pool import _BatchNormBase
 from ...tensor import flatten
+
+
+def _bn_act(bn, x, residual=None, relu=True):
+    """bn(x) (+ residual) (+ relu) as ONE fused pass when ``bn`` is a plain BatchNorm layer
+    (the reference's fuse_bn_add_act_ops pass, done eagerly); otherwise the unfused ops."""
+    if type(bn) in (nn.BatchNorm2D, nn.BatchNorm) and getattr(bn, "_act", None) is None:
+        return F.batch_norm_act(x, bn._mean, bn._variance, bn.weight, bn.bias, bn.training, bn._momentum,
+                                bn._epsilon, bn._data_format, bn._use_global_stats, residual=residual,
+                                act="relu" if relu else None)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
 
 __all__ = ["ResNet", "BasicBlock", "BottleneckBlock", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
            "resnext50_32x4d", "resnext50_64x4d", "resnext101_32x4d", "resnext101_64x4d", "resnext152_32x4d",
@@ -34,11 +49,10 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        out = _bn_act(self.bn1, self.conv1(x))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn2, self.conv2(out), residual=identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -62,12 +76,11 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
+        out = _bn_act(self.bn1, self.conv1(x))
+        out = _bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn3, self.conv3(out), residual=identity)
 
 
 class ResNet(nn.Layer):
@@ -116,7 +129,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -213,3 +213,173 @@ def test_flash_attention_gqa():
     o = hip.FlashAttention.apply(q, k, v, True, None)
     ref = _ref_attn(q, k, v, True)
     assert (o.float() - ref).abs().max().item() < 2e-2
+
+
+# ----------------------------------------------------------------------------- batch norm (NHWC)
+def _bn_ref(x, w, b, res, relu, eps):
+    xf = x.float()
+    dims = tuple(range(x.dim() - 1))
+    mean = xf.mean(dims)
+    var = xf.var(dims, unbiased=False)
+    y = (xf - mean) / torch.sqrt(var + eps) * w + b
+    if res is not None:
+        y = y + res.float()
+    return torch.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 7, 7, 64), (4, 5, 3, 2048), (2, 3, 3, 4096), (3, 1, 1, 24), (1000, 8)])
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_batch_norm_nhwc_fwd_bwd(dt, shape, res, relu):
+    from paddle_hackathon_amd.ops import fused
+    torch.manual_seed(0)
+    C = shape[-1]
+    x = (torch.randn(shape, device="cuda") * 2 + 3).to(dt)  # non-zero mean exercises the shifted stats
+    w = (torch.rand(C, device="cuda") + 0.5).requires_grad_(True)
+    b = torch.randn(C, device="cuda").requires_grad_(True)
+    r = torch.randn(shape, device="cuda").to(dt) if res else None
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    xg = x.clone().requires_grad_(True)
+    rg = r.clone().requires_grad_(True) if res else None
+    y = fused.batch_norm_train(xg, w, b, rm, rv, 0.9, 1e-5, -1, residual=rg, relu=relu)
+    assert y.grad_fn is not None and "BatchNormNHWC" in type(y.grad_fn).__name__  # HIP path ran
+    xr = x.float().requires_grad_(True)
+    wr, br = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    ref = _bn_ref(xr, wr, br, rr, relu, 1e-5)
+    tol = _tol(dt) * 10
+    assert torch.allclose(y.float(), ref, atol=tol, rtol=tol), (y.float() - ref).abs().max()
+    # running stats: Paddle momentum semantics with unbiased variance
+    dims = tuple(range(x.dim() - 1))
+    assert torch.allclose(rm, 0.1 * x.float().mean(dims), atol=1e-3, rtol=1e-3)
+    assert torch.allclose(rv, 0.9 + 0.1 * x.float().var(dims, unbiased=True), atol=1e-2, rtol=1e-2)
+    dy = torch.randn(shape, device="cuda").to(dt)
+    y.backward(dy)
+    ref.backward(dy.float())
+    assert torch.allclose(xg.grad.float(), xr.grad, atol=tol * 4, rtol=tol * 4), (xg.grad.float() - xr.grad).abs().max()
+    assert torch.allclose(w.grad, wr.grad, atol=tol * 20, rtol=tol), (w.grad - wr.grad).abs().max()
+    assert torch.allclose(b.grad, br.grad, atol=tol * 20, rtol=tol)
+    if res:
+        assert torch.allclose(rg.grad.float(), rr.grad, atol=tol, rtol=tol)
+
+
+def test_batch_norm_large_m_stats_precision():
+    """3.2M rows/channel with mean 50, std 0.5 — E[x^2]-E[x]^2 in fp32 would lose the variance."""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(1)
+    x = (torch.randn(3200000, 64, device="cuda") * 0.5 + 50.0).to(torch.bfloat16)
+    w, b = torch.ones(64, device="cuda"), torch.zeros(64, device="cuda")
+    y, mean, istd = hip.bn_fwd_train(x, w, b, None, None, 1e-5, 0.9)
+    xf = x.double()
+    assert torch.allclose(mean.double(), xf.mean(0), atol=1e-4)
+    assert torch.allclose((1 / istd.double() ** 2), xf.var(0, unbiased=False), rtol=2e-3)
+
+
+def test_batch_norm_infer_fused():
+    from paddle_hackathon_amd.ops import fused
+    x = torch.randn(4, 6, 6, 128, device="cuda").to(torch.bfloat16)
+    w, b = torch.rand(128, device="cuda") + 0.5, torch.randn(128, device="cuda")
+    rm, rv = torch.randn(128, device="cuda"), torch.rand(128, device="cuda") + 0.5
+    r = torch.randn_like(x)
+    with torch.no_grad():
+        y = fused.batch_norm_infer(x, w, b, rm, rv, 1e-5, -1, residual=r, relu=True)
+    ref = torch.relu((x.float() - rm) / torch.sqrt(rv + 1e-5) * w + b + r.float())
+    assert torch.allclose(y.float(), ref, atol=5e-2, rtol=2e-2)
+
+
+def test_resnet50_nhwc_step_uses_fused_bn():
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.vision.models import resnet50
+    paddle.seed(0)
+    m = resnet50(data_format="NHWC", num_classes=10)
+    m = paddle.amp.decorate(m, level="O2", dtype="bfloat16")
+    opt = paddle.optimizer.Momentum(0.01, parameters=m.parameters(), multi_precision=True)
+    x = paddle.to_tensor(torch.randn(4, 64, 64, 3, device="cuda").to(torch.bfloat16))
+    y = paddle.to_tensor(torch.randint(0, 10, (4,), device="cuda"))
+    losses = []
+    for _ in range(3):
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            out = m(x)
+        loss = paddle.nn.functional.cross_entropy(out, y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    assert all(math.isfinite(l) for l in losses) and losses[-1] < losses[0]
+    assert float(m.bn1._variance.numpy().mean()) != 1.0  # running stats were updated by the HIP kernel
+
+
+# ----------------------------------------------------------------------------- MFMA GEMM / implicit-GEMM conv
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 264), (1024, 512, 4096), (8, 64, 8)])
+def test_mfma_gemm_layouts(ta, tb, M, N, K):
+    from paddle_hackathon_amd.ops import conv_gemm
+    if ta and M % 8:
+        pytest.skip("column-major A needs M % 8 == 0")
+    torch.manual_seed(0)
+    a = torch.randn((K, M) if ta else (M, K), device="cuda").to(torch.bfloat16)
+    b = torch.randn((N, K) if tb else (K, N), device="cuda").to(torch.bfloat16)
+    c = conv_gemm.matmul(a, b, ta, tb)
+    ref = (a.float().t() if ta else a.float()) @ (b.float().t() if tb else b.float())
+    err = (c.float() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+@pytest.mark.parametrize("splitk", [1, 4])
+def test_mfma_gemm_epilogue_and_splitk(act, splitk):
+    from paddle_hackathon_amd.ops import conv_gemm
+    torch.manual_seed(1)
+    M, N, K = 96, 256, 2048
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    bt = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    conv_gemm.gemm_raw(conv_gemm.A_ROW, conv_gemm.B_ROW, a, K, bt, K, out, N, M, N, K, bias=bias, act=act,
+                       splitk=splitk)
+    ref = a.float() @ bt.float().t() + bias
+    ref = {None: ref, "relu": torch.relu(ref), "gelu": TF.gelu(ref)}[act]
+    assert (out.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [
+    # N, H, W, Cin, Cout, k, stride, pad, dil
+    (2, 14, 14, 64, 64, 1, 1, 0, 1),
+    (2, 14, 14, 64, 128, 3, 1, 1, 1),
+    (2, 15, 13, 32, 64, 3, 2, 1, 1),
+    (2, 14, 14, 64, 128, 1, 2, 0, 1),
+    (2, 32, 32, 3, 64, 7, 2, 3, 1),
+    (1, 12, 12, 16, 32, 3, 1, 2, 2),
+    (3, 9, 9, 24, 40, 5, 2, 2, 1),
+])
+def test_conv2d_nhwc_fwd_bwd(cfg):
+    from paddle_hackathon_amd.nn.functional.conv import _hip_conv2d
+    N, H, W, Ci, Co, k, s, p, d = cfg
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Ci, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(Co, Ci, k, k, device="cuda") / (Ci * k * k) ** 0.5).to(torch.bfloat16).requires_grad_(True)
+    y = _hip_conv2d(x, w, None, [s, s], [p, p], [d, d], 1)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    ref = TF.conv2d(xr, wr, None, s, p, d).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    scale = ref.abs().max()
+    assert (y.float() - ref).abs().max() / scale < 2e-2
+    gy = torch.randn_like(ref)
+    y.backward(gy.to(torch.bfloat16))
+    ref.backward(gy)
+    gx = xr.grad.permute(0, 2, 3, 1)
+    assert (x.grad.float() - gx).abs().max() / gx.abs().max() < 3e-2
+    assert (w.grad.float() - wr.grad).abs().max() / wr.grad.abs().max() < 3e-2
+
+
+def test_conv_layer_nhwc_routes_to_hip():
+    import paddle_hackathon_amd as paddle
+    conv = paddle.nn.Conv2D(16, 32, 3, padding=1, data_format="NHWC")
+    conv = paddle.amp.decorate(conv, level="O2", dtype="bfloat16")
+    x = paddle.to_tensor(torch.randn(2, 8, 8, 16, device="cuda").to(torch.bfloat16))
+    x.stop_gradient = False
+    y = conv(x)
+    assert "Conv2dNHWC" in type(y._t.grad_fn).__name__
+    y.mean().backward()
+    assert conv.weight.grad is not None and x.grad is not None

@@ -25,9 +25,20 @@ for s in "$@"; do
       rm -rf $OUT/prof
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $ROOT/bench.py --steps 3 --warmup 2 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; rc=$?
       tail -3 $OUT/prof.log ;;
+    prof_resnet)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_resnet
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_resnet -o run --output-format csv -- python3 $ROOT/bench.py --model resnet50 --steps 3 --warmup 2 > $OUT/prof_resnet.log 2>&1; rc=$?
+      tail -3 $OUT/prof_resnet.log ;;
     tests)
       timeout -k 10 900 python -m pytest tests -m gpu -v -x --timeout 240 -k "not flash" > $OUT/pytest_gpu.log 2>&1; rc=$?
       tail -5 $OUT/pytest_gpu.log ;;
+    bench_gemm)
+      timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
+      cat $OUT/bench_gemm.log | tail -20 ;;
+    tests_k)
+      timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 240 -k "${TESTK}" > $OUT/pytest_k.log 2>&1; rc=$?
+      tail -15 $OUT/pytest_k.log ;;
     tests_fa)
       timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 120 -k "flash" > $OUT/pytest_fa.log 2>&1; rc=$?
       tail -5 $OUT/pytest_fa.log ;;
