@@ -400,7 +400,8 @@ PHA_API int pha_gemm(int dt, int amode, int bmode, int epi, const void* a, long 
                      void* c, long ldc, const float* bias, long M, long N, long K, int splitk, float* ws,
                      const int* conv, const void* zero, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
-  if (K % 8 != 0) return (int)hipErrorInvalidValue;
+  // K must be a multiple of 8 only when it is a contiguous (16-byte vector) dimension
+  if ((amode == A_ROW || amode == A_CONV || bmode == B_ROW) && K % 8 != 0) return (int)hipErrorInvalidValue;
   Params p{};
   p.a = a; p.b = b; p.c = c; p.bias = bias;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;

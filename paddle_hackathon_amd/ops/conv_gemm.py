@@ -63,11 +63,12 @@ def _num_cus(dev):
 def _pick_splitk(M, N, K, dev, force=None):
     if force is not None:
         return max(1, int(force))
+    # enough (tile x K-slice) blocks to cover every CU twice; each slice keeps >= 256 of K
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     target = 2 * _num_cus(dev)
-    if tiles >= target or K < 2048:
+    if tiles >= target or K < 1024:
         return 1
-    s = min(target // max(tiles, 1), K // 1024, 64)
+    s = min((target + tiles - 1) // tiles, K // 256, 1024)
     return max(1, s)
 
 

@@ -373,8 +373,9 @@ def test_conv2d_nhwc_fwd_bwd(cfg):
     assert (w.grad.float() - wr.grad).abs().max() / wr.grad.abs().max() < 3e-2
 
 
-def test_conv_layer_nhwc_routes_to_hip():
+def test_conv_layer_nhwc_routes_to_hip(monkeypatch):
     import paddle_hackathon_amd as paddle
+    monkeypatch.setenv("PHA_CONV_IMPL", "hip")
     conv = paddle.nn.Conv2D(16, 32, 3, padding=1, data_format="NHWC")
     conv = paddle.amp.decorate(conv, level="O2", dtype="bfloat16")
     x = paddle.to_tensor(torch.randn(2, 8, 8, 16, device="cuda").to(torch.bfloat16))
