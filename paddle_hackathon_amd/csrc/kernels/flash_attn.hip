@@ -19,6 +19,7 @@
 // Backward: a key-parallel dK/dV kernel and a query-parallel dQ kernel (see below) — no
 // atomics and no cross-workgroup reduction; both prefetch their next tile into registers.
 #include "common.h"
+#include <cstdlib>
 
 using namespace pha;
 
@@ -279,6 +280,215 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
         u32x2 w;
         w[0] = MF<T>::pack(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
         w[1] = MF<T>::pack(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *reinterpret_cast<u32x2*>(orow + d) = w;
+      }
+    if (h == 0) {
+      const float lse = (l_run > 0.f) ? (m_run + log2f(l_run)) * kLn2 : INFINITY;
+      LSE[((long)b * H + head) * S + q] = lse;
+    }
+  }
+}
+
+// ============================================================================================
+// Forward v2 (D = 128): workgroup = 8 waves = 256 query rows, 64-key tiles.
+//  * K and V staged row-major in a double-buffered LDS ring (one barrier per tile, tile t+1
+//    fetched into registers during tile t's MFMAs and written after them — T14).
+//  * V is never transposed in software: the PV A-operand (V^T[d][key]) is read with
+//    ds_read_b64_tr_b16 straight from the row-major V image (T10); rows are 256 B with the
+//    16-B chunk XOR (ch ^ ((row&3)<<2 | (row>>2)&3)) that makes those reads conflict-free.
+//  * K rows XOR-swizzled by (row & 15) for the conflict-free ds_read_b128 S^T A-operand.
+//  * everything else (swapped S^T = K Q^T, lane-local online softmax, deferred rescale,
+//    accumulator-as-B-operand P^T) as in fa_fwd_kernel.
+// ============================================================================================
+constexpr int BM2 = 256;
+constexpr int NT2 = 512;
+
+__device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR
+  return row * 256 + 16 * (chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x2 ds_read_tr16(const unsigned char* lds_ptr) {
+  const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(lds_ptr));
+  return __builtin_bit_cast(u32x2, r);
+}
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                        const T* __restrict__ V, T* __restrict__ O,
+                                                        float* __restrict__ LSE, int S, int Sk, int H, int Hk,
+                                                        float scale_log2) {
+  typedef typename MF<T>::frag frag;
+  constexpr int D = 128, CH = 16, ND = 4, NK = 8;
+  constexpr int TILE = BN * D * 2;                   // 16 KiB per K or V tile
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
+  const int nqb = (S + BM2 - 1) / BM2;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM2;
+  const int q = q0 + wid * 32 + lr;
+  const long qstride = (long)H * D, kstride = (long)Hk * D;
+  const T* Qb = Q + ((long)b * S) * qstride + (long)head * D;
+  const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * D;
+  const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * D;
+
+  frag qf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 v = {0, 0, 0, 0};
+    if (q < S) v = *reinterpret_cast<const u32x4*>(Qb + (long)q * qstride + 16 * kk + 8 * h);
+    qf[kk] = as_frag<frag>(v);
+  }
+  f32x16 o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) o[i] = zero16();
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM2);
+  const int ntile = (kend + BN - 1) / BN;
+  const int wave_q0 = q0 + wid * 32, wave_qmax = wave_q0 + 31;
+
+  // 64 keys x 16 chunks = 1024 chunks per operand: 2 per thread each for K and V
+  u32x4 kreg[2], vreg[2];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + NT2 * i;
+      const int key = k0 + (c >> 4), ch = c & 15;
+      const bool ok = key < Sk;
+      kreg[i] = ok ? *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+      vreg[i] = ok ? *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_tile = [&](int buf) {
+    unsigned char* kl = smem + buf * 2 * TILE;
+    unsigned char* vl = kl + TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + NT2 * i;
+      const int row = c >> 4, ch = c & 15;
+      *reinterpret_cast<u32x4*>(kl + k_lds_off<D>(row, ch)) = kreg[i];
+      *reinterpret_cast<u32x4*>(vl + v_lds_off(row, ch)) = vreg[i];
+    }
+  };
+
+  // per-lane constant parts of the transposed V read address
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+
+  if (ntile > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * BN;
+    const int cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + BN);
+    const unsigned char* kl = smem + cur * 2 * TILE;
+    const unsigned char* vl = kl + TILE;
+    if (!(CAUSAL && k0 > wave_qmax)) {
+      f32x16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        s[kb] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(kl + k_lds_off<D>(kb * 32 + lr, 2 * kk + h));
+          s[kb] = MF<T>::mma(as_frag<frag>(a), qf[kk], s[kb]);
+        }
+      }
+      const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wave_q0);
+      float tmax = -INFINITY;
+      if (need_mask) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + acc_row(r, h);
+            const bool masked = (key >= Sk) || (CAUSAL && key > q);
+            const float v = masked ? -INFINITY : s[kb][r] * scale_log2;
+            s[kb][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = s[kb][r] * scale_log2;
+            s[kb][r] = v;
+            tmax = fmaxf(tmax, v);
+          }
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      constexpr float kThr = 8.f;
+      if (!__all(tmax <= m_run + kThr)) {
+        const float m_new = fmaxf(m_run, tmax);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = exp2f(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        m_run = m_new;
+      }
+      const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(s[kb][r] - m_use);
+          s[kb][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 32, 64);
+      l_run += psum;
+
+      // O^T += V^T P^T : A = V^T via two transposed reads (keys 16ks+4h+{0..3}, +8)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f32x16& sv = s[ks >> 1];
+        const int s8 = (ks & 1) * 8;
+        u32x4 pw;
+        pw[0] = MF<T>::pack(sv[s8 + 0], sv[s8 + 1]);
+        pw[1] = MF<T>::pack(sv[s8 + 2], sv[s8 + 3]);
+        pw[2] = MF<T>::pack(sv[s8 + 4], sv[s8 + 5]);
+        pw[3] = MF<T>::pack(sv[s8 + 6], sv[s8 + 7]);
+        const frag pf = as_frag<frag>(pw);
+        const int row0 = 16 * ks + 4 * h + tq;
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          const int chunk = 4 * db + 2 * (g & 1) + (tp >> 1);
+          const u32x2 lo = ds_read_tr16(vl + v_lds_off(row0, chunk) + 8 * (tp & 1));
+          const u32x2 hi = ds_read_tr16(vl + v_lds_off(row0 + 8, chunk) + 8 * (tp & 1));
+          const u32x4 a = {lo[0], lo[1], hi[0], hi[1]};
+          o[db] = MF<T>::mma(as_frag<frag>(a), pf, o[db]);
+        }
+      }
+    }
+    if (t + 1 < ntile) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (q < S) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    T* orow = O + ((long)b * S + q) * qstride + (long)head * D;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(o[db][4 * gg + 0] * inv, o[db][4 * gg + 1] * inv);
+        w[1] = MF<T>::pack(o[db][4 * gg + 2] * inv, o[db][4 * gg + 3] * inv);
         *reinterpret_cast<u32x2*>(orow + d) = w;
       }
     if (h == 0) {
@@ -662,11 +872,24 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
   }
 }
 
+bool fwd_v2_enabled() {  // PHA_FA_FWD_V1=1 selects the 4-wave kernel (A/B comparisons)
+  const char* e = getenv("PHA_FA_FWD_V1");
+  return !(e && e[0] == '1');
+}
+
 template <typename T>
 int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk, int H, int Hk,
                int D, float scale, int causal, hipStream_t st) {
-  const dim3 grid((S + BM - 1) / BM, H, B), block(256);
   const float sl = scale * kLog2e;
+  if (D == 128 && fwd_v2_enabled()) {
+    const dim3 g2((S + BM2 - 1) / BM2, H, B), b2(NT2);
+    if (causal)
+      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl);
+    else
+      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl);
+    return (int)hipGetLastError();
+  }
+  const dim3 grid((S + BM - 1) / BM, H, B), block(256);
 #define FA_L(DD, CC) hipLaunchKernelGGL((fa_fwd_kernel<T, DD, CC>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl)
   if (D == 128) { if (causal) FA_L(128, true); else FA_L(128, false); }
   else if (D == 64) { if (causal) FA_L(64, true); else FA_L(64, false); }

@@ -33,6 +33,9 @@ for s in "$@"; do
     tests)
       timeout -k 10 900 python -m pytest tests -m gpu -v -x --timeout 240 -k "not flash" > $OUT/pytest_gpu.log 2>&1; rc=$?
       tail -5 $OUT/pytest_gpu.log ;;
+    bench_fa)
+      timeout -k 10 300 python tools/bench_fa.py > $OUT/bench_fa.log 2>&1; rc=$?
+      cat $OUT/bench_fa.log | tail -10 ;;
     bench_gemm)
       timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
       cat $OUT/bench_gemm.log | tail -20 ;;
