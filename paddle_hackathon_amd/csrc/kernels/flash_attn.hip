@@ -872,6 +872,324 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
   }
 }
 
+// ============================================================================================
+// Backward v2 (D = 128): 8-wave workgroups, one row-major LDS image per operand tile read
+// both by rows (ds_read_b128) and transposed (ds_read_b64_tr_b16) — the dual-use image of
+// T10 (256-B rows, chunk ^ ((row&3)<<2 | (row>>2)&3)), double-buffered, one barrier per tile.
+//
+//  fa_bwd_dkdv_v2: 128 keys per workgroup (4 waves, 32 per wave, key on the lane, K/V fragments and
+//    dK^T/dV^T accumulators in registers); 64-query tiles processed as two 32-row halves:
+//      S = Q K^T, dP = dO V^T        A = Q / dO rows (row reads)
+//      dV^T += dO^T P, dK^T += Q^T dS  A = dO^T / Q^T (transposed reads), B = accumulators
+//  fa_bwd_dq_v2: 256 queries per workgroup (query on the lane, Q/dO fragments in registers);
+//    64-key tiles:  S^T = K Q^T, dP^T = V dO^T (row reads), dQ^T += K^T dS^T (tr reads of K).
+// ============================================================================================
+__device__ __forceinline__ int dual_off(int row, int chunk) { return v_lds_off(row, chunk); }
+
+// 8 elements of a transposed operand: rows r0+{0..3} and r0+8+{0..3} of a dual image, the
+// lane's 32-column block (column block cb = 32-wide d block index)
+__device__ __forceinline__ u32x4 tr_frag(const unsigned char* img, int r0, int db, int g, int tq, int tp) {
+  const int chunk = 4 * db + 2 * (g & 1) + (tp >> 1);
+  const u32x2 lo = ds_read_tr16(img + dual_off(r0 + tq, chunk) + 8 * (tp & 1));
+  const u32x2 hi = ds_read_tr16(img + dual_off(r0 + 8 + tq, chunk) + 8 * (tp & 1));
+  return u32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// 4 waves (128 keys) with one wave per SIMD: the per-wave state (K/V fragments 64 regs, dK^T/dV^T
+// 128, S/dP 32, staging 32) exceeds the 256-register share two waves per SIMD would leave.
+constexpr int NTKV = 256;
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v2(const T* __restrict__ Q, const T* __restrict__ K,
+                                                      const T* __restrict__ V, const T* __restrict__ dO,
+                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                      T* __restrict__ dK, T* __restrict__ dV, int S, int Sk, int H,
+                                                      int Hk, float scale) {
+  typedef typename MF<T>::frag frag;
+  constexpr int D = 128, NK = 8, ND = 4, BQ = 64;
+  constexpr int IMG = BQ * 256;                         // 16 KiB per operand image
+  constexpr int BUF = 2 * IMG + 2 * BQ * 4;             // Q, dO, lse, delta
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int hk = head / (H / Hk);
+  const int k0 = blockIdx.x * (NTKV / 2);
+  const int wk0 = k0 + wid * 32;
+  const int key = wk0 + lr;
+  const long qstride = (long)H * D, kstride = (long)Hk * D;
+  const T* Qb = Q + (long)b * S * qstride + (long)head * D;
+  const T* dOb = dO + (long)b * S * qstride + (long)head * D;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * D;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * D;
+  const float* lse_b = LSE + ((long)b * H + head) * S;
+  const float* del_b = DELTA + ((long)b * H + head) * S;
+  const float scale_log2 = scale * kLog2e;
+
+  frag kf[NK], vf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (key < Sk) {
+      a = *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + 16 * kk + 8 * h);
+      c = *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + 16 * kk + 8 * h);
+    }
+    kf[kk] = as_frag<frag>(a);
+    vf[kk] = as_frag<frag>(c);
+  }
+  f32x16 dvt[ND], dkt[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
+
+  // staging: 64 rows x 16 chunks for Q and dO = 2048 chunks, 8 per thread; lse/delta 128 floats
+  constexpr int SPT = 2048 / NTKV;
+  u32x4 sreg[SPT];
+  float srow = 0.f;
+  auto load_tile = [&](int qt) {
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int c = tid + NTKV * i;              // [0, 2048): first 1024 Q, then dO
+      const int which = c >> 10, cc = c & 1023;
+      const int row = cc >> 4, ch = cc & 15;
+      const int qq = qt + row;
+      const T* src = which ? dOb : Qb;
+      sreg[i] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8) : u32x4{0, 0, 0, 0};
+    }
+    if (tid < 2 * BQ) {
+      const int qq = qt + (tid & (BQ - 1));
+      srow = (qq < S) ? (tid < BQ ? lse_b[qq] * kLog2e : del_b[qq]) : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) {
+      const int c = tid + NTKV * i;
+      const int which = c >> 10, cc = c & 1023;
+      *reinterpret_cast<u32x4*>(base + which * IMG + dual_off(cc >> 4, cc & 15)) = sreg[i];
+    }
+    if (tid < 2 * BQ) reinterpret_cast<float*>(base + 2 * IMG)[tid] = srow;
+  };
+
+  const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
+  const int ntile = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+  if (ntile > 0) {
+    load_tile(qstart);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int qt = qstart + t * BQ;
+    const int cur = t & 1;
+    if (t + 1 < ntile) load_tile(qt + BQ);
+    const unsigned char* q_img = smem + cur * BUF;
+    const unsigned char* do_img = q_img + IMG;
+    const float* lse_l = reinterpret_cast<const float*>(q_img + 2 * IMG);
+    const float* del_l = lse_l + BQ;
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      const int qh = qt + half * 32;
+      if (CAUSAL && wk0 > qh + 31) continue;      // every key of this wave is after every query
+      f32x16 sacc = zero16(), dpacc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const int row = half * 32 + lr;
+        const u32x4 qa = *reinterpret_cast<const u32x4*>(q_img + dual_off(row, 2 * kk + h));
+        const u32x4 ga = *reinterpret_cast<const u32x4*>(do_img + dual_off(row, 2 * kk + h));
+        sacc = MF<T>::mma(as_frag<frag>(qa), kf[kk], sacc);
+        dpacc = MF<T>::mma(as_frag<frag>(ga), vf[kk], dpacc);
+      }
+      const bool need_mask = (qh + 32 > S) || (wk0 + 32 > Sk) || (CAUSAL && wk0 + 31 > qh);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ql = half * 32 + acc_row(r, h);
+        const int qq = qt + ql;
+        float p = exp2f(sacc[r] * scale_log2 - lse_l[ql]);
+        if (need_mask && (qq >= S || key >= Sk || (CAUSAL && key > qq))) p = 0.f;
+        sacc[r] = p;
+        dpacc[r] = p * (dpacc[r] - del_l[ql]);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 pw, dw;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pw[j] = MF<T>::pack(sacc[8 * s2 + 2 * j], sacc[8 * s2 + 2 * j + 1]);
+          dw[j] = MF<T>::pack(dpacc[8 * s2 + 2 * j], dpacc[8 * s2 + 2 * j + 1]);
+        }
+        const int r0 = half * 32 + 16 * s2 + 4 * h;
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          const u32x4 av = tr_frag(do_img, r0, db, g, tq, tp);
+          const u32x4 bv = tr_frag(q_img, r0, db, g, tq, tp);
+          dvt[db] = MF<T>::mma(as_frag<frag>(av), as_frag<frag>(pw), dvt[db]);
+          dkt[db] = MF<T>::mma(as_frag<frag>(bv), as_frag<frag>(dw), dkt[db]);
+        }
+      }
+    }
+    if (t + 1 < ntile) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  if (key < Sk) {
+    T* dkr = dK + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;   // dK/dV are [B, Sk, H, D]
+    T* dvr = dV + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 wk, wv;
+        wk[0] = MF<T>::pack(dkt[db][4 * gg + 0] * scale, dkt[db][4 * gg + 1] * scale);
+        wk[1] = MF<T>::pack(dkt[db][4 * gg + 2] * scale, dkt[db][4 * gg + 3] * scale);
+        wv[0] = MF<T>::pack(dvt[db][4 * gg + 0], dvt[db][4 * gg + 1]);
+        wv[1] = MF<T>::pack(dvt[db][4 * gg + 2], dvt[db][4 * gg + 3]);
+        *reinterpret_cast<u32x2*>(dkr + d) = wk;
+        *reinterpret_cast<u32x2*>(dvr + d) = wv;
+      }
+  }
+}
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, const T* __restrict__ K,
+                                                    const T* __restrict__ V, const T* __restrict__ dO,
+                                                    const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale) {
+  typedef typename MF<T>::frag frag;
+  constexpr int D = 128, NK = 8, ND = 4;
+  constexpr int IMG = BN * 256;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const int nqb = (S + BM2 - 1) / BM2;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM2;
+  const int wq0 = q0 + wid * 32;
+  const int q = wq0 + lr;
+  const long qstride = (long)H * D, kstride = (long)Hk * D;
+  const T* Qb = Q + (long)b * S * qstride + (long)head * D;
+  const T* dOb = dO + (long)b * S * qstride + (long)head * D;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * D;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * D;
+  const float scale_log2 = scale * kLog2e;
+  const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
+  const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
+
+  frag qf[NK], gf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (q < S) {
+      a = *reinterpret_cast<const u32x4*>(Qb + (long)q * qstride + 16 * kk + 8 * h);
+      c = *reinterpret_cast<const u32x4*>(dOb + (long)q * qstride + 16 * kk + 8 * h);
+    }
+    qf[kk] = as_frag<frag>(a);
+    gf[kk] = as_frag<frag>(c);
+  }
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = zero16();
+
+  u32x4 kreg[2], vreg[2];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + NT2 * i;
+      const int kk = k0 + (c >> 4), ch = c & 15;
+      const bool ok = kk < Sk;
+      kreg[i] = ok ? *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+      vreg[i] = ok ? *reinterpret_cast<const u32x4*>(Vb + (long)kk * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_tile = [&](int buf) {
+    unsigned char* kl = smem + buf * 2 * IMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + NT2 * i;
+      *reinterpret_cast<u32x4*>(kl + dual_off(c >> 4, c & 15)) = kreg[i];
+      *reinterpret_cast<u32x4*>(kl + IMG + dual_off(c >> 4, c & 15)) = vreg[i];
+    }
+  };
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM2);
+  const int ntile = (kend + BN - 1) / BN;
+  if (ntile > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * BN;
+    const int cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + BN);
+    const unsigned char* k_img = smem + cur * 2 * IMG;
+    const unsigned char* v_img = k_img + IMG;
+    if (!(CAUSAL && k0 > wq0 + 31)) {
+      const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wq0);
+      // one 32-key block at a time keeps only 32 accumulator registers live for S/dP
+#pragma unroll 1
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 st = zero16(), dpt = zero16();
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const u32x4 ka = *reinterpret_cast<const u32x4*>(k_img + dual_off(kb * 32 + lr, 2 * kk + h));
+          const u32x4 va = *reinterpret_cast<const u32x4*>(v_img + dual_off(kb * 32 + lr, 2 * kk + h));
+          st = MF<T>::mma(as_frag<frag>(ka), qf[kk], st);
+          dpt = MF<T>::mma(as_frag<frag>(va), gf[kk], dpt);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kk = k0 + kb * 32 + acc_row(r, h);
+          float p = exp2f(st[r] * scale_log2 - lse2);
+          if (need_mask && (kk >= Sk || (CAUSAL && kk > q))) p = 0.f;
+          dpt[r] = p * (dpt[r] - dlt);
+        }
+        // dQ^T[d][q] += K^T[d][key] dS^T[key][q] for this block's two 16-key steps
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int s8 = s2 * 8;
+          u32x4 pw;
+          pw[0] = MF<T>::pack(dpt[s8 + 0], dpt[s8 + 1]);
+          pw[1] = MF<T>::pack(dpt[s8 + 2], dpt[s8 + 3]);
+          pw[2] = MF<T>::pack(dpt[s8 + 4], dpt[s8 + 5]);
+          pw[3] = MF<T>::pack(dpt[s8 + 6], dpt[s8 + 7]);
+          const frag pf = as_frag<frag>(pw);
+          const int r0 = kb * 32 + 16 * s2 + 4 * h;
+#pragma unroll
+          for (int db = 0; db < ND; ++db) {
+            const u32x4 a = tr_frag(k_img, r0, db, g, tq, tp);
+            dq[db] = MF<T>::mma(as_frag<frag>(a), pf, dq[db]);
+          }
+        }
+      }
+    }
+    if (t + 1 < ntile) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  if (q < S) {
+    T* qrow = dQ + ((long)b * S + q) * qstride + (long)head * D;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(dq[db][4 * gg + 0] * scale, dq[db][4 * gg + 1] * scale);
+        w[1] = MF<T>::pack(dq[db][4 * gg + 2] * scale, dq[db][4 * gg + 3] * scale);
+        *reinterpret_cast<u32x2*>(qrow + d) = w;
+      }
+  }
+}
+
+bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comparisons)
+  const char* e = getenv("PHA_FA_BWD_V1");
+  return !(e && e[0] == '1');
+}
+
 bool fwd_v2_enabled() {  // PHA_FA_FWD_V1=1 selects the 4-wave kernel (A/B comparisons)
   const char* e = getenv("PHA_FA_FWD_V1");
   return !(e && e[0] == '1');
@@ -902,6 +1220,17 @@ template <typename T>
 int launch_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
                void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
                hipStream_t st) {
+  if (D == 128 && bwd_v2_enabled()) {
+    const dim3 gk2((Sk + NTKV / 2 - 1) / (NTKV / 2), H, B), gq2((S + BM2 - 1) / BM2, H, B), b2(NT2), bk(NTKV);
+#define FB2(CC)                                                                                                    \
+    hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
+                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale);                           \
+    hipLaunchKernelGGL((fa_bwd_dq_v2<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,              \
+                       (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale)
+    if (causal) { FB2(true); } else { FB2(false); }
+#undef FB2
+    return (int)hipGetLastError();
+  }
   const dim3 gkv((Sk + 127) / 128, H, B), gq((S + BM - 1) / BM, H, B), block(256);
 #define FB_L(DD, CC)                                                                                               \
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, DD, CC>), gkv, block, 0, st, (const T*)q, (const T*)k, (const T*)v,   \

@@ -46,8 +46,15 @@ def main():
     qg, kg, vg = (x.clone().requires_grad_(True) for x in (q, k, v))
     o = hip.FlashAttention.apply(qg, kg, vg, causal, None)
     do = torch.randn_like(o)
-    t = timeit(lambda: torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True), 5)
-    print(f"bwd ours: {t * 1e3:.3f} ms  {2.5 * fl / t / 1e12:.1f} TF", flush=True)
+    grads = {}
+    for name, env in (("v1", "1"), ("v2", "0")):
+        os.environ["PHA_FA_BWD_V1"] = env
+        grads[name] = torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True)
+        t = timeit(lambda: torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True), 5)
+        print(f"bwd {name}: {t * 1e3:.3f} ms  {2.5 * fl / t / 1e12:.1f} TF", flush=True)
+    for n, a, b in zip("qkv", grads["v1"], grads["v2"]):
+        print(f"  d{n} v1 vs v2 max diff {(a.float() - b.float()).abs().max().item():.4f} "
+              f"(scale {a.float().abs().max().item():.3f})", flush=True)
     qs, ks, vs = (x.transpose(1, 2).clone().requires_grad_(True) for x in (q, k, v))
     os_ = TF.scaled_dot_product_attention(qs, ks, vs, is_causal=causal)
     dos = do.transpose(1, 2)
