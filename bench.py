@@ -34,6 +34,7 @@ def _args():
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--tp", type=int, default=1, help="GPT tensor-parallel degree (dp = gpus / tp)")
     return ap.parse_args()
 
 
@@ -52,26 +53,32 @@ def main():
 
     if a.model.startswith("resnet"):
         return bench_resnet(a, paddle, dist, world, rank)
+    if a.model.startswith("bert"):
+        return bench_bert(a, paddle, dist, world, rank)
 
     from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
-    cfg = gpt_config(a.model, max_position_embeddings=max(2048, a.seq_len), recompute=a.recompute)
+    tp = max(1, a.tp)
+    if world % tp:
+        raise SystemExit(f"--tp {tp} must divide the world size {world}")
+    dp = world // tp
+    if world > 1:
+        strategy = dist.fleet.DistributedStrategy()
+        strategy.hybrid_configs = {"dp_degree": dp, "mp_degree": tp, "pp_degree": 1}
+        dist.fleet.init(is_collective=True, strategy=strategy)
+    cfg = gpt_config(a.model, max_position_embeddings=max(2048, a.seq_len), recompute=a.recompute,
+                     tensor_parallel_degree=tp)
     model = GPTForPretraining(cfg)
     model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
     opt = paddle.optimizer.AdamW(learning_rate=1e-4, beta1=0.9, beta2=0.95, weight_decay=0.1,
                                  parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0),
                                  multi_precision=True)
     if world > 1:
-        strategy = dist.fleet.DistributedStrategy() if hasattr(dist, "fleet") else None
-        if strategy is not None:
-            strategy.hybrid_configs = {"dp_degree": world, "mp_degree": 1, "pp_degree": 1}
-            dist.fleet.init(is_collective=True, strategy=strategy)
-            model = dist.fleet.distributed_model(model)
-            opt = dist.fleet.distributed_optimizer(opt)
-        else:
-            model = paddle.DataParallel(model)
+        model = dist.fleet.distributed_model(model)
+        opt = dist.fleet.distributed_optimizer(opt)
     B, S = a.micro_batch, a.seq_len
     gen = torch.Generator(device="cuda")
-    gen.manual_seed(rank)
+    # tensor-parallel peers must see the same tokens: seed by data-parallel rank
+    gen.manual_seed(rank // tp)
     ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (B, S + 1), device="cuda", generator=gen))
     inp, lab = ids[:, :-1], ids[:, 1:]
     inp = paddle.Tensor(inp._t.contiguous())
@@ -107,7 +114,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / a.steps * 1000.0
-    tokens = B * S * world * a.steps
+    tokens = B * S * dp * a.steps
     value = tokens / elapsed
     if rank == 0:
         n_params = sum(p._t.numel() for p in (model._layers if hasattr(model, "_layers") else model).parameters())
@@ -117,11 +124,91 @@ def main():
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic (random token ids), random-init weights",
-            "config": {"model": "GPT-3-1.3B" if a.model == "gpt3-1.3b" else a.model, "global_batch": B * world,
-                       "seq_len": S, "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "n_params": n_params,
+            "config": {"model": "GPT-3-1.3B" if a.model == "gpt3-1.3b" else a.model, "global_batch": B * dp,
+                       "seq_len": S, "parallelism": f"dp{dp}" + (f"_tp{tp}" if tp > 1 else ""), "micro_batch_per_gpu": B,
+                       "n_params": n_params,
                        "optimizer": "AdamW fp32-master", "final_loss": round(float(loss.item()), 4)},
         }
         print(json.dumps(out), flush=True)
+
+
+def _timed(a, step, world, rank, dist):
+    import torch
+    for i in range(a.warmup):
+        tw = time.perf_counter()
+        loss = step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup {i} loss={float(loss.item()):.4f} {time.perf_counter() - tw:.3f}s", file=sys.stderr,
+                  flush=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, loss
+
+
+def bench_bert(a, paddle, dist, world, rank):
+    """BERT-base pre-training (MLM 15 % masked positions + NSP), seq 512, bf16 O2, AdamW."""
+    import torch
+    from paddle_hackathon_amd.models import bert_config, BertForPretraining, BertPretrainingCriterion
+    S = a.seq_len if a.seq_len != 2048 else 512
+    B = a.micro_batch if a.micro_batch != 8 else 32
+    cfg = bert_config(a.model if a.model in ("bert-base", "bert-large", "bert-tiny") else "bert-base",
+                      max_position_embeddings=max(512, S))
+    model = BertForPretraining(cfg)
+    crit = BertPretrainingCriterion(cfg.vocab_size)
+    model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, weight_decay=0.01, parameters=model.parameters(),
+                                 multi_precision=True)
+    if world > 1:
+        strategy = dist.fleet.DistributedStrategy()
+        strategy.hybrid_configs = {"dp_degree": world, "mp_degree": 1, "pp_degree": 1}
+        dist.fleet.init(is_collective=True, strategy=strategy)
+        model = dist.fleet.distributed_model(model)
+        opt = dist.fleet.distributed_optimizer(opt)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(rank)
+    ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (B, S), device="cuda", generator=g))
+    tt = paddle.to_tensor((torch.arange(S, device="cuda") >= S // 2).long().expand(B, S).contiguous())
+    n_mask = max(1, int(0.15 * S))
+    mpos = paddle.to_tensor((torch.randperm(S, device="cuda", generator=g)[:n_mask].unsqueeze(0)
+                             + S * torch.arange(B, device="cuda").unsqueeze(1)).reshape(-1))
+    mlab = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (B * n_mask,), device="cuda", generator=g))
+    nlab = paddle.to_tensor(torch.randint(0, 2, (B,), device="cuda", generator=g))
+
+    def step():
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            mlm, nsp = model(ids, tt, masked_positions=mpos)
+        loss = crit(mlm, nsp, mlab, nlab)
+        loss.backward()
+        opt.step()
+        opt.clear_grad(set_to_zero=False)
+        return loss
+
+    elapsed, loss = _timed(a, step, world, rank, dist)
+    value = B * world * a.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "samples/sec BERT-base pretraining bf16 (whole job)", "baseline_metric": BASELINE_METRIC,
+            "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic token ids / masks, random-init weights",
+            "config": {"model": "BERT-base" if cfg.hidden_size == 768 else a.model, "global_batch": B * world,
+                       "seq_len": S, "parallelism": f"dp{world}", "tokens_per_sec": round(value * S, 1),
+                       "final_loss": round(float(loss.item()), 4)}}), flush=True)
 
 
 def bench_resnet(a, paddle, dist, world, rank):

@@ -303,6 +303,13 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
 constexpr int BM2 = 256;
 constexpr int NT2 = 512;
 
+// element strides (token, head) of each operand, so packed [B, S, H, 3D] QKV projections and
+// their packed gradient are read/written in place (no split copies, no concat of dq/dk/dv)
+struct FaStrides {
+  long q_tok, kv_tok, o_tok, dq_tok, dkv_tok;
+  int q_head, kv_head, o_head, dq_head, dkv_head;
+};
+
 __device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR
   return row * 256 + 16 * (chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
@@ -319,7 +326,7 @@ template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                         const T* __restrict__ V, T* __restrict__ O,
                                                         float* __restrict__ LSE, int S, int Sk, int H, int Hk,
-                                                        float scale_log2) {
+                                                        float scale_log2, FaStrides fs) {
   typedef typename MF<T>::frag frag;
   constexpr int D = 128, CH = 16, ND = 4, NK = 8;
   constexpr int TILE = BN * D * 2;                   // 16 KiB per K or V tile
@@ -332,10 +339,10 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
   const int q = q0 + wid * 32 + lr;
-  const long qstride = (long)H * D, kstride = (long)Hk * D;
-  const T* Qb = Q + ((long)b * S) * qstride + (long)head * D;
-  const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * D;
-  const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * D;
+  const long qstride = fs.q_tok, kstride = fs.kv_tok;
+  const T* Qb = Q + ((long)b * S) * qstride + (long)head * fs.q_head;
+  const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
 
   frag qf[NK];
 #pragma unroll
@@ -480,7 +487,7 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 
   if (q < S) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-    T* orow = O + ((long)b * S + q) * qstride + (long)head * D;
+    T* orow = O + ((long)b * S + q) * fs.o_tok + (long)head * fs.o_head;
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
@@ -899,12 +906,12 @@ __device__ __forceinline__ u32x4 tr_frag(const unsigned char* img, int r0, int d
 // 128, S/dP 32, staging 32) exceeds the 256-register share two waves per SIMD would leave.
 constexpr int NTKV = 256;
 
-template <typename T, bool CAUSAL>
+template <typename T, bool CAUSAL, bool ILP2>
 __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v2(const T* __restrict__ Q, const T* __restrict__ K,
                                                       const T* __restrict__ V, const T* __restrict__ dO,
                                                       const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                       T* __restrict__ dK, T* __restrict__ dV, int S, int Sk, int H,
-                                                      int Hk, float scale) {
+                                                      int Hk, float scale, FaStrides fs) {
   typedef typename MF<T>::frag frag;
   constexpr int D = 128, NK = 8, ND = 4, BQ = 64;
   constexpr int IMG = BQ * 256;                         // 16 KiB per operand image
@@ -918,11 +925,11 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   const int k0 = blockIdx.x * (NTKV / 2);
   const int wk0 = k0 + wid * 32;
   const int key = wk0 + lr;
-  const long qstride = (long)H * D, kstride = (long)Hk * D;
-  const T* Qb = Q + (long)b * S * qstride + (long)head * D;
-  const T* dOb = dO + (long)b * S * qstride + (long)head * D;
-  const T* Kb = K + (long)b * Sk * kstride + (long)hk * D;
-  const T* Vb = V + (long)b * Sk * kstride + (long)hk * D;
+  const long kstride = fs.kv_tok;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * fs.kv_head;
   const float* lse_b = LSE + ((long)b * H + head) * S;
   const float* del_b = DELTA + ((long)b * H + head) * S;
   const float scale_log2 = scale * kLog2e;
@@ -954,7 +961,8 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       const int row = cc >> 4, ch = cc & 15;
       const int qq = qt + row;
       const T* src = which ? dOb : Qb;
-      sreg[i] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8) : u32x4{0, 0, 0, 0};
+      const long rs = which ? fs.o_tok : fs.q_tok;
+      sreg[i] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * rs + ch * 8) : u32x4{0, 0, 0, 0};
     }
     if (tid < 2 * BQ) {
       const int qq = qt + (tid & (BQ - 1));
@@ -987,8 +995,11 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     const unsigned char* do_img = q_img + IMG;
     const float* lse_l = reinterpret_cast<const float*>(q_img + 2 * IMG);
     const float* del_l = lse_l + BQ;
-#pragma unroll 1
+    // ILP2: both 32-row halves unrolled so the scheduler can overlap one half's LDS reads and
+    // softmax with the other's MFMAs (one wave per SIMD has no other wave to hide latency)
+#pragma unroll
     for (int half = 0; half < 2; ++half) {
+      if (!ILP2 && half == 1) __builtin_amdgcn_sched_barrier(0);
       const int qh = qt + half * 32;
       if (CAUSAL && wk0 > qh + 31) continue;      // every key of this wave is after every query
       f32x16 sacc = zero16(), dpacc = zero16();
@@ -1032,8 +1043,8 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     __syncthreads();
   }
   if (key < Sk) {
-    T* dkr = dK + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;   // dK/dV are [B, Sk, H, D]
-    T* dvr = dV + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;
+    T* dkr = dK + ((long)b * Sk + key) * fs.dkv_tok + (long)head * fs.dkv_head;   // per query head (GQA summed by caller)
+    T* dvr = dV + ((long)b * Sk + key) * fs.dkv_tok + (long)head * fs.dkv_head;
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
@@ -1054,7 +1065,7 @@ template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, const T* __restrict__ K,
                                                     const T* __restrict__ V, const T* __restrict__ dO,
                                                     const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale) {
+                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale, FaStrides fs) {
   typedef typename MF<T>::frag frag;
   constexpr int D = 128, NK = 8, ND = 4;
   constexpr int IMG = BN * 256;
@@ -1069,11 +1080,11 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
   const int q0 = qb * BM2;
   const int wq0 = q0 + wid * 32;
   const int q = wq0 + lr;
-  const long qstride = (long)H * D, kstride = (long)Hk * D;
-  const T* Qb = Q + (long)b * S * qstride + (long)head * D;
-  const T* dOb = dO + (long)b * S * qstride + (long)head * D;
-  const T* Kb = K + (long)b * Sk * kstride + (long)hk * D;
-  const T* Vb = V + (long)b * Sk * kstride + (long)hk * D;
+  const long kstride = fs.kv_tok;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * fs.kv_head;
   const float scale_log2 = scale * kLog2e;
   const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
   const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
@@ -1083,8 +1094,8 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
   for (int kk = 0; kk < NK; ++kk) {
     u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
     if (q < S) {
-      a = *reinterpret_cast<const u32x4*>(Qb + (long)q * qstride + 16 * kk + 8 * h);
-      c = *reinterpret_cast<const u32x4*>(dOb + (long)q * qstride + 16 * kk + 8 * h);
+      a = *reinterpret_cast<const u32x4*>(Qb + (long)q * fs.q_tok + 16 * kk + 8 * h);
+      c = *reinterpret_cast<const u32x4*>(dOb + (long)q * fs.o_tok + 16 * kk + 8 * h);
     }
     qf[kk] = as_frag<frag>(a);
     gf[kk] = as_frag<frag>(c);
@@ -1171,7 +1182,7 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
     __syncthreads();
   }
   if (q < S) {
-    T* qrow = dQ + ((long)b * S + q) * qstride + (long)head * D;
+    T* qrow = dQ + ((long)b * S + q) * fs.dq_tok + (long)head * fs.dq_head;
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
@@ -1185,6 +1196,11 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
   }
 }
 
+bool dkdv_ilp2() {  // PHA_FA_DKDV_ILP=0 serialises the two 32-row halves (A/B comparisons)
+  const char* e = getenv("PHA_FA_DKDV_ILP");
+  return !(e && e[0] == '0');
+}
+
 bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comparisons)
   const char* e = getenv("PHA_FA_BWD_V1");
   return !(e && e[0] == '1');
@@ -1195,16 +1211,26 @@ bool fwd_v2_enabled() {  // PHA_FA_FWD_V1=1 selects the 4-wave kernel (A/B compa
   return !(e && e[0] == '1');
 }
 
+FaStrides dense_strides(int H, int Hk, int D) {
+  FaStrides f;
+  f.q_tok = f.o_tok = f.dq_tok = f.dkv_tok = (long)H * D;
+  f.kv_tok = (long)Hk * D;
+  f.q_head = f.kv_head = f.o_head = f.dq_head = f.dkv_head = D;
+  return f;
+}
+
 template <typename T>
 int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk, int H, int Hk,
-               int D, float scale, int causal, hipStream_t st) {
+               int D, float scale, int causal, hipStream_t st, const FaStrides* fsp = nullptr) {
   const float sl = scale * kLog2e;
+  const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  if (fsp && !(D == 128 && fwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && fwd_v2_enabled()) {
     const dim3 g2((S + BM2 - 1) / BM2, H, B), b2(NT2);
     if (causal)
-      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl);
+      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
     else
-      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl);
+      hipLaunchKernelGGL((fa_fwd_v2_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
     return (int)hipGetLastError();
   }
   const dim3 grid((S + BM - 1) / BM, H, B), block(256);
@@ -1219,14 +1245,20 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
 template <typename T>
 int launch_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
                void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
-               hipStream_t st) {
+               hipStream_t st, const FaStrides* fsp = nullptr) {
+  const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  if (fsp && !(D == 128 && bwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && bwd_v2_enabled()) {
     const dim3 gk2((Sk + NTKV / 2 - 1) / (NTKV / 2), H, B), gq2((S + BM2 - 1) / BM2, H, B), b2(NT2), bk(NTKV);
 #define FB2(CC)                                                                                                    \
-    hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
-                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale);                           \
+    if (dkdv_ilp2())                                                                                               \
+      hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, true>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,    \
+                         (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                     \
+    else                                                                                                           \
+    hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, false>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
+                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                       \
     hipLaunchKernelGGL((fa_bwd_dq_v2<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,              \
-                       (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale)
+                       (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs)
     if (causal) { FB2(true); } else { FB2(false); }
 #undef FB2
     return (int)hipGetLastError();
@@ -1278,5 +1310,45 @@ PHA_API int pha_flash_attn_bwd(int dt, const void* q, const void* k, const void*
   if (H % Hk || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_bwd<bf16_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   if (dt == kF16) return launch_bwd<half_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+// Packed-QKV variants: q/k/v (and dq/dk/dv) are views into one [B, S, H, 3D] buffer with
+// token stride tok = 3*H*D and head stride 3*D; o / dO are dense [B, S, H, D]. D must be 128.
+PHA_API int pha_flash_attn_fwd_packed(int dt, const void* qkv, void* o, float* lse, int B, int S, int H, int D,
+                                      float scale, int causal, hipStream_t stream) {
+  if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
+  FaStrides f;
+  f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
+  f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
+  f.o_tok = (long)H * D;
+  f.o_head = D;
+  const size_t es = 2;
+  const char* base = static_cast<const char*>(qkv);
+  if (dt == kBF16)
+    return launch_fwd<bf16_t>(base, base + D * es, base + 2 * D * es, o, lse, B, S, S, H, H, D, scale, causal, stream, &f);
+  if (dt == kF16)
+    return launch_fwd<half_t>(base, base + D * es, base + 2 * D * es, o, lse, B, S, S, H, H, D, scale, causal, stream, &f);
+  return (int)hipErrorInvalidValue;
+}
+
+PHA_API int pha_flash_attn_bwd_packed(int dt, const void* qkv, const void* dout, const float* lse, const float* delta,
+                                      void* dqkv, int B, int S, int H, int D, float scale, int causal,
+                                      hipStream_t stream) {
+  if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
+  FaStrides f;
+  f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
+  f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
+  f.o_tok = (long)H * D;
+  f.o_head = D;
+  const size_t es = 2;
+  const char* in = static_cast<const char*>(qkv);
+  char* out = static_cast<char*>(dqkv);
+  if (dt == kBF16)
+    return launch_bwd<bf16_t>(in, in + D * es, in + 2 * D * es, dout, lse, delta, out, out + D * es, out + 2 * D * es, B,
+                              S, S, H, H, D, scale, causal, stream, &f);
+  if (dt == kF16)
+    return launch_bwd<half_t>(in, in + D * es, in + 2 * D * es, dout, lse, delta, out, out + D * es, out + 2 * D * es, B,
+                              S, S, H, H, D, scale, causal, stream, &f);
   return (int)hipErrorInvalidValue;
 }

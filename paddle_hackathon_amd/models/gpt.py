@@ -91,9 +91,9 @@ class GPTAttention(nn.Layer):
     def forward(self, x):
         B, S = x._t.shape[0], x._t.shape[1]
         qkv = self.qkv_proj(x)._t.reshape(B, S, self.num_heads, 3 * self.head_dim)
-        q, k, v = qkv.split(self.head_dim, dim=-1)
         drop = self.cfg.attention_dropout if self.training else 0.0
-        o = _ops.flash_attention(q, k, v, causal=True, dropout_p=drop, training=self.training)
+        o = _ops.fused.flash_attention_qkvpacked(qkv, self.num_heads, causal=True, dropout_p=drop,
+                                                 training=self.training)
         o = o.reshape(B, S, self.num_heads * self.head_dim)
         return self.out_proj(_wrap(o))
 

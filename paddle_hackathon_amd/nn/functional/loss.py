@@ -12,6 +12,12 @@ from ... import ops as _ops
 
 _w = _wrap
 
+
+def _up(t):
+    """Compute losses in fp32 for half inputs, at input precision otherwise (fp64 stays fp64)."""
+    return t.float() if t.dtype in (torch.float16, torch.bfloat16) else t
+
+
 __all__ = ["binary_cross_entropy", "binary_cross_entropy_with_logits", "cross_entropy", "softmax_with_cross_entropy",
            "ctc_loss", "dice_loss", "hinge_embedding_loss", "hsigmoid_loss", "kl_div", "l1_loss", "log_loss",
            "margin_ranking_loss", "mse_loss", "nll_loss", "npair_loss", "sigmoid_focal_loss", "smooth_l1_loss",
@@ -38,7 +44,7 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
     lab = label._t
     axis = axis % x.dim()
     if soft_label:
-        logp = TF.log_softmax(x.float(), axis) if use_softmax else torch.log(x.float())
+        logp = TF.log_softmax(_up(x), axis) if use_softmax else torch.log(_up(x))
         lf = lab.float()
         loss = -(lf * logp)
         if weight is not None:
@@ -60,7 +66,7 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
         if reduction == "sum":
             return _w(loss.sum())
         return _w(loss.unsqueeze(-1) if axis == input._t.dim() - 1 else loss)
-    logp = TF.log_softmax(x.float(), -1) if use_softmax else torch.log(x.float())
+    logp = TF.log_softmax(_up(x), -1) if use_softmax else torch.log(_up(x))
     C = logp.shape[-1]
     flat = logp.reshape(-1, C)
     lf = lab.reshape(-1)
@@ -86,8 +92,8 @@ def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-10
     x = logits._t
     axis = axis % x.dim()
     if soft_label:
-        logp = TF.log_softmax(x.float(), axis)
-        loss = -(label._t.float() * logp).sum(axis, keepdim=True)
+        logp = TF.log_softmax(_up(x), axis)
+        loss = -(label._t.to(logp.dtype) * logp).sum(axis, keepdim=True)
     else:
         lab = label._t
         if lab.dim() == x.dim():
@@ -230,7 +236,7 @@ def cosine_embedding_loss(input1, input2, label, margin=0, reduction="mean", nam
 
 def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, scale=64.0, group=None,
                          return_softmax=False, reduction="mean"):
-    x = logits._t.float()
+    x = _up(logits._t)
     lab = label._t.reshape(-1).long()
     theta = torch.acos(x.clamp(-1 + 1e-7, 1 - 1e-7))
     tgt = torch.cos(margin1 * theta + margin2) - margin3

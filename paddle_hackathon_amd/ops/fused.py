@@ -114,7 +114,9 @@ def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
             and weight is not None and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 4096
             and (bias is None or bias.dtype == weight.dtype)):
         return _LayerNorm.apply(x, weight.reshape(-1), None if bias is None else bias.reshape(-1), float(eps))
-    return TF.layer_norm(x, list(normalized_shape), weight, bias, eps)
+    ns = list(normalized_shape)
+    return TF.layer_norm(x, ns, None if weight is None else weight.reshape(ns),
+                         None if bias is None else bias.reshape(ns), eps)
 
 
 def rms_norm(x, weight, eps=1e-6):
@@ -160,7 +162,8 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
             l2 = l2.contiguous()
         loss = _SoftmaxCE.apply(l2, lab.to(torch.int64).contiguous(), int(ignore_index))
     else:
-        loss = TF.cross_entropy(l2.float(), lab.long(), reduction="none", ignore_index=ignore_index)
+        l2 = l2.float() if l2.dtype in (torch.float16, torch.bfloat16) else l2
+        loss = TF.cross_entropy(l2, lab.long(), reduction="none", ignore_index=ignore_index)
     return loss.reshape(shp)
 
 
@@ -199,6 +202,18 @@ def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=T
     o = TF.scaled_dot_product_attention(qt, kt, vt, dropout_p=dropout_p if training else 0.0,
                                         is_causal=causal, scale=scale)
     return o.transpose(1, 2)
+
+
+def flash_attention_qkvpacked(qkv, num_heads, causal=False, dropout_p=0.0, scale=None, training=True):
+    """qkv: [B, S, 3*H*D] or [B, S, H, 3D] fused projection (per head q|k|v) -> [B, S, H, D]."""
+    B, S = qkv.shape[0], qkv.shape[1]
+    q4 = qkv.reshape(B, S, num_heads, -1)
+    if (_use_hip(q4) and not (training and dropout_p > 0) and q4.is_contiguous()
+            and _hip.flash_attn_packed_supported(q4, num_heads)):
+        return _hip.FlashAttentionPacked.apply(q4, bool(causal), scale)
+    D = q4.shape[-1] // 3
+    q, k, v = q4.split(D, dim=-1)
+    return flash_attention(q, k, v, causal=causal, dropout_p=dropout_p, scale=scale, training=training)
 
 
 # ----------------------------------------------------------------------------

@@ -421,3 +421,54 @@ class FlashAttention(torch.autograd.Function):
             dk = dk.view(B, Sk, Hk, g, D).sum(3)
             dv = dv.view(B, Sk, Hk, g, D).sum(3)
         return dq, dk, dv, None, None
+
+
+def flash_attn_packed_supported(qkv, num_heads):
+    """qkv: [B, S, H, 3D] contiguous projection output (q|k|v per head), D == 128."""
+    import os
+    if os.environ.get("PHA_DISABLE_FLASH") == "1" or os.environ.get("PHA_FA_FWD_V1") == "1" \
+            or os.environ.get("PHA_FA_BWD_V1") == "1":
+        return False
+    L = _lib.lib
+    return (L is not None and hasattr(L, "pha_flash_attn_fwd_packed") and qkv.is_cuda and qkv.dim() == 4
+            and qkv.dtype in (torch.bfloat16, torch.float16) and qkv.is_contiguous() and qkv.shape[2] == num_heads
+            and qkv.shape[3] == 3 * 128)
+
+
+class FlashAttentionPacked(torch.autograd.Function):
+    """Self-attention straight from the fused QKV projection [B, S, H, 3D]: the kernels read q/k/v
+    in place (strided) and the backward writes dq/dk/dv into one packed [B, S, H, 3D] gradient,
+    so neither the three split copies nor the concat of their gradients exists."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale):
+        B, S, H, D3 = qkv.shape
+        D = D3 // 3
+        sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+        o = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+        L = _L()
+        L.pha_flash_attn_fwd_packed.restype = c_int
+        _check(L.pha_flash_attn_fwd_packed(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(o), _ptr(lse), c_int(B), c_int(S),
+                                           c_int(H), c_int(D), c_float(sc), c_int(int(causal)), _stream(qkv)),
+               "flash_attn_fwd_packed")
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale = causal, sc
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        B, S, H, D3 = qkv.shape
+        D = D3 // 3
+        L = _L()
+        L.pha_flash_attn_bwd_packed.restype = c_int
+        delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+        dqkv = torch.empty_like(qkv)
+        _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[qkv.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B),
+                                               c_int(S), c_int(H), c_int(D), _stream(qkv)), "flash_attn_bwd_preprocess")
+        _check(L.pha_flash_attn_bwd_packed(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(do), _ptr(lse), _ptr(delta),
+                                           _ptr(dqkv), c_int(B), c_int(S), c_int(H), c_int(D), c_float(ctx.scale),
+                                           c_int(int(ctx.causal)), _stream(qkv)), "flash_attn_bwd_packed")
+        return dqkv, None, None

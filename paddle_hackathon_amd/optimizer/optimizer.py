@@ -215,7 +215,17 @@ class Optimizer:
                     src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
                     with torch.no_grad():
                         m._t.copy_(src.to(m._t.device, torch.float32))
-        self._state_loaded.update(state_dict)
+        # snapshot the rest (loaded lazily on first use): the caller's dict may hold live tensors
+        # of another optimizer that keep changing after this call
+        snap = {}
+        for k, v in state_dict.items():
+            if isinstance(v, Tensor):
+                snap[k] = _wrap(v._t.detach().clone())
+            elif isinstance(v, dict):
+                snap[k] = {kk: (_wrap(vv._t.detach().clone()) if isinstance(vv, Tensor) else vv) for kk, vv in v.items()}
+            else:
+                snap[k] = v
+        self._state_loaded.update(snap)
 
     set_dict = set_state_dict
 

@@ -215,6 +215,27 @@ def test_flash_attention_gqa():
     assert (o.float() - ref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("S", [256, 320])
+def test_flash_attention_qkv_packed(causal, S):
+    """Packed [B,S,H,3D] path (strided reads, packed dqkv) == fp32 SDPA on the split views."""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(0)
+    B, H, D = 2, 4, 128
+    qkv = torch.randn(B, S, H, 3 * D, device="cuda").bfloat16().requires_grad_(True)
+    assert hip.flash_attn_packed_supported(qkv, H)
+    o = hip.FlashAttentionPacked.apply(qkv, causal, None)
+    qr = qkv.detach().float().requires_grad_(True)
+    q, k, v = qr.split(D, dim=-1)
+    ref = _ref_attn(q, k, v, causal)
+    assert (o.float() - ref).abs().max().item() < 2e-2
+    g = torch.randn_like(ref)
+    o.backward(g.bfloat16())
+    ref.backward(g)
+    err = (qkv.grad.float() - qr.grad).abs().max().item()
+    assert err < 3e-2 * max(1.0, qr.grad.abs().max().item()), err
+
+
 # ----------------------------------------------------------------------------- batch norm (NHWC)
 def _bn_ref(x, w, b, res, relu, eps):
     xf = x.float()

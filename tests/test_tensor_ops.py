@@ -1,0 +1,226 @@
+"""OpTest-style checks (reference strategy: fluid/tests/unittests/op_test.py): each op's output
+against a NumPy reference, and analytic gradients against central finite differences in
+float64 (``get_numeric_gradient``)."""
+import numpy as np
+import pytest
+import torch
+
+import paddle_hackathon_amd as paddle
+
+rng = np.random.RandomState(0)
+
+
+def _r(*shape, lo=-1.0, hi=1.0):
+    return rng.uniform(lo, hi, shape).astype("float64")
+
+
+# ------------------------------------------------------------------- forward vs numpy
+UNARY = [
+    ("abs", np.abs), ("exp", np.exp), ("log", np.log, lambda x: np.abs(x) + 1.5),
+    ("sqrt", np.sqrt, lambda x: np.abs(x) + 0.1), ("rsqrt", lambda x: 1 / np.sqrt(x), lambda x: np.abs(x) + 0.1),
+    ("sin", np.sin), ("cos", np.cos), ("tanh", np.tanh), ("sigmoid", lambda x: 1 / (1 + np.exp(-x))),
+    ("floor", np.floor), ("ceil", np.ceil), ("round", np.round), ("square", np.square), ("sign", np.sign),
+    ("reciprocal", lambda x: 1 / x, lambda x: np.abs(x) + 0.5), ("log1p", np.log1p, lambda x: np.abs(x)),
+    ("erf", None), ("atan", np.arctan), ("sinh", np.sinh), ("cosh", np.cosh), ("expm1", np.expm1),
+]
+
+
+@pytest.mark.parametrize("case", UNARY, ids=[c[0] for c in UNARY])
+def test_unary_forward(case):
+    name, ref = case[0], case[1]
+    prep = case[2] if len(case) > 2 else (lambda x: x)
+    x = prep(_r(3, 5))
+    out = getattr(paddle, name)(paddle.to_tensor(x)).numpy()
+    if ref is None:
+        from scipy.special import erf
+        ref = erf
+    np.testing.assert_allclose(out, ref(x), rtol=1e-6, atol=1e-6)
+
+
+BINARY = [("add", np.add), ("subtract", np.subtract), ("multiply", np.multiply), ("divide", np.divide),
+          ("maximum", np.maximum), ("minimum", np.minimum), ("pow", lambda a, b: np.power(np.abs(a) + 0.5, b)),
+          ("atan2", np.arctan2), ("fmax", np.fmax), ("fmin", np.fmin)]
+
+
+@pytest.mark.parametrize("case", BINARY, ids=[c[0] for c in BINARY])
+def test_binary_broadcast(case):
+    name, ref = case
+    a, b = _r(4, 1, 5), _r(3, 1)
+    if name == "pow":
+        out = paddle.pow(paddle.to_tensor(np.abs(a) + 0.5), paddle.to_tensor(b)).numpy()
+    elif name == "divide":
+        b = np.abs(b) + 0.5
+        out = paddle.divide(paddle.to_tensor(a), paddle.to_tensor(b)).numpy()
+    else:
+        out = getattr(paddle, name)(paddle.to_tensor(a), paddle.to_tensor(b)).numpy()
+    np.testing.assert_allclose(out, ref(a, b), rtol=1e-6, atol=1e-7)
+
+
+def test_reductions():
+    x = _r(3, 4, 5)
+    t = paddle.to_tensor(x)
+    np.testing.assert_allclose(paddle.sum(t, axis=[0, 2]).numpy(), x.sum((0, 2)))
+    np.testing.assert_allclose(paddle.mean(t, axis=-1, keepdim=True).numpy(), x.mean(-1, keepdims=True))
+    np.testing.assert_allclose(paddle.max(t, axis=1).numpy(), x.max(1))
+    np.testing.assert_allclose(paddle.min(t).numpy(), x.min())
+    np.testing.assert_allclose(paddle.prod(t, axis=0).numpy(), x.prod(0))
+    np.testing.assert_allclose(paddle.std(t, axis=1).numpy(), x.std(1, ddof=1))
+    np.testing.assert_allclose(paddle.var(t, axis=1, unbiased=False).numpy(), x.var(1))
+    np.testing.assert_allclose(paddle.logsumexp(t, axis=2).numpy(), np.log(np.exp(x).sum(2)))
+    np.testing.assert_array_equal(paddle.argmax(t, axis=1).numpy(), x.argmax(1))
+    np.testing.assert_allclose(paddle.cumsum(t, axis=2).numpy(), np.cumsum(x, 2))
+    np.testing.assert_allclose(paddle.median(paddle.to_tensor(x[0])).numpy(), np.median(x[0]))
+    assert bool(paddle.all(paddle.to_tensor(x > -2)).numpy()) and not bool(paddle.any(t > 5).numpy())
+
+
+def test_manipulation():
+    x = _r(2, 3, 4)
+    t = paddle.to_tensor(x)
+    np.testing.assert_array_equal(paddle.reshape(t, [4, -1]).numpy(), x.reshape(4, -1))
+    np.testing.assert_array_equal(paddle.transpose(t, [2, 0, 1]).numpy(), x.transpose(2, 0, 1))
+    np.testing.assert_array_equal(paddle.concat([t, t], axis=1).numpy(), np.concatenate([x, x], 1))
+    np.testing.assert_array_equal(paddle.stack([t, t], axis=0).numpy(), np.stack([x, x]))
+    parts = paddle.split(t, [1, 3], axis=2)
+    np.testing.assert_array_equal(parts[1].numpy(), x[:, :, 1:])
+    np.testing.assert_array_equal(paddle.flip(t, [0, 2]).numpy(), x[::-1, :, ::-1])
+    np.testing.assert_array_equal(paddle.tile(t, [1, 2, 1]).numpy(), np.tile(x, (1, 2, 1)))
+    np.testing.assert_array_equal(paddle.squeeze(paddle.unsqueeze(t, 1), 1).numpy(), x)
+    idx = np.array([2, 0])
+    np.testing.assert_array_equal(paddle.gather(t, paddle.to_tensor(idx), axis=1).numpy(), x[:, idx])
+    np.testing.assert_array_equal(paddle.roll(t, 1, axis=2).numpy(), np.roll(x, 1, 2))
+    np.testing.assert_array_equal(paddle.flatten(t, 1).numpy(), x.reshape(2, -1))
+    np.testing.assert_array_equal(t[:, 1:, ::2].numpy(), x[:, 1:, ::2])
+    u = paddle.to_tensor(x.copy())
+    u[0, 1] = 5.0
+    y = x.copy()
+    y[0, 1] = 5.0
+    np.testing.assert_array_equal(u.numpy(), y)
+    s = paddle.scatter(paddle.zeros([4, 2]), paddle.to_tensor([1, 3]), paddle.ones([2, 2]))
+    assert s.numpy()[[1, 3]].sum() == 4 and s.numpy()[[0, 2]].sum() == 0
+
+
+def test_search_and_logic():
+    x = _r(5, 6)
+    t = paddle.to_tensor(x)
+    v, i = paddle.topk(t, 3, axis=1)
+    np.testing.assert_allclose(v.numpy(), -np.sort(-x, 1)[:, :3])
+    np.testing.assert_array_equal(paddle.argsort(t, axis=0).numpy(), np.argsort(x, 0, kind="stable"))
+    np.testing.assert_array_equal(paddle.where(t > 0, t, paddle.zeros_like(t)).numpy(), np.where(x > 0, x, 0))
+    np.testing.assert_array_equal(paddle.nonzero(t > 0.5).numpy(), np.stack(np.nonzero(x > 0.5), 1))
+    np.testing.assert_array_equal(paddle.logical_and(t > 0, t < 0.5).numpy(), (x > 0) & (x < 0.5))
+    np.testing.assert_array_equal(paddle.unique(paddle.to_tensor([3, 1, 3, 2])).numpy(), [1, 2, 3])
+    assert bool(paddle.allclose(t, t + 1e-9).numpy())
+    np.testing.assert_array_equal(paddle.masked_select(t, t > 0).numpy(), x[x > 0])
+
+
+def test_linalg_and_einsum():
+    a, b = _r(3, 4), _r(4, 5)
+    np.testing.assert_allclose(paddle.matmul(paddle.to_tensor(a), paddle.to_tensor(b)).numpy(), a @ b)
+    np.testing.assert_allclose(paddle.matmul(paddle.to_tensor(a), paddle.to_tensor(b.T), transpose_y=True).numpy(),
+                               a @ b)
+    m = _r(4, 4) + 4 * np.eye(4)
+    np.testing.assert_allclose(paddle.linalg.inv(paddle.to_tensor(m)).numpy(), np.linalg.inv(m), rtol=1e-6)
+    np.testing.assert_allclose(paddle.linalg.det(paddle.to_tensor(m)).numpy(), np.linalg.det(m), rtol=1e-6)
+    np.testing.assert_allclose(paddle.einsum("ij,jk->ik", paddle.to_tensor(a), paddle.to_tensor(b)).numpy(), a @ b)
+    np.testing.assert_allclose(paddle.linalg.norm(paddle.to_tensor(a)).numpy(), np.linalg.norm(a))
+    q, r = paddle.linalg.qr(paddle.to_tensor(m))
+    np.testing.assert_allclose((q.numpy() @ r.numpy()), m, atol=1e-8)
+
+
+def test_creation_and_random():
+    np.testing.assert_array_equal(paddle.arange(0, 10, 3).numpy(), np.arange(0, 10, 3))
+    np.testing.assert_allclose(paddle.linspace(0, 1, 5).numpy(), np.linspace(0, 1, 5), rtol=1e-6)
+    np.testing.assert_array_equal(paddle.eye(3).numpy(), np.eye(3))
+    np.testing.assert_array_equal(paddle.full([2, 2], 7).numpy(), np.full((2, 2), 7))
+    np.testing.assert_array_equal(paddle.tril(paddle.ones([3, 3])).numpy(), np.tril(np.ones((3, 3))))
+    paddle.seed(5)
+    a = paddle.rand([3]).numpy()
+    paddle.seed(5)
+    assert (paddle.rand([3]).numpy() == a).all()
+    assert paddle.randint(0, 5, [100]).numpy().max() < 5
+    assert paddle.randn([1000]).numpy().std() == pytest.approx(1.0, abs=0.15)
+    x = paddle.to_tensor([1, 2, 3], dtype="float32")
+    assert x.dtype == paddle.float32 and x.astype("int64").dtype == paddle.int64
+    assert x.shape == [3] and x.stop_gradient
+
+
+# ------------------------------------------------------------------- finite-difference gradients
+def _numeric_grad(f, x, eps=1e-6):
+    g = np.zeros_like(x)
+    it = np.nditer(x, flags=["multi_index"])
+    while not it.finished:
+        i = it.multi_index
+        xp, xm = x.copy(), x.copy()
+        xp[i] += eps
+        xm[i] -= eps
+        g[i] = (f(xp) - f(xm)) / (2 * eps)
+        it.iternext()
+    return g
+
+
+GRAD_CASES = [
+    ("tanh", lambda t: paddle.tanh(t).sum()),
+    ("matmul", lambda t: paddle.matmul(t, paddle.to_tensor(np.arange(12.0).reshape(4, 3) / 10)).sum()),
+    ("softmax", lambda t: (paddle.nn.functional.softmax(t, -1) * paddle.to_tensor(np.arange(4.0))).sum()),
+    ("log_softmax", lambda t: paddle.nn.functional.log_softmax(t, 0)[1].sum()),
+    ("layer_norm", lambda t: (paddle.nn.functional.layer_norm(t, [4]) * paddle.to_tensor(np.arange(4.0))).sum()),
+    ("gelu", lambda t: paddle.nn.functional.gelu(t).sum()),
+    ("silu", lambda t: paddle.nn.functional.silu(t).sum()),
+    ("cumprod", lambda t: paddle.cumprod(t, dim=1).sum()),
+    ("norm", lambda t: paddle.linalg.norm(t)),
+    ("gather", lambda t: paddle.gather(t, paddle.to_tensor([2, 0, 2]), axis=0).pow(2).sum()),
+    ("concat_split", lambda t: paddle.split(paddle.concat([t, t * 2], 1), 2, 1)[1].exp().sum()),
+    ("max", lambda t: paddle.max(t, axis=1).sum()),
+    ("cross_entropy", lambda t: paddle.nn.functional.cross_entropy(t, paddle.to_tensor([0, 3, 1]))),
+    ("mse", lambda t: paddle.nn.functional.mse_loss(t, paddle.ones_like(t))),
+    ("where", lambda t: paddle.where(t > 0, t * t, -t).sum()),
+    ("logsumexp", lambda t: paddle.logsumexp(t, axis=1).sum()),
+]
+
+
+@pytest.mark.parametrize("case", GRAD_CASES, ids=[c[0] for c in GRAD_CASES])
+def test_gradient_vs_finite_difference(case):
+    name, f = case
+    x = _r(3, 4)
+
+    def scalar(xv):
+        return float(f(paddle.to_tensor(xv)).numpy())
+
+    t = paddle.to_tensor(x, stop_gradient=False)
+    out = f(t)
+    out.backward()
+    np.testing.assert_allclose(t.grad.numpy(), _numeric_grad(scalar, x), rtol=1e-4, atol=1e-6)
+
+
+def test_paddle_grad_and_hooks():
+    x = paddle.to_tensor(_r(3), stop_gradient=False)
+    y = (x * x).sum()
+    (g,) = paddle.grad([y], [x], create_graph=True)
+    np.testing.assert_allclose(g.numpy(), 2 * x.numpy())
+    (g2,) = paddle.grad([g.sum()], [x])
+    np.testing.assert_allclose(g2.numpy(), 2 * np.ones(3))
+    seen = []
+    z = paddle.to_tensor(_r(3), stop_gradient=False)
+    z.register_hook(lambda grad: seen.append(grad.numpy()) or grad * 2)
+    (z * 3).sum().backward()
+    np.testing.assert_allclose(z.grad.numpy(), 6 * np.ones(3))
+    assert len(seen) == 1
+
+
+def test_pylayer_custom_backward():
+    from paddle_hackathon_amd.autograd import PyLayer
+
+    class Cube(PyLayer):
+        @staticmethod
+        def forward(ctx, x):
+            ctx.save_for_backward(x)
+            return x ** 3
+
+        @staticmethod
+        def backward(ctx, dy):
+            (x,) = ctx.saved_tensor()
+            return dy * 3 * x ** 2
+
+    x = paddle.to_tensor(_r(4), stop_gradient=False)
+    Cube.apply(x).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), 3 * x.numpy() ** 2)

@@ -17,6 +17,9 @@ for s in "$@"; do
     bench)
       timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
       tail -3 $OUT/bench.log ;;
+    bench_bert)
+      timeout -k 10 400 python bench.py --model bert-base --steps 10 --warmup 3 > $OUT/bench_bert.log 2>&1; rc=$?
+      tail -3 $OUT/bench_bert.log ;;
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
@@ -36,6 +39,9 @@ for s in "$@"; do
     bench_fa)
       timeout -k 10 300 python tools/bench_fa.py > $OUT/bench_fa.log 2>&1; rc=$?
       cat $OUT/bench_fa.log | tail -10 ;;
+    bench_fa_serial)
+      PHA_FA_DKDV_ILP=0 timeout -k 10 300 python tools/bench_fa.py > $OUT/bench_fa_serial.log 2>&1; rc=$?
+      cat $OUT/bench_fa_serial.log | tail -10 ;;
     bench_gemm)
       timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
       cat $OUT/bench_gemm.log | tail -20 ;;
