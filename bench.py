@@ -35,6 +35,10 @@ def _args():
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--tp", type=int, default=1, help="GPT tensor-parallel degree (dp = gpus / tp)")
+    ap.add_argument("--gemm-tuning", default="db", choices=["db", "tune", "off"],
+                    help="db: load the in-tree hipBLASLt solution database (TunableOp, no tuning); "
+                         "tune: benchmark solutions for new shapes and write the database; off: library heuristics")
+    ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     return ap.parse_args()
 
 
@@ -50,6 +54,12 @@ def main():
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     paddle.set_device(f"gpu:{torch.cuda.current_device()}")
     paddle.seed(1234 + rank)
+    if a.gemm_tuning != "off":
+        from paddle_hackathon_amd.incubate import autotune
+        n = autotune.enable_gemm_tuning(tune=(a.gemm_tuning == "tune"), filename=a.gemm_tuning_file,
+                                        max_tuning_ms=15)
+        if rank == 0:
+            print(f"[bench] gemm tuning={a.gemm_tuning} entries={n}", file=sys.stderr, flush=True)
 
     if a.model.startswith("resnet"):
         return bench_resnet(a, paddle, dist, world, rank)

@@ -271,6 +271,7 @@ class _Mode:
     static = False
     record_depth = 0
     trace = False  # op/layer host tracing on (paddle.profiler)
+    check_nan_inf = False  # FLAGS_check_nan_inf: scan every op/layer output (and its grad)
 
 
 _mode = _Mode()

@@ -21,9 +21,16 @@ def _record_hook(fn, name, args, kwargs):
 
 
 def _traced(fn, name, args, kwargs):
-    from ..profiler import _op_range
-    with _op_range(name, "Operator"):
-        return fn(*args, **kwargs)
+    if _mode.trace:
+        from ..profiler import _op_range
+        with _op_range(name, "Operator"):
+            out = fn(*args, **kwargs)
+    else:
+        out = fn(*args, **kwargs)
+    if _mode.check_nan_inf:
+        from .nan_inf import check_outputs
+        check_outputs(name, out)
+    return out
 
 
 def static_op(fn, name=None):
@@ -33,7 +40,7 @@ def static_op(fn, name=None):
     def wrapper(*args, **kwargs):
         if _mode.static and _mode.record_depth == 0:
             return _record_hook(fn, opname, args, kwargs)
-        if _mode.trace:
+        if _mode.trace or _mode.check_nan_inf:
             return _traced(fn, opname, args, kwargs)
         return fn(*args, **kwargs)
 

@@ -7,6 +7,7 @@ __all__ = ["set_flags", "get_flags", "flag"]
 
 _FLAGS = {
     "FLAGS_check_nan_inf": False,
+    "FLAGS_check_nan_inf_level": 0,
     "FLAGS_cudnn_deterministic": False,
     "FLAGS_use_autotune": False,
     "FLAGS_eager_delete_tensor_gb": 0.0,
@@ -25,9 +26,16 @@ for _k in list(_FLAGS):
         _FLAGS[_k] = (v.lower() in ("1", "true")) if isinstance(d, bool) else type(d)(v)
 
 
+def _sync_mode():
+    from .core import _mode
+    _mode.check_nan_inf = bool(_FLAGS["FLAGS_check_nan_inf"])
+
+
 def set_flags(flags):
     for k, v in flags.items():
         _FLAGS[k] = v
+        if k == "FLAGS_check_nan_inf":
+            _sync_mode()
         if k == "FLAGS_cudnn_deterministic":
             import torch
             torch.backends.cudnn.deterministic = bool(v)
@@ -41,3 +49,7 @@ def get_flags(flags):
 
 def flag(name, default=None):
     return _FLAGS.get(name, default)
+
+
+if _FLAGS["FLAGS_check_nan_inf"]:
+    _sync_mode()

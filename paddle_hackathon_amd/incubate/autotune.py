@@ -2,15 +2,49 @@
 
 kernel.enable → let MIOpen/hipBLASLt benchmark algorithms (torch.backends.cudnn.benchmark);
 layout.enable → prefer channels-last (NHWC) convolution layouts, the fast path on MI355X;
-dataloader.enable → let the DataLoader tune its worker count on first use."""
+dataloader.enable → let the DataLoader tune its worker count on first use.
+
+GEMM algorithm selection (the reference's kernel autotune for matmul, phi/kernels/autotune/)
+maps onto PyTorch's TunableOp over hipBLASLt/rocBLAS solutions: ``enable_gemm_tuning(tune=True)``
+benchmarks every solution for each new GEMM shape and writes the winners to a CSV;
+``enable_gemm_tuning()`` (tune=False) only loads the in-tree database
+(``paddle_hackathon_amd/tuning/gemm_tunableop_gfx950.csv``) so a run pays no tuning cost."""
 from __future__ import annotations
 
 import json
+import os
 import warnings
 
 import torch
 
-__all__ = ["set_config", "get_config"]
+__all__ = ["set_config", "get_config", "enable_gemm_tuning", "GEMM_TUNING_DB"]
+
+GEMM_TUNING_DB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                              "gemm_tunableop_gfx950.csv")
+
+
+def enable_gemm_tuning(tune=False, filename=None, max_tuning_ms=30):
+    """Turn on TunableOp GEMM dispatch. Returns the number of tuned entries loaded (or -1
+    when tuning writes to ``filename`` at process exit)."""
+    import torch.cuda.tunable as tun
+    path = filename or GEMM_TUNING_DB
+    tun.enable(True)
+    if tune:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        tun.set_filename(path, False)
+        tun.set_max_tuning_duration(int(max_tuning_ms))
+        tun.tuning_enable(True)
+        return -1
+    tun.tuning_enable(False)
+    if not os.path.exists(path):
+        tun.enable(False)
+        return 0
+    ok = tun.read_file(path)
+    if not ok:
+        warnings.warn(f"GEMM tuning database {path} rejected (library versions changed?)")
+        tun.enable(False)
+        return 0
+    return sum(1 for line in open(path) if line and not line.startswith("Validator"))
 
 _config = {"kernel": {"enable": False, "tuning_range": [1, 10]}, "layout": {"enable": False},
            "dataloader": {"enable": False, "tuning_steps": 500}}

@@ -247,10 +247,17 @@ class Layer:
         return h
 
     def __call__(self, *inputs, **kwargs):
-        if _core._mode.trace:
-            from ...profiler import _op_range
-            with _op_range(type(self).__name__, "Forward"):
-                return self._call_impl(*inputs, **kwargs)
+        if _core._mode.trace or _core._mode.check_nan_inf:
+            if _core._mode.trace:
+                from ...profiler import _op_range
+                with _op_range(type(self).__name__, "Forward"):
+                    out = self._call_impl(*inputs, **kwargs)
+            else:
+                out = self._call_impl(*inputs, **kwargs)
+            if _core._mode.check_nan_inf:
+                from ...framework.nan_inf import check_outputs
+                check_outputs(self.full_name() if hasattr(self, "full_name") else type(self).__name__, out)
+            return out
         return self._call_impl(*inputs, **kwargs)
 
     def _call_impl(self, *inputs, **kwargs):

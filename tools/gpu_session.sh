@@ -42,6 +42,14 @@ for s in "$@"; do
     bench_fa_serial)
       PHA_FA_DKDV_ILP=0 timeout -k 10 300 python tools/bench_fa.py > $OUT/bench_fa_serial.log 2>&1; rc=$?
       cat $OUT/bench_fa_serial.log | tail -10 ;;
+    tune_gemm)
+      # tune GPT + BERT GEMM shapes into gpurun_out/gemm_tunableop_gfx950.csv (copy into paddle_hackathon_amd/tuning/)
+      PYTORCH_TUNABLEOP_VERBOSE=1 timeout -k 10 900 python bench.py --steps 1 --warmup 1 --gemm-tuning tune --gemm-tuning-file $OUT/gemm_tunableop_gfx950.csv > $OUT/tune_gpt.log 2>&1; rc=$?
+      tail -2 $OUT/tune_gpt.log
+      if [ $rc = 0 ]; then PYTORCH_TUNABLEOP_VERBOSE=1 timeout -k 10 600 python bench.py --model bert-base --steps 1 --warmup 1 --gemm-tuning tune --gemm-tuning-file $OUT/gemm_tunableop_gfx950.csv > $OUT/tune_bert.log 2>&1; rc=$?; tail -2 $OUT/tune_bert.log; fi ;;
+    bench_tuned)
+      timeout -k 10 400 python bench.py --steps 10 --warmup 3 --gemm-tuning db --gemm-tuning-file $OUT/gemm_tunableop_gfx950.csv > $OUT/bench_tuned.log 2>&1; rc=$?
+      tail -3 $OUT/bench_tuned.log ;;
     bench_gemm)
       timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
       cat $OUT/bench_gemm.log | tail -20 ;;
