@@ -44,6 +44,12 @@ template <> struct Cvt<half_t> {
   static __device__ __forceinline__ void st(half_t* p, long i, float v) { p[i].v = (_Float16)v; }
 };
 
+// round a float to T's precision and back (what storing to T and reloading would give)
+template <typename T> __device__ __forceinline__ float round_to(float v);
+template <> __device__ __forceinline__ float round_to<float>(float v) { return v; }
+template <> __device__ __forceinline__ float round_to<bf16_t>(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+template <> __device__ __forceinline__ float round_to<half_t>(float v) { return (float)(_Float16)v; }
+
 // ---- 8-wide vector load/store (16 B for 2-byte types, 2x16 B for fp32) -----------
 template <typename T> struct Vec8;
 template <> struct Vec8<bf16_t> {

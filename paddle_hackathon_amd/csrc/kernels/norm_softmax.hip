@@ -18,10 +18,13 @@ namespace {
 constexpr int kWaves = 4;
 
 template <typename T, typename W, int NCH>
+// With `r` set: the pre-LN residual add is fused in — hs = x + r (rounded to T, exactly what
+// a separate add would store) is written out and normalised, saving one full read+write pass.
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int rows, int H, float eps) {
+                                                     int rows, int H, float eps, const T* __restrict__ r = nullptr,
+                                                     T* __restrict__ hs = nullptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -33,6 +36,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
     const int col = c * 512 + lane * 8;
     if (col < H) {
       Vec8<T>::ld(xr + col, v[c]);
+      if (r) {
+        float rv[8];
+        Vec8<T>::ld(r + (long)row * H + col, rv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = round_to<T>(v[c][i] + rv[i]);  // stats on the stored sum
+        Vec8<T>::st(hs + (long)row * H + col, v[c]);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) s += v[c][i];
     } else {
@@ -68,12 +78,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 }
 
 // dx per row + per-block partial column sums of dy*xhat (dw) and dy (db).
-template <typename T, typename W, int NCH>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                     const W* __restrict__ w, const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd, T* __restrict__ dx,
-                                                     float* __restrict__ part_w, float* __restrict__ part_b,
-                                                     int rows, int H) {
+// BW waves per block (16 -> 1024 threads): a grid of one block per CU then still gives 4
+// waves per SIMD to hide HBM latency, while the dw/db partials stay one [H] row per block.
+template <typename T, typename W, int NCH, int BW>
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 4 ? 4 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                         const W* __restrict__ w, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, T* __restrict__ dx,
+                                                         float* __restrict__ part_w, float* __restrict__ part_b,
+                                                         int rows, int H, const T* __restrict__ dres) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float aw[NCH][8], ab[NCH][8];
@@ -82,7 +94,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
     for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; }
 
-  for (int row = blockIdx.x * kWaves + wid; row < rows; row += gridDim.x * kWaves) {
+  for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
     const float mu = mean[row], rs = rstd[row];
     const T* xr = x + (long)row * H;
     const T* gr = dy + (long)row * H;
@@ -122,30 +134,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
           aw[c][i] += gv[i] * xh;
           ab[c][i] += gv[i];
         }
+        if (dres) {  // fused residual branch: dx += d(sum output)
+          float rv[8];
+          Vec8<T>::ld(dres + (long)row * H + col, rv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += rv[i];
+        }
         Vec8<T>::st(dr + col, o);
       }
     }
   }
-  // block reduction of the 4 waves' partial column sums through LDS, one column chunk at a time
-  __shared__ float red[kWaves][512];
+  // block reduction of the BW waves' partial column sums through LDS, one column chunk at a time
+  __shared__ float red[BW][512];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int col = c * 512 + lane * 8;
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = pass == 0 ? aw[c][i] : ab[c][i];
       __syncthreads();
-      // 256 threads reduce 512 columns: 2 columns per thread
-      for (int k = threadIdx.x; k < 512; k += 256) {
+      for (int k = threadIdx.x; k < 512; k += BW * 64) {
         const int cc = c * 512 + k;
         if (cc < H) {
-          float t = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+          float t = 0.f;
+#pragma unroll
+          for (int q = 0; q < BW; ++q) t += red[q][k];
           float* dst = pass == 0 ? part_w : part_b;
           dst[(long)blockIdx.x * H + cc] = t;
         }
       }
       __syncthreads();
-      (void)col;
     }
   }
 }
@@ -270,47 +287,69 @@ int dispatch_nch(int H, F&& f) {
 
 }  // namespace
 
-PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
-                               float* mean, float* rstd, int rows, int H, float eps, hipStream_t stream) {
-  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
+// r / hs (optional, both or neither): fused residual add, hs = x + r is normalised and stored.
+PHA_API int pha_layer_norm_fwd2(int dt, int wdt, const void* x, const void* r, void* hs, const void* w, const void* b,
+                                void* y, float* mean, float* rstd, int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 || rows <= 0 || (!r) != (!hs)) return (int)hipErrorInvalidValue;
   const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
   int rc = 0;
   PHA_DISPATCH_T(dt, T, {
     if (wdt == kF32) {
       rc = dispatch_nch(H, [&](auto nch) {
         hipLaunchKernelGGL((ln_fwd_kernel<T, float, decltype(nch)::value>), grid, block, 0, stream,
-                           (const T*)x, (const float*)w, (const float*)b, (T*)y, mean, rstd, rows, H, eps);
+                           (const T*)x, (const float*)w, (const float*)b, (T*)y, mean, rstd, rows, H, eps,
+                           (const T*)r, (T*)hs);
       });
     } else {
       rc = dispatch_nch(H, [&](auto nch) {
         hipLaunchKernelGGL((ln_fwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
-                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, H, eps);
+                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, H, eps,
+                           (const T*)r, (T*)hs);
       });
     }
   });
   return rc;
 }
 
-// part_w / part_b: workspace [nblocks, H] fp32 each; dw/db outputs (may be null db).
-PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, const void* w, const float* mean,
-                               const float* rstd, void* dx, void* dw, void* db, float* part_w, float* part_b,
-                               int nblocks, int rows, int H, hipStream_t stream) {
-  if (H % 8 || rows <= 0) return (int)hipErrorInvalidValue;
-  const dim3 grid(nblocks), block(256);
+// waves per block of the LN backward: 16 while the dw/db accumulators fit the 128-VGPR
+// budget of 4 waves/SIMD (H <= 1536), 8 above (two blocks per CU).
+constexpr int bwd_waves(int nch) { return nch <= 3 ? 16 : 8; }
+
+PHA_API int pha_layer_norm_bwd_nblocks(int rows, int H) {
+  const int bw = bwd_waves((H + 511) / 512);
+  const int cap = bw == 16 ? 256 : 512;
+  const int need = (rows + bw - 1) / bw;
+  return need < cap ? need : cap;
+}
+
+PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
+                               float* mean, float* rstd, int rows, int H, float eps, hipStream_t stream) {
+  return pha_layer_norm_fwd2(dt, wdt, x, nullptr, nullptr, w, b, y, mean, rstd, rows, H, eps, stream);
+}
+
+// part_w / part_b: workspace [nblocks, H] fp32 each (nblocks = pha_layer_norm_bwd_nblocks);
+// dw/db outputs (may be null db); dres (optional): gradient of the fused residual sum, added to dx.
+PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, const void* w, const float* mean,
+                                const float* rstd, const void* dres, void* dx, void* dw, void* db, float* part_w,
+                                float* part_b, int nblocks, int rows, int H, hipStream_t stream) {
+  if (H % 8 || rows <= 0 || nblocks <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid(nblocks);
   int rc = 0;
   PHA_DISPATCH_T(dt, T, {
     if (wdt == kF32) {
       rc = dispatch_nch_small(H, [&](auto nch) {
-        hipLaunchKernelGGL((ln_bwd_kernel<T, float, decltype(nch)::value>), grid, block, 0, stream,
-                           (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, decltype(nch)::value, bwd_waves(decltype(nch)::value)>), grid, dim3(bwd_waves(decltype(nch)::value) * 64), 0, stream,
+                           (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H,
+                           (const T*)dres);
       });
       if (rc) return rc;
       hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (float*)dw, nblocks, H);
       if (db) hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_b, (float*)db, nblocks, H);
     } else {
       rc = dispatch_nch_small(H, [&](auto nch) {
-        hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
-                           (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H);
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value, bwd_waves(decltype(nch)::value)>), grid, dim3(bwd_waves(decltype(nch)::value) * 64), 0, stream,
+                           (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H,
+                           (const T*)dres);
       });
       if (rc) return rc;
       hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (T*)dw, nblocks, H);
@@ -318,6 +357,13 @@ PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, c
     }
   });
   return rc ? rc : (int)hipGetLastError();
+}
+
+PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, const void* w, const float* mean,
+                               const float* rstd, void* dx, void* dw, void* db, float* part_w, float* part_b,
+                               int nblocks, int rows, int H, hipStream_t stream) {
+  return pha_layer_norm_bwd2(dt, wdt, dy, x, w, mean, rstd, nullptr, dx, dw, db, part_w, part_b, nblocks, rows, H,
+                             stream);
 }
 
 PHA_API int pha_softmax_fwd(int dt, const void* x, void* y, int rows, int H, hipStream_t stream) {

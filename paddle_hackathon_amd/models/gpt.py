@@ -131,9 +131,24 @@ class GPTDecoderLayer(nn.Layer):
         return F.dropout(t, self.dropout, training=self.training) if self.dropout and self.training else t
 
     def forward(self, x):
-        x = x + self._drop(self.self_attn(self.norm1(x)))
-        x = x + self._drop(self.mlp(self.norm2(x)))
-        return x
+        h, m = self.forward_fused(x, None)
+        return h + m
+
+    def _add_ln(self, norm, x, delta):
+        if delta is None:
+            return x, norm(x)
+        h, y = _ops.fused.add_layer_norm(x._t, delta._t, norm.weight._t, None if norm.bias is None else norm.bias._t,
+                                         norm._epsilon)
+        return _wrap(h), _wrap(y)
+
+    def forward_fused(self, x, delta):
+        """Residual stream with the adds deferred into the next LayerNorm kernel: the layer
+        input is ``x + delta`` (delta None = already summed); returns (h, m) whose sum is the
+        layer output. Same math as forward(); one pass over the activations fewer per add."""
+        h, a_in = self._add_ln(self.norm1, x, delta)
+        a = self._drop(self.self_attn(a_in))
+        h2, m_in = self._add_ln(self.norm2, h, a)
+        return h2, self._drop(self.mlp(m_in))
 
 
 class GPTEmbeddings(nn.Layer):
@@ -167,13 +182,16 @@ class GPTModel(nn.Layer):
 
     def forward(self, input_ids, position_ids=None):
         x = self.embeddings(input_ids, position_ids)
+        delta = None
         for layer in self.layers:
             if self.cfg.recompute and self.training:
                 from ..parallel.recompute import recompute
-                x = recompute(layer, x)
+                x, delta = recompute(layer.forward_fused, x, delta)
             else:
-                x = layer(x)
-        return self.final_norm(x)
+                x, delta = layer.forward_fused(x, delta)
+        if delta is None:
+            return self.final_norm(x)
+        return self.layers[-1]._add_ln(self.final_norm, x, delta)[1]
 
 
 class GPTForPretraining(nn.Layer):

@@ -119,6 +119,38 @@ def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
                          None if bias is None else bias.reshape(ns), eps)
 
 
+class _AddLayerNorm(torch.autograd.Function):
+    """(x, r) -> (h = x + r, y = LN(h)) in one kernel; backward folds dh into dx."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps):
+        y, mean, rstd, h = _hip.layer_norm_fwd(x, w, b, eps, residual=r)
+        ctx.save_for_backward(h, w, b, mean, rstd)
+        return h, y
+
+    @staticmethod
+    def backward(ctx, gh, gy):
+        h, w, b, mean, rstd = ctx.saved_tensors
+        if gy is None:
+            return gh, gh, None, None, None
+        gx, gw, gb = _hip.layer_norm_bwd(gy.contiguous(), h, w, mean, rstd, b is not None,
+                                         dres=None if gh is None else gh.contiguous())
+        return gx, gx, gw, gb, None
+
+
+def add_layer_norm(x, residual, weight, bias=None, eps=1e-5):
+    """Pre-LN residual step: returns (h, LN(h)) with h = x + residual (one HIP kernel each way)."""
+    H = weight.numel()
+    if (_use_hip(x) and x.is_contiguous() and residual.is_contiguous() and residual.dtype == x.dtype
+            and residual.shape == x.shape and x.dtype in (torch.bfloat16, torch.float32, torch.float16)
+            and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 4096
+            and (bias is None or bias.dtype == weight.dtype)):
+        return _AddLayerNorm.apply(x, residual, weight.reshape(-1), None if bias is None else bias.reshape(-1),
+                                   float(eps))
+    h = x + residual
+    return h, layer_norm(h, [H], weight, bias, eps)
+
+
 def rms_norm(x, weight, eps=1e-6):
     v = x.float().pow(2).mean(-1, keepdim=True)
     y = (x.float() * torch.rsqrt(v + eps)).to(x.dtype)

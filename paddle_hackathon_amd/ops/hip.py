@@ -29,6 +29,9 @@ def _L():
         sig = {
             "pha_layer_norm_fwd": [I, I, P, P, P, P, P, P, I, I, F, P],
             "pha_layer_norm_bwd": [I, I, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+            "pha_layer_norm_bwd_nblocks": [I, I],
+            "pha_layer_norm_fwd2": [I, I, P, P, P, P, P, P, P, P, I, I, F, P],
+            "pha_layer_norm_bwd2": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
             "pha_softmax_bwd": [I, P, P, P, I, I, P],
             "pha_softmax_ce_fwd": [I, P, P, P, P, LG, I, I, P],
@@ -75,28 +78,39 @@ def _check(rc, name):
 # ----------------------------------------------------------------------------
 # layer norm / softmax
 # ----------------------------------------------------------------------------
-def layer_norm_fwd(x, w, b, eps):
+def layer_norm_fwd(x, w, b, eps, residual=None):
+    """y = LN(x) — or, with ``residual``, hs = x + residual and y = LN(hs) in one pass.
+    Returns (y, mean, rstd) or (y, mean, rstd, hs)."""
     H = w.numel()
     rows = x.numel() // H
     assert x.numel() == rows * H and H % 8 == 0 and H <= 4096
     y = torch.empty_like(x)
     mean = torch.empty(rows, dtype=torch.float32, device=x.device)
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-    _check(_L().pha_layer_norm_fwd(_DT[x.dtype], _DT[w.dtype], _ptr(x), _ptr(w.contiguous()), _ptr(None if b is None else b.contiguous()),
-                                   _ptr(y), _ptr(mean), _ptr(rstd), rows, H, float(eps), _stream(x)), "layer_norm_fwd")
-    return y, mean, rstd
+    hs = None
+    if residual is not None:
+        assert residual.shape == x.shape and residual.dtype == x.dtype and residual.is_contiguous()
+        hs = torch.empty_like(x)
+    _check(_L().pha_layer_norm_fwd2(_DT[x.dtype], _DT[w.dtype], _ptr(x), _ptr(residual), _ptr(hs), _ptr(w.contiguous()),
+                                    _ptr(None if b is None else b.contiguous()), _ptr(y), _ptr(mean), _ptr(rstd), rows, H,
+                                    float(eps), _stream(x)), "layer_norm_fwd")
+    return (y, mean, rstd) if residual is None else (y, mean, rstd, hs)
 
 
-def layer_norm_bwd(dy, x, w, mean, rstd, has_bias):
+def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None):
+    """dx = LN'(dy) (+ dres: gradient of a fused residual sum). ``x`` is the normalised input."""
     H = w.numel()
     rows = x.numel() // H
-    nblocks = max(1, min((rows + 3) // 4, 256))   # one block per CU; partials [256, H]
+    nblocks = int(_L().pha_layer_norm_bwd_nblocks(rows, H))  # partials [nblocks, H]
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     db = torch.empty_like(w) if has_bias else None
+    if dres is not None:
+        assert dres.shape == x.shape and dres.dtype == x.dtype and dres.is_contiguous()
     part = torch.empty((2, nblocks, H), dtype=torch.float32, device=x.device)
-    _check(_L().pha_layer_norm_bwd(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd), _ptr(dx),
-                                   _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H, _stream(x)), "layer_norm_bwd")
+    _check(_L().pha_layer_norm_bwd2(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd),
+                                    _ptr(dres), _ptr(dx), _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H,
+                                    _stream(x)), "layer_norm_bwd")
     return dx, dw, db
 
 

@@ -55,6 +55,33 @@ def test_layer_norm_fp32_weight_bf16_input():
     assert torch.allclose(y.float(), ref, atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("H", [768, 2048, 4096])
+@pytest.mark.parametrize("rows", [5, 3000])
+def test_add_layer_norm_fused(H, rows):
+    """(x, r) -> (x + r, LN(x + r)) and its backward (dx = dr = LN'(dy) + dh) vs fp32 autograd,
+    bf16 activations with fp32 LN parameters (the AMP-O2 layout)."""
+    from paddle_hackathon_amd.ops import fused
+    torch.manual_seed(0)
+    x = torch.randn(rows, H, device="cuda").bfloat16().requires_grad_(True)
+    r = torch.randn(rows, H, device="cuda").bfloat16().requires_grad_(True)
+    w = (torch.rand(H, device="cuda") + 0.5).requires_grad_(True)
+    b = torch.randn(H, device="cuda").requires_grad_(True)
+    h, y = fused.add_layer_norm(x, r, w, b, 1e-5)
+    hr = (x.detach() + r.detach()).float().requires_grad_(True)  # the bf16-rounded sum, as unfused
+    xr, wr, br = hr, w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yr = TF.layer_norm(xr, [H], wr, br, 1e-5)
+    assert torch.equal(h, (x + r).detach())
+    assert (y.float() - yr).abs().max().item() < 5e-2
+    dy, dh = torch.randn_like(yr), torch.randn_like(yr)
+    torch.autograd.backward([h, y], [dh.bfloat16(), dy.bfloat16()])
+    torch.autograd.backward([yr], [dy.bfloat16().float()])
+    want = xr.grad + dh.bfloat16().float()
+    assert (x.grad.float() - want).abs().max().item() < 6e-2 * max(1.0, want.abs().max().item() / 8)
+    assert torch.equal(x.grad, r.grad)
+    assert torch.allclose(w.grad, wr.grad, atol=0.5, rtol=2e-2)
+    assert torch.allclose(b.grad, br.grad, atol=0.5, rtol=2e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H", [128, 1024, 2048, 4096])
 def test_softmax(dt, H):
