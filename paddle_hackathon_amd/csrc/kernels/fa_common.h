@@ -1,0 +1,95 @@
+// Shared pieces of the flash-attention kernels (flash_attn.hip: forward + two-kernel backward,
+// flash_attn_bwd.hip: single-kernel backward): MFMA fragment types, the 32x32x16 accumulator
+// row map, the dual-use LDS image (row reads + ds_read_b64_tr_b16 transposed reads) and the
+// per-operand (token, head) strides that let packed [B, S, H, 3D] QKV be read in place.
+#pragma once
+#include "common.h"
+
+using namespace pha;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <typename T> struct MF;
+template <> struct MF<bf16_t> {
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
+    // plain conversions: hipcc lowers the pair to one v_cvt_pk_bf16_f32 (RNE) on gfx950
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+};
+template <> struct MF<half_t> {
+  typedef f16x8 frag;
+  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
+    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+    const f16x2 v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+};
+
+template <typename F>
+__device__ __forceinline__ F as_frag(u32x4 v) { return __builtin_bit_cast(F, v); }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// row of the 32x32 accumulator held in register r by lane-half h
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+struct FaStrides {
+  long q_tok, kv_tok, o_tok, dq_tok, dkv_tok;
+  int q_head, kv_head, o_head, dq_head, dkv_head;
+};
+
+__device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR
+  return row * 256 + 16 * (chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x2 ds_read_tr16(const unsigned char* lds_ptr) {
+  const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(lds_ptr));
+  return __builtin_bit_cast(u32x2, r);
+}
+
+__device__ __forceinline__ int dual_off(int row, int chunk) { return v_lds_off(row, chunk); }
+
+// 8 elements of a transposed operand: rows r0+{0..3} and r0+8+{0..3} of a dual image, the
+// lane's 32-column block (column block cb = 32-wide d block index)
+__device__ __forceinline__ u32x4 tr_frag(const unsigned char* img, int r0, int db, int g, int tq, int tp) {
+  const int chunk = 4 * db + 2 * (g & 1) + (tp >> 1);
+  const u32x2 lo = ds_read_tr16(img + dual_off(r0 + tq, chunk) + 8 * (tp & 1));
+  const u32x2 hi = ds_read_tr16(img + dual_off(r0 + 8 + tq, chunk) + 8 * (tp & 1));
+  return u32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+FaStrides dense_strides(int H, int Hk, int D) {
+  FaStrides f;
+  f.q_tok = f.o_tok = f.dq_tok = f.dkv_tok = (long)H * D;
+  f.kv_tok = (long)Hk * D;
+  f.q_head = f.kv_head = f.o_head = f.dq_head = f.dkv_head = D;
+  return f;
+}
+
+}  // namespace

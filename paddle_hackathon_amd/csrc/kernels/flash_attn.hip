@@ -18,59 +18,13 @@
 //
 // Backward: a key-parallel dK/dV kernel and a query-parallel dQ kernel (see below) — no
 // atomics and no cross-workgroup reduction; both prefetch their next tile into registers.
-#include "common.h"
+#include "fa_common.h"
 #include <cstdlib>
 
 using namespace pha;
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
-typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
-
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
-
-template <typename T> struct MF;
-template <> struct MF<bf16_t> {
-  typedef bf16x8 frag;
-  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
-    // plain conversions: hipcc lowers the pair to one v_cvt_pk_bf16_f32 (RNE) on gfx950
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-    const bf16x2 v = {(__bf16)lo, (__bf16)hi};
-    return __builtin_bit_cast(uint32_t, v);
-  }
-};
-template <> struct MF<half_t> {
-  typedef f16x8 frag;
-  static __device__ __forceinline__ f32x16 mma(frag a, frag b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
-  static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
-    typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
-    const f16x2 v = {(_Float16)lo, (_Float16)hi};
-    return __builtin_bit_cast(uint32_t, v);
-  }
-};
-
-template <typename F>
-__device__ __forceinline__ F as_frag(u32x4 v) { return __builtin_bit_cast(F, v); }
-
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-// row of the 32x32 accumulator held in register r by lane-half h
-__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 constexpr int BM = 128;   // query rows per workgroup (4 waves x 32)
 constexpr int BN = 64;    // keys per tile
@@ -305,22 +259,6 @@ constexpr int NT2 = 512;
 
 // element strides (token, head) of each operand, so packed [B, S, H, 3D] QKV projections and
 // their packed gradient are read/written in place (no split copies, no concat of dq/dk/dv)
-struct FaStrides {
-  long q_tok, kv_tok, o_tok, dq_tok, dkv_tok;
-  int q_head, kv_head, o_head, dq_head, dkv_head;
-};
-
-__device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR
-  return row * 256 + 16 * (chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-}
-
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ u32x2 ds_read_tr16(const unsigned char* lds_ptr) {
-  const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) v4i16*)(lds_ptr));
-  return __builtin_bit_cast(u32x2, r);
-}
 
 template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q, const T* __restrict__ K,
@@ -334,8 +272,8 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int nqb = (S + BM2 - 1) / BM2;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int head = blockIdx.y, b = blockIdx.z;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.y) : (int)blockIdx.y;
+  const int head = blockIdx.x % H, b = blockIdx.x / H;   // (b, h) fastest: every pair's heaviest block first
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
   const int q = q0 + wid * 32 + lr;
@@ -891,16 +829,6 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
 //  fa_bwd_dq_v2: 256 queries per workgroup (query on the lane, Q/dO fragments in registers);
 //    64-key tiles:  S^T = K Q^T, dP^T = V dO^T (row reads), dQ^T += K^T dS^T (tr reads of K).
 // ============================================================================================
-__device__ __forceinline__ int dual_off(int row, int chunk) { return v_lds_off(row, chunk); }
-
-// 8 elements of a transposed operand: rows r0+{0..3} and r0+8+{0..3} of a dual image, the
-// lane's 32-column block (column block cb = 32-wide d block index)
-__device__ __forceinline__ u32x4 tr_frag(const unsigned char* img, int r0, int db, int g, int tq, int tp) {
-  const int chunk = 4 * db + 2 * (g & 1) + (tp >> 1);
-  const u32x2 lo = ds_read_tr16(img + dual_off(r0 + tq, chunk) + 8 * (tp & 1));
-  const u32x2 hi = ds_read_tr16(img + dual_off(r0 + 8 + tq, chunk) + 8 * (tp & 1));
-  return u32x4{lo[0], lo[1], hi[0], hi[1]};
-}
 
 // 4 waves (128 keys) with one wave per SIMD: the per-wave state (K/V fragments 64 regs, dK^T/dV^T
 // 128, S/dP 32, staging 32) exceeds the 256-register share two waves per SIMD would leave.
@@ -920,9 +848,9 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
-  const int head = blockIdx.y, b = blockIdx.z;
+  const int head = blockIdx.x % H, b = blockIdx.x / H;
   const int hk = head / (H / Hk);
-  const int k0 = blockIdx.x * (NTKV / 2);
+  const int k0 = blockIdx.y * (NTKV / 2);
   const int wk0 = k0 + wid * 32;
   const int key = wk0 + lr;
   const long kstride = fs.kv_tok;
@@ -1074,8 +1002,8 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nqb = (S + BM2 - 1) / BM2;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int head = blockIdx.y, b = blockIdx.z;
+  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.y) : (int)blockIdx.y;
+  const int head = blockIdx.x % H, b = blockIdx.x / H;
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
   const int wq0 = q0 + wid * 32;
@@ -1211,13 +1139,6 @@ bool fwd_v2_enabled() {  // PHA_FA_FWD_V1=1 selects the 4-wave kernel (A/B compa
   return !(e && e[0] == '1');
 }
 
-FaStrides dense_strides(int H, int Hk, int D) {
-  FaStrides f;
-  f.q_tok = f.o_tok = f.dq_tok = f.dkv_tok = (long)H * D;
-  f.kv_tok = (long)Hk * D;
-  f.q_head = f.kv_head = f.o_head = f.dq_head = f.dkv_head = D;
-  return f;
-}
 
 template <typename T>
 int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk, int H, int Hk,
@@ -1226,7 +1147,7 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
   const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   if (fsp && !(D == 128 && fwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && fwd_v2_enabled()) {
-    const dim3 g2((S + BM2 - 1) / BM2, H, B), b2(NT2);
+    const dim3 g2(B * H, (S + BM2 - 1) / BM2), b2(NT2);
     if (causal)
       hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
     else
@@ -1249,7 +1170,7 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
   const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   if (fsp && !(D == 128 && bwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && bwd_v2_enabled()) {
-    const dim3 gk2((Sk + NTKV / 2 - 1) / (NTKV / 2), H, B), gq2((S + BM2 - 1) / BM2, H, B), b2(NT2), bk(NTKV);
+    const dim3 gk2(B * H, (Sk + NTKV / 2 - 1) / (NTKV / 2)), gq2(B * H, (S + BM2 - 1) / BM2), b2(NT2), bk(NTKV);
 #define FB2(CC)                                                                                                    \
     if (dkdv_ilp2())                                                                                               \
       hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, true>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,    \
@@ -1275,6 +1196,7 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
 #undef FB_L
   return (int)hipGetLastError();
 }
+
 
 }  // namespace
 

@@ -43,6 +43,15 @@ def _run(cmd):
     return r.stdout
 
 
+def _file_flags(src):
+    """Per-source extra compiler flags from a ``// pha-build-flags: ...`` line in its header."""
+    with open(src) as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// pha-build-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def build_kernels(force=False, verbose=True):
     os.makedirs(BUILD, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
@@ -58,7 +67,7 @@ def build_kernels(force=False, verbose=True):
     def compile_one(src):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         if force or _newer([src] + hdrs, obj):
-            _run([hipcc, "-c", src, "-o", obj] + flags)
+            _run([hipcc, "-c", src, "-o", obj] + flags + _file_flags(src))
         return obj
 
     jobs = int(os.environ.get("MAX_JOBS", "8"))

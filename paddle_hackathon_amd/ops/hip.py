@@ -395,6 +395,16 @@ def flash_attn_supported(q, k, v, dropout_p):
     return True
 
 
+def _bwd_fused(D):
+    """Single-kernel backward (dK, dV and atomically summed dQ) when PHA_FA_BWD=fused; the default
+    is the two-kernel v2 backward, measured faster at the GPT shape (0.95 vs 1.14 ms, B8 S2048
+    H16 D128 causal: the fused kernel's one wave per SIMD exposes its LDS latency)."""
+    import os
+    if D != 128 or os.environ.get("PHA_FA_BWD", "v2") != "fused" or os.environ.get("PHA_FA_BWD_V1") == "1":
+        return False
+    return hasattr(_lib.lib, "pha_flash_attn_bwd_fused")
+
+
 class FlashAttention(torch.autograd.Function):
     """Forward/backward on our MFMA flash-attention kernels. Layout [B, S, H, D]."""
 
@@ -427,9 +437,18 @@ class FlashAttention(torch.autograd.Function):
         dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S), c_int(H), c_int(D),
                                                _stream(q)), "flash_attn_bwd_preprocess")
-        _check(L.pha_flash_attn_bwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq),
-                                    _ptr(dk), _ptr(dv), c_int(B), c_int(S), c_int(Sk), c_int(H), c_int(Hk), c_int(D),
-                                    c_float(ctx.scale), c_int(int(ctx.causal)), _stream(q)), "flash_attn_bwd")
+        if _bwd_fused(D):
+            # single-kernel backward; dQ is summed over key blocks in an fp32 workspace
+            acc = torch.empty((B, S, H, D), dtype=torch.float32, device=q.device)
+            L.pha_flash_attn_bwd_fused.restype = c_int
+            _check(L.pha_flash_attn_bwd_fused(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse),
+                                              _ptr(delta), _ptr(dq), _ptr(dk), _ptr(dv), _ptr(acc), c_int(B), c_int(S),
+                                              c_int(Sk), c_int(H), c_int(Hk), c_int(D), c_float(ctx.scale),
+                                              c_int(int(ctx.causal)), _stream(q)), "flash_attn_bwd_fused")
+        else:
+            _check(L.pha_flash_attn_bwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta), _ptr(dq),
+                                        _ptr(dk), _ptr(dv), c_int(B), c_int(S), c_int(Sk), c_int(H), c_int(Hk), c_int(D),
+                                        c_float(ctx.scale), c_int(int(ctx.causal)), _stream(q)), "flash_attn_bwd")
         if Hk != H:
             g = H // Hk
             dk = dk.view(B, Sk, Hk, g, D).sum(3)
@@ -482,7 +501,15 @@ class FlashAttentionPacked(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[qkv.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B),
                                                c_int(S), c_int(H), c_int(D), _stream(qkv)), "flash_attn_bwd_preprocess")
-        _check(L.pha_flash_attn_bwd_packed(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(do), _ptr(lse), _ptr(delta),
-                                           _ptr(dqkv), c_int(B), c_int(S), c_int(H), c_int(D), c_float(ctx.scale),
-                                           c_int(int(ctx.causal)), _stream(qkv)), "flash_attn_bwd_packed")
+        if _bwd_fused(D):
+            acc = torch.empty((B, S, H, D), dtype=torch.float32, device=qkv.device)
+            L.pha_flash_attn_bwd_packed_fused.restype = c_int
+            _check(L.pha_flash_attn_bwd_packed_fused(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(do), _ptr(lse),
+                                                     _ptr(delta), _ptr(dqkv), _ptr(acc), c_int(B), c_int(S), c_int(H),
+                                                     c_int(D), c_float(ctx.scale), c_int(int(ctx.causal)),
+                                                     _stream(qkv)), "flash_attn_bwd_packed_fused")
+        else:
+            _check(L.pha_flash_attn_bwd_packed(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(do), _ptr(lse), _ptr(delta),
+                                               _ptr(dqkv), c_int(B), c_int(S), c_int(H), c_int(D), c_float(ctx.scale),
+                                               c_int(int(ctx.causal)), _stream(qkv)), "flash_attn_bwd_packed")
         return dqkv, None, None

@@ -231,6 +231,30 @@ def test_flash_attention_fwd_bwd(dt, D, causal, S):
         assert err < 3e-2 * max(1.0, scale), (name, err, scale)
 
 
+@pytest.mark.parametrize("mode", ["v2", "fused"])
+@pytest.mark.parametrize("causal,S,Sk", [(True, 300, 300), (True, 1024, 1024), (False, 200, 520)])
+def test_flash_attention_bwd_paths_gqa(mode, causal, S, Sk, monkeypatch):
+    """Both D=128 backward paths (two-kernel v2, single-kernel with atomic fp32 dQ) against fp32,
+    with GQA (8 query heads on 2 kv heads), ragged lengths and cross attention."""
+    from paddle_hackathon_amd.ops import hip
+    monkeypatch.setenv("PHA_FA_BWD", mode)
+    torch.manual_seed(1)
+    B, H, Hk, D = 2, 8, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_(True)
+    k = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16().requires_grad_(True)
+    v = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16().requires_grad_(True)
+    o = hip.FlashAttention.apply(q, k, v, causal, None)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qr, kr, vr, causal)
+    g = torch.randn_like(ref)
+    o.backward(g.bfloat16())
+    ref.backward(g)
+    for got, want, name in ((q.grad, qr.grad, "dq"), (k.grad, kr.grad, "dk"), (v.grad, vr.grad, "dv")):
+        err = (got.float() - want).abs().max().item()
+        scale = want.abs().max().item()
+        assert err < 3e-2 * max(1.0, scale), (mode, name, err, scale)
+
+
 def test_flash_attention_gqa():
     from paddle_hackathon_amd.ops import hip
     torch.manual_seed(0)

@@ -47,14 +47,21 @@ def main():
     o = hip.FlashAttention.apply(qg, kg, vg, causal, None)
     do = torch.randn_like(o)
     grads = {}
-    for name, env in (("v1", "1"), ("v2", "0")):
-        os.environ["PHA_FA_BWD_V1"] = env
+    for name, v1, mode in (("v1", "1", "v2"), ("v2", "0", "v2"), ("fused", "0", "fused")):
+        os.environ["PHA_FA_BWD_V1"] = v1
+        os.environ["PHA_FA_BWD"] = mode
         grads[name] = torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True)
         t = timeit(lambda: torch.autograd.grad(o, (qg, kg, vg), do, retain_graph=True), 5)
         print(f"bwd {name}: {t * 1e3:.3f} ms  {2.5 * fl / t / 1e12:.1f} TF", flush=True)
-    for n, a, b in zip("qkv", grads["v1"], grads["v2"]):
-        print(f"  d{n} v1 vs v2 max diff {(a.float() - b.float()).abs().max().item():.4f} "
-              f"(scale {a.float().abs().max().item():.3f})", flush=True)
+    # fp32 reference gradients
+    qr, kr, vr = (x.detach().transpose(1, 2).float().requires_grad_(True) for x in (q, k, v))
+    orf = TF.scaled_dot_product_attention(qr, kr, vr, is_causal=causal)
+    gref = torch.autograd.grad(orf, (qr, kr, vr), do.transpose(1, 2).float())
+    gref = [x.transpose(1, 2) for x in gref]
+    for name in ("v2", "fused"):
+        for n, a, r in zip("qkv", grads[name], gref):
+            print(f"  {name} d{n} max err vs fp32 {(a.float() - r).abs().max().item():.4f} "
+                  f"(scale {r.abs().max().item():.3f})", flush=True)
     qs, ks, vs = (x.transpose(1, 2).clone().requires_grad_(True) for x in (q, k, v))
     os_ = TF.scaled_dot_product_attention(qs, ks, vs, is_causal=causal)
     dos = do.transpose(1, 2)

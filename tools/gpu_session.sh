@@ -56,6 +56,14 @@ for s in "$@"; do
     tests_k)
       timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 240 -k "${TESTK}" > $OUT/pytest_k.log 2>&1; rc=$?
       tail -15 $OUT/pytest_k.log ;;
+    prof_fa)
+      # per-kernel times + PMC passes for the flash-attention backward (PHA_FA_BWD selects the path)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_fa; mkdir -p $OUT/prof_fa
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/prof_fa/trace -o run --output-format csv -- python3 $ROOT/tools/fa_prof.py > $OUT/prof_fa/trace.log 2>&1; rc=$?
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_fa/pmc1 -o run --output-format csv -- python3 $ROOT/tools/fa_prof.py > $OUT/prof_fa/pmc1.log 2>&1; rc=$?; fi
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_fa/pmc2 -o run --output-format csv -- python3 $ROOT/tools/fa_prof.py > $OUT/prof_fa/pmc2.log 2>&1; rc=$?; fi
+      tail -3 $OUT/prof_fa/*.log ;;
     tests_fa)
       timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 120 -k "flash" > $OUT/pytest_fa.log 2>&1; rc=$?
       tail -5 $OUT/pytest_fa.log ;;
