@@ -10,6 +10,7 @@ try:  # optional subsystems (filled in progressively)
     from . import fleet  # noqa: F401
     from .mp_layers import split  # noqa: F401
     from .sharding import group_sharded_parallel, save_group_sharded_model  # noqa: F401
+    from . import ps  # noqa: F401
 except ImportError:  # pragma: no cover
     pass
 

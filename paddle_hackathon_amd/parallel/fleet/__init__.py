@@ -2,10 +2,13 @@
 meta_parallel/{tensor_parallel,pipeline_parallel,sharding_parallel}.py,
 meta_optimizers/dygraph_optimizer/hybrid_parallel_optimizer.py).
 
-Collective mode only (the parameter-server mode is out of scope for the GPU build;
-see SURVEY.md §2.7). ``fleet.init`` builds the dp×pp×sharding×mp topology,
-``distributed_model`` picks the wrapper, ``distributed_optimizer`` returns a
-HybridParallelOptimizer (TP/PP-aware global-norm clip, sharding stage-1).
+Collective mode: ``fleet.init`` builds the dp×pp×sharding×mp topology, ``distributed_model``
+picks the wrapper, ``distributed_optimizer`` returns a HybridParallelOptimizer (TP/PP-aware
+global-norm clip, sharding stage-1). Parameter-server mode (``is_collective=False`` with the
+reference's TRAINING_ROLE / PADDLE_PSERVERS_IP_PORT_LIST environment or a UserDefinedRoleMaker):
+``init_server``/``run_server`` host the native tables (``parallel/ps``), trainers
+``init_worker``, train with ``DistributedEmbedding`` + ``distributed_optimizer`` (PSOptimizer:
+sync / async / geo by ``strategy.a_sync`` and ``a_sync_configs["k_steps"]``) and ``stop_worker``.
 """
 from __future__ import annotations
 
@@ -69,12 +72,22 @@ class Fleet:
         self._role_maker = None
         self._is_collective = True
         self._topology = None
+        self._ps = None
         self.util = UtilBase()
 
     def init(self, role_maker=None, is_collective=False, strategy=None, log_level="INFO"):
         self._role_maker = role_maker
-        self._is_collective = True
         self._strategy = strategy if strategy is not None else DistributedStrategy()
+        rm = role_maker if role_maker is not None else PaddleCloudRoleMaker(is_collective=is_collective)
+        if not is_collective and rm._is_ps_mode():
+            from .. import ps
+            self._is_collective = False
+            self._role_maker = rm
+            self._ps = ps.TheOnePSRuntime(rm, self._strategy)
+            ps.set_runtime(self._ps)
+            return self
+        self._is_collective = True
+        self._ps = None
         if not C.is_initialized() and int(os.environ.get("WORLD_SIZE", os.environ.get("PADDLE_TRAINERS_NUM", "1"))) > 1:
             C.init_parallel_env()
         ws = C.get_world_size()
@@ -95,14 +108,17 @@ class Fleet:
         return self
 
     # -- role info --------------------------------------------------------------------
+    def _ps_mode(self):
+        return getattr(self, "_ps", None) is not None
+
     def worker_index(self):
-        return C.get_rank()
+        return self._role_maker._worker_index() if self._ps_mode() else C.get_rank()
 
     def worker_num(self):
-        return C.get_world_size()
+        return self._role_maker._worker_num() if self._ps_mode() else C.get_world_size()
 
     def is_first_worker(self):
-        return C.get_rank() == 0
+        return self.is_worker() and self.worker_index() == 0
 
     def worker_endpoints(self, to_string=False):
         eps = os.environ.get("PADDLE_TRAINER_ENDPOINTS", "")
@@ -110,34 +126,58 @@ class Fleet:
         return ",".join(lst) if to_string else lst
 
     def server_num(self):
-        return 0
+        return self._role_maker._server_num() if self._ps_mode() else 0
+
+    def server_index(self):
+        return self._role_maker._server_index() if self._ps_mode() else 0
+
+    def server_endpoints(self, to_string=False):
+        lst = self._role_maker._get_pserver_endpoints() if self._ps_mode() else []
+        return ",".join(lst) if to_string else lst
 
     def is_worker(self):
-        return True
+        return self._role_maker._is_worker() if self._ps_mode() else True
 
     def is_server(self):
-        return False
+        return self._role_maker._is_server() if self._ps_mode() else False
 
     def barrier_worker(self):
-        C.barrier()
+        if self._ps_mode():
+            self._ps.barrier_worker()
+        else:
+            C.barrier()
 
-    def init_worker(self):
-        pass
+    def init_worker(self, scopes=None):
+        if self._ps_mode():
+            self._ps.init_worker(scopes)
 
     def init_server(self, *args, **kwargs):
-        pass
+        if self._ps_mode():
+            self._ps.init_server(*args, **kwargs)
 
     def run_server(self):
-        raise RuntimeError("parameter-server mode is not supported by the MI355X collective build")
+        if not self._ps_mode():
+            raise RuntimeError("run_server() needs parameter-server mode (fleet.init(is_collective=False) with "
+                               "TRAINING_ROLE=PSERVER and PADDLE_PSERVERS_IP_PORT_LIST)")
+        self._ps.run_server()
 
     def stop_worker(self):
-        pass
+        if self._ps_mode():
+            self._ps.stop_worker()
+
+    def shrink(self, threshold=None):
+        """Drop sparse rows unseen for ``threshold`` shrink passes (parameter-server mode)."""
+        if self._ps_mode() and self._ps.client is not None:
+            for t in sorted(self._ps.client._sparse):
+                self._ps.client.shrink(t, int(threshold or 0))
 
     def get_hybrid_communicate_group(self):
         return self._hcg
 
     # -- wrappers -------------------------------------------------------------------------
     def distributed_model(self, model):
+        if self._ps_mode():
+            return model   # dense sync happens in the PS optimizer, sparse tables in DistributedEmbedding
         hcg, st = self._hcg, self._strategy
         if hcg is None:
             self.init(is_collective=True)
@@ -158,6 +198,10 @@ class Fleet:
     def distributed_optimizer(self, optimizer, strategy=None):
         if strategy is not None:
             self._strategy = strategy
+        if self._ps_mode():
+            from ..ps import PSOptimizer
+            self._ps.strategy = self._strategy
+            return PSOptimizer(optimizer, self._ps, self._strategy)
         if self._hcg is None:
             self.init(is_collective=True)
         return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
@@ -167,7 +211,18 @@ class Fleet:
 
     # -- persistence ------------------------------------------------------------------------
     def save_persistables(self, executor=None, dirname=None, main_program=None, mode=0):
-        pass
+        """Parameter-server mode: every table of the job (dense and sparse) into ``dirname``,
+        one file per table per server (mode 0 with optimizer state, 1 weights only)."""
+        if self._ps_mode() and self._ps.client is not None and dirname:
+            c = self._ps.client
+            for t in sorted(set(c._dense) | set(c._sparse)):
+                c.save(t, dirname, mode)
+
+    def load_persistables(self, dirname):
+        if self._ps_mode() and self._ps.client is not None:
+            c = self._ps.client
+            for t in sorted(set(c._dense) | set(c._sparse)):
+                c.load(t, dirname)
 
     def save_inference_model(self, *args, **kwargs):
         from ...static import save_inference_model
@@ -256,6 +311,10 @@ init_server = fleet.init_server
 run_server = fleet.run_server
 stop_worker = fleet.stop_worker
 save_persistables = fleet.save_persistables
+load_persistables = fleet.load_persistables
+shrink = fleet.shrink
+server_index = fleet.server_index
+server_endpoints = fleet.server_endpoints
 save_inference_model = fleet.save_inference_model
 util = fleet.util
 

@@ -112,9 +112,16 @@ def launch(argv=None):
     ap.add_argument("--master_port", "--master-port", type=int, default=None)
     ap.add_argument("--log_dir", "--log-dir", type=str, default=None)
     ap.add_argument("--heartbeat-timeout", type=float, default=0.0)
+    # parameter-server mode (reference: launch --server_num/--servers/--worker_num/--workers)
+    ap.add_argument("--server_num", "--server-num", type=int, default=0)
+    ap.add_argument("--servers", type=str, default="")
+    ap.add_argument("--worker_num", "--worker-num", type=int, default=0)
+    ap.add_argument("--workers", type=str, default="")
     ap.add_argument("script")
     ap.add_argument("script_args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
+    if a.server_num or a.servers:
+        return _launch_ps(a)
     n = a.nproc_per_node or (len(a.gpus.split(",")) if a.gpus else 1)
     port = a.master_port or _free_port()
     procs = []
@@ -169,6 +176,66 @@ def launch(argv=None):
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
         rc = rc or 1
+    return rc
+
+
+def _launch_ps(a):
+    """Parameter-server job on this node: server processes (TRAINING_ROLE=PSERVER) and trainer
+    processes (TRAINING_ROLE=TRAINER) with the reference's PADDLE_* environment. Any failing
+    trainer ends the job; once every trainer has exited the servers get 30 s to stop."""
+    servers = [e for e in a.servers.split(",") if e] or [f"127.0.0.1:{_free_port()}" for _ in range(a.server_num)]
+    nw = a.worker_num or len([w for w in a.workers.split(",") if w]) or a.nproc_per_node or 1
+    base = dict(os.environ)
+    base.update({"PADDLE_PSERVERS_IP_PORT_LIST": ",".join(servers), "PADDLE_TRAINERS_NUM": str(nw)})
+    log = (lambda name: open(os.path.join(a.log_dir, name), "w")) if a.log_dir else (lambda name: None)
+    if a.log_dir:
+        os.makedirs(a.log_dir, exist_ok=True)
+
+    def start(env, name):
+        out = log(name)
+        return subprocess.Popen([sys.executable, a.script] + a.script_args, env=env, stdout=out,
+                                stderr=subprocess.STDOUT if out else None, start_new_session=True)
+
+    srv, trn = [], []
+    for i, ep in enumerate(servers):
+        host, port = ep.rsplit(":", 1)
+        env = dict(base, TRAINING_ROLE="PSERVER", POD_IP=host, PADDLE_PORT=port)
+        srv.append(start(env, f"serverlog.{i}"))
+    for r in range(nw):
+        env = dict(base, TRAINING_ROLE="TRAINER", PADDLE_TRAINER_ID=str(r), POD_IP="127.0.0.1",
+                   PADDLE_PORT=str(_free_port()))
+        trn.append(start(env, f"workerlog.{r}"))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in trn):
+            for r, p in enumerate(trn):
+                c = p.poll()
+                if c not in (None, 0):
+                    print(f"[launch] trainer {r} exited with {c}; terminating job", file=sys.stderr)
+                    rc = c
+                    raise KeyboardInterrupt
+            for i, p in enumerate(srv):
+                if p.poll() not in (None, 0):
+                    print(f"[launch] server {i} exited with {p.returncode}; terminating job", file=sys.stderr)
+                    rc = p.returncode
+                    raise KeyboardInterrupt
+            time.sleep(0.2)
+        deadline = time.time() + 30
+        while any(p.poll() is None for p in srv) and time.time() < deadline:
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        rc = rc or 1
+    for p in srv + trn:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    for p in srv + trn:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
     return rc
 
 

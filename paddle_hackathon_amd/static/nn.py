@@ -67,7 +67,15 @@ def embedding(input, size, is_sparse=False, is_distributed=False, padding_idx=No
     return F.embedding(input, w, padding_idx)
 
 
-sparse_embedding = embedding
+def sparse_embedding(input, size, padding_idx=None, is_test=False, entry=None, table_class="MemorySparseTable",
+                     param_attr=None, dtype="float32", slot=None):
+    """Parameter-server mode (fleet.init with a PS role maker + init_worker): rows live in a
+    server sparse table (parallel/ps DistributedEmbedding); otherwise a local embedding."""
+    from ..parallel import ps
+    if ps._runtime is not None and ps._runtime.client is not None:
+        return ps.sparse_embedding(input, size, padding_idx=padding_idx, is_test=is_test, entry=entry,
+                                   param_attr=param_attr)
+    return embedding(input, size, padding_idx=padding_idx, param_attr=param_attr, dtype=dtype)
 
 
 def _conv(fn, transpose, input, num_filters, filter_size, stride, padding, dilation, groups, param_attr, bias_attr,
