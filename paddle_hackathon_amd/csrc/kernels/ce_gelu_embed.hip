@@ -146,6 +146,38 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
   }
 }
 
+// bias-GELU backward that also forms the bias gradient: thread = one 8-column chunk, block row
+// y = a contiguous range of rows; the column sums of gx over that range go to part[y][H] (fp32),
+// so db needs no second pass over gx (reference: fused_gemm_epilogue / fused_feedforward's
+// bias grad reduction).
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_db_kernel(const T* __restrict__ gy, const T* __restrict__ x,
+                                                               const T* __restrict__ b, T* __restrict__ gx,
+                                                               float* __restrict__ part, int rows, int H,
+                                                               int rows_per_block, bool approx) {
+  const int c8 = blockIdx.x * 256 + threadIdx.x;   // chunk of 8 columns
+  if (c8 * 8 >= H) return;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  float bv[8], acc[8];
+  Vec8<T>::ld(b + c8 * 8, bv);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll 4
+  for (int r = r0; r < r1; ++r) {
+    const long off = (long)r * H + c8 * 8;
+    float v[8], g[8], o[8];
+    Vec8<T>::ld(x + off, v);
+    Vec8<T>::ld(gy + off, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = g[k] * gelu_grad(v[k] + bv[k], approx);
+      acc[k] += round_to<T>(o[k]);   // the bias gradient of the stored (rounded) gx
+    }
+    Vec8<T>::st(gx + off, o);
+  }
+  Vec8<float>::st(part + (long)blockIdx.y * H + c8 * 8, acc);
+}
+
 // one wave per output row; row bytes multiple of 16
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const uint4* __restrict__ w,
                                                             uint4* __restrict__ out, long rows, int row_vecs, long vocab) {
@@ -203,6 +235,18 @@ PHA_API int pha_bias_gelu_bwd(int dt, const void* gy, const void* x, const void*
   const long n8 = n / 8;
   PHA_DISPATCH_T(dt, T, {
     hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(grid_for(n8, 256)), dim3(256), 0, stream, (const T*)gy, (const T*)x, (const T*)b, (T*)gx, n8, H, approx != 0);
+  });
+  return (int)hipGetLastError();
+}
+
+// part: [ceil(rows / rows_per_block), H] fp32 workspace; db = part.sum(0) (done by the caller)
+PHA_API int pha_bias_gelu_bwd_db(int dt, const void* gy, const void* x, const void* b, void* gx, float* part, int rows,
+                                 int H, int rows_per_block, int approx, hipStream_t stream) {
+  if (H % 8 || rows <= 0 || rows_per_block <= 0 || !b) return (int)hipErrorInvalidValue;
+  const dim3 grid((H / 8 + 255) / 256, (rows + rows_per_block - 1) / rows_per_block);
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((bias_gelu_bwd_db_kernel<T>), grid, dim3(256), 0, stream, (const T*)gy, (const T*)x,
+                       (const T*)b, (T*)gx, part, rows, H, rows_per_block, approx != 0);
   });
   return (int)hipGetLastError();
 }

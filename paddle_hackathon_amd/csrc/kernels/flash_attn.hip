@@ -447,20 +447,24 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 template <typename T, int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const T* __restrict__ O, const T* __restrict__ dO,
                                                          float* __restrict__ delta, int B, int S, int H) {
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over (b, q, head)
+  // D/8 lanes per (b, q, head) row, 8 elements each: every lane of the wave loads (a whole wave
+  // per 128-element row would leave 3/4 of the lanes idle)
+  constexpr int LPR = D / 8, RPW = 64 / LPR;
   const int lane = threadIdx.x & 63;
-  if (row >= (long)B * S * H) return;
-  const long off = row * D;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool ok = row < (long)B * S * H;
   float s = 0.f;
-  for (int c = lane * 8; c < D; c += 512) {
+  if (ok) {
+    const long off = row * D + (lane % LPR) * 8;
     float a[8], g[8];
-    Vec8<T>::ld(O + off + c, a);
-    Vec8<T>::ld(dO + off + c, g);
+    Vec8<T>::ld(O + off, a);
+    Vec8<T>::ld(dO + off, g);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += a[i] * g[i];
   }
-  s = wave_sum(s);
-  if (lane == 0) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (ok && lane % LPR == 0) {
     const int head = row % H;
     const long bq = row / H;
     const int q = bq % S;
@@ -1211,7 +1215,8 @@ PHA_API int pha_flash_attn_fwd(int dt, const void* q, const void* k, const void*
 PHA_API int pha_flash_attn_bwd_preprocess(int dt, const void* o, const void* dout, float* delta, int B, int S, int H,
                                           int D, hipStream_t stream) {
   const long rows = (long)B * S * H;
-  const dim3 grid((rows + 3) / 4), block(256);
+  const int rpb = 4 * (64 / (D / 8));   // rows per 256-thread block
+  const dim3 grid((rows + rpb - 1) / rpb), block(256);
   if (dt == kBF16) {
     if (D == 128) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 128>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
     else hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 64>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);

@@ -169,6 +169,25 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
 
 // sum partials [P, H] over P -> out [H] (cast to W). 64 columns per block (one per lane, so
 // every row read is a coalesced 256-B segment), the 4 waves split the P rows.
+// first stage of the [P, H] column sum: grid (H/64, kColSplit) so the whole chip streams the
+// partials (one 64-column stripe per block would leave 224 of 256 CUs idle at H = 2048)
+constexpr int kColSplit = 8;
+__global__ __launch_bounds__(256) void col_partial_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                          int P, int H) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int chunk = (P + kColSplit - 1) / kColSplit;
+  const int p0 = blockIdx.y * chunk, p1 = min(P, p0 + chunk);
+  float s = 0.f;
+  if (col < H)
+#pragma unroll 4
+    for (int p = p0 + w; p < p1; p += 4) s += part[(long)p * H + col];
+  __shared__ float red[4][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < H) out[(long)blockIdx.y * H + col] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
 template <typename W>
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, W* __restrict__ out, int P, int H) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -327,7 +346,21 @@ PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, co
   return pha_layer_norm_fwd2(dt, wdt, x, nullptr, nullptr, w, b, y, mean, rstd, rows, H, eps, stream);
 }
 
-// part_w / part_b: workspace [nblocks, H] fp32 each (nblocks = pha_layer_norm_bwd_nblocks);
+// column sums of the [P, H] partials into out: P > 4 * kColSplit rows go through the chip-wide first
+// stage into rows [P, P + kColSplit) of the same workspace
+template <typename W>
+void col_sum(float* part, W* out, int P, int H, hipStream_t stream) {
+  if (P > 4 * kColSplit) {
+    float* stage = part + (long)P * H;
+    hipLaunchKernelGGL(col_partial_kernel, dim3((H + 63) / 64, kColSplit), dim3(256), 0, stream, part, stage, P, H);
+    hipLaunchKernelGGL((col_reduce_kernel<W>), dim3((H + 63) / 64), dim3(256), 0, stream, stage, out, kColSplit, H);
+  } else {
+    hipLaunchKernelGGL((col_reduce_kernel<W>), dim3((H + 63) / 64), dim3(256), 0, stream, part, out, P, H);
+  }
+}
+
+// part_w / part_b: workspace [nblocks + 8, H] fp32 each (nblocks = pha_layer_norm_bwd_nblocks;
+// the last 8 rows are the column-sum stage);
 // dw/db outputs (may be null db); dres (optional): gradient of the fused residual sum, added to dx.
 PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, const void* w, const float* mean,
                                 const float* rstd, const void* dres, void* dx, void* dw, void* db, float* part_w,
@@ -343,8 +376,8 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
                            (const T*)dres);
       });
       if (rc) return rc;
-      hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (float*)dw, nblocks, H);
-      if (db) hipLaunchKernelGGL((col_reduce_kernel<float>), dim3((H + 63) / 64), dim3(256), 0, stream, part_b, (float*)db, nblocks, H);
+      col_sum<float>(part_w, (float*)dw, nblocks, H, stream);
+      if (db) col_sum<float>(part_b, (float*)db, nblocks, H, stream);
     } else {
       rc = dispatch_nch_small(H, [&](auto nch) {
         hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value, bwd_waves(decltype(nch)::value)>), grid, dim3(bwd_waves(decltype(nch)::value) * 64), 0, stream,
@@ -352,8 +385,8 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
                            (const T*)dres);
       });
       if (rc) return rc;
-      hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, stream, part_w, (T*)dw, nblocks, H);
-      if (db) hipLaunchKernelGGL((col_reduce_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, stream, part_b, (T*)db, nblocks, H);
+      col_sum<T>(part_w, (T*)dw, nblocks, H, stream);
+      if (db) col_sum<T>(part_b, (T*)db, nblocks, H, stream);
     }
   });
   return rc ? rc : (int)hipGetLastError();

@@ -107,7 +107,7 @@ def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None):
     db = torch.empty_like(w) if has_bias else None
     if dres is not None:
         assert dres.shape == x.shape and dres.dtype == x.dtype and dres.is_contiguous()
-    part = torch.empty((2, nblocks, H), dtype=torch.float32, device=x.device)
+    part = torch.empty((2, nblocks + 8, H), dtype=torch.float32, device=x.device)  # + column-sum stage rows
     _check(_L().pha_layer_norm_bwd2(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd),
                                     _ptr(dres), _ptr(dx), _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H,
                                     _stream(x)), "layer_norm_bwd")
@@ -229,6 +229,17 @@ def bias_gelu_bwd(gy, x, b, approximate):
             y = TF.gelu(xx, approximate="tanh" if approximate else "none")
             (gx,) = torch.autograd.grad(y, xx, gy.float())
         gx = gx.to(x.dtype)
+    elif b is not None and x.dtype != torch.float32 and hasattr(_L(), "pha_bias_gelu_bwd_db"):
+        # gx and the per-row-block column sums of gx in one pass; db = sum of the partials
+        gx = torch.empty_like(x)
+        rows = n // H
+        rpb = max(16, -(-rows // 512))   # >= 2048 blocks at 16384 x 8192: 8 per CU for streaming
+        part = torch.empty((-(-rows // rpb), H), dtype=torch.float32, device=x.device)
+        L = _L()
+        L.pha_bias_gelu_bwd_db.restype = c_int
+        _check(L.pha_bias_gelu_bwd_db(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), _ptr(part), c_int(rows),
+                                      c_int(H), c_int(rpb), c_int(int(approximate)), _stream(x)), "bias_gelu_bwd_db")
+        return gx, part.sum(0).to(b.dtype)
     else:
         gx = torch.empty_like(x)
         _check(_L().pha_bias_gelu_bwd(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), n, H, int(approximate), _stream(x)), "bias_gelu_bwd")
