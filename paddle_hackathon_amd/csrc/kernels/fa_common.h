@@ -59,6 +59,7 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 struct FaStrides {
   long q_tok, kv_tok, o_tok, dq_tok, dkv_tok;
   int q_head, kv_head, o_head, dq_head, dkv_head;
+  int order_g;   // key/query blocks of one (b, h) kept together on an XCD (see fa_block)
 };
 
 __device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR
@@ -86,10 +87,30 @@ __device__ __forceinline__ u32x4 tr_frag(const unsigned char* img, int r0, int d
 
 FaStrides dense_strides(int H, int Hk, int D) {
   FaStrides f;
+  f.order_g = 0;
   f.q_tok = f.o_tok = f.dq_tok = f.dkv_tok = (long)H * D;
   f.kv_tok = (long)Hk * D;
   f.q_head = f.kv_head = f.o_head = f.dq_head = f.dkv_head = D;
   return f;
+}
+
+// Workgroup id -> ((b, h) index, block rank), block rank 0 = the heaviest causal block.
+// Workgroups are dispatched round-robin over the 8 XCDs (CDNA guide T1), so XCD x runs the ids
+// x, x+8, ...: give each XCD its own (b, h) pairs (bh = x mod 8), walk them heaviest block group
+// first (longest-processing-time order, no tail of long workgroups), and keep the G blocks of a
+// group of one pair consecutive on that XCD so they stream the same Q/dO or K/V tiles through its
+// L2. Falls back to plain (b, h)-fastest order when the shape does not split evenly.
+__device__ __forceinline__ void fa_block(int BH, int nblk, int G, int& bh, int& blk) {
+  const int id = blockIdx.x + gridDim.x * blockIdx.y;
+  if (G <= 0 || BH % 8 || nblk % G) {
+    bh = id % BH;
+    blk = id / BH;
+    return;
+  }
+  const int xcd = id & 7, slot = id >> 3, nbx = BH >> 3;
+  const int grp = slot / (nbx * G), rem = slot - grp * (nbx * G);
+  bh = (rem / G) * 8 + xcd;
+  blk = grp * G + rem % G;
 }
 
 }  // namespace

@@ -272,8 +272,10 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int nqb = (S + BM2 - 1) / BM2;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.y) : (int)blockIdx.y;
-  const int head = blockIdx.x % H, b = blockIdx.x / H;   // (b, h) fastest: every pair's heaviest block first
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / nqb, nqb, fs.order_g, bh, rank);
+  const int qb = CAUSAL ? (nqb - 1 - rank) : rank;
+  const int head = bh % H, b = bh / H;
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
   const int q = q0 + wid * 32 + lr;
@@ -852,9 +854,11 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
-  const int head = blockIdx.x % H, b = blockIdx.x / H;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / ((Sk + NTKV / 2 - 1) / (NTKV / 2)), (Sk + NTKV / 2 - 1) / (NTKV / 2), fs.order_g, bh, rank);
+  const int head = bh % H, b = bh / H;
   const int hk = head / (H / Hk);
-  const int k0 = blockIdx.y * (NTKV / 2);
+  const int k0 = rank * (NTKV / 2);
   const int wk0 = k0 + wid * 32;
   const int key = wk0 + lr;
   const long kstride = fs.kv_tok;
@@ -1006,8 +1010,10 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, lr = lane & 31;
   const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
   const int nqb = (S + BM2 - 1) / BM2;
-  const int qb = CAUSAL ? (nqb - 1 - (int)blockIdx.y) : (int)blockIdx.y;
-  const int head = blockIdx.x % H, b = blockIdx.x / H;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / nqb, nqb, fs.order_g, bh, rank);
+  const int qb = CAUSAL ? (nqb - 1 - rank) : rank;
+  const int head = bh % H, b = bh / H;
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
   const int wq0 = q0 + wid * 32;
@@ -1138,6 +1144,11 @@ bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comp
   return !(e && e[0] == '1');
 }
 
+int fa_order_g() {  // PHA_FA_ORDER_G: blocks of one (b, h) kept together per XCD (0 = plain order)
+  const char* e = getenv("PHA_FA_ORDER_G");
+  return e ? atoi(e) : 0;   // measured: G = 0 fastest (0.923 ms bwd; G = 4: 1.036 ms)
+}
+
 bool fwd_v2_enabled() {  // PHA_FA_FWD_V1=1 selects the 4-wave kernel (A/B comparisons)
   const char* e = getenv("PHA_FA_FWD_V1");
   return !(e && e[0] == '1');
@@ -1148,7 +1159,8 @@ template <typename T>
 int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk, int H, int Hk,
                int D, float scale, int causal, hipStream_t st, const FaStrides* fsp = nullptr) {
   const float sl = scale * kLog2e;
-  const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  fs.order_g = fa_order_g();
   if (fsp && !(D == 128 && fwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && fwd_v2_enabled()) {
     const dim3 g2(B * H, (S + BM2 - 1) / BM2), b2(NT2);
@@ -1171,7 +1183,8 @@ template <typename T>
 int launch_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
                void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
                hipStream_t st, const FaStrides* fsp = nullptr) {
-  const FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
+  fs.order_g = fa_order_g();
   if (fsp && !(D == 128 && bwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && bwd_v2_enabled()) {
     const dim3 gk2(B * H, (Sk + NTKV / 2 - 1) / (NTKV / 2)), gq2(B * H, (S + BM2 - 1) / BM2), b2(NT2), bk(NTKV);
@@ -1246,6 +1259,7 @@ PHA_API int pha_flash_attn_fwd_packed(int dt, const void* qkv, void* o, float* l
                                       float scale, int causal, hipStream_t stream) {
   if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
   FaStrides f;
+  f.order_g = 0;
   f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
   f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
   f.o_tok = (long)H * D;
@@ -1264,6 +1278,7 @@ PHA_API int pha_flash_attn_bwd_packed(int dt, const void* qkv, const void* dout,
                                       hipStream_t stream) {
   if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
   FaStrides f;
+  f.order_g = 0;
   f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
   f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
   f.o_tok = (long)H * D;

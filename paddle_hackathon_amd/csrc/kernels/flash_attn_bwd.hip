@@ -322,6 +322,7 @@ PHA_API int pha_flash_attn_bwd_packed_fused(int dt, const void* qkv, const void*
                                             float scale, int causal, hipStream_t stream) {
   if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
   FaStrides f;
+  f.order_g = 0;
   f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
   f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
   f.o_tok = (long)H * D;

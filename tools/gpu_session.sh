@@ -64,6 +64,9 @@ for s in "$@"; do
       if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_fa/pmc1 -o run --output-format csv -- python3 $ROOT/tools/fa_prof.py > $OUT/prof_fa/pmc1.log 2>&1; rc=$?; fi
       if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_fa/pmc2 -o run --output-format csv -- python3 $ROOT/tools/fa_prof.py > $OUT/prof_fa/pmc2.log 2>&1; rc=$?; fi
       tail -3 $OUT/prof_fa/*.log ;;
+    fa_order)
+      for g in 0 1 2 4 8; do echo "--- PHA_FA_ORDER_G=$g"; PHA_FA_ORDER_G=$g PHA_FA_BENCH_FAST=1 timeout -k 10 120 python tools/bench_fa.py 2>&1 | grep -E "v2|fused"; rc=$?; done > $OUT/fa_order.log 2>&1
+      cat $OUT/fa_order.log ;;
     tests_fa)
       timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 120 -k "flash" > $OUT/pytest_fa.log 2>&1; rc=$?
       tail -5 $OUT/pytest_fa.log ;;
