@@ -24,10 +24,15 @@ from . import hip as _hip
 _native = None
 
 
+def _is_dtensor(t):
+    from torch.distributed.tensor import DTensor
+    return isinstance(t, DTensor)
+
+
 def _use_hip(t: torch.Tensor) -> bool:
     global _native
-    if not t.is_cuda:
-        return False
+    if not t.is_cuda or type(t) is not torch.Tensor and _is_dtensor(t):
+        return False   # distributed tensors run on torch ops (sharding propagation), not raw pointers
     if _native is None:
         _native = _lib.require_native()
     return _native
