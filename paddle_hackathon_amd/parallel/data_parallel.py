@@ -74,6 +74,7 @@ class _Reducer:
         for g in sorted(groups):
             self._add(groups[g], groups[g][0]._t.dtype)
         self.handles = []
+        self.comm_dtype = None   # e.g. bf16: fp32 buckets all-reduced in 16 bit (strategy.fp16_allreduce)
         self._callback_queued = False
         for p in self.params:
             self.handles.append(p._t.register_post_accumulate_grad_hook(self._make_hook(p)))
@@ -104,9 +105,13 @@ class _Reducer:
     def _launch(self, b):
         grads = [p._t.grad for p in b.params]
         n = sum(g.numel() for g in grads)
-        if b.buf is None or b.buf.numel() != n or b.buf.device != grads[0].device:
-            b.buf = torch.empty(n, dtype=b.dtype, device=grads[0].device)
-        torch.cat([g.reshape(-1) for g in grads], out=b.buf)
+        cdt = self.comm_dtype if self.comm_dtype is not None and b.dtype == torch.float32 else b.dtype
+        if b.buf is None or b.buf.numel() != n or b.buf.device != grads[0].device or b.buf.dtype != cdt:
+            b.buf = torch.empty(n, dtype=cdt, device=grads[0].device)
+        if cdt == b.dtype:
+            torch.cat([g.reshape(-1) for g in grads], out=b.buf)
+        else:
+            b.buf.copy_(torch.cat([g.reshape(-1) for g in grads]))
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         b.work = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
 
@@ -136,6 +141,8 @@ class _Reducer:
             for g in grads:
                 views.append(b.buf[off:off + g.numel()].view_as(g))
                 off += g.numel()
+            if views and views[0].dtype != grads[0].dtype:
+                views = [v.to(grads[0].dtype) for v in views]
             torch._foreach_copy_(grads, views)
 
     def remove(self):

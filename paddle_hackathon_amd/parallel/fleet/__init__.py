@@ -73,7 +73,10 @@ class Fleet:
         self._is_collective = True
         self._topology = None
         self._ps = None
+        self._dp_model = None
         self.util = UtilBase()
+        from . import meta_optimizers as _mo
+        _mo._dp_model_hook[0] = lambda: self._dp_model
 
     def init(self, role_maker=None, is_collective=False, strategy=None, log_level="INFO"):
         self._role_maker = role_maker
@@ -190,9 +193,13 @@ class Fleet:
         if mode == ParallelMode.SHARDING_PARALLEL:
             return ShardingParallel(model, hcg, st)
         if C.get_world_size() > 1:
-            return DataParallel(model, comm_buffer_size=st.fuse_grad_size_in_MB,
-                                last_comm_buffer_size=st.last_comm_group_size_MB,
-                                find_unused_parameters=st.find_unused_parameters, group=hcg.get_data_parallel_group())
+            self._dp_model = DataParallel(model, comm_buffer_size=st.fuse_grad_size_in_MB,
+                                          last_comm_buffer_size=st.last_comm_group_size_MB,
+                                          find_unused_parameters=st.find_unused_parameters,
+                                          group=hcg.get_data_parallel_group())
+            if st.fp16_allreduce and self._dp_model._reducer is not None:
+                self._dp_model._reducer.comm_dtype = torch.bfloat16
+            return self._dp_model
         return model
 
     def distributed_optimizer(self, optimizer, strategy=None):
@@ -204,7 +211,11 @@ class Fleet:
             return PSOptimizer(optimizer, self._ps, self._strategy)
         if self._hcg is None:
             self.init(is_collective=True)
-        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+        from . import meta_optimizers as mo
+        optimizer = mo.apply_meta_optimizers(optimizer, self._strategy, self._dp_model)
+        hp = HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+        dp_g = self._hcg.get_data_parallel_group() if self._hcg is not None else None
+        return mo.wrap_meta_optimizers(hp, self._strategy, self._dp_model, group=dp_g if dp_g is not None and dp_g.nranks > 1 else None)
 
     def distributed_scaler(self, scaler):
         return scaler

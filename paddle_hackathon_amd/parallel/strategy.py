@@ -34,6 +34,7 @@ _DEFAULTS = {
     "localsgd": False,
     "localsgd_configs": {"k_steps": 1, "begin_step": 1},
     "adaptive_localsgd": False,
+    "adaptive_localsgd_configs": {"init_k_steps": 1, "begin_step": 1},
     "fp16_allreduce": False,
     "fuse_all_reduce_ops": True,
     "fuse_grad_size_in_MB": 64,
