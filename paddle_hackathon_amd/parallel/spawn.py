@@ -117,11 +117,23 @@ def launch(argv=None):
     ap.add_argument("--servers", type=str, default="")
     ap.add_argument("--worker_num", "--worker-num", type=int, default=0)
     ap.add_argument("--workers", type=str, default="")
+    # elastic / fault-tolerant mode (reference: launch --elastic_server --job_id --np)
+    ap.add_argument("--elastic_server", "--elastic-server", type=str, default=None)
+    ap.add_argument("--host_store", action="store_true")
+    ap.add_argument("--job_id", "--job-id", type=str, default="default")
+    ap.add_argument("--np", type=str, default=None)
+    ap.add_argument("--max_restart", "--max-restart", type=int, default=3)
     ap.add_argument("script")
     ap.add_argument("script_args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     if a.server_num or a.servers:
         return _launch_ps(a)
+    if a.elastic_server:
+        from .elastic import launch_elastic
+        a.nproc_per_node = a.nproc_per_node or 1
+        a.np = a.np or "1"
+        a.heartbeat_timeout = a.heartbeat_timeout or 10.0
+        return launch_elastic(a)
     n = a.nproc_per_node or (len(a.gpus.split(",")) if a.gpus else 1)
     port = a.master_port or _free_port()
     procs = []
