@@ -24,7 +24,6 @@ from ..topology import CommunicateTopology, HybridCommunicateGroup, ParallelMode
 from .. import mp_layers, pipeline
 from ..data_parallel import DataParallel, sync_params_buffers
 from . import meta_parallel, utils  # noqa: F401
-from .. import elastic  # noqa: F401  (fleet.elastic)
 from .role_maker import PaddleCloudRoleMaker, UserDefinedRoleMaker, Role  # noqa: F401
 
 __all__ = ["CommunicateTopology", "DistributedStrategy", "Fleet", "HybridCommunicateGroup", "MultiSlotDataGenerator",
@@ -369,3 +368,10 @@ class MultiSlotDataGenerator:
 
 class MultiSlotStringDataGenerator(MultiSlotDataGenerator):
     pass
+
+
+def __getattr__(name):   # fleet.elastic, imported lazily (it is also a `python -m` entry point)
+    if name == "elastic":
+        from .. import elastic
+        return elastic
+    raise AttributeError(name)
