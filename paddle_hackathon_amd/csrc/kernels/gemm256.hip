@@ -1,0 +1,307 @@
+// Large-tile MFMA GEMM / implicit-GEMM convolution for gfx950 (reference behaviour:
+// phi/kernels/gpu/matmul_kernel.cu and conv_kernel.cu — cuBLAS / cuDNN there).
+//
+//   C[M, N] (row-major, ldc) = sum_k A[m, k] * Bt[n, k]  (+ bias[n]) (relu | gelu)
+//
+//   A: K-contiguous rows (lda) — or, A_CONV, the NHWC implicit im2col of x: row m = output pixel,
+//      k = (kh, kw, cin) with cin fastest (Cin % 8 == 0, so a 16-B chunk never straddles taps)
+//   Bt: K-contiguous rows of B^T (ldb) — a [Cout][KH][KW][Cin] filter for convolution
+//
+// Structure (CDNA guide §5 "glds vs register staging", "Pipelining across barriers"):
+//  * 256 x BN x 64 block tile (BN = 64 | 128 | 256), 512 threads = 8 waves laid out
+//    (8 / (BN/64)) x (BN/64), each wave a (256 / WM) x 64 sub-tile of 16x16 accumulators
+//    (v_mfma_f32_16x16x32_bf16: the shape the chip clocks highest on random data).
+//  * A and Bt tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write):
+//    the LDS image is lane-linear per wave-instruction, so the XOR swizzle (16-B chunk ^= row & 7,
+//    conflict-free ds_read_b128 fragment reads) is applied to each lane's SOURCE address and the
+//    same involution on the read. The conv gather is just a per-lane source address (a zero page
+//    stands in for padding taps and out-of-range rows).
+//  * Two LDS stages; tile k+1 is issued before tile k is multiplied and retired by a COUNTED
+//    s_waitcnt vmcnt (never 0 in the loop) ahead of a raw s_barrier — __syncthreads() would drain
+//    the prefetch too.
+#include "common.h"
+#include <type_traits>
+
+namespace pha {
+namespace g256 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BK = 64, NT = 512;
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+struct ConvGeo {
+  int N, H, W, C;   // input NHWC
+  int OH, OW;
+  int KH, KW;
+  int sh, sw, ph, pw, dh, dw;
+};
+
+struct Args {
+  const void* a;
+  const void* b;
+  void* c;
+  const float* bias;
+  long M, N, K;
+  long lda, ldb, ldc;
+  int act;
+  const void* zero;   // >= 16 B of zeros
+  ConvGeo g;
+};
+
+template <typename T> struct Mf;
+template <> struct Mf<bf16_t> {
+  static __device__ __forceinline__ f32x4 mma(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+  static __device__ __forceinline__ uint16_t cvt(float v) {
+    return __builtin_bit_cast(uint16_t, (__bf16)v);
+  }
+};
+template <> struct Mf<half_t> {
+  static __device__ __forceinline__ f32x4 mma(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+  static __device__ __forceinline__ uint16_t cvt(float v) {
+    return __builtin_bit_cast(uint16_t, (_Float16)v);
+  }
+};
+
+// byte offset in a [rows][64] bf16 image (128-B rows, 16-B chunks swizzled by row & 7)
+__device__ __forceinline__ int img_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// per-lane row state of the A gather for one of the wave's A instructions
+struct ARow {
+  const char* base;   // row base (plain) or image pixel base (conv: n, oh*sh-ph, ow*sw-pw folded)
+  int ih0, iw0;       // conv: top-left input coordinate of the row's receptive field
+  bool ok;
+};
+
+template <typename T, int BN, bool CONV>
+__global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
+  constexpr int WN = BN / 64, WM = 8 / WN;          // wave grid
+  constexpr int WTM = BM / WM;                       // wave tile rows (32 | 64 | 128)
+  constexpr int RB = WTM / 16, CB = 4;               // 16x16 blocks per wave
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INS = A_BYTES / (NT * 16), B_INS = B_BYTES / (NT * 16);   // glds per thread per stage
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform (glds M0 base)
+  const int wm = wid / WN, wn = wid % WN;
+  const long M = p.M, N = p.N, K = p.K;
+
+  // XCD-aware tile order (CDNA guide T1): the 8 XCDs take contiguous runs of tiles, walked in
+  // GROUP_M-row panels so consecutive tiles of an XCD share their A or B panel in its L2
+  const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+  const int ntiles = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int q = ntiles / 8, r = ntiles % 8, xcd = bid % 8;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  constexpr int GROUP_M = 8;
+  const int group = tile / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (tile % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (tile % (GROUP_M * tiles_n)) / gsize;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+
+  const T* A = static_cast<const T*>(p.a);
+  const T* Bt = static_cast<const T*>(p.b);
+  const char* zero = static_cast<const char*>(p.zero);
+
+  // ---- per-lane source rows of this thread's glds instructions ------------------------------
+  // wave-instruction j of wave w fills image bytes [(j*8 + w) * 1024, +1024) = 8 rows; lane l
+  // takes row (j*8 + w)*8 + l/8 and LDS chunk l&7, i.e. source chunk (l&7) ^ (row&7)
+  const int lrow = lane >> 3, lch = lane & 7;
+  ARow ar[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (j * 8 + wid) * 8 + lrow;
+    const long m = m0 + row;
+    ar[j].ok = m < M;
+    if constexpr (CONV) {
+      const ConvGeo& g = p.g;
+      const long mm = ar[j].ok ? m : 0;
+      const int hw = g.OH * g.OW;
+      const int n = (int)(mm / hw);
+      const int rem = (int)(mm - (long)n * hw);
+      const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
+      ar[j].ih0 = oh * g.sh - g.ph;
+      ar[j].iw0 = ow * g.sw - g.pw;
+      ar[j].base = reinterpret_cast<const char*>(A + (long)n * g.H * g.W * g.C);
+    } else {
+      ar[j].base = reinterpret_cast<const char*>(A + (ar[j].ok ? m : 0) * p.lda);
+      ar[j].ih0 = ar[j].iw0 = 0;
+    }
+  }
+  const char* brow[B_INS];
+  bool bok[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (j * 8 + wid) * 8 + lrow;
+    const long n = n0 + row;
+    bok[j] = n < N;
+    brow[j] = reinterpret_cast<const char*>(Bt + (bok[j] ? n : 0) * p.ldb);
+  }
+  const int src_ch = lch;   // LDS chunk of this lane; source chunk = lch ^ (row & 7) = lch ^ lrow
+  const int sch = src_ch ^ lrow;
+
+  auto issue = [&](int stage, long k0) {
+    unsigned char* sa = smem + stage * STAGE;
+    unsigned char* sb = sa + A_BYTES;
+    const long k = k0 + sch * 8;
+    const bool kok = k < K;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const char* src = zero;
+      if (ar[j].ok && kok) {
+        if constexpr (CONV) {
+          const ConvGeo& g = p.g;
+          const int tap = (int)(k / g.C), cin = (int)(k - (long)tap * g.C);
+          const int kh = tap / g.KW, kw = tap - kh * g.KW;
+          const int ih = ar[j].ih0 + kh * g.dh, iw = ar[j].iw0 + kw * g.dw;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            src = ar[j].base + (((long)ih * g.W + iw) * g.C + cin) * sizeof(T);
+        } else {
+          src = ar[j].base + k * sizeof(T);
+        }
+      }
+      glds16(src, sa + (j * 8 + wid) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const char* src = (bok[j] && kok) ? brow[j] + k * sizeof(T) : zero;
+      glds16(src, sb + (j * 8 + wid) * 1024);
+    }
+  };
+
+  f32x4 acc[RB][CB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((K + BK - 1) / BK);
+  issue(0, 0);
+  const int fr = lane & 15, fk = lane >> 4;   // fragment row / k-chunk of this lane
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    // tile kt's loads are the only ones in flight: retire them, then one barrier both publishes
+    // every wave's share of stage `cur` and certifies that stage cur^1 (read in iteration kt-1)
+    // is free, so tile kt+1 streams into it while tile kt is multiplied
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(cur ^ 1, (long)(kt + 1) * BK);
+    const unsigned char* sa = smem + cur * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      uint4 bf[CB];
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
+        bf[j] = *reinterpret_cast<const uint4*>(sb + img_off(wn * 64 + j * 16 + fr, kh * 4 + fk));
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const uint4 af = *reinterpret_cast<const uint4*>(sa + img_off(wm * WTM + i * 16 + fr, kh * 4 + fk));
+#pragma unroll
+        for (int j = 0; j < CB; ++j) acc[i][j] = Mf<T>::mma(af, bf[j], acc[i][j]);
+      }
+    }
+  }
+  __builtin_amdgcn_s_barrier();   // all fragment reads done: the LDS is reused for the C tile
+
+  // ---- epilogue: bias / activation, C tile staged through LDS so every lane stores 16 B --------
+  // acc[i][j] register e = C[row 4*(lane>>4) + e][col lane&15] of 16x16 block (i, j)
+  constexpr int CROW = BN * 2 + 16;                   // padded LDS row (bytes) of the C tile
+  static_assert(BM * CROW <= 2 * STAGE, "C tile must fit the staging LDS");
+  unsigned char* ct = smem;
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    const int nl = wn * 64 + j * 16 + fr;
+    const float bv = (p.bias && n0 + nl < N) ? p.bias[n0 + nl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[i][j][e] + bv;
+        if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
+        else if (p.act == ACT_GELU) v = gelu_tanh(v);
+        const int ml = wm * WTM + i * 16 + 4 * fk + e;
+        *reinterpret_cast<uint16_t*>(ct + ml * CROW + nl * 2) = Mf<T>::cvt(v);
+      }
+  }
+  __syncthreads();
+  T* C = static_cast<T*>(p.c);
+  constexpr int CH = BN / 8;                          // 16-B chunks per C row
+  const bool full_n = n0 + BN <= N && (p.ldc % 8) == 0;
+  for (int idx = tid; idx < BM * CH; idx += NT) {
+    const int ml = idx / CH, c8 = idx % CH;
+    const long m = m0 + ml, n = n0 + c8 * 8;
+    if (m >= M) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(ct + ml * CROW + c8 * 16);
+    if (full_n) {
+      *reinterpret_cast<uint4*>(C + m * p.ldc + n) = v;
+    } else {
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+      for (int t = 0; t < 8 && n + t < N; ++t) reinterpret_cast<uint16_t*>(C)[m * p.ldc + n + t] = e[t];
+    }
+  }
+}
+
+template <typename T, bool CONV>
+int launch(const Args& a, hipStream_t st) {
+  const long tiles_m = (a.M + BM - 1) / BM;
+  auto go = [&](auto bn) {
+    constexpr int BN = decltype(bn)::value;
+    const long tiles = tiles_m * ((a.N + BN - 1) / BN);
+    hipLaunchKernelGGL((gemm256_kernel<T, BN, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+  };
+  if (a.N <= 64) go(std::integral_constant<int, 64>());
+  else if (a.N <= 128) go(std::integral_constant<int, 128>());
+  else go(std::integral_constant<int, 256>());
+  return (int)hipGetLastError();
+}
+
+}  // namespace g256
+}  // namespace pha
+
+using namespace pha;
+
+// C[M,N] = A[M,K] . Bt[N,K]^T (+bias)(act); A, Bt K-contiguous, K % 8 == 0, 16-B aligned rows.
+PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const float* bias, long M, long N, long K,
+                           long lda, long ldb, long ldc, int act, const void* zero16, hipStream_t stream) {
+  if (K % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}};
+  if (dt == kBF16) return g256::launch<bf16_t, false>(p, stream);
+  if (dt == kF16) return g256::launch<half_t, false>(p, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+// NHWC conv forward: y[N*OH*OW, Cout] = im2col(x) . w^T, w as [Cout][KH][KW][Cin], Cin % 8 == 0.
+PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H, int W,
+                            int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
+                            const void* zero16, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
+                  KH, KW, sh, sw, ph, pw, dh, dw};
+  const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
+  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g};
+  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream);
+  if (dt == kF16) return g256::launch<half_t, true>(p, stream);
+  return (int)hipErrorInvalidValue;
+}

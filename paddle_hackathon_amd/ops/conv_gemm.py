@@ -210,3 +210,62 @@ class Conv2dNHWC(torch.autograd.Function):
 
 def conv2d_nhwc(x, weight, bias, stride, padding, dilation):
     return Conv2dNHWC.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))
+
+
+# ----------------------------------------------------------------------------------------------
+# 256-row-tile kernels (csrc/kernels/gemm256.hip): glds-staged, 8 waves, 16x16x32 MFMA
+# ----------------------------------------------------------------------------------------------
+_ACT = {None: 0, "relu": 1, "gelu": 2}
+
+
+def _L256():
+    L = _L()
+    if not getattr(L, "_g256_sig", False):
+        P, I, LG = c_void_p, c_int, c_long
+        L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, P]
+        L.pha_gemm256_nt.restype = c_int
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, P]
+        L.pha_conv256_fwd.restype = c_int
+        L._g256_sig = True
+    return L
+
+
+def gemm256_nt(a, bt, bias=None, act=None, out=None):
+    """C[M, N] = a[M, K] @ bt[N, K]^T (+ bias fp32[N]) (+ relu/gelu). K-contiguous operands."""
+    assert a.dtype in _DT and bt.dtype == a.dtype and a.dim() == 2 and bt.dim() == 2 and a.shape[1] == bt.shape[1]
+    assert a.stride(1) == 1 and bt.stride(1) == 1 and a.shape[1] % 8 == 0 and a.stride(0) % 8 == 0 and bt.stride(0) % 8 == 0
+    M, K = a.shape
+    N = bt.shape[0]
+    c = out if out is not None else torch.empty((M, N), dtype=a.dtype, device=a.device)
+    assert c.shape == (M, N) and c.stride(1) == 1
+    if bias is not None:
+        bias = bias.float().contiguous()
+        assert bias.numel() == N
+    rc = _L256().pha_gemm256_nt(_DT[a.dtype], _ptr(a), _ptr(bt), _ptr(c), _ptr(bias), M, N, K, a.stride(0),
+                                bt.stride(0), c.stride(0), _ACT[act], _ptr(_zero_page(a.device)),
+                                c_void_p(torch.cuda.current_stream(a.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm256_nt failed ({rc})")
+    return c
+
+
+def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None):
+    """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout]."""
+    assert x.dtype in _DT and w_okkc.dtype == x.dtype and x.is_contiguous() and w_okkc.is_contiguous()
+    N, H, W, C = x.shape
+    Co, KH, KW, Cw = w_okkc.shape
+    assert C == Cw and C % 8 == 0
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+    y = torch.empty((N, OH, OW, Co), dtype=x.dtype, device=x.device)
+    if bias is not None:
+        bias = bias.float().contiguous()
+    rc = _L256().pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
+                                 sh, sw, ph, pw, dh, dw, _ACT[act], _ptr(_zero_page(x.device)),
+                                 c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
+    return y

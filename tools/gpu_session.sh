@@ -23,6 +23,12 @@ for s in "$@"; do
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
+    bench_resnet_hip)
+      PHA_CONV_IMPL=hip timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet_hip.log 2>&1; rc=$?
+      tail -3 $OUT/bench_resnet_hip.log ;;
+    bench_g256)
+      timeout -k 10 300 python tools/bench_gemm256.py > $OUT/bench_g256.log 2>&1; rc=$?
+      cat $OUT/bench_g256.log | tail -20 ;;
     prof)
       export TMPDIR=/tmp
       rm -rf $OUT/prof
