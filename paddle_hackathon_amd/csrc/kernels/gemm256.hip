@@ -20,6 +20,7 @@
 //    s_waitcnt vmcnt (never 0 in the loop) ahead of a raw s_barrier — __syncthreads() would drain
 //    the prefetch too.
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace pha {
@@ -29,7 +30,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 256, BK = 64, NT = 512;
+constexpr int BM = 256, NT = 512;
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
@@ -72,8 +73,14 @@ template <> struct Mf<half_t> {
   }
 };
 
-// byte offset in a [rows][64] bf16 image (128-B rows, 16-B chunks swizzled by row & 7)
-__device__ __forceinline__ int img_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// byte offset in a [rows][BK] bf16 image. BK = 64: 128-B rows, 16-B chunk ^= row & 7; BK = 32:
+// 64-B rows, chunk ^= (row >> 2) & 3 — either way the 16 rows of a fragment read cover all 16
+// chunk slots of a 256-B bank row (SQ_LDS_BANK_CONFLICT = 0 measured)
+template <int BK>
+__device__ __forceinline__ int img_off(int row, int chunk) {
+  if constexpr (BK == 64) return row * 128 + ((chunk ^ (row & 7)) << 4);
+  else return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
 
 __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -91,14 +98,20 @@ struct ARow {
   bool ok;
 };
 
-template <typename T, int BN, bool CONV>
+template <typename T, int BN, int BK, bool CONV>
 __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
+  constexpr int NSTAGE = BK == 64 ? 2 : 4;   // BK 64: one tile in flight; BK 32: three
   constexpr int WN = BN / 64, WM = 8 / WN;          // wave grid
   constexpr int WTM = BM / WM;                       // wave tile rows (32 | 64 | 128)
   constexpr int RB = WTM / 16, CB = 4;               // 16x16 blocks per wave
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INS = A_BYTES / (NT * 16), B_INS = B_BYTES / (NT * 16);   // glds per thread per stage
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+  constexpr int A_INS = A_BYTES / (NT * 16);                  // glds per thread per stage (2)
+  constexpr int B_WI = B_BYTES / 1024;                        // B wave-instructions per stage (4 | 8 | 16)
+  constexpr int B_INS = (B_WI + 7) / 8;                       // per thread (waves beyond B_WI repeat one)
+  constexpr int INS = A_INS + B_INS;
+  constexpr int CROW = BN * 2 + 16;                   // padded LDS row (bytes) of the staged C tile
+  constexpr int SMEM = NSTAGE * STAGE > BM * CROW ? NSTAGE * STAGE : BM * CROW;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // provably wave-uniform (glds M0 base)
@@ -125,13 +138,14 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   const char* zero = static_cast<const char*>(p.zero);
 
   // ---- per-lane source rows of this thread's glds instructions ------------------------------
-  // wave-instruction j of wave w fills image bytes [(j*8 + w) * 1024, +1024) = 8 rows; lane l
-  // takes row (j*8 + w)*8 + l/8 and LDS chunk l&7, i.e. source chunk (l&7) ^ (row&7)
-  const int lrow = lane >> 3, lch = lane & 7;
+  // wave-instruction i fills image bytes [i * 1024, +1024) = RPI rows of 2*BK bytes; lane l takes
+  // row i*RPI + l/CPR and LDS chunk l%CPR; its SOURCE chunk is the swizzle of that (involution)
+  constexpr int CPR = BK / 8, RPI = 64 / CPR;      // 16-B chunks per row, rows per wave-instruction
+  const int lrow = lane / CPR, lch = lane % CPR;
   ARow ar[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
-    const int row = (j * 8 + wid) * 8 + lrow;
+    const int row = (j * 8 + wid) * RPI + lrow;
     const long m = m0 + row;
     ar[j].ok = m < M;
     if constexpr (CONV) {
@@ -153,13 +167,13 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   bool bok[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
-    const int row = (j * 8 + wid) * 8 + lrow;
+    const int row = ((j * 8 + wid) % B_WI) * RPI + lrow;
     const long n = n0 + row;
     bok[j] = n < N;
     brow[j] = reinterpret_cast<const char*>(Bt + (bok[j] ? n : 0) * p.ldb);
   }
-  const int src_ch = lch;   // LDS chunk of this lane; source chunk = lch ^ (row & 7) = lch ^ lrow
-  const int sch = src_ch ^ lrow;
+  // source chunk: row % RPI == lrow for every instruction, so the swizzle is per lane constant
+  const int sch = BK == 64 ? (lch ^ (lrow & 7)) : (lch ^ ((lrow >> 2) & 3));
 
   auto issue = [&](int stage, long k0) {
     unsigned char* sa = smem + stage * STAGE;
@@ -186,7 +200,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
       const char* src = (bok[j] && kok) ? brow[j] + k * sizeof(T) : zero;
-      glds16(src, sb + (j * 8 + wid) * 1024);
+      glds16(src, sb + ((j * 8 + wid) % B_WI) * 1024);   // duplicate waves rewrite identical bytes
     }
   };
 
@@ -197,27 +211,32 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
     for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((K + BK - 1) / BK);
-  issue(0, 0);
+  // prologue: tiles 0..NSTAGE-2 in flight
+#pragma unroll
+  for (int t = 0; t < NSTAGE - 1; ++t)
+    if (t < nk) issue(t, (long)t * BK);
   const int fr = lane & 15, fk = lane >> 4;   // fragment row / k-chunk of this lane
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    // tile kt's loads are the only ones in flight: retire them, then one barrier both publishes
-    // every wave's share of stage `cur` and certifies that stage cur^1 (read in iteration kt-1)
-    // is free, so tile kt+1 streams into it while tile kt is multiplied
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = kt % NSTAGE;
+    // retire tile kt (this thread's loads), leaving the later prefetched tiles in flight
+    const int later = min(NSTAGE - 2, nk - 1 - kt);
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * INS) : "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(INS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // one barrier publishes every wave's share of tile kt and certifies that the stage read in
+    // iteration kt-1 is free for tile kt + NSTAGE - 1
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) issue(cur ^ 1, (long)(kt + 1) * BK);
+    if (kt + NSTAGE - 1 < nk) issue((kt + NSTAGE - 1) % NSTAGE, (long)(kt + NSTAGE - 1) * BK);
     const unsigned char* sa = smem + cur * STAGE;
     const unsigned char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
+    for (int kh = 0; kh < BK / 32; ++kh) {
       uint4 bf[CB];
 #pragma unroll
-      for (int j = 0; j < CB; ++j)
-        bf[j] = *reinterpret_cast<const uint4*>(sb + img_off(wn * 64 + j * 16 + fr, kh * 4 + fk));
+      for (int j = 0; j < CB; ++j) bf[j] = *reinterpret_cast<const uint4*>(sb + img_off<BK>(wn * 64 + j * 16 + fr, kh * 4 + fk));
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        const uint4 af = *reinterpret_cast<const uint4*>(sa + img_off(wm * WTM + i * 16 + fr, kh * 4 + fk));
+        const uint4 af = *reinterpret_cast<const uint4*>(sa + img_off<BK>(wm * WTM + i * 16 + fr, kh * 4 + fk));
 #pragma unroll
         for (int j = 0; j < CB; ++j) acc[i][j] = Mf<T>::mma(af, bf[j], acc[i][j]);
       }
@@ -227,8 +246,6 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 
   // ---- epilogue: bias / activation, C tile staged through LDS so every lane stores 16 B --------
   // acc[i][j] register e = C[row 4*(lane>>4) + e][col lane&15] of 16x16 block (i, j)
-  constexpr int CROW = BN * 2 + 16;                   // padded LDS row (bytes) of the C tile
-  static_assert(BM * CROW <= 2 * STAGE, "C tile must fit the staging LDS");
   unsigned char* ct = smem;
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
@@ -263,13 +280,18 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   }
 }
 
+// BK = 64 (one tile in flight, half the barriers) suits compute-bound GEMMs; BK = 32 (three tiles
+// in flight) the short-K, bandwidth-heavy convolutions. PHA_G256_BK overrides.
 template <typename T, bool CONV>
 int launch(const Args& a, hipStream_t st) {
   const long tiles_m = (a.M + BM - 1) / BM;
+  const char* e = getenv("PHA_G256_BK");
+  const int bk = e ? atoi(e) : ((CONV || a.K <= 1024) ? 32 : 64);
   auto go = [&](auto bn) {
     constexpr int BN = decltype(bn)::value;
     const long tiles = tiles_m * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm256_kernel<T, BN, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    if (bk == 32) hipLaunchKernelGGL((gemm256_kernel<T, BN, 32, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm256_kernel<T, BN, 64, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
   };
   if (a.N <= 64) go(std::integral_constant<int, 64>());
   else if (a.N <= 128) go(std::integral_constant<int, 128>());
