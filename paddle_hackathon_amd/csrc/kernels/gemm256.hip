@@ -30,7 +30,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 256, NT = 512;
+constexpr int NT = 512;
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
@@ -98,14 +98,16 @@ struct ARow {
   bool ok;
 };
 
-template <typename T, int BN, int BK, bool CONV>
+template <typename T, int BM, int BN, int BK, bool CONV>
 __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   constexpr int NSTAGE = BK == 64 ? 2 : 4;   // BK 64: one tile in flight; BK 32: three
   constexpr int WN = BN / 64, WM = 8 / WN;          // wave grid
-  constexpr int WTM = BM / WM;                       // wave tile rows (32 | 64 | 128)
+  constexpr int WTM = BM / WM;                       // wave tile rows (16 .. 128)
+  static_assert(WTM % 16 == 0, "wave tile rows");
   constexpr int RB = WTM / 16, CB = 4;               // 16x16 blocks per wave
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INS = A_BYTES / (NT * 16);                  // glds per thread per stage (2)
+  constexpr int A_WI = A_BYTES / 1024;                        // A wave-instructions per stage
+  constexpr int A_INS = (A_WI + 7) / 8;                       // per thread
   constexpr int B_WI = B_BYTES / 1024;                        // B wave-instructions per stage (4 | 8 | 16)
   constexpr int B_INS = (B_WI + 7) / 8;                       // per thread (waves beyond B_WI repeat one)
   constexpr int INS = A_INS + B_INS;
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   ARow ar[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
-    const int row = (j * 8 + wid) * RPI + lrow;
+    const int row = ((j * 8 + wid) % A_WI) * RPI + lrow;
     const long m = m0 + row;
     ar[j].ok = m < M;
     if constexpr (CONV) {
@@ -195,7 +197,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
           src = ar[j].base + k * sizeof(T);
         }
       }
-      glds16(src, sa + (j * 8 + wid) * 1024);
+      glds16(src, sa + ((j * 8 + wid) % A_WI) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
@@ -282,21 +284,44 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 
 // BK = 64 (one tile in flight, half the barriers) suits compute-bound GEMMs; BK = 32 (three tiles
 // in flight) the short-K, bandwidth-heavy convolutions. PHA_G256_BK overrides.
+// tile: index into cands (-1 = heuristic), bk: 32 | 64 (0 = heuristic); the host autotuner
+// (ops/conv_gemm.py) times the candidates once per shape and passes its choice
 template <typename T, bool CONV>
-int launch(const Args& a, hipStream_t st) {
-  const long tiles_m = (a.M + BM - 1) / BM;
-  const char* e = getenv("PHA_G256_BK");
-  const int bk = e ? atoi(e) : ((CONV || a.K <= 1024) ? 32 : 64);
-  auto go = [&](auto bn) {
-    constexpr int BN = decltype(bn)::value;
-    const long tiles = tiles_m * ((a.N + BN - 1) / BN);
-    if (bk == 32) hipLaunchKernelGGL((gemm256_kernel<T, BN, 32, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((gemm256_kernel<T, BN, 64, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0) {
+  if (bk != 32 && bk != 64) bk = (CONV || a.K <= 1024) ? 32 : 64;
+  // tile shape: the fewest "CU rounds x tile work / tile efficiency" (a 784-tile grid on 256 CUs
+  // wastes a quarter of the chip in its last round; small tiles pay in operand re-reads)
+  static const int cands[6][2] = {{256, 256}, {256, 128}, {128, 256}, {256, 64}, {128, 128}, {128, 64}};
+  static const float eff[6] = {1.0f, 0.9f, 0.88f, 0.72f, 0.75f, 0.55f};
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  int best = 0;
+  double best_t = 1e300;
+  for (int c = 0; c < 6; ++c) {
+    const int bm = cands[c][0], bn = cands[c][1];
+    if (bn > 64 && a.N <= bn / 2) continue;   // half-empty column tiles
+    const long tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+    const int per_cu = bm == 128 ? 2 : 1;      // 128-row tiles fit two workgroups per CU
+    const double rounds = (double)((tiles + (long)cus * per_cu - 1) / ((long)cus * per_cu));
+    const double t = rounds * bm * bn / (eff[c] * per_cu);
+    if (t < best_t * 0.97) { best_t = t; best = c; }
+  }
+  if (tile >= 0 && tile < 6) best = tile;
+  const int bm = cands[best][0], bn = cands[best][1];
+  auto go = [&](auto bm_c, auto bn_c) {
+    constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;
+    const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
+    if (bk == 32) hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 32, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 64, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
   };
-  if (a.N <= 64) go(std::integral_constant<int, 64>());
-  else if (a.N <= 128) go(std::integral_constant<int, 128>());
-  else go(std::integral_constant<int, 256>());
-  return (int)hipGetLastError();
+#define G256_CASE(M_, N_) if (bm == M_ && bn == N_) { go(std::integral_constant<int, M_>(), std::integral_constant<int, N_>()); return (int)hipGetLastError(); }
+  G256_CASE(256, 256) G256_CASE(256, 128) G256_CASE(256, 64) G256_CASE(128, 256) G256_CASE(128, 128) G256_CASE(128, 64)
+#undef G256_CASE
+  return (int)hipErrorInvalidValue;
 }
 
 }  // namespace g256
@@ -306,24 +331,25 @@ using namespace pha;
 
 // C[M,N] = A[M,K] . Bt[N,K]^T (+bias)(act); A, Bt K-contiguous, K % 8 == 0, 16-B aligned rows.
 PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const float* bias, long M, long N, long K,
-                           long lda, long ldb, long ldc, int act, const void* zero16, hipStream_t stream) {
+                           long lda, long ldb, long ldc, int act, const void* zero16, int tile, int bk,
+                           hipStream_t stream) {
   if (K % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}};
-  if (dt == kBF16) return g256::launch<bf16_t, false>(p, stream);
-  if (dt == kF16) return g256::launch<half_t, false>(p, stream);
+  if (dt == kBF16) return g256::launch<bf16_t, false>(p, stream, tile, bk);
+  if (dt == kF16) return g256::launch<half_t, false>(p, stream, tile, bk);
   return (int)hipErrorInvalidValue;
 }
 
 // NHWC conv forward: y[N*OH*OW, Cout] = im2col(x) . w^T, w as [Cout][KH][KW][Cin], Cin % 8 == 0.
 PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H, int W,
                             int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
-                            const void* zero16, hipStream_t stream) {
+                            const void* zero16, int tile, int bk, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
                   KH, KW, sh, sw, ph, pw, dh, dw};
   const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
   g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g};
-  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream);
-  if (dt == kF16) return g256::launch<half_t, true>(p, stream);
+  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk);
+  if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk);
   return (int)hipErrorInvalidValue;
 }

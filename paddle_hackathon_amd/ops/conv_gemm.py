@@ -222,12 +222,41 @@ def _L256():
     L = _L()
     if not getattr(L, "_g256_sig", False):
         P, I, LG = c_void_p, c_int, c_long
-        L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, P]
+        L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
-        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, P]
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P]
         L.pha_conv256_fwd.restype = c_int
         L._g256_sig = True
     return L
+
+
+_tuned = {}
+_CANDS = [(t, bk) for t in range(6) for bk in (32, 64)]
+
+
+def _autotune(key, run):
+    """Pick the (tile shape, BK) of the 256-row-tile kernels for this problem once: time every
+    candidate on the real operands (first call only; later calls reuse the choice)."""
+    ch = _tuned.get(key)
+    if ch is not None:
+        return ch
+    import os
+    if os.environ.get("PHA_G256_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing():
+        return (-1, 0)
+    best, best_t = (-1, 0), float("inf")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for tile, bk in _CANDS:
+        run(tile, bk)
+        ev0.record()
+        for _ in range(3):
+            run(tile, bk)
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1)
+        if t < best_t:
+            best, best_t = (tile, bk), t
+    _tuned[key] = best
+    return best
 
 
 def gemm256_nt(a, bt, bias=None, act=None, out=None):
@@ -241,11 +270,14 @@ def gemm256_nt(a, bt, bias=None, act=None, out=None):
     if bias is not None:
         bias = bias.float().contiguous()
         assert bias.numel() == N
-    rc = _L256().pha_gemm256_nt(_DT[a.dtype], _ptr(a), _ptr(bt), _ptr(c), _ptr(bias), M, N, K, a.stride(0),
-                                bt.stride(0), c.stride(0), _ACT[act], _ptr(_zero_page(a.device)),
-                                c_void_p(torch.cuda.current_stream(a.device).cuda_stream))
-    if rc != 0:
-        raise RuntimeError(f"pha_gemm256_nt failed ({rc})")
+    L, z, st = _L256(), _ptr(_zero_page(a.device)), c_void_p(torch.cuda.current_stream(a.device).cuda_stream)
+
+    def run(tile, bk):
+        rc = L.pha_gemm256_nt(_DT[a.dtype], _ptr(a), _ptr(bt), _ptr(c), _ptr(bias), M, N, K, a.stride(0), bt.stride(0),
+                              c.stride(0), _ACT[act], z, tile, bk, st)
+        if rc != 0:
+            raise RuntimeError(f"pha_gemm256_nt failed ({rc})")
+    run(*_autotune(("gemm", a.dtype, M, N, K), run))
     return c
 
 
@@ -263,9 +295,12 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None):
     y = torch.empty((N, OH, OW, Co), dtype=x.dtype, device=x.device)
     if bias is not None:
         bias = bias.float().contiguous()
-    rc = _L256().pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
-                                 sh, sw, ph, pw, dh, dw, _ACT[act], _ptr(_zero_page(x.device)),
-                                 c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
-    if rc != 0:
-        raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
+    L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+
+    def run(tile, bk):
+        rc = L.pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
+                               sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, st)
+        if rc != 0:
+            raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
+    run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw), run))
     return y

@@ -29,6 +29,13 @@ for s in "$@"; do
     bench_g256)
       timeout -k 10 300 python tools/bench_gemm256.py > $OUT/bench_g256.log 2>&1; rc=$?
       cat $OUT/bench_g256.log | tail -20 ;;
+    prof_g256)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_g256; mkdir -p $OUT/prof_g256
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_g256/pmc1 -o run --output-format csv -- python3 $ROOT/tools/g256_prof.py > $OUT/prof_g256/pmc1.log 2>&1; rc=$?
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g256/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g256_prof.py > $OUT/prof_g256/pmc2.log 2>&1; rc=$?; fi
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d $OUT/prof_g256/pmc3 -o run --output-format csv -- python3 $ROOT/tools/g256_prof.py > $OUT/prof_g256/pmc3.log 2>&1; rc=$?; fi
+      tail -2 $OUT/prof_g256/*.log ;;
     prof)
       export TMPDIR=/tmp
       rm -rf $OUT/prof
