@@ -20,6 +20,7 @@
 //    s_waitcnt vmcnt (never 0 in the loop) ahead of a raw s_barrier — __syncthreads() would drain
 //    the prefetch too.
 #include "common.h"
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -39,6 +40,10 @@ struct ConvGeo {
   int OH, OW;
   int KH, KW;
   int sh, sw, ph, pw, dh, dw;
+  // output row remap (osh > 0): output pixel (n, oh, ow) is stored at row
+  // (n * OHF + oh0 + oh * osh) * OWF + ow0 + ow * osw — one phase of a strided conv's dgrad
+  int OHF, OWF, oh0, ow0, osh, osw;
+  int ozero;   // also store zeros at the osh x osw - 1 other pixels of the output's stride cell
 };
 
 struct Args {
@@ -270,9 +275,26 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   const bool full_n = n0 + BN <= N && (p.ldc % 8) == 0;
   for (int idx = tid; idx < BM * CH; idx += NT) {
     const int ml = idx / CH, c8 = idx % CH;
-    const long m = m0 + ml, n = n0 + c8 * 8;
+    long m = m0 + ml;
+    const long n = n0 + c8 * 8;
     if (m >= M) continue;
     const uint4 v = *reinterpret_cast<const uint4*>(ct + ml * CROW + c8 * 16);
+    if constexpr (CONV) {
+      const ConvGeo& g = p.g;
+      if (g.osh > 0) {
+        const int hw = g.OH * g.OW;
+        const int b = (int)(m / hw), rem = (int)(m - (long)b * hw);
+        const int oh = rem / g.OW, ow = rem - oh * g.OW;
+        const int fh = g.oh0 + oh * g.osh, fw = g.ow0 + ow * g.osw;
+        m = ((long)b * g.OHF + fh) * g.OWF + fw;
+        if (g.ozero && full_n) {   // taps reach only phase (0, 0): the rest of the cell is zero
+          for (int a = 0; a < g.osh; ++a)
+            for (int c = 0; c < g.osw; ++c)
+              if ((a | c) && fh + a < g.OHF && fw + c < g.OWF)
+                *reinterpret_cast<uint4*>(C + (m + (long)a * g.OWF + c) * p.ldc + n) = uint4{0, 0, 0, 0};
+        }
+      }
+    }
     if (full_n) {
       *reinterpret_cast<uint4*>(C + m * p.ldc + n) = v;
     } else {
@@ -324,6 +346,299 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0) {
   return (int)hipErrorInvalidValue;
 }
 
+
+// ================================================================================================
+// TN: C[M, N] = sum_k A[k, m] * B[k, n] — both operands K-OUTER (M / N contiguous): the weight
+// gradient of a linear layer (dW = X^T dY over tokens) and of a convolution (dW = dY^T im2col(X)
+// over output pixels, B_CONV gathers the im2col rows). K is long and M x N small, so the K range
+// is split over blockIdx (split s writes fp32 partials ws[s][M][N]; tn_finalize sums the splits,
+// converts and, for convolutions, permutes [Cout][tap][Cin] to the [Cout][Cin][KH][KW] filter).
+//
+// The LDS images are [BK k-rows][BM | BN] exactly as the operands lie in HBM (glds, lane-linear),
+// and the MFMA fragments are read TRANSPOSED with ds_read_b64_tr_b16 (CDNA guide T10): per 16-lane
+// group a 4 k-row x 16 column block arrives column-major, i.e. as 4 consecutive k of one m / n —
+// two reads give the 8-k operand of v_mfma_f32_16x16x32. Chunk swizzle: the 8 k-rows a 32-lane
+// half reads (rows r0+{0..3} and r0+8+{0..3}) land on 8 distinct 32-B bank groups.
+// ================================================================================================
+__device__ __forceinline__ int tn_mask(int row, int row_bytes) {
+  if (row_bytes >= 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
+  return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;   // 128-B rows: two rows per bank row
+}
+
+typedef short tn_v4i16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint2 tr16(const unsigned char* ptr) {
+  const tn_v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tn_v4i16*)(ptr));
+  return __builtin_bit_cast(uint2, r);
+}
+
+// 8-k operand of a 16-column block starting at column c0 (multiple of 16), k-rows r0 .. r0+7 of
+// the group (the caller passes r0 = kbase + 8 * (lane >> 4))
+template <int ROWB>
+__device__ __forceinline__ uint4 tn_frag(const unsigned char* img, int r0, int c0, int q, int pp) {
+  const int ch = (c0 >> 3) + (pp >> 1);
+  const int ra = r0 + q, rb = r0 + 4 + q;
+  const uint2 lo = tr16(img + ra * ROWB + ((ch ^ tn_mask(ra, ROWB)) << 4) + 8 * (pp & 1));
+  const uint2 hi = tr16(img + rb * ROWB + ((ch ^ tn_mask(rb, ROWB)) << 4) + 8 * (pp & 1));
+  return uint4{lo.x, lo.y, hi.x, hi.y};
+}
+
+struct TnArgs {
+  const void* a;   // [K][lda] (M contiguous)
+  const void* b;   // [K][ldb] (N contiguous) — or the NHWC input x (B_CONV)
+  float* ws;       // [S][M][N] fp32 partials
+  long M, N, K;
+  long lda, ldb;
+  long kchunk;     // rows of K per split (multiple of BK)
+  int splits;
+  const void* zero;
+  ConvGeo g;       // B_CONV: K = N*OH*OW output pixels, N = KH*KW*C
+};
+
+template <typename T, int BM, int BN, bool BCONV>
+__global__ __launch_bounds__(NT) void gemm256_tn_kernel(TnArgs p) {
+  constexpr int BK = 32, NSTAGE = 4;
+  constexpr int WN = BN / 64, WM = 8 / WN, WTM = BM / WM;
+  static_assert(WTM % 16 == 0, "wave tile rows");
+  constexpr int RB = WTM / 16, CB = 4;
+  constexpr int RA = BM * 2, RBB = BN * 2;                  // image row bytes
+  constexpr int A_BYTES = BK * RA, B_BYTES = BK * RBB, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_WI = A_BYTES / 1024, B_WI = B_BYTES / 1024;
+  constexpr int A_INS = (A_WI + 7) / 8, B_INS = (B_WI + 7) / 8, INS = A_INS + B_INS;
+  constexpr int ACPR = RA / 16, ARPI = 1024 / RA;           // chunks per row / rows per wave-instr
+  constexpr int BCPR = RBB / 16, BRPI = 1024 / RBB;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NSTAGE * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const long M = p.M, N = p.N;
+
+  // XCD-bijective order over (split, tile): an XCD walks consecutive tiles of one K split, so
+  // they share the split's A / B rows in its L2
+  const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+  const int ntiles = tiles_m * tiles_n, total = ntiles * p.splits;
+  const int bid = blockIdx.x;
+  const int q8 = total / 8, r8 = total % 8, xcd = bid % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int split = lin / ntiles, tile = lin % ntiles;
+  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+  const long kbeg = (long)split * p.kchunk;
+  const long kend = min(p.K, kbeg + p.kchunk);
+
+  const T* A = static_cast<const T*>(p.a);
+  const T* B = static_cast<const T*>(p.b);
+  const char* zero = static_cast<const char*>(p.zero);
+
+  // per-lane source columns (constant over the K loop) and image rows of each glds instruction
+  int arow[A_INS];
+  const char* acol[A_INS];
+#pragma unroll
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = ((j * 8 + wid) % A_WI) * ARPI + lane / ACPR;
+    const int sch = (lane % ACPR) ^ tn_mask(row, RA);
+    const long m = m0 + sch * 8;
+    arow[j] = row;
+    acol[j] = m < M ? reinterpret_cast<const char*>(A + m) : nullptr;
+  }
+  int brow[B_INS];
+  const char* bcol[B_INS];
+  int bkh[B_INS], bkw[B_INS];   // conv: tap offsets kh*dh - ph, kw*dw - pw of the lane's column
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = ((j * 8 + wid) % B_WI) * BRPI + lane / BCPR;
+    const int sch = (lane % BCPR) ^ tn_mask(row, RBB);
+    const long n = n0 + sch * 8;
+    brow[j] = row;
+    bkh[j] = bkw[j] = 0;
+    if constexpr (BCONV) {
+      const ConvGeo& g = p.g;
+      const int tap = (int)(n / g.C), cin = (int)(n - (long)tap * g.C);
+      const int kh = tap / g.KW, kw = tap - kh * g.KW;
+      bkh[j] = kh * g.dh - g.ph;
+      bkw[j] = kw * g.dw - g.pw;
+      bcol[j] = n < N ? reinterpret_cast<const char*>(B + cin) : nullptr;
+    } else {
+      bcol[j] = n < N ? reinterpret_cast<const char*>(B + n) : nullptr;
+    }
+  }
+
+  auto issue = [&](int stage, long k0) {
+    unsigned char* sa = smem + stage * STAGE;
+    unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const long k = k0 + arow[j];
+      const char* src = (acol[j] && k < kend) ? acol[j] + k * p.lda * (long)sizeof(T) : zero;
+      glds16(src, sa + ((j * 8 + wid) % A_WI) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const long k = k0 + brow[j];
+      const char* src = zero;
+      if (bcol[j] && k < kend) {
+        if constexpr (BCONV) {
+          const ConvGeo& g = p.g;
+          const int hw = g.OH * g.OW, ki = (int)k;   // pixel count < 2^31: 32-bit division
+          const int b = ki / hw, rem = ki - b * hw;
+          const int oh = rem / g.OW, ow = rem - oh * g.OW;
+          const int ih = oh * g.sh + bkh[j], iw = ow * g.sw + bkw[j];
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            src = bcol[j] + (((long)b * g.H + ih) * g.W + iw) * g.C * (long)sizeof(T);
+        } else {
+          src = bcol[j] + k * p.ldb * (long)sizeof(T);
+        }
+      }
+      glds16(src, sb + ((j * 8 + wid) % B_WI) * 1024);
+    }
+  };
+
+  f32x4 acc[RB][CB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kend > kbeg ? (int)((kend - kbeg + BK - 1) / BK) : 0;
+#pragma unroll
+  for (int t = 0; t < NSTAGE - 1; ++t)
+    if (t < nk) issue(t, kbeg + (long)t * BK);
+  const int fk = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % NSTAGE;
+    const int later = min(NSTAGE - 2, nk - 1 - kt);
+    if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * INS) : "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(INS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSTAGE - 1 < nk) issue((kt + NSTAGE - 1) % NSTAGE, kbeg + (long)(kt + NSTAGE - 1) * BK);
+    const unsigned char* sa = smem + cur * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+    const int r0 = 8 * fk;
+    uint4 bf[CB];
+#pragma unroll
+    for (int j = 0; j < CB; ++j) bf[j] = tn_frag<RBB>(sb, r0, wn * 64 + j * 16, q, pp);
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const uint4 af = tn_frag<RA>(sa, r0, wm * WTM + i * 16, q, pp);
+#pragma unroll
+      for (int j = 0; j < CB; ++j) acc[i][j] = Mf<T>::mma(af, bf[j], acc[i][j]);
+    }
+  }
+
+  // fp32 partials straight from the accumulators: register e of block (i, j) is
+  // C[4 * (lane >> 4) + e][lane & 15]; 16 lanes store 64 contiguous bytes of a row
+  float* ws = p.ws + (long)split * M * N;
+  const int fr = lane & 15;
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    const long n = n0 + wn * 64 + j * 16 + fr;
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long m = m0 + wm * WTM + i * 16 + 4 * fk + e;
+        if (m < M) ws[m * N + n] = acc[i][j][e];
+      }
+  }
+}
+
+// first level of the split-K sum: ws2[g][i] = sum of splits [16g, 16g + 16) of ws, 4 floats per thread
+// (grid.y = split groups: the sum reads S x M x N floats across the whole chip, not 16 CUs)
+__global__ __launch_bounds__(256) void tn_reduce16_kernel(const float* __restrict__ ws, float* __restrict__ ws2, long MN,
+                                                         int S) {
+  const long i4 = (blockIdx.x * 256L + threadIdx.x) * 4;
+  if (i4 >= MN) return;
+  const int s0 = blockIdx.y * 16, s1 = min(S, s0 + 16);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int s = s0; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(ws + s * MN + i4);
+  *reinterpret_cast<f32x4*>(ws2 + blockIdx.y * MN + i4) = acc;
+}
+
+// out = sum_s ws[s] (+ out if accumulate), converted to T (or fp32 when OUTF32); conv_c > 0
+// permutes column n = tap * conv_c + cin of row m to out[m][cin][tap] (taps = N / conv_c)
+template <typename T, bool OUTF32>
+__global__ __launch_bounds__(256) void tn_finalize_kernel(const float* __restrict__ ws, void* out, long M, long N,
+                                                           int S, int conv_c, int accumulate) {
+  const long total = M * N;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += ws[s * total + idx];
+    long o = idx;
+    if (conv_c > 0) {
+      const long m = idx / N, n = idx - m * N;
+      const int taps = (int)(N / conv_c);
+      const int tap = (int)(n / conv_c), cin = (int)(n - (long)tap * conv_c);
+      o = m * N + (long)cin * taps + tap;
+    }
+    if constexpr (OUTF32) {
+      float* y = static_cast<float*>(out);
+      y[o] = accumulate ? y[o] + v : v;
+    } else {
+      T* y = static_cast<T*>(out);
+      if (accumulate) v += Cvt<T>::ld(y, o);
+      Cvt<T>::st(y, o, v);
+    }
+  }
+}
+
+// tile: 0 (256x256) 1 (256x128) 2 (128x256) 3 (128x128) 4 (64x256) 5 (256x64) 6 (128x64) 7 (64x128)
+template <typename T, bool BCONV>
+int launch_tn(TnArgs a, void* out, int out_f32, int conv_c, int accumulate, int tile, int splits, hipStream_t st) {
+  static const int cands[8][2] = {{256, 256}, {256, 128}, {128, 256}, {128, 128},
+                                  {64, 256}, {256, 64}, {128, 64}, {64, 128}};
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  if (tile < 0 || tile > 7) {   // the fewest MFMA-padded tiles, then the largest tile
+    tile = 0;
+    double best = 1e300;
+    for (int c = 0; c < 8; ++c) {
+      const int bm = cands[c][0], bn = cands[c][1];
+      const double pad = (double)((a.M + bm - 1) / bm * bm) * ((a.N + bn - 1) / bn * bn);
+      const double cost = pad * (1.0 + 0.15 * (bm < 256) + 0.15 * (bn < 256));
+      if (cost < best * 0.999) { best = cost; tile = c; }
+    }
+  }
+  const int bm = cands[tile][0], bn = cands[tile][1];
+  const long tiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  const long kblocks = (a.K + 31) / 32;
+  if (splits <= 0) splits = (int)std::max(1L, std::min(kblocks / 8, (2L * cus + tiles - 1) / tiles));
+  splits = (int)std::max(1L, std::min((long)splits, kblocks));
+  a.kchunk = ((kblocks + splits - 1) / splits) * 32;
+  a.splits = (int)((a.K + a.kchunk - 1) / a.kchunk);
+  const unsigned grid = (unsigned)(tiles * a.splits);
+#define TN_CASE(M_, N_) \
+  if (bm == M_ && bn == N_) hipLaunchKernelGGL((gemm256_tn_kernel<T, M_, N_, BCONV>), dim3(grid), dim3(NT), 0, st, a);
+  TN_CASE(256, 256) TN_CASE(256, 128) TN_CASE(128, 256) TN_CASE(128, 128)
+  TN_CASE(64, 256) TN_CASE(256, 64) TN_CASE(128, 64) TN_CASE(64, 128)
+#undef TN_CASE
+  const long total = a.M * a.N;
+  const float* part = a.ws;
+  int S = a.splits;
+  if (S > 32) {   // ws holds (S + ceil(S / 16)) x M x N floats
+    float* ws2 = a.ws + (long)S * total;
+    const int G = (S + 15) / 16;
+    hipLaunchKernelGGL(tn_reduce16_kernel, dim3((unsigned)((total / 4 + 255) / 256), G), dim3(256), 0, st, a.ws, ws2,
+                       total, S);
+    part = ws2;
+    S = G;
+  }
+  const unsigned fg = (unsigned)std::min((total + 255) / 256, 8192L);
+  if (out_f32) hipLaunchKernelGGL((tn_finalize_kernel<T, true>), dim3(fg), dim3(256), 0, st, part, out, a.M, a.N,
+                                  S, conv_c, accumulate);
+  else hipLaunchKernelGGL((tn_finalize_kernel<T, false>), dim3(fg), dim3(256), 0, st, part, out, a.M, a.N,
+                          S, conv_c, accumulate);
+  return (int)hipGetLastError();
+}
+
+
 }  // namespace g256
 }  // namespace pha
 
@@ -341,15 +656,47 @@ PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const
 }
 
 // NHWC conv forward: y[N*OH*OW, Cout] = im2col(x) . w^T, w as [Cout][KH][KW][Cin], Cin % 8 == 0.
+// oremap (host int[9], may be null): strided output rows and explicit output size, see ConvGeo.
 PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H, int W,
                             int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
-                            const void* zero16, int tile, int bk, hipStream_t stream) {
+                            const void* zero16, int tile, int bk, const int* oremap, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
-                  KH, KW, sh, sw, ph, pw, dh, dw};
+                  KH, KW, sh, sw, ph, pw, dh, dw, 0, 0, 0, 0, 0, 0, 0};
+  if (oremap) {   // {OHF, OWF, oh0, ow0, osh, osw, OH, OW, ozero}: phase output size given explicitly
+    g.OHF = oremap[0]; g.OWF = oremap[1]; g.oh0 = oremap[2]; g.ow0 = oremap[3]; g.osh = oremap[4]; g.osw = oremap[5];
+    g.OH = oremap[6]; g.OW = oremap[7]; g.ozero = oremap[8];
+  }
   const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
   g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g};
   if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk);
   if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk);
+  return (int)hipErrorInvalidValue;
+}
+
+// C[M,N] = sum_k A[k][m] B[k][n] (K-outer operands, M/N contiguous, lda/ldb % 8 == 0), split-K over
+// `splits` fp32 partials in ws (>= (splits + (splits > 32 ? ceil(splits/16) : 0))*M*N floats), summed into out (T, or fp32 when out_f32; += when accumulate).
+PHA_API int pha_gemm256_tn(int dt, const void* a, const void* b, void* out, float* ws, long M, long N, long K, long lda,
+                           long ldb, int out_f32, int accumulate, const void* zero16, int tile, int splits,
+                           hipStream_t stream) {
+  if (M % 8 || N % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  g256::TnArgs p{a, b, ws, M, N, K, lda, ldb, 0, 1, zero16, {}};
+  if (dt == kBF16) return g256::launch_tn<bf16_t, false>(p, out, out_f32, 0, accumulate, tile, splits, stream);
+  if (dt == kF16) return g256::launch_tn<half_t, false>(p, out, out_f32, 0, accumulate, tile, splits, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+// NHWC conv weight gradient: dw[Cout][Cin][KH][KW] = sum over output pixels of dy[p][cout] *
+// im2col(x)[p][(kh, kw, cin)]; dy [N*OH*OW][Cout], Cin % 8 == 0, Cout % 8 == 0.
+PHA_API int pha_conv256_wgrad(int dt, const void* dy, const void* x, void* dw, float* ws, int N, int H, int W, int C,
+                              int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw_,
+                              int out_f32, const void* zero16, int tile, int splits, hipStream_t stream) {
+  if (C % 8 || Cout % 8) return (int)hipErrorInvalidValue;
+  g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw_ * (KW - 1) - 1) / sw + 1,
+                  KH, KW, sh, sw, ph, pw, dh, dw_, 0, 0, 0, 0, 0, 0, 0};
+  const long K = (long)N * g.OH * g.OW;
+  g256::TnArgs p{dy, x, ws, (long)Cout, (long)KH * KW * C, K, (long)Cout, (long)C, 0, 1, zero16, g};
+  if (dt == kBF16) return g256::launch_tn<bf16_t, true>(p, dw, out_f32, C, 0, tile, splits, stream);
+  if (dt == kF16) return g256::launch_tn<half_t, true>(p, dw, out_f32, C, 0, tile, splits, stream);
   return (int)hipErrorInvalidValue;
 }

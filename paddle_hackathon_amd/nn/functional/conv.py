@@ -67,15 +67,20 @@ def _to_ncx(t, data_format):
 
 
 def _hip_conv2d(x, w, bias, stride, pad, dilation, groups):
-    """NHWC conv on the gfx950 implicit-GEMM MFMA kernels (ops/conv_gemm.py). Inputs whose
-    channel count is not a multiple of 8 (the RGB stem) are zero-padded to 8 channels."""
+    """NHWC conv on the gfx950 implicit-GEMM MFMA kernels (ops/conv_gemm.py: forward, dgrad and
+    wgrad on the 256-tile glds kernels of gemm256.hip; PHA_CONV_KERNEL=v1 selects the older
+    gemm_conv.hip path). Inputs whose channel count is not a multiple of 8 (the RGB stem) are
+    zero-padded to 8 channels."""
+    import os
     from ...ops import conv_gemm
     if x.shape[-1] % 8 != 0:
         c = x.shape[-1]
         cp = (c + 7) // 8 * 8
         x = TF.pad(x, [0, cp - c])
         w = TF.pad(w, [0, 0, 0, 0, 0, cp - c])
-    return conv_gemm.conv2d_nhwc(x, w, bias, stride, pad, dilation)
+    if os.environ.get("PHA_CONV_KERNEL", "256") == "v1":
+        return conv_gemm.conv2d_nhwc(x, w, bias, stride, pad, dilation)
+    return conv_gemm.conv2d_nhwc256(x, w, bias, stride, pad, dilation)
 
 
 def _hip_conv_ok(t_nhwc, w, groups):

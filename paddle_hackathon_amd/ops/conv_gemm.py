@@ -224,7 +224,11 @@ def _L256():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
-        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P]
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
+        L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
+        L.pha_gemm256_tn.restype = c_int
+        L.pha_conv256_wgrad.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P]
+        L.pha_conv256_wgrad.restype = c_int
         L.pha_conv256_fwd.restype = c_int
         L._g256_sig = True
     return L
@@ -281,8 +285,12 @@ def gemm256_nt(a, bt, bias=None, act=None, out=None):
     return c
 
 
-def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None):
-    """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout]."""
+def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None):
+    """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout].
+
+    ``remap = (oh0, ow0, osh, osw, OH, OW[, zero_rest])`` computes an OH x OW output and stores pixel
+    (oh, ow) at (oh0 + oh*osh, ow0 + ow*osw) of ``out`` — one phase of a strided convolution's dgrad;
+    ``zero_rest`` (with oh0 = ow0 = 0) also zero-fills the other pixels of each stride cell."""
     assert x.dtype in _DT and w_okkc.dtype == x.dtype and x.is_contiguous() and w_okkc.is_contiguous()
     N, H, W, C = x.shape
     Co, KH, KW, Cw = w_okkc.shape
@@ -290,17 +298,228 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None):
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
-    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
-    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
-    y = torch.empty((N, OH, OW, Co), dtype=x.dtype, device=x.device)
+    rm = None
+    if remap is not None:
+        assert out is not None and out.is_contiguous() and out.shape[0] == N and out.shape[3] == Co
+        oh0, ow0, osh, osw, OH, OW = remap[:6]
+        zr = int(len(remap) > 6 and bool(remap[6]))
+        assert oh0 + (OH - 1) * osh < out.shape[1] and ow0 + (OW - 1) * osw < out.shape[2]
+        assert not zr or (oh0 == ow0 == 0 and OH * osh >= out.shape[1] and OW * osw >= out.shape[2] and Co % 8 == 0)
+        rm = (c_int * 9)(out.shape[1], out.shape[2], oh0, ow0, osh, osw, OH, OW, zr)
+        y = out
+    else:
+        OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+        OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+        y = out if out is not None else torch.empty((N, OH, OW, Co), dtype=x.dtype, device=x.device)
+        assert y.shape == (N, OH, OW, Co) and y.is_contiguous()
     if bias is not None:
         bias = bias.float().contiguous()
     L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
 
     def run(tile, bk):
         rc = L.pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
-                               sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, st)
+                               sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, rm, st)
         if rc != 0:
             raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
-    run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw), run))
+    run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw, OH, OW), run))
     return y
+
+
+def conv256_dgrad(dy, w, x_shape, stride, padding, dilation):
+    """dx [N, H, W, Ci] of an NHWC conv from dy [N, OH, OW, Co] and w [Co, Ci, KH, KW], on the forward
+    kernel: stride 1 is the conv of dy with the flipped, transposed filter (pad' = d*(K-1) - p);
+    stride s splits dx into s*s phases, each a stride-1 conv over the taps that reach it, stored
+    in place through the kernel's output remap (no scatter copy)."""
+    N, H, W, Ci = x_shape
+    Co, _, KH, KW = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    _, OH, OW, _ = dy.shape
+    dy = dy.contiguous()
+    if (sh, sw) == (1, 1):
+        wt = _wlayout(w, "dgrad", lambda t: t.flip(2, 3).permute(1, 2, 3, 0).contiguous())   # [Ci][KH][KW][Co]
+        dx = torch.empty(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
+        return conv256_fwd(dy, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
+                           remap=(0, 0, 1, 1, H, W))
+    if (dh, dw) != (1, 1):
+        raise NotImplementedError("strided + dilated conv dgrad")
+    phases = []
+    for rh in range(sh):
+        for rw in range(sw):
+            PH, PW = len(range(rh, H, sh)), len(range(rw, W, sw))
+            kh0, kw0 = (rh + ph) % sh, (rw + pw) % sw
+            khs, kws = list(range(kh0, KH, sh)), list(range(kw0, KW, sw))
+            phases.append((rh, rw, PH, PW, khs, kws, kh0, kw0))
+    live = [p for p in phases if p[2] and p[3] and p[4] and p[5]]
+    # only phase (0, 0) reached (1x1 stride-s filters): its kernel zero-fills the stride cells
+    zero_rest = len(live) == 1 and live[0][:2] == (0, 0) and live[0][2] * sh >= H and live[0][3] * sw >= W \
+        and Ci % 8 == 0
+    full = len(live) == len(phases) or zero_rest
+    dx = (torch.empty if full else torch.zeros)(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
+    for rh, rw, PH, PW, khs, kws, kh0, kw0 in live:
+        # output row i of the phase (input row rh + i*sh) receives dy row i + bh - j through tap
+        # khs[j]: a stride-1 conv over the reversed taps with top padding nh - 1 - bh
+        bh, bw = (rh + ph - kh0) // sh, (rw + pw - kw0) // sw
+        nh, nw = len(khs), len(kws)
+        wt = _wlayout(w, ("phase", rh, rw, sh, sw, ph, pw), lambda t, khs=khs, kws=kws:
+                      t[:, :, khs[::-1], :][:, :, :, kws[::-1]].permute(1, 2, 3, 0).contiguous())   # [Ci][nh][nw][Co]
+        conv256_fwd(dy, wt, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
+                    remap=(rh, rw, sh, sw, PH, PW, zero_rest))
+    return dx
+
+
+_wlayouts = {}
+
+
+def _wlayout(w, kind, make):
+    """filter re-layouts (forward [Co][KH][KW][Ci], flipped dgrad filters, dgrad phase filters)
+    cached per parameter version: computed once per optimizer step, not once per call"""
+    import weakref
+    key = (w.data_ptr(), w._version, tuple(w.shape), w.dtype, kind)
+    hit = _wlayouts.get(key)
+    if hit is not None and hit[0]() is w:
+        return hit[1]
+    if len(_wlayouts) > 512:
+        _wlayouts.clear()
+    with torch.no_grad():
+        v = make(w.detach())
+    _wlayouts[key] = (weakref.ref(w), v)
+    return v
+
+
+_TN_CANDS = [(256, 256), (256, 128), (128, 256), (128, 128), (64, 256), (256, 64), (128, 64), (64, 128)]
+
+
+def _tn_splits(M, N, K, tile, dev):
+    bm, bn = _TN_CANDS[tile]
+    tiles = -(-M // bm) * -(-N // bn)
+    kblocks = -(-K // 32)
+    return max(1, min(kblocks // 8, -(-2 * _num_cus(dev) // tiles), kblocks))
+
+
+def _tn_tiles(M, N):
+    """candidate tiles whose padding waste stays under 2x"""
+    out = []
+    for t, (bm, bn) in enumerate(_TN_CANDS):
+        pad = (-(-M // bm) * bm) * (-(-N // bn) * bn)
+        if pad <= 2 * M * N or (bm == 64 and bn == 128):
+            out.append(t)
+    return out
+
+
+def _tn_ws(sp, M, N, dev):
+    """fp32 split-K workspace: the partials plus the first-level sums of 16 (splits > 32)"""
+    return torch.empty((sp + (-(-sp // 16) if sp > 32 else 0)) * M * N, dtype=torch.float32, device=dev)
+
+
+def _run_tn(key, M, N, K, dev, call):
+    """autotune the tile of a TN launch once per shape; call(tile, splits, ws) launches it"""
+    ch = _tuned.get(key)
+    if ch is None:
+        import os
+        tiles = _tn_tiles(M, N)
+        if os.environ.get("PHA_G256_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing() or \
+                len(tiles) == 1:
+            # fewest tiles (least MFMA padding), larger tiles first on ties
+            ch = min(tiles, key=lambda t: -(-M // _TN_CANDS[t][0]) * -(-N // _TN_CANDS[t][1]))
+        else:
+            best_t = float("inf")
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for t in tiles:
+                sp = _tn_splits(M, N, K, t, dev)
+                ws = _tn_ws(sp, M, N, dev)
+                call(t, sp, ws)
+                ev0.record()
+                for _ in range(3):
+                    call(t, sp, ws)
+                ev1.record()
+                ev1.synchronize()
+                el = ev0.elapsed_time(ev1)
+                if el < best_t:
+                    best_t, ch = el, t
+        _tuned[key] = ch
+    sp = _tn_splits(M, N, K, ch, dev)
+    call(ch, sp, _tn_ws(sp, M, N, dev))
+
+
+def gemm256_tn(a, b, out=None, out_dtype=None, accumulate=False):
+    """C[M, N] = a[K, M]^T @ b[K, N] — the weight-gradient product (X^T dY) with both operands
+    K-outer as they come out of the forward; fp32 split-K partials, result in ``out_dtype``
+    (default a.dtype; torch.float32 for master-weight gradients) or added into ``out``."""
+    assert a.dtype in _DT and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2 and a.shape[0] == b.shape[0]
+    assert a.stride(1) == 1 and b.stride(1) == 1
+    K, M = a.shape
+    N = b.shape[1]
+    od = out.dtype if out is not None else (out_dtype or a.dtype)
+    if out is None:
+        out = torch.empty(M, N, dtype=od, device=a.device)
+        accumulate = False
+    assert out.shape == (M, N) and out.is_contiguous() and od in (a.dtype, torch.float32)
+    L, z, st = _L256(), _ptr(_zero_page(a.device)), c_void_p(torch.cuda.current_stream(a.device).cuda_stream)
+
+    tgt = {"out": out, "acc": int(accumulate)}
+
+    def call(tile, splits, ws):
+        rc = L.pha_gemm256_tn(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(tgt["out"]), _ptr(ws), M, N, K, a.stride(0),
+                              b.stride(0), int(od == torch.float32), tgt["acc"], z, tile, splits, st)
+        if rc != 0:
+            raise RuntimeError(f"pha_gemm256_tn failed ({rc})")
+    if accumulate and ("tn", a.dtype, M, N, K) not in _tuned:
+        # autotuning launches the product several times: tune on a scratch output first
+        tgt.update(out=torch.empty_like(out), acc=0)
+        _run_tn(("tn", a.dtype, M, N, K), M, N, K, a.device, call)
+        tgt.update(out=out, acc=1)
+    _run_tn(("tn", a.dtype, M, N, K), M, N, K, a.device, call)
+    return out
+
+
+def conv256_wgrad(dy, x, w_shape, stride, padding, dilation, out_dtype=None):
+    """dw [Co, Ci, KH, KW] of an NHWC conv: dy [N, OH, OW, Co], x [N, H, W, Ci] (Ci, Co % 8 == 0)."""
+    Co, Ci, KH, KW = w_shape
+    N, H, W, C = x.shape
+    assert C == Ci and C % 8 == 0 and Co % 8 == 0 and dy.shape[-1] == Co
+    dy, x = dy.contiguous(), x.contiguous()
+    _, OH, OW, _ = dy.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    od = out_dtype or dy.dtype
+    out = torch.empty(Co, Ci, KH, KW, dtype=od, device=dy.device)
+    M, Nn, K = Co, KH * KW * Ci, N * OH * OW
+    L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+
+    def call(tile, splits, ws):
+        rc = L.pha_conv256_wgrad(_DT[dy.dtype], _ptr(dy), _ptr(x), _ptr(out), _ptr(ws), N, H, W, C, Co, KH, KW,
+                                 sh, sw, ph, pw, dh, dw, int(od == torch.float32), z, tile, splits, st)
+        if rc != 0:
+            raise RuntimeError(f"pha_conv256_wgrad failed ({rc})")
+    _run_tn(("wgrad", dy.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw), M, Nn, K, x.device, call)
+    return out
+
+
+class Conv2dNHWC256(torch.autograd.Function):
+    """NHWC conv2d with forward, dgrad and wgrad all on the 256-tile MFMA kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation):
+        ctx.save_for_backward(x)
+        ctx.weight = weight   # the parameter object itself (a leaf input): its layout cache entries match
+        ctx.conf = (stride, padding, dilation, bias is not None)
+        w_okkc = _wlayout(weight, "fwd", lambda t: t.permute(0, 2, 3, 1).contiguous())
+        return conv256_fwd(x.contiguous(), w_okkc, stride, padding, dilation, bias=bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        weight = ctx.weight
+        stride, padding, dilation, has_bias = ctx.conf
+        gy = gy.contiguous()
+        dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation) if ctx.needs_input_grad[0] else None
+        dw = conv256_wgrad(gy, x, weight.shape, stride, padding, dilation) if ctx.needs_input_grad[1] else None
+        db = gy.float().sum((0, 1, 2)).to(gy.dtype) if has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+def conv2d_nhwc256(x, weight, bias, stride, padding, dilation):
+    return Conv2dNHWC256.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))

@@ -433,6 +433,24 @@ def test_mfma_gemm_epilogue_and_splitk(act, splitk):
     assert (out.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(64, 128, 1000), (512, 384, 4096), (200, 136, 77)])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm256_tn_weight_grad(shape, out_f32):
+    """C = A^T B with K-outer operands (split-K, transposed LDS reads) vs fp32 torch"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    M, N, K = shape
+    torch.manual_seed(2)
+    a = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    b = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+    c = conv_gemm.gemm256_tn(a, b, out_dtype=torch.float32 if out_f32 else None)
+    ref = a.float().t() @ b.float()
+    assert c.dtype == (torch.float32 if out_f32 else torch.bfloat16)
+    assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+    acc = torch.ones(M, N, device="cuda", dtype=c.dtype)
+    conv_gemm.gemm256_tn(a, b, out=acc, accumulate=True)
+    assert (acc.float() - 1 - ref).abs().max() / ref.abs().max() < 1e-2
+
+
 @pytest.mark.parametrize("cfg", [
     # N, H, W, Cin, Cout, k, stride, pad, dil
     (2, 14, 14, 64, 64, 1, 1, 0, 1),

@@ -29,6 +29,14 @@ for s in "$@"; do
     bench_g256)
       timeout -k 10 300 python tools/bench_gemm256.py > $OUT/bench_g256.log 2>&1; rc=$?
       cat $OUT/bench_g256.log | tail -20 ;;
+    prof_resnet_hip)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_resnet_hip
+      PHA_CONV_IMPL=hip timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_resnet_hip -o run --output-format csv -- python3 $ROOT/bench.py --model resnet50 --steps 3 --warmup 2 > $OUT/prof_resnet_hip.log 2>&1; rc=$?
+      tail -2 $OUT/prof_resnet_hip.log ;;
+    bench_g256bwd)
+      timeout -k 10 400 python tools/bench_gemm256.py bwd > $OUT/bench_g256bwd.log 2>&1; rc=$?
+      cat $OUT/bench_g256bwd.log | tail -20 ;;
     prof_g256)
       export TMPDIR=/tmp
       rm -rf $OUT/prof_g256; mkdir -p $OUT/prof_g256
