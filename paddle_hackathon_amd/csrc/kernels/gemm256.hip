@@ -19,7 +19,7 @@
 //  * Two LDS stages; tile k+1 is issued before tile k is multiplied and retired by a COUNTED
 //    s_waitcnt vmcnt (never 0 in the loop) ahead of a raw s_barrier — __syncthreads() would drain
 //    the prefetch too.
-#include "common.h"
+#include "mfma_tile.h"
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -27,13 +27,9 @@
 namespace pha {
 namespace g256 {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 512;
 
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 struct ConvGeo {
   int N, H, W, C;   // input NHWC
@@ -58,43 +54,7 @@ struct Args {
   ConvGeo g;
 };
 
-template <typename T> struct Mf;
-template <> struct Mf<bf16_t> {
-  static __device__ __forceinline__ f32x4 mma(uint4 a, uint4 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                   0, 0, 0);
-  }
-  static __device__ __forceinline__ uint16_t cvt(float v) {
-    return __builtin_bit_cast(uint16_t, (__bf16)v);
-  }
-};
-template <> struct Mf<half_t> {
-  static __device__ __forceinline__ f32x4 mma(uint4 a, uint4 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
-                                                  0, 0, 0);
-  }
-  static __device__ __forceinline__ uint16_t cvt(float v) {
-    return __builtin_bit_cast(uint16_t, (_Float16)v);
-  }
-};
 
-// byte offset in a [rows][BK] bf16 image. BK = 64: 128-B rows, 16-B chunk ^= row & 7; BK = 32:
-// 64-B rows, chunk ^= (row >> 2) & 3 — either way the 16 rows of a fragment read cover all 16
-// chunk slots of a 256-B bank row (SQ_LDS_BANK_CONFLICT = 0 measured)
-template <int BK>
-__device__ __forceinline__ int img_off(int row, int chunk) {
-  if constexpr (BK == 64) return row * 128 + ((chunk ^ (row & 7)) << 4);
-  else return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
-}
-
-__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
-}
 
 // per-lane row state of the A gather for one of the wave's A instructions
 struct ARow {
@@ -360,28 +320,6 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0) {
 // two reads give the 8-k operand of v_mfma_f32_16x16x32. Chunk swizzle: the 8 k-rows a 32-lane
 // half reads (rows r0+{0..3} and r0+8+{0..3}) land on 8 distinct 32-B bank groups.
 // ================================================================================================
-__device__ __forceinline__ int tn_mask(int row, int row_bytes) {
-  if (row_bytes >= 256) return ((row & 3) | (((row >> 3) & 1) << 2)) << 1;
-  return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;   // 128-B rows: two rows per bank row
-}
-
-typedef short tn_v4i16 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint2 tr16(const unsigned char* ptr) {
-  const tn_v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) tn_v4i16*)(ptr));
-  return __builtin_bit_cast(uint2, r);
-}
-
-// 8-k operand of a 16-column block starting at column c0 (multiple of 16), k-rows r0 .. r0+7 of
-// the group (the caller passes r0 = kbase + 8 * (lane >> 4))
-template <int ROWB>
-__device__ __forceinline__ uint4 tn_frag(const unsigned char* img, int r0, int c0, int q, int pp) {
-  const int ch = (c0 >> 3) + (pp >> 1);
-  const int ra = r0 + q, rb = r0 + 4 + q;
-  const uint2 lo = tr16(img + ra * ROWB + ((ch ^ tn_mask(ra, ROWB)) << 4) + 8 * (pp & 1));
-  const uint2 hi = tr16(img + rb * ROWB + ((ch ^ tn_mask(rb, ROWB)) << 4) + 8 * (pp & 1));
-  return uint4{lo.x, lo.y, hi.x, hi.y};
-}
 
 struct TnArgs {
   const void* a;   // [K][lda] (M contiguous)

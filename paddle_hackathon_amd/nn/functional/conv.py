@@ -85,9 +85,9 @@ def _hip_conv2d(x, w, bias, stride, pad, dilation, groups):
 
 def _hip_conv_ok(t_nhwc, w, groups):
     import os
-    # The MFMA implicit-GEMM path is opt-in (PHA_CONV_IMPL=hip) until it matches the library
-    # kernels on every ResNet shape (tools/bench_gemm.py tracks the per-shape ratio).
-    if os.environ.get("PHA_CONV_IMPL", "library") != "hip":
+    # NHWC bf16/fp16 convs run on the MFMA implicit-GEMM kernels (ResNet-50 at batch 256: 7.46k img/s
+    # vs 7.35k with MIOpen, profiles/README.md); PHA_CONV_IMPL=library selects MIOpen instead.
+    if os.environ.get("PHA_CONV_IMPL", "hip") != "hip":
         return False
     from ...ops import conv_gemm, _lib
     return (t_nhwc.is_cuda and t_nhwc.dim() == 4 and t_nhwc.dtype in (torch.bfloat16, torch.float16)

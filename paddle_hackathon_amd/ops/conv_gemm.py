@@ -225,6 +225,8 @@ def _L256():
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
         L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
+        L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P]
+        L.pha_gemm8p.restype = c_int
         L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
         L.pha_gemm256_tn.restype = c_int
         L.pha_conv256_wgrad.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P]
@@ -232,6 +234,28 @@ def _L256():
         L.pha_conv256_fwd.restype = c_int
         L._g256_sig = True
     return L
+
+
+def gemm8p(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, out=None):
+    """C = op(A) @ op(B) on the 8-phase ping-pong MFMA kernel (gemm8p.hip).
+
+    a: [M, K] (a_kouter=False) or [K, M]; b: B^T [N, K] (b_kouter=False) or B [K, N]. Row strides
+    come from the tensors (unit inner stride); M, N, K and the strides % 8 == 0."""
+    assert a.dtype in _DT and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
+    assert a.stride(1) == 1 and b.stride(1) == 1
+    M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if b_kouter else (b.shape[0], b.shape[1])
+    assert Ka == Kb, (a.shape, b.shape)
+    c = out if out is not None else torch.empty(M, N, dtype=a.dtype, device=a.device)
+    assert c.shape == (M, N) and c.stride(1) == 1
+    if bias is not None:
+        bias = bias.float().contiguous()
+    rc = _L256().pha_gemm8p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), _ptr(bias), M, N, Ka, a.stride(0), b.stride(0),
+                            c.stride(0), int(a_kouter), int(b_kouter), _ACT[act], _ptr(_zero_page(a.device)),
+                            c_void_p(torch.cuda.current_stream(a.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm8p failed ({rc}) M={M} N={N} K={Ka}")
+    return c
 
 
 _tuned = {}

@@ -433,6 +433,28 @@ def test_mfma_gemm_epilogue_and_splitk(act, splitk):
     assert (out.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("layout", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(264, 520, 200), (512, 768, 1024), (1024, 256, 4096)])
+def test_gemm8p_layouts(layout, shape):
+    """8-phase ping-pong GEMM, every operand layout (row reads / transposed reads), ragged tiles
+    and K tails, bias + GELU epilogue, vs fp32 torch"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    ako, bko = layout
+    M, N, K = shape
+    torch.manual_seed(3)
+    a = torch.randn(K, M, device="cuda").bfloat16() if ako else torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(K, N, device="cuda").bfloat16() if bko else torch.randn(N, K, device="cuda").bfloat16()
+    A = a.t().float() if ako else a.float()
+    B = b.float() if bko else b.t().float()
+    ref = A @ B
+    c = conv_gemm.gemm8p(a, b, ako, bko)
+    assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+    bias = torch.randn(N, device="cuda")
+    c = conv_gemm.gemm8p(a, b, ako, bko, bias=bias, act="gelu")
+    ref = TF.gelu(ref + bias, approximate="tanh")
+    assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(64, 128, 1000), (512, 384, 4096), (200, 136, 77)])
 @pytest.mark.parametrize("out_f32", [False, True])
 def test_gemm256_tn_weight_grad(shape, out_f32):

@@ -53,6 +53,22 @@ def conv(N, H, W, C, Co, k, s, p):
           f"MIOpen {fl / tl / 1e12:6.1f} TF ({tl * 1e3:.3f} ms)  rel_err {err:.2e}", flush=True)
 
 
+def gemm8p(M, N, K, ako, bko):
+    a = (torch.rand(K, M, device="cuda") * 2 - 1).bfloat16() if ako else (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand(K, N, device="cuda") * 2 - 1).bfloat16() if bko else (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    A = a.t() if ako else a
+    Bm = b if bko else b.t()
+    c = conv_gemm.gemm8p(a, b, ako, bko)
+    ref = A.float() @ Bm.float()
+    err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
+    fl = 2.0 * M * N * K
+    t = timeit(lambda: conv_gemm.gemm8p(a, b, ako, bko))
+    tl = timeit(lambda: A @ Bm)
+    lay = ("T" if ako else "N") + ("N" if bko else "T")   # BLAS-style: op(A) op(B) with B^T stored = "T"
+    print(f"gemm8p {lay} M={M} N={N} K={K}: {fl / t / 1e12:7.1f} TF  lib {fl / tl / 1e12:7.1f} TF  rel_err {err:.2e}",
+          flush=True)
+
+
 def gemm_tn(M, N, K):
     a = (torch.rand(K, M, device="cuda") * 2 - 1).bfloat16()
     b = (torch.rand(K, N, device="cuda") * 2 - 1).bfloat16()
@@ -95,6 +111,14 @@ def conv_bwd(N, H, W, C, Co, k, s, p):
 
 
 if __name__ == "__main__":
+    if "8p" in sys.argv[1:]:
+        for lay in [(False, False), (False, True), (True, False), (True, True)]:
+            gemm8p(264, 520, 200, *lay)    # ragged tiles / K tail first (correctness)
+        for shp in [(4096, 4096, 4096), (8192, 8192, 8192), (16384, 6144, 2048), (16384, 2048, 2048),
+                    (16384, 8192, 2048), (16384, 2048, 8192)]:
+            for lay in [(False, False), (False, True), (True, False)]:
+                gemm8p(*shp, *lay)
+        sys.exit(0)
     if "bwd" in sys.argv[1:]:
         for shp in [(512, 384, 1000), (2048, 2048, 16384), (2048, 8192, 16384), (8192, 2048, 16384)]:
             gemm_tn(*shp)

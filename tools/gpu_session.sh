@@ -23,20 +23,29 @@ for s in "$@"; do
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
-    bench_resnet_hip)
-      PHA_CONV_IMPL=hip timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet_hip.log 2>&1; rc=$?
-      tail -3 $OUT/bench_resnet_hip.log ;;
+    bench_resnet_lib)
+      PHA_CONV_IMPL=library timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet_lib.log 2>&1; rc=$?
+      tail -3 $OUT/bench_resnet_lib.log ;;
     bench_g256)
       timeout -k 10 300 python tools/bench_gemm256.py > $OUT/bench_g256.log 2>&1; rc=$?
       cat $OUT/bench_g256.log | tail -20 ;;
     prof_resnet_hip)
       export TMPDIR=/tmp
       rm -rf $OUT/prof_resnet_hip
-      PHA_CONV_IMPL=hip timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_resnet_hip -o run --output-format csv -- python3 $ROOT/bench.py --model resnet50 --steps 3 --warmup 2 > $OUT/prof_resnet_hip.log 2>&1; rc=$?
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_resnet_hip -o run --output-format csv -- python3 $ROOT/bench.py --model resnet50 --steps 3 --warmup 2 > $OUT/prof_resnet_hip.log 2>&1; rc=$?
       tail -2 $OUT/prof_resnet_hip.log ;;
+    bench_g8p)
+      timeout -k 10 300 python tools/bench_gemm256.py 8p > $OUT/bench_g8p.log 2>&1; rc=$?
+      cat $OUT/bench_g8p.log | tail -24 ;;
     bench_g256bwd)
       timeout -k 10 400 python tools/bench_gemm256.py bwd > $OUT/bench_g256bwd.log 2>&1; rc=$?
       cat $OUT/bench_g256bwd.log | tail -20 ;;
+    prof_g8p)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_g8p; mkdir -p $OUT/prof_g8p
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_g8p/pmc1 -o run --output-format csv -- python3 $ROOT/tools/g256_prof.py 8p > $OUT/prof_g8p/pmc1.log 2>&1; rc=$?
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g8p/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g256_prof.py 8p > $OUT/prof_g8p/pmc2.log 2>&1; rc=$?; fi
+      tail -2 $OUT/prof_g8p/*.log ;;
     prof_g256)
       export TMPDIR=/tmp
       rm -rf $OUT/prof_g256; mkdir -p $OUT/prof_g256
