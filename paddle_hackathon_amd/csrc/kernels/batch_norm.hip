@@ -129,7 +129,8 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   float s1, s2;
   sum_partials(part, nblk, C, c, s1, s2, sm);
   if (threadIdx.x >= 64 || c >= C) return;
-  const float x0 = dt == kF32 ? ((const float*)x)[c]
+  // x == nullptr: unshifted partial sums (from the producing convolution's epilogue)
+  const float x0 = !x ? 0.f : dt == kF32 ? ((const float*)x)[c]
                    : dt == kBF16 ? bf16_to_f32(((const uint16_t*)x)[c]) : (float)((const _Float16*)x)[c];
   const float n = (float)M;
   const float dm = s1 / n;
@@ -319,15 +320,20 @@ PHA_API int pha_bn_num_blocks(long M, int C) {
 PHA_API int pha_bn_fwd_train(int dt, const void* x, const void* res, void* y, long M, int C, const float* w,
                              const float* b, float* run_mean, float* run_var, float* save_mean, float* save_istd,
                              float* scale, float* shift, float* part, float eps, float momentum, int relu,
-                             hipStream_t s) {
+                             const float* ext_part, int ext_rows, hipStream_t s) {
   if (C % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
-  int tiles;
-  const int nb = grid_rows(M, C, &tiles);
-  PHA_DISPATCH_T(dt, T, {
-    hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)x, M, C, part);
-  });
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, nb, C, M, x, dt, eps, momentum, w,
-                     b, run_mean, run_var, save_mean, save_istd, scale, shift);
+  if (ext_part) {   // [ext_rows][2][C] unshifted sums computed by the producer of x
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ext_part, ext_rows, C, M, nullptr, dt,
+                       eps, momentum, w, b, run_mean, run_var, save_mean, save_istd, scale, shift);
+  } else {
+    int tiles;
+    const int nb = grid_rows(M, C, &tiles);
+    PHA_DISPATCH_T(dt, T, {
+      hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)x, M, C, part);
+    });
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, nb, C, M, x, dt, eps, momentum,
+                       w, b, run_mean, run_var, save_mean, save_istd, scale, shift);
+  }
   const long nvec = M * (C / 8);
   const int ge = grid_elem(nvec);
   PHA_DISPATCH_T(dt, T, {

@@ -52,6 +52,7 @@ struct Args {
   int act;
   const void* zero;   // >= 16 B of zeros
   ConvGeo g;
+  float* stats;       // optional [tiles_m][2][N]: per-tile column sum / sum of squares of the stored C
 };
 
 
@@ -262,6 +263,32 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
       for (int t = 0; t < 8 && n + t < N; ++t) reinterpret_cast<uint16_t*>(C)[m * p.ldc + n + t] = e[t];
     }
   }
+  if (p.stats) {
+    // batch-norm statistics of this tile (the BN that follows a convolution then skips its own
+    // read of the output): column sums over the tile's rows of the values as stored (rounded to T)
+    constexpr int G = NT / BN;                          // row groups
+    const int c = tid % BN, rg = tid / BN;
+    const int rows = (int)min((long)BM, M - m0);
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = rg; r < rows; r += G) {
+      const float v = Cvt<T>::ld(reinterpret_cast<const T*>(ct + r * CROW), c);
+      s1 += v;
+      s2 = fmaf(v, v, s2);
+    }
+    __syncthreads();                                    // C tile fully stored: reuse the LDS
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = s1;
+    red[NT + tid] = s2;
+    __syncthreads();
+    if (rg == 0 && n0 + c < N) {
+      for (int g2 = 1; g2 < G; ++g2) {
+        s1 += red[g2 * BN + c];
+        s2 += red[NT + g2 * BN + c];
+      }
+      p.stats[(long)tm * 2 * N + n0 + c] = s1;
+      p.stats[(long)tm * 2 * N + N + n0 + c] = s2;
+    }
+  }
 }
 
 // BK = 64 (one tile in flight, half the barriers) suits compute-bound GEMMs; BK = 32 (three tiles
@@ -269,7 +296,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 // tile: index into cands (-1 = heuristic), bk: 32 | 64 (0 = heuristic); the host autotuner
 // (ops/conv_gemm.py) times the candidates once per shape and passes its choice
 template <typename T, bool CONV>
-int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0) {
+int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_rows = nullptr) {
   if (bk != 32 && bk != 64) bk = (CONV || a.K <= 1024) ? 32 : 64;
   // tile shape: the fewest "CU rounds x tile work / tile efficiency" (a 784-tile grid on 256 CUs
   // wastes a quarter of the chip in its last round; small tiles pay in operand re-reads)
@@ -294,6 +321,7 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0) {
   }
   if (tile >= 0 && tile < 6) best = tile;
   const int bm = cands[best][0], bn = cands[best][1];
+  if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;
     const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
@@ -587,7 +615,7 @@ PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const
                            long lda, long ldb, long ldc, int act, const void* zero16, int tile, int bk,
                            hipStream_t stream) {
   if (K % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}};
+  g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}, nullptr};
   if (dt == kBF16) return g256::launch<bf16_t, false>(p, stream, tile, bk);
   if (dt == kF16) return g256::launch<half_t, false>(p, stream, tile, bk);
   return (int)hipErrorInvalidValue;
@@ -595,9 +623,12 @@ PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const
 
 // NHWC conv forward: y[N*OH*OW, Cout] = im2col(x) . w^T, w as [Cout][KH][KW][Cin], Cin % 8 == 0.
 // oremap (host int[9], may be null): strided output rows and explicit output size, see ConvGeo.
+// stats (may be null, >= ceil(M/128)*2*Cout floats): per-row-tile channel sum / sum of squares of y
+// for a following batch norm; *stats_rows receives the number of row tiles written.
 PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H, int W,
                             int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
-                            const void* zero16, int tile, int bk, const int* oremap, hipStream_t stream) {
+                            const void* zero16, int tile, int bk, const int* oremap, float* stats, int* stats_rows,
+                            hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
                   KH, KW, sh, sw, ph, pw, dh, dw, 0, 0, 0, 0, 0, 0, 0};
@@ -606,9 +637,10 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
     g.OH = oremap[6]; g.OW = oremap[7]; g.ozero = oremap[8];
   }
   const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
-  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g};
-  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk);
-  if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk);
+  if (stats && oremap) return (int)hipErrorInvalidValue;
+  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g, stats};
+  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, stats_rows);
+  if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, stats_rows);
   return (int)hipErrorInvalidValue;
 }
 

@@ -17,7 +17,7 @@ other shapes use the portable path in nn.functional.conv.
 from __future__ import annotations
 
 import ctypes
-from ctypes import c_int, c_long, c_void_p
+from ctypes import byref, c_int, c_long, c_void_p
 
 import torch
 
@@ -224,7 +224,7 @@ def _L256():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
-        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P]
         L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P]
         L.pha_gemm8p.restype = c_int
         L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
@@ -309,12 +309,14 @@ def gemm256_nt(a, bt, bias=None, act=None, out=None):
     return c
 
 
-def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None):
+def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None, bn_stats=False):
     """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout].
 
     ``remap = (oh0, ow0, osh, osw, OH, OW[, zero_rest])`` computes an OH x OW output and stores pixel
     (oh, ow) at (oh0 + oh*osh, ow0 + ow*osw) of ``out`` — one phase of a strided convolution's dgrad;
-    ``zero_rest`` (with oh0 = ow0 = 0) also zero-fills the other pixels of each stride cell."""
+    ``zero_rest`` (with oh0 = ow0 = 0) also zero-fills the other pixels of each stride cell.
+    ``bn_stats``: the epilogue also writes per-row-tile channel sums / sums of squares of y, attached
+    as ``y._pha_bn_stats = (partials, rows, y._version)`` for the batch norm that consumes y."""
     assert x.dtype in _DT and w_okkc.dtype == x.dtype and x.is_contiguous() and w_okkc.is_contiguous()
     N, H, W, C = x.shape
     Co, KH, KW, Cw = w_okkc.shape
@@ -339,13 +341,19 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
     if bias is not None:
         bias = bias.float().contiguous()
     L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    part, rows = None, c_int(0)
+    if bn_stats and rm is None:
+        part = torch.empty(-(-(N * OH * OW) // 128) * 2 * Co, dtype=torch.float32, device=x.device)
 
     def run(tile, bk):
         rc = L.pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
-                               sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, rm, st)
+                               sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, rm, _ptr(part),
+                               byref(rows) if part is not None else None, st)
         if rc != 0:
             raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
     run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw, OH, OW), run))
+    if part is not None:
+        y._pha_bn_stats = (part, rows.value, y._version)
     return y
 
 
@@ -522,6 +530,11 @@ def conv256_wgrad(dy, x, w_shape, stride, padding, dilation, out_dtype=None):
     return out
 
 
+def _bn_stats_on():
+    import os
+    return os.environ.get("PHA_CONV_BN_STATS", "1") != "0"
+
+
 class Conv2dNHWC256(torch.autograd.Function):
     """NHWC conv2d with forward, dgrad and wgrad all on the 256-tile MFMA kernels."""
 
@@ -531,7 +544,10 @@ class Conv2dNHWC256(torch.autograd.Function):
         ctx.weight = weight   # the parameter object itself (a leaf input): its layout cache entries match
         ctx.conf = (stride, padding, dilation, bias is not None)
         w_okkc = _wlayout(weight, "fwd", lambda t: t.permute(0, 2, 3, 1).contiguous())
-        return conv256_fwd(x.contiguous(), w_okkc, stride, padding, dilation, bias=bias)
+        # training: the epilogue also emits batch-norm partial statistics of y (ResNet-style
+        # conv -> BN pairs then skip the BN's own statistics pass over y); PHA_CONV_BN_STATS=0 disables
+        stats = _bn_stats_on() and bias is None
+        return conv256_fwd(x.contiguous(), w_okkc, stride, padding, dilation, bias=bias, bn_stats=stats)
 
     @staticmethod
     def backward(ctx, gy):

@@ -347,7 +347,11 @@ class _BatchNormNHWC(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
         w32 = weight.float() if weight is not None else torch.ones(x.shape[-1], device=x.device)
         b32 = bias.float() if bias is not None else None
-        y, mean, istd = _hip.bn_fwd_train(x, w32, b32, running_mean, running_var, eps, momentum, residual, relu)
+        ext = getattr(x, "_pha_bn_stats", None)   # partial sums from the producing conv's epilogue
+        if ext is not None and (ext[2] != x._version or ext[0].device != x.device or ext[1] <= 0):
+            ext = None
+        y, mean, istd = _hip.bn_fwd_train(x, w32, b32, running_mean, running_var, eps, momentum, residual, relu,
+                                          ext_stats=None if ext is None else (ext[0], ext[1]))
         ctx.save_for_backward(x, y if relu else None, w32, mean, istd)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.wdt = None if weight is None else weight.dtype

@@ -43,7 +43,7 @@ def _L():
             "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
             "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
             "pha_bn_num_blocks": [LG, I],
-            "pha_bn_fwd_train": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, F, F, I, P],
+            "pha_bn_fwd_train": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, F, F, I, P, I, P],
             "pha_bn_apply": [I, P, P, P, LG, I, P, P, I, P],
             "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P],
             "pha_chunk_size": [],
@@ -121,8 +121,10 @@ def bn_supported(x, C):
     return x.is_cuda and x.dtype in _DT and x.is_contiguous() and C % 8 == 0 and x.numel() > 0 and x.shape[-1] == C
 
 
-def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=None, relu=False):
-    """x: [..., C] contiguous (NHWC). Returns y, save_mean, save_istd. Updates running stats in place."""
+def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=None, relu=False, ext_stats=None):
+    """x: [..., C] contiguous (NHWC). Returns y, save_mean, save_istd. Updates running stats in place.
+    ext_stats = (partials [rows][2][C] fp32, rows): unshifted channel sums / sums of squares of x
+    already computed by x's producer (the conv epilogue) — the statistics pass over x is skipped."""
     C = x.shape[-1]
     M = x.numel() // C
     assert bn_supported(x, C) and w.dtype == torch.float32 and w.numel() == C
@@ -136,7 +138,9 @@ def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=Non
     y = torch.empty_like(x)
     _check(L.pha_bn_fwd_train(_DT[x.dtype], _ptr(x), _ptr(residual), _ptr(y), M, C, _ptr(w), _ptr(b),
                               _ptr(running_mean), _ptr(running_var), _ptr(stats[0]), _ptr(stats[1]), _ptr(stats[2]),
-                              _ptr(stats[3]), _ptr(part), float(eps), float(momentum), int(relu), _stream(x)),
+                              _ptr(stats[3]), _ptr(part), float(eps), float(momentum), int(relu),
+                              _ptr(ext_stats[0]) if ext_stats else None, int(ext_stats[1]) if ext_stats else 0,
+                              _stream(x)),
            "bn_fwd_train")
     return y, stats[0], stats[1]
 

@@ -433,6 +433,30 @@ def test_mfma_gemm_epilogue_and_splitk(act, splitk):
     assert (out.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+def test_conv_epilogue_bn_stats():
+    """the conv forward epilogue's batch-norm partial sums match the output, and the BN that
+    consumes them gives the same normalisation / running stats as its own statistics pass"""
+    from paddle_hackathon_amd.ops import conv_gemm, fused
+    torch.manual_seed(4)
+    x = torch.randn(4, 20, 20, 64, device="cuda").bfloat16()
+    w = (torch.randn(128, 64, 3, 3, device="cuda") * 0.05).bfloat16()
+    y = conv_gemm.conv2d_nhwc256(x, w, None, (1, 1), (1, 1), (1, 1))
+    part, rows, ver = y._pha_bn_stats
+    assert ver == y._version and rows == -(-y.numel() // 128 // 128) or rows > 0
+    s = part[: rows * 2 * 128].view(rows, 2, 128).double().sum(0)
+    yf = y.double().reshape(-1, 128)
+    assert torch.allclose(s[0], yf.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+    g, b = torch.rand(128, device="cuda") + 0.5, torch.randn(128, device="cuda")
+    rm1, rv1 = torch.zeros(128, device="cuda"), torch.ones(128, device="cuda")
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    out1 = fused.batch_norm_train(y, g, b, rm1, rv1, 0.9, 1e-5, -1, relu=True)
+    y2 = y.clone()   # no partials attached: the BN's own statistics pass
+    out2 = fused.batch_norm_train(y2, g, b, rm2, rv2, 0.9, 1e-5, -1, relu=True)
+    assert (out1.float() - out2.float()).abs().max() < 2e-2
+    assert torch.allclose(rm1, rm2, atol=1e-4) and torch.allclose(rv1, rv2, rtol=1e-3)
+
+
 @pytest.mark.parametrize("layout", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("shape", [(264, 520, 200), (512, 768, 1024), (1024, 256, 4096)])
 def test_gemm8p_layouts(layout, shape):
