@@ -27,6 +27,8 @@
 //  B1(t+1), A1(t+1), A0(t+2), B0(t+2) — each half-tile is retired by the vmcnt(8) of the phase
 //  before its first read.
 #include "mfma_tile.h"
+#include <cstdlib>
+#include <type_traits>
 
 namespace pha {
 namespace g8p {
@@ -52,7 +54,9 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-template <typename T, bool AKO, bool BKO>
+// V: schedule experiments (0 = the schedule above; bit 0: no wave-row stagger, bit 1: no setprio,
+// bit 2: fragment reads retired (lgkmcnt(0)) before the barrier instead of after it)
+template <typename T, bool AKO, bool BKO, int V = 0>
 __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
   constexpr int HALF = 16384, BUF = 4 * HALF;
   constexpr int CROW = 256 * 2 + 16;
@@ -169,15 +173,20 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto mfma = [&](f32x4 (&c)[4][2], const uint4 (&af)[4][2], const uint4 (&bf)[2][2]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(V & 4)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(V & 2)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) c[i][j] = Mf<T>::mma(af[i][kh], bf[j][kh], c[i][j]);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(V & 2)) __builtin_amdgcn_s_setprio(0);
+  };
+  auto wait_bar = [&]() {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (V & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
   };
 
   // prologue: A0 B0 B1 A1 of tile 0, A0 B0 of tile 1; retire tile 0's A0 and B0
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
   issue(2, 1, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   bar();
-  if (wr == 1) bar();   // the ping-pong stagger
+  if (!(V & 1) && wr == 1) bar();   // the ping-pong stagger
 
   uint4 af[4][2], b0[2][2], b1[2][2];
   for (int t = 0; t < nk; ++t) {
@@ -199,32 +208,28 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
     readA(img + 0 * HALF, af);
     readB(img + 2 * HALF, b0);
     issue(3, t + 1, buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    bar();
+    wait_bar();
     mfma(acc[0][0], af, b0);
     bar();
     // phase 1: quadrant (0, 1)
     readB(img + 3 * HALF, b1);
     issue(1, t + 1, buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    bar();
+    wait_bar();
     mfma(acc[0][1], af, b1);
     bar();
     // phase 2: quadrant (1, 1)
     readA(img + 1 * HALF, af);
     issue(0, t + 2, buf);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    bar();
+    wait_bar();
     mfma(acc[1][1], af, b1);
     bar();
     // phase 3: quadrant (1, 0)
     issue(2, t + 2, buf);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    bar();
+    wait_bar();
     mfma(acc[1][0], af, b0);
     bar();
   }
-  if (wr == 0) bar();
+  if (!(V & 1) && wr == 0) bar();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
 
@@ -270,6 +275,21 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
 template <typename T>
 int launch(const Args& a, int ako, int bko, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  static int var = -1;
+  if (var < 0) {
+    const char* e = getenv("PHA_G8P_VAR");
+    var = e ? atoi(e) : 0;
+  }
+  if (std::is_same<T, bf16_t>::value && !ako && var > 0) {
+#define G8P_VAR(v_)                                                                                      \
+    if (var == v_) {                                                                                     \
+      if (bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, true, v_>), dim3(grid), dim3(512), 0, st, a);  \
+      else hipLaunchKernelGGL((gemm8p_kernel<T, false, false, v_>), dim3(grid), dim3(512), 0, st, a);     \
+      return (int)hipGetLastError();                                                                     \
+    }
+    G8P_VAR(1) G8P_VAR(2) G8P_VAR(4) G8P_VAR(6)
+#undef G8P_VAR
+  }
   if (!ako && !bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, false>), dim3(grid), dim3(512), 0, st, a);
   else if (!ako && bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, true>), dim3(grid), dim3(512), 0, st, a);
   else if (ako && !bko) hipLaunchKernelGGL((gemm8p_kernel<T, true, false>), dim3(grid), dim3(512), 0, st, a);

@@ -25,6 +25,7 @@ from .. import nn
 from ..nn import functional as F
 from ..nn import initializer as I
 from .. import ops as _ops
+from ..ops import conv_gemm as _cg
 
 
 @dataclass
@@ -112,7 +113,7 @@ class GPTMLP(nn.Layer):
             self.linear2 = nn.Linear(f, h, weight_attr=_w_attr(cfg, out_scale))
 
     def forward(self, x):
-        h = torch.matmul(x._t, self.linear1.weight._t)
+        h = _cg.matmul_kn(x._t, self.linear1.weight._t)
         h = _ops.bias_gelu(h, self.linear1.bias._t, approximate=True)
         return self.linear2(_wrap(h))
 
@@ -207,7 +208,7 @@ class GPTForPretraining(nn.Layer):
         if self.cfg.tensor_parallel_degree > 1:
             from ..parallel.mp_layers import _c_identity
             h = _c_identity(h)
-        return _wrap(torch.matmul(h._t, w._t.t()))
+        return _wrap(_cg.matmul_nt(h._t, w._t))
 
     def forward(self, input_ids, labels=None, loss_mask=None, position_ids=None):
         h = self.gpt(input_ids, position_ids)

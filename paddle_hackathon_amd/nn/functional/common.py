@@ -24,8 +24,12 @@ def _t(x):
 
 
 def linear(x, weight, bias=None, name=None):
-    """y = x @ W + b with Paddle's [in, out] weight layout (hipBLASLt GEMM + fused bias epilogue)."""
+    """y = x @ W + b with Paddle's [in, out] weight layout (hipBLASLt GEMM + fused bias epilogue;
+    PHA_MATMUL_IMPL=hip: the 8-phase MFMA GEMM of gemm8p.hip for forward and both gradients)."""
     xt, wt = x._t, weight._t
+    from ...ops import conv_gemm as _cg
+    if _cg.linear_ok(xt, wt):
+        return _w(_cg.linear(xt, wt, None if bias is None else bias._t))
     if bias is not None and xt.dim() >= 2:
         b = bias._t
         out = torch.addmm(b, xt.reshape(-1, xt.shape[-1]), wt)
@@ -51,7 +55,8 @@ def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, nam
 def linear_bias_gelu(x, weight, bias, approximate=False):
     """gelu(x @ W + b): GEMM on hipBLASLt, bias+GELU fused in one HIP pass."""
     xt = x._t
-    h = torch.matmul(xt, weight._t)
+    from ...ops import conv_gemm as _cg
+    h = _cg.linear(xt, weight._t) if _cg.linear_ok(xt, weight._t) else torch.matmul(xt, weight._t)
     return _w(_ops.bias_gelu(h, bias._t, approximate))
 
 

@@ -563,3 +563,77 @@ class Conv2dNHWC256(torch.autograd.Function):
 
 def conv2d_nhwc256(x, weight, bias, stride, padding, dilation):
     return Conv2dNHWC256.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))
+
+
+class LinearHip(torch.autograd.Function):
+    """y = x @ W (+ b), Paddle [in, out] weight, on the 8-phase MFMA GEMM for all three products:
+    forward NN (W k-outer), dX = dY W^T (NT), dW = X^T dY (both operands k-outer)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b):
+        ctx.save_for_backward(x2d, w)
+        ctx.has_b = b is not None
+        return gemm8p(x2d, w, a_kouter=False, b_kouter=True, bias=b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = gemm8p(gy, w, a_kouter=False, b_kouter=False) if ctx.needs_input_grad[0] else None
+        dw = gemm8p(x2d, gy, a_kouter=True, b_kouter=True) if ctx.needs_input_grad[1] else None
+        db = gy.float().sum(0).to(gy.dtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear_ok(x, w):
+    """shapes / dtypes the own-GEMM linear path takes (PHA_MATMUL_IMPL=hip)"""
+    import os
+    if os.environ.get("PHA_MATMUL_IMPL", "library") != "hip":
+        return False
+    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype and w.dim() == 2):
+        return False
+    K, N = w.shape
+    M = x.numel() // max(1, x.shape[-1])
+    return (x.shape[-1] == K and M % 8 == 0 and K % 8 == 0 and N % 8 == 0 and M * K < 2 ** 32 and M * N < 2 ** 32
+            and K * N < 2 ** 32 and _lib.native_available())
+
+
+def linear(x, w, b=None):
+    x2d = x.reshape(-1, x.shape[-1])
+    if not x2d.is_contiguous():
+        x2d = x2d.contiguous()
+    y = LinearHip.apply(x2d, w, b)
+    return y.reshape(list(x.shape[:-1]) + [w.shape[1]])
+
+
+class MatmulNTHip(torch.autograd.Function):
+    """y = x @ w^T with w [N, K] (tied output embedding / logits) on gemm8p: forward NT,
+    dX = dY w (B k-outer), dW = dY^T X (both k-outer)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w):
+        ctx.save_for_backward(x2d, w)
+        return gemm8p(x2d, w, a_kouter=False, b_kouter=False)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = gemm8p(gy, w, a_kouter=False, b_kouter=True) if ctx.needs_input_grad[0] else None
+        dw = gemm8p(gy, x2d, a_kouter=True, b_kouter=True) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def matmul_nt(x, w):
+    """x @ w^T, own GEMM when PHA_MATMUL_IMPL=hip admits the shapes, torch otherwise"""
+    if linear_ok(x, w.t()):
+        x2d = x.reshape(-1, x.shape[-1]).contiguous()
+        return MatmulNTHip.apply(x2d, w).reshape(list(x.shape[:-1]) + [w.shape[0]])
+    return torch.matmul(x, w.t())
+
+
+def matmul_kn(x, w):
+    """x @ w with w [K, N] (Paddle linear weight), own GEMM when admitted"""
+    if linear_ok(x, w):
+        return linear(x, w)
+    return torch.matmul(x, w)

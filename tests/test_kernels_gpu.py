@@ -433,6 +433,37 @@ def test_mfma_gemm_epilogue_and_splitk(act, splitk):
     assert (out.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+def test_linear_own_gemm_fwd_bwd(monkeypatch):
+    """PHA_MATMUL_IMPL=hip: linear (x @ W + b) and tied-logits (x @ E^T) forward and both
+    gradients on gemm8p vs fp32 torch"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    monkeypatch.setenv("PHA_MATMUL_IMPL", "hip")
+    torch.manual_seed(5)
+    x = torch.randn(2, 136, 256, device="cuda").bfloat16().requires_grad_(True)
+    w = (torch.randn(256, 392, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(392, device="cuda").bfloat16().requires_grad_(True)
+    assert conv_gemm.linear_ok(x, w)
+    y = conv_gemm.linear(x, w, b)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr + br
+    gy = torch.randn_like(yr)
+    y.backward(gy.bfloat16())
+    yr.backward(gy)
+    rel = lambda a, r: ((a.float() - r).abs().max() / r.abs().max()).item()
+    assert rel(y, yr) < 1e-2 and rel(x.grad, xr.grad) < 1e-2 and rel(w.grad, wr.grad) < 1e-2
+    assert rel(b.grad, br.grad) < 1e-2
+    e = (torch.randn(504, 256, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    x.grad = None
+    z = conv_gemm.matmul_nt(x, e)
+    er = e.detach().float().requires_grad_(True)
+    xr.grad = None
+    zr = xr @ er.t()
+    gz = torch.randn_like(zr)
+    z.backward(gz.bfloat16())
+    zr.backward(gz)
+    assert rel(z, zr) < 1e-2 and rel(x.grad, xr.grad) < 1e-2 and rel(e.grad, er.grad) < 1e-2
+
+
 def test_conv_epilogue_bn_stats():
     """the conv forward epilogue's batch-norm partial sums match the output, and the BN that
     consumes them gives the same normalisation / running stats as its own statistics pass"""

@@ -111,6 +111,12 @@ def conv_bwd(N, H, W, C, Co, k, s, p):
 
 
 if __name__ == "__main__":
+    if "8pvar" in sys.argv[1:]:
+        gemm8p(264, 520, 200, False, True)
+        for shp in [(8192, 8192, 8192), (16384, 6144, 2048)]:
+            for lay in [(False, False), (False, True)]:
+                gemm8p(*shp, *lay)
+        sys.exit(0)
     if "8p" in sys.argv[1:]:
         for lay in [(False, False), (False, True), (True, False), (True, True)]:
             gemm8p(264, 520, 200, *lay)    # ragged tiles / K tail first (correctness)

@@ -20,6 +20,9 @@ for s in "$@"; do
     bench_bert)
       timeout -k 10 400 python bench.py --model bert-base --steps 10 --warmup 3 > $OUT/bench_bert.log 2>&1; rc=$?
       tail -3 $OUT/bench_bert.log ;;
+    bench_gpt_hipmm)
+      PHA_MATMUL_IMPL=hip timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $OUT/bench_gpt_hipmm.log 2>&1; rc=$?
+      tail -3 $OUT/bench_gpt_hipmm.log ;;
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
@@ -37,6 +40,8 @@ for s in "$@"; do
     bench_g8p)
       timeout -k 10 300 python tools/bench_gemm256.py 8p > $OUT/bench_g8p.log 2>&1; rc=$?
       cat $OUT/bench_g8p.log | tail -24 ;;
+    g8p_var)
+      rc=0; for v in 0 1 2 4 6; do PHA_G8P_VAR=$v timeout -k 10 120 python tools/bench_gemm256.py 8pvar > $OUT/g8p_var$v.log 2>&1 || break; echo "var $v"; tail -4 $OUT/g8p_var$v.log; done ;;
     bench_g256bwd)
       timeout -k 10 400 python tools/bench_gemm256.py bwd > $OUT/bench_g256bwd.log 2>&1; rc=$?
       cat $OUT/bench_g256bwd.log | tail -20 ;;
