@@ -129,7 +129,8 @@ def main():
     if rank == 0:
         n_params = sum(p._t.numel() for p in (model._layers if hasattr(model, "_layers") else model).parameters())
         out = {
-            "metric": "tokens/sec GPT-3-1.3B fleet DP (bf16, whole job)",
+            "metric": ("tokens/sec GPT-3-1.3B fleet DP (bf16, whole job)" if a.model == "gpt3-1.3b" else
+                       f"tokens/sec {a.model} (bf16, whole job)"),
             "baseline_metric": BASELINE_METRIC,
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

@@ -120,8 +120,9 @@ def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
             and (bias is None or bias.dtype == weight.dtype)):
         return _LayerNorm.apply(x, weight.reshape(-1), None if bias is None else bias.reshape(-1), float(eps))
     ns = list(normalized_shape)
-    return TF.layer_norm(x, ns, None if weight is None else weight.reshape(ns),
-                         None if bias is None else bias.reshape(ns), eps)
+    # torch's kernel wants one dtype: fp32 master LN weights (AMP O2) are cast to the input's
+    return TF.layer_norm(x, ns, None if weight is None else weight.reshape(ns).to(x.dtype),
+                         None if bias is None else bias.reshape(ns).to(x.dtype), eps)
 
 
 class _AddLayerNorm(torch.autograd.Function):

@@ -23,6 +23,9 @@ for s in "$@"; do
     bench_gpt_hipmm)
       PHA_MATMUL_IMPL=hip timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $OUT/bench_gpt_hipmm.log 2>&1; rc=$?
       tail -3 $OUT/bench_gpt_hipmm.log ;;
+    bench_gpt13b)
+      timeout -k 10 600 python bench.py --model gpt3-13b --micro-batch 2 --recompute --steps 3 --warmup 1 > $OUT/bench_gpt13b.log 2>&1; rc=$?
+      tail -4 $OUT/bench_gpt13b.log ;;
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
