@@ -117,6 +117,37 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
   }
 }
 
+// First stage for many partial rows: block (channel block, g) sums rows [g*rows_per, +rows_per)
+// of `part` into out[g][2][C] (64 channels x 16 slices, four independent accumulators per thread
+// so the loads overlap), so the finalize kernels read <= 64 rows instead of thousands.
+__global__ __launch_bounds__(1024) void bn_partial_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                 int rows_per, float* __restrict__ out) {
+  __shared__ float sm[16][2][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * rows_per, r1 = min(nblk, r0 + rows_per);
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int k = r0 + sl, u = 0;
+    for (; k < r1; k += 16, u = (u + 1) & 3) {
+      a[u] += part[(long)k * 2 * C + c];
+      b[u] += part[(long)k * 2 * C + C + c];
+    }
+  }
+  sm[sl][0][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  sm[sl][1][cl] = (b[0] + b[1]) + (b[2] + b[3]);
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k < 16; ++k) {
+      sa += sm[k][0][cl];
+      sb += sm[k][1][cl];
+    }
+    out[(long)blockIdx.y * 2 * C + c] = sa;
+    out[(long)blockIdx.y * 2 * C + C + c] = sb;
+  }
+}
+
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int nblk, int C, long M,
                                                            const void* __restrict__ x, int dt, float eps,
                                                            float momentum, const float* __restrict__ w,
@@ -306,12 +337,24 @@ int grid_elem(long nvec) {
   return (int)(b > 0 ? b : 1);
 }
 
+// fold `nblk` partial rows to <= 64 in `scratch` (>= 64 x 2 x C floats) when there are many
+const float* fold_rows(const float* part, int& nblk, int C, float* scratch, hipStream_t s) {
+  if (nblk <= 64) return part;
+  const int G = min(64, (nblk + 31) / 32);
+  const int rows_per = (nblk + G - 1) / G;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, G), dim3(1024), 0, s, part, nblk, C, rows_per,
+                     scratch);
+  nblk = (nblk + rows_per - 1) / rows_per;
+  return scratch;
+}
+
 }  // namespace
 }  // namespace pha
 
 using namespace pha;
 
-// Number of row blocks the stats / reduce kernels use (host sizes the partial buffer).
+// Number of row blocks the stats / reduce kernels use; the host sizes the partial buffer for
+// (this + 64) rows of [2][C] floats (the tail takes the folded first-stage sums).
 PHA_API int pha_bn_num_blocks(long M, int C) {
   int tiles;
   return grid_rows(M, C, &tiles);
@@ -322,16 +365,20 @@ PHA_API int pha_bn_fwd_train(int dt, const void* x, const void* res, void* y, lo
                              float* scale, float* shift, float* part, float eps, float momentum, int relu,
                              const float* ext_part, int ext_rows, hipStream_t s) {
   if (C % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
+  // part: >= (pha_bn_num_blocks + 64) x 2 x C floats; its tail holds the folded rows
   if (ext_part) {   // [ext_rows][2][C] unshifted sums computed by the producer of x
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, ext_part, ext_rows, C, M, nullptr, dt,
+    int rows = ext_rows;
+    const float* pp = fold_rows(ext_part, rows, C, part, s);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, pp, rows, C, M, nullptr, dt,
                        eps, momentum, w, b, run_mean, run_var, save_mean, save_istd, scale, shift);
   } else {
     int tiles;
-    const int nb = grid_rows(M, C, &tiles);
+    int nb = grid_rows(M, C, &tiles);
     PHA_DISPATCH_T(dt, T, {
       hipLaunchKernelGGL((bn_stats_kernel<T>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)x, M, C, part);
     });
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, nb, C, M, x, dt, eps, momentum,
+    const float* pp = fold_rows(part, nb, C, part + (long)grid_rows(M, C, &tiles) * 2 * C, s);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, pp, nb, C, M, x, dt, eps, momentum,
                        w, b, run_mean, run_var, save_mean, save_istd, scale, shift);
   }
   const long nvec = M * (C / 8);
@@ -389,7 +436,9 @@ PHA_API int pha_bn_bwd(int dt, const void* dy, const void* x, const void* y, lon
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)dy,
                          (const T*)x, (const T*)y, save_mean, M, C, part);
   });
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, part, nb, C, 1.f / (float)M, w,
+  int rows = nb;
+  const float* pp = fold_rows(part, rows, C, part + (long)nb * 2 * C, s);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, pp, rows, C, 1.f / (float)M, w,
                      save_mean, save_istd, dw, db, coef);
   const long nvec = M * (C / 8);
   const int ge = grid_elem(nvec);

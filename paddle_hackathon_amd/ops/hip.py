@@ -133,7 +133,7 @@ def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=Non
     L = _L()
     nb = L.pha_bn_num_blocks(M, C)
     f32 = dict(dtype=torch.float32, device=x.device)
-    part = torch.empty(nb * 2 * C, **f32)
+    part = torch.empty((max(nb, 64) + 64) * 2 * C, **f32)
     stats = torch.empty(4, C, **f32)  # save_mean, save_istd, scale, shift
     y = torch.empty_like(x)
     _check(L.pha_bn_fwd_train(_DT[x.dtype], _ptr(x), _ptr(residual), _ptr(y), M, C, _ptr(w), _ptr(b),
@@ -163,7 +163,7 @@ def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False):
     L = _L()
     nb = L.pha_bn_num_blocks(M, C)
     f32 = dict(dtype=torch.float32, device=x.device)
-    part = torch.empty(nb * 2 * C, **f32)
+    part = torch.empty((max(nb, 64) + 64) * 2 * C, **f32)
     coef = torch.empty(3 * C, **f32)
     dwb = torch.empty(2, C, **f32)
     dx = torch.empty_like(x)
