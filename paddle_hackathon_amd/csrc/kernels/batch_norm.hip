@@ -208,11 +208,33 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const T* __restrict_
 }
 
 // ------------------------------------------------------------------------- backward
+// ReLU mask: from the saved output y, or — y == nullptr, no residual was added — recomputed from x
+// as x*scale + shift > 0 with the forward's affine (aff = [scale | shift]); y > 0 <=> that > 0, and
+// the backward then reads two tensors per pass instead of three.
+template <typename T>
+__device__ __forceinline__ void relu_mask(const T* __restrict__ y, const float* __restrict__ aff, int C, long off, int c,
+                                          const float (&xv)[8], float (&d)[8]) {
+  if (y) {
+    float yv[8];
+    Vec8<T>::ld(y + off, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+  } else {
+    const float4 s0 = *reinterpret_cast<const float4*>(aff + c), s1 = *reinterpret_cast<const float4*>(aff + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(aff + C + c), h1 = *reinterpret_cast<const float4*>(aff + C + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = fmaf(xv[i], sc[i], sh[i]) > 0.f ? d[i] : 0.f;
+  }
+}
+
 template <typename T, bool kRelu>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                  const T* __restrict__ y,
                                                                  const float* __restrict__ mean, long M, int C,
-                                                                 float* __restrict__ part) {
+                                                                 float* __restrict__ part,
+                                                                 const float* __restrict__ aff) {
   __shared__ float sm[2][kThreads][8];
   const Geo g = geo(C);
   float sdy[8], sdx[8], mu[8];
@@ -229,12 +251,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
       float d[8], xv[8];
       Vec8<T>::ld(dy + off, d);
       Vec8<T>::ld(x + off, xv);
-      if (kRelu) {
-        float yv[8];
-        Vec8<T>::ld(y + off, yv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
-      }
+      if (kRelu) relu_mask<T>(y, aff, C, off, g.v * 8, xv, d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         sdy[i] += d[i];
@@ -290,19 +307,15 @@ template <typename T, bool kRelu, bool kDres>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                 const T* __restrict__ y,
                                                                 const float* __restrict__ coef, T* __restrict__ dx,
-                                                                T* __restrict__ dres, long nvec, int cv) {
+                                                                T* __restrict__ dres, long nvec, int cv,
+                                                                const float* __restrict__ aff) {
   const int C = cv * 8;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % cv) * 8;
     float d[8], xv[8];
     Vec8<T>::ld(dy + i * 8, d);
     Vec8<T>::ld(x + i * 8, xv);
-    if (kRelu) {
-      float yv[8];
-      Vec8<T>::ld(y + i * 8, yv);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
-    }
+    if (kRelu) relu_mask<T>(y, aff, C, i * 8, c, xv, d);
     if (kDres) Vec8<T>::st(dres + i * 8, d);
     float A[8], B[8], C0[8], o[8];
     *reinterpret_cast<float4*>(A) = *reinterpret_cast<const float4*>(coef + c);
@@ -423,18 +436,18 @@ PHA_API int pha_bn_apply(int dt, const void* x, const void* res, void* y, long M
 
 PHA_API int pha_bn_bwd(int dt, const void* dy, const void* x, const void* y, long M, int C, const float* w,
                        const float* save_mean, const float* save_istd, void* dx, void* dres, float* dw, float* db,
-                       float* part, float* coef, int relu, hipStream_t s) {
+                       float* part, float* coef, int relu, const float* aff, hipStream_t s) {
   if (C % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
-  if (relu && !y) return (int)hipErrorInvalidValue;
+  if (relu && !y && !aff) return (int)hipErrorInvalidValue;
   int tiles;
   const int nb = grid_rows(M, C, &tiles);
   PHA_DISPATCH_T(dt, T, {
     if (relu)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)dy,
-                         (const T*)x, (const T*)y, save_mean, M, C, part);
+                         (const T*)x, (const T*)y, save_mean, M, C, part, aff);
     else
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)dy,
-                         (const T*)x, (const T*)y, save_mean, M, C, part);
+                         (const T*)x, (const T*)y, save_mean, M, C, part, aff);
   });
   int rows = nb;
   const float* pp = fold_rows(part, rows, C, part + (long)nb * 2 * C, s);
@@ -447,13 +460,13 @@ PHA_API int pha_bn_bwd(int dt, const void* dy, const void* x, const void* y, lon
     const T* xr = (const T*)x;
     const T* yr = (const T*)y;
     if (relu && dres)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8, aff);
     else if (relu)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8, aff);
     else if (dres)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8, aff);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), dim3(ge), dim3(kThreads), 0, s, d, xr, yr, coef, (T*)dx, (T*)dres, nvec, C / 8, aff);
   });
   return (int)hipGetLastError();
 }

@@ -351,9 +351,11 @@ class _BatchNormNHWC(torch.autograd.Function):
         ext = getattr(x, "_pha_bn_stats", None)   # partial sums from the producing conv's epilogue
         if ext is not None and (ext[2] != x._version or ext[0].device != x.device or ext[1] <= 0):
             ext = None
-        y, mean, istd = _hip.bn_fwd_train(x, w32, b32, running_mean, running_var, eps, momentum, residual, relu,
-                                          ext_stats=None if ext is None else (ext[0], ext[1]))
-        ctx.save_for_backward(x, y if relu else None, w32, mean, istd)
+        y, mean, istd, aff = _hip.bn_fwd_train(x, w32, b32, running_mean, running_var, eps, momentum, residual,
+                                               relu, ext_stats=None if ext is None else (ext[0], ext[1]))
+        # ReLU without a residual: the backward recomputes the mask from x and the affine, y is not kept
+        keep_y = relu and residual is not None
+        ctx.save_for_backward(x, y if keep_y else None, w32, mean, istd, aff if relu else None)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.wdt = None if weight is None else weight.dtype
         ctx.bdt = None if bias is None else bias.dtype
@@ -361,8 +363,8 @@ class _BatchNormNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        x, y, w32, mean, istd = ctx.saved_tensors
-        dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res)
+        x, y, w32, mean, istd, aff = ctx.saved_tensors
+        dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res, affine=aff)
         return (dx, None if ctx.wdt is None else dw.to(ctx.wdt), None if ctx.bdt is None else db.to(ctx.bdt),
                 None, None, dres, None, None, None)
 

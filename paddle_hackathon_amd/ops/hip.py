@@ -45,7 +45,7 @@ def _L():
             "pha_bn_num_blocks": [LG, I],
             "pha_bn_fwd_train": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, F, F, I, P, I, P],
             "pha_bn_apply": [I, P, P, P, LG, I, P, P, I, P],
-            "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P],
+            "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P, P],
             "pha_chunk_size": [],
             "pha_tensor_meta_size": [],
         }
@@ -142,7 +142,7 @@ def bn_fwd_train(x, w, b, running_mean, running_var, eps, momentum, residual=Non
                               _ptr(ext_stats[0]) if ext_stats else None, int(ext_stats[1]) if ext_stats else 0,
                               _stream(x)),
            "bn_fwd_train")
-    return y, stats[0], stats[1]
+    return y, stats[0], stats[1], stats[2:4]
 
 
 def bn_apply(x, scale, shift, residual=None, relu=False):
@@ -155,11 +155,13 @@ def bn_apply(x, scale, shift, residual=None, relu=False):
     return y
 
 
-def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False):
+def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False, affine=None):
+    """affine ([2, C] fp32 forward scale / shift): with relu and y None the ReLU mask is recomputed
+    from x (no residual in the forward), so y need not be kept or read."""
     C = x.shape[-1]
     M = x.numel() // C
     assert bn_supported(x, C) and dy.shape == x.shape and dy.dtype == x.dtype and dy.is_contiguous()
-    assert not relu or (y is not None and y.shape == x.shape)
+    assert not relu or (y is not None and y.shape == x.shape) or (affine is not None and affine.shape == (2, C))
     L = _L()
     nb = L.pha_bn_num_blocks(M, C)
     f32 = dict(dtype=torch.float32, device=x.device)
@@ -169,7 +171,8 @@ def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False):
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if want_dres else None
     _check(L.pha_bn_bwd(_DT[x.dtype], _ptr(dy), _ptr(x), _ptr(y), M, C, _ptr(w), _ptr(save_mean), _ptr(save_istd),
-                        _ptr(dx), _ptr(dres), _ptr(dwb[0]), _ptr(dwb[1]), _ptr(part), _ptr(coef), int(relu), _stream(x)),
+                        _ptr(dx), _ptr(dres), _ptr(dwb[0]), _ptr(dwb[1]), _ptr(part), _ptr(coef), int(relu),
+                        _ptr(affine.contiguous()) if affine is not None else None, _stream(x)),
            "bn_bwd")
     return dx, dwb[0], dwb[1], dres
 
