@@ -30,6 +30,7 @@ struct TensorMeta {
 struct AdamArgs {
   float lr, beta1, beta2, eps, bc1, bc2, grad_scale;
   int decoupled;
+  const float* gscale;   // optional device scalar multiplying every gradient (global-norm clip factor)
 };
 
 template <typename P, typename G>
@@ -45,13 +46,14 @@ __global__ __launch_bounds__(256) void adam_kernel(const TensorMeta* __restrict_
   P* p = (P*)mt.p;
   const G* g = (const G*)mt.g;
   float* master = mt.master;
+  const float gsc = a.grad_scale * (a.gscale ? *a.gscale : 1.f);
   for (long base = start + threadIdx.x; base < end; base += 256L * kILP) {
     float gv[kILP], pv[kILP], mv[kILP], vv[kILP];
 #pragma unroll
     for (int k = 0; k < kILP; ++k) {
       const long i = base + (long)k * 256;
       if (i < end) {
-        gv[k] = Cvt<G>::ld(g, i) * a.grad_scale;
+        gv[k] = Cvt<G>::ld(g, i) * gsc;
         pv[k] = master ? master[i] : Cvt<P>::ld(p, i);
         mv[k] = mt.m[i];
         vv[k] = mt.v[i];
@@ -148,9 +150,9 @@ PHA_API int pha_tensor_meta_size() { return (int)sizeof(TensorMeta); }
 
 PHA_API int pha_multi_tensor_adam(int pdt, int gdt, const void* metas, const void* chunks, int nchunks, float lr,
                                   float beta1, float beta2, float eps, float bc1, float bc2, float grad_scale,
-                                  int decoupled, hipStream_t stream) {
+                                  int decoupled, const float* gscale, hipStream_t stream) {
   if (nchunks <= 0) return 0;
-  AdamArgs a{lr, beta1, beta2, eps, bc1, bc2, grad_scale, decoupled};
+  AdamArgs a{lr, beta1, beta2, eps, bc1, bc2, grad_scale, decoupled, gscale};
   PHA_DISPATCH_T(pdt, P, {
     PHA_DISPATCH_T(gdt, G, {
       hipLaunchKernelGGL((adam_kernel<P, G>), dim3(nchunks), dim3(256), 0, stream, (const TensorMeta*)metas, (const int2*)chunks, a);

@@ -69,7 +69,16 @@ class ClipGradByGlobalNorm(ClipGradBase):
             sq = sq + dsq
         return sq
 
-    def _dygraph_clip(self, params_grads):
+    def scale_factor(self, params_grads):
+        """fp32 device scalar min(1, clip_norm / global_norm) over the clipped gradients, or None
+        when no gradient takes part (the fused optimizers multiply it in as they read gradients)."""
+        grads, dist_grads = self._split(params_grads)
+        if not grads and not dist_grads:
+            return None
+        norm = torch.sqrt(self.global_norm_sq(grads, dist_grads))
+        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+
+    def _split(self, params_grads):
         grads, dist_grads = [], []
         for p, g in params_grads:
             if g is None or not getattr(p, "need_clip", True):
@@ -78,6 +87,10 @@ class ClipGradByGlobalNorm(ClipGradBase):
                 dist_grads.append(g._t)
             else:
                 grads.append(g._t)
+        return grads, dist_grads
+
+    def _dygraph_clip(self, params_grads):
+        grads, dist_grads = self._split(params_grads)
         if not grads and not dist_grads:
             return params_grads
         sq = self.global_norm_sq(grads, dist_grads)

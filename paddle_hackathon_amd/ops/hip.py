@@ -39,7 +39,7 @@ def _L():
             "pha_bias_gelu_fwd": [I, P, P, P, LG, I, I, P],
             "pha_bias_gelu_bwd": [I, P, P, P, P, LG, I, I, P],
             "pha_embedding_fwd": [P, P, P, LG, I, LG, P],
-            "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P],
+            "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P, P],
             "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
             "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
             "pha_bn_num_blocks": [LG, I],
@@ -324,7 +324,9 @@ def _tables_cached(tag, recs, device):
 
 
 def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, step, weight_decay, decoupled,
-                      lr_ratios, grad_scale, wds=None):
+                      lr_ratios, grad_scale, wds=None, gscale_dev=None):
+    """gscale_dev: optional fp32 device scalar multiplied into every gradient as it is read (the
+    global-norm clip factor — no separate pass over the gradients)."""
     L = _L()
     dev = params[0].device
     items = []
@@ -343,7 +345,8 @@ def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, ste
     for (pdt, gdt), its in _group_by_dtype(items, lambda t: (t[0], t[1])).items():
         metas, chunks, n = _tables_cached(("adam", pdt, gdt), [t[2] for t in its], dev)
         _check(L.pha_multi_tensor_adam(_DT[pdt], _DT[gdt], _ptr(metas), _ptr(chunks), n, float(lr), float(beta1), float(beta2),
-                                       float(eps), float(bc1), float(bc2), float(grad_scale), int(bool(decoupled)), stream),
+                                       float(eps), float(bc1), float(bc2), float(grad_scale), int(bool(decoupled)),
+                                       _ptr(gscale_dev), stream),
                "multi_tensor_adam")
 
 

@@ -121,7 +121,17 @@ class Optimizer:
         return out
 
     def _apply_clip(self, pgs):
+        self._gscale_dev = None
         if self._grad_clip is None:
+            return
+        from ..nn.clip import ClipGradByGlobalNorm
+        import os
+        if type(self._grad_clip) is ClipGradByGlobalNorm and getattr(self, "_fuses_grad_scale", False) and pgs \
+                and os.environ.get("PHA_FUSED_CLIP", "1") != "0" \
+                and pgs[0][0]._t.is_cuda and all(p.need_clip if hasattr(p, "need_clip") else True for p, _, _ in pgs):
+            # global-norm clip folded into the fused optimizer kernel: it multiplies the factor in
+            # as it reads each gradient (no extra read + write pass over all gradients)
+            self._gscale_dev = self._grad_clip.scale_factor([(p, g) for p, g, _ in pgs])
             return
         self._grad_clip([(p, g) for p, g, _ in pgs])
 
@@ -295,6 +305,7 @@ class Adam(Optimizer):
         self._epsilon = float(epsilon._t.item()) if isinstance(epsilon, Tensor) else float(epsilon)
         self._lazy_mode = lazy_mode
         self._grad_scale = 1.0
+        self._fuses_grad_scale = True   # _update feeds the clip factor to the multi-tensor kernel
 
     def _decay_for(self, p, group):
         wd, kind = self._wd_for(p, group)
@@ -304,6 +315,15 @@ class Adam(Optimizer):
         lr = self.get_lr()
         params, grads, m1, m2, masters, ratios, wds = [], [], [], [], [], [], []
         step_pows = []
+        if getattr(self, "_gscale_dev", None) is not None and \
+                any(self._decay_for(p, group)[1] == "l1" for p, _, group in pgs):
+            # L1 decay is added to the CLIPPED gradient: apply the clip factor up front instead
+            by_dt = {}
+            for _, g, _ in pgs:
+                by_dt.setdefault(g._t.dtype, []).append(g._t)
+            for dt, gs in by_dt.items():
+                torch._foreach_mul_(gs, self._gscale_dev.to(dt))
+            self._gscale_dev = None
         for p, g, group in pgs:
             wd, kind = self._decay_for(p, group)
             if kind == "l1":
@@ -328,7 +348,8 @@ class Adam(Optimizer):
         if params[0].is_cuda:
             from ..ops import hip
             hip.multi_tensor_adam(params, grads, m1, m2, masters, lr, self._beta1, self._beta2, self._epsilon, step, 0.0,
-                                  self._decoupled, ratios, self._grad_scale, wds)
+                                  self._decoupled, ratios, self._grad_scale, wds,
+                                  gscale_dev=getattr(self, "_gscale_dev", None))
         else:
             for i in range(len(params)):
                 _ops.fused_adam_([params[i]], [grads[i]], [m1[i]], [m2[i]], [masters[i]], lr, self._beta1, self._beta2,

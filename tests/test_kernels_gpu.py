@@ -464,6 +464,29 @@ def test_linear_own_gemm_fwd_bwd(monkeypatch):
     assert rel(z, zr) < 1e-2 and rel(x.grad, xr.grad) < 1e-2 and rel(e.grad, er.grad) < 1e-2
 
 
+def test_adamw_fused_global_norm_clip():
+    """ClipGradByGlobalNorm folded into the multi-tensor AdamW kernel == clip pass + AdamW"""
+    import paddle_hackathon_amd as paddle
+    torch.manual_seed(6)
+    paddle.set_device("gpu:0")
+    ref = None
+    outs = []
+    for fused in (True, False):
+        paddle.seed(7)
+        lin = paddle.nn.Linear(64, 32)
+        opt = paddle.optimizer.AdamW(learning_rate=1e-2, parameters=lin.parameters(), weight_decay=0.1,
+                                     grad_clip=paddle.nn.ClipGradByGlobalNorm(0.05))
+        opt._fuses_grad_scale = fused
+        for _ in range(3):
+            x = paddle.to_tensor(torch.randn(16, 64, device="cuda", generator=torch.Generator("cuda").manual_seed(1)))
+            loss = (lin(x) ** 2).mean() * 100.0
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+        outs.append(lin.weight._t.detach().clone())
+    assert torch.allclose(outs[0], outs[1], rtol=1e-5, atol=1e-6), (outs[0] - outs[1]).abs().max()
+
+
 def test_conv_epilogue_bn_stats():
     """the conv forward epilogue's batch-norm partial sums match the output, and the BN that
     consumes them gives the same normalisation / running stats as its own statistics pass"""
