@@ -178,6 +178,39 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_db_kernel(const T* __restri
   Vec8<float>::st(part + (long)blockIdx.y * H + c8 * 8, acc);
 }
 
+// bias gradient of a linear layer: per-row-block column sums of gy [rows, H] (thread = 8-column
+// chunk, 16-B loads, fp32 accumulation); part[blockIdx.y] is summed by the caller
+template <typename T>
+__global__ __launch_bounds__(256) void col_sum_partial_kernel(const T* __restrict__ gy, float* __restrict__ part,
+                                                              int rows, int H, int rows_per_block) {
+  const int c8 = blockIdx.x * 256 + threadIdx.x;
+  if (c8 * 8 >= H) return;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  float acc[8], acc2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = acc2[k] = 0.f;
+  int r = r0;
+  for (; r + 1 < r1; r += 2) {   // two rows in flight per iteration
+    float g[8], h[8];
+    Vec8<T>::ld(gy + (long)r * H + c8 * 8, g);
+    Vec8<T>::ld(gy + (long)(r + 1) * H + c8 * 8, h);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc[k] += g[k];
+      acc2[k] += h[k];
+    }
+  }
+  if (r < r1) {
+    float g[8];
+    Vec8<T>::ld(gy + (long)r * H + c8 * 8, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += g[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] += acc2[k];
+  Vec8<float>::st(part + (long)blockIdx.y * H + c8 * 8, acc);
+}
+
 // one wave per output row; row bytes multiple of 16
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const uint4* __restrict__ w,
                                                             uint4* __restrict__ out, long rows, int row_vecs, long vocab) {
@@ -247,6 +280,18 @@ PHA_API int pha_bias_gelu_bwd_db(int dt, const void* gy, const void* x, const vo
   PHA_DISPATCH_T(dt, T, {
     hipLaunchKernelGGL((bias_gelu_bwd_db_kernel<T>), grid, dim3(256), 0, stream, (const T*)gy, (const T*)x,
                        (const T*)b, (T*)gx, part, rows, H, rows_per_block, approx != 0);
+  });
+  return (int)hipGetLastError();
+}
+
+// part: [ceil(rows / rows_per_block), H] fp32; column sums of gy = part.sum(0) (done by the caller)
+PHA_API int pha_col_sum_partial(int dt, const void* gy, float* part, int rows, int H, int rows_per_block,
+                                hipStream_t stream) {
+  if (H % 8 || rows <= 0 || rows_per_block <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((H / 8 + 255) / 256, (rows + rows_per_block - 1) / rows_per_block);
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((col_sum_partial_kernel<T>), grid, dim3(256), 0, stream, (const T*)gy, part, rows, H,
+                       rows_per_block);
   });
   return (int)hipGetLastError();
 }

@@ -23,6 +23,25 @@ def _t(x):
     return x._t if isinstance(x, Tensor) else x
 
 
+class _LinearBias(torch.autograd.Function):
+    """addmm (hipBLASLt, bias in the epilogue) whose bias gradient is the HIP column-sum kernel
+    instead of a generic reduction; dx / dW stay on hipBLASLt."""
+
+    @staticmethod
+    def forward(ctx, x2d, w, b):
+        ctx.save_for_backward(x2d, w)
+        return torch.addmm(b, x2d, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2d, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = gy.mm(w.t()) if ctx.needs_input_grad[0] else None
+        dw = x2d.t().mm(gy) if ctx.needs_input_grad[1] else None
+        db = _ops.hip.col_sum(gy) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
 def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with Paddle's [in, out] weight layout (hipBLASLt GEMM + fused bias epilogue;
     PHA_MATMUL_IMPL=hip: the 8-phase MFMA GEMM of gemm8p.hip for forward and both gradients)."""
@@ -32,7 +51,12 @@ def linear(x, weight, bias=None, name=None):
         return _w(_cg.linear(xt, wt, None if bias is None else bias._t))
     if bias is not None and xt.dim() >= 2:
         b = bias._t
-        out = torch.addmm(b, xt.reshape(-1, xt.shape[-1]), wt)
+        x2d = xt.reshape(-1, xt.shape[-1])
+        if _ops.fused._use_hip(xt) and xt.dtype in (torch.bfloat16, torch.float16) and b.dtype == xt.dtype \
+                and wt.dtype == xt.dtype and wt.shape[-1] % 8 == 0:
+            out = _LinearBias.apply(x2d, wt, b)
+        else:
+            out = torch.addmm(b, x2d, wt)
         return _w(out.reshape(list(xt.shape[:-1]) + [wt.shape[-1]]))
     out = torch.matmul(xt, wt)
     if bias is not None:

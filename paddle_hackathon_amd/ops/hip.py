@@ -254,6 +254,21 @@ def bias_gelu_bwd(gy, x, b, approximate):
     return gx, gb
 
 
+def col_sum(gy2d, out_dtype=None):
+    """column sums of a [rows, H] bf16/fp16 tensor (a linear layer's bias gradient): row-block
+    partials in fp32 on the HIP kernel, then one small reduction of the partials"""
+    rows, H = gy2d.shape
+    if gy2d.dtype == torch.float32 or H % 8 or not gy2d.is_contiguous():
+        return gy2d.sum(0, dtype=torch.float32).to(out_dtype or gy2d.dtype)
+    rpb = max(16, -(-rows // 512))
+    part = torch.empty((-(-rows // rpb), H), dtype=torch.float32, device=gy2d.device)
+    L = _L()
+    L.pha_col_sum_partial.restype = c_int
+    _check(L.pha_col_sum_partial(_DT[gy2d.dtype], _ptr(gy2d), _ptr(part), c_int(rows), c_int(H), c_int(rpb),
+                                 _stream(gy2d)), "col_sum_partial")
+    return part.sum(0).to(out_dtype or gy2d.dtype)
+
+
 def embedding_fwd(ids, w):
     ids = ids.to(torch.int64)
     rows = ids.numel()

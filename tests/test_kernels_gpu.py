@@ -464,6 +464,23 @@ def test_linear_own_gemm_fwd_bwd(monkeypatch):
     assert rel(z, zr) < 1e-2 and rel(x.grad, xr.grad) < 1e-2 and rel(e.grad, er.grad) < 1e-2
 
 
+def test_linear_bias_grad_col_sum():
+    """F.linear with bias on bf16: bias gradient from the HIP column-sum kernel, vs fp32 torch"""
+    import paddle_hackathon_amd as paddle
+    import paddle_hackathon_amd.nn.functional as F
+    torch.manual_seed(8)
+    x = torch.randn(3, 100, 64, device="cuda").bfloat16().requires_grad_(True)
+    w = (torch.randn(64, 136, device="cuda") * 0.1).bfloat16().requires_grad_(True)
+    b = torch.randn(136, device="cuda").bfloat16().requires_grad_(True)
+    y = F.linear(paddle.Tensor(x), paddle.Tensor(w), paddle.Tensor(b))._t
+    gy = torch.randn_like(y.float())
+    y.backward(gy.bfloat16())
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    (xr @ wr + br).backward(gy)
+    for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert (a.float() - r).abs().max() / r.abs().max() < 1e-2
+
+
 def test_adamw_fused_global_norm_clip():
     """ClipGradByGlobalNorm folded into the multi-tensor AdamW kernel == clip pass + AdamW"""
     import paddle_hackathon_amd as paddle
