@@ -231,5 +231,75 @@ def gpt_pretraining_loss(logits, labels, loss_mask=None, tp_degree=1):
     return _wrap(per_tok.mean())
 
 
+# ------------------------------------------------------------------------------ pipeline form
+class GPTEmbeddingPipe(GPTEmbeddings):
+    """First-stage embedding; the same layer (SharedLayerDesc key "gpt_embed") is rebuilt on the
+    last stage as the tied LM head, its weight kept identical by the shared-weight group."""
+
+    @property
+    def weight(self):
+        return self.word_embeddings.weight
+
+    def forward(self, input_ids):
+        return super().forward(input_ids)
+
+
+def _tied_lm_head(embed, h):
+    w = embed.word_embeddings.weight
+    if embed.word_embeddings.__class__.__name__ == "VocabParallelEmbedding":
+        from ..parallel.mp_layers import _c_identity
+        h = _c_identity(h)
+    return _wrap(_cg.matmul_nt(h._t, w._t))
+
+
+class GPTPretrainingCriterionPipe(nn.Layer):
+    def __init__(self, tp_degree=1):
+        super().__init__()
+        self.tp_degree = tp_degree
+
+    def forward(self, logits, labels):
+        return gpt_pretraining_loss(logits, labels, None, self.tp_degree)
+
+
+def _gpt_pipe_descs(cfg):
+    from ..parallel.pipeline import LayerDesc, SharedLayerDesc
+    descs = [SharedLayerDesc("gpt_embed", GPTEmbeddingPipe, None, "weight", cfg)]
+    descs += [LayerDesc(GPTDecoderLayer, cfg) for _ in range(cfg.num_layers)]
+    descs += [LayerDesc(nn.LayerNorm, cfg.hidden_size, epsilon=cfg.layer_norm_eps),
+              SharedLayerDesc("gpt_embed", GPTEmbeddingPipe, _tied_lm_head, "weight", cfg)]
+    return descs
+
+
+def GPTForPretrainingPipe(cfg: GPTConfig, num_stages=None, topology=None, seg_method="layer:GPTDecoderLayer",
+                          recompute_interval=0):
+    """GPT pre-training model as a ``PipelineLayer`` (PaddleNLP's GPTForPretrainingPipe layout):
+    [embedding] + num_layers x [decoder] + [final LayerNorm, tied LM head], cut at decoder
+    layers; loss = GPTPretrainingCriterion on the last stage. Run it under
+    ``fleet.distributed_model`` with ``pp_degree`` > 1 (1F1B over RCCL p2p), combinable with TP
+    (``cfg.tensor_parallel_degree``) and sharding."""
+    from ..parallel.pipeline import PipelineLayer
+
+    class _GPTPipe(PipelineLayer):
+        def set_state_dict_from_gpt(self, state):
+            """load this stage's slice from a GPTForPretraining state dict (same parameter names as
+            the non-pipeline model: gpt.embeddings.*, gpt.layers.{i}.*, gpt.final_norm.*)"""
+            import numpy as np
+            for i in range(self._start, self._end):
+                if i == 0 or i == len(self._layers_desc) - 1:
+                    prefix = "gpt.embeddings."
+                elif i == len(self._layers_desc) - 2:
+                    prefix = "gpt.final_norm."
+                else:
+                    prefix = f"gpt.layers.{i - 1}."
+                layer = self._built[i - self._start]   # every desc builds (or reuses) one layer
+                for name, prm in layer.named_parameters():
+                    v = state[prefix + name]
+                    prm.set_value(v.numpy() if hasattr(v, "numpy") else np.asarray(v))
+
+    return _GPTPipe(_gpt_pipe_descs(cfg), num_stages=num_stages, topology=topology,
+                    loss_fn=GPTPretrainingCriterionPipe(cfg.tensor_parallel_degree), seg_method=seg_method,
+                    recompute_interval=recompute_interval)
+
+
 def gpt_1_3b(**kw):
     return GPTForPretraining(gpt_config("gpt3-1.3b", **kw))

@@ -293,3 +293,51 @@ def test_topology():
     assert t.get_comm_list("data")[0] == [0, 4]
     assert t.get_comm_list("pipe")[0] == [0, 2]
     assert t.get_coord(5) == t.coordinate(1, 0, 0, 1)
+
+
+def _gpt_pp_train(rank, world, state):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretrainingPipe
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 2}
+    st.pipeline_configs = {"micro_batch_size": 2, "accumulate_steps": 2}
+    fleet.init(is_collective=True, strategy=st)
+    cfg = gpt_config("gpt-tiny", hidden_dropout=0.0, attention_dropout=0.0)
+    pipe = GPTForPretrainingPipe(cfg)
+    pipe.set_state_dict_from_gpt(state)
+    model = fleet.distributed_model(pipe)
+    opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.1, parameters=pipe.parameters()))
+    rng = np.random.RandomState(3)
+    ids = rng.randint(0, cfg.vocab_size, (4, 17)).astype("int64")
+    losses = []
+    for _ in range(3):
+        loss = model.train_batch([paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])], opt)
+        losses.append(float(loss.numpy()))
+    return {"losses": losses, "stage": pipe._stage_id, "n_layers": len(pipe.run_function)}
+
+
+def test_gpt_pipeline_parallel_matches_single_process():
+    """GPTForPretrainingPipe (tied LM head shared across the first and last stage) under 2-stage
+    1F1B == GPTForPretraining trained on the whole batch in one process"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    paddle.set_device("cpu")
+    paddle.seed(11)
+    cfg = gpt_config("gpt-tiny", hidden_dropout=0.0, attention_dropout=0.0)
+    ref_model = GPTForPretraining(cfg)
+    state = {k: v.numpy() for k, v in ref_model.state_dict().items()}
+    res = run_dist(_gpt_pp_train, 2, args=(state,))
+    opt = paddle.optimizer.SGD(0.1, parameters=ref_model.parameters())
+    rng = np.random.RandomState(3)
+    ids = rng.randint(0, cfg.vocab_size, (4, 17)).astype("int64")
+    ref = []
+    for _ in range(3):
+        loss = ref_model(paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:]))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        ref.append(float(loss.numpy()))
+    assert {r["stage"] for r in res} == {0, 1}
+    for r in res:
+        np.testing.assert_allclose(r["losses"], ref, rtol=2e-4, atol=2e-5)
