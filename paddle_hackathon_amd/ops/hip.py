@@ -363,6 +363,7 @@ def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, ste
                                        float(eps), float(bc1), float(bc2), float(grad_scale), int(bool(decoupled)),
                                        _ptr(gscale_dev), stream),
                "multi_tensor_adam")
+    _bump([p for p, g in zip(params, grads) if g is not None])
 
 
 def multi_tensor_momentum(params, grads, vels, masters, lr, mu, nesterov, weight_decay, lr_ratios, grad_scale, wds=None):
@@ -383,6 +384,15 @@ def multi_tensor_momentum(params, grads, vels, masters, lr, mu, nesterov, weight
         metas, chunks, n = _tables_cached(("mom", pdt, gdt), [t[2] for t in its], dev)
         _check(L.pha_multi_tensor_momentum(_DT[pdt], _DT[gdt], _ptr(metas), _ptr(chunks), n, float(lr), float(mu),
                                            float(grad_scale), int(bool(nesterov)), stream), "multi_tensor_momentum")
+    _bump([p for p, g in zip(params, grads) if g is not None])
+
+
+def _bump(params):
+    """The multi-tensor kernels write parameters through raw pointers, invisible to torch's
+    version counters: bump them, so version-keyed caches of derived layouts (conv filter
+    re-layouts, transposed linear weights) and autograd's saved-tensor checks see the update."""
+    if params:
+        torch.autograd.graph.increment_version(params)
 
 
 def multi_tensor_l2norm_sq(tensors):

@@ -464,6 +464,27 @@ def test_linear_own_gemm_fwd_bwd(monkeypatch):
     assert rel(z, zr) < 1e-2 and rel(x.grad, xr.grad) < 1e-2 and rel(e.grad, er.grad) < 1e-2
 
 
+def test_conv_layout_cache_sees_optimizer_updates():
+    """the conv filter re-layout cache is keyed by the parameter version: a step of the HIP
+    multi-tensor optimizer (raw-pointer writes) must invalidate it"""
+    import paddle_hackathon_amd as paddle
+    paddle.set_device("gpu:0")
+    paddle.seed(9)
+    conv = paddle.nn.Conv2D(16, 32, 3, padding=1, bias_attr=False, data_format="NHWC")
+    conv.to(dtype="bfloat16")
+    opt = paddle.optimizer.Momentum(learning_rate=0.5, momentum=0.9, parameters=conv.parameters())
+    x = paddle.to_tensor(torch.randn(2, 8, 8, 16, device="cuda").bfloat16())
+    for _ in range(2):
+        y = conv(x)
+        (y * y).mean().backward()
+        opt.step()
+        opt.clear_grad()
+    y = conv(x)._t.float()
+    w = conv.weight._t.float()
+    ref = TF.conv2d(x._t.float().permute(0, 3, 1, 2), w, None, 1, 1).permute(0, 2, 3, 1)
+    assert (y - ref).abs().max() / ref.abs().max() < 2e-2
+
+
 def test_linear_bias_grad_col_sum():
     """F.linear with bias on bf16: bias gradient from the HIP column-sum kernel, vs fp32 torch"""
     import paddle_hackathon_amd as paddle
