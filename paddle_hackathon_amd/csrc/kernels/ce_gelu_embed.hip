@@ -211,6 +211,38 @@ __global__ __launch_bounds__(256) void col_sum_partial_kernel(const T* __restric
   Vec8<float>::st(part + (long)blockIdx.y * H + c8 * 8, acc);
 }
 
+// dst[C][R] = src[R][C]^T for 2-byte elements: 64 x 64 tiles through LDS (rows padded by 2
+// elements), 16-B loads and stores on both sides (R, C % 8 == 0)
+__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                          int R, int C) {
+  __shared__ uint16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j;       // 64 rows x 8 chunks
+    const int rr = idx >> 3, cc = (idx & 7) * 8;
+    if (r0 + rr < R && c0 + cc < C) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + (long)(r0 + rr) * C + c0 + cc);
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[rr][cc + k] = e[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j;       // 64 output rows (input columns) x 8 chunks
+    const int oc = idx >> 3, orr = (idx & 7) * 8;
+    if (c0 + oc < C && r0 + orr < R) {
+      uint4 v;
+      uint16_t* e = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = tile[orr + k][oc];
+      *reinterpret_cast<uint4*>(dst + (long)(c0 + oc) * R + r0 + orr) = v;
+    }
+  }
+}
+
 // one wave per output row; row bytes multiple of 16
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const uint4* __restrict__ w,
                                                             uint4* __restrict__ out, long rows, int row_vecs, long vocab) {
@@ -293,6 +325,14 @@ PHA_API int pha_col_sum_partial(int dt, const void* gy, float* part, int rows, i
     hipLaunchKernelGGL((col_sum_partial_kernel<T>), grid, dim3(256), 0, stream, (const T*)gy, part, rows, H,
                        rows_per_block);
   });
+  return (int)hipGetLastError();
+}
+
+// dst [C][R] = src [R][C]^T, 2-byte elements, R % 8 == C % 8 == 0
+PHA_API int pha_transpose16(const void* src, void* dst, int R, int C, hipStream_t stream) {
+  if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose16_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, stream,
+                     (const uint16_t*)src, (uint16_t*)dst, R, C);
   return (int)hipGetLastError();
 }
 

@@ -9,6 +9,7 @@ from ...framework.core import Tensor, _wrap, convert_dtype
 from ...framework.dispatch import register_ops
 from ...tensor._helpers import _int_list
 from ... import ops as _ops
+from ...ops import conv_gemm as _cg
 
 _w = _wrap
 
@@ -46,13 +47,14 @@ def linear(x, weight, bias=None, name=None):
     """y = x @ W + b with Paddle's [in, out] weight layout (hipBLASLt GEMM + fused bias epilogue;
     PHA_MATMUL_IMPL=hip: the 8-phase MFMA GEMM of gemm8p.hip for forward and both gradients)."""
     xt, wt = x._t, weight._t
-    from ...ops import conv_gemm as _cg
     if _cg.linear_ok(xt, wt):
         return _w(_cg.linear(xt, wt, None if bias is None else bias._t))
     if bias is not None and xt.dim() >= 2:
         b = bias._t
         x2d = xt.reshape(-1, xt.shape[-1])
-        if _ops.fused._use_hip(xt) and xt.dtype in (torch.bfloat16, torch.float16) and b.dtype == xt.dtype \
+        if _cg.nt_forward_ok(xt, wt) and _ops.fused._use_hip(xt) and b.dtype == xt.dtype:
+            out = _cg.LinearNT.apply(x2d, wt, b)
+        elif _ops.fused._use_hip(xt) and xt.dtype in (torch.bfloat16, torch.float16) and b.dtype == xt.dtype \
                 and wt.dtype == xt.dtype and wt.shape[-1] % 8 == 0:
             out = _LinearBias.apply(x2d, wt, b)
         else:

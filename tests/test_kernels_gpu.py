@@ -485,6 +485,38 @@ def test_conv_layout_cache_sees_optimizer_updates():
     assert (y - ref).abs().max() / ref.abs().max() < 2e-2
 
 
+@pytest.mark.parametrize("shape", [(64, 64), (136, 200), (2048, 520)])
+def test_transpose16(shape):
+    from paddle_hackathon_amd.ops import conv_gemm
+    t = torch.randn(*shape, device="cuda").bfloat16()
+    assert torch.equal(conv_gemm._transpose2d(t), t.t().contiguous())
+
+
+def test_linear_nt_forward_tracks_updates():
+    """x @ W through the cached transposed weight: gradients vs fp32, and after an AdamW step
+    (raw-pointer update) the cache is refreshed"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import conv_gemm
+    paddle.set_device("gpu:0")
+    paddle.seed(10)
+    lin = paddle.nn.Linear(64, 96)
+    lin.to(dtype="bfloat16")
+    x = torch.randn(40, 64, device="cuda").bfloat16().requires_grad_(True)
+    y = paddle.nn.functional.linear(paddle.Tensor(x), lin.weight, lin.bias)._t
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, lin.weight._t, lin.bias._t))
+    gy = torch.randn(40, 96, device="cuda")
+    y.backward(gy.bfloat16())
+    (xr @ wr + br).backward(gy)
+    for a, r in ((y.detach(), (xr @ wr + br).detach()), (x.grad, xr.grad), (lin.weight._t.grad, wr.grad),
+                 (lin.bias._t.grad, br.grad)):
+        assert (a.float() - r).abs().max() / r.abs().max() < 1e-2
+    opt = paddle.optimizer.AdamW(learning_rate=0.1, parameters=lin.parameters())
+    opt.step()
+    y2 = conv_gemm.matmul_kn(x.detach(), lin.weight._t)
+    ref = x.detach().float() @ lin.weight._t.float()
+    assert (y2.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
 def test_linear_bias_grad_col_sum():
     """F.linear with bias on bf16: bias gradient from the HIP column-sum kernel, vs fp32 torch"""
     import paddle_hackathon_amd as paddle

@@ -40,6 +40,9 @@ for s in "$@"; do
       rm -rf $OUT/prof_resnet_hip
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_resnet_hip -o run --output-format csv -- python3 $ROOT/bench.py --model resnet50 --steps 3 --warmup 2 > $OUT/prof_resnet_hip.log 2>&1; rc=$?
       tail -2 $OUT/prof_resnet_hip.log ;;
+    gpt_gemms)
+      timeout -k 10 300 python tools/bench_gpt_gemms.py > $OUT/gpt_gemms.log 2>&1; rc=$?
+      cat $OUT/gpt_gemms.log | tail -20 ;;
     bench_g8p)
       timeout -k 10 300 python tools/bench_gemm256.py 8p > $OUT/bench_g8p.log 2>&1; rc=$?
       cat $OUT/bench_g8p.log | tail -24 ;;
