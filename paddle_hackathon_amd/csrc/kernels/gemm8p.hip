@@ -27,6 +27,7 @@
 //  B1(t+1), A1(t+1), A0(t+2), B0(t+2) — each half-tile is retired by the vmcnt(8) of the phase
 //  before its first read.
 #include "mfma_tile.h"
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -44,6 +45,8 @@ struct Args {
   int lda, ldb, ldc;
   int act;
   const void* zero;   // >= 16 B of zeros
+  float* ws;          // splits > 1: fp32 partials [splits][M][N] (bias / act applied by the reduction)
+  int splits, kchunk; // split-K: split s covers k in [s * kchunk, (s + 1) * kchunk), kchunk % 64 == 0
 };
 
 constexpr unsigned kNone = 0xffffffffu;
@@ -54,8 +57,9 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-// V: schedule experiments (0 = the schedule above; bit 0: no wave-row stagger, bit 1: no setprio,
-// bit 2: fragment reads retired (lgkmcnt(0)) before the barrier instead of after it)
+// V: schedule ablations (0 = the schedule above; bit 0: no wave-row stagger, bit 1: no setprio,
+// bit 2: fragment reads retired before the barrier). Measured at 8192^3 / 16384x6144x2048 bf16:
+// dropping the stagger costs 10-12 %, dropping setprio 10-12 %, bit 2 is neutral.
 template <typename T, bool AKO, bool BKO, int V = 0>
 __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
   constexpr int HALF = 16384, BUF = 4 * HALF;
@@ -70,10 +74,12 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
 
   // XCD-bijective tile order, GROUP_M-row panels (as gemm256)
   const int tiles_m = (M + 255) / 256, tiles_n = (N + 255) / 256;
-  const int ntiles = tiles_m * tiles_n;
+  const int ntiles = tiles_m * tiles_n, total = ntiles * p.splits;
   const int bid = blockIdx.x;
-  const int q8 = ntiles / 8, r8 = ntiles % 8, xcd = bid % 8;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int q8 = total / 8, r8 = total % 8, xcd = bid % 8;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int split = lin / ntiles, tile = lin % ntiles;   // an XCD walks consecutive tiles of one split
+  const int kbeg = split * p.kchunk, kend = min(K, kbeg + p.kchunk);
   constexpr int GROUP_M = 8;
   const int group = tile / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
@@ -115,19 +121,19 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
                            : kNone;
       skoff[h][u] = koff;
     }
-  const int nk = (K + 63) / 64;
+  const int nk = (kend - kbeg + 63) / 64;
 
   auto issue = [&](int h, int t, int buf) {
     const bool isA = h < 2;
     const bool ko = isA ? AKO : BKO;
     const T* base = isA ? A : B;
     const int ld = isA ? p.lda : p.ldb;
-    const int k0 = t * 64;
+    const int k0 = kbeg + t * 64;
     unsigned char* dst = smem + buf * BUF + h * HALF + wid * 2048;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const char* src = zero;
-      if (t < nk && soff[h][u] != kNone && k0 + skoff[h][u] < K)
+      if (t < nk && soff[h][u] != kNone && k0 + skoff[h][u] < kend)
         src = reinterpret_cast<const char*>(base + soff[h][u] + (ko ? (long)k0 * ld : (long)k0));
       glds16(src, dst + u * 1024);
     }
@@ -233,8 +239,29 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
 
-  // ---- epilogue: bias / activation, C tile staged through LDS so every lane stores 16 B ------
   // acc[qm][qn][i][j] register e = C[wr*128 + qm*64 + i*16 + 4*fk + e][wc*64 + qn*32 + j*16 + fr]
+  if (p.splits > 1) {   // split-K: fp32 partials straight from the accumulators (16 lanes = 64 B of a row)
+    float* ws = p.ws + (long)split * M * N;
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc * 64 + qn * 32 + j * 16 + fr;
+        if (n >= N) continue;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int m = m0 + wr * 128 + qm * 64 + i * 16 + 4 * fk + e;
+              if (m < M) ws[(long)m * N + n] = acc[qm][qn][i][j][e];
+            }
+      }
+    return;
+  }
+
+  // ---- epilogue: bias / activation, C tile staged through LDS so every lane stores 16 B ------
   unsigned char* ct = smem;
 #pragma unroll
   for (int qn = 0; qn < 2; ++qn)
@@ -272,28 +299,40 @@ __global__ __launch_bounds__(512) void gemm8p_kernel(Args p) {
   }
 }
 
+// C = sum of the split partials (+ bias)(act), 4 columns per thread
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, T* __restrict__ C,
+                                                            const float* __restrict__ bias, int M, int N, int ldc,
+                                                            int S, int act) {
+  const long MN = (long)M * N;
+  for (long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i4 < MN; i4 += (long)gridDim.x * 256 * 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(ws + i4);
+    for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(ws + s * MN + i4);
+    const long m = i4 / N;
+    const int n = (int)(i4 - m * N);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e] + (bias ? bias[n + e] : 0.f);
+      if (act == ACT_RELU) x = fmaxf(x, 0.f);
+      else if (act == ACT_GELU) x = gelu_tanh(x);
+      Cvt<T>::st(C, m * ldc + n + e, x);
+    }
+  }
+}
+
 template <typename T>
 int launch(const Args& a, int ako, int bko, hipStream_t st) {
-  const unsigned grid = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
-  static int var = -1;
-  if (var < 0) {
-    const char* e = getenv("PHA_G8P_VAR");
-    var = e ? atoi(e) : 0;
-  }
-  if (std::is_same<T, bf16_t>::value && !ako && var > 0) {
-#define G8P_VAR(v_)                                                                                      \
-    if (var == v_) {                                                                                     \
-      if (bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, true, v_>), dim3(grid), dim3(512), 0, st, a);  \
-      else hipLaunchKernelGGL((gemm8p_kernel<T, false, false, v_>), dim3(grid), dim3(512), 0, st, a);     \
-      return (int)hipGetLastError();                                                                     \
-    }
-    G8P_VAR(1) G8P_VAR(2) G8P_VAR(4) G8P_VAR(6)
-#undef G8P_VAR
-  }
+  const unsigned grid = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256) * a.splits);
   if (!ako && !bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, false>), dim3(grid), dim3(512), 0, st, a);
   else if (!ako && bko) hipLaunchKernelGGL((gemm8p_kernel<T, false, true>), dim3(grid), dim3(512), 0, st, a);
   else if (ako && !bko) hipLaunchKernelGGL((gemm8p_kernel<T, true, false>), dim3(grid), dim3(512), 0, st, a);
   else hipLaunchKernelGGL((gemm8p_kernel<T, true, true>), dim3(grid), dim3(512), 0, st, a);
+  if (a.splits > 1) {
+    const long MN = (long)a.M * a.N;
+    const unsigned rg = (unsigned)std::min((MN / 4 + 255) / 256, 8192L);
+    hipLaunchKernelGGL((splitk_reduce_kernel<T>), dim3(rg), dim3(256), 0, st, a.ws, static_cast<T*>(a.c), a.bias, a.M,
+                       a.N, a.ldc, a.splits, a.act);
+  }
   return (int)hipGetLastError();
 }
 
@@ -304,14 +343,20 @@ using namespace pha;
 
 // C[M,N] = A . B (+bias)(act). a_kouter: A stored [K][lda] (else [M][lda]); b_kouter: B stored
 // [K][ldb] (else B^T stored [N][ldb]). M, N, K, lda, ldb % 8 == 0; every operand < 2^32 elements.
+// splits > 1: split-K over fp32 partials in ws (>= splits * M * N floats, ldc == N), for products
+// with few output tiles and a long K (a weight gradient of a square projection).
 PHA_API int pha_gemm8p(int dt, const void* a, const void* b, void* c, const float* bias, long M, long N, long K,
                        long lda, long ldb, long ldc, int a_kouter, int b_kouter, int act, const void* zero16,
-                       hipStream_t stream) {
+                       int splits, float* ws, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % 8 || N % 8 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   const double asz = (double)(a_kouter ? K : M) * lda, bsz = (double)(b_kouter ? K : N) * ldb;
   if (asz >= 4294967295.0 || bsz >= 4294967295.0 || M > (1L << 30) || N > (1L << 30) || K > (1L << 30))
     return (int)hipErrorInvalidValue;
-  g8p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, act, zero16};
+  if (splits < 1) splits = 1;
+  const long kchunk = ((K + 64L * splits - 1) / (64L * splits)) * 64;
+  splits = (int)((K + kchunk - 1) / kchunk);
+  if (splits > 1 && (!ws || N % 4 || ldc != N)) return (int)hipErrorInvalidValue;
+  g8p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, act, zero16, ws, splits, (int)kchunk};
   if (dt == kBF16) return g8p::launch<bf16_t>(p, a_kouter, b_kouter, stream);
   if (dt == kF16) return g8p::launch<half_t>(p, a_kouter, b_kouter, stream);
   return (int)hipErrorInvalidValue;

@@ -225,7 +225,7 @@ def _L256():
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
         L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P]
-        L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P]
+        L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, I, P, P]
         L.pha_gemm8p.restype = c_int
         L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
         L.pha_gemm256_tn.restype = c_int
@@ -236,7 +236,7 @@ def _L256():
     return L
 
 
-def gemm8p(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, out=None):
+def gemm8p(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, out=None, splits=1):
     """C = op(A) @ op(B) on the 8-phase ping-pong MFMA kernel (gemm8p.hip).
 
     a: [M, K] (a_kouter=False) or [K, M]; b: B^T [N, K] (b_kouter=False) or B [K, N]. Row strides
@@ -250,9 +250,13 @@ def gemm8p(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, out=None):
     assert c.shape == (M, N) and c.stride(1) == 1
     if bias is not None:
         bias = bias.float().contiguous()
+    ws = None
+    if splits > 1:
+        assert c.is_contiguous()
+        ws = torch.empty(splits * M * N, dtype=torch.float32, device=a.device)
     rc = _L256().pha_gemm8p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), _ptr(bias), M, N, Ka, a.stride(0), b.stride(0),
                             c.stride(0), int(a_kouter), int(b_kouter), _ACT[act], _ptr(_zero_page(a.device)),
-                            c_void_p(torch.cuda.current_stream(a.device).cuda_stream))
+                            int(splits), _ptr(ws), c_void_p(torch.cuda.current_stream(a.device).cuda_stream))
     if rc != 0:
         raise RuntimeError(f"pha_gemm8p failed ({rc}) M={M} N={N} K={Ka}")
     return c
@@ -673,6 +677,53 @@ def nt_forward_ok(x, w):
             and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype)
 
 
+_gemm_pick = {}
+
+
+def _pick(key, fns):
+    """index of the fastest of ``fns`` (zero-arg launchers of the same product), timed once per
+    key on the real operands; the library candidate is fns[0] (used while capturing a graph or
+    with PHA_GEMM_PICK=0)"""
+    import os
+    ch = _gemm_pick.get(key)
+    if ch is not None:
+        return ch
+    if len(fns) == 1 or os.environ.get("PHA_GEMM_PICK", "1") == "0" or torch.cuda.is_current_stream_capturing():
+        return 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best, best_t = 0, float("inf")
+    for i, f in enumerate(fns):
+        f()
+        ev0.record()
+        for _ in range(3):
+            f()
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1)
+        if t < best_t:
+            best, best_t = i, t
+    _gemm_pick[key] = best
+    return best
+
+
+def weight_grad(x2d, gy):
+    """dW = x^T @ dY for a linear layer ([in, out]): hipBLASLt or the own 8-phase kernel in its
+    TN layout (split-K when the [in, out] tile grid is too small to fill the chip), whichever
+    measured faster for this shape"""
+    Tk, Kin = x2d.shape
+    N = gy.shape[1]
+    fns = [lambda: x2d.t().mm(gy)]
+    if (x2d.dtype in (torch.bfloat16, torch.float16) and gy.dtype == x2d.dtype and Kin % 8 == 0 and N % 8 == 0
+            and Tk % 8 == 0 and x2d.is_contiguous() and gy.is_contiguous() and x2d.numel() < 2 ** 32
+            and gy.numel() < 2 ** 32 and _lib.native_available()):
+        tiles = -(-Kin // 256) * -(-N // 256)
+        fns.append(lambda: gemm8p(x2d, gy, True, True))
+        if tiles < 2 * _num_cus(x2d.device):
+            sp = min(8, max(2, -(-2 * _num_cus(x2d.device) // tiles)))
+            fns.append(lambda: gemm8p(x2d, gy, True, True, splits=sp))
+    return fns[_pick(("dw", x2d.dtype, Tk, Kin, N), fns)]()
+
+
 class LinearNT(torch.autograd.Function):
     """y = x @ W (+ b) computed as x @ (W^T)^T on the cached transposed weight (NT GEMM, bias
     in the hipBLASLt epilogue); dX = dY W^T (NT on W itself), dW = X^T dY, db by the HIP
@@ -691,7 +742,7 @@ class LinearNT(torch.autograd.Function):
         x2d, w = ctx.saved_tensors
         gy = gy.contiguous()
         dx = gy.mm(w.t()) if ctx.needs_input_grad[0] else None
-        dw = x2d.t().mm(gy) if ctx.needs_input_grad[1] else None
+        dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
         db = hip.col_sum(gy) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 

@@ -603,6 +603,22 @@ def test_gemm8p_layouts(layout, shape):
     assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("splits", [2, 3, 8])
+def test_gemm8p_split_k(splits):
+    """split-K weight-gradient layout (A, B k-outer) with bias + ReLU applied by the reduction"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    torch.manual_seed(12)
+    x = torch.randn(3000, 264, device="cuda").bfloat16()
+    gy = torch.randn(3000, 520, device="cuda").bfloat16()
+    bias = torch.randn(520, device="cuda")
+    c = conv_gemm.gemm8p(x, gy, True, True, bias=bias, act="relu", splits=splits)
+    ref = torch.relu(x.float().t() @ gy.float() + bias)
+    assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+    dw = conv_gemm.weight_grad(x, gy)
+    ref = x.float().t() @ gy.float()
+    assert (dw.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(64, 128, 1000), (512, 384, 4096), (200, 136, 77)])
 @pytest.mark.parametrize("out_f32", [False, True])
 def test_gemm256_tn_weight_grad(shape, out_f32):

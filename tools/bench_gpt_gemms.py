@@ -36,6 +36,9 @@ for name, K, N in [("qkv", 2048, 6144), ("out", 2048, 2048), ("fc1", 2048, 8192)
         ("dX   dY@W^T ", lambda: dy @ w.t(), lambda: conv_gemm.gemm8p(dy, w, False, False)),
         ("dW   x^T@dY ", lambda: x.t() @ dy, lambda: conv_gemm.gemm8p(x, dy, True, True)),
     ]
+    tp = timeit(lambda: conv_gemm.weight_grad(x, dy))
+    print(f"{name} dW picked (lib / own / own split-K): {fl / tp / 1e12:7.1f} TF ({tp * 1e3:.3f} ms) "
+          f"choice={conv_gemm._gemm_pick.get(('dw', x.dtype, T, K, N))}", flush=True)
     for lab, f_lib, f_own in cases:
         tl, to = timeit(f_lib), timeit(f_own)
         total_lib += tl * 24
