@@ -436,11 +436,18 @@ PHA_API int pha_bn_apply(int dt, const void* x, const void* res, void* y, long M
 
 PHA_API int pha_bn_bwd(int dt, const void* dy, const void* x, const void* y, long M, int C, const float* w,
                        const float* save_mean, const float* save_istd, void* dx, void* dres, float* dw, float* db,
-                       float* part, float* coef, int relu, const float* aff, hipStream_t s) {
+                       float* part, float* coef, int relu, const float* aff, const float* ext_part, int ext_rows,
+                       hipStream_t s) {
   if (C % 8 != 0 || M <= 0) return (int)hipErrorInvalidValue;
   if (relu && !y && !aff) return (int)hipErrorInvalidValue;
   int tiles;
   const int nb = grid_rows(M, C, &tiles);
+  if (ext_part) {   // [ext_rows][2][C] sums of dy' and dy' (x - mean) from the producer of dy
+    int rows = ext_rows;
+    const float* pp = fold_rows(ext_part, rows, C, part, s);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, pp, rows, C, 1.f / (float)M, w,
+                       save_mean, save_istd, dw, db, coef);
+  } else {
   PHA_DISPATCH_T(dt, T, {
     if (relu)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb, tiles), dim3(kThreads), 0, s, (const T*)dy,
@@ -453,6 +460,7 @@ PHA_API int pha_bn_bwd(int dt, const void* dy, const void* x, const void* y, lon
   const float* pp = fold_rows(part, rows, C, part + (long)nb * 2 * C, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, pp, rows, C, 1.f / (float)M, w,
                      save_mean, save_istd, dw, db, coef);
+  }
   const long nvec = M * (C / 8);
   const int ge = grid_elem(nvec);
   PHA_DISPATCH_T(dt, T, {

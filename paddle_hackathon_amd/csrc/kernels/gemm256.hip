@@ -53,6 +53,14 @@ struct Args {
   const void* zero;   // >= 16 B of zeros
   ConvGeo g;
   float* stats;       // optional [tiles_m][2][N]: per-tile column sum / sum of squares of the stored C
+  // optional fused batch-norm backward reduction over the stored C (= dL/dy of a BN whose input
+  // was bn_x, same layout as C): per-tile column sums of dy' and dy' * (bn_x - mean), with
+  // dy' = dy masked by bn_x * scale + shift > 0 when bn_aff ([scale | shift]) is given
+  const void* bn_x;
+  const float* bn_mean;
+  const float* bn_aff;
+  float* bn_part;     // [bn_row0 + tiles_m][2][N]
+  int bn_row0;
 };
 
 
@@ -263,7 +271,68 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
       for (int t = 0; t < 8 && n + t < N; ++t) reinterpret_cast<uint16_t*>(C)[m * p.ldc + n + t] = e[t];
     }
   }
-  if (p.stats) {
+  if (p.bn_part) {
+    // batch-norm backward sums over this tile (this product is the BN's output gradient dy; the
+    // BN then skips its own reduction pass): thread = 8-column chunk x row group, 16-B loads of
+    // bn_x and of the staged C rows, so a tile costs a few vector loads per thread, not a
+    // dependent scalar loop
+    constexpr int CW = BN / 8, G2 = NT / CW;
+    const int c8 = tid % CW, rg2 = tid / CW;
+    const int rows = (int)min((long)BM, M - m0);
+    const long n = n0 + c8 * 8;
+    float a1[8], a2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
+    if (n < N) {
+      const T* bx = static_cast<const T*>(p.bn_x);
+      float mu[8], sc[8], sh[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mu[k] = p.bn_mean[n + k];
+        sc[k] = p.bn_aff ? p.bn_aff[n + k] : 0.f;
+        sh[k] = p.bn_aff ? p.bn_aff[N + n + k] : 0.f;
+      }
+      for (int r = rg2; r < rows; r += G2) {
+        long m = m0 + r;
+        if constexpr (CONV) {
+          const ConvGeo& g = p.g;
+          if (g.osh > 0) {
+            const int hw = g.OH * g.OW;
+            const int b = (int)(m / hw), rem = (int)(m - (long)b * hw);
+            const int oh = rem / g.OW, ow = rem - oh * g.OW;
+            m = ((long)b * g.OHF + g.oh0 + oh * g.osh) * g.OWF + g.ow0 + ow * g.osw;
+          }
+        }
+        float xv[8], d[8];
+        Vec8<T>::ld(bx + m * p.ldc + n, xv);
+        Vec8<T>::ld(reinterpret_cast<const T*>(ct + r * CROW + c8 * 16), d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float dd = (p.bn_aff && !(fmaf(xv[k], sc[k], sh[k]) > 0.f)) ? 0.f : d[k];
+          a1[k] += dd;
+          a2[k] = fmaf(dd, xv[k] - mu[k], a2[k]);
+        }
+      }
+    }
+    __syncthreads();                                    // C tile fully stored: reuse the LDS (32 KiB)
+    float* red = reinterpret_cast<float*>(smem);        // [G2][2][BN]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[(rg2 * 2) * BN + c8 * 8 + k] = a1[k];
+      red[(rg2 * 2 + 1) * BN + c8 * 8 + k] = a2[k];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < N) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int g2 = 0; g2 < G2; ++g2) {
+        s1 += red[(g2 * 2) * BN + tid];
+        s2 += red[(g2 * 2 + 1) * BN + tid];
+      }
+      float* out = p.bn_part + (long)(p.bn_row0 + tm) * 2 * N;
+      out[n0 + tid] = s1;
+      out[N + n0 + tid] = s2;
+    }
+  } else if (p.stats) {
     // batch-norm statistics of this tile (the BN that follows a convolution then skips its own
     // read of the output): column sums over the tile's rows of the values as stored (rounded to T)
     constexpr int G = NT / BN;                          // row groups
@@ -321,7 +390,7 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_
   }
   if (tile >= 0 && tile < 6) best = tile;
   const int bm = cands[best][0], bn = cands[best][1];
-  if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);
+  if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);   // row tiles with stats / bn_part rows
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;
     const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
@@ -615,7 +684,7 @@ PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const
                            long lda, long ldb, long ldc, int act, const void* zero16, int tile, int bk,
                            hipStream_t stream) {
   if (K % 8 || lda % 8 || ldb % 8 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}, nullptr};
+  g256::Args p{a, bt, c, bias, M, N, K, lda, ldb, ldc, act, zero16, {}, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (dt == kBF16) return g256::launch<bf16_t, false>(p, stream, tile, bk);
   if (dt == kF16) return g256::launch<half_t, false>(p, stream, tile, bk);
   return (int)hipErrorInvalidValue;
@@ -625,9 +694,13 @@ PHA_API int pha_gemm256_nt(int dt, const void* a, const void* bt, void* c, const
 // oremap (host int[9], may be null): strided output rows and explicit output size, see ConvGeo.
 // stats (may be null, >= ceil(M/128)*2*Cout floats): per-row-tile channel sum / sum of squares of y
 // for a following batch norm; *stats_rows receives the number of row tiles written.
+// bn_part (may be null): y is the output gradient of a batch norm with input bn_x / batch mean
+// bn_mean (/ ReLU affine bn_aff): rows [bn_row0, bn_row0 + *stats_rows) of bn_part receive the
+// per-tile sums of the BN backward (the BN then skips its own reduction pass).
 PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H, int W,
                             int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
                             const void* zero16, int tile, int bk, const int* oremap, float* stats, int* stats_rows,
+                            const void* bn_x, const float* bn_mean, const float* bn_aff, float* bn_part, int bn_row0,
                             hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
@@ -637,8 +710,10 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
     g.OH = oremap[6]; g.OW = oremap[7]; g.ozero = oremap[8];
   }
   const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
-  if (stats && oremap) return (int)hipErrorInvalidValue;
-  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g, stats};
+  if (stats && (oremap || bn_part)) return (int)hipErrorInvalidValue;
+  if (bn_part && (!bn_x || !bn_mean || Cout % 8)) return (int)hipErrorInvalidValue;
+  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g, stats,
+               bn_x, bn_mean, bn_aff, bn_part, bn_row0};
   if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, stats_rows);
   if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, stats_rows);
   return (int)hipErrorInvalidValue;

@@ -224,7 +224,7 @@ def _L256():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
-        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P]
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P, P, P, P, I, P]
         L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, I, P, P]
         L.pha_gemm8p.restype = c_int
         L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
@@ -313,14 +313,18 @@ def gemm256_nt(a, bt, bias=None, act=None, out=None):
     return c
 
 
-def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None, bn_stats=False):
+def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None, bn_stats=False,
+                bn_bwd=None):
     """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout].
 
     ``remap = (oh0, ow0, osh, osw, OH, OW[, zero_rest])`` computes an OH x OW output and stores pixel
     (oh, ow) at (oh0 + oh*osh, ow0 + ow*osw) of ``out`` — one phase of a strided convolution's dgrad;
     ``zero_rest`` (with oh0 = ow0 = 0) also zero-fills the other pixels of each stride cell.
     ``bn_stats``: the epilogue also writes per-row-tile channel sums / sums of squares of y, attached
-    as ``y._pha_bn_stats = (partials, rows, y._version)`` for the batch norm that consumes y."""
+    as ``y._pha_bn_stats = (partials, rows, y._version)`` for the batch norm that consumes y.
+    ``bn_bwd = (bn_x, mean, affine|None, partials, row0)``: y is the output gradient of that batch
+    norm; the epilogue writes the BN backward's per-tile sums into partials from row row0 on and
+    the call returns the number of rows written (with y in ``out``)."""
     assert x.dtype in _DT and w_okkc.dtype == x.dtype and x.is_contiguous() and w_okkc.is_contiguous()
     N, H, W, C = x.shape
     Co, KH, KW, Cw = w_okkc.shape
@@ -346,26 +350,33 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
         bias = bias.float().contiguous()
     L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
     part, rows = None, c_int(0)
-    if bn_stats and rm is None:
+    if bn_stats and rm is None and bn_bwd is None:
         part = torch.empty(-(-(N * OH * OW) // 128) * 2 * Co, dtype=torch.float32, device=x.device)
+    bx, bmean, baff, bpart, brow0 = bn_bwd if bn_bwd is not None else (None, None, None, None, 0)
 
     def run(tile, bk):
         rc = L.pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
                                sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, rm, _ptr(part),
-                               byref(rows) if part is not None else None, st)
+                               byref(rows) if (part is not None or bpart is not None) else None,
+                               _ptr(bx), _ptr(bmean), _ptr(baff), _ptr(bpart), int(brow0), st)
         if rc != 0:
             raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
     run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw, OH, OW), run))
     if part is not None:
         y._pha_bn_stats = (part, rows.value, y._version)
+    if bpart is not None:
+        return y, rows.value
     return y
 
 
-def conv256_dgrad(dy, w, x_shape, stride, padding, dilation):
+def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None):
     """dx [N, H, W, Ci] of an NHWC conv from dy [N, OH, OW, Co] and w [Co, Ci, KH, KW], on the forward
     kernel: stride 1 is the conv of dy with the flipped, transposed filter (pad' = d*(K-1) - p);
     stride s splits dx into s*s phases, each a stride-1 conv over the taps that reach it, stored
-    in place through the kernel's output remap (no scatter copy)."""
+    in place through the kernel's output remap (no scatter copy).
+
+    ``bn_src = (bn_x, mean, affine|None, token)``: dx is the output gradient of that batch norm;
+    its backward sums are reduced in the epilogue and attached as ``dx._pha_bn_bwd``."""
     N, H, W, Ci = x_shape
     Co, _, KH, KW = w.shape
     sh, sw = stride
@@ -373,11 +384,30 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation):
     dh, dw = dilation
     _, OH, OW, _ = dy.shape
     dy = dy.contiguous()
+    bn = None
+    if bn_src is not None and Ci % 8 == 0 and bn_src[0].shape == (N, H, W, Ci) and bn_src[0].is_contiguous():
+        # rows: every launch below writes <= ceil(rows / 128) partial rows
+        bn = [bn_src, torch.empty((-(-(N * H * W) // 128) + 4 * sh * sw) * 2 * Ci, dtype=torch.float32,
+                                  device=dy.device), 0]
+
+    def _bn(): return None if bn is None else (bn[0][0], bn[0][1], bn[0][2], bn[1], bn[2])
+
+    def _run(*args, **kw):
+        r = conv256_fwd(*args, bn_bwd=_bn(), **kw)
+        if bn is not None:
+            bn[2] += r[1]
+            return r[0]
+        return r
+
+    def _done(dx):
+        if bn is not None:
+            dx._pha_bn_bwd = (bn[1], bn[2], bn[0][3], dx._version)
+        return dx
     if (sh, sw) == (1, 1):
         wt = _wlayout(w, "dgrad", lambda t: t.flip(2, 3).permute(1, 2, 3, 0).contiguous())   # [Ci][KH][KW][Co]
         dx = torch.empty(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
-        return conv256_fwd(dy, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
-                           remap=(0, 0, 1, 1, H, W))
+        return _done(_run(dy, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
+                          remap=(0, 0, 1, 1, H, W)))
     if (dh, dw) != (1, 1):
         raise NotImplementedError("strided + dilated conv dgrad")
     phases = []
@@ -393,6 +423,8 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation):
         and Ci % 8 == 0
     full = len(live) == len(phases) or zero_rest
     dx = (torch.empty if full else torch.zeros)(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
+    if bn is not None and not full:
+        bn = None   # rows of never-written (zero) phases would miss the epilogue sums: BN reduces itself
     for rh, rw, PH, PW, khs, kws, kh0, kw0 in live:
         # output row i of the phase (input row rh + i*sh) receives dy row i + bh - j through tap
         # khs[j]: a stride-1 conv over the reversed taps with top padding nh - 1 - bh
@@ -400,9 +432,9 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation):
         nh, nw = len(khs), len(kws)
         wt = _wlayout(w, ("phase", rh, rw, sh, sw, ph, pw), lambda t, khs=khs, kws=kws:
                       t[:, :, khs[::-1], :][:, :, :, kws[::-1]].permute(1, 2, 3, 0).contiguous())   # [Ci][nh][nw][Co]
-        conv256_fwd(dy, wt, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
-                    remap=(rh, rw, sh, sw, PH, PW, zero_rest))
-    return dx
+        _run(dy, wt, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
+             remap=(rh, rw, sh, sw, PH, PW, zero_rest))
+    return _done(dx)
 
 
 _wlayouts = {}
@@ -539,6 +571,14 @@ def _bn_stats_on():
     return os.environ.get("PHA_CONV_BN_STATS", "1") != "0"
 
 
+def _bn_bwd_on():
+    """dgrad epilogue reduces the preceding batch norm's backward sums (PHA_CONV_BN_BWD=1: on).
+    Off by default: measured on ResNet-50 (batch 256) the extra bn_x reads at the end of every dgrad
+    tile cost more than the skipped reduction pass saves (7.74k img/s vs 7.94k with it off, same box)."""
+    import os
+    return _bn_stats_on() and os.environ.get("PHA_CONV_BN_BWD", "0") == "1"
+
+
 class Conv2dNHWC256(torch.autograd.Function):
     """NHWC conv2d with forward, dgrad and wgrad all on the 256-tile MFMA kernels."""
 
@@ -547,6 +587,8 @@ class Conv2dNHWC256(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.weight = weight   # the parameter object itself (a leaf input): its layout cache entries match
         ctx.conf = (stride, padding, dilation, bias is not None)
+        src = getattr(x, "_pha_bn_src", None)   # x is a batch norm's output: fuse its backward sums
+        ctx.bn_src = src if src is not None and src[0].shape[:3] == x.shape[:3] else None
         w_okkc = _wlayout(weight, "fwd", lambda t: t.permute(0, 2, 3, 1).contiguous())
         # training: the epilogue also emits batch-norm partial statistics of y (ResNet-style
         # conv -> BN pairs then skip the BN's own statistics pass over y); PHA_CONV_BN_STATS=0 disables
@@ -559,7 +601,8 @@ class Conv2dNHWC256(torch.autograd.Function):
         weight = ctx.weight
         stride, padding, dilation, has_bias = ctx.conf
         gy = gy.contiguous()
-        dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation) if ctx.needs_input_grad[0] else None
+        dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation,
+                           bn_src=ctx.bn_src if _bn_bwd_on() else None) if ctx.needs_input_grad[0] else None
         dw = conv256_wgrad(gy, x, weight.shape, stride, padding, dilation) if ctx.needs_input_grad[1] else None
         db = gy.float().sum((0, 1, 2)).to(gy.dtype) if has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None

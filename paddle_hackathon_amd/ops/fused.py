@@ -356,6 +356,10 @@ class _BatchNormNHWC(torch.autograd.Function):
         # ReLU without a residual: the backward recomputes the mask from x and the affine, y is not kept
         keep_y = relu and residual is not None
         ctx.save_for_backward(x, y if keep_y else None, w32, mean, istd, aff if relu else None)
+        if residual is None:
+            # the convolution consuming y can reduce this BN's backward sums in its dgrad epilogue
+            ctx.bn_token = object()
+            y._pha_bn_src = (x, mean, aff if relu else None, ctx.bn_token)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.wdt = None if weight is None else weight.dtype
         ctx.bdt = None if bias is None else bias.dtype
@@ -364,7 +368,11 @@ class _BatchNormNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, y, w32, mean, istd, aff = ctx.saved_tensors
-        dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res, affine=aff)
+        ext = getattr(gy, "_pha_bn_bwd", None)   # sums from the producing dgrad's epilogue
+        if ext is not None and (ext[2] is not getattr(ctx, "bn_token", None) or ext[3] != gy._version):
+            ext = None
+        dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res, affine=aff,
+                                       ext_part=None if ext is None else (ext[0], ext[1]))
         return (dx, None if ctx.wdt is None else dw.to(ctx.wdt), None if ctx.bdt is None else db.to(ctx.bdt),
                 None, None, dres, None, None, None)
 

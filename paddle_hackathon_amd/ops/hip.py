@@ -45,7 +45,7 @@ def _L():
             "pha_bn_num_blocks": [LG, I],
             "pha_bn_fwd_train": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, F, F, I, P, I, P],
             "pha_bn_apply": [I, P, P, P, LG, I, P, P, I, P],
-            "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P, P],
+            "pha_bn_bwd": [I, P, P, P, LG, I, P, P, P, P, P, P, P, P, P, I, P, P, I, P],
             "pha_chunk_size": [],
             "pha_tensor_meta_size": [],
         }
@@ -155,7 +155,7 @@ def bn_apply(x, scale, shift, residual=None, relu=False):
     return y
 
 
-def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False, affine=None):
+def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False, affine=None, ext_part=None):
     """affine ([2, C] fp32 forward scale / shift): with relu and y None the ReLU mask is recomputed
     from x (no residual in the forward), so y need not be kept or read."""
     C = x.shape[-1]
@@ -172,7 +172,8 @@ def bn_bwd(dy, x, y, w, save_mean, save_istd, relu=False, want_dres=False, affin
     dres = torch.empty_like(x) if want_dres else None
     _check(L.pha_bn_bwd(_DT[x.dtype], _ptr(dy), _ptr(x), _ptr(y), M, C, _ptr(w), _ptr(save_mean), _ptr(save_istd),
                         _ptr(dx), _ptr(dres), _ptr(dwb[0]), _ptr(dwb[1]), _ptr(part), _ptr(coef), int(relu),
-                        _ptr(affine.contiguous()) if affine is not None else None, _stream(x)),
+                        _ptr(affine.contiguous()) if affine is not None else None,
+                        _ptr(ext_part[0]) if ext_part else None, int(ext_part[1]) if ext_part else 0, _stream(x)),
            "bn_bwd")
     return dx, dwb[0], dwb[1], dres
 
