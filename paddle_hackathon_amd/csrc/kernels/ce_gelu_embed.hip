@@ -9,6 +9,7 @@
 // embedding: one wave per output row, 16-byte vector row copies.
 //   Reference: phi/kernels/gpu/embedding_kernel.cu.
 #include "common.h"
+#include <algorithm>
 
 using namespace pha;
 
@@ -243,6 +244,89 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __rest
   }
 }
 
+// NHWC max pooling (reference: phi/kernels/funcs/pooling.cu, max_pool2d_with_index): a thread
+// owns 8 channels (16 B) of one output pixel; the window position of the max (kh * KW + kw, first
+// max wins like the reference) is kept as one byte per element for the backward.
+struct PoolGeo {
+  int N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, PoolGeo g) {
+  const int cv = g.C / 8;
+  const long total = (long)g.N * g.OH * g.OW * cv;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = (int)(i % cv);
+    const long pix = i / cv;
+    const int ow = (int)(pix % g.OW), oh = (int)((pix / g.OW) % g.OH), n = (int)(pix / ((long)g.OW * g.OH));
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int ih = oh * g.sh - g.ph + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int iw = ow * g.sw - g.pw + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        Vec8<T>::ld(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c8 * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (v[k] > best[k] || (v[k] != v[k] && best[k] == best[k])) {   // NaN propagates
+            best[k] = v[k];
+            bi[k] = (uint8_t)(kh * g.KW + kw);
+          }
+      }
+    }
+    Vec8<T>::st(y + i * 8, best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(idx + i * 8) = packed;
+  }
+}
+
+// gather form (no atomics): an input pixel sums the gradients of the <= ceil(K/s)^2 windows that
+// cover it and chose it
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx,
+                                                          T* __restrict__ gx, PoolGeo g) {
+  const int cv = g.C / 8;
+  const long total = (long)g.N * g.H * g.W * cv;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = (int)(i % cv);
+    const long pix = i / cv;
+    const int iw = (int)(pix % g.W), ih = (int)((pix / g.W) % g.H), n = (int)(pix / ((long)g.W * g.H));
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    // windows oh with oh*sh - ph <= ih <= oh*sh - ph + KH - 1
+    const int oh_lo = max(0, (ih + g.ph - g.KH + g.sh) / g.sh), oh_hi = min(g.OH - 1, (ih + g.ph) / g.sh);
+    const int ow_lo = max(0, (iw + g.pw - g.KW + g.sw) / g.sw), ow_hi = min(g.OW - 1, (iw + g.pw) / g.sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = ih - (oh * g.sh - g.ph);
+      if (kh < 0 || kh >= g.KH) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int kw = iw - (ow * g.sw - g.pw);
+        if (kw < 0 || kw >= g.KW) continue;
+        const long o = (((long)n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+        const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
+        float d[8];
+        Vec8<T>::ld(gy + o, d);
+        const uint8_t me = (uint8_t)(kh * g.KW + kw);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t w = k < 4 ? packed.x : packed.y;
+          if (((w >> (8 * (k & 3))) & 0xff) == me) acc[k] += d[k];
+        }
+      }
+    }
+    Vec8<T>::st(gx + i * 8, acc);
+  }
+}
+
 // one wave per output row; row bytes multiple of 16
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __restrict__ ids, const uint4* __restrict__ w,
                                                             uint4* __restrict__ out, long rows, int row_vecs, long vocab) {
@@ -333,6 +417,31 @@ PHA_API int pha_transpose16(const void* src, void* dst, int R, int C, hipStream_
   if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(transpose16_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, stream,
                      (const uint16_t*)src, (uint16_t*)dst, R, C);
+  return (int)hipGetLastError();
+}
+
+// NHWC max pool forward (idx: one byte per output element, the window position of the max)
+PHA_API int pha_maxpool2d_nhwc_fwd(int dt, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C, int OH,
+                                   int OW, int KH, int KW, int sh, int sw, int ph, int pw, hipStream_t stream) {
+  if (C % 8 || KH * KW > 256 || ph >= KH || pw >= KW) return (int)hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw};
+  const long total = (long)N * OH * OW * (C / 8);
+  const unsigned grid = (unsigned)std::min((total + 255) / 256, 8192L);
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((maxpool_fwd_kernel<T>), dim3(grid), dim3(256), 0, stream, (const T*)x, (T*)y, idx, g);
+  });
+  return (int)hipGetLastError();
+}
+
+PHA_API int pha_maxpool2d_nhwc_bwd(int dt, const void* gy, const uint8_t* idx, void* gx, int N, int H, int W, int C,
+                                   int OH, int OW, int KH, int KW, int sh, int sw, int ph, int pw, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw};
+  const long total = (long)N * H * W * (C / 8);
+  const unsigned grid = (unsigned)std::min((total + 255) / 256, 8192L);
+  PHA_DISPATCH_T(dt, T, {
+    hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(grid), dim3(256), 0, stream, (const T*)gy, idx, (T*)gx, g);
+  });
   return (int)hipGetLastError();
 }
 

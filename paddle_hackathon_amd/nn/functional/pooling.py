@@ -56,6 +56,13 @@ def _pool(n, kind, x, kernel_size, stride, padding, ceil_mode, exclusive, diviso
     k = _tup(kernel_size, n)
     s = _tup(stride, n) if stride is not None else k
     pad, pre = _pad_arg(padding, n, t, k, s, ceil_mode)
+    if n == 2 and kind == "max" and cl and pre is None and not ceil_mode and not return_mask:
+        from ...ops import hip as _hip, fused as _fused
+        xt = x._t
+        p2 = list(_tup(pad, 2)) if not isinstance(pad, (list, tuple)) else list(pad)
+        if len(p2) == 2 and _fused._use_hip(xt) and _hip.maxpool_nhwc_ok(xt, k, s, p2):
+            # NHWC max pool on the HIP kernels (byte window index, gather backward)
+            return _w(_hip.MaxPool2dNHWC.apply(xt, tuple(k), tuple(s), tuple(p2)))
     if pre is not None:
         fl = []
         for a, b in reversed(pre):

@@ -270,6 +270,44 @@ def col_sum(gy2d, out_dtype=None):
     return part.sum(0).to(out_dtype or gy2d.dtype)
 
 
+class MaxPool2dNHWC(torch.autograd.Function):
+    """NHWC max pool on the HIP kernels: forward keeps the window position of each max (1 byte per
+    output element), backward gathers per input pixel (no atomics, no scatter)."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        N, H, W, C = x.shape
+        OH = (H + 2 * p[0] - k[0]) // s[0] + 1
+        OW = (W + 2 * p[1] - k[1]) // s[1] + 1
+        y = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
+        idx = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=x.device)
+        L = _L()
+        L.pha_maxpool2d_nhwc_fwd.restype = c_int
+        _check(L.pha_maxpool2d_nhwc_fwd(_DT[x.dtype], _ptr(x), _ptr(y), _ptr(idx), *[c_int(v) for v in (
+            N, H, W, C, OH, OW, k[0], k[1], s[0], s[1], p[0], p[1])], _stream(x)), "maxpool2d_nhwc_fwd")
+        ctx.save_for_backward(idx)
+        ctx.conf = (x.shape, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        idx, = ctx.saved_tensors
+        (N, H, W, C), k, s, p = ctx.conf
+        gy = gy.contiguous()
+        gx = torch.empty(N, H, W, C, dtype=gy.dtype, device=gy.device)
+        L = _L()
+        L.pha_maxpool2d_nhwc_bwd.restype = c_int
+        _check(L.pha_maxpool2d_nhwc_bwd(_DT[gy.dtype], _ptr(gy), _ptr(idx), _ptr(gx), *[c_int(v) for v in (
+            N, H, W, C, idx.shape[1], idx.shape[2], k[0], k[1], s[0], s[1], p[0], p[1])], _stream(gy)),
+               "maxpool2d_nhwc_bwd")
+        return gx, None, None, None
+
+
+def maxpool_nhwc_ok(x, k, s, p):
+    return (x.is_cuda and x.dim() == 4 and x.dtype in _DT and x.shape[-1] % 8 == 0 and x.is_contiguous()
+            and k[0] * k[1] <= 256 and p[0] < k[0] and p[1] < k[1] and hasattr(_L(), "pha_maxpool2d_nhwc_fwd"))
+
+
 def embedding_fwd(ids, w):
     ids = ids.to(torch.int64)
     rows = ids.numel()

@@ -485,6 +485,24 @@ def test_conv_layout_cache_sees_optimizer_updates():
     assert (y - ref).abs().max() / ref.abs().max() < 2e-2
 
 
+@pytest.mark.parametrize("cfg", [(2, 17, 15, 64, 3, 2, 1), (3, 8, 8, 16, 2, 2, 0), (2, 12, 12, 24, 3, 1, 1)])
+def test_maxpool2d_nhwc(cfg):
+    """NHWC max pool fwd/bwd HIP kernels vs torch (ResNet stem: 3x3 s2 p1)"""
+    import paddle_hackathon_amd as paddle
+    import paddle_hackathon_amd.nn.functional as F
+    N, H, W, C, k, st, p = cfg
+    torch.manual_seed(14)
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16().requires_grad_(True)
+    y = F.max_pool2d(paddle.Tensor(x), k, st, p, data_format="NHWC")._t
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = TF.max_pool2d(xr, k, st, p).permute(0, 2, 3, 1)
+    assert torch.equal(y.float(), yr)
+    gy = torch.randn_like(yr)
+    y.backward(gy.bfloat16())
+    yr.backward(gy.bfloat16().float())
+    assert torch.allclose(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("shape", [(64, 64), (136, 200), (2048, 520)])
 def test_transpose16(shape):
     from paddle_hackathon_amd.ops import conv_gemm
