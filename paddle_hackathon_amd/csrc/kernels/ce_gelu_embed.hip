@@ -88,11 +88,18 @@ __global__ __launch_bounds__(256) void softmax_ce_bwd_kernel(const float* __rest
   }
 }
 
+// tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp_f32 + v_rcp_f32 (a few instructions; libm tanhf is a
+// long branchy sequence that made the bias+GELU passes VALU-bound); saturates to +-1, error ~1e-7
+__device__ __forceinline__ float fast_tanh(float u) {
+  const float e = __expf(2.f * u);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
 __device__ __forceinline__ float gelu_f(float x, bool approx) {
   if (approx) {
     const float k = 0.7978845608028654f;  // sqrt(2/pi)
     const float u = k * (x + 0.044715f * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
+    return 0.5f * x * (1.f + fast_tanh(u));
   }
   return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
 }
@@ -102,7 +109,7 @@ __device__ __forceinline__ float gelu_grad(float x, bool approx) {
     const float k = 0.7978845608028654f;
     const float x2 = x * x;
     const float u = k * (x + 0.044715f * x2 * x);
-    const float t = tanhf(u);
+    const float t = fast_tanh(u);
     return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x2);
   }
   const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const T* __restrict_
     Vec8<T>::ld(x + i * 8, v);
     if (b) {
       float bv[8];
-      Vec8<T>::ld(b + (i * 8) % H, bv);
+      Vec8<T>::ld(b + (int)((unsigned)i % (unsigned)(H / 8)) * 8, bv);   // n8 < 2^32 (host check)
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += bv[k];
     }
@@ -137,7 +144,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
     Vec8<T>::ld(gy + i * 8, g);
     if (b) {
       float bv[8];
-      Vec8<T>::ld(b + (i * 8) % H, bv);
+      Vec8<T>::ld(b + (int)((unsigned)i % (unsigned)(H / 8)) * 8, bv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += bv[k];
     }
@@ -371,7 +378,7 @@ PHA_API int pha_softmax_ce_bwd(int dt, const float* gloss, const void* logits, c
 }
 
 PHA_API int pha_bias_gelu_fwd(int dt, const void* x, const void* b, void* y, long n, int H, int approx, hipStream_t stream) {
-  if (n % 8 || (b && H % 8)) return (int)hipErrorInvalidValue;
+  if (n % 8 || (b && H % 8) || n / 8 >= (1L << 32)) return (int)hipErrorInvalidValue;
   const long n8 = n / 8;
   PHA_DISPATCH_T(dt, T, {
     hipLaunchKernelGGL((bias_gelu_fwd_kernel<T>), dim3(grid_for(n8, 256)), dim3(256), 0, stream, (const T*)x, (const T*)b, (T*)y, n8, H, approx != 0);
@@ -380,7 +387,7 @@ PHA_API int pha_bias_gelu_fwd(int dt, const void* x, const void* b, void* y, lon
 }
 
 PHA_API int pha_bias_gelu_bwd(int dt, const void* gy, const void* x, const void* b, void* gx, long n, int H, int approx, hipStream_t stream) {
-  if (n % 8 || (b && H % 8)) return (int)hipErrorInvalidValue;
+  if (n % 8 || (b && H % 8) || n / 8 >= (1L << 32)) return (int)hipErrorInvalidValue;
   const long n8 = n / 8;
   PHA_DISPATCH_T(dt, T, {
     hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(grid_for(n8, 256)), dim3(256), 0, stream, (const T*)gy, (const T*)x, (const T*)b, (T*)gx, n8, H, approx != 0);
