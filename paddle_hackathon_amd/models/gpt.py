@@ -102,6 +102,7 @@ class GPTAttention(nn.Layer):
 class GPTMLP(nn.Layer):
     def __init__(self, cfg: GPTConfig):
         super().__init__()
+        self.cfg = cfg
         h, f = cfg.hidden_size, cfg.ffn_hidden_size
         out_scale = 1.0 / math.sqrt(2.0 * cfg.num_layers)
         if cfg.tensor_parallel_degree > 1:
@@ -113,6 +114,11 @@ class GPTMLP(nn.Layer):
             self.linear2 = nn.Linear(f, h, weight_attr=_w_attr(cfg, out_scale))
 
     def forward(self, x):
+        if self.cfg.tensor_parallel_degree > 1:
+            # column-parallel fc1 computed here (bias fused into the GELU): its input must pass
+            # c_identity so the backward all-reduces the partial input gradients over the TP group
+            from ..parallel.mp_layers import _c_identity
+            x = _c_identity(x, self.linear1.model_parallel_group)
         h = _cg.matmul_kn(x._t, self.linear1.weight._t)
         h = _ops.bias_gelu(h, self.linear1.bias._t, approximate=True)
         return self.linear2(_wrap(h))

@@ -341,3 +341,49 @@ def test_gpt_pipeline_parallel_matches_single_process():
     assert {r["stage"] for r in res} == {0, 1}
     for r in res:
         np.testing.assert_allclose(r["losses"], ref, rtol=2e-4, atol=2e-5)
+
+
+def _gpt_tp_grads(rank, world, state, ids, names):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 1, "mp_degree": 2, "pp_degree": 1}
+    fleet.init(is_collective=True, strategy=st)
+    cfg = gpt_config("gpt-tiny", tensor_parallel_degree=2, hidden_dropout=0.0, attention_dropout=0.0)
+    m = GPTForPretraining(cfg)
+    for name, prm in m.named_parameters():
+        full = state[name]
+        shp = tuple(prm.shape)
+        if shp != full.shape:   # the split dim is the one whose size differs; this rank's chunk
+            d = [i for i in range(full.ndim) if full.shape[i] != shp[i]][0]
+            full = np.split(full, world, axis=d)[rank]
+        prm.set_value(np.ascontiguousarray(full))
+    m = fleet.distributed_model(m)
+    loss = m(paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:]))
+    loss.backward()
+    params = dict((m._layers if hasattr(m, "_layers") else m).named_parameters())
+    return {"loss": float(loss.numpy()), **{n: params[n]._t.grad.numpy() for n in names}}
+
+
+def test_gpt_tensor_parallel_matches_single_process():
+    """TP=2 GPT (column/row-parallel attention + MLP, vocab-parallel embedding and CE): loss and the
+    gradients of replicated parameters equal the single-process model's"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    paddle.set_device("cpu")
+    paddle.seed(21)
+    cfg = gpt_config("gpt-tiny", hidden_dropout=0.0, attention_dropout=0.0)
+    ref = GPTForPretraining(cfg)
+    state = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ids = np.random.RandomState(4).randint(0, cfg.vocab_size, (2, 17)).astype("int64")
+    names = ["gpt.layers.0.norm1.weight", "gpt.layers.0.norm2.weight", "gpt.layers.1.norm2.bias",
+             "gpt.embeddings.position_embeddings.weight", "gpt.final_norm.weight"]
+    res = run_dist(_gpt_tp_grads, 2, args=(state, ids, names))
+    loss = ref(paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:]))
+    loss.backward()
+    params = dict(ref.named_parameters())
+    for r in res:
+        np.testing.assert_allclose(r["loss"], float(loss.numpy()), rtol=1e-5)
+        for n in names:
+            np.testing.assert_allclose(r[n], params[n]._t.grad.numpy(), rtol=2e-4, atol=2e-6, err_msg=n)
