@@ -387,3 +387,54 @@ def test_gpt_tensor_parallel_matches_single_process():
         np.testing.assert_allclose(r["loss"], float(loss.numpy()), rtol=1e-5)
         for n in names:
             np.testing.assert_allclose(r[n], params[n]._t.grad.numpy(), rtol=2e-4, atol=2e-6, err_msg=n)
+
+
+def _gpt_fleet_dp(rank, world, state, ids, names):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 2, "mp_degree": 1, "pp_degree": 1}
+    fleet.init(is_collective=True, strategy=st)
+    cfg = gpt_config("gpt-tiny", hidden_dropout=0.0, attention_dropout=0.0)
+    m = GPTForPretraining(cfg)
+    m.set_state_dict({k: paddle.to_tensor(v) for k, v in state.items()})
+    model = fleet.distributed_model(m)
+    opt = fleet.distributed_optimizer(paddle.optimizer.AdamW(1e-2, parameters=m.parameters(), weight_decay=0.01,
+                                                             grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5)))
+    mine = ids[rank::world]
+    for _ in range(3):
+        loss = model(paddle.to_tensor(mine[:, :-1]), paddle.to_tensor(mine[:, 1:]))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    params = dict(m.named_parameters())
+    return {n: params[n].numpy() for n in names}
+
+
+def test_gpt_fleet_data_parallel_matches_single_process():
+    """the bench.py multi-GPU path (fleet DP, AdamW + global-norm clip): after 3 steps on half
+    batches each, every rank's parameters equal single-process training on the full batch"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
+    paddle.set_device("cpu")
+    paddle.seed(31)
+    cfg = gpt_config("gpt-tiny", hidden_dropout=0.0, attention_dropout=0.0)
+    ref = GPTForPretraining(cfg)
+    state = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ids = np.random.RandomState(6).randint(0, cfg.vocab_size, (4, 17)).astype("int64")
+    names = ["gpt.layers.0.self_attn.qkv_proj.weight", "gpt.layers.1.mlp.linear2.bias",
+             "gpt.embeddings.word_embeddings.weight", "gpt.final_norm.weight"]
+    res = run_dist(_gpt_fleet_dp, 2, args=(state, ids, names))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=ref.parameters(), weight_decay=0.01,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    order = np.concatenate([ids[0::2], ids[1::2]])   # same rows; the mean loss is order-free
+    for _ in range(3):
+        loss = ref(paddle.to_tensor(order[:, :-1]), paddle.to_tensor(order[:, 1:]))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    params = dict(ref.named_parameters())
+    for r in res:
+        for n in names:
+            np.testing.assert_allclose(r[n], params[n].numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
