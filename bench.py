@@ -39,6 +39,7 @@ def _args():
                     help="db: load the in-tree hipBLASLt solution database (TunableOp, no tuning); "
                          "tune: benchmark solutions for new shapes and write the database; off: library heuristics")
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
+    ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
     return ap.parse_args()
 
 
@@ -57,7 +58,7 @@ def main():
     if a.gemm_tuning != "off":
         from paddle_hackathon_amd.incubate import autotune
         n = autotune.enable_gemm_tuning(tune=(a.gemm_tuning == "tune"), filename=a.gemm_tuning_file,
-                                        max_tuning_ms=15)
+                                        max_tuning_ms=a.gemm_tuning_ms)
         if rank == 0:
             print(f"[bench] gemm tuning={a.gemm_tuning} entries={n}", file=sys.stderr, flush=True)
 
