@@ -114,22 +114,36 @@ struct NormMeta {
   int pad;
 };
 
+// Sum of squares of x[start, end): 16-byte vector loads (8 elements per lane, 8 KB per wave
+// instruction group) over the aligned bulk, scalar tail. The scalar-only loop moved 128 B per wave
+// load and ran at ~2 TB/s on the 1.3B-parameter GPT gradients.
+template <typename T>
+__device__ __forceinline__ float l2sq_range(const T* __restrict__ x, long start, long end) {
+  float s = 0.f;
+  long tail = start;
+  if ((reinterpret_cast<uintptr_t>(x + start) & 15) == 0) {
+    const long nvec = (end - start) >> 3;
+    for (long j = threadIdx.x; j < nvec; j += 256) {
+      float v[8];
+      Vec8<T>::ld(x + start + 8 * j, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k] * v[k];
+    }
+    tail = start + 8 * nvec;
+  }
+  for (long i = tail + threadIdx.x; i < end; i += 256) { float v = Cvt<T>::ld(x, i); s += v * v; }
+  return s;
+}
+
 __global__ __launch_bounds__(256) void l2sq_partial_kernel(const NormMeta* __restrict__ metas, const int2* __restrict__ chunks, float* __restrict__ partial) {
   const int2 ch = chunks[blockIdx.x];
   const NormMeta mt = metas[ch.x];
   const long start = (long)ch.y * kChunk;
   const long end = min(start + (long)kChunk, mt.n);
-  float s = 0.f;
-  if (mt.dtype == kF32) {
-    const float* x = (const float*)mt.x;
-    for (long i = start + threadIdx.x; i < end; i += 256) { float v = x[i]; s += v * v; }
-  } else if (mt.dtype == kBF16) {
-    const bf16_t* x = (const bf16_t*)mt.x;
-    for (long i = start + threadIdx.x; i < end; i += 256) { float v = Cvt<bf16_t>::ld(x, i); s += v * v; }
-  } else {
-    const half_t* x = (const half_t*)mt.x;
-    for (long i = start + threadIdx.x; i < end; i += 256) { float v = Cvt<half_t>::ld(x, i); s += v * v; }
-  }
+  float s;
+  if (mt.dtype == kF32) s = l2sq_range((const float*)mt.x, start, end);
+  else if (mt.dtype == kBF16) s = l2sq_range((const bf16_t*)mt.x, start, end);
+  else s = l2sq_range((const half_t*)mt.x, start, end);
   __shared__ float red[4];
   s = block_reduce<false>(s, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;

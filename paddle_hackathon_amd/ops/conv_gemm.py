@@ -442,17 +442,22 @@ _wlayouts = {}
 
 def _wlayout(w, kind, make):
     """filter re-layouts (forward [Co][KH][KW][Ci], flipped dgrad filters, dgrad phase filters)
-    cached per parameter version: computed once per optimizer step, not once per call"""
+    cached per parameter version: computed once per optimizer step, not once per call. One entry
+    per (parameter, kind): a new version replaces (and frees) the stale copy before the new one is
+    made, so the cache holds at most one re-layout of every weight (keying by version kept up to
+    512 stale copies alive: +50 GB on GPT-3 13B)."""
     import weakref
-    key = (w.data_ptr(), w._version, tuple(w.shape), w.dtype, kind)
+    key = (w.data_ptr(), tuple(w.shape), w.dtype, kind)
     hit = _wlayouts.get(key)
-    if hit is not None and hit[0]() is w:
+    if hit is not None and hit[0]() is w and hit[2] == w._version:
         return hit[1]
-    if len(_wlayouts) > 512:
+    _wlayouts.pop(key, None)
+    hit = None
+    if len(_wlayouts) > 4096:
         _wlayouts.clear()
     with torch.no_grad():
         v = make(w.detach())
-    _wlayouts[key] = (weakref.ref(w), v)
+    _wlayouts[key] = (weakref.ref(w), v, w._version)
     return v
 
 

@@ -731,3 +731,17 @@ def test_conv_layer_nhwc_routes_to_hip(monkeypatch):
     assert "Conv2dNHWC" in type(y._t.grad_fn).__name__
     y.mean().backward()
     assert conv.weight.grad is not None and x.grad is not None
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+def test_multi_tensor_l2norm_sq_vector_and_tail(dt):
+    """global-norm partial sums (16-byte vector bulk + scalar tail, misaligned views fall back to
+    the scalar loop) == fp32 torch sum of squares over chunk-crossing, odd and offset tensors"""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(0)
+    base = torch.randn(70001, device="cuda").to(dt)
+    ts = [torch.randn(16384 * 3 + 5, device="cuda").to(dt), torch.randn(7, device="cuda").to(dt),
+          base[3:], base[:40000], torch.randn(2048, 2048, device="cuda").to(dt)]
+    got = hip.multi_tensor_l2norm_sq(ts)
+    ref = sum((t.float() ** 2).sum() for t in ts)
+    assert abs(float(got) - float(ref)) <= 1e-4 * float(ref)
