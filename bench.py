@@ -2,8 +2,13 @@
 """Headline benchmark: GPT-3 1.3B pre-training tokens/sec under fleet data parallelism
 (BASELINE.json: "samples/sec/GPU ResNet-50 bf16 + tokens/sec GPT-3-1.3B fleet DP at 1/2/4/8 MI355X").
 
-    python bench.py --gpus N --steps K --warmup W            # N=1 runs in-process
-    torchrun --nproc-per-node N bench.py --gpus N ...         # driver launch for N>1
+    python bench.py --gpus N --steps K --warmup W            # N>1: spawns N ranks itself
+    torchrun --nproc-per-node N bench.py --gpus N ...         # or the driver's launcher
+
+With ``--gpus N > 1`` and no ``WORLD_SIZE`` in the environment the script starts N worker
+processes of itself (one per GPU, RCCL rendezvous on 127.0.0.1) through the in-tree launcher
+before anything touches the GPU, and exits with the job's code. Under a launcher, ``WORLD_SIZE``
+must equal ``--gpus`` or the script exits non-zero.
 
 Each step = forward + backward + AdamW update (fp32 master weights) of the full
 24-layer GPT-3 1.3B (hidden 2048, 16 heads, ffn 8192, vocab 50304, seq 2048) in
@@ -46,8 +51,26 @@ def _args():
     return ap.parse_args()
 
 
+def _self_launch(a):
+    """--gpus N without a launcher: run N ranks of this script (children, not exec: the parent never
+    initialises the GPU) and return the job's exit code."""
+    from paddle_hackathon_amd.parallel.spawn import launch
+    import torch
+    n_dev = torch.cuda.device_count()   # does not initialise HIP on this image
+    if n_dev < a.gpus:
+        print(f"[bench] --gpus {a.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    return launch(["--nproc_per_node", str(a.gpus), os.path.abspath(__file__)] + sys.argv[1:])
+
+
 def main():
     a = _args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(_self_launch(a))
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"[bench] WORLD_SIZE={env_world} disagrees with --gpus {a.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
     import torch
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd import distributed as dist

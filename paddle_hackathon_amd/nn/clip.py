@@ -2,8 +2,8 @@
 
 ``ClipGradByGlobalNorm`` computes the global norm with one multi-tensor HIP
 reduction (ops.global_norm_sq) and scales all grads in place; under tensor /
-pipeline parallelism the squared norm is all-reduced across the model-parallel
-groups first (set ``_mp_group``), matching HybridParallelClipGrad.
+pipeline / sharding parallelism the squared norm is all-reduced across the hybrid
+"check" group first (see the class), matching HybridParallelClipGrad.
 """
 from __future__ import annotations
 
@@ -54,51 +54,80 @@ class ClipGradByNorm(ClipGradBase):
 
 
 class ClipGradByGlobalNorm(ClipGradBase):
+    """Global-norm clip. Under hybrid parallelism fleet sets ``_check_group`` (every rank that
+    shares this rank's data-parallel coordinate: the mp x pp x sharding ranks) and ``_mp_degree``.
+    The squared norm is then reduced with ONE all-reduce over that group (reference
+    ``hybrid_parallel_optimizer.py:122-139`` issues up to three):
+
+      * tensor-parallel-split gradients (``p.is_distributed``) are disjoint slices: summed;
+      * replicated gradients are identical on the mp ranks of one pipeline stage: summed over the
+        group and divided by the mp degree, which leaves the sum over pipeline stages and
+        sharding owners;
+      * a weight shared by pipeline stages (the tied embedding; ``is_firstly_shared`` False on
+        every stage but the first that holds it) is counted once, but still scaled everywhere.
+
+    The collective is issued even when this rank has no clipped gradient, so ranks never
+    disagree on the number of collectives."""
+
     def __init__(self, clip_norm, group_name="default_group", auto_skip_clip=False):
         self.clip_norm = float(clip_norm)
         self.group_name = group_name
-        self._mp_groups = []   # filled by fleet for hybrid parallel
-
-    def global_norm_sq(self, grads, dist_grads=None):
-        sq = _ops.global_norm_sq([g for g in grads])
-        if dist_grads:
-            dsq = _ops.global_norm_sq(dist_grads)
-            for grp in self._mp_groups:
-                import torch.distributed as dist
-                dist.all_reduce(dsq, group=grp)
-            sq = sq + dsq
-        return sq
-
-    def scale_factor(self, params_grads):
-        """fp32 device scalar min(1, clip_norm / global_norm) over the clipped gradients, or None
-        when no gradient takes part (the fused optimizers multiply it in as they read gradients)."""
-        grads, dist_grads = self._split(params_grads)
-        if not grads and not dist_grads:
-            return None
-        norm = torch.sqrt(self.global_norm_sq(grads, dist_grads))
-        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
+        self._check_group = None   # torch ProcessGroup, set by fleet for hybrid parallel
+        self._mp_degree = 1
 
     def _split(self, params_grads):
-        grads, dist_grads = [], []
+        """-> (clipped grads, replicated grads counted in the norm, distributed grads counted)."""
+        scaled, rep, dist_g = [], [], []
         for p, g in params_grads:
             if g is None or not getattr(p, "need_clip", True):
                 continue
-            if getattr(p, "is_distributed", False) and self._mp_groups:
-                dist_grads.append(g._t)
-            else:
-                grads.append(g._t)
-        return grads, dist_grads
+            scaled.append(g._t)
+            if getattr(p, "is_firstly_shared", True) is False:
+                continue
+            (dist_g if getattr(p, "is_distributed", False) else rep).append(g._t)
+        return scaled, rep, dist_g
+
+    def global_norm_sq(self, rep, dist_g, device=None):
+        dev = (rep or dist_g)[0].device if (rep or dist_g) else device
+        sq = _ops.global_norm_sq(rep) if rep else torch.zeros((), dtype=torch.float32, device=dev)
+        if self._check_group is not None:
+            import torch.distributed as dist
+            sq = sq.reshape(1).float()
+            if self._mp_degree > 1:
+                sq = sq / float(self._mp_degree)
+            if dist_g:
+                sq = sq + _ops.global_norm_sq(dist_g).float()
+            dist.all_reduce(sq, group=self._check_group)
+            return sq.reshape(())
+        if dist_g:
+            sq = sq + _ops.global_norm_sq(dist_g)
+        return sq
+
+    def _device_of(self, params_grads):
+        for p, _ in params_grads:
+            return p._t.device
+        if getattr(self, "_device", None) is not None:
+            return self._device
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    def scale_factor(self, params_grads):
+        """fp32 device scalar min(1, clip_norm / global_norm) over the clipped gradients, or None
+        when no gradient takes part and no group needs the collective (the fused optimizers
+        multiply it in as they read gradients)."""
+        scaled, rep, dist_g = self._split(params_grads)
+        if not scaled and self._check_group is None:
+            return None
+        norm = torch.sqrt(self.global_norm_sq(rep, dist_g, self._device_of(params_grads)))
+        return torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0).float().reshape(1)
 
     def _dygraph_clip(self, params_grads):
-        grads, dist_grads = self._split(params_grads)
-        if not grads and not dist_grads:
+        scaled, rep, dist_g = self._split(params_grads)
+        if not scaled and self._check_group is None:
             return params_grads
-        sq = self.global_norm_sq(grads, dist_grads)
-        norm = torch.sqrt(sq)
+        norm = torch.sqrt(self.global_norm_sq(rep, dist_g, self._device_of(params_grads)))
         scale = torch.clamp(self.clip_norm / torch.clamp(norm, min=1e-6), max=1.0)
-        allg = grads + dist_grads
         by_dt = {}
-        for g in allg:
+        for g in scaled:
             by_dt.setdefault(g.dtype, []).append(g)
         for dt, gs in by_dt.items():
             torch._foreach_mul_(gs, scale.to(dt))

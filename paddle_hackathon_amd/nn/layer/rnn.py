@@ -223,6 +223,20 @@ class _RNNBase(LayerList):
                 self.append(BiRNN(self._cell_cls(ins, hidden_size, **kw), self._cell_cls(ins, hidden_size, **kw), time_major))
             else:
                 self.append(RNN(self._cell_cls(ins, hidden_size, **kw), False, time_major))
+        # the reference also registers every cell parameter on the RNN itself as
+        # weight_ih_l{k}[_reverse] / weight_hh_l{k} / bias_ih_l{k} / bias_hh_l{k}, so its state
+        # dicts carry both key sets (python/paddle/nn/layer/rnn.py:941-950)
+        names = []
+        for layer in range(num_layers):
+            for d in range(self.num_directions):
+                sfx = "_reverse" if d == 1 else ""
+                names += [f"weight_ih_l{layer}{sfx}", f"weight_hh_l{layer}{sfx}"]
+                if bias_ih_attr is not False:
+                    names.append(f"bias_ih_l{layer}{sfx}")
+                if bias_hh_attr is not False:
+                    names.append(f"bias_hh_l{layer}{sfx}")
+        for name, param in zip(names, [p for p in self.parameters() if p is not None]):
+            setattr(self, name, param)
 
     def forward(self, inputs, initial_states=None, sequence_length=None):
         x = inputs

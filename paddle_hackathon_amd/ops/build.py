@@ -29,11 +29,32 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def _newer(src_files, target):
-    if not os.path.exists(target):
+def _digest(src_files, flags):
+    """content hash of the sources + compiler flags + arch (what the library was built from)"""
+    import hashlib
+    h = hashlib.sha256()
+    for s in sorted(src_files):
+        h.update(os.path.basename(s).encode())
+        with open(s, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
+def _stale(src_files, target, flags):
+    """True unless ``target`` exists and its ``.stamp`` holds the digest of exactly these sources and
+    flags. Content-based, not mtime-based: a library that travelled (gpurun snapshot, copy) with
+    newer mtimes than edited sources is still rebuilt, and a touched-but-unchanged tree is not."""
+    stamp = target + ".stamp"
+    if not os.path.exists(target) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(s) > t for s in src_files)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(src_files, flags)
+
+
+def _write_stamp(src_files, target, flags):
+    with open(target + ".stamp", "w") as f:
+        f.write(_digest(src_files, flags) + "\n")
 
 
 def _run(cmd):
@@ -57,17 +78,19 @@ def build_kernels(force=False, verbose=True):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     target = os.path.join(OUT, "libpha_kernels.so")
-    if not force and not _newer(srcs + hdrs + [__file__], target):
-        return target
-    hipcc = _hipcc()
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-I", os.path.join(CSRC, "kernels")]
+    if not force and not _stale(srcs + hdrs + [__file__], target, flags):
+        return target
+    hipcc = _hipcc()
     objs = []
 
     def compile_one(src):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        if force or _newer([src] + hdrs, obj):
-            _run([hipcc, "-c", src, "-o", obj] + flags + _file_flags(src))
+        oflags = flags + _file_flags(src)
+        if force or _stale([src] + hdrs, obj, oflags):
+            _run([hipcc, "-c", src, "-o", obj] + oflags)
+            _write_stamp([src] + hdrs, obj, oflags)
         return obj
 
     jobs = int(os.environ.get("MAX_JOBS", "8"))
@@ -75,6 +98,7 @@ def build_kernels(force=False, verbose=True):
         objs = list(ex.map(compile_one, srcs))
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target + ".tmp"] + objs)
     os.replace(target + ".tmp", target)
+    _write_stamp(srcs + hdrs + [__file__], target, flags)
     if verbose:
         print(f"[pha] built {target} from {len(srcs)} HIP sources for {ARCH}")
     return target
@@ -87,11 +111,13 @@ def build_runtime(force=False, verbose=True):
     if not srcs:
         return None
     target = os.path.join(OUT, "libpha_runtime.so")
-    if not force and not _newer(srcs + hdrs + [__file__], target):
+    flags = ["-O3", "-std=c++17", "-Wall", "-shared", "-fPIC", "-pthread"]
+    if not force and not _stale(srcs + hdrs + [__file__], target, flags):
         return target
     cxx = shutil.which("g++") or shutil.which("c++")
-    _run([cxx, "-O3", "-std=c++17", "-Wall", "-shared", "-fPIC", "-pthread", "-o", target + ".tmp"] + srcs)
+    _run([cxx] + flags + ["-o", target + ".tmp"] + srcs)
     os.replace(target + ".tmp", target)
+    _write_stamp(srcs + hdrs + [__file__], target, flags)
     if verbose:
         print(f"[pha] built {target} from {len(srcs)} C++ sources")
     return target

@@ -209,6 +209,7 @@ class Optimizer:
         if isinstance(self._learning_rate, LRScheduler) and "LR_Scheduler" in state_dict:
             self._learning_rate.set_state_dict(state_dict.pop("LR_Scheduler"))
         self._step_count = int(state_dict.pop("@step_count@", self._step_count))
+        self.__dict__.pop("_pstep", None)   # per-parameter counts are re-read from the loaded beta-pow accumulators
         # existing accumulators are overwritten now; the rest are loaded lazily on first use
         for name, d in self._accumulators.items():
             for pname, t in d.items():
@@ -342,20 +343,51 @@ class Adam(Optimizer):
             wds.append(wd)
         if not params:
             return
-        # bias correction uses the optimizer step count; the per-param beta-pow accumulators
-        # are still maintained (one foreach launch) so .pdopt checkpoints keep the reference keys
-        step = self._step_count
-        if params[0].is_cuda:
-            from ..ops import hip
-            hip.multi_tensor_adam(params, grads, m1, m2, masters, lr, self._beta1, self._beta2, self._epsilon, step, 0.0,
-                                  self._decoupled, ratios, self._grad_scale, wds,
-                                  gscale_dev=getattr(self, "_gscale_dev", None))
-        else:
-            for i in range(len(params)):
-                _ops.fused_adam_([params[i]], [grads[i]], [m1[i]], [m2[i]], [masters[i]], lr, self._beta1, self._beta2,
-                                 self._epsilon, step, wds[i], self._decoupled, [ratios[i]], self._grad_scale)
+        # Bias correction is per parameter, as the reference's beta1_pow_acc / beta2_pow_acc
+        # (adam_kernel.cu): a parameter that got no gradient in some steps (unused embedding rows'
+        # table, an idle MoE expert) or state resumed from a reference .pdopt keeps its own count.
+        # The count lives on the host (no device sync per step); it is recovered once from the
+        # beta1_pow accumulator value (beta1^(t+1) after t updates) for parameters it has not seen.
+        steps = self._param_steps([p for p, _, _ in pgs], step_pows)
+        groups = {}
+        for i, st in enumerate(steps):
+            groups.setdefault(st, []).append(i)
+        for step, idx in groups.items():
+            sel = (lambda xs: [xs[i] for i in idx]) if len(groups) > 1 else (lambda xs: xs)
+            if params[0].is_cuda:
+                from ..ops import hip
+                hip.multi_tensor_adam(sel(params), sel(grads), sel(m1), sel(m2), sel(masters), lr, self._beta1,
+                                      self._beta2, self._epsilon, step, 0.0, self._decoupled, sel(ratios),
+                                      self._grad_scale, sel(wds), gscale_dev=getattr(self, "_gscale_dev", None))
+            else:
+                for i in idx:
+                    _ops.fused_adam_([params[i]], [grads[i]], [m1[i]], [m2[i]], [masters[i]], lr, self._beta1,
+                                     self._beta2, self._epsilon, step, wds[i], self._decoupled, [ratios[i]],
+                                     self._grad_scale)
         torch._foreach_mul_([b[0]._t for b in step_pows], self._beta1)
         torch._foreach_mul_([b[1]._t for b in step_pows], self._beta2)
+
+    def _param_steps(self, params, pows):
+        """1-based update index of every parameter for this step (host counters). A count not seen
+        yet is read back once from the beta-pow accumulators (beta^(t+1) after t updates; beta2's
+        decays slower, so it is preferred while it has not underflowed)."""
+        cnt = self.__dict__.setdefault("_pstep", {})
+        missing = [i for i, p in enumerate(params) if p.name not in cnt]
+        if missing:
+            vals = torch.stack([torch.stack([pows[i][0]._t.reshape(()).float(), pows[i][1]._t.reshape(()).float()])
+                                for i in missing]).cpu().tolist()
+            for i, (v1, v2) in zip(missing, vals):
+                t = None
+                for beta, v in ((self._beta2, v2), (self._beta1, v1)):
+                    if 0.0 < beta < 1.0 and v > 0.0:
+                        t = int(round(math.log(v) / math.log(beta))) - 1
+                        break
+                cnt[params[i].name] = max(0, self._step_count - 1 if t is None else t)
+        out = []
+        for p in params:
+            cnt[p.name] += 1
+            out.append(cnt[p.name])
+        return out
 
 
 class AdamW(Adam):

@@ -277,11 +277,12 @@ class HybridParallelOptimizer:
         clip = optimizer._grad_clip
         from ...nn.clip import ClipGradByGlobalNorm
         if isinstance(clip, ClipGradByGlobalNorm) and hcg is not None:
-            groups = []
-            for g in (hcg.get_model_parallel_group(), hcg.get_pipe_parallel_group(), hcg.get_sharding_parallel_group()):
-                if g is not None and g.nranks > 1 and g.pg is not None:
-                    groups.append(g.pg)
-            clip._mp_groups = groups
+            cg = hcg.get_check_parallel_group()
+            if cg is not None and cg.nranks > 1 and cg.pg is not None:
+                clip._check_group = cg.pg
+                clip._mp_degree = hcg.get_model_parallel_world_size()
+                plist = optimizer._parameter_list or []
+                clip._device = plist[0]._t.device if plist else None
         self._sharding = None
         sg = hcg.get_sharding_parallel_group() if hcg is not None else None
         if sg is not None and sg.nranks > 1:

@@ -147,6 +147,12 @@ class PipelineLayer(Layer):
                 g = C.new_group(ranks)
                 if C.get_rank() in ranks:
                     groups[key] = g
+        # the norm of a shared weight's (all-reduced, identical) gradient counts on the first
+        # stage holding it only (reference: is_firstly_shared in pp_layers.py)
+        for key in keys:
+            if key in self.shared_layers:
+                w = getattr(self.shared_layers[key], self.shared_weight_attrs[key])
+                w.is_firstly_shared = self._stage_id == min(keys[key])
         # make shared weights identical (first stage wins)
         for key, g in groups.items():
             if key in self.shared_layers:

@@ -157,8 +157,12 @@ def divide(x, y, name=None):
 
 @_export
 def floor_divide(x, y, name=None):
+    """Truncating division, as the reference kernel: FloorDivideFunctor returns trunc(a / b)
+    (phi/kernels/funcs/elementwise_functor.h:555-561), so floor_divide(-7, 2) == -3."""
     xt, yt = _bin(x, y)
-    return _w(torch.div(xt, yt, rounding_mode="floor"))
+    if not torch.is_floating_point(xt) and bool((yt == 0).any()):
+        raise ZeroDivisionError("floor_divide: divisor contains zero")
+    return _w(torch.div(xt, yt, rounding_mode="trunc"))
 
 
 @_export

@@ -152,7 +152,7 @@ def test_tensor_parallel_layers():
         np.testing.assert_allclose(r["ce"].reshape(-1), r["ref_ce"].reshape(-1), rtol=1e-5, atol=1e-5)
 
 
-def _pp_train(rank, world):
+def _pp_train(rank, world, clip=None):
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.distributed import fleet
     from paddle_hackathon_amd.distributed.fleet.meta_parallel import LayerDesc, PipelineLayer
@@ -174,7 +174,8 @@ def _pp_train(rank, world):
         l.weight.set_value(weights[order[gi]])
         l.bias.set_value(np.zeros(l.bias.shape, "float32"))
     model = fleet.distributed_model(pl)
-    opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.05, parameters=pl.parameters()))
+    gc = paddle.nn.ClipGradByGlobalNorm(clip) if clip else None
+    opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.05, parameters=pl.parameters(), grad_clip=gc))
     X = rng.randn(8, 8).astype("float32")
     Y = rng.randn(8, 4).astype("float32")
     losses = []
@@ -184,10 +185,12 @@ def _pp_train(rank, world):
     return losses
 
 
-def test_pipeline_parallel_1f1b_matches_single_process():
+@pytest.mark.parametrize("clip", [None, 0.05])
+def test_pipeline_parallel_1f1b_matches_single_process(clip):
+    """with ClipGradByGlobalNorm the norm must cover BOTH stages' gradients (clip 0.05 is active)"""
     import paddle_hackathon_amd as paddle
     paddle.set_device("cpu")
-    res = run_dist(_pp_train, 2)
+    res = run_dist(_pp_train, 2, (clip,))
     rng = np.random.RandomState(5)
     W = [rng.randn(8, 8).astype("float32") * 0.3, rng.randn(8, 8).astype("float32") * 0.3,
          rng.randn(8, 4).astype("float32") * 0.3]
@@ -198,7 +201,8 @@ def test_pipeline_parallel_1f1b_matches_single_process():
     for l, w in zip([m[0], m[2], m[4]], W):
         l.weight.set_value(w)
         l.bias.set_value(np.zeros(l.bias.shape, "float32"))
-    opt = paddle.optimizer.SGD(0.05, parameters=m.parameters())
+    opt = paddle.optimizer.SGD(0.05, parameters=m.parameters(),
+                               grad_clip=paddle.nn.ClipGradByGlobalNorm(clip) if clip else None)
     ref = []
     for _ in range(3):
         tot = 0.0

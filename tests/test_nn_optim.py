@@ -292,3 +292,98 @@ def test_lenet_trains_on_cpu():
         opt.clear_grad()
         losses.append(float(loss))
     assert losses[-1] < losses[0] * 0.7
+
+
+def _adam_numpy(p0, grads, lr=0.1, b1=0.9, b2=0.999, eps=1e-8):
+    """reference Adam (adam_kernel.cu semantics: per-parameter beta-pow accumulators; a step with
+    no gradient leaves the parameter, moments and pows untouched)"""
+    p, m, v, b1p, b2p = p0.astype(np.float64).copy(), np.zeros_like(p0, np.float64), np.zeros_like(p0, np.float64), b1, b2
+    for g in grads:
+        if g is None:
+            continue
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        lr_t = lr * math.sqrt(1 - b2p) / (1 - b1p)
+        p = p - lr_t * m / (np.sqrt(v) + eps * math.sqrt(1 - b2p))
+        b1p, b2p = b1p * b1, b2p * b2
+    return p
+
+
+def test_adam_bias_correction_is_per_parameter():
+    """a parameter that gets no gradient in some steps keeps its own bias-correction count"""
+    paddle.seed(0)
+    a = paddle.create_parameter([4], "float32")
+    b = paddle.create_parameter([4], "float32")
+    a0, b0 = a.numpy().copy(), b.numpy().copy()
+    opt = paddle.optimizer.Adam(0.1, parameters=[a, b])
+    rng = np.random.RandomState(0)
+    ga, gb = [], []
+    for step in range(6):
+        g1 = rng.randn(4).astype(np.float32)
+        g2 = rng.randn(4).astype(np.float32) if step % 2 == 0 else None
+        loss = (a * paddle.to_tensor(g1)).sum()
+        if g2 is not None:
+            loss = loss + (b * paddle.to_tensor(g2)).sum()
+        loss.backward()
+        opt.step()
+        opt.clear_grad(set_to_zero=False)
+        ga.append(g1)
+        gb.append(g2)
+    np.testing.assert_allclose(a.numpy(), _adam_numpy(a0, ga), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b.numpy(), _adam_numpy(b0, gb), rtol=1e-5, atol=1e-6)
+
+
+def test_adam_resume_from_reference_keys_matches_uninterrupted():
+    """resume from a state dict holding only the reference keys (moment1/2 + beta-pow accumulators,
+    no '@step_count@'): bias correction continues from the loaded pows"""
+    def run(n_steps, params, opt, rng):
+        for _ in range(n_steps):
+            loss = sum(((p * paddle.to_tensor(rng.randn(*p.shape).astype(np.float32))).sum() for p in params))
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+
+    paddle.seed(1)
+    w = paddle.create_parameter([3, 5], "float32")
+    init = w.numpy().copy()
+    opt = paddle.optimizer.AdamW(0.05, parameters=[w], weight_decay=0.01)
+    run(7, [w], opt, np.random.RandomState(3))
+    full = w.numpy().copy()
+
+    w2 = paddle.create_parameter([3, 5], "float32")
+    w2.set_value(init)
+    opt2 = paddle.optimizer.AdamW(0.05, parameters=[w2], weight_decay=0.01)
+    rng = np.random.RandomState(3)
+    run(4, [w2], opt2, rng)
+    sd = {k: v for k, v in opt2.state_dict().items() if k != "@step_count@"}
+    snap = w2.numpy().copy()
+    w3 = paddle.create_parameter([3, 5], "float32")
+    w3.name = w2.name
+    w3.set_value(snap)
+    opt3 = paddle.optimizer.AdamW(0.05, parameters=[w3], weight_decay=0.01)
+    opt3.set_state_dict(sd)
+    run(3, [w3], opt3, rng)
+    np.testing.assert_allclose(w3.numpy(), full, rtol=1e-5, atol=1e-6)
+
+
+def test_rnn_reference_parameter_aliases():
+    m = paddle.nn.LSTM(4, 8, num_layers=2, direction="bidirect")
+    assert m.weight_ih_l0 is m[0].cell_fw.weight_ih
+    assert m.weight_hh_l1_reverse is m[1].cell_bw.weight_hh
+    assert m.bias_hh_l1_reverse is m[1].cell_bw.bias_hh
+    sd = m.state_dict()
+    for k in ("weight_ih_l0", "bias_ih_l1_reverse", "0.cell_fw.weight_ih", "1.cell_bw.bias_hh"):
+        assert k in sd
+    assert len(m.parameters()) == 16
+    g = paddle.nn.GRU(3, 5)
+    assert "weight_hh_l0" in g.state_dict() and g.weight_hh_l0 is g[0].cell.weight_hh
+
+
+def test_floor_divide_truncates_like_reference():
+    x = paddle.to_tensor(np.array([-7, 7, -8, 9], np.int64))
+    y = paddle.to_tensor(np.array([2, -2, 3, 4], np.int64))
+    np.testing.assert_array_equal(paddle.floor_divide(x, y).numpy(), [-3, -3, -2, 2])
+    np.testing.assert_array_equal((x // y).numpy(), [-3, -3, -2, 2])
+    xf = paddle.to_tensor(np.array([-7.5, 7.5], np.float32))
+    np.testing.assert_array_equal(paddle.floor_divide(xf, paddle.to_tensor(np.array([2.0, -2.0], np.float32))).numpy(),
+                                  [-3.0, -3.0])
