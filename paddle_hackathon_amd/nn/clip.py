@@ -97,6 +97,12 @@ class ClipGradByGlobalNorm(ClipGradBase):
                 sq = sq / float(self._mp_degree)
             if dist_g:
                 sq = sq + _ops.global_norm_sq(dist_g).float()
+            if sq.device.type == "cpu" and dist.get_backend(self._check_group) == "nccl":
+                # host-side gradients (sharding offload): RCCL needs a device tensor
+                dev = torch.device("cuda", torch.cuda.current_device())
+                red = sq.to(dev)
+                dist.all_reduce(red, group=self._check_group)
+                return red.to(sq.device).reshape(())
             dist.all_reduce(sq, group=self._check_group)
             return sq.reshape(())
         if dist_g:
@@ -130,7 +136,7 @@ class ClipGradByGlobalNorm(ClipGradBase):
         for g in scaled:
             by_dt.setdefault(g.dtype, []).append(g)
         for dt, gs in by_dt.items():
-            torch._foreach_mul_(gs, scale.to(dt))
+            torch._foreach_mul_(gs, scale.to(device=gs[0].device, dtype=dt))
         return params_grads
 
 

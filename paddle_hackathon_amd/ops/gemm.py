@@ -1,0 +1,127 @@
+"""Own-GEMM entry points on the one-wave-per-SIMD 256x256x64 MFMA kernel (csrc/kernels/gemm4w.hip).
+
+Reference behaviour: every matmul of the reference goes through
+``phi/kernels/impl/matmul_kernel_impl.h:88`` (cuBLAS), the fused linear-epilogue op through
+``paddle/fluid/operators/fused/fused_gemm_epilogue_op.cu:29,298`` (cuBLASLt bias/gelu/relu
+forward, dgelu + bias-grad backward). Here the same products run on our own gfx950 kernel with
+the epilogues folded in:
+
+  * ``gemm(a, b, a_kouter, b_kouter, ...)``   C = op(A) @ op(B) (+bias)(gelu|relu)
+      a: [M, K] (a_kouter=False) or [K, M];  b: B^T [N, K] (b_kouter=False) or B [K, N]
+  * forward fc1:   h = x @ W1 + b1 stored as pre-activation AND a = gelu(h) in one pass
+  * backward fc2-dgrad: dH = (dY @ W2^T) * gelu'(h) with the bias-gradient column sums of dH
+
+Operands need K % 64 == 0 and M, N, row strides % 8 == 0 (``supported``); anything else goes to
+the caller's fallback.
+"""
+from __future__ import annotations
+
+import os
+from ctypes import c_int, c_long, c_void_p
+
+import torch
+
+from . import _lib
+
+EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT = 1, 2, 4, 8, 16, 32
+_DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
+
+
+def _L():
+    L = _lib._load()
+    if L is None:
+        raise RuntimeError(f"libpha_kernels.so not loaded: {_lib._load_error}")
+    if not getattr(L, "_g4w_sig", False):
+        P, I, LG = c_void_p, c_int, c_long
+        L.pha_gemm4w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P, LG, P, I, P]
+        L.pha_gemm4w.restype = c_int
+        L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
+        L.pha_colsum_finish.restype = c_int
+        L._g4w_sig = True
+    return L
+
+
+def _ptr(t):
+    return c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(t):
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def sched_variant():
+    return int(os.environ.get("PHA_G4W_SCHED", "0"))
+
+
+def supported(M, N, K, *tensors):
+    """the shapes / strides the kernel takes"""
+    if K % 64 or M % 8 or N % 8 or K <= 0 or M <= 0 or N <= 0:
+        return False
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda or t.dtype not in (torch.bfloat16, torch.float16) or t.dim() != 2 or t.stride(1) != 1 \
+                or t.stride(0) % 8:
+            return False
+        if t.stride(0) * 256 * 2 >= 2 ** 32:
+            return False
+    return _lib.native_available()
+
+
+def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, aux_out=False, colsum=False,
+         out=None):
+    """C = epi(op(A) @ op(B)).
+
+    act: None | "gelu" | "relu" | "dgelu" (C = acc * gelu'(aux), aux = forward pre-activation).
+    aux_out: with act="gelu", also write the pre-activation (acc + bias) into ``aux`` (allocated
+    when None) and return it. colsum: also return the fp32 column sums of C (bias gradient).
+    Returns C, or (C, aux) / (C, colsum) / (C, aux, colsum) as requested."""
+    assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
+    assert a.stride(1) == 1 and b.stride(1) == 1
+    M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if b_kouter else (b.shape[0], b.shape[1])
+    assert Ka == Kb, (a.shape, b.shape, a_kouter, b_kouter)
+    c = out if out is not None else torch.empty(M, N, dtype=a.dtype, device=a.device)
+    assert c.shape == (M, N) and c.stride(1) == 1
+    epi = 0
+    if bias is not None:
+        bias = bias.float().contiguous()
+        epi |= EPI_BIAS
+    if act == "gelu":
+        epi |= EPI_GELU
+    elif act == "relu":
+        epi |= EPI_RELU
+    elif act == "dgelu":
+        assert aux is not None and aux.shape == (M, N) and aux.stride(1) == 1
+        epi |= EPI_DGELU
+    elif act is not None:
+        raise ValueError(f"unknown epilogue activation {act}")
+    if aux_out:
+        if aux is None:
+            aux = torch.empty(M, N, dtype=a.dtype, device=a.device)
+        epi |= EPI_AUXOUT
+    cs = None
+    if colsum:
+        cs = torch.empty((M + 255) // 256, N, dtype=torch.float32, device=a.device)
+        epi |= EPI_COLSUM
+    rc = _L().pha_gemm4w(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
+                         int(a_kouter), int(b_kouter), epi, _ptr(bias), _ptr(aux),
+                         aux.stride(0) if aux is not None else 0, _ptr(cs), sched_variant(), _stream(a))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm4w failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
+    res = [c]
+    if aux_out:
+        res.append(aux)
+    if colsum:
+        res.append(cs)
+    return res[0] if len(res) == 1 else tuple(res)
+
+
+def colsum_finish(part, dtype):
+    """[rows, N] fp32 partial column sums -> [N] in ``dtype``"""
+    rows, N = part.shape
+    out = torch.empty(N, dtype=dtype, device=part.device)
+    rc = _L().pha_colsum_finish(_DT[dtype], _ptr(part), _ptr(out), rows, N, _stream(part))
+    if rc != 0:
+        raise RuntimeError(f"pha_colsum_finish failed ({rc})")
+    return out

@@ -298,7 +298,11 @@ class HybridParallelOptimizer:
         self.step()
 
     def clear_grad(self, set_to_zero=True):
+        if self._sharding is not None:
+            return self._sharding.clear_grad(set_to_zero)
         self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
 
     def __getattr__(self, item):
         return getattr(self._inner_opt, item)

@@ -218,12 +218,86 @@ def test_pipeline_parallel_1f1b_matches_single_process(clip):
     np.testing.assert_allclose(res[1], ref, rtol=1e-5)
 
 
-def _sharding(rank, world, level):
+def _sharding(rank, world, level, clip=None, extra=None):
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.distributed import group_sharded_parallel
+    from paddle_hackathon_amd.parallel import sharding as S
     model = _mlp(paddle)
-    opt = paddle.optimizer.AdamW(0.01, parameters=model.parameters(), weight_decay=0.0)
-    model, opt, _ = group_sharded_parallel(model, opt, level)
+    gc = paddle.nn.ClipGradByGlobalNorm(clip) if clip else None
+    opt = paddle.optimizer.AdamW(0.01, parameters=model.parameters(), weight_decay=0.0, grad_clip=gc)
+    model, opt, _ = group_sharded_parallel(model, opt, level, **(extra or {}))
+    rng = np.random.RandomState(123)
+    X = rng.randn(8, 8).astype("float32")
+    Y = rng.randn(8, 4).astype("float32")
+    counts = []
+    for _ in range(3):
+        before = dict(S.comm_stats)
+        xs = paddle.to_tensor(X[rank * 4:(rank + 1) * 4])
+        ys = paddle.to_tensor(Y[rank * 4:(rank + 1) * 4])
+        loss = ((model(xs) - ys) ** 2).mean()
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        counts.append({k: S.comm_stats[k] - before[k] for k in before})
+    sd = model.state_dict()
+    return {"sd": {k: v.numpy() for k, v in sd.items()}, "counts": counts}
+
+
+def _sharding_ref(clip=None):
+    import paddle_hackathon_amd as paddle
+    paddle.set_device("cpu")
+    model = _mlp(paddle)
+    gc = paddle.nn.ClipGradByGlobalNorm(clip) if clip else None
+    opt = paddle.optimizer.AdamW(0.01, parameters=model.parameters(), weight_decay=0.0, grad_clip=gc)
+    rng = np.random.RandomState(123)
+    X = rng.randn(8, 8).astype("float32")
+    Y = rng.randn(8, 4).astype("float32")
+    for _ in range(3):
+        loss = ((model(paddle.to_tensor(X)) - paddle.to_tensor(Y)) ** 2).mean()
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    return {k: v.numpy() for k, v in model.state_dict().items()}
+
+
+@pytest.mark.parametrize("level,clip,extra", [
+    ("os", None, None), ("os_g", None, None), ("p_g_os", None, None),
+    ("os", 0.05, None), ("os_g", 0.05, {"buffer_max_size": 64}), ("p_g_os", 0.05, {"segment_size": 16}),
+    ("os_g", 0.05, {"offload": True}), ("p_g_os", 0.05, {"segment_size": 16, "offload": True}),
+])
+def test_group_sharded_matches_single_process(level, clip, extra):
+    """every stage (with the global-norm clip active, tiny buckets, sharded + replicated stage-3
+    parameters, host offload) trains like one process on the full batch"""
+    res = run_dist(_sharding, 2, (level, clip, extra))
+    ref = _sharding_ref(clip)
+    for r in res:
+        for k in ref:
+            np.testing.assert_allclose(r["sd"][k], ref[k], rtol=1e-4, atol=1e-5)
+
+
+def test_group_sharded_collective_count_is_per_bucket():
+    """stage 1/2: one reduce-scatter + one all-gather per flat bucket per step, never per parameter"""
+    res = run_dist(_sharding, 2, ("os_g", None, {"buffer_max_size": 2 ** 25}))
+    for r in res:
+        for c in r["counts"]:
+            assert c["reduce_scatter"] == 1 and c["all_gather"] == 1, c   # 4 parameters, one bucket
+    res = run_dist(_sharding, 2, ("os", None, {"buffer_max_size": 100}))
+    for r in res:
+        for c in r["counts"]:
+            assert c["reduce_scatter"] == c["all_gather"] and 1 < c["reduce_scatter"] < 4, c
+
+
+def _fleet_sharding(rank, world, clip):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 2}
+    fleet.init(is_collective=True, strategy=st)
+    model = _mlp(paddle)
+    opt = paddle.optimizer.AdamW(0.01, parameters=model.parameters(), weight_decay=0.0,
+                                 grad_clip=paddle.nn.ClipGradByGlobalNorm(clip))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
     rng = np.random.RandomState(123)
     X = rng.randn(8, 8).astype("float32")
     Y = rng.randn(8, 4).astype("float32")
@@ -234,29 +308,15 @@ def _sharding(rank, world, level):
         loss.backward()
         opt.step()
         opt.clear_grad()
-    sd = model.state_dict()
-    return {k: v.numpy() for k, v in sd.items()}
+    return {"sd": {k: v.numpy() for k, v in model.state_dict().items()}}
 
 
-@pytest.mark.parametrize("level", ["os", "os_g", "p_g_os"])
-def test_group_sharded_matches_single_process(level):
-    import paddle_hackathon_amd as paddle
-    paddle.set_device("cpu")
-    res = run_dist(_sharding, 2, (level,))
-    model = _mlp(paddle)
-    opt = paddle.optimizer.AdamW(0.01, parameters=model.parameters(), weight_decay=0.0)
-    rng = np.random.RandomState(123)
-    X = rng.randn(8, 8).astype("float32")
-    Y = rng.randn(8, 4).astype("float32")
-    for _ in range(3):
-        loss = ((model(paddle.to_tensor(X)) - paddle.to_tensor(Y)) ** 2).mean()
-        loss.backward()
-        opt.step()
-        opt.clear_grad()
-    ref = {k: v.numpy() for k, v in model.state_dict().items()}
+def test_fleet_sharding_with_global_norm_clip_matches_single_process():
+    res = run_dist(_fleet_sharding, 2, (0.05,))
+    ref = _sharding_ref(0.05)
     for r in res:
         for k in ref:
-            np.testing.assert_allclose(r[k], ref[k], rtol=1e-4, atol=1e-5)
+            np.testing.assert_allclose(r["sd"][k], ref[k], rtol=1e-4, atol=1e-5)
 
 
 def _gpt_tp_dp(rank, world):

@@ -94,6 +94,21 @@ for s in "$@"; do
     bench_gemm)
       timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
       cat $OUT/bench_gemm.log | tail -20 ;;
+    g4w)
+      timeout -k 10 300 python tools/bench_g4w.py > $OUT/g4w.log 2>&1; rc=$?
+      tail -40 $OUT/g4w.log ;;
+    g4w_s1)
+      PHA_G4W_SCHED=1 timeout -k 10 300 python tools/bench_g4w.py > $OUT/g4w_s1.log 2>&1; rc=$?
+      tail -30 $OUT/g4w_s1.log ;;
+    g4w_var)
+      rc=0; for v in 2 4 6; do PHA_G4W_SCHED=$v timeout -k 10 200 python tools/bench_g4w.py > $OUT/g4w_var$v.log 2>&1 || { rc=$?; break; }; echo "var $v"; grep -E "TF|per-step" $OUT/g4w_var$v.log | tail -20; done ;;
+    prof_g4w)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_g4w; mkdir -p $OUT/prof_g4w
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_g4w/pmc1 -o run --output-format csv -- python3 $ROOT/tools/g4w_prof.py > $OUT/prof_g4w/pmc1.log 2>&1; rc=$?
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g4w/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g4w_prof.py > $OUT/prof_g4w/pmc2.log 2>&1; rc=$?; fi
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d $OUT/prof_g4w/pmc3 -o run --output-format csv -- python3 $ROOT/tools/g4w_prof.py > $OUT/prof_g4w/pmc3.log 2>&1; rc=$?; fi
+      tail -2 $OUT/prof_g4w/*.log ;;
     tests_k)
       timeout -k 10 600 python -m pytest tests -m gpu -v -x --timeout 240 -k "${TESTK}" > $OUT/pytest_k.log 2>&1; rc=$?
       tail -15 $OUT/pytest_k.log ;;
