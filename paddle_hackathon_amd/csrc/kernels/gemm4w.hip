@@ -273,6 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 
   int t = 0;
+  static_assert(!((SCHED & 4) && (SCHED & 2)), "early staging needs the front-loaded reads");
   if constexpr (SCHED & 4) {
     // early staging: buffer b is free once every wave has its F1 fragments (mid phase A), so tile
     // t+2 is issued there and has ~1.5 K-tiles to land; the boundary waits only for tile t+1
@@ -427,7 +428,6 @@ PHA_API int pha_gemm4w(int dt, const void* a, const void* b, void* c, long M, lo
     switch (sched) {
       case 2: return g4w::launch<bf16_t, 2>(p, a_kouter, b_kouter, stream);
       case 4: return g4w::launch<bf16_t, 4>(p, a_kouter, b_kouter, stream);
-      case 6: return g4w::launch<bf16_t, 6>(p, a_kouter, b_kouter, stream);
       default: return g4w::launch<bf16_t, 0>(p, a_kouter, b_kouter, stream);
     }
   }

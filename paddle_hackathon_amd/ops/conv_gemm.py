@@ -676,11 +676,38 @@ class MatmulNTHip(torch.autograd.Function):
         return dx, dw
 
 
+class MatmulNTPick(torch.autograd.Function):
+    """y = x @ w^T (tied logits): every product on the faster of the library GEMM and the own
+    kernels for its shape (ops/gemm.py mm_nt / mm_nn / mm_tn)."""
+
+    @staticmethod
+    def forward(ctx, x2d, w):
+        from . import gemm as _g4
+        ctx.save_for_backward(x2d, w)
+        return _g4.mm_nt(x2d, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from . import gemm as _g4
+        x2d, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        dx = _g4.mm_nn(gy, w) if ctx.needs_input_grad[0] else None
+        dw = _g4.mm_tn(gy, x2d) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
 def matmul_nt(x, w):
-    """x @ w^T, own GEMM when PHA_MATMUL_IMPL=hip admits the shapes, torch otherwise"""
+    """x @ w^T: gemm8p when PHA_MATMUL_IMPL=hip admits the shapes, else per-shape own/library pick"""
     if linear_ok(x, w.t()):
         x2d = x.reshape(-1, x.shape[-1]).contiguous()
         return MatmulNTHip.apply(x2d, w).reshape(list(x.shape[:-1]) + [w.shape[0]])
+    if x.is_cuda and w.dim() == 2 and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype \
+            and type(x).__name__ != "DTensor" and type(w).__name__ != "DTensor":
+        x2d = x.reshape(-1, x.shape[-1])
+        if not x2d.is_contiguous():
+            x2d = x2d.contiguous()
+        return MatmulNTPick.apply(x2d, w.contiguous() if not w.is_contiguous() else w).reshape(
+            list(x.shape[:-1]) + [w.shape[0]])
     return torch.matmul(x, w.t())
 
 
@@ -760,7 +787,10 @@ def weight_grad(x2d, gy):
     measured faster for this shape"""
     Tk, Kin = x2d.shape
     N = gy.shape[1]
+    from . import gemm as _g4
     fns = [lambda: x2d.t().mm(gy)]
+    if _g4._own_ok(x2d, gy) and gy.dtype == x2d.dtype and _g4.supported(Kin, N, Tk, x2d, gy):
+        fns.append(lambda: _g4.gemm(x2d, gy, True, True))   # one-wave-per-SIMD kernel, TN layout
     if (x2d.dtype in (torch.bfloat16, torch.float16) and gy.dtype == x2d.dtype and Kin % 8 == 0 and N % 8 == 0
             and Tk % 8 == 0 and x2d.is_contiguous() and gy.is_contiguous() and x2d.numel() < 2 ** 32
             and gy.numel() < 2 ** 32 and _lib.native_available()):
@@ -782,14 +812,16 @@ class LinearNT(torch.autograd.Function):
         ctx.save_for_backward(x2d, w)
         ctx.has_b = b is not None
         wt = weight_t(w)
-        return torch.addmm(b, x2d, wt.t()) if b is not None else x2d @ wt.t()
+        from . import gemm as _g4
+        return _g4.mm_nt_bias(x2d, wt, b) if b is not None else _g4.mm_nt(x2d, wt)
 
     @staticmethod
     def backward(ctx, gy):
         from . import hip
         x2d, w = ctx.saved_tensors
         gy = gy.contiguous()
-        dx = gy.mm(w.t()) if ctx.needs_input_grad[0] else None
+        from . import gemm as _g4
+        dx = _g4.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
         dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
         db = hip.col_sum(gy) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db

@@ -49,8 +49,14 @@ def _stream(t):
     return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-def sched_variant():
-    return int(os.environ.get("PHA_G4W_SCHED", "0"))
+def sched_variant(a_kouter=False, b_kouter=False):
+    """main-loop schedule: fragment reads front-loaded (0) for the both-K-outer (weight-gradient)
+    layout, spread one per MFMA group (2) otherwise — the per-layout winners on MI355X
+    (tools/bench_g4w.py); PHA_G4W_SCHED overrides"""
+    env = os.environ.get("PHA_G4W_SCHED")
+    if env is not None:
+        return int(env)
+    return 0 if (a_kouter and b_kouter) else 2
 
 
 def supported(M, N, K, *tensors):
@@ -106,7 +112,7 @@ def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, au
         epi |= EPI_COLSUM
     rc = _L().pha_gemm4w(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), epi, _ptr(bias), _ptr(aux),
-                         aux.stride(0) if aux is not None else 0, _ptr(cs), sched_variant(), _stream(a))
+                         aux.stride(0) if aux is not None else 0, _ptr(cs), sched_variant(a_kouter, b_kouter), _stream(a))
     if rc != 0:
         raise RuntimeError(f"pha_gemm4w failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
     res = [c]
@@ -125,3 +131,82 @@ def colsum_finish(part, dtype):
     if rc != 0:
         raise RuntimeError(f"pha_colsum_finish failed ({rc})")
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# per-shape choice between the library GEMM and the own kernels
+# ----------------------------------------------------------------------------------------------
+_picks = {}
+
+
+def _pick(key, fns):
+    """index of the fastest zero-argument launcher (timed once per key on the real operands;
+    fns[0] while capturing a graph or with PHA_GEMM_PICK=0)"""
+    ch = _picks.get(key)
+    if ch is not None:
+        return ch
+    if len(fns) == 1 or os.environ.get("PHA_GEMM_PICK", "1") == "0" or torch.cuda.is_current_stream_capturing():
+        return 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best, best_t = 0, float("inf")
+    for i, f in enumerate(fns):
+        f()
+        ev0.record()
+        for _ in range(3):
+            f()
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1)
+        if t < best_t:
+            best, best_t = i, t
+    _picks[key] = best
+    if os.environ.get("PHA_GEMM_PICK_LOG"):
+        import sys
+        print(f"[gemm-pick] {key}: candidate {best} of {len(fns)} ({'library' if best == 0 else 'own'})",
+              file=sys.stderr, flush=True)
+    return best
+
+
+def _own_ok(*ts):
+    return all(t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
+               for t in ts) and _lib.native_available() and os.environ.get("PHA_OWN_GEMM", "1") != "0"
+
+
+def mm_nt(a, bt):
+    """a [M, K] @ bt[N, K]^T"""
+    fns = [lambda: a @ bt.t()]
+    M, K = a.shape
+    N = bt.shape[0]
+    if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
+        fns.append(lambda: gemm(a, bt, False, False))
+    return fns[_pick(("nt", a.dtype, M, N, K), fns)]()
+
+
+def mm_nt_bias(a, bt, bias):
+    """a [M, K] @ bt[N, K]^T + bias (bias folded into the own kernel's epilogue)"""
+    fns = [lambda: torch.addmm(bias, a, bt.t())]
+    M, K = a.shape
+    N = bt.shape[0]
+    if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
+        fns.append(lambda: gemm(a, bt, False, False, bias=bias))
+    return fns[_pick(("ntb", a.dtype, M, N, K), fns)]()
+
+
+def mm_nn(a, b):
+    """a [M, K] @ b [K, N]"""
+    fns = [lambda: a @ b]
+    M, K = a.shape
+    N = b.shape[1]
+    if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
+        fns.append(lambda: gemm(a, b, False, True))
+    return fns[_pick(("nn", a.dtype, M, N, K), fns)]()
+
+
+def mm_tn(a, b):
+    """a [K, M]^T @ b [K, N] (weight gradients: x^T dY)"""
+    fns = [lambda: a.t() @ b]
+    K, M = a.shape
+    N = b.shape[1]
+    if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
+        fns.append(lambda: gemm(a, b, True, True))
+    return fns[_pick(("tn", a.dtype, M, N, K), fns)]()

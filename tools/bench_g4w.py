@@ -90,6 +90,16 @@ def bench():
         tot["g4w"] += to
         print(f"head {lab}: lib {fl / tl / 1e12:7.1f} TF  g4w {fl / to / 1e12:7.1f} TF   g4w/lib {tl / to:5.3f}",
               flush=True)
+    # stride experiment: NT with power-of-two vs padded row strides (L2 channel / TLB effects)
+    for K, pad in ((2048, 0), (2048, 64), (2048, 128), (8192, 0), (8192, 64)):
+        M, N = 32768, 8192
+        ab = r(M, K + pad)
+        bb = r(N, K + pad)
+        a, bt = ab[:, :K], bb[:, :K]
+        fl = 2.0 * M * N * K
+        to = timeit(lambda: G.gemm(a, bt, False, False))
+        tl = timeit(lambda: a @ bt.t())
+        print(f"NT stride K={K} ld={K + pad}: g4w {fl / to / 1e12:7.1f} TF  lib {fl / tl / 1e12:7.1f} TF", flush=True)
     for M in (4096, 8192):
         a, bt = r(M, M), r(M, M)
         fl = 2.0 * M ** 3

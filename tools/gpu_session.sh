@@ -14,6 +14,9 @@ for s in "$@"; do
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
       tail -3 $OUT/smoke.log ;;
+    bench_picks)
+      PHA_GEMM_PICK_LOG=1 timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $OUT/bench_picks.log 2>&1; rc=$?
+      grep -E "gemm-pick|metric" $OUT/bench_picks.log | tail -40 ;;
     bench)
       timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
       tail -3 $OUT/bench.log ;;
@@ -101,7 +104,7 @@ for s in "$@"; do
       PHA_G4W_SCHED=1 timeout -k 10 300 python tools/bench_g4w.py > $OUT/g4w_s1.log 2>&1; rc=$?
       tail -30 $OUT/g4w_s1.log ;;
     g4w_var)
-      rc=0; for v in 2 4 6; do PHA_G4W_SCHED=$v timeout -k 10 200 python tools/bench_g4w.py > $OUT/g4w_var$v.log 2>&1 || { rc=$?; break; }; echo "var $v"; grep -E "TF|per-step" $OUT/g4w_var$v.log | tail -20; done ;;
+      rc=0; for v in 0 2; do PHA_G4W_SCHED=$v timeout -k 10 200 python tools/bench_g4w.py > $OUT/g4w_var$v.log 2>&1 || { rc=$?; break; }; echo "var $v"; grep -E "TF|per-step" $OUT/g4w_var$v.log | tail -20; done ;;
     prof_g4w)
       export TMPDIR=/tmp
       rm -rf $OUT/prof_g4w; mkdir -p $OUT/prof_g4w
