@@ -114,3 +114,35 @@ __device__ __forceinline__ void fa_block(int BH, int nblk, int G, int& bh, int& 
 }
 
 }  // namespace
+
+namespace pha {
+// Extensions of the 4-wave flash-attention kernels (template bit EXT): an additive score bias
+// (EXT & 1: key-padding mask [B,1,1,Sk] or full [B|1, H|1, S, Sk], fp32, natural-log units,
+// key stride 1) and in-kernel dropout of the attention probabilities (EXT & 2), regenerated bit
+// for bit in the backward from (seed, b*H+h, query, key) — reference: fmha_ref.h:87-172 (src_mask +
+// dropout) and fused_attention_op.cu.
+struct FaExt {
+  const float* bias;
+  long sb, sh, sq;       // bias element strides of batch, head, query (0 = broadcast)
+  unsigned seed;         // dropout stream
+  unsigned thresh;       // drop when the element's 16-bit random < thresh  (thresh = rate * 65536)
+  float keep_scale;      // 1 / (1 - rate)
+};
+
+__device__ __forceinline__ unsigned fa_mix(unsigned x) {   // lowbias32 finaliser
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+// per-(b, h) stream, then per query row, then one 32-bit draw per key pair (16 bits per key)
+__device__ __forceinline__ unsigned fa_stream(unsigned seed, int bh) { return fa_mix(seed ^ ((unsigned)bh * 0x85ebca77U)); }
+__device__ __forceinline__ unsigned fa_row(unsigned sbh, int q) { return fa_mix(sbh + (unsigned)q * 0x9e3779b1U); }
+__device__ __forceinline__ bool fa_keep(unsigned row, int key, unsigned thresh) {
+  const unsigned r = fa_mix(row ^ (unsigned)(key >> 1));
+  return ((key & 1) ? (r >> 16) : (r & 0xffffU)) >= thresh;
+}
+}  // namespace pha
+

@@ -37,11 +37,11 @@ __device__ __forceinline__ int k_lds_off(int row, int chunk) {
   return row * (D * 2) + ((chunk ^ (row & (CH - 1))) * 16);
 }
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EXT = 0>
 __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                      const T* __restrict__ V, T* __restrict__ O,
                                                      float* __restrict__ LSE, int S, int Sk, int H, int Hk,
-                                                     float scale_log2) {
+                                                     float scale_log2, FaExt ex) {
   typedef typename MF<T>::frag frag;
   constexpr int CH = D / 8;
   constexpr int ND = D / 32;            // 32-wide d blocks of O^T
@@ -62,6 +62,9 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
   const T* Qb = Q + ((long)b * S) * qstride + (long)head * D;
   const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * D;
   const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * D;
+  // extensions: this lane's bias row and dropout stream (query on the lane)
+  const float* brow = ((EXT & 1) && q < S) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)q * ex.sq : nullptr;
+  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(ex.seed, b * H + head), q) : 0u;
 
   // Q fragments (B operand of S^T = K Q^T): Q[q][16kk + 8h + j]
   frag qf[NK];
@@ -148,7 +151,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
       }
     }
     // ---- masking (only on diagonal / ragged tiles) + online softmax (query on the lane) ----
-    const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
+    const bool need_mask = (EXT & 1) || (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
     float tmax = -INFINITY;
     if (need_mask) {
 #pragma unroll
@@ -157,7 +160,10 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kb * 32 + acc_row(r, h);
           const bool masked = (key >= Sk) || (CAUSAL && key > q);
-          const float v = masked ? -INFINITY : s[kb][r] * scale_log2;
+          float v = masked ? -INFINITY : s[kb][r] * scale_log2;
+          if constexpr (EXT & 1) {
+            if (!masked && brow) v += brow[key] * kLog2e;
+          }
           s[kb][r] = v;
           tmax = fmaxf(tmax, v);
         }
@@ -198,6 +204,15 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
       }
     psum += __shfl_xor(psum, 32, 64);
     l_run += psum;
+    if constexpr (EXT & 2) {   // dropout on P for the PV product only (the softmax sum is undropped)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kb * 32 + acc_row(r, h);
+          s[kb][r] = fa_keep(drow, key, ex.thresh) ? s[kb][r] * ex.keep_scale : 0.f;
+        }
+    }
 
     // ---- O^T += V^T . P^T ---------------------------------------------------------------
 #pragma unroll
@@ -507,12 +522,12 @@ __device__ __forceinline__ void write_t4(unsigned char* img, int row_stride_byte
   }
 }
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EXT = 0>
 __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                           const T* __restrict__ V, const T* __restrict__ dO,
                                                           const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                           T* __restrict__ dK, T* __restrict__ dV,
-                                                          int S, int Sk, int H, int Hk, float scale) {
+                                                          int S, int Sk, int H, int Hk, float scale, FaExt ex) {
   typedef typename MF<T>::frag frag;
   constexpr int NK = D / 16;
   constexpr int ND = D / 32;
@@ -541,6 +556,9 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
   const float* lse_b = LSE + ((long)b * H + head) * S;
   const float* del_b = DELTA + ((long)b * H + head) * S;
   const float scale_log2 = scale * kLog2e;
+  // extensions (key on the lane): bias column of this key, dropout stream of the (b, h)
+  const float* bcol = ((EXT & 1) && key < Sk) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + key : nullptr;
+  const unsigned dstream = (EXT & 2) ? fa_stream(ex.seed, b * H + head) : 0u;
 
   frag kf[NK], vf[NK];
 #pragma unroll
@@ -606,7 +624,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
       sacc = MF<T>::mma(as_frag<frag>(qa), kf[kk], sacc);
       dpacc = MF<T>::mma(as_frag<frag>(ga), vf[kk], dpacc);
     }
-    const bool need_mask = (qt + BQ > S) || (k0 + 128 > Sk) || (CAUSAL && k0 + wid * 32 + 31 > qt);
+    const bool need_mask = EXT || (qt + BQ > S) || (k0 + 128 > Sk) || (CAUSAL && k0 + wid * 32 + 31 > qt);
     if (need_mask) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -614,8 +632,20 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
         const int qq = qt + ql;
         float p = 0.f, ds = 0.f;
         if (qq < S && key < Sk && !(CAUSAL && key > qq)) {
-          p = exp2f(sacc[r] * scale_log2 - lse_lds[ql] * kLog2e);
-          ds = p * (dpacc[r] - del_lds[ql]);
+          float sv = sacc[r] * scale_log2;
+          if constexpr (EXT & 1) {
+            if (bcol) sv += bcol[(long)qq * ex.sq] * kLog2e;
+          }
+          p = exp2f(sv - lse_lds[ql] * kLog2e);
+          float dpv = dpacc[r];
+          if constexpr (EXT & 2) {   // dV sees the dropped P; dS = P (Z dP / (1-rate) - delta)
+            const bool kp = fa_keep(fa_row(dstream, qq), key, ex.thresh);
+            dpv = kp ? dpv * ex.keep_scale : 0.f;
+            ds = p * (dpv - del_lds[ql]);
+            p = kp ? p * ex.keep_scale : 0.f;
+          } else {
+            ds = p * (dpv - del_lds[ql]);
+          }
         }
         sacc[r] = p;
         dpacc[r] = ds;
@@ -667,11 +697,12 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
   }
 }
 
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EXT = 0>
 __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K,
                                                         const T* __restrict__ V, const T* __restrict__ dO,
                                                         const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                        T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale) {
+                                                        T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale,
+                                                        FaExt ex) {
   typedef typename MF<T>::frag frag;
   constexpr int CH = D / 8;
   constexpr int ND = D / 32;
@@ -697,6 +728,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
   const float scale_log2 = scale * kLog2e;
   const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
   const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
+  const float* brow = ((EXT & 1) && q < S) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)q * ex.sq : nullptr;
+  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(ex.seed, b * H + head), q) : 0u;
 
   frag qf[NK], gf[NK];
 #pragma unroll
@@ -770,7 +803,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
         dp[kb] = MF<T>::mma(as_frag<frag>(c), gf[kk], dp[kb]);
       }
     }
-    const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
+    const bool need_mask = EXT || (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > q0 + wid * 32);
     if (need_mask) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -778,8 +811,14 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
         for (int r = 0; r < 16; ++r) {
           const int kk = k0 + kb * 32 + acc_row(r, h);
           const bool ok = (kk < Sk) && !(CAUSAL && kk > q);
-          const float p = ok ? exp2f(s[kb][r] * scale_log2 - lse2) : 0.f;
-          s[kb][r] = p * (dp[kb][r] - dlt);   // dS^T
+          float sv = s[kb][r] * scale_log2;
+          if constexpr (EXT & 1) {
+            if (ok && brow) sv += brow[kk] * kLog2e;
+          }
+          const float p = ok ? exp2f(sv - lse2) : 0.f;
+          float dpv = dp[kb][r];
+          if constexpr (EXT & 2) dpv = fa_keep(drow, kk, ex.thresh) ? dpv * ex.keep_scale : 0.f;
+          s[kb][r] = p * (dpv - dlt);   // dS^T
         }
     } else {
 #pragma unroll
@@ -1171,7 +1210,7 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
     return (int)hipGetLastError();
   }
   const dim3 grid((S + BM - 1) / BM, H, B), block(256);
-#define FA_L(DD, CC) hipLaunchKernelGGL((fa_fwd_kernel<T, DD, CC>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl)
+#define FA_L(DD, CC) hipLaunchKernelGGL((fa_fwd_kernel<T, DD, CC>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, FaExt{})
   if (D == 128) { if (causal) FA_L(128, true); else FA_L(128, false); }
   else if (D == 64) { if (causal) FA_L(64, true); else FA_L(64, false); }
   else return (int)hipErrorInvalidValue;
@@ -1204,9 +1243,9 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
   const dim3 gkv((Sk + 127) / 128, H, B), gq((S + BM - 1) / BM, H, B), block(256);
 #define FB_L(DD, CC)                                                                                               \
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, DD, CC>), gkv, block, 0, st, (const T*)q, (const T*)k, (const T*)v,   \
-                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale);                              \
+                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, FaExt{});                     \
   hipLaunchKernelGGL((fa_bwd_dq_kernel<T, DD, CC>), gq, block, 0, st, (const T*)q, (const T*)k, (const T*)v,       \
-                     (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale)
+                     (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, FaExt{})
   if (D == 128) { if (causal) { FB_L(128, true); } else { FB_L(128, false); } }
   else if (D == 64) { if (causal) { FB_L(64, true); } else { FB_L(64, false); } }
   else return (int)hipErrorInvalidValue;
@@ -1214,8 +1253,75 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
   return (int)hipGetLastError();
 }
 
+// 4-wave kernels with the bias / dropout extensions; head dims 32, 64, 128
+template <typename T, int EXT>
+int launch_ext(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
+               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D,
+               float scale, int causal, const FaExt& ex, hipStream_t st) {
+  const dim3 grid((S + BM - 1) / BM, H, B), gkv((Sk + 127) / 128, H, B), block(256);
+#define FX_F(DD, CC) hipLaunchKernelGGL((fa_fwd_kernel<T, DD, CC, EXT>), grid, block, 0, st, (const T*)q, (const T*)k, \
+                                        (const T*)v, (T*)o, lse, S, Sk, H, Hk, scale * kLog2e, ex)
+#define FX_B(DD, CC)                                                                                               \
+  hipLaunchKernelGGL((fa_bwd_dkdv_kernel<T, DD, CC, EXT>), gkv, block, 0, st, (const T*)q, (const T*)k,            \
+                     (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, ex);             \
+  hipLaunchKernelGGL((fa_bwd_dq_kernel<T, DD, CC, EXT>), grid, block, 0, st, (const T*)q, (const T*)k,             \
+                     (const T*)v, (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, ex)
+#define FX(DD)                                                                                                     \
+  if (!bwd) { if (causal) FX_F(DD, true); else FX_F(DD, false); }                                                  \
+  else { if (causal) { FX_B(DD, true); } else { FX_B(DD, false); } }
+  if (D == 128) { FX(128) }
+  else if (D == 64) { FX(64) }
+  else if (D == 32) { FX(32) }
+  else return (int)hipErrorInvalidValue;
+#undef FX
+#undef FX_B
+#undef FX_F
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int dispatch_ext(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
+                 const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D,
+                 float scale, int causal, const FaExt& ex, hipStream_t st) {
+  const int ext = (ex.bias ? 1 : 0) | (ex.thresh ? 2 : 0);
+  switch (ext) {
+    case 1: return launch_ext<T, 1>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, st);
+    case 2: return launch_ext<T, 2>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, st);
+    case 3: return launch_ext<T, 3>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, st);
+    default: return launch_ext<T, 0>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, st);
+  }
+}
 
 }  // namespace
+
+// Attention with an additive fp32 bias (natural-log units, key stride 1; element strides sb / sh /
+// sq of batch / head / query, 0 = broadcast: a key-padding mask [B,1,1,Sk] has sh = sq = 0) and/or
+// dropout of the probabilities (rate in [0, 1): 16-bit threshold; seed selects the stream, the
+// backward regenerates the same mask from it). Head dims 32 / 64 / 128.
+PHA_API int pha_flash_attn_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
+                                   int S, int Sk, int H, int Hk, int D, float scale, int causal, const float* bias,
+                                   long sb, long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
+  if (H % Hk || (D != 32 && D != 64 && D != 128) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
+    return (int)hipErrorInvalidValue;
+  FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
+  if (dt == kBF16) return dispatch_ext<bf16_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
+  if (dt == kF16) return dispatch_ext<half_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* dout,
+                                   const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int S,
+                                   int Sk, int H, int Hk, int D, float scale, int causal, const float* bias, long sb,
+                                   long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
+  if (H % Hk || (D != 32 && D != 64 && D != 128) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
+    return (int)hipErrorInvalidValue;
+  FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
+  if (dt == kBF16) return dispatch_ext<bf16_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
+  if (dt == kF16) return dispatch_ext<half_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
+  return (int)hipErrorInvalidValue;
+}
 
 PHA_API int pha_flash_attn_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S,
                                int Sk, int H, int Hk, int D, float scale, int causal, hipStream_t stream) {
@@ -1232,9 +1338,11 @@ PHA_API int pha_flash_attn_bwd_preprocess(int dt, const void* o, const void* dou
   const dim3 grid((rows + rpb - 1) / rpb), block(256);
   if (dt == kBF16) {
     if (D == 128) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 128>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
+    else if (D == 32) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 32>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
     else hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 64>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
   } else if (dt == kF16) {
     if (D == 128) hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 128>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
+    else if (D == 32) hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 32>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
     else hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 64>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
   } else {
     return (int)hipErrorInvalidValue;

@@ -103,10 +103,11 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
 
 
 def _attention(q, k, v, mask, attn_dropout, training, mode, causal=False):
-    """q/k/v: [B, H, S, D]. Flash kernel when mask-free, fused SDPA otherwise."""
-    if mask is None and (attn_dropout == 0.0 or not training):
+    """q/k/v: [B, H, S, D]. The flash kernels (mask and upscale-in-train dropout in-kernel); the
+    downscale-in-infer dropout mode keeps the explicit composite."""
+    if mode in ("upscale_in_train", "upscale-in-train") or attn_dropout == 0.0 or not training:
         o = _ops.fused.flash_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), causal=causal,
-                                       training=training)
+                                       dropout_p=attn_dropout, training=training, mask=mask)
         return o.transpose(1, 2)
     if mode not in ("upscale_in_train", "upscale-in-train") and attn_dropout > 0:
         s = (q @ k.transpose(-1, -2)) / (q.shape[-1] ** 0.5)

@@ -99,11 +99,8 @@ class BertSelfAttention(nn.Layer):
         qkv = self.qkv(x)._t.reshape(B, S, Hn, 3 * Dh)
         q, k, v = qkv.split(Dh, dim=-1)
         drop = self.cfg.attention_dropout if self.training else 0.0
-        if attn_bias is None:
-            o = _ops.flash_attention(q, k, v, causal=False, dropout_p=drop, training=self.training)
-        else:  # padded batch: additive mask [B, 1, 1, S]
-            o = TF.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
-                                                attn_mask=attn_bias.to(q.dtype), dropout_p=drop).transpose(1, 2)
+        # padded batch: additive key mask [B, 1, 1, S]; attention dropout in-kernel
+        o = _ops.flash_attention(q, k, v, causal=False, dropout_p=drop, training=self.training, mask=attn_bias)
         return self.out(_wrap(o.reshape(B, S, Hn * Dh)))
 
 

@@ -22,15 +22,8 @@ __all__ = ["scaled_dot_product_attention", "flash_attention", "sparse_attention"
 def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0, is_causal=False,
                                  training=True, name=None, scale=None):
     q, k, v = query._t, key._t, value._t
-    if attn_mask is None:
-        return _w(_ops.flash_attention(q, k, v, is_causal, dropout_p, scale, training))
-    m = attn_mask._t
-    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
-    if m.dtype != torch.bool:
-        m = m.to(q.dtype)
-    o = torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, attn_mask=m, dropout_p=dropout_p if training else 0.0,
-                                                         is_causal=is_causal, scale=scale)
-    return _w(o.transpose(1, 2))
+    m = None if attn_mask is None else attn_mask._t
+    return _w(_ops.flash_attention(q, k, v, is_causal, dropout_p, scale, training, mask=m))
 
 
 def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False, fixed_seed_offset=None,

@@ -91,9 +91,11 @@ class MultiHeadAttention(Layer):
         mask = _convert_attn_mask(attn_mask, q.dtype)
         drop = self.dropout if self.training else 0.0
         weights = None
-        if mask is None and not self.need_weights and drop == 0.0:
+        if not self.need_weights:
+            # mask and attention dropout run inside the flash kernels (the probabilities are
+            # never materialised); only need_weights=True keeps the explicit composite
             from ... import ops
-            out = ops.flash_attention(q, k, v, False, 0.0, None, self.training)
+            out = ops.flash_attention(q, k, v, False, drop, None, self.training, mask=mask)
         else:
             qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
             scores = torch.matmul(qt, kt.transpose(-1, -2)) * (self.head_dim ** -0.5)

@@ -232,13 +232,18 @@ def embedding(ids, weight, padding_idx=None, sparse=False):
 # ----------------------------------------------------------------------------
 # attention
 # ----------------------------------------------------------------------------
-def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=True):
-    """q, k, v: [B, S, H, D] (Paddle's fused-attention layout). Returns [B, S, H, D]."""
-    if _use_hip(q) and _hip.flash_attn_supported(q, k, v, dropout_p if training else 0.0):
-        return _hip.FlashAttention.apply(q, k, v, bool(causal), scale)
+def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=True, mask=None):
+    """q, k, v: [B, S, H, D] (Paddle's fused-attention layout). Returns [B, S, H, D].
+    mask: additive float (or boolean keep-) mask broadcastable to [B, H, S, Sk]."""
+    drop = dropout_p if training else 0.0
+    if _use_hip(q) and _hip.flash_attn_supported(q, k, v, drop, mask):
+        return _hip.flash_attention_any(q, k, v, causal, scale, mask, drop)
     qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
-    o = TF.scaled_dot_product_attention(qt, kt, vt, dropout_p=dropout_p if training else 0.0,
-                                        is_causal=causal, scale=scale)
+    m = mask
+    if m is not None and m.dtype != torch.bool:
+        m = m.to(q.dtype)
+    o = TF.scaled_dot_product_attention(qt, kt, vt, attn_mask=m, dropout_p=drop, is_causal=causal and m is None,
+                                        scale=scale)
     return o.transpose(1, 2)
 
 

@@ -461,23 +461,129 @@ def multi_tensor_l2norm_sq(tensors):
 # ----------------------------------------------------------------------------
 # flash attention (csrc/kernels/flash_attn.hip)
 # ----------------------------------------------------------------------------
-def flash_attn_supported(q, k, v, dropout_p):
+def flash_attn_supported(q, k, v, dropout_p, mask=None):
+    """shapes the own kernels take: bf16/fp16 [B, S, H, D] with D <= 128 (32 / 64 / 128 natively,
+    other multiples of 8 zero-padded up), GQA (H % Hk == 0); optional additive / boolean mask
+    broadcastable to [B, H, S, Sk] that needs no gradient; optional dropout"""
     import os
     if os.environ.get("PHA_DISABLE_FLASH") == "1":
-        return False
-    if dropout_p and dropout_p > 0:
         return False
     L = _lib.lib
     if L is None or not hasattr(L, "pha_flash_attn_fwd"):
         return False
     if q.dtype not in (torch.bfloat16, torch.float16) or k.dtype != q.dtype or v.dtype != q.dtype:
         return False
+    if q.dim() != 4 or k.dim() != 4 or v.dim() != 4:
+        return False
     B, S, H, D = q.shape
-    if D not in (64, 128) or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
+    if D > 128 or D % 8 or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
         return False
     if H % k.shape[2] != 0:
         return False
+    if dropout_p and not (0.0 < dropout_p < 1.0):
+        return False
+    if mask is not None:
+        if not isinstance(mask, torch.Tensor) or mask.requires_grad or mask.dim() > 4:
+            return False
+        try:
+            torch.broadcast_shapes(tuple(mask.shape), (B, H, S, k.shape[1]))
+        except RuntimeError:
+            return False
     return True
+
+
+def _fa_head_dim(D):
+    return D if D in (32, 64, 128) else (64 if D < 64 else 128)
+
+
+def _fa_bias(mask, B, H, S, Sk, device):
+    """additive fp32 bias view [B, H, S, Sk] (broadcast dims stride 0, keys contiguous) and its
+    (batch, head, query) element strides"""
+    if mask.dtype == torch.bool:
+        mask = torch.zeros(mask.shape, dtype=torch.float32, device=device).masked_fill_(~mask.to(device), float("-inf"))
+    else:
+        mask = mask.to(device=device, dtype=torch.float32)
+    while mask.dim() < 4:
+        mask = mask.unsqueeze(0)
+    if mask.stride(-1) != 1 and mask.shape[-1] != 1:
+        mask = mask.contiguous()
+    if mask.shape[-1] == 1:   # broadcast over keys: materialise the key dimension
+        mask = mask.expand(*mask.shape[:-1], Sk).contiguous()
+    mask = mask.expand(B, H, S, Sk)
+    return mask, (mask.stride(0), mask.stride(1), mask.stride(2))
+
+
+class FlashAttentionExt(torch.autograd.Function):
+    """Flash attention with an additive mask and / or dropout (4-wave kernels, head dims
+    32 / 64 / 128): the dropout mask is a counter-based hash of (seed, b*H+h, query, key),
+    regenerated in the backward instead of stored."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, mask, dropout_p):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, S, H, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+        bias, (sb, sh, sq) = (None, (0, 0, 0)) if mask is None else _fa_bias(mask, B, H, S, Sk, q.device)
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout_p else 0
+        o = torch.empty_like(q)
+        lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        L = _L()
+        if not getattr(L, "_fa_ext_sig", False):
+            P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
+            L.pha_flash_attn_fwd_ext.argtypes = [I, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG, F, U, P]
+            L.pha_flash_attn_fwd_ext.restype = c_int
+            L.pha_flash_attn_bwd_ext.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG,
+                                                 F, U, P]
+            L.pha_flash_attn_bwd_ext.restype = c_int
+            L._fa_ext_sig = True
+        _check(L.pha_flash_attn_fwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, S, Sk, H, Hk, D,
+                                        sc, int(causal), _ptr(bias), sb, sh, sq, float(dropout_p), seed, _stream(q)),
+               "flash_attn_fwd_ext")
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.bias, ctx.strides, ctx.seed = bias, (sb, sh, sq), seed
+        ctx.causal, ctx.scale, ctx.dropout_p = causal, sc, float(dropout_p)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        B, S, H, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        L = _L()
+        delta = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        dq = torch.empty_like(q)
+        dk = torch.empty_like(k) if Hk == H else torch.empty((B, Sk, H, D), dtype=k.dtype, device=k.device)
+        dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
+        _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S),
+                                               c_int(H), c_int(D), _stream(q)), "flash_attn_bwd_preprocess")
+        sb, sh, sq = ctx.strides
+        _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
+                                        _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk, H, Hk, D, ctx.scale, int(ctx.causal),
+                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q)),
+               "flash_attn_bwd_ext")
+        if Hk != H:
+            g = H // Hk
+            dk = dk.view(B, Sk, Hk, g, D).sum(3)
+            dv = dv.view(B, Sk, Hk, g, D).sum(3)
+        return dq, dk, dv, None, None, None, None
+
+
+def flash_attention_any(q, k, v, causal, scale, mask=None, dropout_p=0.0):
+    """dispatch: the 8-wave D=128 / 4-wave D=64 kernels without mask or dropout, the extension
+    kernels otherwise; head dims other than 32 / 64 / 128 are zero-padded up"""
+    D = q.shape[-1]
+    Dp = _fa_head_dim(D)
+    sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+    if Dp != D:
+        pad = (0, Dp - D)
+        q, k, v = (torch.nn.functional.pad(t, pad) for t in (q, k, v))
+    if mask is None and not dropout_p and Dp in (64, 128):
+        o = FlashAttention.apply(q, k, v, bool(causal), sc)
+    else:
+        o = FlashAttentionExt.apply(q, k, v, bool(causal), sc, mask, float(dropout_p or 0.0))
+    return o[..., :D] if Dp != D else o
 
 
 def _bwd_fused(D):

@@ -128,7 +128,8 @@ class Optimizer:
         import os
         if type(self._grad_clip) is ClipGradByGlobalNorm and getattr(self, "_fuses_grad_scale", False) and pgs \
                 and os.environ.get("PHA_FUSED_CLIP", "1") != "0" \
-                and pgs[0][0]._t.is_cuda and all(p.need_clip if hasattr(p, "need_clip") else True for p, _, _ in pgs):
+                and all(p._t.is_cuda for p, _, _ in pgs) \
+                and all(p.need_clip if hasattr(p, "need_clip") else True for p, _, _ in pgs):
             # global-norm clip folded into the fused optimizer kernel: it multiplies the factor in
             # as it reads each gradient (no extra read + write pass over all gradients)
             self._gscale_dev = self._grad_clip.scale_factor([(p, g) for p, g, _ in pgs])
@@ -350,11 +351,11 @@ class Adam(Optimizer):
         # beta1_pow accumulator value (beta1^(t+1) after t updates) for parameters it has not seen.
         steps = self._param_steps([p for p, _, _ in pgs], step_pows)
         groups = {}
-        for i, st in enumerate(steps):
-            groups.setdefault(st, []).append(i)
-        for step, idx in groups.items():
+        for i, st in enumerate(steps):   # one launch per (update index, device): host-offloaded and
+            groups.setdefault((st, params[i].device), []).append(i)   # device parameters may mix
+        for (step, dev), idx in groups.items():
             sel = (lambda xs: [xs[i] for i in idx]) if len(groups) > 1 else (lambda xs: xs)
-            if params[0].is_cuda:
+            if dev.type == "cuda":
                 from ..ops import hip
                 hip.multi_tensor_adam(sel(params), sel(grads), sel(m1), sel(m2), sel(masters), lr, self._beta1,
                                       self._beta2, self._epsilon, step, 0.0, self._decoupled, sel(ratios),
@@ -374,8 +375,8 @@ class Adam(Optimizer):
         cnt = self.__dict__.setdefault("_pstep", {})
         missing = [i for i, p in enumerate(params) if p.name not in cnt]
         if missing:
-            vals = torch.stack([torch.stack([pows[i][0]._t.reshape(()).float(), pows[i][1]._t.reshape(()).float()])
-                                for i in missing]).cpu().tolist()
+            vals = torch.stack([torch.stack([pows[i][0]._t.reshape(()).float().cpu(),
+                                             pows[i][1]._t.reshape(()).float().cpu()]) for i in missing]).tolist()
             for i, (v1, v2) in zip(missing, vals):
                 t = None
                 for beta, v in ((self._beta2, v2), (self._beta1, v1)):

@@ -1,0 +1,429 @@
+"""Custom C++ / HIP operators (reference: python/paddle/utils/cpp_extension/cpp_extension.py:51
+``setup`` and :738 ``load``, extension_utils.py; C++ side paddle/phi/api/ext/op_meta_info.h:635).
+
+Users write ops against ``#include "paddle/extension.h"`` (``paddle_hackathon_amd/include``):
+``PD_BUILD_OP`` / ``PD_BUILD_GRAD_OP`` registration, ``paddle::Tensor``, ``PD_DISPATCH_*``. This
+module compiles the sources for gfx950 — ``.cc/.cpp`` with the host compiler, ``.hip/.cu`` with
+``hipcc --offload-arch=gfx950`` (device code is HIP) — links one shared library, loads it with
+ctypes and turns every registered op into a Python function on framework tensors; an op with a
+``*_grad`` op gets autograd through it.
+
+    mod = load(name="custom_relu", sources=["relu.cc", "relu.hip"])
+    y = mod.custom_relu(x)          # paddle Tensor in, paddle Tensor out; y.backward() works
+
+``setup(name=..., ext_modules=CUDAExtension(sources=[...]))`` builds the same library in-tree
+(``python setup.py install`` style, the reference's packaging entry point) and writes a small
+Python module next to it that loads it.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+
+import torch
+
+__all__ = ["CppExtension", "CUDAExtension", "BuildExtension", "load", "setup", "get_build_directory",
+           "parse_op_info", "load_op_meta_info_and_register_op"]
+
+INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "include")
+ARCH = os.environ.get("PHA_OFFLOAD_ARCH", "gfx950")
+
+# paddle::DataType codes (include/paddle/extension.h) <-> torch dtypes
+_DTYPE_CODES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3, torch.int32: 4,
+                torch.int64: 5, torch.int8: 6, torch.uint8: 7, torch.bool: 8, torch.int16: 9}
+_CODE_DTYPE = {v: k for k, v in _DTYPE_CODES.items()}
+_ATTR_KINDS = {"bool": 0, "int": 1, "float": 2, "int64_t": 3, "std::string": 4, "std::vector<int>": 5,
+               "std::vector<float>": 6, "std::vector<int64_t>": 7, "std::vector<std::string>": 8}
+
+
+def get_build_directory(verbose=False):
+    d = os.environ.get("PADDLE_EXTENSION_DIR") or os.path.join(os.path.expanduser("~"), ".cache",
+                                                                 "paddle_hackathon_amd_extensions")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+class _Ext:
+    def __init__(self, sources, kind, extra_compile_args=None, include_dirs=None, extra_link_args=None,
+                 name=None, **kwargs):
+        self.sources = [sources] if isinstance(sources, str) else list(sources)
+        self.kind = kind
+        self.extra_compile_args = extra_compile_args or {}
+        self.include_dirs = list(include_dirs or [])
+        self.extra_link_args = list(extra_link_args or [])
+        self.name = name
+
+
+def CppExtension(sources, *args, **kwargs):
+    return _Ext(sources, "cpp", *args, **kwargs)
+
+
+def CUDAExtension(sources, *args, **kwargs):
+    """HIP extension (the reference's name): .hip / .cu sources compile with hipcc for gfx950"""
+    return _Ext(sources, "hip", *args, **kwargs)
+
+
+class BuildExtension:
+    """kept for ``cmdclass={'build_ext': BuildExtension}`` call sites; setup() builds directly"""
+
+    @classmethod
+    def with_options(cls, **options):
+        return cls
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: custom HIP operators need ROCm")
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print("[cpp_extension] " + " ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("custom op build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+
+
+def _split_flags(flags, key):
+    if isinstance(flags, dict):
+        return list(flags.get(key, []))
+    return list(flags or [])
+
+
+def _compile(name, sources, build_dir, extra_cxx=None, extra_hip=None, extra_ldflags=None, include_paths=None,
+             verbose=False):
+    """compile + link into ``build_dir/<name>.so``; rebuilt only when sources or flags change"""
+    os.makedirs(build_dir, exist_ok=True)
+    incs = ["-I", INCLUDE_DIR] + sum((["-I", p] for p in (include_paths or [])), [])
+    cxx = ["-O3", "-std=c++17", "-fPIC"] + list(extra_cxx or [])
+    hip = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}"] + list(extra_hip or [])
+    h = hashlib.sha256()
+    for s in sources:
+        with open(s, "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(INCLUDE_DIR, "paddle", "extension.h"), "rb") as f:
+        h.update(f.read())
+    h.update(" ".join(cxx + hip + list(extra_ldflags or []) + incs).encode())
+    digest = h.hexdigest()[:16]
+    target = os.path.join(build_dir, f"{name}.so")
+    stamp = target + ".stamp"
+    if os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == digest:
+        return target
+    hipcc = _hipcc()
+    objs = []
+    for s in sources:
+        obj = os.path.join(build_dir, f"{name}_{os.path.basename(s)}.o")
+        if s.endswith((".hip", ".cu")):
+            _run([hipcc, "-x", "hip", "-c", s, "-o", obj] + hip + incs, verbose)
+        else:
+            # host-only sources still include hip_runtime.h (streams): compile them with hipcc
+            # without offload so they need no device code
+            _run([hipcc, "-c", s, "-o", obj] + cxx + ["-D__HIP_PLATFORM_AMD__"] + incs, verbose)
+        objs.append(obj)
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", target + ".tmp"] + objs
+         + list(extra_ldflags or []), verbose)
+    os.replace(target + ".tmp", target)
+    with open(stamp, "w") as f:
+        f.write(digest + "\n")
+    return target
+
+
+# ---- runtime: registered ops -> Python functions ------------------------------------------------
+class _PhaTensor(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int), ("device", ctypes.c_int), ("ndim", ctypes.c_int),
+                ("shape", ctypes.c_int64 * 8), ("handle", ctypes.c_int64)]
+
+
+class _PhaAttr(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("i", ctypes.c_int64), ("f", ctypes.c_double), ("s", ctypes.c_char_p),
+                ("n", ctypes.c_int), ("iv", ctypes.POINTER(ctypes.c_int64)), ("fv", ctypes.POINTER(ctypes.c_double)),
+                ("sv", ctypes.POINTER(ctypes.c_char_p))]
+
+
+_ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                             ctypes.POINTER(ctypes.c_int64))
+
+
+def parse_op_info(desc):
+    name, ins, outs, attrs = (desc.split("\n") + ["", "", ""])[:4]
+    sp = lambda s, sep: [x.strip() for x in s.split(sep) if x.strip()]  # noqa: E731
+    return {"name": name, "inputs": sp(ins, ","), "outputs": sp(outs, ","), "attrs": sp(attrs, ";")}
+
+
+class _OpLibrary:
+    def __init__(self, path):
+        self.path = path
+        self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        L = self.lib
+        L.pha_ext_num_ops.restype = ctypes.c_int
+        L.pha_ext_op_desc.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.pha_ext_op_desc.restype = ctypes.c_int
+        L.pha_ext_call.argtypes = [ctypes.c_int, ctypes.POINTER(_PhaTensor), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                   ctypes.POINTER(_PhaAttr), ctypes.c_int, ctypes.POINTER(_PhaTensor), ctypes.c_int,
+                                   _ALLOC_FN, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.pha_ext_call.restype = ctypes.c_int
+        self.ops = {}
+        for i in range(L.pha_ext_num_ops()):
+            buf = ctypes.create_string_buffer(1 << 16)
+            if L.pha_ext_op_desc(i, buf, len(buf)) != 0:
+                raise RuntimeError("op description too long")
+            info = parse_op_info(buf.value.decode())
+            info["index"] = i
+            self.ops[info["name"]] = info
+        self._pending = {}
+        self._next = [0]
+
+        def alloc(dtype, device, ndim, shape, handle):
+            shp = [shape[k] for k in range(ndim)]
+            dev = torch.device("cpu") if device < 0 else torch.device("cuda", device)
+            t = torch.empty(shp, dtype=_CODE_DTYPE[dtype], device=dev)
+            h = self._next[0]
+            self._next[0] += 1
+            self._pending[h] = t
+            handle[0] = h
+            return t.data_ptr() if t.numel() else None
+        self._alloc = _ALLOC_FN(alloc)   # keep the callback alive
+
+    def call(self, info, tensors, attrs):
+        """tensors: list (per declared input) of torch tensors or lists of them (Vec inputs)"""
+        flat, groups = [], []
+        for t in tensors:
+            grp = t if isinstance(t, (list, tuple)) else [t]
+            groups.append(len(grp))
+            flat.extend(grp)
+        flat = [t.contiguous() for t in flat]
+        ins = (_PhaTensor * max(1, len(flat)))()
+        for k, t in enumerate(flat):
+            if t.dim() > 8:
+                raise ValueError("custom ops take tensors of at most 8 dimensions")
+            ins[k].data = t.data_ptr() if t.numel() else None
+            ins[k].dtype = _DTYPE_CODES[t.dtype]
+            ins[k].device = t.device.index if t.is_cuda else -1
+            ins[k].ndim = t.dim()
+            for e, d in enumerate(t.shape):
+                ins[k].shape[e] = d
+        gr = (ctypes.c_int * max(1, len(groups)))(*groups)
+        av = (_PhaAttr * max(1, len(attrs)))()
+        keep = []
+        for k, (kind, v) in enumerate(attrs):
+            a = av[k]
+            a.kind = kind
+            if kind in (0, 1, 3):
+                a.i = int(v)
+            elif kind == 2:
+                a.f = float(v)
+            elif kind == 4:
+                b = str(v).encode()
+                keep.append(b)
+                a.s = b
+            elif kind in (5, 7):
+                arr = (ctypes.c_int64 * len(v))(*[int(x) for x in v])
+                keep.append(arr)
+                a.iv, a.n = arr, len(v)
+            elif kind == 6:
+                arr = (ctypes.c_double * len(v))(*[float(x) for x in v])
+                keep.append(arr)
+                a.fv, a.n = arr, len(v)
+            elif kind == 8:
+                bs = [str(x).encode() for x in v]
+                arr = (ctypes.c_char_p * len(bs))(*bs)
+                keep += [bs, arr]
+                a.sv, a.n = arr, len(bs)
+        outs = (_PhaTensor * 16)()
+        err = ctypes.create_string_buffer(4096)
+        dev = next((t.device for t in flat if t.is_cuda), None)
+        stream = torch.cuda.current_stream(dev).cuda_stream if dev is not None else None
+        self._pending = {}
+        n = self.lib.pha_ext_call(info["index"], ins, gr, len(groups), av, len(attrs), outs, 16, self._alloc,
+                                  ctypes.c_void_p(stream), err, len(err))
+        if n < 0:
+            self._pending = {}
+            raise RuntimeError(f"custom op {info['name']} failed: {err.value.decode()}")
+        res = []
+        for k in range(n):
+            o = outs[k]
+            shp = [o.shape[e] for e in range(o.ndim)]
+            if o.handle >= 0 and o.handle in self._pending:
+                t = self._pending[o.handle]
+                res.append(t.reshape(shp) if list(t.shape) != shp else t)
+            else:   # an input returned as output (in-place op)
+                src = next((t for t in flat if t.data_ptr() == (o.data or 0)), None)
+                if src is None:
+                    raise RuntimeError(f"custom op {info['name']}: output {k} is not a framework tensor")
+                res.append(src.reshape(shp))
+        self._pending = {}
+        return res
+
+
+def _attr_kinds(decls):
+    out = []
+    for d in decls:
+        name, _, typ = d.partition(":")
+        typ = typ.strip().replace(" ", "")
+        typ = {"std::vector<int>": "std::vector<int>"}.get(typ, typ)
+        if typ not in _ATTR_KINDS:
+            raise ValueError(f"unsupported custom op attribute type {typ!r} ({d})")
+        out.append((name.strip(), _ATTR_KINDS[typ]))
+    return out
+
+
+def _make_op(lib, info, grad_info):
+    from ...framework.core import Tensor, _wrap
+    ins_decl = info["inputs"]
+    attr_decl = _attr_kinds(info["attrs"])
+    n_out = len(info["outputs"])
+
+    def unwrap(x):
+        if isinstance(x, (list, tuple)):
+            return [unwrap(v) for v in x]
+        return x._t if isinstance(x, Tensor) else torch.as_tensor(x)
+
+    class _Fn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, nflat, groups, attrs, *flat):
+            tensors, pos = [], 0
+            for g in groups:
+                tensors.append(list(flat[pos:pos + g]) if g != 1 or isinstance(g, list) else flat[pos])
+                pos += g
+            outs = lib.call(info, tensors, attrs)
+            ctx.groups, ctx.attrs = groups, attrs
+            ctx.save_for_backward(*flat, *outs)
+            ctx.nflat = len(flat)
+            return tuple(outs) if len(outs) != 1 else outs[0]
+
+        @staticmethod
+        def backward(ctx, *gouts):
+            saved = ctx.saved_tensors
+            flat, outs = saved[:ctx.nflat], saved[ctx.nflat:]
+            named = {}
+            pos = 0
+            for name, g in zip(ins_decl, ctx.groups):
+                named[name] = flat[pos] if g == 1 else list(flat[pos:pos + g])
+                pos += g
+            for name, t, g in zip(info["outputs"], outs, gouts):
+                named[name] = t
+                named[name + "@GRAD"] = g if g is not None else torch.zeros_like(t)
+            args = []
+            for name in grad_info["inputs"]:
+                key = name.replace("@VECTOR", "")
+                if key not in named:
+                    raise RuntimeError(f"grad op {grad_info['name']} input {name} unknown")
+                args.append(named[key])
+            gattrs = [(k, v) for (k, v) in ctx.attrs][:len(grad_info["attrs"])]
+            res = lib.call(grad_info, args, gattrs)
+            by_name = dict(zip([o.replace("@VECTOR", "") for o in grad_info["outputs"]], res))
+            grads = []
+            for name, g in zip(ins_decl, ctx.groups):
+                gr = by_name.get(name + "@GRAD")
+                if g == 1:
+                    grads.append(gr)
+                else:
+                    grads.extend(gr if gr is not None else [None] * g)
+            return (None, None, None) + tuple(grads)
+
+    def op(*args, **kwargs):
+        n_in = len(ins_decl)
+        tens = list(args[:n_in])
+        rest = list(args[n_in:])
+        for name in ins_decl[len(tens):]:
+            tens.append(kwargs.pop(name.replace("@VECTOR", "").lower(), kwargs.pop(name, None)))
+        attrs = []
+        for k, (aname, kind) in enumerate(attr_decl):
+            v = rest[k] if k < len(rest) else kwargs[aname]
+            attrs.append((kind, v))
+        t_in = [unwrap(t) for t in tens]
+        groups, flat = [], []
+        for t in t_in:
+            if isinstance(t, list):
+                groups.append(len(t))
+                flat.extend(t)
+            else:
+                groups.append(1)
+                flat.append(t)
+        if grad_info is not None and torch.is_grad_enabled() and any(t.requires_grad for t in flat):
+            out = _Fn.apply(len(flat), groups, attrs, *flat)
+        else:
+            with torch.no_grad():
+                tensors, pos = [], 0
+                for g, t in zip(groups, t_in):
+                    tensors.append(t)
+                outs = lib.call(info, tensors, attrs)
+            out = tuple(outs) if len(outs) != 1 else outs[0]
+        if isinstance(out, tuple):
+            return [_wrap(o) for o in out]
+        return _wrap(out)
+
+    op.__name__ = info["name"]
+    op.__doc__ = f"custom operator {info['name']}: inputs {ins_decl}, outputs {info['outputs']}, attrs {info['attrs']}"
+    op._n_out = n_out
+    return op
+
+
+class _OpModule:
+    def __init__(self, name, lib):
+        self.__name__ = name
+        self._lib = lib
+        for opname, info in lib.ops.items():
+            if opname.endswith("_grad"):
+                continue
+            grad = lib.ops.get(opname + "_grad")
+            setattr(self, opname, _make_op(lib, info, grad))
+
+    def __repr__(self):
+        return f"<custom op module {self.__name__} from {self._lib.path}>"
+
+
+_LOADED = {}
+
+
+def load_op_meta_info_and_register_op(lib_filename):
+    """load a built custom-op library; returns its op names"""
+    lib = _OpLibrary(lib_filename)
+    _LOADED[lib_filename] = lib
+    return [n for n in lib.ops if not n.endswith("_grad")]
+
+
+def load(name, sources, extra_cxx_cflags=None, extra_cuda_cflags=None, extra_ldflags=None, extra_include_paths=None,
+         build_directory=None, verbose=False):
+    """JIT: compile ``sources`` into ``<build_directory>/<name>.so`` (cached by content) and return
+    a module whose attributes are the registered ops"""
+    build_dir = build_directory or os.path.join(get_build_directory(), name)
+    path = _compile(name, [os.path.abspath(s) for s in sources], build_dir, extra_cxx_cflags, extra_cuda_cflags,
+                    extra_ldflags, extra_include_paths, verbose)
+    lib = _OpLibrary(path)
+    _LOADED[path] = lib
+    return _OpModule(name, lib)
+
+
+def setup(**attr):
+    """Build the extension(s) named by ``ext_modules`` into ``build_directory`` (default: the current
+    directory) and write ``<name>.py`` that loads them, so ``import <name>`` gives the op module."""
+    name = attr.get("name")
+    exts = attr.get("ext_modules")
+    if exts is None:
+        raise ValueError("setup() needs ext_modules=CppExtension(...) / CUDAExtension(...)")
+    exts = exts if isinstance(exts, (list, tuple)) else [exts]
+    out_dir = attr.get("build_directory") or os.getcwd()
+    sources, cxx, hip, ld, incs = [], [], [], [], []
+    for e in exts:
+        sources += [os.path.abspath(s) for s in e.sources]
+        cxx += _split_flags(e.extra_compile_args, "cxx")
+        hip += _split_flags(e.extra_compile_args, "nvcc") + _split_flags(e.extra_compile_args, "hipcc")
+        ld += e.extra_link_args
+        incs += e.include_dirs
+    # the library is lib<name>.so: a <name>.so would shadow the generated <name>.py on import
+    path = _compile("lib" + name, sources, out_dir, cxx, hip, ld, incs, attr.get("verbose", False))
+    with open(os.path.join(out_dir, f"{name}.py"), "w") as f:
+        f.write("# generated by paddle_hackathon_amd.utils.cpp_extension.setup\n"
+                "import os as _os\n"
+                "from paddle_hackathon_amd.utils.cpp_extension import _OpLibrary, _OpModule\n"
+                f"_m = _OpModule({name!r}, _OpLibrary(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "
+                f"{os.path.basename(path)!r})))\n"
+                "globals().update({k: v for k, v in vars(_m).items() if not k.startswith('_')})\n")
+    return path

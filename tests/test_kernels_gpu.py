@@ -745,3 +745,176 @@ def test_multi_tensor_l2norm_sq_vector_and_tail(dt):
     got = hip.multi_tensor_l2norm_sq(ts)
     ref = sum((t.float() ** 2).sum() for t in ts)
     assert abs(float(got) - float(ref)) <= 1e-4 * float(ref)
+
+
+@pytest.mark.parametrize("sched", [0, 2, 4])
+@pytest.mark.parametrize("ako,bko", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (264, 520, 128), (1024, 768, 640)])
+def test_gemm4w_layouts(monkeypatch, sched, ako, bko, M, N, K):
+    """one-wave-per-SIMD 256x256x64 GEMM (gemm4w.hip), every operand layout and schedule vs fp32"""
+    from paddle_hackathon_amd.ops import gemm as G
+    monkeypatch.setenv("PHA_G4W_SCHED", str(sched))
+    torch.manual_seed(2)
+    a = (torch.rand((K, M) if ako else (M, K), device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand((K, N) if bko else (N, K), device="cuda") * 2 - 1).bfloat16()
+    ref = (a.float().t() if ako else a.float()) @ (b.float() if bko else b.float().t())
+    c = G.gemm(a, b, ako, bko)
+    assert (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+def test_gemm4w_fused_epilogues():
+    """bias + tanh-GELU with the pre-activation stored; dGELU against a stored pre-activation with
+    the bias-gradient column sums (fused_gemm_epilogue semantics) vs fp32 torch"""
+    from paddle_hackathon_amd.ops import gemm as G
+    torch.manual_seed(3)
+    M, N, K = 520, 768, 256
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = (torch.rand(K, N, device="cuda") * 2 - 1).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    act, pre = G.gemm(x, w, False, True, bias=bias, act="gelu", aux_out=True)
+    h = x.float() @ w.float() + bias
+    assert (pre.float() - h).abs().max() / h.abs().max() < 1e-2
+    g = TF.gelu(h, approximate="tanh")
+    assert (act.float() - g).abs().max() / g.abs().max() < 1e-2
+    dy = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    wt = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    da = dy.float() @ wt.float().t()
+    hp = pre.float().requires_grad_()
+    dh_ref = torch.autograd.grad(TF.gelu(hp, approximate="tanh"), hp, da)[0]
+    dh, part = G.gemm(dy, wt, False, False, act="dgelu", aux=pre, colsum=True)
+    assert (dh.float() - dh_ref).abs().max() / dh_ref.abs().max() < 1e-2
+    db = G.colsum_finish(part, torch.float32)   # sums of the fp32 values, before the bf16 rounding
+    ref_db = dh_ref.sum(0)
+    assert (db - ref_db).abs().max() / ref_db.abs().max() < 1e-2
+    relu = G.gemm(x, w, False, True, bias=bias, act="relu")
+    assert (relu.float() - torch.relu(h)).abs().max() / h.abs().max() < 1e-2
+
+
+def test_gemm_picks_match_reference():
+    """the per-shape own/library pick entry points (mm_nt / mm_nn / mm_tn / mm_nt_bias) vs fp32"""
+    from paddle_hackathon_amd.ops import gemm as G
+    torch.manual_seed(4)
+    a = (torch.rand(512, 256, device="cuda") * 2 - 1).bfloat16()
+    bt = (torch.rand(384, 256, device="cuda") * 2 - 1).bfloat16()
+    b = (torch.rand(256, 384, device="cuda") * 2 - 1).bfloat16()
+    bias = torch.randn(384, device="cuda").bfloat16()
+    for got, ref in [(G.mm_nt(a, bt), a.float() @ bt.float().t()), (G.mm_nn(a, b), a.float() @ b.float()),
+                     (G.mm_tn(a, (torch.rand(512, 128, device="cuda") * 2 - 1).bfloat16()), None),
+                     (G.mm_nt_bias(a, bt, bias), a.float() @ bt.float().t() + bias.float())]:
+        if ref is not None:
+            assert (got.float() - ref).abs().max() / ref.abs().max() < 1e-2
+
+
+def _attn_ref(q, k, v, causal, scale, bias=None, keep=None, rate=0.0):
+    """fp32 attention on [B, S, H, D] with an additive bias [*, *, S, Sk] and a fixed keep mask"""
+    qt, kt, vt = (t.float().transpose(1, 2) for t in (q, k, v))
+    if kt.shape[1] != qt.shape[1]:
+        g = qt.shape[1] // kt.shape[1]
+        kt, vt = kt.repeat_interleave(g, 1), vt.repeat_interleave(g, 1)
+    s = (qt @ kt.transpose(-1, -2)) * scale
+    if bias is not None:
+        s = s + bias
+    if causal:
+        S, Sk = s.shape[-2:]
+        s = s.masked_fill(torch.ones(S, Sk, dtype=torch.bool, device=s.device).triu(1), float("-inf"))
+    p = torch.softmax(s, -1)
+    if keep is not None:
+        p = p * keep / (1.0 - rate)
+    return (p @ vt).transpose(1, 2)
+
+
+@pytest.mark.parametrize("D", [32, 64, 80, 96, 128])
+@pytest.mark.parametrize("mask_kind", ["keypad", "full", "bool"])
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_mask_and_head_dims(D, mask_kind, causal):
+    """additive key-padding [B,1,1,Sk], full [B,H,S,Sk] and boolean masks, head dims 32..128
+    (80/96 zero-padded), forward + all input gradients vs fp32"""
+    from paddle_hackathon_amd import ops
+    torch.manual_seed(11)
+    B, S, H = 2, 200, 3
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_()
+    k = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_()
+    v = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_()
+    if mask_kind == "keypad":
+        lens = torch.tensor([S - 37, S], device="cuda")
+        mask = torch.where(torch.arange(S, device="cuda")[None, :] < lens[:, None], 0.0, -1e4).reshape(B, 1, 1, S)
+        bias = mask
+    elif mask_kind == "full":
+        mask = torch.randn(B, H, S, S, device="cuda")
+        bias = mask
+    else:
+        mask = torch.rand(B, 1, S, S, device="cuda") > 0.2
+        mask[..., 0] = True
+        bias = torch.zeros(mask.shape, device="cuda").masked_fill(~mask, float("-inf"))
+    scale = 1.0 / math.sqrt(D)
+    o = ops.flash_attention(q, k, v, causal=causal, mask=mask)
+    ref = _attn_ref(q, k, v, causal, scale, bias)
+    assert (o.float() - ref).abs().max() < 3e-2
+    do = torch.randn_like(o)
+    g = torch.autograd.grad(o, (q, k, v), do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    gr = torch.autograd.grad(_attn_ref(qr, kr, vr, causal, scale, bias), (qr, kr, vr), do.float())
+    for a, b in zip(g, gr):
+        assert (a.float() - b).abs().max() / b.abs().max() < 3e-2
+
+
+@pytest.mark.parametrize("rate", [0.1, 0.5])
+@pytest.mark.parametrize("with_mask", [False, True])
+def test_flash_attention_dropout_regenerated_in_backward(rate, with_mask):
+    """in-kernel dropout: the keep mask is read back through V = I (O = dropped P), its density is
+    1 - rate, and forward + backward equal the fp32 reference with that same mask"""
+    from paddle_hackathon_amd import ops
+    B, S, H, D = 2, 64, 2, 64
+    torch.manual_seed(7)
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    k = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    mask = None
+    bias = None
+    if with_mask:
+        mask = torch.where(torch.arange(S, device="cuda") < S - 5, 0.0, -1e4).reshape(1, 1, 1, S).expand(B, 1, 1, S)
+        bias = mask
+    eye = torch.eye(S, device="cuda").bfloat16()[None, :, None, :].expand(B, S, H, S).contiguous()
+    torch.manual_seed(123)
+    pd = ops.flash_attention(q, k, eye, dropout_p=rate, training=True, mask=mask).float()   # [B, S, H, Sk]
+    keep = (pd != 0).transpose(1, 2).float()                                                 # [B, H, S, Sk]
+    valid = torch.ones_like(keep) if mask is None else (bias.expand_as(keep) == 0).float()
+    frac = (keep * valid).sum() / valid.sum()
+    assert abs(frac.item() - (1 - rate)) < 0.03, frac
+    v = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    qg, kg, vg = (t.clone().requires_grad_() for t in (q, k, v))
+    torch.manual_seed(123)   # same stream as the probe above
+    o = ops.flash_attention(qg, kg, vg, dropout_p=rate, training=True, mask=mask)
+    scale = 1.0 / math.sqrt(D)
+    ref = _attn_ref(q, k, v, False, scale, bias, keep, rate)
+    assert (o.float() - ref).abs().max() / ref.abs().max() < 3e-2
+    do = torch.randn_like(o)
+    g = torch.autograd.grad(o, (qg, kg, vg), do)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    gr = torch.autograd.grad(_attn_ref(qr, kr, vr, False, scale, bias, keep, rate), (qr, kr, vr), do.float())
+    for a, b in zip(g, gr):
+        assert (a.float() - b).abs().max() / b.abs().max() < 3e-2
+
+
+def test_bert_attention_runs_on_own_kernels():
+    """BERT-base attention (dropout 0.1, key-padding mask) goes to FlashAttentionExt, not SDPA"""
+    from paddle_hackathon_amd.ops import hip
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.models import bert_config, BertForPretraining
+    calls = {"n": 0}
+    orig = hip.FlashAttentionExt.forward
+
+    def counting(ctx, *a):
+        calls["n"] += 1
+        return orig(ctx, *a)
+    hip.FlashAttentionExt.forward = staticmethod(counting)
+    try:
+        paddle.set_device("gpu:0")
+        cfg = bert_config("bert-tiny")
+        m = paddle.amp.decorate(BertForPretraining(cfg), level="O2", dtype="bfloat16")
+        ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (2, 64), device="cuda"))
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            mlm, nsp = m(ids)
+        (mlm.astype("float32").mean() + nsp.astype("float32").mean()).backward()
+    finally:
+        hip.FlashAttentionExt.forward = orig
+    assert calls["n"] >= cfg.num_layers
