@@ -351,7 +351,8 @@ class Tensor:
 
     @property
     def shape(self):
-        return list(self._t.shape)
+        # the reference has no 0-d tensors: a full reduction / scalar reads as shape [1]
+        return list(self._t.shape) or [1]
 
     @property
     def ndim(self):
@@ -499,8 +500,11 @@ class Tensor:
         t = self._t.detach()
         if t.dtype == torch.bfloat16:
             # paddle exposes bf16 as uint16 bit patterns
-            return t.cpu().view(torch.int16).numpy().view(np.uint16)
-        return t.cpu().numpy()
+            a = t.cpu().view(torch.int16).numpy().view(np.uint16)
+        else:
+            a = t.cpu().numpy()
+        # the reference has no 0-d tensors: scalars come back as shape-(1,) arrays (``loss.numpy()[0]``)
+        return a.reshape(1) if a.ndim == 0 else a
 
     def __array__(self, dtype=None, copy=None):
         a = self.numpy()

@@ -7,7 +7,8 @@ training works unchanged. In eval mode without grad, ``build_strategy.use_hip_gr
 (default on for inference) freezes the program into a HIP graph: one graph launch per
 call instead of one launch per op. ``jit.save`` writes ``.pdmodel``/``.pdiparams``;
 ``jit.load`` returns a ``TranslatedLayer`` that runs the saved program.
-Data-dependent Python control flow is specialised at trace time (no AST transcription).
+Data-dependent Python control flow (``if`` / ``while`` / ``for range`` on tensors) is transcribed
+from the function's AST into static ``cond`` / ``while`` sub-block ops (jit/dy2static.py).
 """
 from __future__ import annotations
 
@@ -157,9 +158,19 @@ class StaticFunction:
         training = self._layer.training if self._layer is not None else None
         return tuple(k), training, torch.is_grad_enabled()
 
+    @property
+    def _static_fn(self):
+        """the function with its Python control flow transcribed (jit/dy2static.py)"""
+        conv = self.__dict__.get("_conv")
+        if conv is None:
+            from .dy2static import convert_function
+            conv = convert_function(self._fn)
+            self.__dict__["_conv"] = conv
+        return conv
+
     def concrete_program_specify_input_spec(self, input_spec=None):
         specs = input_spec or self._input_spec
-        prog, in_vars, out = _trace(self._fn, specs, specs)
+        prog, in_vars, out = _trace(self._static_fn, specs, specs)
         return _Concrete(prog, in_vars, out)
 
     def get_concrete_program(self, *args, **kwargs):
@@ -175,7 +186,7 @@ class StaticFunction:
                 for i, s in enumerate(self._input_spec):
                     if i < len(specs) and isinstance(s, InputSpec):
                         specs[i] = InputSpec(specs[i].shape, specs[i].dtype, s.name or specs[i].name)
-            prog, in_vars, out = _trace(self._fn, specs, args)
+            prog, in_vars, out = _trace(self._static_fn, specs, args)
             c = _Concrete(prog, in_vars, out)
             self._cache[key] = c
         return c
@@ -251,8 +262,10 @@ def save(layer, path, input_spec=None, **configs):
     fn = layer.forward
     if isinstance(fn, StaticFunction):
         spec = input_spec or fn._input_spec
-        fn = fn._fn
+        fn = fn._static_fn
     else:
+        from .dy2static import convert_function
+        fn = convert_function(fn)
         spec = input_spec
     if spec is None:
         raise ValueError("jit.save needs input_spec (or a to_static layer with input_spec)")
@@ -292,29 +305,10 @@ class TranslatedLayer(Layer):
 
 
 def load(path, **configs):
+    """``path.pdmodel`` (ProgramDesc) + ``path.pdiparams`` (save_combine) -> TranslatedLayer whose
+    parameters are the loaded persistables marked ``is_parameter``"""
     prog, feeds, fetches = _static.load_inference_model(path)
-    # parameters loaded as plain tensors: promote to trainable Parameters in place
-    for op in prog.global_block().ops:
-        op.args = tuple(_promote(a) for a in op.args)
-        op.kwargs = {k: _promote(v) for k, v in op.kwargs.items()}
     return TranslatedLayer(prog, feeds, fetches)
-
-
-_promoted = {}
-
-
-def _promote(a):
-    if isinstance(a, Tensor) and not isinstance(a, (Parameter, Variable)) and a._t.is_floating_point():
-        p = _promoted.get(id(a))
-        if p is None:
-            p = Parameter(data=a._t.clone(), name=a.name)
-            _promoted[id(a)] = p
-        return p
-    if isinstance(a, list):
-        return [_promote(x) for x in a]
-    if isinstance(a, tuple):
-        return tuple(_promote(x) for x in a)
-    return a
 
 
 class TracedLayer:

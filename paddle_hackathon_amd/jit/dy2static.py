@@ -1,0 +1,437 @@
+"""Dygraph-to-static AST transcription of Python control flow (reference:
+python/paddle/fluid/dygraph/dygraph_to_static/program_translator.py:991, ifelse_transformer.py:46,
+loop_transformer.py:475, return_transformer.py, logical_transformer.py, convert_operators.py).
+
+``convert_function(fn)`` parses ``fn``'s source and rewrites
+
+  * ``if <test>: A else: B``  ->  two nested functions over the names either branch assigns and
+    ``names = __pha_jst__.convert_ifelse(test, true_fn, false_fn, (current values))``
+  * ``if c: return x`` / ``if c: return x else: return y`` (early returns): the statements after an
+    ``if`` whose body returns move into its ``else`` so both branches return, then
+    ``return __pha_jst__.convert_ifelse(...)``
+  * ``while <test>: body``  ->  cond / body functions over the loop-carried names and
+    ``names = __pha_jst__.convert_while_loop(cond_fn, body_fn, (current values))``
+  * ``for i in range(a, b, s): body``  ->  an index ``while`` loop (then as above)
+  * ``a and b`` / ``a or b`` / ``not a`` in tests  ->  ``convert_logical_*`` (tensor-aware, lazy)
+
+At run time the ``convert_*`` helpers look at the predicate: a static ``Variable`` (tracing under
+``jit.to_static``) records ``static.nn.cond`` / ``while_loop`` sub-blocks, so the traced Program
+keeps the data-dependent control flow; a dygraph Tensor or a Python value just runs the Python
+branch / loop. Loops and branches containing ``break`` / ``continue`` (or a ``return`` that the
+lifting above cannot reach) are left as Python and must then have Python predicates.
+"""
+from __future__ import annotations
+
+import ast
+import functools
+import inspect
+import textwrap
+
+from ..framework.core import Tensor
+
+JST = "__pha_jst__"
+
+
+class _Undefined:
+    """value of a name not bound yet when control flow starts"""
+    _inst = None
+
+    def __new__(cls):
+        if cls._inst is None:
+            cls._inst = super().__new__(cls)
+        return cls._inst
+
+    def __repr__(self):
+        return "UNDEFINED"
+
+
+UNDEFINED = _Undefined()
+
+
+# ---------------------------------------------------------------------------------------------
+# runtime helpers (the __pha_jst__ namespace)
+# ---------------------------------------------------------------------------------------------
+def _is_static_var(x):
+    from ..static.program import Variable
+    return isinstance(x, Variable)
+
+
+def ld(getter):
+    try:
+        return getter()
+    except NameError:
+        return UNDEFINED
+
+
+def _to_bool(x):
+    if isinstance(x, Tensor):
+        return bool(x._t.reshape(-1)[0].item())
+    return bool(x)
+
+
+def convert_ifelse(pred, true_fn, false_fn, args):
+    if _is_static_var(pred):
+        from ..static import control_flow
+        # a name bound in only one branch reads as zeros of the other branch's shape / dtype on the
+        # branch that leaves it unbound (the reference's UndefinedVar placeholder)
+        return control_flow.cond(pred, lambda: true_fn(*args), lambda: false_fn(*args), undefined=UNDEFINED)
+    return true_fn(*args) if _to_bool(pred) else false_fn(*args)
+
+
+def convert_while_loop(cond_fn, body_fn, loop_vars):
+    loop_vars = tuple(loop_vars)
+    c = cond_fn(*loop_vars)
+    if _is_static_var(c):
+        # tensor-dependent loop: one `while` op (variables first bound inside the body start UNDEFINED)
+        from ..static import control_flow
+        out = control_flow.while_loop(cond_fn, lambda *a: list(body_fn(*a)), list(loop_vars), undefined=UNDEFINED)
+        return tuple(out)
+    while _to_bool(c):
+        loop_vars = tuple(body_fn(*loop_vars))
+        c = cond_fn(*loop_vars)
+    return loop_vars
+
+
+def convert_logical_and(*getters):
+    val = getters[0]()
+    for g in getters[1:]:
+        if _is_static_var(val) or isinstance(val, Tensor):
+            from .. import tensor as _T
+            nxt = g()
+            val = _T.logical_and(val, nxt if isinstance(nxt, Tensor) else _const_like(val, nxt))
+        else:
+            if not val:
+                return val
+            val = g()
+    return val
+
+
+def convert_logical_or(*getters):
+    val = getters[0]()
+    for g in getters[1:]:
+        if _is_static_var(val) or isinstance(val, Tensor):
+            from .. import tensor as _T
+            nxt = g()
+            val = _T.logical_or(val, nxt if isinstance(nxt, Tensor) else _const_like(val, nxt))
+        else:
+            if val:
+                return val
+            val = g()
+    return val
+
+
+def convert_logical_not(x):
+    if _is_static_var(x) or isinstance(x, Tensor):
+        from .. import tensor as _T
+        return _T.logical_not(x)
+    return not x
+
+
+def _const_like(ref, v):
+    from ..framework import core
+    return core.to_tensor(bool(v))
+
+
+def range_cond(i, stop, step):
+    if isinstance(step, Tensor) or _is_static_var(step):
+        raise ValueError("dy2static: range() step must be a Python number")
+    return i < stop if step > 0 else i > stop
+
+
+def convert_numpy(x):
+    """``t.numpy()`` inside converted code: the symbolic tensor itself while tracing"""
+    return x if _is_static_var(x) else x.numpy()
+
+
+class _JstNamespace:
+    UNDEFINED = UNDEFINED
+    convert_numpy = staticmethod(convert_numpy)
+    ld = staticmethod(ld)
+    convert_ifelse = staticmethod(convert_ifelse)
+    convert_while_loop = staticmethod(convert_while_loop)
+    convert_logical_and = staticmethod(convert_logical_and)
+    convert_logical_or = staticmethod(convert_logical_or)
+    convert_logical_not = staticmethod(convert_logical_not)
+    range_cond = staticmethod(range_cond)
+
+
+# ---------------------------------------------------------------------------------------------
+# AST analysis / transformation
+# ---------------------------------------------------------------------------------------------
+def _assigned(stmts):
+    """names bound by ``stmts`` (not descending into nested function / class bodies)"""
+    out = []
+
+    class V(ast.NodeVisitor):
+        def visit_Name(self, n):
+            if isinstance(n.ctx, ast.Store) and n.id not in out:
+                out.append(n.id)
+
+        def visit_FunctionDef(self, n):
+            if n.name not in out:
+                out.append(n.name)
+
+        visit_AsyncFunctionDef = visit_FunctionDef
+
+        def visit_ClassDef(self, n):
+            if n.name not in out:
+                out.append(n.name)
+
+        def visit_Lambda(self, n):
+            pass
+
+    for s in stmts:
+        V().visit(s)
+    gen = ("__pha_true_", "__pha_false_", "__pha_cond_", "__pha_body_")   # generated helper functions
+    return [n for n in out if not n.startswith(gen)]
+
+
+def _contains(stmts, types, stop_at_loops=False):
+    class V(ast.NodeVisitor):
+        found = False
+
+        def generic_visit(self, n):
+            if isinstance(n, types):
+                V.found = True
+                return
+            if isinstance(n, (ast.FunctionDef, ast.AsyncFunctionDef, ast.Lambda, ast.ClassDef)):
+                return
+            if stop_at_loops and isinstance(n, (ast.For, ast.While)):
+                return
+            super().generic_visit(n)
+
+    v = V()
+    V.found = False
+    for s in stmts:
+        v.visit(s)
+    return V.found
+
+
+def _name(id_, ctx=None):
+    return ast.Name(id=id_, ctx=ctx or ast.Load())
+
+
+def _jst_attr(attr):
+    return ast.Attribute(value=_name(JST), attr=attr, ctx=ast.Load())
+
+
+def _call(fn, args):
+    return ast.Call(func=fn, args=args, keywords=[])
+
+
+def _getters(names):
+    """(ld(lambda: a), ld(lambda: b), ...) — UNDEFINED for names not bound yet"""
+    return ast.Tuple(elts=[_call(_jst_attr("ld"), [ast.Lambda(args=_noargs(), body=_name(n))]) for n in names],
+                     ctx=ast.Load())
+
+
+def _noargs():
+    return ast.arguments(posonlyargs=[], args=[], vararg=None, kwonlyargs=[], kw_defaults=[], kwarg=None, defaults=[])
+
+
+def _fndef(name, params, body):
+    return ast.FunctionDef(name=name, args=ast.arguments(posonlyargs=[], args=[ast.arg(arg=p) for p in params],
+                                                         vararg=None, kwonlyargs=[], kw_defaults=[], kwarg=None,
+                                                         defaults=[]),
+                           body=body or [ast.Pass()], decorator_list=[], returns=None, type_comment=None)
+
+
+def _ret_tuple(names):
+    return ast.Return(value=ast.Tuple(elts=[_name(n) for n in names], ctx=ast.Load()))
+
+
+def _assign_tuple(names, value):
+    return ast.Assign(targets=[ast.Tuple(elts=[_name(n, ast.Store()) for n in names], ctx=ast.Store())], value=value)
+
+
+def _always_returns(stmts):
+    if not stmts:
+        return False
+    last = stmts[-1]
+    if isinstance(last, ast.Return):
+        return True
+    if isinstance(last, ast.If):
+        return _always_returns(last.body) and _always_returns(last.orelse)
+    return False
+
+
+def _lift_returns(stmts):
+    """``if c: ...return`` followed by more statements -> those statements become the else branch"""
+    out = []
+    for i, s in enumerate(stmts):
+        if isinstance(s, ast.If):
+            s.body = _lift_returns(s.body)
+            s.orelse = _lift_returns(s.orelse)
+            rest = stmts[i + 1:]
+            if rest and _always_returns(s.body) and not s.orelse and not _contains(rest, (ast.Break, ast.Continue)):
+                s.orelse = _lift_returns(rest)
+                out.append(s)
+                return out
+        out.append(s)
+    return out
+
+
+class _Transformer(ast.NodeTransformer):
+    def __init__(self):
+        self.k = 0
+
+    def _next(self):
+        self.k += 1
+        return self.k
+
+    # ---- tests: logical operators -------------------------------------------------------------
+    def _test(self, node):
+        if isinstance(node, ast.BoolOp):
+            fn = "convert_logical_and" if isinstance(node.op, ast.And) else "convert_logical_or"
+            return _call(_jst_attr(fn), [ast.Lambda(args=_noargs(), body=self._test(v)) for v in node.values])
+        if isinstance(node, ast.UnaryOp) and isinstance(node.op, ast.Not):
+            return _call(_jst_attr("convert_logical_not"), [self._test(node.operand)])
+        return node
+
+    # ---- if ------------------------------------------------------------------------------------
+    def visit_If(self, node):
+        self.generic_visit(node)
+        if _contains(node.body + node.orelse, (ast.Break, ast.Continue), stop_at_loops=True) or \
+                _contains(node.body + node.orelse, (ast.Yield, ast.YieldFrom, ast.Global, ast.Nonlocal)):
+            return node
+        body_ret, else_ret = _always_returns(node.body), _always_returns(node.orelse)
+        has_ret = _contains(node.body + node.orelse, (ast.Return,))
+        k = self._next()
+        tname, fname = f"__pha_true_{k}", f"__pha_false_{k}"
+        test = self._test(node.test)
+        if has_ret:
+            if not (body_ret and else_ret):
+                return node   # a return the lifting could not pair: keep Python semantics
+            names = []
+            tdef = _fndef(tname, names, node.body)
+            fdef = _fndef(fname, names, node.orelse)
+            call = _call(_jst_attr("convert_ifelse"), [test, _name(tname), _name(fname), _getters(names)])
+            return [tdef, fdef, ast.Return(value=call)]
+        names = _assigned(node.body + node.orelse)
+        tdef = _fndef(tname, names, node.body + [_ret_tuple(names)])
+        fdef = _fndef(fname, names, (node.orelse or []) + [_ret_tuple(names)])
+        call = _call(_jst_attr("convert_ifelse"), [test, _name(tname), _name(fname), _getters(names)])
+        if names:
+            return [tdef, fdef, _assign_tuple(names, call)]
+        return [tdef, fdef, ast.Expr(value=call)]
+
+    # ---- while ---------------------------------------------------------------------------------
+    def visit_While(self, node):
+        self.generic_visit(node)
+        if node.orelse or _contains(node.body, (ast.Break, ast.Continue, ast.Return), stop_at_loops=True) or \
+                _contains(node.body, (ast.Yield, ast.YieldFrom, ast.Global, ast.Nonlocal)):
+            return node
+        names = _assigned(node.body)
+        k = self._next()
+        cname, bname = f"__pha_cond_{k}", f"__pha_body_{k}"
+        cdef = _fndef(cname, names, [ast.Return(value=self._test(node.test))])
+        bdef = _fndef(bname, names, node.body + [_ret_tuple(names)])
+        call = _call(_jst_attr("convert_while_loop"), [_name(cname), _name(bname), _getters(names)])
+        if names:
+            return [cdef, bdef, _assign_tuple(names, call)]
+        return [cdef, bdef, ast.Expr(value=call)]
+
+    # ---- for i in range(...) -------------------------------------------------------------------
+    def visit_For(self, node):
+        it = node.iter
+        if not (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"
+                and not it.keywords and 1 <= len(it.args) <= 3 and isinstance(node.target, ast.Name)
+                and not node.orelse):
+            self.generic_visit(node)
+            return node
+        if _contains(node.body, (ast.Break, ast.Continue, ast.Return), stop_at_loops=True):
+            self.generic_visit(node)
+            return node
+        k = self._next()
+        idx, stop, step = f"__pha_idx_{k}", f"__pha_stop_{k}", f"__pha_step_{k}"
+        a = it.args
+        start_e = a[0] if len(a) >= 2 else ast.Constant(value=0)
+        stop_e = a[1] if len(a) >= 2 else a[0]
+        step_e = a[2] if len(a) == 3 else ast.Constant(value=1)
+        pre = [ast.Assign(targets=[_name(idx, ast.Store())], value=start_e),
+               ast.Assign(targets=[_name(stop, ast.Store())], value=stop_e),
+               ast.Assign(targets=[_name(step, ast.Store())], value=step_e)]
+        body = [ast.Assign(targets=[_name(node.target.id, ast.Store())], value=_name(idx))] + node.body + [
+            ast.Assign(targets=[_name(idx, ast.Store())],
+                       value=ast.BinOp(left=_name(idx), op=ast.Add(), right=_name(step)))]
+        loop = ast.While(test=_call(_jst_attr("range_cond"), [_name(idx), _name(stop), _name(step)]), body=body,
+                         orelse=[])
+        # loop-carried set must include the hidden index: it is assigned in the body
+        res = self.visit_While(loop)
+        return pre + (res if isinstance(res, list) else [res])
+
+    def visit_Call(self, node):
+        self.generic_visit(node)
+        f = node.func
+        if isinstance(f, ast.Attribute) and f.attr == "numpy" and not node.args and not node.keywords:
+            return _call(_jst_attr("convert_numpy"), [f.value])
+        return node
+
+    def visit_FunctionDef(self, node):
+        if node.name.startswith("__pha_"):
+            return node
+        node.body = _lift_returns(node.body)
+        self.generic_visit(node)
+        return node
+
+
+def _transform_source(fn):
+    src = textwrap.dedent(inspect.getsource(fn))
+    tree = ast.parse(src)
+    fdef = tree.body[0]
+    if not isinstance(fdef, (ast.FunctionDef, ast.AsyncFunctionDef)):
+        raise TypeError("not a function definition")
+    fdef.decorator_list = []
+    _Transformer().visit(fdef)
+    ast.fix_missing_locations(tree)
+    return tree, fdef.name
+
+
+@functools.lru_cache(maxsize=None)
+def _convert_cached(fn):
+    tree, name = _transform_source(fn)
+    free = fn.__code__.co_freevars
+    glb = fn.__globals__
+    if JST not in glb:
+        glb[JST] = _JstNamespace
+    if free:   # rebuild the closure: a factory taking the free variables' current values
+        factory = ast.FunctionDef(name="__pha_factory", args=ast.arguments(
+            posonlyargs=[], args=[ast.arg(arg=v) for v in free], vararg=None, kwonlyargs=[], kw_defaults=[],
+            kwarg=None, defaults=[]), body=[tree.body[0], ast.Return(value=_name(name))], decorator_list=[],
+            returns=None, type_comment=None)
+        tree = ast.Module(body=[factory], type_ignores=[])
+        ast.fix_missing_locations(tree)
+    code = compile(tree, filename=f"<dy2static {getattr(fn, '__qualname__', name)}>", mode="exec")
+    ns = {}
+    exec(code, glb, ns)
+    if free:
+        cells = [c.cell_contents for c in fn.__closure__]
+        new = ns["__pha_factory"](*cells)
+    else:
+        new = ns[name]
+    new.__defaults__ = fn.__defaults__
+    new.__kwdefaults__ = fn.__kwdefaults__
+    new.__pha_converted__ = True
+    functools.update_wrapper(new, fn)
+    return new
+
+
+def convert_function(fn):
+    """the control-flow-converted version of ``fn`` (a bound method stays bound), or ``fn`` itself
+    when its source is unavailable"""
+    if getattr(fn, "__pha_converted__", False):
+        return fn
+    target = fn.__func__ if inspect.ismethod(fn) else fn
+    if not inspect.isfunction(target):
+        return fn
+    try:
+        new = _convert_cached(target)
+    except (OSError, TypeError, SyntaxError, IndentationError):
+        return fn
+    return new.__get__(fn.__self__, type(fn.__self__)) if inspect.ismethod(fn) else new
+
+
+def transformed_code(fn):
+    """the source of the transformed function (for inspection / ``jit.set_code_level``)"""
+    tree, _ = _transform_source(fn.__func__ if inspect.ismethod(fn) else fn)
+    return ast.unparse(tree)

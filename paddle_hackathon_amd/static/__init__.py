@@ -15,7 +15,7 @@ from ..framework.io import save as _save_obj, load as _load_obj
 from .program import (Variable, Program, Block, OpDesc, default_main_program, default_startup_program,  # noqa: F401
                       program_guard, data, Executor, global_scope, scope_guard, append_backward, gradients,
                       enable_static, disable_static, name_scope, CompiledProgram, BuildStrategy, ExecutionStrategy,
-                      InputSpec, Scope, run_program, serialize_program_dict, deserialize_program_dict)
+                      InputSpec, Scope, run_program)
 from . import nn  # noqa: F401
 
 __all__ = ["BuildStrategy", "CompiledProgram", "ExecutionStrategy", "Executor", "ExponentialMovingAverage", "InputSpec",
@@ -200,9 +200,8 @@ def save(program, model_path, protocol=4, **configs):
     if d:
         os.makedirs(d, exist_ok=True)
     _save_obj({k: v for k, v in _params_of(program).items()}, base + ".pdparams", protocol)
-    with open(base + ".pdmodel", "w") as f:
-        prog, _ = serialize_program_dict(program, [v for v in program.list_vars() if getattr(v, "is_data", False)], [])
-        json.dump(prog, f)
+    save_to_file(base + ".pdmodel", serialize_program([v for v in program.list_vars() if getattr(v, "is_data", False)],
+                                                      [], program=program))
 
 
 def load(program, model_path, executor=None, var_list=None):
@@ -223,47 +222,51 @@ def set_program_state(program, state_dict):
             own[k].set_value(np.asarray(v) if not isinstance(v, Tensor) else v.numpy())
 
 
+def _as_list(v):
+    return list(v) if isinstance(v, (list, tuple)) else [v]
+
+
 def serialize_program(feed_vars, fetch_vars, **kwargs):
+    """ProgramDesc bytes (framework.proto wire format; static/serialize.py)"""
+    from .serialize import serialize_program_bytes
     program = kwargs.get("program") or default_main_program()
-    feed_vars = feed_vars if isinstance(feed_vars, (list, tuple)) else [feed_vars]
-    fetch_vars = fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars]
-    d, consts = serialize_program_dict(program, feed_vars, fetch_vars)
-    d["const_names"] = sorted(consts)
-    return json.dumps(d).encode()
+    return serialize_program_bytes(program, _as_list(feed_vars), _as_list(fetch_vars))
 
 
 def serialize_persistables(feed_vars, fetch_vars, executor=None, **kwargs):
+    """the persistables the pruned program reads, as one save_combine stream sorted by name"""
+    from .serialize import serialize_persistables_bytes
     program = kwargs.get("program") or default_main_program()
-    feed_vars = feed_vars if isinstance(feed_vars, (list, tuple)) else [feed_vars]
-    fetch_vars = fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars]
-    _, consts = serialize_program_dict(program, feed_vars, fetch_vars)
-    import io
-    buf = io.BytesIO()
-    _save_obj({k: v for k, v in consts.items()}, buf)
-    return buf.getvalue()
+    return serialize_persistables_bytes(program, _as_list(feed_vars), _as_list(fetch_vars))
 
 
 def deserialize_program(data):
-    d = json.loads(data.decode() if isinstance(data, (bytes, bytearray)) else data)
-    return _ProgramStub(d)
+    from .serialize import parse_program
+    return _ProgramStub(parse_program(data))
 
 
 class _ProgramStub:
-    """A deserialised program whose constants arrive later (deserialize_persistables)."""
+    """A deserialised ProgramDesc whose persistable values arrive with deserialize_persistables."""
 
-    def __init__(self, d):
-        self.desc = d
+    def __init__(self, desc):
+        self.desc = desc
         self.program = None
+
+    @property
+    def num_blocks(self):
+        return len(self.desc.blocks)
 
 
 def deserialize_persistables(program, data, executor=None):
-    import io
-    consts = _load_obj(io.BytesIO(data))
+    from .serialize import desc_to_program, load_persistables
     if isinstance(program, _ProgramStub):
-        prog, feeds, fetches = deserialize_program_dict(program.desc, consts)
+        persist = load_persistables(program.desc, data)
+        prog, feeds, fetches = desc_to_program(program.desc, persist)
         program.program, program.feeds, program.fetches = prog, feeds, fetches
         return prog
-    set_program_state(program, {k: v for k, v in consts.items()})
+    from .serialize import program_to_desc
+    desc, _ = program_to_desc(program, [], [])
+    set_program_state(program, {k: v for k, v in load_persistables(desc, data).items()})
     return program
 
 
@@ -282,7 +285,8 @@ def normalize_program(program, feed_vars, fetch_vars):
 
 
 def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, **kwargs):
-    """Writes ``{prefix}.pdmodel`` (JSON op list) and ``{prefix}.pdiparams`` (parameters + constants)."""
+    """Writes ``{prefix}.pdmodel`` (a framework.proto ProgramDesc with feed/fetch ops) and
+    ``{prefix}.pdiparams`` (the persistables as one save_combine LoDTensor stream, sorted by name)."""
     program = kwargs.get("program") or default_main_program()
     program = program.clone(for_test=True)
     d = os.path.dirname(path_prefix)

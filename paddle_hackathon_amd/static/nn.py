@@ -286,7 +286,13 @@ def _cond(pred, true_fn, false_fn):
 
 
 def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
-    return static_op(_cond, "cond")(pred, true_fn, false_fn)
+    """dynamic mode / Python predicate: run the taken branch; static Variable predicate: record
+    both branches as sub-blocks and one conditional_block op (static/control_flow.py)"""
+    from .program import Variable
+    if isinstance(pred, Variable):
+        from . import control_flow
+        return control_flow.cond(pred, true_fn, false_fn)
+    return _cond(pred, true_fn, false_fn)
 
 
 def _case(preds, fns, default):
@@ -327,7 +333,12 @@ def _while(cond_fn, body, loop_vars):
 
 
 def while_loop(cond, body, loop_vars, is_test=False, name=None):
-    return static_op(_while, "while_loop")(cond, body, list(loop_vars))
+    from .program import Variable
+    from ..framework import core as _c
+    if not _c.in_dynamic_mode() and any(isinstance(v, Variable) for v in loop_vars):
+        from . import control_flow
+        return control_flow.while_loop(cond, body, loop_vars)
+    return _while(cond, body, list(loop_vars))
 
 
 class StaticRNN:

@@ -90,7 +90,7 @@ class Variable(Tensor):
     def shape(self):
         if self.declared_shape is not None:
             return list(self.declared_shape)
-        return list(self._t.shape)
+        return list(self._t.shape) or [1]
 
     @property
     def stop_gradient(self):
@@ -112,6 +112,20 @@ class Variable(Tensor):
     def __len__(self):
         return self.shape[0]
 
+    # augmented assignment on a symbolic tensor records an out-of-place op (an in-place update of
+    # the meta tensor would vanish from the program)
+    def __iadd__(self, o):
+        return self + o
+
+    def __isub__(self, o):
+        return self - o
+
+    def __imul__(self, o):
+        return self * o
+
+    def __itruediv__(self, o):
+        return self / o
+
     def __deepcopy__(self, memo):
         return self
 
@@ -120,11 +134,16 @@ class Variable(Tensor):
 
 
 class OpDesc:
-    __slots__ = ("type", "fn", "args", "kwargs", "outputs", "attrs")
+    """One recorded op: ``type`` (registered qualified op name, or a control-flow op type), the
+    bound arguments (``kwargs``; Variables are the inputs, everything else the attributes) and the
+    output Variables. Control-flow ops (``conditional_block``, ``while``) carry an ``exec`` handler
+    that runs their sub-blocks (static/control_flow.py)."""
+    __slots__ = ("type", "fn", "args", "kwargs", "outputs", "attrs", "exec")
 
-    def __init__(self, type, fn, args, kwargs, outputs, attrs=None):
+    def __init__(self, type, fn, args, kwargs, outputs, attrs=None, exec=None):
         self.type, self.fn, self.args, self.kwargs, self.outputs = type, fn, args, kwargs, outputs
         self.attrs = attrs or {}
+        self.exec = exec
 
     def input_arg_names(self):
         return [v.name for v in _iter_vars((self.args, self.kwargs))]
@@ -182,7 +201,20 @@ class Program:
         return self.blocks[i]
 
     def current_block(self):
-        return self.blocks[-1]
+        return self.blocks[self._cur] if hasattr(self, "_cur") else self.blocks[0]
+
+    def _create_block(self, parent_idx=None):
+        """new sub-block (control flow) under the current one; recording goes there until
+        _rollback()"""
+        parent = self.current_block().idx if parent_idx is None else parent_idx
+        b = Block(self, len(self.blocks), parent)
+        self.blocks.append(b)
+        self._stack = getattr(self, "_stack", []) + [getattr(self, "_cur", 0)]
+        self._cur = b.idx
+        return b
+
+    def _rollback(self):
+        self._cur = self._stack.pop() if getattr(self, "_stack", None) else 0
 
     @property
     def num_blocks(self):
@@ -193,8 +225,8 @@ class Program:
 
     def all_parameters(self):
         seen, out = set(), []
-        for op in self.global_block().ops:
-            for a in _iter_tensors((op.args, op.kwargs)):
+        for op in (o for b in self.blocks for o in b.ops):
+            for a in _iter_tensors((op.args, op.kwargs, op.attrs.get("captured", []))):
                 if isinstance(a, Parameter) and id(a) not in seen:
                     seen.add(id(a))
                     out.append(a)
@@ -215,7 +247,8 @@ class Program:
                         kwargs[k] = (k == "is_test")
                 if "use_global_stats" in kwargs and "training" in op.kwargs:
                     pass
-            blk.ops.append(OpDesc(op.type, op.fn, op.args, kwargs, op.outputs, dict(op.attrs)))
+            blk.ops.append(OpDesc(op.type, op.fn, op.args, kwargs, op.outputs, dict(op.attrs), op.exec))
+        p.blocks += self.blocks[1:]   # control-flow sub-blocks are shared (their ops reference them)
         p._is_test = for_test
         return p
 
@@ -562,9 +595,7 @@ def run_program(program, feed, fetch_list):
     prev_static = _core._mode.static
     _core._mode.record_depth += 1
     try:
-        for op in blk.ops:
-            out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
-            _bind_outputs(op.outputs, out, env)
+        run_block(program, blk, env)
     finally:
         _core._mode.record_depth -= 1
         _core._mode.static = prev_static
@@ -579,6 +610,20 @@ def run_program(program, feed, fetch_list):
         else:
             raise TypeError(f"cannot fetch {f!r}")
     return res
+
+
+def run_block(program, blk, env):
+    """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor)"""
+    for op in blk.ops:
+        if op.exec is not None:
+            op.exec(program, env, op)
+            continue
+        out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
+        _bind_outputs(op.outputs, out, env)
+
+
+def has_control_flow(program):
+    return len(program.blocks) > 1 or any(op.exec is not None for op in program.global_block().ops)
 
 
 class Executor:
@@ -652,7 +697,8 @@ class CompiledProgram:
 
     def _run(self, feed, fetch_list):
         has_opt = any(op.type.startswith("@") for op in self._program.global_block().ops)
-        if not self._build_strategy.use_hip_graph or has_opt or not torch.cuda.is_available():
+        if not self._build_strategy.use_hip_graph or has_opt or not torch.cuda.is_available() \
+                or has_control_flow(self._program):   # data-dependent branches cannot be captured
             return run_program(self._program, feed, fetch_list)
         key = tuple((k, tuple(np.shape(v if not isinstance(v, Tensor) else v._t)), str(getattr(v, "dtype", "")))
                     for k, v in sorted(feed.items()))
@@ -680,39 +726,6 @@ class CompiledProgram:
 
 
 # ----------------------------------------------------------------------------- serialisation
-def _encode(x, consts):
-    if isinstance(x, Variable):
-        return {"@var": x.name}
-    if isinstance(x, Parameter):
-        consts[x.name] = x
-        return {"@param": x.name}
-    if isinstance(x, Tensor):
-        name = f"@const_{len(consts)}"
-        consts[name] = x
-        return {"@const": name}
-    if isinstance(x, torch.dtype):
-        return {"@dtype": dtype_to_str(x)}
-    if isinstance(x, np.ndarray):
-        return {"@ndarray": x.tolist(), "dtype": str(x.dtype)}
-    if isinstance(x, (np.integer,)):
-        return int(x)
-    if isinstance(x, (np.floating,)):
-        return float(x)
-    if isinstance(x, tuple):
-        return {"@tuple": [_encode(v, consts) for v in x]}
-    if isinstance(x, list):
-        return [_encode(v, consts) for v in x]
-    if isinstance(x, dict):
-        return {"@dict": {k: _encode(v, consts) for k, v in x.items()}}
-    if isinstance(x, (int, float, str, bool)) or x is None:
-        return x
-    if isinstance(x, slice):
-        return {"@slice": [x.start, x.stop, x.step]}
-    if x is Ellipsis:
-        return {"@ellipsis": True}
-    raise TypeError(f"cannot serialise op argument of type {type(x)}")
-
-
 def prune_ops(ops, fetch_vars):
     """Keep only the ops the fetch targets depend on (reference: Program._prune)."""
     if not fetch_vars:
@@ -723,20 +736,8 @@ def prune_ops(ops, fetch_vars):
         if any(id(v) in needed for v in _iter_vars(op.outputs)):
             kept.append(op)
             needed.update(id(v) for v in _iter_vars((op.args, op.kwargs)))
+            needed.update(id(v) for v in _iter_vars(op.attrs.get("captured", [])))
     return kept[::-1]
-
-
-def serialize_program_dict(program, feed_vars, fetch_vars):
-    consts = {}
-    ops = []
-    for op in prune_ops(program.global_block().ops, fetch_vars):
-        if op.type.startswith("@"):
-            continue
-        ops.append({"type": op.type, "args": _encode(list(op.args), consts), "kwargs": _encode(op.kwargs, consts),
-                    "outputs": _encode(op.outputs if isinstance(op.outputs, (list, tuple)) else op.outputs, consts)})
-    feeds = [{"name": v.name, "shape": v.shape, "dtype": dtype_to_str(v._t.dtype)} for v in feed_vars]
-    fetches = [v.name for v in fetch_vars]
-    return {"format": "paddle_hackathon_amd.program/1", "ops": ops, "feeds": feeds, "fetches": fetches}, consts
 
 
 def _resolve_fn(qual):
@@ -748,53 +749,3 @@ def _resolve_fn(qual):
     m = importlib.import_module(mod)
     f = getattr(m, name)
     return getattr(f, "__wrapped_op__", f)
-
-
-def deserialize_program_dict(d, params):
-    prog = Program()
-    blk = prog.global_block()
-    vars_ = {}
-
-    def var(name, meta=None):
-        if name not in vars_:
-            v = Variable(blk, meta if meta is not None else torch.empty(0, device="meta"), name)
-            vars_[name] = v
-            blk.vars[name] = v
-        return vars_[name]
-
-    for f in d["feeds"]:
-        meta = torch.empty([1 if s == -1 else s for s in f["shape"]], dtype=convert_dtype(f["dtype"]), device="meta")
-        v = var(f["name"], meta)
-        v.is_data, v.declared_shape = True, f["shape"]
-
-    def dec(x):
-        if isinstance(x, dict):
-            if "@var" in x:
-                return var(x["@var"])
-            if "@param" in x:
-                return params[x["@param"]]
-            if "@const" in x:
-                return params[x["@const"]]
-            if "@dtype" in x:
-                return convert_dtype(x["@dtype"])
-            if "@ndarray" in x:
-                return np.asarray(x["@ndarray"], dtype=x["dtype"])
-            if "@tuple" in x:
-                return tuple(dec(v) for v in x["@tuple"])
-            if "@dict" in x:
-                return {k: dec(v) for k, v in x["@dict"].items()}
-            if "@slice" in x:
-                return slice(*x["@slice"])
-            if "@ellipsis" in x:
-                return Ellipsis
-        if isinstance(x, list):
-            return [dec(v) for v in x]
-        return x
-
-    for o in d["ops"]:
-        fn = _resolve_fn(o["type"])
-        outs = dec(o["outputs"])
-        blk.append_op(OpDesc(o["type"], fn, tuple(dec(o["args"])), dec(o["kwargs"]), outs))
-    feeds = [vars_[f["name"]] for f in d["feeds"]]
-    fetches = [vars_[n] for n in d["fetches"]]
-    return prog, feeds, fetches

@@ -38,7 +38,16 @@ def _index(idx):
 
 
 def getitem(x, idx):
-    return _wrap(x._t[_index(idx)])
+    t = x._t
+    if t.dim() == 0 and idx is not Ellipsis and idx != ():   # 0-d reads as shape [1] (no 0-d tensors in the reference)
+        t = t.reshape(1)
+    if isinstance(idx, Tensor) and idx._t.numel() == 1 and idx._t.dim() <= 1 and not idx._t.is_floating_point() \
+            and idx._t.dtype != torch.bool:
+        # scalar tensor index (e.g. a traced loop counter): a gather, so the shape is data-independent
+        i = idx._t.reshape(1).to(torch.int64)
+        i = torch.where(i < 0, i + t.shape[0], i)
+        return _wrap(torch.index_select(t, 0, i.to(t.device)).squeeze(0))
+    return _wrap(t[_index(idx)])
 
 
 def setitem(x, idx, value):

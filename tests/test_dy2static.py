@@ -1,0 +1,208 @@
+"""dy2static: Python control flow on tensors inside ``paddle.jit.to_static``.
+
+Modelled on the reference's dygraph_to_static suite
+(python/paddle/fluid/tests/unittests/dygraph_to_static/ifelse_simple_func.py, test_loop.py,
+test_return.py, test_logical.py): each function runs eagerly and through ``to_static`` and the
+two results must agree; one traced program must serve inputs that take different branches /
+iteration counts (the control flow lives in conditional_block / while sub-blocks, not in the
+trace).
+"""
+import numpy as np
+import pytest
+
+import paddle_hackathon_amd as paddle
+from paddle_hackathon_amd.jit.dy2static import convert_function, transformed_code
+
+pytestmark = pytest.mark.timeout(120)
+
+
+def if_else_mean(x):
+    if paddle.mean(x) > 0:
+        y = x + 1
+    else:
+        y = x - 1
+    return y * 2
+
+
+def if_else_numpy_pred(x):
+    # the reference writes predicates through .numpy(); in a trace that is the tensor itself
+    if paddle.mean(x).numpy()[0] > 5:
+        y = x * 3
+    else:
+        y = x / 2
+    return y
+
+
+def if_only_one_branch_binds(x):
+    if paddle.mean(x) > 0:
+        q = x + 10
+    else:
+        z = x - 10      # noqa: F841
+        q = x
+    return q
+
+
+def nested_if_in_while(x):
+    i = paddle.zeros([1], dtype="int64")
+    s = paddle.zeros_like(x)
+    while i < 4 and paddle.sum(s) < 1000:      # data-dependent: a while op, not an unrolled trace
+        if paddle.sum(s) > 20:
+            s = s + 1
+        else:
+            s = s + x
+        i += 1
+    return s
+
+
+def early_return(x):
+    if paddle.sum(x) > 0:
+        return x * 10
+    y = x - 5
+    return y
+
+
+def while_tensor_bound(x):
+    n = paddle.sum(paddle.ones([3], dtype="int64"))
+    i = paddle.zeros([1], dtype="int64")
+    acc = x
+    while i < n:
+        acc = acc * 2
+        i = i + 1
+    return acc
+
+
+def for_range_tensor_stop(x):
+    acc = paddle.zeros_like(x)
+    for k in range(paddle.shape(x)[0]):
+        acc = acc + x[k]
+    return acc
+
+
+def logical_ops(x):
+    s = paddle.sum(x)
+    if s > 0 and s < 100:
+        y = x + 1
+    elif not s > -100 or s > 1000:
+        y = x - 1
+    else:
+        y = x * 0
+    return y
+
+
+def python_control_flow_stays(x, flag=True):
+    # predicates on Python values are evaluated at trace time, as in dygraph
+    out = x
+    for _ in range(3):
+        out = out + 1
+    if flag:
+        out = out * 2
+    return out
+
+
+CASES = [
+    (if_else_mean, [np.ones((2, 3)), -np.ones((2, 3))]),
+    (if_else_numpy_pred, [np.full((2, 2), 10.0), np.full((2, 2), 1.0)]),
+    (if_only_one_branch_binds, [np.ones((3,)), -np.ones((3,))]),
+    (nested_if_in_while, [np.full((2, 2), 1.0), np.full((2, 2), 7.0)]),
+    (early_return, [np.ones((4,)), -np.ones((4,))]),
+    (while_tensor_bound, [np.array([1.0, 2.0])]),
+    (for_range_tensor_stop, [np.arange(6.0).reshape(3, 2)]),
+    (logical_ops, [np.ones((2,)), -np.full((2,), 60.0), np.full((2,), 600.0)]),
+    (python_control_flow_stays, [np.ones((2,))]),
+]
+
+
+@pytest.mark.parametrize("fn,inputs", CASES, ids=[c[0].__name__ for c in CASES])
+def test_static_matches_dygraph(fn, inputs):
+    sf = paddle.jit.to_static(fn)
+    for x in inputs:
+        x = x.astype("float32")
+        ref = fn(paddle.to_tensor(x)).numpy()
+        got = sf(paddle.to_tensor(x)).numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+    # same-shape inputs share ONE traced program: the branches live in its sub-blocks
+    shapes = {x.shape for x in inputs}
+    assert len(sf._cache) == len(shapes)
+
+
+def test_program_holds_control_flow_blocks():
+    sf = paddle.jit.to_static(nested_if_in_while)
+    sf(paddle.to_tensor(np.ones((2, 2), "float32")))
+    prog = sf.concrete_program.program
+    types = [op.type for b in prog.blocks for op in b.ops]
+    assert "while" in types and "conditional_block" in types
+    assert len(prog.blocks) >= 4
+
+
+def test_transformed_code_is_readable():
+    code = transformed_code(if_else_mean)
+    assert "convert_ifelse" in code and "def if_else_mean" in code
+
+
+def test_undefined_in_both_branches_is_an_error_when_used():
+    def f(x):
+        if paddle.mean(x) > 0:
+            a = x   # noqa: F841
+        else:
+            b = x   # noqa: F841
+        return x
+    sf = paddle.jit.to_static(f)
+    np.testing.assert_allclose(sf(paddle.to_tensor(np.ones(2, "float32"))).numpy(), np.ones(2))
+
+
+class GatedNet(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = paddle.nn.Linear(4, 8)
+        self.fc2 = paddle.nn.Linear(8, 1)
+
+    def forward(self, x):
+        h = self.fc1(x)
+        if paddle.mean(h) > 0:
+            h = paddle.nn.functional.relu(h)
+        else:
+            h = paddle.tanh(h) * 2
+        steps = paddle.zeros([1], dtype="int64")
+        while steps < 2:
+            h = h * 0.5 + 0.1
+            steps = steps + 1
+        return self.fc2(h)
+
+
+def test_layer_gradients_through_control_flow():
+    paddle.seed(3)
+    eager = GatedNet()
+    stat = GatedNet()
+    stat.set_state_dict(eager.state_dict())
+    stat = paddle.jit.to_static(stat)
+    opt_e = paddle.optimizer.SGD(0.1, parameters=eager.parameters())
+    opt_s = paddle.optimizer.SGD(0.1, parameters=stat.parameters())
+    rng = np.random.RandomState(0)
+    for step in range(4):
+        x = paddle.to_tensor(rng.randn(5, 4).astype("float32") * (1 if step % 2 else -3))
+        le = paddle.mean(eager(x) ** 2)
+        ls = paddle.mean(stat(x) ** 2)
+        np.testing.assert_allclose(ls.numpy(), le.numpy(), rtol=1e-5, atol=1e-6)
+        le.backward()
+        ls.backward()
+        for pe, ps in zip(eager.parameters(), stat.parameters()):
+            np.testing.assert_allclose(ps.grad.numpy(), pe.grad.numpy(), rtol=1e-4, atol=1e-6)
+        opt_e.step(); opt_e.clear_grad()
+        opt_s.step(); opt_s.clear_grad()
+
+
+def test_jit_save_load_keeps_control_flow(tmp_path):
+    paddle.seed(4)
+    net = GatedNet()
+    net.eval()
+    path = str(tmp_path / "gated")
+    paddle.jit.save(net, path, input_spec=[paddle.static.InputSpec([None, 4], "float32", "x")])
+    loaded = paddle.jit.load(path)
+    for scale in (1.0, -3.0):
+        x = np.random.RandomState(1).randn(3, 4).astype("float32") * scale
+        np.testing.assert_allclose(loaded(paddle.to_tensor(x)).numpy(), net(paddle.to_tensor(x)).numpy(),
+                                   rtol=1e-5, atol=1e-6)
+
+
+def test_convert_function_is_cached():
+    assert convert_function(if_else_mean) is convert_function(if_else_mean)

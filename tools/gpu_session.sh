@@ -29,6 +29,11 @@ for s in "$@"; do
     bench_gpt13b)
       timeout -k 10 600 python bench.py --model gpt3-13b --micro-batch 2 --recompute --steps 3 --warmup 1 > $OUT/bench_gpt13b.log 2>&1; rc=$?
       tail -4 $OUT/bench_gpt13b.log ;;
+    prof_bert)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_bert
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_bert -o run --output-format csv -- python3 $ROOT/bench.py --model bert-base --steps 3 --warmup 2 > $OUT/prof_bert.log 2>&1; rc=$?
+      tail -3 $OUT/prof_bert.log ;;
     bench_resnet)
       timeout -k 10 400 python bench.py --model resnet50 --steps 10 --warmup 3 > $OUT/bench_resnet.log 2>&1; rc=$?
       tail -3 $OUT/bench_resnet.log ;;
