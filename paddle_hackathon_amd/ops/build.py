@@ -37,7 +37,10 @@ def _digest(src_files, flags):
         h.update(os.path.basename(s).encode())
         with open(s, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(flags).encode())
+    # flags name absolute include paths: hash them relative to the package so a tree that moved
+    # (the gpurun snapshot lives at another path) still matches its stamps
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h.update(" ".join(f.replace(root, "<pkg>") for f in flags).encode())
     return h.hexdigest()
 
 

@@ -109,7 +109,11 @@ def _compile(name, sources, build_dir, extra_cxx=None, extra_hip=None, extra_ldf
             h.update(f.read())
     with open(os.path.join(INCLUDE_DIR, "paddle", "extension.h"), "rb") as f:
         h.update(f.read())
-    h.update(" ".join(cxx + hip + list(extra_ldflags or []) + incs).encode())
+    # include paths hashed relative to the package / sources so a moved tree keeps its build
+    src_root = os.path.commonpath([os.path.dirname(os.path.abspath(x)) for x in sources])
+    rel = [f.replace(os.path.dirname(INCLUDE_DIR), "<pkg>").replace(src_root, "<src>")
+           for f in cxx + hip + list(extra_ldflags or []) + incs]
+    h.update(" ".join(rel).encode())
     digest = h.hexdigest()[:16]
     target = os.path.join(build_dir, f"{name}.so")
     stamp = target + ".stamp"
