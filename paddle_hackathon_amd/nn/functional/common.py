@@ -212,7 +212,12 @@ def embedding(x, weight, padding_idx=None, sparse=False, name=None):
     w = weight._t
     if padding_idx is not None and padding_idx < 0:
         padding_idx += w.shape[0]
-    return _w(_ops.embedding(_t(x), w, padding_idx, sparse))
+    ids = _t(x)
+    out = _ops.embedding(ids, w, padding_idx, sparse)
+    if padding_idx is not None:
+        # reference lookup_table_v2: rows of padding_idx read as zeros (and get no gradient)
+        out = out.masked_fill((ids == padding_idx).unsqueeze(-1), 0)
+    return _w(out)
 
 
 def one_hot(x, num_classes, name=None):

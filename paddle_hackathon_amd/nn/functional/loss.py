@@ -71,14 +71,15 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
     flat = logp.reshape(-1, C)
     lf = lab.reshape(-1)
     w = _t(weight)
-    loss = TF.nll_loss(flat, lf, weight=None if w is None else w.float(), ignore_index=ignore_index, reduction="none")
+    loss = TF.nll_loss(flat, lf, weight=None if w is None else w.to(flat.dtype), ignore_index=ignore_index,
+                       reduction="none")
     if label_smoothing:
         smooth = -flat.mean(-1)
         loss = (1 - label_smoothing) * loss + label_smoothing * smooth
     if reduction == "mean":
         if w is not None:
             valid = lf != ignore_index
-            den = w.float()[lf.clamp_min(0)] * valid
+            den = w.to(flat.dtype)[lf.clamp_min(0)] * valid
             return _w(loss.sum() / den.sum())
         valid = (lf != ignore_index).sum().clamp_min(1)
         return _w(loss.sum() / valid)

@@ -30,13 +30,22 @@ def _export(fn):
 # ----------------------------------------------------------------------------
 # unary elementwise
 # ----------------------------------------------------------------------------
+def _round_half_away(t):
+    """reference RoundFunctor is Eigen ``x.round()`` = std::round: halves go away from zero
+    (torch.round rounds them to even)"""
+    if not t.is_floating_point():
+        return t
+    tr = torch.trunc(t)
+    return torch.where((t - tr).abs() == 0.5, tr + torch.sign(t), torch.round(t))
+
+
 _UNARY = {
     "abs": torch.abs, "acos": torch.acos, "asin": torch.asin, "atan": torch.atan,
     "acosh": torch.acosh, "asinh": torch.asinh, "atanh": torch.atanh,
     "ceil": torch.ceil, "cos": torch.cos, "cosh": torch.cosh, "exp": torch.exp,
     "expm1": torch.expm1, "floor": torch.floor, "log": torch.log, "log2": torch.log2,
     "log10": torch.log10, "log1p": torch.log1p, "reciprocal": torch.reciprocal,
-    "round": torch.round, "rsqrt": torch.rsqrt, "sign": torch.sign, "sin": torch.sin,
+    "round": _round_half_away, "rsqrt": torch.rsqrt, "sign": torch.sign, "sin": torch.sin,
     "sinh": torch.sinh, "sqrt": torch.sqrt, "square": torch.square, "tan": torch.tan,
     "tanh": torch.tanh, "erf": torch.erf, "erfinv": torch.erfinv, "lgamma": torch.lgamma,
     "digamma": torch.digamma, "trunc": torch.trunc, "neg": torch.neg, "conj": torch.conj,
@@ -57,6 +66,9 @@ def _make_unary(name, f):
 
 def _make_inplace(name):
     tf = getattr(torch.Tensor, name + "_")
+    if name == "round":
+        def tf(t):
+            return t.copy_(_round_half_away(t))
 
     def op(x, name=None):
         tf(x._t)
