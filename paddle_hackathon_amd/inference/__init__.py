@@ -2,7 +2,12 @@
 analysis_predictor.cc, paddle_analysis_config.h, python/paddle/fluid/inference/wrapper.py).
 
 A Predictor loads a saved inference program (``jit.save`` / ``static.save_inference_model``
-format), optionally casts weights to fp16/bf16 (``PrecisionType``), and runs it; on the
+format: a framework.proto ProgramDesc + save_combine params), runs the IR pass pipeline over it
+(``Config.switch_ir_optim``, default on; ``Config.pass_builder()`` edits the list — conv+BN
+folding, conv+add+ReLU, fc(+act), skip-LayerNorm and multi-head attention fusion, dropout /
+identity-scale removal, constant folding, dead-code elimination; inference/passes.py), with
+``PrecisionType.Half``/``Bfloat16`` the auto-mixed-precision pass (GEMM/conv weights in 16 bit,
+norm parameters fp32, feeds cast on entry), and runs it; on the
 MI355X with ``enable_use_gpu`` the whole forward is captured into a HIP graph per input
 signature (``Config.enable_hip_graph``, default on) so a request costs one graph launch.
 TensorRT / MKLDNN / Lite / XPU switches of the reference are accepted and ignored."""
@@ -95,6 +100,8 @@ class Config:
         self._memory_optim = False
         self._cpu_threads = 1
         self._glog = True
+        self._pass_builder = None
+        self._mp_black_list = set()
 
     # model location ----------------------------------------------------------------
     def set_model(self, prog_file, params_file=None):
@@ -153,6 +160,18 @@ class Config:
 
     def ir_optim(self):
         return self._ir_optim
+
+    def pass_builder(self):
+        if self._pass_builder is None:
+            from .passes import PassStrategy
+            self._pass_builder = PassStrategy()
+        return self._pass_builder
+
+    def delete_pass(self, name):
+        self.pass_builder().delete_pass(name)
+
+    def exp_disable_mixed_precision_ops(self, black_list):
+        self._mp_black_list |= set(black_list)
 
     def enable_memory_optim(self, x=True):
         self._memory_optim = x
@@ -259,6 +278,9 @@ class Predictor:
             self._device = torch.device("cpu")
         if _shared is not None:
             self._prog, self._feeds, self._fetches = _shared
+            self._amp = {PrecisionType.Half: torch.float16,
+                         PrecisionType.Bfloat16: torch.bfloat16}.get(config._precision)
+            self.ir_stats = {}
         else:
             prev = _core._default_device
             _core._default_device = self._device
@@ -266,7 +288,15 @@ class Predictor:
                 self._prog, self._feeds, self._fetches = static.load_inference_model(config._prefix())
             finally:
                 _core._default_device = prev
-            self._cast_params(config._precision)
+            self._fetches = list(self._fetches)
+            self._amp = {PrecisionType.Half: torch.float16,
+                         PrecisionType.Bfloat16: torch.bfloat16}.get(config._precision)
+            self.ir_stats = {}
+            if config.ir_optim():
+                self.ir_stats = config.pass_builder().run(self._prog, self._fetches, amp_dtype=self._amp,
+                                                          black_list=config._mp_black_list)
+            elif self._amp is not None:
+                self._cast_params(config._precision)
         bs = static.BuildStrategy()
         bs.use_hip_graph = bool(config._hip_graph and self._device.type == "cuda")
         self._compiled = static.CompiledProgram(self._prog, bs)
@@ -304,6 +334,8 @@ class Predictor:
             with torch.no_grad():
                 feed = {k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))).to(self._device)
                         for k, v in self._inputs.items()}
+                if self._amp is not None:   # low-precision program: float feeds enter in its dtype
+                    feed = {k: v.to(self._amp) if v.is_floating_point() else v for k, v in feed.items()}
                 outs = self._compiled._run({k: _wrap(v) for k, v in feed.items()}, self._fetches)
         finally:
             _core._default_device = prev
