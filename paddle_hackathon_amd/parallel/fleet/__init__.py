@@ -209,6 +209,10 @@ class Fleet:
             from ..ps import PSOptimizer
             self._ps.strategy = self._strategy
             return PSOptimizer(optimizer, self._ps, self._strategy)
+        if not _core_in_dynamic():
+            # static graph: meta-optimizers rewrite the Program (static_optimizers.py)
+            from .static_optimizers import StaticFleetOptimizer
+            return StaticFleetOptimizer(optimizer, self._strategy)
         if self._hcg is None:
             self.init(is_collective=True)
         from . import meta_optimizers as mo
@@ -380,3 +384,8 @@ def __getattr__(name):   # fleet.elastic, imported lazily (it is also a `python 
         from .. import elastic
         return elastic
     raise AttributeError(name)
+
+
+def _core_in_dynamic():
+    from ...framework import core
+    return core.in_dynamic_mode()

@@ -1,0 +1,97 @@
+"""Static-graph distributed training (fleet meta-optimizers as Program rewrites; reference
+meta_optimizers/raw_program_optimizer.py, sharding_optimizer.py, gradient_merge_optimizer.py).
+Two gloo ranks train a static MLP on halves of the batch; parameters must match one process
+training on the whole batch."""
+import numpy as np
+import pytest
+
+from dist_helper import run_dist
+
+pytestmark = [pytest.mark.dist, pytest.mark.timeout(300)]
+
+X = np.random.RandomState(5).randn(8, 6).astype("float32")
+Y = np.random.RandomState(6).randn(8, 3).astype("float32")
+
+
+def _build(paddle, seed=0):
+    paddle.seed(seed)
+    x = paddle.static.data("x", [None, 6], "float32")
+    y = paddle.static.data("y", [None, 3], "float32")
+    h = paddle.nn.functional.relu(paddle.nn.Linear(6, 16)(x))
+    out = paddle.nn.Linear(16, 3)(h)
+    loss = paddle.mean((out - y) ** 2)
+    return loss
+
+
+def _static_train(rank, world, strategy_kw, steps, opt_name="sgd"):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    from paddle_hackathon_amd.parallel.fleet.static_optimizers import comm_op_types
+    paddle.enable_static()
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        loss = _build(paddle)
+        strategy = fleet.DistributedStrategy()
+        for k, v in strategy_kw.items():
+            setattr(strategy, k, v)
+        inner = paddle.optimizer.SGD(0.1) if opt_name == "sgd" else paddle.optimizer.Adam(0.01)
+        opt = fleet.distributed_optimizer(inner, strategy)
+        opt.minimize(loss)
+    exe = paddle.static.Executor()
+    exe.run(start)
+    half = 8 // world
+    for _ in range(steps):
+        exe.run(main, feed={"x": X[rank * half:(rank + 1) * half], "y": Y[rank * half:(rank + 1) * half]},
+                fetch_list=[loss])
+    params = [p.numpy() for p in main.all_parameters()]
+    return {"params": params, "comm": comm_op_types(main), "types": [op.type for op in main.global_block().ops]}
+
+
+def _single(steps, k_merge=1, opt_name="sgd"):
+    """one process, whole batch; gradient merge = mean of k micro-step gradients"""
+    import paddle_hackathon_amd as paddle
+    paddle.disable_static()
+    paddle.set_device("cpu")
+    paddle.seed(0)
+    l1, l2 = paddle.nn.Linear(6, 16), paddle.nn.Linear(16, 3)
+    ps = l1.parameters() + l2.parameters()
+    opt = paddle.optimizer.SGD(0.1, parameters=ps) if opt_name == "sgd" else paddle.optimizer.Adam(0.01, parameters=ps)
+    for s in range(steps):
+        loss = paddle.mean((l2(paddle.nn.functional.relu(l1(paddle.to_tensor(X)))) - paddle.to_tensor(Y)) ** 2)
+        (loss / k_merge).backward()
+        if (s + 1) % k_merge == 0:
+            opt.step()
+            opt.clear_grad()
+    return [p.numpy() for p in ps]
+
+
+@pytest.mark.parametrize("opt_name", ["sgd", "adam"])
+def test_static_data_parallel_allreduce_ops(opt_name):
+    res = run_dist(_static_train, 2, args=({"fuse_grad_size_in_MB": 0.0005}, 3, opt_name))
+    ref = _single(3, opt_name=opt_name)
+    for r in res:
+        for a, b in zip(r["params"], ref):
+            np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    # gradients go through coalesced all-reduce ops in the Program (several buckets at this size)
+    assert res[0]["comm"].count("c_allreduce_coalesced") >= 2
+    assert "@backward" in res[0]["types"] and "@update" in res[0]["types"]
+
+
+def test_static_sharding_reduce_and_broadcast():
+    res = run_dist(_static_train, 2, args=({"sharding": True}, 3, "adam"))
+    ref = _single(3, opt_name="adam")
+    for r in res:
+        for a, b in zip(r["params"], ref):
+            np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    comm = res[0]["comm"]
+    assert "c_reduce_coalesced" in comm and "c_broadcast_coalesced" in comm and "c_allreduce_coalesced" not in comm
+
+
+def test_static_gradient_merge_single_process():
+    out = _static_train(0, 1, {"gradient_merge": True, "gradient_merge_configs": {"k_steps": 2, "avg": True}}, 4)
+    ref = _single(4, k_merge=2)
+    for a, b in zip(out["params"], ref):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+    assert "conditional_block" in out["types"]
+    import paddle_hackathon_amd as paddle
+    paddle.disable_static()
