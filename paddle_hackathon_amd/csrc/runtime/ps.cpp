@@ -12,6 +12,14 @@
 // optional synchronous-merge mode (the grads of all trainers averaged and applied once,
 // version bumped; pulls may wait for a version).
 //
+// Round 2 depth (reference paddle/fluid/distributed/ps/table/): a CTR accessor rule
+// (ctr_accessor.cc: show/click statistics per feature, embedding + lazily created embedx with
+// their own AdaGrad state, score-based embedx creation, decay/delete shrink and base-threshold
+// save), a spill-to-disk mode of the sparse table (ssd_sparse_table.cc: a bounded in-memory row
+// cache per shard, the coldest rows appended to a per-shard file and read back on access), and a
+// graph table (common_graph_table.cc: weighted adjacency lists + node features, uniform or
+// weighted neighbour sampling without replacement, random node sampling).
+//
 // Wire format (little endian): request  = {u32 magic, u32 cmd, u32 table, u32 arg, u64 n, u64 nbytes} + payload
 //                              response = {i32 status, u32 pad, u64 nbytes} + payload
 #include <arpa/inet.h>
@@ -47,12 +55,14 @@ constexpr int kShards = 64;
 enum Cmd : uint32_t {
   CREATE_DENSE = 1, CREATE_SPARSE = 2, PULL_DENSE = 3, PUSH_DENSE = 4, SET_DENSE = 5, PULL_SPARSE = 6,
   PUSH_SPARSE = 7, BARRIER = 8, SAVE = 9, LOAD = 10, TABLE_SIZE = 11, SHRINK = 12, STOP = 13,
-  PUSH_SPARSE_DELTA = 14, PING = 15,
+  PUSH_SPARSE_DELTA = 14, PING = 15, SET_SPILL = 16,
+  GRAPH_ADD_EDGES = 20, GRAPH_SAMPLE = 21, GRAPH_SET_FEAT = 22, GRAPH_GET_FEAT = 23, GRAPH_RANDOM_NODES = 24,
+  GRAPH_NODE_COUNT = 25,
 };
 
 // optimizer rules applied on the server (sparse_sgd_rule.cc: Naive / AdaGrad (one g2sum per
 // row) / StdAdaGrad (per element) / Adam; SUM = geo-SGD delta accumulation)
-enum Rule : int32_t { SGD = 0, ADAGRAD = 1, STD_ADAGRAD = 2, ADAM = 3, SUM = 4 };
+enum Rule : int32_t { SGD = 0, ADAGRAD = 1, STD_ADAGRAD = 2, ADAM = 3, SUM = 4, CTR = 5 };
 
 #pragma pack(push, 1)
 struct ReqHdr { uint32_t magic, cmd, table, arg; uint64_t n, nbytes; };
@@ -61,6 +71,10 @@ struct TableCfg {
   int32_t rule, dim, sync_trainers, entry_kind;   // entry: 0 always, 1 probability, 2 count filter
   float lr, beta1, beta2, eps, initial_g2sum, initial_range, min_bound, max_bound, entry_value;
   uint64_t seed;
+  // CTR accessor (ctr_accessor.h CtrCommonAccessor parameters)
+  float nonclk_coeff, click_coeff, embedx_threshold, show_click_decay, delete_threshold, delete_after_unseen_days,
+      base_threshold;
+  uint64_t cache_rows;   // spill mode: resident rows per table (0 = unbounded)
 };
 #pragma pack(pop)
 
@@ -98,6 +112,7 @@ int state_width(int rule, int dim) {
     case ADAGRAD: return 1;
     case STD_ADAGRAD: return dim;
     case ADAM: return 2 * dim + 2;   // m, v, beta1^t, beta2^t
+    case CTR: return 6;              // show, click, unseen_days, embed_g2sum, embedx_g2sum, has_embedx
     default: return 0;
   }
 }
@@ -150,6 +165,35 @@ void apply_rule(const TableCfg& c, int rule, float* w, float* st, const float* g
     for (int i = 0; i < dim; ++i) w[i] = std::min(std::max(w[i], c.min_bound), c.max_bound);
 }
 
+inline float ctr_score(const TableCfg& c, const float* st) {
+  return (st[0] - st[1]) * c.nonclk_coeff + st[1] * c.click_coeff;
+}
+
+// one CTR push: p = [show, click, g_embed, g_embedx(dim-1)]; row = [embed_w, embedx | state]
+void apply_ctr(const TableCfg& c, float* w, float* st, const float* p, int dim, std::mt19937_64& rng) {
+  st[0] += p[0];
+  st[1] += p[1];
+  st[2] = 0.f;
+  const float* g = p + 2;
+  float r = c.lr * std::sqrt(c.initial_g2sum / (c.initial_g2sum + st[3]));
+  w[0] -= r * g[0];
+  st[3] += g[0] * g[0];
+  if (st[5] > 0.f) {
+    r = c.lr * std::sqrt(c.initial_g2sum / (c.initial_g2sum + st[4]));
+    double add = 0;
+    for (int i = 1; i < dim; ++i) {
+      w[i] -= r * g[i];
+      add += (double)g[i] * g[i];
+    }
+    st[4] += dim > 1 ? (float)(add / (dim - 1)) : 0.f;
+  } else if (ctr_score(c, st) >= c.embedx_threshold) {   // feature became frequent: create embedx
+    std::uniform_real_distribution<float> u(-c.initial_range, c.initial_range);
+    for (int i = 1; i < dim; ++i) w[i] = c.initial_range > 0.f ? u(rng) : 0.f;
+    st[5] = 1.f;
+  }
+  for (int i = 0; i < dim; ++i) w[i] = std::min(std::max(w[i], c.min_bound), c.max_bound);
+}
+
 struct DenseTable {
   TableCfg cfg;
   std::mutex mu;
@@ -164,18 +208,95 @@ struct SparseRow {
   uint32_t seen = 0;      // training pulls (count-filter entry)
   uint32_t idle = 0;      // shrink passes since the last pull
   bool live = false;      // materialised (admitted by the entry policy)
+  uint64_t last = 0;      // access tick (spill mode: coldest rows leave first)
 };
 
 struct SparseShard {
   std::mutex mu;
   std::unordered_map<uint64_t, SparseRow> rows;
   std::mt19937_64 rng;
+  // spill mode (ssd_sparse_table): rows evicted to an append-only file, id -> byte offset
+  std::unordered_map<uint64_t, uint64_t> disk;
+  FILE* f = nullptr;
+  uint64_t tick = 0;
+  ~SparseShard() {
+    if (f) fclose(f);
+  }
 };
 
 struct SparseTable {
   TableCfg cfg;
   int sw = 0;
   SparseShard shards[kShards];
+  size_t cap_per_shard() const { return cfg.cache_rows ? std::max<size_t>(1, cfg.cache_rows / kShards) : 0; }
+};
+
+// row record in a spill file: u32 seen | f32 v[dim + sw]
+bool spill_read(SparseTable* t, SparseShard& sh, uint64_t id, SparseRow& r) {
+  auto it = sh.disk.find(id);
+  if (it == sh.disk.end() || !sh.f) return false;
+  const size_t w = (size_t)t->cfg.dim + t->sw;
+  r.v.assign(w, 0.f);
+  uint32_t seen = 0;
+  if (fseeko(sh.f, (off_t)it->second, SEEK_SET) != 0 || fread(&seen, 4, 1, sh.f) != 1 ||
+      fread(r.v.data(), 4, w, sh.f) != w)
+    return false;
+  r.seen = seen;
+  r.live = true;
+  sh.disk.erase(it);
+  return true;
+}
+
+void spill_evict(SparseTable* t, SparseShard& sh) {   // keep the hottest 3/4 of the cap resident
+  const size_t cap = t->cap_per_shard();
+  if (!cap || !sh.f || sh.rows.size() <= cap) return;
+  std::vector<std::pair<uint64_t, uint64_t>> age;   // (last access, id)
+  age.reserve(sh.rows.size());
+  for (auto& kv : sh.rows)
+    if (kv.second.live) age.emplace_back(kv.second.last, kv.first);
+  const size_t keep = cap * 3 / 4;
+  if (age.size() <= keep) return;
+  std::nth_element(age.begin(), age.begin() + (age.size() - keep), age.end());
+  fseeko(sh.f, 0, SEEK_END);
+  const size_t w = (size_t)t->cfg.dim + t->sw;
+  for (size_t i = 0; i < age.size() - keep; ++i) {
+    auto it = sh.rows.find(age[i].second);
+    const uint64_t off = (uint64_t)ftello(sh.f);
+    const uint32_t seen = it->second.seen;
+    fwrite(&seen, 4, 1, sh.f);
+    fwrite(it->second.v.data(), 4, w, sh.f);
+    sh.disk[it->first] = off;
+    sh.rows.erase(it);
+  }
+  fflush(sh.f);
+}
+
+// resident row of ``id`` (read back from the spill file if it was evicted); nullptr if unknown
+SparseRow* resident(SparseTable* t, SparseShard& sh, uint64_t id, bool create) {
+  auto it = sh.rows.find(id);
+  if (it == sh.rows.end()) {
+    SparseRow r;
+    const bool from_disk = spill_read(t, sh, id, r);
+    if (!from_disk && !create) return nullptr;
+    it = sh.rows.emplace(id, std::move(r)).first;
+  }
+  it->second.last = ++sh.tick;
+  return &it->second;
+}
+
+struct GNode {
+  std::vector<uint64_t> nbr;
+  std::vector<float> w;
+  std::vector<float> feat;
+};
+
+struct GraphTable {
+  std::mutex mu[kShards];
+  std::unordered_map<uint64_t, GNode> nodes[kShards];
+  std::mt19937_64 rng[kShards];
+  GraphTable() {
+    for (int i = 0; i < kShards; ++i) rng[i].seed(0x9e3779b97f4a7c15ULL * (i + 1));
+  }
 };
 
 struct Server {
@@ -188,6 +309,7 @@ struct Server {
   std::mutex tab_mu;
   std::map<uint32_t, std::unique_ptr<DenseTable>> dense;
   std::map<uint32_t, std::unique_ptr<SparseTable>> sparse;
+  std::map<uint32_t, std::unique_ptr<GraphTable>> graph;
   std::mutex bar_mu;
   std::condition_variable bar_cv;
   std::map<uint32_t, std::pair<uint64_t, uint64_t>> bar;   // tag -> (arrived, generation)
@@ -203,6 +325,12 @@ struct Server {
     std::lock_guard<std::mutex> g(tab_mu);
     auto it = sparse.find(t);
     return it == sparse.end() ? nullptr : it->second.get();
+  }
+  GraphTable* get_graph(uint32_t t) {
+    std::lock_guard<std::mutex> g(tab_mu);
+    auto& p = graph[t];
+    if (!p) p = std::make_unique<GraphTable>();
+    return p.get();
   }
   void wake_all() {
     bar_cv.notify_all();
@@ -226,7 +354,9 @@ void init_row(const TableCfg& c, SparseShard& sh, SparseRow& r, int sw) {
   r.v.assign((size_t)c.dim + sw, 0.f);
   if (c.initial_range > 0.f) {
     std::uniform_real_distribution<float> u(-c.initial_range, c.initial_range);
-    for (int i = 0; i < c.dim; ++i) r.v[i] = u(sh.rng);
+    // CTR: only the 1-d embed starts random; embedx appears once the feature is frequent
+    const int n = c.rule == CTR ? 1 : c.dim;
+    for (int i = 0; i < n; ++i) r.v[i] = u(sh.rng);
   }
   r.live = true;
 }
@@ -240,18 +370,31 @@ bool entry_admits(const TableCfg& c, SparseShard& sh, const SparseRow& r) {
 int32_t save_or_load(Server* s, const ReqHdr& h, const std::string& path) {
   if (SparseTable* t = s->get_sparse(h.table)) {
     const int dim = t->cfg.dim;
-    if (h.cmd == SAVE) {   // arg 1: weights only (the reference's save mode 1, for inference)
-      const int w = h.arg == 1 ? dim : dim + t->sw;
+    if (h.cmd == SAVE) {   // arg 1: weights only (inference); arg 2: CTR base save (score >= base_threshold)
+      const int w = h.arg >= 1 ? dim : dim + t->sw;
+      const bool base = h.arg == 2 && t->cfg.rule == CTR;
       FILE* f = fopen(path.c_str(), "wb");
       if (!f) return -4;
       const int32_t hdr[2] = {dim, w};
       fwrite(hdr, 4, 2, f);
+      auto emit = [&](uint64_t id, const SparseRow& r) {
+        if (!r.live || (base && ctr_score(t->cfg, r.v.data() + dim) < t->cfg.base_threshold)) return;
+        fwrite(&id, 8, 1, f);
+        fwrite(r.v.data(), 4, w, f);
+      };
       for (auto& sh : t->shards) {
         std::lock_guard<std::mutex> g(sh.mu);
-        for (auto& kv : sh.rows) {
-          if (!kv.second.live) continue;
-          fwrite(&kv.first, 8, 1, f);
-          fwrite(kv.second.v.data(), 4, w, f);
+        for (auto& kv : sh.rows) emit(kv.first, kv.second);
+        std::vector<std::pair<uint64_t, uint64_t>> spilled(sh.disk.begin(), sh.disk.end());
+        const size_t rw = (size_t)dim + t->sw;
+        SparseRow r;
+        r.v.assign(rw, 0.f);
+        r.live = true;
+        for (auto& kv : spilled) {   // rows living in the spill file
+          uint32_t seen;
+          if (fseeko(sh.f, (off_t)kv.second, SEEK_SET) == 0 && fread(&seen, 4, 1, sh.f) == 1 &&
+              fread(r.v.data(), 4, rw, sh.f) == rw)
+            emit(kv.first, r);
         }
       }
       fclose(f);
@@ -399,17 +542,19 @@ void handle(Server* s, int fd) {
           SparseShard& sh = t->shards[mix(ids[i]) % kShards];
           std::lock_guard<std::mutex> g(sh.mu);
           if (!h.arg) {   // inference pull: never creates rows
-            auto it = sh.rows.find(ids[i]);
-            if (it != sh.rows.end() && it->second.live) memcpy(o + i * dim, it->second.v.data(), dim * 4);
+            SparseRow* r = resident(t, sh, ids[i], false);
+            if (r && r->live) memcpy(o + i * dim, r->v.data(), dim * 4);
             else memset(o + i * dim, 0, dim * 4);
+            spill_evict(t, sh);
             continue;
           }
-          SparseRow& r = sh.rows[ids[i]];
+          SparseRow& r = *resident(t, sh, ids[i], true);
           ++r.seen;
           r.idle = 0;
           if (!r.live && entry_admits(t->cfg, sh, r)) init_row(t->cfg, sh, r, t->sw);
           if (r.live) memcpy(o + i * dim, r.v.data(), dim * 4);
           else memset(o + i * dim, 0, dim * 4);
+          spill_evict(t, sh);
         }
         break;
       }
@@ -417,16 +562,19 @@ void handle(Server* s, int fd) {
       case PUSH_SPARSE_DELTA: {   // n ids + n x dim grads (or geo-SGD deltas)
         SparseTable* t = s->get_sparse(h.table);
         const int dim = t ? t->cfg.dim : 0;
-        if (!t || h.nbytes != h.n * 8 + h.n * (size_t)dim * 4) { status = -1; break; }
+        const int rule = h.cmd == PUSH_SPARSE_DELTA ? SUM : (t ? t->cfg.rule : 0);
+        const int pw = rule == CTR ? dim + 2 : dim;   // CTR pushes carry show and click
+        if (!t || h.nbytes != h.n * 8 + h.n * (size_t)pw * 4) { status = -1; break; }
         const uint64_t* ids = reinterpret_cast<const uint64_t*>(in.data());
         const float* g = reinterpret_cast<const float*>(in.data() + h.n * 8);
-        const int rule = h.cmd == PUSH_SPARSE_DELTA ? SUM : t->cfg.rule;
         for (uint64_t i = 0; i < h.n; ++i) {
           SparseShard& sh = t->shards[mix(ids[i]) % kShards];
           std::lock_guard<std::mutex> lk(sh.mu);
-          auto it = sh.rows.find(ids[i]);
-          if (it == sh.rows.end() || !it->second.live) continue;   // not admitted: gradient dropped
-          apply_rule(t->cfg, rule, it->second.v.data(), it->second.v.data() + dim, g + i * dim, dim, 1.f);
+          SparseRow* r = resident(t, sh, ids[i], false);
+          if (!r || !r->live) continue;   // not admitted: gradient dropped
+          if (rule == CTR) apply_ctr(t->cfg, r->v.data(), r->v.data() + dim, g + i * pw, dim, sh.rng);
+          else apply_rule(t->cfg, rule, r->v.data(), r->v.data() + dim, g + i * dim, dim, 1.f);
+          spill_evict(t, sh);
         }
         break;
       }
@@ -449,6 +597,7 @@ void handle(Server* s, int fd) {
           for (auto& sh : t->shards) {
             std::lock_guard<std::mutex> g(sh.mu);
             for (auto& kv : sh.rows) n += kv.second.live ? 1 : 0;
+            n += sh.disk.size();
           }
         } else if (DenseTable* d = s->get_dense(h.table)) {
           n = d->w.size();
@@ -463,6 +612,30 @@ void handle(Server* s, int fd) {
         SparseTable* t = s->get_sparse(h.table);
         if (!t) { status = -1; break; }
         uint64_t dropped = 0;
+        if (t->cfg.rule == CTR) {   // ctr_accessor Shrink: decay show/click, age, delete weak / stale
+          const int dim = t->cfg.dim;
+          for (auto& sh : t->shards) {
+            std::lock_guard<std::mutex> g(sh.mu);
+            for (auto it = sh.rows.begin(); it != sh.rows.end();) {
+              float* st = it->second.v.data() + dim;
+              if (it->second.live) {
+                st[0] *= t->cfg.show_click_decay;
+                st[1] *= t->cfg.show_click_decay;
+                st[2] += 1.f;
+              }
+              if (!it->second.live || ctr_score(t->cfg, st) < t->cfg.delete_threshold ||
+                  st[2] > t->cfg.delete_after_unseen_days) {
+                it = sh.rows.erase(it);
+                ++dropped;
+              } else {
+                ++it;
+              }
+            }
+          }
+          out.resize(8);
+          memcpy(out.data(), &dropped, 8);
+          break;
+        }
         for (auto& sh : t->shards) {
           std::lock_guard<std::mutex> g(sh.mu);
           for (auto it = sh.rows.begin(); it != sh.rows.end();) {
@@ -482,6 +655,138 @@ void handle(Server* s, int fd) {
       case LOAD:
         status = save_or_load(s, h, std::string(in.data(), in.size()));
         break;
+      case SET_SPILL: {   // payload = directory; per-shard append-only spill files
+        SparseTable* t = s->get_sparse(h.table);
+        if (!t || !t->cfg.cache_rows) { status = -1; break; }
+        const std::string dir(in.data(), in.size());
+        for (int k = 0; k < kShards; ++k) {
+          SparseShard& sh = t->shards[k];
+          std::lock_guard<std::mutex> g(sh.mu);
+          if (sh.f) continue;
+          const std::string path = dir + "/table" + std::to_string(h.table) + "_shard" + std::to_string(k) + ".spill";
+          sh.f = fopen(path.c_str(), "w+b");
+          if (!sh.f) { status = -4; break; }
+        }
+        break;
+      }
+      case GRAPH_ADD_EDGES: {   // n edges: src[n] u64, dst[n] u64, w[n] f32; arg 1 = also the reverse edges;
+                                // arg 2: payload = n node ids to register (no edges)
+        GraphTable* gt = s->get_graph(h.table);
+        if (h.arg == 2) {
+          if (h.nbytes != h.n * 8) { status = -1; break; }
+          const uint64_t* ids = reinterpret_cast<const uint64_t*>(in.data());
+          for (uint64_t i = 0; i < h.n; ++i) {
+            const int k = (int)(mix(ids[i]) % kShards);
+            std::lock_guard<std::mutex> g(gt->mu[k]);
+            gt->nodes[k].emplace(ids[i], GNode());
+          }
+          break;
+        }
+        if (h.nbytes != h.n * 20) { status = -1; break; }
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(in.data());
+        const uint64_t* dst = src + h.n;
+        const float* w = reinterpret_cast<const float*>(dst + h.n);
+        for (int pass = 0; pass < (h.arg ? 2 : 1); ++pass)
+          for (uint64_t i = 0; i < h.n; ++i) {
+            const uint64_t a = pass ? dst[i] : src[i], b = pass ? src[i] : dst[i];
+            const int k = (int)(mix(a) % kShards);
+            std::lock_guard<std::mutex> g(gt->mu[k]);
+            GNode& nd = gt->nodes[k][a];
+            nd.nbr.push_back(b);
+            nd.w.push_back(w[i]);
+          }
+        break;
+      }
+      case GRAPH_SAMPLE: {   // n node ids -> counts u32[n] + sampled ids; arg = k | (weighted << 31)
+        if (h.nbytes != h.n * 8) { status = -1; break; }
+        GraphTable* gt = s->get_graph(h.table);
+        const uint64_t* ids = reinterpret_cast<const uint64_t*>(in.data());
+        const uint32_t k = h.arg & 0x7fffffffu;
+        const bool weighted = (h.arg >> 31) != 0;
+        std::vector<uint32_t> counts(h.n);
+        std::vector<uint64_t> picked;
+        for (uint64_t i = 0; i < h.n; ++i) {
+          const int sk = (int)(mix(ids[i]) % kShards);
+          std::lock_guard<std::mutex> g(gt->mu[sk]);
+          auto it = gt->nodes[sk].find(ids[i]);
+          if (it == gt->nodes[sk].end()) continue;
+          const GNode& nd = it->second;
+          const size_t deg = nd.nbr.size();
+          std::mt19937_64& rng = gt->rng[sk];
+          if (deg <= k) {
+            picked.insert(picked.end(), nd.nbr.begin(), nd.nbr.end());
+            counts[i] = (uint32_t)deg;
+          } else if (!weighted) {   // k distinct positions (partial Fisher-Yates)
+            std::vector<uint32_t> pos(deg);
+            for (size_t j = 0; j < deg; ++j) pos[j] = (uint32_t)j;
+            for (uint32_t j = 0; j < k; ++j) {
+              const size_t r = j + std::uniform_int_distribution<size_t>(0, deg - 1 - j)(rng);
+              std::swap(pos[j], pos[r]);
+              picked.push_back(nd.nbr[pos[j]]);
+            }
+            counts[i] = k;
+          } else {   // weighted without replacement: the k largest keys u^(1/w) (Efraimidis-Spirakis)
+            std::vector<std::pair<double, uint32_t>> key(deg);
+            std::uniform_real_distribution<double> u(1e-12, 1.0);
+            for (size_t j = 0; j < deg; ++j)
+              key[j] = {std::log(u(rng)) / std::max(1e-12, (double)nd.w[j]), (uint32_t)j};
+            std::partial_sort(key.begin(), key.begin() + k, key.end(),
+                              [](const auto& a, const auto& b) { return a.first > b.first; });
+            for (uint32_t j = 0; j < k; ++j) picked.push_back(nd.nbr[key[j].second]);
+            counts[i] = k;
+          }
+        }
+        out.resize(h.n * 4 + picked.size() * 8);
+        memcpy(out.data(), counts.data(), h.n * 4);
+        if (!picked.empty()) memcpy(out.data() + h.n * 4, picked.data(), picked.size() * 8);
+        break;
+      }
+      case GRAPH_SET_FEAT:
+      case GRAPH_GET_FEAT: {   // n ids (+ n x arg floats for SET)
+        GraphTable* gt = s->get_graph(h.table);
+        const uint32_t dim = h.arg;
+        const bool set = h.cmd == GRAPH_SET_FEAT;
+        if (h.nbytes != h.n * 8 + (set ? h.n * (size_t)dim * 4 : 0)) { status = -1; break; }
+        const uint64_t* ids = reinterpret_cast<const uint64_t*>(in.data());
+        const float* fv = reinterpret_cast<const float*>(in.data() + h.n * 8);
+        if (!set) out.assign(h.n * (size_t)dim * 4, 0);
+        float* o = reinterpret_cast<float*>(out.data());
+        for (uint64_t i = 0; i < h.n; ++i) {
+          const int sk = (int)(mix(ids[i]) % kShards);
+          std::lock_guard<std::mutex> g(gt->mu[sk]);
+          if (set) {
+            GNode& nd = gt->nodes[sk][ids[i]];
+            nd.feat.assign(fv + i * dim, fv + (i + 1) * dim);
+          } else {
+            auto it = gt->nodes[sk].find(ids[i]);
+            if (it != gt->nodes[sk].end())
+              memcpy(o + i * dim, it->second.feat.data(), 4 * std::min<size_t>(dim, it->second.feat.size()));
+          }
+        }
+        break;
+      }
+      case GRAPH_RANDOM_NODES:
+      case GRAPH_NODE_COUNT: {   // arg = how many (uniform, without replacement) / node count
+        GraphTable* gt = s->get_graph(h.table);
+        std::vector<uint64_t> all;
+        for (int k = 0; k < kShards; ++k) {
+          std::lock_guard<std::mutex> g(gt->mu[k]);
+          for (auto& kv : gt->nodes[k]) all.push_back(kv.first);
+        }
+        if (h.cmd == GRAPH_NODE_COUNT) {
+          const uint64_t n = all.size();
+          out.resize(8);
+          memcpy(out.data(), &n, 8);
+          break;
+        }
+        std::sort(all.begin(), all.end());
+        std::mt19937_64 rng(h.n);   // n = seed
+        const size_t k = std::min<size_t>(h.arg, all.size());
+        for (size_t j = 0; j < k; ++j) std::swap(all[j], all[j + std::uniform_int_distribution<size_t>(0, all.size() - 1 - j)(rng)]);
+        out.resize(k * 8);
+        if (k) memcpy(out.data(), all.data(), k * 8);
+        break;
+      }
       case STOP: {
         s->stopping = true;
         s->wake_all();
@@ -559,6 +864,14 @@ TableCfg make_cfg(const int32_t* iv, const float* fv, uint64_t seed) {
   c.max_bound = fv[7];
   c.entry_value = fv[8];
   c.seed = seed;
+  c.nonclk_coeff = fv[9];
+  c.click_coeff = fv[10];
+  c.embedx_threshold = fv[11];
+  c.show_click_decay = fv[12];
+  c.delete_threshold = fv[13];
+  c.delete_after_unseen_days = fv[14];
+  c.base_threshold = fv[15];
+  c.cache_rows = (uint64_t)(uint32_t)iv[4];
   return c;
 }
 
@@ -650,8 +963,10 @@ PHA_API void pha_ps_client_close(void* h) {
   delete c;
 }
 
-// iv = {rule, dim, sync_trainers, entry_kind}
-// fv = {lr, beta1, beta2, eps, initial_g2sum, initial_range, min_bound, max_bound, entry_value}
+// iv = {rule, dim, sync_trainers, entry_kind, cache_rows}
+// fv = {lr, beta1, beta2, eps, initial_g2sum, initial_range, min_bound, max_bound, entry_value,
+//       nonclk_coeff, click_coeff, embedx_threshold, show_click_decay, delete_threshold,
+//       delete_after_unseen_days, base_threshold}
 PHA_API int64_t pha_ps_create_dense(void* h, uint32_t table, uint64_t numel, const int32_t* iv, const float* fv,
                                     const float* init) {
   const TableCfg c = make_cfg(iv, fv, 0);
@@ -716,4 +1031,54 @@ PHA_API int64_t pha_ps_save(void* h, uint32_t table, const char* path, int mode,
 
 PHA_API int64_t pha_ps_stop_server(void* h) {
   return call(static_cast<Client*>(h), STOP, 0, 0, 0, nullptr, 0, nullptr, 0, nullptr, 0, nullptr);
+}
+
+PHA_API int64_t pha_ps_set_spill(void* h, uint32_t table, const char* dir) {
+  return call(static_cast<Client*>(h), SET_SPILL, table, 0, 0, dir, strlen(dir), nullptr, 0, nullptr, 0, nullptr);
+}
+
+// ------------------------------------------------------------------------------- graph ABI
+PHA_API int64_t pha_ps_graph_add_edges(void* h, uint32_t table, const uint64_t* src, const uint64_t* dst,
+                                       const float* w, uint64_t n, int bidirectional) {
+  if (bidirectional == 2)   // register the n node ids in ``src``
+    return call(static_cast<Client*>(h), GRAPH_ADD_EDGES, table, 2, n, src, n * 8, nullptr, 0, nullptr, 0, nullptr);
+  std::vector<char> buf(n * 20);
+  memcpy(buf.data(), src, n * 8);
+  memcpy(buf.data() + n * 8, dst, n * 8);
+  memcpy(buf.data() + n * 16, w, n * 4);
+  return call(static_cast<Client*>(h), GRAPH_ADD_EDGES, table, bidirectional ? 1 : 0, n, buf.data(), buf.size(),
+              nullptr, 0, nullptr, 0, nullptr);
+}
+
+// out: u32 counts[n] followed by the sampled u64 ids (capacity out_cap bytes); returns bytes written
+PHA_API int64_t pha_ps_graph_sample(void* h, uint32_t table, const uint64_t* ids, uint64_t n, uint32_t k,
+                                    int weighted, void* out, uint64_t out_cap) {
+  uint64_t nb = 0;
+  const uint32_t arg = (k & 0x7fffffffu) | (weighted ? 0x80000000u : 0u);
+  const int64_t st = call(static_cast<Client*>(h), GRAPH_SAMPLE, table, arg, n, ids, n * 8, nullptr, 0, out, out_cap,
+                          &nb);
+  return st < 0 ? st : (int64_t)nb;
+}
+
+PHA_API int64_t pha_ps_graph_feat(void* h, uint32_t table, const uint64_t* ids, uint64_t n, uint32_t dim, float* feat,
+                                  int set) {
+  if (set)
+    return call(static_cast<Client*>(h), GRAPH_SET_FEAT, table, dim, n, ids, n * 8, feat, n * (size_t)dim * 4, nullptr,
+                0, nullptr);
+  return call(static_cast<Client*>(h), GRAPH_GET_FEAT, table, dim, n, ids, n * 8, nullptr, 0, feat,
+              n * (size_t)dim * 4, nullptr);
+}
+
+PHA_API int64_t pha_ps_graph_random_nodes(void* h, uint32_t table, uint32_t k, uint64_t seed, uint64_t* out) {
+  uint64_t nb = 0;
+  const int64_t st = call(static_cast<Client*>(h), GRAPH_RANDOM_NODES, table, k, seed, nullptr, 0, nullptr, 0, out,
+                          (size_t)k * 8, &nb);
+  return st < 0 ? st : (int64_t)(nb / 8);
+}
+
+PHA_API int64_t pha_ps_graph_node_count(void* h, uint32_t table) {
+  uint64_t v = 0;
+  const int64_t st = call(static_cast<Client*>(h), GRAPH_NODE_COUNT, table, 0, 0, nullptr, 0, nullptr, 0, &v, 8,
+                          nullptr);
+  return st < 0 ? st : (int64_t)v;
 }

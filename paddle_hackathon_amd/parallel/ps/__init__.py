@@ -31,7 +31,11 @@ from ...utils import native
 __all__ = ["PSServer", "PSClient", "DistributedEmbedding", "PSOptimizer", "TheOnePSRuntime", "RULES",
            "sparse_embedding"]
 
-RULES = {"sgd": 0, "naive": 0, "adagrad": 1, "std_adagrad": 2, "adam": 3, "sum": 4}
+RULES = {"sgd": 0, "naive": 0, "adagrad": 1, "std_adagrad": 2, "adam": 3, "sum": 4, "ctr": 5}
+
+# CtrCommonAccessor defaults (reference ps/table/ctr_accessor.cc + the_one_ps.py accessor config)
+CTR_DEFAULTS = {"nonclk_coeff": 0.1, "click_coeff": 1.0, "embedx_threshold": 10.0, "show_click_decay_rate": 0.98,
+                "delete_threshold": 0.8, "delete_after_unseen_days": 30.0, "base_threshold": 1.5}
 
 _P = ctypes.c_void_p
 _sigs_done = False
@@ -61,6 +65,12 @@ def _lib():
             "pha_ps_shrink": (i64, [_P, u32, u32]),
             "pha_ps_save": (i64, [_P, u32, ctypes.c_char_p, i32, i32]),
             "pha_ps_stop_server": (i64, [_P]),
+            "pha_ps_set_spill": (i64, [_P, u32, ctypes.c_char_p]),
+            "pha_ps_graph_add_edges": (i64, [_P, u32, _P, _P, _P, u64, i32]),
+            "pha_ps_graph_sample": (i64, [_P, u32, _P, u64, u32, i32, _P, u64]),
+            "pha_ps_graph_feat": (i64, [_P, u32, _P, u64, u32, _P, i32]),
+            "pha_ps_graph_random_nodes": (i64, [_P, u32, u32, u64, _P]),
+            "pha_ps_graph_node_count": (i64, [_P, u32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -162,11 +172,16 @@ class PSClient:
         return b
 
     @staticmethod
-    def _cfg(rule, dim, sync_trainers, entry, lr, beta1, beta2, epsilon, initial_g2sum, initial_range, bounds):
+    def _cfg(rule, dim, sync_trainers, entry, lr, beta1, beta2, epsilon, initial_g2sum, initial_range, bounds,
+             ctr=None, cache_rows=0):
         kind, value = _entry_cfg(entry)
-        iv = _a([RULES[rule] if isinstance(rule, str) else int(rule), dim, sync_trainers, kind], np.int32)
+        iv = _a([RULES[rule] if isinstance(rule, str) else int(rule), dim, sync_trainers, kind, int(cache_rows)],
+                np.int32)
         lo, hi = bounds if bounds is not None else (-3.4e38, 3.4e38)
-        fv = _a([lr, beta1, beta2, epsilon, initial_g2sum, initial_range, lo, hi, value], np.float32)
+        c = dict(CTR_DEFAULTS, **(ctr or {}))
+        fv = _a([lr, beta1, beta2, epsilon, initial_g2sum, initial_range, lo, hi, value, c["nonclk_coeff"],
+                 c["click_coeff"], c["embedx_threshold"], c["show_click_decay_rate"], c["delete_threshold"],
+                 c["delete_after_unseen_days"], c["base_threshold"]], np.float32)
         return iv, fv
 
     # ---- dense -------------------------------------------------------------------------
@@ -212,11 +227,26 @@ class PSClient:
 
     # ---- sparse ------------------------------------------------------------------------
     def create_sparse(self, table, dim, rule="adagrad", lr=0.05, initial_range=1e-4, entry=None, seed=0,
-                      beta1=0.9, beta2=0.999, epsilon=1e-8, initial_g2sum=3.0, bounds=(-10.0, 10.0)):
-        iv, fv = self._cfg(rule, dim, 1, entry, lr, beta1, beta2, epsilon, initial_g2sum, initial_range, bounds)
+                      beta1=0.9, beta2=0.999, epsilon=1e-8, initial_g2sum=3.0, bounds=(-10.0, 10.0), accessor=None,
+                      ctr_config=None, cache_rows=0, spill_dir=None):
+        """``accessor="ctr"``: CtrCommonAccessor rows — pulls return [embed_w, embedx(dim-1)], pushes
+        carry [show, click, grads] (``push_sparse_ctr``); embedx is created once the feature's score
+        (show-click)*nonclk_coeff + click*click_coeff reaches ``embedx_threshold``.
+        ``cache_rows`` + ``spill_dir``: SSD-table mode, at most ``cache_rows`` rows resident per
+        server, colder rows spilled to files under ``spill_dir`` and read back on access."""
+        if accessor == "ctr":
+            rule = "ctr"
+        iv, fv = self._cfg(rule, dim, 1, entry, lr, beta1, beta2, epsilon, initial_g2sum, initial_range, bounds,
+                           ctr_config, cache_rows)
         for h in self._h:
             _ok(_lib().pha_ps_create_sparse(h, table, iv.ctypes.data, fv.ctypes.data, int(seed)), "create_sparse")
+            if cache_rows and spill_dir:
+                os.makedirs(spill_dir, exist_ok=True)
+                _ok(_lib().pha_ps_set_spill(h, table, os.path.abspath(spill_dir).encode()), "set_spill")
         self._sparse[table] = int(dim)
+        self._ctr = getattr(self, "_ctr", set())
+        if rule == "ctr":
+            self._ctr.add(table)
 
     def _route(self, ids):
         ids = _a(ids, np.uint64).reshape(-1)
@@ -253,6 +283,110 @@ class PSClient:
             sub_g = np.ascontiguousarray(g[sel])
             _ok(L.pha_ps_push_sparse(h, table, sub_ids.ctypes.data, sel.size, dim, sub_g.ctypes.data, int(delta)),
                 "push_sparse")
+
+    def push_sparse_ctr(self, table, ids, shows, clicks, grads):
+        """CTR accessor push: per id its show / click counts and the gradient of [embed, embedx]"""
+        dim = self._sparse[table]
+        ids, srv = self._route(ids)
+        g = _a(grads, np.float32).reshape(ids.size, dim)
+        payload = np.concatenate([_a(shows, np.float32).reshape(-1, 1), _a(clicks, np.float32).reshape(-1, 1), g], 1)
+        L = _lib()
+        for i, h in enumerate(self._h):
+            sel = np.nonzero(srv == i)[0]
+            if sel.size == 0:
+                continue
+            sub_ids = np.ascontiguousarray(ids[sel])
+            sub = np.ascontiguousarray(payload[sel])
+            _ok(L.pha_ps_push_sparse(h, table, sub_ids.ctypes.data, sel.size, dim + 2, sub.ctypes.data, 0),
+                "push_sparse_ctr")
+
+    # ---- graph table (common_graph_table) ------------------------------------------------
+    def _graph_route(self, ids):
+        ids = _a(ids, np.uint64).reshape(-1)
+        return ids, (ids % np.uint64(self.n_servers)).astype(np.int64)
+
+    def graph_add_edges(self, table, src, dst, weight=None, bidirectional=False):
+        """edges live on the server of their source node"""
+        src = _a(src, np.uint64).reshape(-1)
+        dst = _a(dst, np.uint64).reshape(-1)
+        w = _a(np.ones(src.size) if weight is None else weight, np.float32).reshape(-1)
+        passes = [(src, dst)] + ([(dst, src)] if bidirectional else [])
+        L = _lib()
+        for a, b in passes:
+            srv = (a % np.uint64(self.n_servers)).astype(np.int64)
+            for i, h in enumerate(self._h):
+                sel = np.nonzero(srv == i)[0]
+                if sel.size:   # keep the contiguous copies alive across the native call
+                    sa, sb, sw = (np.ascontiguousarray(v[sel]) for v in (a, b, w))
+                    _ok(L.pha_ps_graph_add_edges(h, table, sa.ctypes.data, sb.ctypes.data, sw.ctypes.data, sel.size,
+                                                 0), "graph_add")
+        # every endpoint is a node on its own server (sink nodes are sampled / counted too)
+        nodes = np.unique(np.concatenate([src, dst]))
+        srv = (nodes % np.uint64(self.n_servers)).astype(np.int64)
+        for i, h in enumerate(self._h):
+            sel = np.nonzero(srv == i)[0]
+            if sel.size:
+                sub = np.ascontiguousarray(nodes[sel])
+                _ok(L.pha_ps_graph_add_edges(h, table, sub.ctypes.data, None, None, sel.size, 2), "graph_nodes")
+
+    def graph_sample_neighbors(self, table, ids, sample_size, weighted=False):
+        """-> list (one per id) of sampled neighbour id arrays (<= sample_size, without replacement)"""
+        ids, srv = self._graph_route(ids)
+        res = [None] * ids.size
+        L = _lib()
+        for i, h in enumerate(self._h):
+            sel = np.nonzero(srv == i)[0]
+            if sel.size == 0:
+                continue
+            sub = np.ascontiguousarray(ids[sel])
+            cap = sel.size * 4 + sel.size * int(sample_size) * 8
+            buf = np.empty(cap, np.uint8)
+            nb = _ok(L.pha_ps_graph_sample(h, table, sub.ctypes.data, sel.size, int(sample_size), int(weighted),
+                                           buf.ctypes.data, cap), "graph_sample")
+            counts = buf[:sel.size * 4].view(np.uint32)
+            picked = buf[sel.size * 4:nb].view(np.uint64)
+            off = 0
+            for j, c in zip(sel, counts):
+                res[j] = picked[off:off + c].astype(np.int64)
+                off += int(c)
+        return res
+
+    def graph_set_node_feat(self, table, ids, feats):
+        ids, srv = self._graph_route(ids)
+        f = _a(feats, np.float32).reshape(ids.size, -1)
+        for i, h in enumerate(self._h):
+            sel = np.nonzero(srv == i)[0]
+            if sel.size:
+                sub_f = np.ascontiguousarray(f[sel])
+                sub_i = np.ascontiguousarray(ids[sel])
+                _ok(_lib().pha_ps_graph_feat(h, table, sub_i.ctypes.data, sel.size, f.shape[1], sub_f.ctypes.data, 1),
+                    "graph_set_feat")
+
+    def graph_get_node_feat(self, table, ids, dim):
+        ids, srv = self._graph_route(ids)
+        out = np.zeros((ids.size, dim), np.float32)
+        for i, h in enumerate(self._h):
+            sel = np.nonzero(srv == i)[0]
+            if sel.size:
+                buf = np.empty((sel.size, dim), np.float32)
+                sub_i = np.ascontiguousarray(ids[sel])
+                _ok(_lib().pha_ps_graph_feat(h, table, sub_i.ctypes.data, sel.size, dim, buf.ctypes.data, 0),
+                    "graph_get_feat")
+                out[sel] = buf
+        return out
+
+    def graph_random_sample_nodes(self, table, k, seed=0):
+        out = []
+        per = [k // self.n_servers + (1 if i < k % self.n_servers else 0) for i in range(self.n_servers)]
+        for h, n in zip(self._h, per):
+            if n:
+                buf = np.empty(n, np.uint64)
+                got = _ok(_lib().pha_ps_graph_random_nodes(h, table, n, int(seed), buf.ctypes.data), "graph_random")
+                out.append(buf[:got])
+        return np.concatenate(out).astype(np.int64) if out else np.zeros(0, np.int64)
+
+    def graph_node_count(self, table):
+        return sum(_ok(_lib().pha_ps_graph_node_count(h, table), "graph_count") for h in self._h)
 
     # ---- control -----------------------------------------------------------------------
     def barrier(self, n, tag=0):
