@@ -17,6 +17,28 @@ namespace {
 
 constexpr int kWaves = 4;
 
+// counter-based dropout mask of the fused bias-dropout-residual-LN (fused_bias_dropout_residual_
+// layer_norm): element idx = row * H + col keeps iff a 16-bit hash of (seed, idx) >= thresh, so the
+// backward regenerates exactly the forward's mask and no mask tensor is stored.
+__device__ __forceinline__ unsigned bd_mix(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool bd_keep(unsigned seed, long idx, unsigned thresh) {
+  const unsigned h = bd_mix(seed ^ bd_mix((unsigned)idx ^ ((unsigned)(idx >> 32) * 0x9e3779b1U)));
+  return (h & 0xffffU) >= thresh;
+}
+
+struct BdArgs {            // x -> dropout(x + xb) before the residual add (thresh 0: no dropout)
+  const void* xb;          // [H] bias of x (type W), may be null
+  unsigned seed, thresh;
+  float kscale;
+};
+
 template <typename T, typename W, int NCH>
 // With `r` set: the pre-LN residual add is fused in — hs = x + r (rounded to T, exactly what
 // a separate add would store) is written out and normalised, saving one full read+write pass.
@@ -24,7 +46,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int H, float eps, const T* __restrict__ r = nullptr,
-                                                     T* __restrict__ hs = nullptr) {
+                                                     T* __restrict__ hs = nullptr, BdArgs bd = BdArgs{nullptr, 0u, 0u, 1.f}) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -39,6 +61,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
       if (r) {
         float rv[8];
         Vec8<T>::ld(r + (long)row * H + col, rv);
+        if (bd.xb || bd.thresh) {   // fused bias + dropout of x (rounded to T as a separate op would store)
+          float bv[8];
+          if (bd.xb) Vec8<W>::ld((const W*)bd.xb + col, bv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float z = round_to<T>(v[c][i] + (bd.xb ? bv[i] : 0.f));
+            if (bd.thresh) z = bd_keep(bd.seed, (long)row * H + col + i, bd.thresh) ? round_to<T>(z * bd.kscale) : 0.f;
+            v[c][i] = z;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[c][i] = round_to<T>(v[c][i] + rv[i]);  // stats on the stored sum
         Vec8<T>::st(hs + (long)row * H + col, v[c]);
@@ -201,6 +233,54 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
   if (w == 0 && col < H) Cvt<W>::st(out, col, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
 }
 
+// backward of x -> dropout(x + xb): dx = dh * keep * kscale (the regenerated mask), per-block
+// partial column sums of dx (the bias gradient) as in ln_bwd_kernel. BW waves per block.
+template <typename T, int NCH, int BW>
+__global__ __launch_bounds__(BW * 64) void dropout_bias_bwd_kernel(const T* __restrict__ dh, T* __restrict__ dx,
+                                                                   float* __restrict__ part, int rows, int H,
+                                                                   unsigned seed, unsigned thresh, float kscale) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float acc[NCH][8];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[c][i] = 0.f;
+  for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        float g[8];
+        Vec8<T>::ld(dh + (long)row * H + col, g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          g[i] = (!thresh || bd_keep(seed, (long)row * H + col + i, thresh)) ? g[i] * kscale : 0.f;
+          acc[c][i] += round_to<T>(g[i]);
+        }
+        Vec8<T>::st(dx + (long)row * H + col, g);
+      }
+    }
+  }
+  __shared__ float red[BW][512];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = acc[c][i];
+    __syncthreads();
+    for (int k = threadIdx.x; k < 512; k += BW * 64) {
+      const int cc = c * 512 + k;
+      if (cc < H) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < BW; ++q) t += red[q][k];
+        part[(long)blockIdx.x * H + cc] = t;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T, int NCH>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int rows, int H) {
   const int lane = threadIdx.x & 63;
@@ -341,6 +421,33 @@ PHA_API int pha_layer_norm_bwd_nblocks(int rows, int H) {
   return need < cap ? need : cap;
 }
 
+// fused_bias_dropout_residual_layer_norm forward: hs = r + dropout(x + xb) (stored), y = LN(hs).
+// thresh = round(p * 65536) (0: no dropout), kscale = 1 / (1 - p).
+PHA_API int pha_bdrln_fwd(int dt, int wdt, const void* x, const void* xb, const void* r, void* hs, const void* w,
+                          const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps, unsigned seed,
+                          unsigned thresh, float kscale, hipStream_t stream) {
+  if (H % 8 || rows <= 0 || !r || !hs) return (int)hipErrorInvalidValue;
+  const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
+  const BdArgs bd{xb, seed, thresh, kscale};
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    if (wdt == kF32) {
+      rc = dispatch_nch(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_fwd_kernel<T, float, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)x, (const float*)w, (const float*)b, (T*)y, mean, rstd, rows, H, eps,
+                           (const T*)r, (T*)hs, bd);
+      });
+    } else {
+      rc = dispatch_nch(H, [&](auto nch) {
+        hipLaunchKernelGGL((ln_fwd_kernel<T, T, decltype(nch)::value>), grid, block, 0, stream,
+                           (const T*)x, (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, H, eps,
+                           (const T*)r, (T*)hs, bd);
+      });
+    }
+  });
+  return rc;
+}
+
 PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
                                float* mean, float* rstd, int rows, int H, float eps, hipStream_t stream) {
   return pha_layer_norm_fwd2(dt, wdt, x, nullptr, nullptr, w, b, y, mean, rstd, rows, H, eps, stream);
@@ -397,6 +504,27 @@ PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, c
                                int nblocks, int rows, int H, hipStream_t stream) {
   return pha_layer_norm_bwd2(dt, wdt, dy, x, w, mean, rstd, nullptr, dx, dw, db, part_w, part_b, nblocks, rows, H,
                              stream);
+}
+
+// backward of the dropout(x + xb) branch: dx = dh * mask * kscale; dbias (type of wdt, may be null)
+// = column sums of dx; part: workspace [nblocks + 8, H] fp32 (nblocks = pha_layer_norm_bwd_nblocks)
+PHA_API int pha_dropout_bias_bwd(int dt, int wdt, const void* dh, void* dx, void* dbias, float* part, int nblocks,
+                                 int rows, int H, unsigned seed, unsigned thresh, float kscale, hipStream_t stream) {
+  if (H % 8 || rows <= 0 || nblocks <= 0) return (int)hipErrorInvalidValue;
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    rc = dispatch_nch_small(H, [&](auto nch) {
+      constexpr int bw = bwd_waves(decltype(nch)::value);
+      hipLaunchKernelGGL((dropout_bias_bwd_kernel<T, decltype(nch)::value, bw>), dim3(nblocks), dim3(bw * 64), 0,
+                         stream, (const T*)dh, (T*)dx, part, rows, H, seed, thresh, kscale);
+    });
+    if (rc) return rc;
+    if (dbias) {
+      if (wdt == kF32) col_sum<float>(part, (float*)dbias, nblocks, H, stream);
+      else col_sum<T>(part, (T*)dbias, nblocks, H, stream);
+    }
+  });
+  return rc ? rc : (int)hipGetLastError();
 }
 
 PHA_API int pha_softmax_fwd(int dt, const void* x, void* y, int rows, int H, hipStream_t stream) {

@@ -75,6 +75,13 @@ def _linear(x, w, b):
 def fused_bias_dropout_residual_layer_norm(x, residual, bias=None, ln_scale=None, ln_bias=None, dropout_rate=0.5,
                                            ln_epsilon=1e-5, training=True, mode="upscale_in_train", name=None):
     h = _u(x)
+    if mode in ("upscale_in_train", "upscale-in-train") or not training or dropout_rate == 0.0:
+        # one fused HIP pass each way (ops/fused.py _BiasDropoutResidualLN); eval-mode upscale dropout is identity
+        w = _u(ln_scale)
+        w = w if w is not None else torch.ones(h.shape[-1], dtype=torch.float32, device=h.device)
+        r = _u(residual)
+        return _wrap(_ops.fused.bias_dropout_residual_layer_norm(h.contiguous(), r.contiguous().to(h.dtype), _u(bias), w,
+                                                                 _u(ln_bias), dropout_rate, training, ln_epsilon))
     if bias is not None:
         h = h + _u(bias)
     h = _dropout(h, dropout_rate, training, mode) + _u(residual)
@@ -94,6 +101,12 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
     if ring_id >= 0:
         from ...parallel import collective as C
         torch.distributed.all_reduce(h)
+    if (not pre_layer_norm and add_residual and
+            (mode in ("upscale_in_train", "upscale-in-train") or not training or dropout2_rate == 0.0)):
+        w = _u(ln2_scale)
+        w = w if w is not None else torch.ones(h.shape[-1], dtype=torch.float32, device=h.device)
+        return _wrap(_ops.fused.bias_dropout_residual_layer_norm(h.contiguous(), residual.contiguous(), None, w,
+                                                                 _u(ln2_bias), dropout2_rate, training, ln2_epsilon))
     h = _dropout(h, dropout2_rate, training, mode)
     if add_residual:
         h = residual + h

@@ -120,11 +120,19 @@ class BertLayer(nn.Layer):
         p = self.cfg.hidden_dropout
         return F.dropout(t, p, training=self.training) if p and self.training else t
 
+    def _add_norm(self, y, x, norm):
+        """LN(x + dropout(y)) as one fused bias-dropout-residual-LayerNorm pass each way"""
+        p = self.cfg.hidden_dropout if self.training else 0.0
+        yt, xt = y._t, x._t
+        return _wrap(_ops.bias_dropout_residual_layer_norm(yt.contiguous(), xt.contiguous().to(yt.dtype), None,
+                                                          norm.weight._t, norm.bias._t, p, self.training,
+                                                          norm._epsilon))
+
     def forward(self, x, attn_bias=None):
-        x = self.norm1(x + self._drop(self.attention(x, attn_bias)))
+        x = self._add_norm(self.attention(x, attn_bias), x, self.norm1)
         h = torch.matmul(x._t, self.linear1.weight._t)
         h = _ops.bias_gelu(h, self.linear1.bias._t, approximate=False)
-        return self.norm2(x + self._drop(self.linear2(_wrap(h))))
+        return self._add_norm(self.linear2(_wrap(h)), x, self.norm2)
 
 
 class BertModel(nn.Layer):

@@ -163,12 +163,50 @@ def rms_norm(x, weight, eps=1e-6):
     return y * weight if weight is not None else y
 
 
+class _BiasDropoutResidualLN(torch.autograd.Function):
+    """y = LN(residual + dropout(x + bias)) in one HIP pass (hs stored for the backward); the dropout
+    mask is a counter hash of (seed, element) regenerated in the backward, never stored.
+    Backward: LN backward (d residual = dh) then one pass dx = dh * mask / (1-p) with the bias
+    gradient as its column sums (reference fused_bias_dropout_residual_layer_norm_op.cu)."""
+
+    @staticmethod
+    def forward(ctx, x, residual, bias, w, b, p, eps):
+        thresh = min(65535, int(round(p * 65536))) if p > 0 else 0
+        kscale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if thresh else 0
+        y, mean, rstd, hs = _hip.bdrln_fwd(x, bias, residual, w, b, eps, seed, thresh, kscale)
+        ctx.save_for_backward(hs, w, mean, rstd)
+        ctx.cfg = (seed, thresh, kscale, b is not None, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        hs, w, mean, rstd = ctx.saved_tensors
+        seed, thresh, kscale, has_b, xb_dt = ctx.cfg
+        dh, dw, db = _hip.layer_norm_bwd(gy.contiguous(), hs, w, mean, rstd, has_b)
+        if thresh == 0 and xb_dt is None:
+            dx, dxb = dh, None
+        else:
+            dx, dxb = _hip.dropout_bias_bwd(dh, seed, thresh, kscale, xb_dt)
+        return dx, dh, dxb, dw, db, None, None
+
+
 def bias_dropout_residual_layer_norm(x, residual, bias, ln_w, ln_b, dropout_p, training, eps):
+    """LN(residual + dropout(x + bias)) over the last dim (reference incubate
+    fused_bias_dropout_residual_layer_norm)."""
+    p = float(dropout_p) if training else 0.0
+    H = x.shape[-1]
+    if (_use_hip(x) and x.is_contiguous() and residual.is_contiguous() and residual.shape == x.shape
+            and residual.dtype == x.dtype and x.dtype in (torch.bfloat16, torch.float32, torch.float16)
+            and ln_w is not None and ln_w.numel() == H and ln_w.dtype in (x.dtype, torch.float32)
+            and (ln_b is None or ln_b.dtype == ln_w.dtype) and H % 8 == 0 and H <= 4096 and p < 1.0):
+        return _BiasDropoutResidualLN.apply(x, residual, bias, ln_w.reshape(-1),
+                                            None if ln_b is None else ln_b.reshape(-1), p, float(eps))
     h = x + bias if bias is not None else x
-    if training and dropout_p > 0:
-        h = TF.dropout(h, dropout_p, True)
+    if p > 0:
+        h = TF.dropout(h, p, True)
     h = h + residual
-    return layer_norm(h, [h.shape[-1]], ln_w, ln_b, eps)
+    return layer_norm(h, [H], ln_w, ln_b, eps)
 
 
 # ----------------------------------------------------------------------------

@@ -8,7 +8,7 @@ graphs. Shape preconditions are checked here on the host before any launch
 from __future__ import annotations
 
 import ctypes
-from ctypes import c_int, c_long, c_float, c_void_p
+from ctypes import c_uint, c_int, c_long, c_float, c_void_p
 
 import numpy as np
 import torch
@@ -32,6 +32,8 @@ def _L():
             "pha_layer_norm_bwd_nblocks": [I, I],
             "pha_layer_norm_fwd2": [I, I, P, P, P, P, P, P, P, P, I, I, F, P],
             "pha_layer_norm_bwd2": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+            "pha_bdrln_fwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
+            "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
             "pha_softmax_bwd": [I, P, P, P, I, I, P],
             "pha_softmax_ce_fwd": [I, P, P, P, P, LG, I, I, P],
@@ -112,6 +114,38 @@ def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None):
                                     _ptr(dres), _ptr(dx), _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H,
                                     _stream(x)), "layer_norm_bwd")
     return dx, dw, db
+
+
+def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale):
+    """fused_bias_dropout_residual_layer_norm forward: hs = residual + dropout(x + xbias), y = LN(hs).
+    Returns (y, mean, rstd, hs)."""
+    H = w.numel()
+    rows = x.numel() // H
+    assert x.numel() == rows * H and H % 8 == 0 and H <= 4096
+    assert residual.shape == x.shape and residual.dtype == x.dtype and residual.is_contiguous() and x.is_contiguous()
+    y, hs = torch.empty_like(x), torch.empty_like(x)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    xb = None if xbias is None else xbias.contiguous().to(w.dtype)
+    _check(_L().pha_bdrln_fwd(_DT[x.dtype], _DT[w.dtype], _ptr(x), _ptr(xb), _ptr(residual), _ptr(hs),
+                              _ptr(w.contiguous()), _ptr(None if b is None else b.contiguous()), _ptr(y), _ptr(mean),
+                              _ptr(rstd), rows, H, float(eps), int(seed), int(thresh), float(kscale), _stream(x)),
+           "bdrln_fwd")
+    return y, mean, rstd, hs
+
+
+def dropout_bias_bwd(dh, seed, thresh, kscale, bias_dtype=None):
+    """dx = dh * mask * kscale (the forward's regenerated mask) and dbias = column sums of dx."""
+    H = dh.shape[-1]
+    rows = dh.numel() // H
+    nblocks = int(_L().pha_layer_norm_bwd_nblocks(rows, H))
+    dx = torch.empty_like(dh)
+    db = torch.empty(H, dtype=bias_dtype, device=dh.device) if bias_dtype is not None else None
+    wdt = _DT[bias_dtype] if bias_dtype is not None else _DT[dh.dtype]
+    part = torch.empty((nblocks + 8, H), dtype=torch.float32, device=dh.device)
+    _check(_L().pha_dropout_bias_bwd(_DT[dh.dtype], wdt, _ptr(dh), _ptr(dx), _ptr(db), _ptr(part), nblocks, rows, H,
+                                     int(seed), int(thresh), float(kscale), _stream(dh)), "dropout_bias_bwd")
+    return dx, db
 
 
 # ----------------------------------------------------------------------------

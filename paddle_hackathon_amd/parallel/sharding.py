@@ -38,6 +38,8 @@ sharding group, replicated parameters are counted on one rank.
 """
 from __future__ import annotations
 
+import os
+
 import contextlib
 import math
 
@@ -420,6 +422,8 @@ class GroupShardedStage3(Layer):
                     if not p.stop_gradient:
                         p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u))
         self._uidx = {id(u): i for i, u in enumerate(self._units)}
+        self._pool_off = {}
+        self._init_pool()
         # replicated (small) parameters: one all-reduce bucket, updated on every rank
         self._rep_train = [p for p in self._replicated if not p.stop_gradient]
         self._rep_ready = 0
@@ -443,12 +447,59 @@ class GroupShardedStage3(Layer):
                 sub.register_forward_pre_hook(self._make_pre_fwd(us))
                 sub.register_forward_post_hook(self._make_post_fwd(us))
 
+    # -- gather buffers: one flat device pool carved by the native best-fit arena -------------
+    def _init_pool(self):
+        """Gathered units live in ONE pre-sized device buffer whose offsets come from the native
+        coalescing allocator (csrc/runtime/arena.cpp): at 13B+ scale the gather/release churn of
+        hundreds of MB-sized unit buffers per step then never fragments the caching allocator,
+        and the peak is fixed up front. Capacity: the current unit + two prefetched ones of the
+        largest size (layer-ahead prefetch, forward and backward), i.e. 3 x the largest unit.
+        A request the pool cannot place falls back to a plain allocation (counted)."""
+        self._arena = self._pool = None
+        self._pool_fallbacks = 0
+        if not self._units or os.environ.get("PHA_STAGE3_ARENA", "1") == "0":
+            return
+        try:
+            from ..utils import native
+            if not native.available():
+                return
+            dev = self._units[0].bucket.device
+            largest = max(u.bucket.total * torch.empty(0, dtype=u.bucket.dtype).element_size() for u in self._units)
+            cap = 3 * ((largest + 255) // 256 * 256)
+            self._arena = native.Arena(cap, 256)
+            self._pool = torch.empty(cap, dtype=torch.uint8, device=dev)
+        except (OSError, RuntimeError, ValueError):
+            self._arena = self._pool = None
+
+    def _alloc_full(self, u):
+        b = u.bucket
+        nbytes = b.total * torch.empty(0, dtype=b.dtype).element_size()
+        if self._arena is not None:
+            try:
+                off = self._arena.alloc(nbytes)
+                self._pool_off[id(u)] = (off, nbytes)
+                return self._pool[off:off + nbytes].view(b.dtype)
+            except MemoryError:
+                self._pool_fallbacks += 1
+        return torch.empty(b.total, dtype=b.dtype, device=b.device)
+
+    def _free_full(self, u):
+        ent = self._pool_off.pop(id(u), None)
+        if ent is not None:
+            self._arena.free(ent[0])
+
+    def pool_stats(self):
+        if self._arena is None:
+            return None
+        return {"capacity": self._arena.capacity, "used": self._arena.used, "peak": self._arena.peak,
+                "fallbacks": self._pool_fallbacks}
+
     # -- gather / release ---------------------------------------------------------------------
     def _issue_gather(self, u):
         if u.gathered or u.full_work is not None:
             return
         b = u.bucket
-        b.flat_param = torch.empty(b.total, dtype=b.dtype, device=b.device)
+        b.flat_param = self._alloc_full(u)
         u.full_src = b.shard
         w = dist.all_gather_into_tensor(b.flat_param, b.shard, group=self._pg, async_op=not self._sync_comm)
         u.full_work = w if w is not None else True   # True: completed synchronously
@@ -472,6 +523,7 @@ class GroupShardedStage3(Layer):
         for p in u.bucket.params:
             p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
         u.bucket.flat_param = None
+        self._free_full(u)
         u.gathered = False
 
     def _neighbor(self, u, step):

@@ -240,7 +240,8 @@ def _sharding(rank, world, level, clip=None, extra=None):
         opt.clear_grad()
         counts.append({k: S.comm_stats[k] - before[k] for k in before})
     sd = model.state_dict()
-    return {"sd": {k: v.numpy() for k, v in sd.items()}, "counts": counts}
+    pool = model.pool_stats() if hasattr(model, "pool_stats") else None
+    return {"sd": {k: v.numpy() for k, v in sd.items()}, "counts": counts, "pool": pool}
 
 
 def _sharding_ref(clip=None):
@@ -273,6 +274,9 @@ def test_group_sharded_matches_single_process(level, clip, extra):
     for r in res:
         for k in ref:
             np.testing.assert_allclose(r["sd"][k], ref[k], rtol=1e-4, atol=1e-5)
+        if level == "p_g_os" and r["pool"] is not None:
+            # stage-3 gathers come from the native arena pool (3 x largest unit), none spilled out
+            assert r["pool"]["peak"] > 0 and r["pool"]["fallbacks"] == 0 and r["pool"]["used"] == 0, r["pool"]
 
 
 def test_group_sharded_collective_count_is_per_bucket():

@@ -918,3 +918,42 @@ def test_bert_attention_runs_on_own_kernels():
     finally:
         hip.FlashAttentionExt.forward = orig
     assert calls["n"] >= cfg.num_layers
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bias_dropout_residual_layer_norm_kernel(dtype):
+    """fused bias + dropout + residual + LayerNorm (ops/fused.py _BiasDropoutResidualLN) vs the fp32
+    composite at p = 0, and the regenerated-mask identities at p > 0."""
+    from paddle_hackathon_amd.ops import fused as FU
+    torch.manual_seed(0)
+    R, H = 2048, 768
+    x = torch.randn(R, H, device="cuda", dtype=dtype, requires_grad=True)
+    r = torch.randn(R, H, device="cuda", dtype=dtype, requires_grad=True)
+    xb = torch.randn(H, device="cuda", dtype=torch.float32, requires_grad=True)
+    w = (torch.rand(H, device="cuda") + 0.5).requires_grad_(True)
+    b = torch.randn(H, device="cuda", requires_grad=True)
+    y = FU.bias_dropout_residual_layer_norm(x, r, xb, w, b, 0.0, True, 1e-5)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    got = [t.grad.float().clone() for t in (x, r, xb, w, b)]
+    xs = [t.detach().float().requires_grad_(True) for t in (x, r, xb, w, b)]
+    yr = TF.layer_norm(xs[1] + (xs[0] + xs[2]), (H,), xs[3], xs[4], 1e-5)
+    yr.backward(gy.float())
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    for g, t in zip(got, xs):
+        torch.testing.assert_close(g, t.grad, atol=tol * 8, rtol=tol)
+    # p > 0: x = 1, no bias, residual 0 -> hs = mask / (1 - p); the backward regenerates that mask
+    p = 0.25
+    x1 = torch.ones(R, H, device="cuda", dtype=dtype, requires_grad=True)
+    r0 = torch.zeros(R, H, device="cuda", dtype=dtype, requires_grad=True)
+    y1 = FU.bias_dropout_residual_layer_norm(x1, r0, None, w.detach(), b.detach(), p, True, 1e-5)
+    g1 = torch.randn_like(y1)
+    y1.backward(g1)
+    keep = x1.grad != 0
+    frac = keep.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01
+    torch.testing.assert_close(x1.grad.float(), r0.grad.float() * keep / (1 - p), atol=1e-2, rtol=1e-2)
+    hs = keep.float() / (1 - p)
+    torch.testing.assert_close(y1.float(), TF.layer_norm(hs, (H,), w.detach(), b.detach(), 1e-5), atol=5e-2, rtol=3e-2)
