@@ -957,3 +957,4 @@ def test_bias_dropout_residual_layer_norm_kernel(dtype):
     torch.testing.assert_close(x1.grad.float(), r0.grad.float() * keep / (1 - p), atol=1e-2, rtol=1e-2)
     hs = keep.float() / (1 - p)
     torch.testing.assert_close(y1.float(), TF.layer_norm(hs, (H,), w.detach(), b.detach(), 1e-5), atol=5e-2, rtol=3e-2)
+
