@@ -29,7 +29,7 @@ import torch
 from ...utils import native
 
 __all__ = ["PSServer", "PSClient", "DistributedEmbedding", "PSOptimizer", "TheOnePSRuntime", "RULES",
-           "sparse_embedding"]
+           "sparse_embedding", "GpuPsTable", "GpuPsEmbedding"]
 
 RULES = {"sgd": 0, "naive": 0, "adagrad": 1, "std_adagrad": 2, "adam": 3, "sum": 4, "ctr": 5}
 
@@ -658,3 +658,6 @@ class PSOptimizer:
 
     def __getattr__(self, item):
         return getattr(self._inner_opt, item)
+
+
+from .gpu_ps import GpuPsTable, GpuPsEmbedding  # noqa: E402,F401  (HBM-resident sharded tables)
