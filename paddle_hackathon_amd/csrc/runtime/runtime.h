@@ -5,6 +5,7 @@
 //   bucket.cpp   - gradient bucket planner for DataParallel / sharding collectives
 //   tracer.cpp   - low-overhead host event tracer with chrome-trace export (profiler)
 //   arena.cpp    - best-fit, coalescing offset allocator (memory planner / flat buffers)
+//   fleet_executor.cpp - credit-based dataflow carrier over a task graph (fleet executor)
 #pragma once
 #include <cstddef>
 #include <cstdint>
