@@ -80,16 +80,19 @@ def convert_ifelse(pred, true_fn, false_fn, args):
 
 def convert_while_loop(cond_fn, body_fn, loop_vars):
     loop_vars = tuple(loop_vars)
-    c = cond_fn(*loop_vars)
-    if _is_static_var(c):
-        # tensor-dependent loop: one `while` op (variables first bound inside the body start UNDEFINED)
-        from ..static import control_flow
-        out = control_flow.while_loop(cond_fn, lambda *a: list(body_fn(*a)), list(loop_vars), undefined=UNDEFINED)
-        return tuple(out)
-    while _to_bool(c):
-        loop_vars = tuple(body_fn(*loop_vars))
+    while True:
         c = cond_fn(*loop_vars)
-    return loop_vars
+        if _is_static_var(c):
+            # tensor-dependent loop (from the start, or once the body made the condition depend on
+            # data, e.g. a break flag set under a tensor `if`): the remaining iterations are ONE
+            # `while` op (variables first bound inside the body start UNDEFINED)
+            from ..static import control_flow
+            out = control_flow.while_loop(cond_fn, lambda *a: list(body_fn(*a)), list(loop_vars),
+                                          undefined=UNDEFINED)
+            return tuple(out)
+        if not _to_bool(c):
+            return loop_vars
+        loop_vars = tuple(body_fn(*loop_vars))
 
 
 def convert_logical_and(*getters):
@@ -271,6 +274,39 @@ def _lift_returns(stmts):
     return out
 
 
+def _flag_set(name, value):
+    return ast.Assign(targets=[_name(name, ast.Store())], value=ast.Constant(value=value))
+
+
+def _flags_clear(brk, cnt):
+    """``not (brk or cnt)`` over the flags in use"""
+    fl = [_name(f) for f in (brk, cnt) if f]
+    return ast.UnaryOp(op=ast.Not(), operand=fl[0] if len(fl) == 1 else ast.BoolOp(op=ast.Or(), values=fl))
+
+
+def _lower_block(stmts, brk, cnt):
+    """break / continue of the enclosing loop -> flag assignments; the statements after a point
+    that may set a flag run under ``if not (brk or cnt)`` (reference break_continue_transformer)"""
+    out = []
+    for i, s in enumerate(stmts):
+        if isinstance(s, ast.Break):
+            out.append(_flag_set(brk, True))
+            return out
+        if isinstance(s, ast.Continue):
+            out.append(_flag_set(cnt, True))
+            return out
+        if isinstance(s, ast.If) and _contains([s], (ast.Break, ast.Continue), stop_at_loops=True):
+            s.body = _lower_block(s.body, brk, cnt) or [ast.Pass()]
+            s.orelse = _lower_block(s.orelse, brk, cnt)
+            out.append(s)
+            rest = stmts[i + 1:]
+            if rest:
+                out.append(ast.If(test=_flags_clear(brk, cnt), body=_lower_block(rest, brk, cnt), orelse=[]))
+            return out
+        out.append(s)
+    return out
+
+
 class _Transformer(ast.NodeTransformer):
     def __init__(self):
         self.k = 0
@@ -315,8 +351,28 @@ class _Transformer(ast.NodeTransformer):
             return [tdef, fdef, _assign_tuple(names, call)]
         return [tdef, fdef, ast.Expr(value=call)]
 
+    def _lower_loop(self, body, test, tail=()):
+        """-> (pre statements, body, test) with break / continue turned into loop-carried flags"""
+        has_b = _contains(body, (ast.Break,), stop_at_loops=True)
+        has_c = _contains(body, (ast.Continue,), stop_at_loops=True)
+        if not (has_b or has_c):
+            return [], body + list(tail), test
+        k = self._next()
+        brk = f"__pha_brk_{k}" if has_b else None
+        cnt = f"__pha_cnt_{k}" if has_c else None
+        pre = [_flag_set(f, False) for f in (brk, cnt) if f]
+        new_body = ([_flag_set(cnt, False)] if cnt else []) + _lower_block(list(body), brk, cnt) + list(tail)
+        if brk:
+            test = ast.BoolOp(op=ast.And(), values=[ast.UnaryOp(op=ast.Not(), operand=_name(brk)), test])
+        return pre, new_body, test
+
     # ---- while ---------------------------------------------------------------------------------
     def visit_While(self, node):
+        if not node.orelse and not _contains(node.body, (ast.Return,), stop_at_loops=True) and \
+                _contains(node.body, (ast.Break, ast.Continue), stop_at_loops=True):
+            pre, node.body, node.test = self._lower_loop(node.body, node.test)
+            res = self.visit_While(node)
+            return pre + (res if isinstance(res, list) else [res])
         self.generic_visit(node)
         if node.orelse or _contains(node.body, (ast.Break, ast.Continue, ast.Return), stop_at_loops=True) or \
                 _contains(node.body, (ast.Yield, ast.YieldFrom, ast.Global, ast.Nonlocal)):
@@ -339,7 +395,7 @@ class _Transformer(ast.NodeTransformer):
                 and not node.orelse):
             self.generic_visit(node)
             return node
-        if _contains(node.body, (ast.Break, ast.Continue, ast.Return), stop_at_loops=True):
+        if _contains(node.body, (ast.Return,), stop_at_loops=True):
             self.generic_visit(node)
             return node
         k = self._next()
@@ -351,14 +407,16 @@ class _Transformer(ast.NodeTransformer):
         pre = [ast.Assign(targets=[_name(idx, ast.Store())], value=start_e),
                ast.Assign(targets=[_name(stop, ast.Store())], value=stop_e),
                ast.Assign(targets=[_name(step, ast.Store())], value=step_e)]
-        body = [ast.Assign(targets=[_name(node.target.id, ast.Store())], value=_name(idx))] + node.body + [
-            ast.Assign(targets=[_name(idx, ast.Store())],
-                       value=ast.BinOp(left=_name(idx), op=ast.Add(), right=_name(step)))]
-        loop = ast.While(test=_call(_jst_attr("range_cond"), [_name(idx), _name(stop), _name(step)]), body=body,
-                         orelse=[])
+        incr = ast.Assign(targets=[_name(idx, ast.Store())],
+                          value=ast.BinOp(left=_name(idx), op=ast.Add(), right=_name(step)))
+        test = _call(_jst_attr("range_cond"), [_name(idx), _name(stop), _name(step)])
+        # break / continue: flags; the index increment stays outside the continue guard
+        fpre, body, test = self._lower_loop(
+            [ast.Assign(targets=[_name(node.target.id, ast.Store())], value=_name(idx))] + node.body, test, [incr])
+        loop = ast.While(test=test, body=body, orelse=[])
         # loop-carried set must include the hidden index: it is assigned in the body
         res = self.visit_While(loop)
-        return pre + (res if isinstance(res, list) else [res])
+        return pre + fpre + (res if isinstance(res, list) else [res])
 
     def visit_Call(self, node):
         self.generic_visit(node)

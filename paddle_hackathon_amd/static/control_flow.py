@@ -119,6 +119,10 @@ def cond(pred, true_fn=None, false_fn=None, undefined=None):
         if isinstance(a, Tensor) or isinstance(b, Tensor):
             like = a if isinstance(a, Tensor) else b
             outs.append(_meta_var(parent, like))
+        elif isinstance(a, (bool, int, float)) and isinstance(b, (bool, int, float)) and a != b:
+            # Python scalars that depend on the branch (dy2static flags, counters) become tensors
+            like = _wrap(torch.as_tensor(a if not isinstance(b, float) else b))
+            outs.append(_meta_var(parent, like))
         else:
             if a != b:
                 raise ValueError(f"cond: non-tensor outputs differ between branches ({a!r} vs {b!r})")

@@ -206,3 +206,65 @@ def test_jit_save_load_keeps_control_flow(tmp_path):
 
 def test_convert_function_is_cached():
     assert convert_function(if_else_mean) is convert_function(if_else_mean)
+
+
+def while_with_break(x):
+    i = paddle.zeros([1], dtype="int64")
+    s = paddle.zeros_like(x)
+    while i < 10:
+        s = s + x
+        if paddle.sum(s) > 12:
+            break
+        i = i + 1
+    return s, i
+
+
+def for_with_continue(x):
+    acc = paddle.zeros_like(x[0])
+    for k in range(paddle.shape(x)[0]):
+        if paddle.sum(x[k]) < 0:
+            continue
+        acc = acc + x[k]
+    return acc
+
+
+def for_break_and_continue(x):
+    acc = paddle.zeros_like(x[0])
+    n = paddle.zeros([1], dtype="int64")
+    for k in range(paddle.shape(x)[0]):
+        if paddle.sum(x[k]) < 0:
+            continue
+        if paddle.sum(acc) > 5:
+            break
+        acc = acc + x[k]
+        n = n + 1
+    return acc, n
+
+
+def python_loop_break(x):
+    out = x
+    for k in range(5):
+        if k == 3:
+            break
+        out = out + 1
+    return out
+
+
+@pytest.mark.parametrize("fn,inputs", [
+    (while_with_break, [np.ones((2,)), np.full((2,), 5.0), -np.ones((2,))]),
+    (for_with_continue, [np.array([[1.0, 2.0], [-5.0, 1.0], [3.0, 3.0]]), -np.ones((3, 2))]),
+    (for_break_and_continue, [np.array([[1.0, 2.0], [-5.0, 1.0], [3.0, 3.0], [9.0, 9.0]]), np.ones((4, 2))]),
+    (python_loop_break, [np.zeros((2,))]),
+], ids=["while_break", "for_continue", "for_break_continue", "python_break"])
+def test_break_continue(fn, inputs):
+    sf = paddle.jit.to_static(fn)
+    for x in inputs:
+        x = x.astype("float32")
+        ref = fn(paddle.to_tensor(x))
+        got = sf(paddle.to_tensor(x))
+        ref = ref if isinstance(ref, tuple) else (ref,)
+        got = got if isinstance(got, tuple) else (got,)
+        for a, b in zip(got, ref):
+            np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-6)
+    if fn is not python_loop_break:
+        assert len(sf._cache) == len({x.shape for x in inputs})
