@@ -3,9 +3,10 @@ python/paddle/distributed/fleet/meta_parallel/parallel_layers/{mp_layers,random}
 python/paddle/distributed/collective.py:_c_identity/_c_concat/_c_split/_mp_allreduce/split,
 python/paddle/distributed/fleet/layers/mpu/mp_ops.py:_c_softmax_with_cross_entropy).
 
-The TP group is a set of consecutive ranks (GPUs of one node, xGMI-connected); every
-collective below is one RCCL call on that group, issued on the compute stream so it
-orders with the GEMMs around it.
+The TP group is a set of consecutive ranks (GPUs of one node, xGMI-connected). The linear
+layers split their rows into pieces (``PHA_TP_OVERLAP_CHUNKS``, default 2) so the all-reduce of
+one piece runs on the RCCL stream while the next piece's GEMM (or, in the column layer's
+backward, the weight-gradient GEMM) runs on the compute stream.
 """
 from __future__ import annotations
 
@@ -114,6 +115,78 @@ class _Concat(torch.autograd.Function):
         return g[..., ctx.rk * n:(ctx.rk + 1) * n].contiguous(), None, None, None
 
 
+def _tp_chunks(rows):
+    """token-dim pieces for GEMM / all-reduce overlap (``PHA_TP_OVERLAP_CHUNKS``, default 2; small
+    inputs stay whole: a collective's latency would not hide behind a tiny GEMM)"""
+    import os
+    k = int(os.environ.get("PHA_TP_OVERLAP_CHUNKS", "2"))
+    return k if k > 1 and rows >= 256 * k else 1
+
+
+def _row_splits(rows, k):
+    step = -(-rows // k)
+    return [(i, min(rows, i + step)) for i in range(0, rows, step)]
+
+
+class _RowParallelMatmul(torch.autograd.Function):
+    """y = all_reduce(x @ W) with the rows in pieces: the all-reduce of piece i runs on the RCCL
+    stream while the GEMM of piece i+1 runs on the compute stream (the output buffer is written in
+    place, no concat). Backward is local (the all-reduce's gradient is the identity)."""
+
+    @staticmethod
+    def forward(ctx, x, w, pg, chunks):
+        ctx.save_for_backward(x, w)
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.empty(x2.shape[0], w.shape[1], dtype=x.dtype, device=x.device)
+        works = []
+        for a, b in _row_splits(x2.shape[0], chunks):
+            torch.mm(x2[a:b], w, out=y[a:b])
+            works.append(dist.all_reduce(y[a:b], group=pg, async_op=True))
+        for wk in works:
+            wk.wait()
+        return y.reshape(*x.shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = (g2 @ w.t()).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dw = x2.t() @ g2 if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None
+
+
+class _ColumnParallelMatmul(torch.autograd.Function):
+    """y = x @ W (+ b) on a column shard; backward: dX = all_reduce(dY W^T) in row pieces whose
+    all-reduces overlap the remaining dX pieces and the dW / db GEMMs (the c_identity of the
+    input folded into this op)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, pg, chunks):
+        ctx.save_for_backward(x, w)
+        ctx.pg, ctx.chunks, ctx.has_b = pg, chunks, b is not None
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(b, x2, w) if b is not None else x2 @ w
+        return y.reshape(*x.shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1])
+        dx, works = None, []
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(g2.shape[0], w.shape[0], dtype=g.dtype, device=g.device)
+            for a, b in _row_splits(g2.shape[0], ctx.chunks):
+                torch.mm(g2[a:b], w.t(), out=dx[a:b])
+                works.append(dist.all_reduce(dx[a:b], group=ctx.pg, async_op=True))
+        dw = x2.t() @ g2 if ctx.needs_input_grad[1] else None      # overlaps the dX all-reduces
+        db = g2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        for wk in works:
+            wk.wait()
+        return (dx.reshape(x.shape) if dx is not None else None), dw, db, None, None
+
+
 def _c_identity(x, group=None):
     group = group if group is not None else _mp_group()
     if _ws(group) == 1:
@@ -189,8 +262,14 @@ class ColumnParallelLinear(Layer):
             self.bias = None
 
     def forward(self, x):
-        x = _c_identity(x, self.model_parallel_group)
-        y = F.linear(x, self.weight, self.bias)
+        xt = x._t if isinstance(x, Tensor) else x
+        if self.world_size > 1 and type(xt).__name__ != "DTensor" and xt.dim() >= 2:
+            rows = xt.numel() // xt.shape[-1]
+            y = _wrap(_ColumnParallelMatmul.apply(xt, self.weight._t, None if self.bias is None else self.bias._t,
+                                                  _pg(self.model_parallel_group), _tp_chunks(rows)))
+        else:
+            x = _c_identity(x, self.model_parallel_group)
+            y = F.linear(x, self.weight, self.bias)
         if self.gather_output and self.world_size > 1:
             y = _c_concat(y, self.model_parallel_group)
         return y
@@ -213,8 +292,13 @@ class RowParallelLinear(Layer):
     def forward(self, x):
         if not self.input_is_parallel and self.world_size > 1:
             x = _c_split(x, self.model_parallel_group)
-        y = F.linear(x, self.weight, None)
-        y = _mp_allreduce(y, self.model_parallel_group)
+        xt = x._t if isinstance(x, Tensor) else x
+        if self.world_size > 1 and type(xt).__name__ != "DTensor" and xt.dim() >= 2:
+            rows = xt.numel() // xt.shape[-1]
+            y = _wrap(_RowParallelMatmul.apply(xt, self.weight._t, _pg(self.model_parallel_group), _tp_chunks(rows)))
+        else:
+            y = F.linear(x, self.weight, None)
+            y = _mp_allreduce(y, self.model_parallel_group)
         if self.bias is not None:
             y = y + self.bias
         return y

@@ -506,3 +506,48 @@ def test_gpt_fleet_data_parallel_matches_single_process():
     for r in res:
         for n in names:
             np.testing.assert_allclose(r[n], params[n].numpy(), rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+def _tp_overlap(rank, world, chunks):
+    import os
+    os.environ["PHA_TP_OVERLAP_CHUNKS"] = str(chunks)
+    import torch
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": 1, "mp_degree": world, "pp_degree": 1}
+    fleet.init(is_collective=True, strategy=strategy)
+    from paddle_hackathon_amd.parallel.mp_layers import ColumnParallelLinear, RowParallelLinear
+    paddle.seed(5)
+    col = ColumnParallelLinear(16, 32, has_bias=True, gather_output=False)
+    row = RowParallelLinear(32, 16, has_bias=True, input_is_parallel=True)
+    rng = np.random.RandomState(9)
+    full_w1 = rng.randn(16, 32).astype("float32") * 0.2
+    full_w2 = rng.randn(32, 16).astype("float32") * 0.2
+    col.weight.set_value(full_w1[:, rank * 16:(rank + 1) * 16])
+    col.bias.set_value(np.zeros(16, "float32") + 0.1)
+    row.weight.set_value(full_w2[rank * 16:(rank + 1) * 16])
+    x = paddle.to_tensor(rng.randn(1024, 16).astype("float32"), stop_gradient=False)
+    y = row(paddle.nn.functional.relu(col(x)))
+    (y ** 2).mean().backward()
+    return {"y": y.numpy(), "dx": x.grad.numpy(), "dw1": col.weight.grad.numpy(), "dw2": row.weight.grad.numpy()}
+
+
+def test_tensor_parallel_chunked_overlap_matches_serial():
+    """row pieces with async all-reduces (GEMM / comm overlap) give the serial MLP's values"""
+    res = run_dist(_tp_overlap, 2, (4,))
+    rng = np.random.RandomState(9)
+    w1 = rng.randn(16, 32).astype("float32") * 0.2
+    w2 = rng.randn(32, 16).astype("float32") * 0.2
+    x = rng.randn(1024, 16).astype("float32")
+    import torch
+    xt = torch.tensor(x, requires_grad=True)
+    W1 = torch.tensor(w1, requires_grad=True)
+    W2 = torch.tensor(w2, requires_grad=True)
+    y = torch.relu(xt @ W1 + 0.1) @ W2
+    (y ** 2).mean().backward()
+    for r, out in enumerate(res):
+        np.testing.assert_allclose(out["y"], y.detach().numpy() + 0.0, rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(out["dx"], xt.grad.numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(out["dw1"], W1.grad.numpy()[:, r * 16:(r + 1) * 16], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(out["dw2"], W2.grad.numpy()[r * 16:(r + 1) * 16], rtol=1e-4, atol=1e-6)
