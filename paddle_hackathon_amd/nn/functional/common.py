@@ -273,11 +273,12 @@ def temporal_shift(x, seg_num, shift_ratio=0.25, name=None, data_format="NCHW"):
     nt, c, h, w = t.shape
     n = nt // seg_num
     t5 = t.reshape(n, seg_num, c, h, w)
-    fold_ = int(c * shift_ratio)
+    # reference temporal_shift_op: channels [0, c1) take frame t-1, [c1, c2) frame t+1, the rest stay
+    c1, c2 = int(c * shift_ratio), int(c * 2 * shift_ratio)
     out = torch.zeros_like(t5)
-    out[:, :-1, :fold_] = t5[:, 1:, :fold_]
-    out[:, 1:, fold_:2 * fold_] = t5[:, :-1, fold_:2 * fold_]
-    out[:, :, 2 * fold_:] = t5[:, :, 2 * fold_:]
+    out[:, 1:, :c1] = t5[:, :-1, :c1]
+    out[:, :-1, c1:c2] = t5[:, 1:, c1:c2]
+    out[:, :, c2:] = t5[:, :, c2:]
     out = out.reshape(nt, c, h, w)
     if data_format == "NHWC":
         out = out.permute(0, 2, 3, 1)

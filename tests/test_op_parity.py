@@ -548,3 +548,138 @@ def test_conv_pool_pad():
     np.testing.assert_allclose(F.dropout(P(x), 0.3, training=False, mode="downscale_in_infer").numpy(), x * 0.7)
     np.testing.assert_allclose(paddle.clip(P(x), -0.2, 0.3).numpy(), np.clip(x, -0.2, 0.3))
     np.testing.assert_allclose(F.linear(P(U(3, 4)), P(w.reshape(4, -1)[:, :5] if False else U(4, 5))).numpy().shape, (3, 5))
+
+
+# ----------------------------------------------------------------------------- batch 2 (less common ops)
+def test_renorm_fixture():
+    # test_renorm_op.py: values and expected output copied from the reference test's fixture
+    x = np.array([[[2.0, 2, -2], [3, 0.3, 3]], [[2, -8, 2], [3.1, 3.7, 3]]])
+    expected = np.array([[[0.40594056, 0.29285714, -0.41000000], [0.60891086, 0.04392857, 0.61500001]],
+                         [[0.40594056, -1.17142856, 0.41000000], [0.62920785, 0.54178572, 0.61500001]]])
+    np.testing.assert_allclose(paddle.renorm(P(x), 1.0, 2, 2.05).numpy(), expected, rtol=1e-6)
+
+
+def test_sigmoid_focal_loss():
+    # test_sigmoid_focal_loss.py calc_sigmoid_focal_loss
+    F = paddle.nn.functional
+    logit = U(5, 3, lo=-3, hi=3)
+    label = (U(5, 3) > 0).astype("float64")
+    norm = np.array([2.5])
+    loss = np.maximum(logit, 0) - logit * label + np.log(1 + np.exp(-np.abs(logit)))
+    pred = 1 / (1 + np.exp(-logit))
+    p_t = pred * label + (1 - pred) * (1 - label)
+    loss = (0.25 * label + 0.75 * (1 - label)) * loss * (1 - p_t) ** 2.0 / norm
+    np.testing.assert_allclose(F.sigmoid_focal_loss(P(logit), P(label), P(norm), reduction="sum").numpy().reshape(-1),
+                               [loss.sum()], rtol=1e-6)
+    np.testing.assert_allclose(F.sigmoid_focal_loss(P(logit), P(label), P(norm), reduction="none").numpy(), loss,
+                               rtol=1e-6)
+
+
+def test_log_loss_and_square_error():
+    F = paddle.nn.functional
+    pred = 1 / (1 + np.exp(-U(10, 1)))
+    lab = (U(10, 1) > 0).astype("float64")
+    want = -lab * np.log(pred + 1e-4) - (1 - lab) * np.log(1 - pred + 1e-4)     # test_log_loss_op.py
+    np.testing.assert_allclose(F.log_loss(P(pred), P(lab), epsilon=1e-4).numpy(), want, rtol=1e-6)
+    a, b = U(4, 3), U(4, 3)
+    np.testing.assert_allclose(F.square_error_cost(P(a), P(b)).numpy(), (a - b) ** 2)
+
+
+def test_temporal_shift():
+    # test_temporal_shift_op.py temporal_shift
+    x = U(6, 4, 2, 2)
+    seg, ratio = 3, 0.25
+    shape = x.shape
+    r = x.reshape((-1, seg) + shape[1:])
+    pad = np.pad(r, ((0, 0), (1, 1), (0, 0), (0, 0), (0, 0)))
+    c1, c2 = int(shape[1] * ratio), int(shape[1] * 2 * ratio)
+    want = np.concatenate([pad[:, :seg, :c1], pad[:, 2:seg + 2, c1:c2], pad[:, 1:seg + 1, c2:]], 2).reshape(shape)
+    np.testing.assert_allclose(paddle.nn.functional.temporal_shift(P(x), seg, ratio).numpy(), want)
+
+
+def test_gather_tree_backtrace():
+    # test_gather_tree_op.py backtrace
+    ids = R.randint(0, 10, (5, 2, 3)).astype("int64")
+    parents = R.randint(0, 3, (5, 2, 3)).astype("int64")
+    T, B, K = ids.shape
+    want = np.zeros_like(ids)
+    for b in range(B):
+        for k in range(K):
+            want[T - 1, b, k] = ids[T - 1, b, k]
+            p = parents[T - 1, b, k]
+            for t in range(T - 2, -1, -1):
+                want[t, b, k] = ids[t, b, p]
+                p = parents[t, b, p]
+    np.testing.assert_array_equal(paddle.nn.functional.gather_tree(P(ids), P(parents)).numpy(), want)
+
+
+def test_multiplex_and_misc_math():
+    rows = 4
+    index = np.array([[2], [0], [3], [1]], dtype="int32")
+    ins = [U(rows, 5) for _ in range(4)]
+    want = np.stack([ins[index[i, 0]][i] for i in range(rows)])            # test_multiplex_op.py
+    np.testing.assert_allclose(paddle.multiplex([P(t) for t in ins], P(index)).numpy(), want)
+    a, b = U(3, 4), U(3, 4)
+    np.testing.assert_allclose(paddle.lerp(P(a), P(b), 0.3).numpy(), a + 0.3 * (b - a))
+    np.testing.assert_allclose(paddle.diff(P(a), axis=1).numpy(), np.diff(a, axis=1))
+    np.testing.assert_allclose(paddle.rot90(P(a), 1, [0, 1]).numpy(), np.rot90(a, 1, (0, 1)))
+    np.testing.assert_allclose(paddle.inner(P(a), P(b)).numpy(), np.inner(a, b))
+    np.testing.assert_allclose(paddle.outer(P(a[0]), P(b[0])).numpy(), np.outer(a[0], b[0]))
+    np.testing.assert_allclose(paddle.addmm(P(a[:, :3]), P(a), P(b.T[:, :3])).numpy(), a[:, :3] + a @ b.T[:, :3])
+    gi, gj = np.array([12, 18, -9]), np.array([8, 12, 6])
+    np.testing.assert_array_equal(paddle.gcd(P(gi), P(gj)).numpy(), np.gcd(gi, gj))
+    np.testing.assert_array_equal(paddle.lcm(P(gi), P(gj)).numpy(), np.lcm(gi, gj))
+    np.testing.assert_allclose(paddle.quantile(P(a), 0.3, axis=1).numpy(), np.quantile(a, 0.3, axis=1))
+    np.testing.assert_allclose(paddle.frac(P(a * 5)).numpy(), np.modf(a * 5)[0])
+    np.testing.assert_allclose(paddle.diagflat(P(a[0])).numpy(), np.diagflat(a[0]))
+    np.testing.assert_allclose(paddle.erfinv(P(x_unit)).numpy(),
+                               np.vectorize(lambda v: _erfinv(v))(x_unit), rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(paddle.angle(P(np.array([1 + 1j, -1 + 0j, 0 - 2j]))).numpy(),
+                               np.angle(np.array([1 + 1j, -1 + 0j, 0 - 2j])))
+
+
+def _erfinv(y):
+    # Newton on erf (no scipy): erf'(x) = 2/sqrt(pi) exp(-x^2)
+    x = 0.0
+    for _ in range(60):
+        x -= (math.erf(x) - y) / (2 / math.sqrt(math.pi) * math.exp(-x * x))
+    return x
+
+
+def test_sequence_mask_channel_shuffle_unfold():
+    F = paddle.nn.functional
+    lens = np.array([1, 3, 0, 2])
+    want = (np.arange(4)[None, :] < lens[:, None]).astype("int64")
+    np.testing.assert_array_equal(F.sequence_mask(P(lens), maxlen=4).numpy(), want)
+    x = U(2, 6, 3, 3)
+    g = 3
+    want = x.reshape(2, g, 2, 3, 3).transpose(0, 2, 1, 3, 4).reshape(2, 6, 3, 3)   # test_channel_shuffle.py
+    np.testing.assert_allclose(F.channel_shuffle(P(x), g).numpy(), want)
+    # unfold (im2col): [N, C*kh*kw, L] (test_unfold_op.py)
+    xx = U(1, 2, 4, 4)
+    cols = F.unfold(P(xx), [2, 2], strides=2).numpy()
+    want = np.stack([xx[0, :, i:i + 2, j:j + 2].reshape(-1) for i in (0, 2) for j in (0, 2)], 1)[None]
+    np.testing.assert_allclose(cols, want)
+    np.testing.assert_allclose(F.pixel_shuffle(F.pixel_unshuffle(P(x[:, :4]), 1), 1).numpy(), x[:, :4]) \
+        if hasattr(F, "pixel_unshuffle") else None
+
+
+def test_margin_and_hinge_losses():
+    F = paddle.nn.functional
+    a = U(6, 4)
+    lab = np.sign(U(6, 4))
+    # soft_margin_loss: mean(log(1 + exp(-y x))) (reference nn/functional/loss.py soft_margin_loss)
+    if hasattr(F, "soft_margin_loss"):
+        np.testing.assert_allclose(F.soft_margin_loss(P(a), P(lab)).numpy().reshape(-1),
+                                   [np.log(1 + np.exp(-lab * a)).mean()], rtol=1e-6)
+    # npair_loss (test_npair_loss_op.py): softmax CE over anchor.positive^T + l2 reg
+    anchor, pos = U(4, 3), U(4, 3)
+    labels = np.array([0, 1, 2, 1]).astype("float64")
+    l2 = 0.002
+    sim = anchor @ pos.T
+    same = (labels[:, None] == labels[None, :]).astype("float64")
+    tgt = same / same.sum(1, keepdims=True)
+    ce = -(tgt * np.log(softmax_np(sim))).sum(1).mean()
+    reg = l2 * 0.25 * ((anchor ** 2).sum(1).mean() + (pos ** 2).sum(1).mean())
+    np.testing.assert_allclose(F.npair_loss(P(anchor), P(pos), P(labels), l2_reg=l2).numpy().reshape(-1),
+                               [ce + reg], rtol=1e-6)
