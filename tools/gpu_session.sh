@@ -20,6 +20,9 @@ for s in "$@"; do
     bench)
       timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
       tail -3 $OUT/bench.log ;;
+    bench_ln)
+      timeout -k 10 300 python tools/bench_ln.py > $OUT/bench_ln.log 2>&1; rc=$?
+      tail -3 $OUT/bench_ln.log ;;
     bench_bert)
       timeout -k 10 400 python bench.py --model bert-base --steps 10 --warmup 3 > $OUT/bench_bert.log 2>&1; rc=$?
       tail -3 $OUT/bench_bert.log ;;
