@@ -45,6 +45,8 @@ enum : int {
   EPI_DGELU = 8,    // C = v * gelu_tanh'(aux[m][n])
   EPI_COLSUM = 16,  // colsum[tile_m][n] = sum of the tile's rows of the final fp32 C
   EPI_AUXOUT = 32,
+  EPI_TRANS = 64,   // store C^T: the kernel computes the transposed product (see pha_gemm4w)
+  EPI_SKIP = 128,   // measurement only: no epilogue (tools/g4w_fixed.py)
 };
 
 struct Args {
@@ -104,7 +106,7 @@ __device__ __forceinline__ float ld_elem(uint4 v, int e) {
 // SCHED bit 0: compiler-scheduled (else fragment reads / LDS-DMA issues pinned between groups of
 // 4 MFMAs by sched_barrier); bit 1: reads spread one per MFMA group (else front-loaded); bit 2:
 // early staging (tile t+2 issued mid phase A behind a second barrier)
-template <typename T, bool AKO, bool BKO, int SCHED>
+template <typename T, bool AKO, bool BKO, int SCHED, bool OT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -312,13 +314,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   bar();
 
   // ---- epilogue ---------------------------------------------------------------------------------
+  // OT: the tile is C^T (kernel rows = output columns). Output rows [r0, r0 + 256) of the Mo x No
+  // result, columns [c0, c0 + 256); the accumulators are staged through LDS in two 128-row halves
+  // of the OUTPUT (kernel row halves wr, or with OT kernel column halves wc, written as 16-B
+  // vectors since a fragment's 4 accumulator rows are 4 consecutive output columns)
   const int epi = p.epi;
+  if (epi & EPI_SKIP) return;
+  const int Mo = OT ? N : M, No = OT ? M : N, r0 = OT ? n0 : m0, c0 = OT ? m0 : n0, rt = OT ? tn : tm;
   T* C = static_cast<T*>(p.c);
   T* AUX = static_cast<T*>(p.aux);
   float* stg = reinterpret_cast<float*>(smem);
-  const int c8 = tid & 31, rl = tid >> 5;   // this thread: columns n0 + c8*8 .. +7, rows rl + 8 r
-  const int n = n0 + c8 * 8;
-  const bool ncol = n < N;
+  const int c8 = tid & 31, rl = tid >> 5;   // this thread: columns c0 + c8*8 .. +7, rows rl + 8 r
+  const int n = c0 + c8 * 8;
+  const bool ncol = n < No;
   float bv[8], cs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -327,25 +335,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (wr == h) {
+    if constexpr (OT) {
+      if (wc == h) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+          for (int j = 0; j < 8; ++j)
+            *reinterpret_cast<f32x4*>(smem + (j * 16 + fr) * CROWF + (wr * 128 + i * 16 + 4 * fk) * 4) = acc[i][j];
+      }
+    } else {
+      if (wr == h) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int ml = i * 16 + 4 * fk + e, nl = wc * 128 + j * 16 + fr;
-            *reinterpret_cast<float*>(smem + ml * CROWF + nl * 4) = acc[i][j][e];
-          }
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int ml = i * 16 + 4 * fk + e, nl = wc * 128 + j * 16 + fr;
+              *reinterpret_cast<float*>(smem + ml * CROWF + nl * 4) = acc[i][j][e];
+            }
+      }
     }
     __syncthreads();
 #pragma unroll 4
     for (int r = 0; r < 16; ++r) {
       const int ml = rl + 8 * r;
-      const long m = m0 + h * 128 + ml;
+      const long m = r0 + h * 128 + ml;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32 + 16);
-      if (m >= M || !ncol) continue;
+      if (m >= Mo || !ncol) continue;
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       uint4 auxv;
       if (epi & EPI_DGELU) auxv = *reinterpret_cast<const uint4*>(AUX + m * p.ldaux + n);
@@ -374,13 +392,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float s = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) s += stg[r * 264 + col];
-    if (n0 + col < N) p.colsum[(long)tm * N + n0 + col] = s;
+    if (c0 + col < No) p.colsum[(long)rt * No + c0 + col] = s;
   }
 }
 
 template <typename T, int SCHED>
 int launch(const Args& a, int ako, int bko, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  if (a.epi & EPI_TRANS) {   // only the layout whose main loop keeps every accumulator in AGPRs
+    if (!(ako && !bko)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED, true>), dim3(grid), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if (!ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, false, SCHED>), dim3(grid), dim3(256), 0, st, a);
   else if (!ako && bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, true, SCHED>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED>), dim3(grid), dim3(256), 0, st, a);
@@ -409,6 +432,10 @@ using namespace pha;
 // operand dims >= 8; every byte offset inside one 256-row / 64-k operand panel < 2^32.
 // epi: see g4w::EPI_*; bias fp32 [N]; aux [M][ldaux] (pre-activation in or out);
 // colsum fp32 [ceil(M/256)][N] partials (finish with pha_colsum_finish).
+// EPI_TRANS (a_kouter = 1, b_kouter = 0 only): C (and aux) hold the TRANSPOSED product, [N][ldc];
+// bias is indexed by C's column (the kernel's m), colsum is [ceil(N/256)][M]. The NN product
+// x[M][K] . W[K][N] runs as this with A = W (K-outer) and B^T = x: the direct NN instantiation
+// leaves accumulators cycling through VGPRs (serialised MFMAs), this one keeps them in AGPRs.
 PHA_API int pha_gemm4w(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
                        long ldc, int a_kouter, int b_kouter, int epi, const float* bias, void* aux, long ldaux,
                        float* colsum, int sched, hipStream_t stream) {

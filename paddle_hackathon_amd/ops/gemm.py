@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 
-EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT = 1, 2, 4, 8, 16, 32
+EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT, EPI_TRANS = 1, 2, 4, 8, 16, 32, 64
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
@@ -56,7 +56,7 @@ def sched_variant(a_kouter=False, b_kouter=False):
     env = os.environ.get("PHA_G4W_SCHED")
     if env is not None:
         return int(env)
-    return 0 if (a_kouter and b_kouter) else 2
+    return 0 if a_kouter else 2
 
 
 def supported(M, N, K, *tensors):
@@ -75,8 +75,13 @@ def supported(M, N, K, *tensors):
 
 
 def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, aux_out=False, colsum=False,
-         out=None):
+         out=None, trans_out=False):
     """C = epi(op(A) @ op(B)).
+
+    trans_out (a_kouter=True, b_kouter=False only): return C^T [N, M] instead — bias is indexed
+    by C^T's column (length M), colsum sums C^T's rows ([ceil(N/256), M] partials). ``nn`` below
+    uses it to run x @ W as (W^T x^T)^T on the layout whose main loop keeps the accumulators in
+    AGPRs.
 
     act: None | "gelu" | "relu" | "dgelu" (C = acc * gelu'(aux), aux = forward pre-activation).
     aux_out: with act="gelu", also write the pre-activation (acc + bias) into ``aux`` (allocated
@@ -87,8 +92,11 @@ def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, au
     M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
     N, Kb = (b.shape[1], b.shape[0]) if b_kouter else (b.shape[0], b.shape[1])
     assert Ka == Kb, (a.shape, b.shape, a_kouter, b_kouter)
-    c = out if out is not None else torch.empty(M, N, dtype=a.dtype, device=a.device)
-    assert c.shape == (M, N) and c.stride(1) == 1
+    if trans_out:
+        assert a_kouter and not b_kouter, "trans_out needs a_kouter=True, b_kouter=False"
+    OM, ON = (N, M) if trans_out else (M, N)
+    c = out if out is not None else torch.empty(OM, ON, dtype=a.dtype, device=a.device)
+    assert c.shape == (OM, ON) and c.stride(1) == 1
     epi = 0
     if bias is not None:
         bias = bias.float().contiguous()
@@ -98,18 +106,20 @@ def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, au
     elif act == "relu":
         epi |= EPI_RELU
     elif act == "dgelu":
-        assert aux is not None and aux.shape == (M, N) and aux.stride(1) == 1
+        assert aux is not None and aux.shape == (OM, ON) and aux.stride(1) == 1
         epi |= EPI_DGELU
     elif act is not None:
         raise ValueError(f"unknown epilogue activation {act}")
     if aux_out:
         if aux is None:
-            aux = torch.empty(M, N, dtype=a.dtype, device=a.device)
+            aux = torch.empty(OM, ON, dtype=a.dtype, device=a.device)
         epi |= EPI_AUXOUT
     cs = None
     if colsum:
-        cs = torch.empty((M + 255) // 256, N, dtype=torch.float32, device=a.device)
+        cs = torch.empty((OM + 255) // 256, ON, dtype=torch.float32, device=a.device)
         epi |= EPI_COLSUM
+    if trans_out:
+        epi |= EPI_TRANS
     rc = _L().pha_gemm4w(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), epi, _ptr(bias), _ptr(aux),
                          aux.stride(0) if aux is not None else 0, _ptr(cs), sched_variant(a_kouter, b_kouter), _stream(a))
@@ -192,13 +202,19 @@ def mm_nt_bias(a, bt, bias):
     return fns[_pick(("ntb", a.dtype, M, N, K), fns)]()
 
 
+def nn(a, b, **epi):
+    """a [M, K] @ b [K, N] (+ epilogue) on the own kernel as (b^T a^T)^T: A = b (K-outer),
+    B^T = a, transposed store"""
+    return gemm(b, a, True, False, trans_out=True, **epi)
+
+
 def mm_nn(a, b):
     """a [M, K] @ b [K, N]"""
     fns = [lambda: a @ b]
     M, K = a.shape
     N = b.shape[1]
     if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
-        fns.append(lambda: gemm(a, b, False, True))
+        fns.append(lambda: nn(a, b))
     return fns[_pick(("nn", a.dtype, M, N, K), fns)]()
 
 

@@ -790,6 +790,34 @@ def test_gemm4w_fused_epilogues():
     assert (relu.float() - torch.relu(h)).abs().max() / h.abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("sched", [0, 4])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (264, 520, 128), (1032, 768, 640)])
+def test_gemm4w_transposed_store(monkeypatch, sched, M, N, K):
+    """x @ W as (W^T x^T)^T on the A-K-outer layout with the transposed-store epilogue (ops/gemm.nn)
+    including bias + GELU + stored pre-activation and dGELU + column sums, vs fp32"""
+    from paddle_hackathon_amd.ops import gemm as G
+    monkeypatch.setenv("PHA_G4W_SCHED", str(sched))
+    torch.manual_seed(5)
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    w = (torch.rand(K, N, device="cuda") * 2 - 1).bfloat16()
+    ref = x.float() @ w.float()
+    c = G.nn(x, w)
+    assert c.shape == (M, N) and (c.float() - ref).abs().max() / ref.abs().max() < 1e-2
+    bias = torch.randn(N, device="cuda")
+    act, pre = G.nn(x, w, bias=bias, act="gelu", aux_out=True)
+    h = ref + bias
+    assert (pre.float() - h).abs().max() / h.abs().max() < 1e-2
+    assert (act.float() - TF.gelu(h, approximate="tanh")).abs().max() / h.abs().max() < 1e-2
+    dy = (torch.rand(M, N, device="cuda") * 2 - 1).bfloat16()
+    hp = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    dh, part = G.nn(dy, w.t().contiguous(), act="dgelu", aux=hp, colsum=True)
+    xg = hp.float().requires_grad_()
+    dh_ref = torch.autograd.grad(TF.gelu(xg, approximate="tanh"), xg, dy.float() @ w.float().t())[0]
+    assert (dh.float() - dh_ref).abs().max() / dh_ref.abs().max() < 1e-2
+    db = G.colsum_finish(part, torch.float32)
+    assert (db - dh_ref.sum(0)).abs().max() / dh_ref.sum(0).abs().max() < 1e-2
+
+
 def test_gemm_picks_match_reference():
     """the per-shape own/library pick entry points (mm_nt / mm_nn / mm_tn / mm_nt_bias) vs fp32"""
     from paddle_hackathon_amd.ops import gemm as G

@@ -105,6 +105,12 @@ for s in "$@"; do
     bench_gemm)
       timeout -k 10 600 python tools/bench_gemm.py > $OUT/bench_gemm.log 2>&1; rc=$?
       cat $OUT/bench_gemm.log | tail -20 ;;
+    g4w_fixed)
+      timeout -k 10 300 python tools/g4w_fixed.py > $OUT/g4w_fixed.log 2>&1; rc=$?
+      tail -12 $OUT/g4w_fixed.log ;;
+    g4w_nn)
+      timeout -k 10 300 python tools/bench_g4w_nn.py > $OUT/g4w_nn.log 2>&1; rc=$?
+      tail -40 $OUT/g4w_nn.log ;;
     g4w)
       timeout -k 10 300 python tools/bench_g4w.py > $OUT/g4w.log 2>&1; rc=$?
       tail -40 $OUT/g4w.log ;;
