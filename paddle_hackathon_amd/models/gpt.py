@@ -114,6 +114,12 @@ class GPTMLP(nn.Layer):
             self.linear2 = nn.Linear(f, h, weight_attr=_w_attr(cfg, out_scale))
 
     def forward(self, x):
+        if self.cfg.tensor_parallel_degree <= 1:
+            from ..ops import mlp as _mlp
+            l1, l2 = self.linear1, self.linear2
+            if _mlp.available(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t):
+                # one node: bias+GELU folded into the GEMM epilogues when that measures faster
+                return _wrap(_mlp.fused_mlp(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t))
         if self.cfg.tensor_parallel_degree > 1:
             # column-parallel fc1 computed here (bias fused into the GELU): its input must pass
             # c_identity so the backward all-reduces the partial input gradients over the TP group

@@ -1,0 +1,132 @@
+"""Transformer MLP  y = gelu_tanh(x W1 + b1) W2 + b2  as ONE autograd node with the GELU folded into
+the GEMMs on either side of it.
+
+Reference behaviour: ``fused_feedforward`` / the fused_gemm_epilogue op
+(paddle/fluid/operators/fused/fused_gemm_epilogue_op.cu:29 bias+gelu forward with the
+pre-activation kept as "reserve space", :298 dgelu + bias-grad backward), as used by the GPT
+fleet models.
+
+Two chains compute the same thing; the faster one is picked once per shape by timing both on the
+real operands (``PHA_FUSED_MLP=0`` forces the first):
+
+  0  library fc1 GEMM (NT on the cached W1^T) -> HIP bias+GELU pass; backward: library NT dgrad of
+     fc2 -> HIP dGELU+bias-grad pass
+  1  own fc1 GEMM (ops/gemm.nn: transposed-store gemm4w) with bias + GELU + stored pre-activation
+     in its epilogue; backward: own NT dgrad of fc2 with dGELU against the stored pre-activation
+     and the fc1 bias-gradient column sums in its epilogue
+
+Everything else (fc2 forward, both weight gradients, fc1 dgrad) runs on the per-shape library /
+own picks of ops/gemm.py and ops/conv_gemm.py in both chains.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import gemm as G
+from . import hip as _hip
+
+_modes = {}
+
+
+def _eligible(x2d, w1, b1, w2, b2):
+    return (x2d.is_cuda and x2d.dtype in (torch.bfloat16, torch.float16)
+            and all(t is not None and t.dtype == x2d.dtype and t.is_contiguous() for t in (w1, b1, w2, b2))
+            and w1.dim() == 2 and w2.dim() == 2 and w1.shape[1] == w2.shape[0] and x2d.shape[1] == w1.shape[0])
+
+
+def _own_ok(x2d, w1, w2):
+    M, H = x2d.shape
+    F = w1.shape[1]
+    return (G._own_ok(x2d, w1, w2) and G.supported(F, M, H, w1, x2d) and G.supported(M, F, H, x2d, w2))
+
+
+def _fwd(mode, x2d, w1, b1):
+    """-> (activation, saved pre-activation); mode 0 saves x W1 (bias not added), mode 1 x W1 + b1"""
+    if mode == 1:
+        return G.nn(x2d, w1, bias=b1, act="gelu", aux_out=True)
+    from .conv_gemm import weight_t
+    h = G.mm_nt(x2d, weight_t(w1))
+    return _hip.bias_gelu_fwd(h, b1, True), h
+
+
+def _bwd_gelu(mode, gy, w2, pre, b1):
+    """-> (d pre-activation, d b1) from the MLP output gradient"""
+    if mode == 1:
+        g, part = G.gemm(gy, w2, False, False, act="dgelu", aux=pre, colsum=True)
+        return g, G.colsum_finish(part, b1.dtype)
+    ga = G.mm_nt(gy, w2)
+    return _hip.bias_gelu_bwd(ga, pre, b1, True)
+
+
+def pick_mode(x2d, w1, b1, w2):
+    M, H = x2d.shape
+    F = w1.shape[1]
+    key = (x2d.dtype, M, H, F)
+    mode = _modes.get(key)
+    if mode is not None:
+        return mode
+    if (os.environ.get("PHA_FUSED_MLP", "1") == "0" or not _own_ok(x2d, w1, w2)
+            or torch.cuda.is_current_stream_capturing()):
+        return 0
+    gy = torch.randn(M, H, device=x2d.device, dtype=x2d.dtype)
+    times = []
+    for m in (0, 1):
+        def chain():
+            _, pre = _fwd(m, x2d, w1, b1)
+            _bwd_gelu(m, gy, w2, pre, b1)
+        chain()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(3):
+            chain()
+        ev1.record()
+        ev1.synchronize()
+        times.append(ev0.elapsed_time(ev1))
+    mode = int(times[1] < times[0])
+    _modes[key] = mode
+    if os.environ.get("PHA_GEMM_PICK_LOG"):
+        import sys
+        print(f"[mlp-pick] {key}: chain {mode} (lib {times[0]:.3f} ms, own-fused {times[1]:.3f} ms for 3)",
+              file=sys.stderr, flush=True)
+    return mode
+
+
+class FusedMLP(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2d, w1, b1, w2, b2, mode):
+        from .conv_gemm import weight_t
+        a, pre = _fwd(mode, x2d, w1, b1)
+        y = G.mm_nt_bias(a, weight_t(w2), b2)
+        ctx.save_for_backward(x2d, w1, b1, w2, pre, a)
+        ctx.mode = mode
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .conv_gemm import weight_grad
+        x2d, w1, b1, w2, pre, a = ctx.saved_tensors
+        gy = gy.contiguous()
+        dw2 = weight_grad(a, gy)
+        db2 = _hip.col_sum(gy)
+        g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1)
+        dx = G.mm_nt(g, w1) if ctx.needs_input_grad[0] else None
+        dw1 = weight_grad(x2d, g)
+        return dx, dw1, db1, dw2, db2, None
+
+
+def fused_mlp(x, w1, b1, w2, b2):
+    """gelu_tanh(x @ w1 + b1) @ w2 + b2 for x [..., H], w1 [H, F], w2 [F, H] (Paddle [in, out])"""
+    x2d = x.reshape(-1, x.shape[-1])
+    if not x2d.is_contiguous():
+        x2d = x2d.contiguous()
+    mode = pick_mode(x2d, w1, b1, w2)
+    y = FusedMLP.apply(x2d, w1, b1, w2, b2, mode)
+    return y.reshape(list(x.shape[:-1]) + [w2.shape[1]])
+
+
+def available(x, w1, b1, w2, b2):
+    from . import fused
+    return fused._use_hip(x) and _eligible(x.reshape(-1, x.shape[-1]), w1, b1, w2, b2) \
+        and os.environ.get("PHA_LINEAR_NT", "1") != "0"

@@ -37,10 +37,16 @@ def check():
     for (M, N, K) in [(256, 256, 64), (264, 520, 128), (1024, 2048, 512), (4096, 1536, 2048)]:
         x, w = r(M, K), r(K, N)
         ref = x.float() @ w.float()
-        c = G.nn(x, w)
-        err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
-        print(f"check nn M={M} N={N} K={K} rel_err={err:.2e}", flush=True)
-        assert c.shape == (M, N) and err < 1e-2, err
+        for P in (False, True):
+            c = G.nn(x, w, persistent=P)
+            err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
+            print(f"check nn M={M} N={N} K={K} persistent={P} rel_err={err:.2e}", flush=True)
+            assert c.shape == (M, N) and err < 1e-2, err
+            bt = w.t().contiguous()
+            c = G.gemm(x, bt, False, False, persistent=P)
+            err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
+            print(f"check NT M={M} N={N} K={K} persistent={P} rel_err={err:.2e}", flush=True)
+            assert err < 1e-2, err
     M, N, K = 520, 768, 256
     x, w = r(M, K), r(K, N)
     bias = torch.randn(N, device="cuda")
@@ -74,9 +80,11 @@ def bench():
         fl = 2.0 * T * K * N
         rows = [
             ("fwd", [("lib NN", lambda: x @ w), ("lib NT(Wt)", lambda: x @ wt.t())],
-             [("own nn", lambda: G.nn(x, w))]),
+             [("own nn", lambda: G.nn(x, w, persistent=False)), ("own nn-P", lambda: G.nn(x, w, persistent=True))]),
             ("dX ", [("lib NT", lambda: dy @ w.t())],
-             [("own NT", lambda: G.gemm(dy, w, False, False)), ("own nn(Wt)", lambda: G.nn(dy, wt))]),
+             [("own NT", lambda: G.gemm(dy, w, False, False, persistent=False)),
+              ("own NT-P", lambda: G.gemm(dy, w, False, False, persistent=True)),
+              ("own nn-P(Wt)", lambda: G.nn(dy, wt, persistent=True))]),
             ("dW ", [("lib TN", lambda: x.t() @ dy)], [("own TN", lambda: G.gemm(x, dy, True, True))]),
         ]
         for lab, libs, owns in rows:
@@ -91,26 +99,29 @@ def bench():
     h, dl = r(T, 2048), r(T, 50304)
     fl = 2.0 * T * 2048 * 50304
     for lab, f_lib, f_own in [("logits h@E^T", lambda: h @ E.t(), lambda: G.gemm(h, E, False, False)),
+                              ("logits np   ", lambda: h @ E.t(), lambda: G.gemm(h, E, False, False, persistent=False)),
                               ("dh dL@E     ", lambda: dl @ E, lambda: G.nn(dl, E)),
                               ("dE dL^T@h   ", lambda: dl.t() @ h, lambda: G.gemm(dl, h, True, True))]:
         tl, to = timeit(f_lib, 5), timeit(f_own, 5)
-        tot["lib"] += tl
-        tot["own"] += to
+        if not lab.startswith("logits np"):
+            tot["lib"] += tl
+            tot["own"] += to
         print(f"head {lab}: lib {fl / tl / 1e12:6.0f} TF  own {fl / to / 1e12:6.0f} TF   own/lib {tl / to:5.3f}",
               flush=True)
     print("per-step GEMM ms (mb16, best of each side): " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()))
 
 
 def sweep():
-    """SCHED variants of the transposed-store layout at the fc1 / out shapes"""
+    """SCHED variants of the persistent NT and transposed-store layouts at the GPT shapes"""
     T = 32768
     for K, N in ((2048, 8192), (2048, 2048), (8192, 2048)):
-        x, w = r(T, K), r(K, N)
+        x, w, bt = r(T, K), r(K, N), r(N, K)
         fl = 2.0 * T * K * N
         out = []
-        for sc in ("0", "4"):
+        for sc in ("0", "2", "4"):
             os.environ["PHA_G4W_SCHED"] = sc
-            out.append(f"sched{sc} {fl / timeit(lambda: G.nn(x, w)) / 1e12:6.0f}")
+            out.append(f"nn-P sched{sc} {fl / timeit(lambda: G.nn(x, w)) / 1e12:6.0f}")
+            out.append(f"NT-P sched{sc} {fl / timeit(lambda: G.gemm(x, bt, False, False)) / 1e12:6.0f}")
         os.environ.pop("PHA_G4W_SCHED", None)
         print(f"nn sweep {T}x{N}x{K}: " + "  ".join(out) + " TF", flush=True)
 
