@@ -618,11 +618,20 @@ def median(x, axis=None, keepdim=False, name=None):
 
 @_export
 def nanmedian(x, axis=None, keepdim=True, name=None):
+    """median ignoring NaNs; an even count averages the two middle values (reference
+    python/paddle/tensor/stat.py nanmedian, phi nanmedian kernel), unlike torch.nanmedian's lower one"""
     t = _u(x)
     if axis is None:
-        out = torch.nanmedian(t)
-        return _w(out.reshape([1] * t.dim()) if keepdim else out)
-    return _w(torch.nanmedian(t, dim=axis, keepdim=keepdim).values)
+        out = torch.nanquantile(t.reshape(-1), 0.5, interpolation="midpoint")
+        return _w(out.reshape([1] * t.dim()) if keepdim else out.reshape([1]))
+    axes = [axis] if isinstance(axis, int) else list(axis)
+    axes = sorted(a % t.dim() for a in axes)
+    keep = [d for d in range(t.dim()) if d not in axes]
+    moved = t.permute(keep + axes).reshape([t.shape[d] for d in keep] + [-1])
+    out = torch.nanquantile(moved, 0.5, dim=-1, interpolation="midpoint")
+    if keepdim:
+        out = out.reshape([1 if d in axes else t.shape[d] for d in range(t.dim())])
+    return _w(out)
 
 
 @_export

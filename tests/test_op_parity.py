@@ -683,3 +683,122 @@ def test_margin_and_hinge_losses():
     reg = l2 * 0.25 * ((anchor ** 2).sum(1).mean() + (pos ** 2).sum(1).mean())
     np.testing.assert_allclose(F.npair_loss(P(anchor), P(pos), P(labels), l2_reg=l2).numpy().reshape(-1),
                                [ce + reg], rtol=1e-6)
+
+
+# ----------------------------------------------------------------------------- batch 3 (search / stat / shape ops)
+def test_logcumsumexp_and_cummax():
+    # test_logcumsumexp_op.py np_logcumsumexp; test_cummax_op.py cummax_dim
+    x = U(3, 5)
+    want = np.log(np.cumsum(np.exp(x), axis=1))
+    np.testing.assert_allclose(paddle.logcumsumexp(P(x), axis=1).numpy(), want, rtol=1e-6)
+    if hasattr(paddle, "cummax"):
+        v, i = paddle.cummax(P(x), axis=1)
+        np.testing.assert_allclose(v.numpy(), np.maximum.accumulate(x, axis=1))
+
+
+def test_bincount_histogram_searchsorted_bucketize():
+    ints = R.randint(0, 6, (20,)).astype("int64")
+    w = U(20)
+    np.testing.assert_array_equal(paddle.bincount(P(ints)).numpy(), np.bincount(ints))       # test_bincount_op.py
+    np.testing.assert_allclose(paddle.bincount(P(ints), weights=P(w)).numpy(), np.bincount(ints, weights=w))
+    xs = U(50, lo=0, hi=10)
+    # test_histogram_op.py: np.histogram(x, bins, range=(min, max)), int64 counts
+    np.testing.assert_array_equal(paddle.histogram(P(xs), bins=5, min=0, max=10).numpy(),
+                                  np.histogram(xs, 5, range=(0, 10))[0])
+    seq = np.sort(U(10))
+    vals = U(6)
+    for right in (False, True):   # test_searchsorted_op.py
+        np.testing.assert_array_equal(paddle.searchsorted(P(seq), P(vals), right=right).numpy(),
+                                      np.searchsorted(seq, vals, side="right" if right else "left"))
+        np.testing.assert_array_equal(paddle.bucketize(P(vals), P(seq), right=right).numpy(),
+                                      np.searchsorted(seq, vals, side="right" if right else "left"))
+
+
+def test_trace_kron_cross_dist():
+    a = U(4, 5)
+    for off in (-1, 0, 2):   # test_trace_op.py
+        np.testing.assert_allclose(paddle.trace(P(a), offset=off).numpy().reshape(-1), [np.trace(a, offset=off)])
+    b = U(2, 3)
+    np.testing.assert_allclose(paddle.kron(P(a), P(b)).numpy(), np.kron(a, b))              # test_kron_op.py
+    u, v = U(4, 3), U(4, 3)
+    np.testing.assert_allclose(paddle.cross(P(u), P(v), axis=1).numpy(), np.cross(u, v, axis=1))
+    for p in (1.0, 2.0, float("inf"), 0.0):   # test_dist_op.py: norm of the difference
+        want = (np.count_nonzero(u - v) if p == 0 else np.max(np.abs(u - v)) if p == float("inf")
+                else (np.abs(u - v) ** p).sum() ** (1 / p))
+        np.testing.assert_allclose(paddle.dist(P(u), P(v), p).numpy().reshape(-1), [want], rtol=1e-6)
+
+
+def test_take_put_along_axis_index_sample_masked_select():
+    x = U(3, 4)
+    idx = R.randint(0, 4, (3, 2)).astype("int64")
+    np.testing.assert_allclose(paddle.take_along_axis(P(x), P(idx), 1).numpy(), np.take_along_axis(x, idx, 1))
+    vals = U(3, 2)
+    want = x.copy()
+    np.put_along_axis(want, idx, vals, 1)                                      # test_put_along_axis_op.py
+    got = paddle.put_along_axis(P(x), P(idx), P(vals), 1).numpy()
+    # duplicate indices in a row: the reference kernel's last write wins, like numpy's
+    np.testing.assert_allclose(got, want)
+    # index_sample (test_index_sample_op.py): out[i][j] = x[i][index[i][j]]
+    np.testing.assert_allclose(paddle.index_sample(P(x), P(idx)).numpy(), np.take_along_axis(x, idx, 1))
+    m = x > 0
+    np.testing.assert_allclose(paddle.masked_select(P(x), P(m)).numpy(), x[m])
+
+
+def test_unique_family_roll_flip_tri():
+    a = R.randint(0, 5, (12,)).astype("int64")
+    out, idx, inv, cnt = paddle.unique(P(a), return_index=True, return_inverse=True, return_counts=True)
+    wo, wi, winv, wc = np.unique(a, return_index=True, return_inverse=True, return_counts=True)   # test_unique.py
+    for g, w in ((out, wo), (idx, wi), (inv, winv), (cnt, wc)):
+        np.testing.assert_array_equal(g.numpy(), w)
+    b = np.array([1, 1, 2, 2, 2, 3, 1, 1], dtype="int64")
+    uc, ucnt = paddle.unique_consecutive(P(b), return_counts=True)
+    np.testing.assert_array_equal(uc.numpy(), [1, 2, 3, 1])                     # test_unique_consecutive_op.py
+    np.testing.assert_array_equal(ucnt.numpy(), [2, 3, 1, 2])
+    x = U(3, 4)
+    np.testing.assert_allclose(paddle.roll(P(x), 1, axis=1).numpy(), np.roll(x, 1, axis=1))
+    np.testing.assert_allclose(paddle.roll(P(x), 5).numpy(), np.roll(x, 5))    # flattened roll
+    np.testing.assert_allclose(paddle.flip(P(x), [0, 1]).numpy(), np.flip(x, (0, 1)))
+    for d in (-1, 0, 1):
+        np.testing.assert_allclose(paddle.tril(P(x), d).numpy(), np.tril(x, d))
+        np.testing.assert_allclose(paddle.triu(P(x), d).numpy(), np.triu(x, d))
+
+
+def test_creation_ranges():
+    np.testing.assert_allclose(paddle.linspace(0, 1, 7).numpy(), np.linspace(0, 1, 7).astype("float32"), rtol=1e-6)
+    np.testing.assert_allclose(paddle.logspace(0, 2, 5, base=10.0).numpy(),
+                               np.logspace(0, 2, 5).astype("float32"), rtol=1e-5)
+    np.testing.assert_array_equal(paddle.arange(2, 11, 3).numpy(), np.arange(2, 11, 3))
+    e = paddle.eye(3, 4).numpy()
+    np.testing.assert_array_equal(e, np.eye(3, 4))
+    g1, g2 = paddle.meshgrid(P(np.arange(3.0)), P(np.arange(4.0)))
+    w1, w2 = np.meshgrid(np.arange(3.0), np.arange(4.0), indexing="ij")          # paddle meshgrid is 'ij'
+    np.testing.assert_array_equal(g1.numpy(), w1)
+    np.testing.assert_array_equal(g2.numpy(), w2)
+    v = U(3)
+    np.testing.assert_allclose(paddle.diag_embed(P(v)).numpy(), np.diag(v))
+    np.testing.assert_array_equal(paddle.nonzero(P(np.array([[0, 1], [2, 0]]))).numpy(), [[0, 1], [1, 0]])
+
+
+def test_stat_cov_corrcoef_mode_nanmedian():
+    x = U(3, 6)
+    if hasattr(paddle.linalg, "cov"):
+        np.testing.assert_allclose(paddle.linalg.cov(P(x)).numpy(), np.cov(x), rtol=1e-6)
+    if hasattr(paddle.linalg, "corrcoef"):
+        np.testing.assert_allclose(paddle.linalg.corrcoef(P(x)).numpy(), np.corrcoef(x), rtol=1e-6)
+    y = x.copy()
+    y[0, 1] = np.nan
+    if hasattr(paddle, "nanmedian"):
+        # test_nanmedian.py: np.nanmedian (even counts average the two middle values)
+        np.testing.assert_allclose(paddle.nanmedian(P(y), axis=1, keepdim=False).numpy(), np.nanmedian(y, axis=1))
+        np.testing.assert_allclose(paddle.nanmedian(P(y), axis=[0, 1]).numpy().reshape(-1), [np.nanmedian(y)])
+        np.testing.assert_allclose(paddle.nanmedian(P(y)).numpy().reshape(-1), [np.nanmedian(y)])
+    np.testing.assert_allclose(paddle.nansum(P(y), axis=1).numpy(), np.nansum(y, axis=1))
+
+
+def test_clip_increment_scale_stanh():
+    x = U(4, 5, lo=-3, hi=3)
+    np.testing.assert_allclose(paddle.clip(P(x), -1.5, 0.7).numpy(), np.clip(x, -1.5, 0.7))
+    np.testing.assert_allclose(paddle.increment(P(np.array([3.0])), 2.5).numpy(), [5.5])
+    # scale_op: bias_after_scale True: x * s + b, False: (x + b) * s (test_scale_op.py)
+    np.testing.assert_allclose(paddle.scale(P(x), 2.0, 0.5, bias_after_scale=True).numpy(), x * 2 + 0.5)
+    np.testing.assert_allclose(paddle.scale(P(x), 2.0, 0.5, bias_after_scale=False).numpy(), (x + 0.5) * 2)
