@@ -15,7 +15,7 @@ from ..framework.io import save as _save_obj, load as _load_obj
 from .program import (Variable, Program, Block, OpDesc, default_main_program, default_startup_program,  # noqa: F401
                       program_guard, data, Executor, global_scope, scope_guard, append_backward, gradients,
                       enable_static, disable_static, name_scope, CompiledProgram, BuildStrategy, ExecutionStrategy,
-                      InputSpec, Scope, run_program)
+                      InputSpec, Scope, run_program, plan_program_memory)
 from . import nn  # noqa: F401
 
 __all__ = ["BuildStrategy", "CompiledProgram", "ExecutionStrategy", "Executor", "ExponentialMovingAverage", "InputSpec",

@@ -22,6 +22,7 @@ import copy
 import inspect
 import itertools
 import json
+import os
 
 import numpy as np
 import torch
@@ -575,8 +576,88 @@ def _bind_outputs(outs, vals, env):
             _bind_outputs(o, v, env)
 
 
+_SUB_BLOCK_ATTRS = ("true_block", "false_block", "cond_block", "body_block", "sub_block")
+
+
+def _op_uses(program, op):
+    """ids of the Variables ``op`` may read: its inputs, and for a control-flow op every Variable
+    named in its attributes or read by any op of its sub-blocks (conservative)"""
+    ids = {id(v) for v in _iter_vars((op.args, op.kwargs))}
+    if op.exec is not None:
+        ids |= {id(v) for v in _iter_vars(list(op.attrs.values()))}
+        for k in _SUB_BLOCK_ATTRS:
+            b = op.attrs.get(k)
+            if isinstance(b, int) and 0 <= b < len(program.blocks):
+                for sop in program.blocks[b].ops:
+                    ids |= _op_uses(program, sop)
+    return ids
+
+
+def _lifetimes(program, blk, keep_ids):
+    """(first definition op, last use op) of every Variable of ``blk``'s top-level ops; Variables
+    in ``keep_ids`` (fetch targets) never end"""
+    first, last = {}, {}
+    for i, op in enumerate(blk.ops):
+        for vid in _op_uses(program, op):
+            last[vid] = i
+            first.setdefault(vid, -1)      # defined before the block (feed) unless seen below
+        for v in _iter_vars(op.outputs):
+            first.setdefault(id(v), i)
+            last.setdefault(id(v), i)
+    for vid in keep_ids:
+        if vid in last:
+            last[vid] = len(blk.ops)
+    return first, last
+
+
+def _gc_plan(program, blk, fetch_ids):
+    """eager deletion (reference framework/ir/memory_optimize_pass/eager_deletion_pass, the
+    InterpreterCore garbage collector): op index -> Variable ids whose last reader it is. Cached per
+    (op count, fetch set)."""
+    key = (len(blk.ops), tuple(sorted(fetch_ids)))
+    cache = program.__dict__.setdefault("_gc_cache", {})
+    plan = cache.get(key)
+    if plan is None:
+        _, last = _lifetimes(program, blk, fetch_ids)
+        plan = {}
+        for vid, i in last.items():
+            if i < len(blk.ops):
+                plan.setdefault(i, []).append(vid)
+        cache[key] = plan
+    return plan
+
+
+def plan_program_memory(program, fetch_list=(), alignment=256):
+    """Static memory plan of the global block from the Variables' inferred shapes and their
+    lifetimes, on the native best-fit planner (csrc/runtime/arena.cpp): returns
+    {"arena_bytes": planned peak with buffer reuse, "naive_bytes": every intermediate kept,
+    "offsets": {name: byte offset}} — what the eager deletion above frees in practice."""
+    from ..utils import native
+    blk = program.global_block()
+    fetch_ids = {id(blk.vars[f]) if isinstance(f, str) else id(f) for f in fetch_list}
+    first, last = _lifetimes(program, blk, fetch_ids)
+    by_id = {}
+    for op in blk.ops:
+        for v in _iter_vars((op.args, op.kwargs, op.outputs)):
+            by_id[id(v)] = v
+    names, sizes, f, e = [], [], [], []
+    for vid, v in by_id.items():
+        t = v._t
+        if t is None or not hasattr(t, "numel") or v.persistable:
+            continue
+        names.append(v.name)
+        sizes.append(max(1, int(t.numel()) * t.element_size()))
+        f.append(max(0, first.get(vid, 0)))
+        e.append(max(f[-1], last.get(vid, f[-1])))
+    if not names:
+        return {"arena_bytes": 0, "naive_bytes": 0, "offsets": {}}
+    offs, total = native.plan_memory(sizes, f, e, alignment)
+    return {"arena_bytes": total, "naive_bytes": int(sum(sizes)), "offsets": dict(zip(names, offs))}
+
+
 def run_program(program, feed, fetch_list):
-    """Interpret ``program`` with ``feed``; returns fetched Tensors (real)."""
+    """Interpret ``program`` with ``feed``; returns fetched Tensors (real). Intermediate values are
+    dropped right after their last reader (eager deletion)."""
     blk = program.global_block()
     env = {}
     for name, val in (feed or {}).items():
@@ -592,10 +673,17 @@ def run_program(program, feed, fetch_list):
         if v.need_grad and t.is_floating_point():
             t = t.detach().requires_grad_(True)
         env[id(v)] = _wrap(t)
+    fetch_ids = set()
+    for f in fetch_list or []:
+        if isinstance(f, str) and f in blk.vars:
+            fetch_ids.add(id(blk.vars[f]))
+        elif isinstance(f, Variable):
+            fetch_ids.add(id(f))
+    free = _gc_plan(program, blk, fetch_ids) if os.environ.get("PHA_EAGER_DELETE", "1") != "0" else None
     prev_static = _core._mode.static
     _core._mode.record_depth += 1
     try:
-        run_block(program, blk, env)
+        run_block(program, blk, env, free)
     finally:
         _core._mode.record_depth -= 1
         _core._mode.static = prev_static
@@ -612,14 +700,20 @@ def run_program(program, feed, fetch_list):
     return res
 
 
-def run_block(program, blk, env):
-    """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor)"""
-    for op in blk.ops:
+def run_block(program, blk, env, free=None):
+    """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor);
+    ``free``: op index -> Variable ids to drop after that op (eager deletion)"""
+    for i, op in enumerate(blk.ops):
         if op.exec is not None:
             op.exec(program, env, op)
-            continue
-        out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
-        _bind_outputs(op.outputs, out, env)
+        else:
+            out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
+            _bind_outputs(op.outputs, out, env)
+        if free:
+            for vid in free.get(i, ()):
+                env.pop(vid, None)
+    if free is not None:
+        program.__dict__["_last_env_size"] = len(env)
 
 
 def has_control_flow(program):

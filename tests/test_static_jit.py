@@ -98,3 +98,44 @@ def test_to_static_cache_per_signature():
     g(paddle.ones([2]))
     g(paddle.ones([3]))
     assert len(calls) == 2  # traced once per input signature
+
+
+def test_eager_deletion_and_memory_plan(static_mode, monkeypatch):
+    """intermediates are dropped after their last reader (the reference's eager-deletion GC), results
+    unchanged; the native lifetime planner packs the chain's buffers below the keep-everything size"""
+    main, startup = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, startup):
+        x = paddle.static.data("x", [64, 256], "float32")
+        h = x
+        for _ in range(8):
+            h = paddle.nn.functional.relu(h * 1.5 - 0.25)
+        out = paddle.mean(h, axis=1)
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    exe.run(startup)
+    X = np.random.RandomState(0).randn(64, 256).astype("float32")
+    (a,) = exe.run(main, feed={"x": X}, fetch_list=[out])
+    kept = main._last_env_size
+    monkeypatch.setenv("PHA_EAGER_DELETE", "0")
+    (b,) = exe.run(main, feed={"x": X}, fetch_list=[out])
+    np.testing.assert_array_equal(a, b)
+    n_ops = len(main.global_block().ops)
+    assert n_ops >= 24 and kept <= 2, (n_ops, kept)      # only the fetch target (and nothing else) survives
+    plan = paddle.static.plan_program_memory(main, [out])
+    assert 0 < plan["arena_bytes"] < plan["naive_bytes"] / 4, plan
+    # buffers whose lifetimes overlap never share bytes
+    offs = plan["offsets"]
+    assert len(set(offs.values())) < len(offs)
+
+
+def test_eager_deletion_keeps_control_flow_inputs(static_mode):
+    """a value read only inside a cond sub-block lives until the cond op has run"""
+    main, startup = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, startup):
+        x = paddle.static.data("x", [4], "float32")
+        y = x * 2.0
+        z = x + 1.0
+        r = paddle.static.nn.cond(paddle.sum(x) > 0, lambda: y * 3.0, lambda: z - 1.0)
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    for X in (np.ones(4, "float32"), -np.ones(4, "float32")):
+        (o,) = exe.run(main, feed={"x": X}, fetch_list=[r])
+        np.testing.assert_allclose(o, X * 6.0 if X.sum() > 0 else X)
