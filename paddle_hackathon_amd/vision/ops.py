@@ -213,6 +213,9 @@ def yolo_box(x, img_size, anchors, class_num, conf_thresh, downsample_ratio, cli
     t = _t(x).float()
     N, _, H, W = t.shape
     na = len(anchors) // 2
+    ioup = None
+    if iou_aware:   # the first na channels are the IoU predictions (reference yolo_box kernel)
+        ioup, t = t[:, :na], t[:, na:]
     t = t.reshape(N, na, 5 + class_num, H, W)
     img = _t(img_size).float()
     gy, gx = torch.meshgrid(torch.arange(H, device=t.device), torch.arange(W, device=t.device), indexing="ij")
@@ -229,6 +232,8 @@ def yolo_box(x, img_size, anchors, class_num, conf_thresh, downsample_ratio, cli
         x1, y1 = x1.clamp(min=0), y1.clamp(min=0)
         x2, y2 = torch.minimum(x2, imw - 1), torch.minimum(y2, imh - 1)
     conf = torch.sigmoid(t[:, :, 4])
+    if ioup is not None:
+        conf = conf ** (1.0 - iou_aware_factor) * torch.sigmoid(ioup) ** iou_aware_factor
     probs = torch.sigmoid(t[:, :, 5:]) * conf[:, :, None]
     keep = (conf >= conf_thresh).float()
     boxes = torch.stack([x1, y1, x2, y2], -1) * keep[..., None]
@@ -324,20 +329,26 @@ def box_coder(prior_box, prior_box_var, target_box, code_type="encode_center_siz
     pb, tb = _t(prior_box).float(), _t(target_box).float()
     pv = _t(prior_box_var).float() if isinstance(prior_box_var, (Tensor, torch.Tensor, np.ndarray)) else \
         torch.tensor(prior_box_var if prior_box_var is not None else [1.0, 1.0, 1.0, 1.0], device=pb.device)
+    """reference phi box_coder kernel (oracle: test_box_coder_op.py box_encoder / box_decoder):
+    prior centres include the +1 of unnormalized boxes, encoded target centres are plain
+    midpoints; ``axis`` says which dimension of a decode input the M priors run along"""
+    code_type = code_type.lower()
     off = 0.0 if box_normalized else 1.0
     pw = pb[:, 2] - pb[:, 0] + off
     ph = pb[:, 3] - pb[:, 1] + off
     pcx = pb[:, 0] + pw / 2
     pcy = pb[:, 1] + ph / 2
-    if code_type == "encode_center_size":
+    if code_type in ("encode_center_size", "encodecentersize"):
         tw = tb[:, 2] - tb[:, 0] + off
         th = tb[:, 3] - tb[:, 1] + off
-        tcx = tb[:, 0] + tw / 2
-        tcy = tb[:, 1] + th / 2
+        tcx = (tb[:, 0] + tb[:, 2]) / 2
+        tcy = (tb[:, 1] + tb[:, 3]) / 2
         out = torch.stack([(tcx[:, None] - pcx) / pw, (tcy[:, None] - pcy) / ph,
-                           torch.log(tw[:, None] / pw), torch.log(th[:, None] / ph)], -1)
-        return _wrap(out / pv.reshape(-1, 4) if pv.dim() > 1 else out / pv)
-    v = pv if pv.dim() > 1 else pv.view(1, 4)
+                           torch.log(torch.abs(tw[:, None] / pw)), torch.log(torch.abs(th[:, None] / ph))], -1)
+        return _wrap(out / pv.reshape(1, -1, 4) if pv.dim() > 1 else out / pv)
+    shp = (1, -1) if axis == 0 else (-1, 1)
+    pw, ph, pcx, pcy = pw.reshape(shp), ph.reshape(shp), pcx.reshape(shp), pcy.reshape(shp)
+    v = pv.reshape(shp + (4,)) if pv.dim() > 1 else pv.view(1, 1, 4)
     d = tb if tb.dim() == 3 else tb.unsqueeze(1)
     cx = v[..., 0] * d[..., 0] * pw + pcx
     cy = v[..., 1] * d[..., 1] * ph + pcy
@@ -368,8 +379,14 @@ def prior_box(input, image, min_sizes, max_sizes=None, aspect_ratios=[1.0], vari
                     bw, bh = ms * math.sqrt(a) / 2, ms / math.sqrt(a) / 2
                     cell.append([(cx - bw) / IW, (cy - bh) / IH, (cx + bw) / IW, (cy + bh) / IH])
                 if max_sizes:
+                    # reference prior_box kernel: [ar = 1, max, other ars] when
+                    # min_max_aspect_ratios_order, else [every ar, max]
                     s = math.sqrt(ms * max_sizes[k]) / 2
-                    cell.insert(1, [(cx - s) / IW, (cy - s) / IH, (cx + s) / IW, (cy + s) / IH])
+                    mx = [(cx - s) / IW, (cy - s) / IH, (cx + s) / IW, (cy + s) / IH]
+                    if min_max_aspect_ratios_order:
+                        cell.insert(1, mx)
+                    else:
+                        cell.append(mx)
                 boxes.extend(cell)
     b = torch.tensor(boxes, dtype=torch.float32, device=default_device()).reshape(H, W, -1, 4)
     if clip:
