@@ -46,9 +46,15 @@ enum : int {
   EPI_COLSUM = 16,  // colsum[tile_m][n] = sum of the tile's rows of the final fp32 C
   EPI_AUXOUT = 32,
   EPI_TRANS = 64,   // store C^T: the kernel computes the transposed product (see pha_gemm4w)
-  EPI_SKIP = 128,   // measurement only: no epilogue (tools/g4w_fixed.py)
-  EPI_PERSIST = 256,   // persistent grid (colsum partials per 128 output rows), see launch()
+  EPI_SKIP = 128,      // measurement only: no epilogue (tools/g4w_fixed.py)
+  EPI_NOSTORE = 512,   // measurement only: epilogue without its global stores
+  EPI_NOSTAGE = 1024,  // measurement only: epilogue without the LDS staging writes
 };
+
+// Epilogue builds (a kernel template parameter): the dGELU build loads the stored pre-activation,
+// the AUX build also stores the pre-activation; keeping them out of the plain build keeps its
+// epilogue free of register spills (every scratch reload is an exposed memory latency per tile)
+enum : int { EK_PLAIN = 0, EK_DGELU = 1, EK_AUX = 2, EK_GEN = 3 };   // PLAIN: convert + store only
 
 struct Args {
   const void* a;
@@ -66,11 +72,6 @@ constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
 constexpr int STAGE = 2 * OPB;      // A image, B image
 constexpr int CROWF = 256 * 4 + 16; // fp32 epilogue staging row (bytes)
 constexpr int SMEM = (128 * CROWF > 2 * STAGE) ? 128 * CROWF : 2 * STAGE;
-// persistent build: the operand stages plus one private epilogue staging block per wave
-// (16 rows x 64 fp32, row pitch 68 floats: conflict-free ds_write_b32 / ds_write_b128)
-constexpr int WP = 68;
-constexpr int WSTG = 16 * WP * 4;
-constexpr int SMEM_P = 2 * STAGE + 4 * WSTG;
 
 __device__ __forceinline__ unsigned lds_u32(const unsigned char* p) {
   return (unsigned)(size_t)(__attribute__((address_space(3))) const unsigned char*)p;
@@ -109,170 +110,59 @@ __device__ __forceinline__ float ld_elem(uint4 v, int e) {
   else return (float)__builtin_bit_cast(_Float16, u);
 }
 
-template <int N_, typename F, int I = 0>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N_) {
-    f(std::integral_constant<int, I>{});
-    static_for<N_, F, I + 1>(static_cast<F&&>(f));
-  }
-}
-
-// Epilogue of one wave's 128 x 128 accumulator block through its private 16 x 64 fp32 staging
-// block (no workgroup barrier: LDS operations of one wave complete in order): 16 rounds of
-// (write 16 rows x 64 columns, read back 8 consecutive columns of a row per lane, epilogue math,
-// 16-B global stores). With OT the block is C^T (accumulator rows are output columns). Column
-// sums go to partial row (output row / 128).
-template <typename T, bool OT>
-__device__ __forceinline__ void epilogue_wave(const Args& p, const f32x4 (&acc)[8][8], unsigned char* stgb,
-                                              int cm0, int cn0, int wr, int wc, int lane) {
-  float* wst = reinterpret_cast<float*>(stgb);
-  const int epi = p.epi;
-  const int Mo = OT ? p.N : p.M, No = OT ? p.M : p.N;
-  const int rb0 = OT ? cn0 + wc * 128 : cm0 + wr * 128;   // output rows / columns of this block
-  const int cb0 = OT ? cm0 + wr * 128 : cn0 + wc * 128;
-  const int fr = lane & 15, fk = lane >> 4, c8 = lane & 7;
-  T* C = static_cast<T*>(p.c);
-  T* AUX = static_cast<T*>(p.aux);
-  float bv[2][8], cs[2][8];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int n = cb0 + h * 64 + c8 * 8 + e;
-      bv[h][e] = ((epi & EPI_BIAS) && n < No) ? p.bias[n] : 0.f;
-      cs[h][e] = 0.f;
-    }
-  // 16 rounds as a compile-time loop: every accumulator index must be static (a runtime index
-  // sends the whole accumulator array to scratch)
-  static_for<16>([&](auto r_c) {
-      constexpr int u = decltype(r_c)::value >> 1, h = decltype(r_c)::value & 1;
-      if constexpr (OT) {
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2)
-          *reinterpret_cast<f32x4*>(wst + fr * WP + i2 * 16 + 4 * fk) = acc[h * 4 + i2][u];
-      } else {
-#pragma unroll
-        for (int j2 = 0; j2 < 4; ++j2)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) wst[(4 * fk + e) * WP + j2 * 16 + fr] = acc[u][h * 4 + j2][e];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int row = (lane >> 3) + 8 * q;
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(wst + row * WP + c8 * 8);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(wst + row * WP + c8 * 8 + 4);
-        const long m = rb0 + u * 16 + row;
-        const int n = cb0 + h * 64 + c8 * 8;
-        if (m >= Mo || n >= No) continue;
-        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        uint4 auxv;
-        if (epi & EPI_DGELU) auxv = *reinterpret_cast<const uint4*>(AUX + m * p.ldaux + n);
-        uint16_t pre[8], out[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = v[e] + bv[h][e];
-          if (epi & EPI_AUXOUT) pre[e] = Mf<T>::cvt(x);
-          if (epi & EPI_GELU) x = gelu_t(x);
-          else if (epi & EPI_RELU) x = fmaxf(x, 0.f);
-          if (epi & EPI_DGELU) x *= gelu_t_grad(ld_elem<T>(auxv, e));
-          cs[h][e] += x;
-          out[e] = Mf<T>::cvt(x);
-        }
-        *reinterpret_cast<uint4*>(C + m * p.ldc + n) = *reinterpret_cast<const uint4*>(out);
-        if (epi & EPI_AUXOUT) *reinterpret_cast<uint4*>(AUX + m * p.ldaux + n) = *reinterpret_cast<const uint4*>(pre);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  });
-  if (epi & EPI_COLSUM) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = cs[h][e];
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        cs[h][e] = v;
-      }
-    if (lane < 8) {
-      const long prow = rb0 >> 7;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int n = cb0 + h * 64 + lane * 8 + e;
-          if (n < No) p.colsum[prow * No + n] = cs[h][e];
-        }
-    }
-  }
-}
-
 // SCHED bit 0: compiler-scheduled (else fragment reads / LDS-DMA issues pinned between groups of
 // 4 MFMAs by sched_barrier); bit 1: reads spread one per MFMA group (else front-loaded); bit 2:
-// early staging (tile t+2 issued mid phase A behind a second barrier).
-// PERSIST: one workgroup per CU walks the tiles vb = blockIdx.x + k * gridDim.x. When a tile's
-// last MFMAs have read the operand stages, the NEXT tile's first two K-stages are DMA'd into them
-// and only then does this tile's epilogue run, through a wave-private staging block (no workgroup
-// barrier), so the next tile's load latency hides behind the epilogue instead of following it.
-template <typename T, bool AKO, bool BKO, int SCHED, bool OT = false, bool PERSIST = false>
+// early staging (tile t+2 issued mid phase A behind a second barrier)
+template <typename T, bool AKO, bool BKO, int SCHED, bool OT = false, int EK = EK_PLAIN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(Args p) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[PERSIST ? SMEM_P : SMEM];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
   const int M = p.M, N = p.N, K = p.K;
 
-  // XCD-bijective block order, GROUP_M-row panels (a grid that is a multiple of 8 keeps every
-  // virtual block of a persistent workgroup on its XCD's contiguous run of tiles)
+  // XCD-bijective block order, GROUP_M-row panels
   const int tiles_m = (M + 255) >> 8, tiles_n = (N + 255) >> 8;
   const int total = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int q8 = total >> 3, r8 = total & 7, xcd = bid & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   constexpr int GROUP_M = 8;
-  auto tile_of = [&](int vb, int& tm_, int& tn_) {
-    const int q8 = total >> 3, r8 = total & 7, xcd = vb & 7;
-    const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (vb >> 3);
-    const int group = lin / (GROUP_M * tiles_n);
-    const int first_m = group * GROUP_M;
-    const int gsize = min(tiles_m - first_m, GROUP_M);
-    tm_ = first_m + (lin % (GROUP_M * tiles_n)) % gsize;
-    tn_ = (lin % (GROUP_M * tiles_n)) / gsize;
-  };
-  int vb = blockIdx.x;
-  int tm, tn;
-  tile_of(vb, tm, tn);
-  int m0 = tm << 8, n0 = tn << 8;
+  const int group = lin / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (lin % (GROUP_M * tiles_n)) % gsize;
+  const int tn = (lin % (GROUP_M * tiles_n)) / gsize;
+  const int m0 = tm << 8, n0 = tn << 8;
 
   // ---- LDS-DMA sources: 8 instructions per operand per wave, g = wid * 8 + u fills LDS bytes
   // [g * 1024, g * 1024 + 1024) of the operand image
   unsigned aoff[8], boff[8];
-  const char* abase;
-  const char* bbase;
-  auto setup = [&](int m0_, int n0_) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int g = wid * 8 + u;
+  for (int u = 0; u < 8; ++u) {
+    const int g = wid * 8 + u;
 #pragma unroll
-      for (int op = 0; op < 2; ++op) {
-        const bool ko = op == 0 ? AKO : BKO;
-        const int dim = op == 0 ? M : N, base = op == 0 ? m0_ : n0_, ld = op == 0 ? p.lda : p.ldb;
-        unsigned off;
-        if (!ko) {
-          const int row = g * 8 + (lane >> 3);
-          const int grow = min(base + row, dim - 1) - base;
-          off = ((unsigned)grow * (unsigned)ld + (unsigned)(((lane & 7) ^ (row & 7)) * 8)) * 2u;
-        } else {
-          const int half = g >> 4, krow = (g & 15) * 4 + (lane >> 4);
-          const int src = (lane & 15) ^ tn_mask(krow, 256);
-          const int idx = min(half * 128 + src * 8, dim - base - 8);
-          off = ((unsigned)krow * (unsigned)ld + (unsigned)idx) * 2u;
-        }
-        if (op == 0) aoff[u] = off; else boff[u] = off;
+    for (int op = 0; op < 2; ++op) {
+      const bool ko = op == 0 ? AKO : BKO;
+      const int dim = op == 0 ? M : N, base = op == 0 ? m0 : n0, ld = op == 0 ? p.lda : p.ldb;
+      unsigned off;
+      if (!ko) {
+        const int row = g * 8 + (lane >> 3);
+        const int grow = min(base + row, dim - 1) - base;
+        off = ((unsigned)grow * (unsigned)ld + (unsigned)(((lane & 7) ^ (row & 7)) * 8)) * 2u;
+      } else {
+        const int half = g >> 4, krow = (g & 15) * 4 + (lane >> 4);
+        const int src = (lane & 15) ^ tn_mask(krow, 256);
+        const int idx = min(half * 128 + src * 8, dim - base - 8);
+        off = ((unsigned)krow * (unsigned)ld + (unsigned)idx) * 2u;
       }
+      if (op == 0) aoff[u] = off; else boff[u] = off;
     }
-    abase = static_cast<const char*>(p.a) + (AKO ? (size_t)m0_ * 2 : (size_t)m0_ * p.lda * 2);
-    bbase = static_cast<const char*>(p.b) + (BKO ? (size_t)n0_ * 2 : (size_t)n0_ * p.ldb * 2);
-  };
-  setup(m0, n0);
+  }
+  const char* abase = static_cast<const char*>(p.a) +
+                      (AKO ? (size_t)m0 * 2 : (size_t)m0 * p.lda * 2);
+  const char* bbase = static_cast<const char*>(p.b) +
+                      (BKO ? (size_t)n0 * 2 : (size_t)n0 * p.ldb * 2);
   const size_t astep = AKO ? (size_t)64 * p.lda * 2 : 128, bstep = BKO ? (size_t)64 * p.ldb * 2 : 128;
   const unsigned lds0 = lds_u32(smem);
   const int nk = K >> 6;
@@ -311,6 +201,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
 
   f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
   uint4 fa0[8], fb0[8], fa1[8], fb1[8];
 
   // MFMA groups [g0, g1) of a phase (16 groups of 4 MFMAs = 64 MFMAs on (ca, cb)). With RD the 16
@@ -347,7 +242,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int idx = s * 4 + q, i = idx >> 3, j = idx & 7;
-        acc[i][j] = Mf<T>::mma(ca[i], cb[j], acc[i][j]);
+        // operand order picks the accumulator layout: (A, B) leaves a lane 4 consecutive C ROWS of
+        // one column, (B, A) 4 consecutive C COLUMNS of one row; the epilogue wants the latter
+        // along the output's rows (C^T rows with OT), so it can stage with 16-B LDS writes
+        if constexpr (OT) acc[i][j] = Mf<T>::mma(ca[i], cb[j], acc[i][j]);
+        else acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
       }
       if constexpr (!(SCHED & 1)) __builtin_amdgcn_sched_barrier(0);
     }
@@ -371,19 +270,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // prologue: the first tile's stages 0 and 1 (a persistent workgroup issues the next tile's
-  // before each epilogue)
+  // prologue
   stage_all(0);
-  if (nk > 1) stage_all(1);
-  bool first = true;
-  for (;;) {
-  if (first && nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nk > 1) {
+    stage_all(1);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   bar();
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     fa0[i] = readA(0, 0, i);
@@ -429,26 +324,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __builtin_amdgcn_sched_barrier(0);
   bar();
 
-  if constexpr (PERSIST) {
-    // every wave is past its last operand read: stage the next tile, then this tile's epilogue
-    const int cm0 = m0, cn0 = n0;
-    const int vb2 = vb + (int)gridDim.x;
-    const bool more = vb2 < total;
-    if (more) {
-      tile_of(vb2, tm, tn);
-      m0 = tm << 8;
-      n0 = tn << 8;
-      setup(m0, n0);
-      stage_all(0);
-      if (nk > 1) stage_all(1);
-    }
-    epilogue_wave<T, OT>(p, acc, smem + 2 * STAGE + wid * WSTG, cm0, cn0, wr, wc, lane);
-    if (!more) break;
-    vb = vb2;
-    first = false;
-    continue;
-  }
-
   // ---- epilogue ---------------------------------------------------------------------------------
   // OT: the tile is C^T (kernel rows = output columns). Output rows [r0, r0 + 256) of the Mo x No
   // result, columns [c0, c0 + 256); the accumulators are staged through LDS in two 128-row halves
@@ -463,15 +338,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int c8 = tid & 31, rl = tid >> 5;   // this thread: columns c0 + c8*8 .. +7, rows rl + 8 r
   const int n = c0 + c8 * 8;
   const bool ncol = n < No;
+  constexpr bool GEN = EK != EK_PLAIN;   // bias / activation / column sums (runtime flags)
   float bv[8], cs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    bv[e] = ((epi & EPI_BIAS) && ncol) ? p.bias[n + e] : 0.f;
+    bv[e] = (GEN && (epi & EPI_BIAS) && ncol) ? p.bias[n + e] : 0.f;
     cs[e] = 0.f;
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if constexpr (OT) {
+    if (epi & EPI_NOSTAGE) {
+    } else if constexpr (OT) {   // acc[i][j][e] = C^T[wc*128 + j*16 + fr][wr*128 + i*16 + 4fk + e]
       if (wc == h) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -479,47 +356,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int j = 0; j < 8; ++j)
             *reinterpret_cast<f32x4*>(smem + (j * 16 + fr) * CROWF + (wr * 128 + i * 16 + 4 * fk) * 4) = acc[i][j];
       }
-    } else {
+    } else {   // acc[i][j][e] = C[wr*128 + i*16 + fr][wc*128 + j*16 + 4fk + e] (operands swapped)
       if (wr == h) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int ml = i * 16 + 4 * fk + e, nl = wc * 128 + j * 16 + fr;
-              *reinterpret_cast<float*>(smem + ml * CROWF + nl * 4) = acc[i][j][e];
-            }
+            *reinterpret_cast<f32x4*>(smem + (i * 16 + fr) * CROWF + (wc * 128 + j * 16 + 4 * fk) * 4) = acc[i][j];
       }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int r = 0; r < 16; ++r) {
-      const int ml = rl + 8 * r;
-      const long m = r0 + h * 128 + ml;
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32 + 16);
-      if (m >= Mo || !ncol) continue;
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      uint4 auxv;
-      if (epi & EPI_DGELU) auxv = *reinterpret_cast<const uint4*>(AUX + m * p.ldaux + n);
-      uint16_t pre[8], out[8];
+    // rows in batches of RB: all RB results are computed into distinct registers before their
+    // stores issue. A register that still holds an in-flight store's data can only be rewritten
+    // after vmcnt(0), i.e. after that store COMPLETED, and a load among the rows (the dGELU aux
+    // read) waits vmcnt(0) too: row-by-row code paid a full memory round trip per row. The dGELU
+    // build loads a batch's aux rows before computing it; the others load nothing.
+    constexpr bool DG = EK == EK_DGELU, AX = EK == EK_AUX;
+    constexpr int RB = (DG || AX) ? (OT ? 2 : 4) : 8;   // the aux builds hold twice the registers per row
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = v[e] + bv[e];
-        if (epi & EPI_AUXOUT) pre[e] = Mf<T>::cvt(x);
-        if (epi & EPI_GELU) x = gelu_t(x);
-        else if (epi & EPI_RELU) x = fmaxf(x, 0.f);
-        if (epi & EPI_DGELU) x *= gelu_t_grad(ld_elem<T>(auxv, e));
-        cs[e] += x;
-        out[e] = Mf<T>::cvt(x);
+    for (int rb = 0; rb < 16; rb += RB) {
+      uint4 ov[RB], pv[AX ? RB : 1], auxv[DG ? RB : 1];
+      if constexpr (DG) {
+#pragma unroll
+        for (int r8 = 0; r8 < RB; ++r8) {
+          const long m = r0 + h * 128 + rl + 8 * (rb + r8);
+          auxv[r8] = (m < Mo && ncol) ? *reinterpret_cast<const uint4*>(AUX + m * p.ldaux + n) : uint4{0, 0, 0, 0};
+        }
       }
-      *reinterpret_cast<uint4*>(C + m * p.ldc + n) = *reinterpret_cast<const uint4*>(out);
-      if (epi & EPI_AUXOUT) *reinterpret_cast<uint4*>(AUX + m * p.ldaux + n) = *reinterpret_cast<const uint4*>(pre);
+#pragma unroll
+      for (int r8 = 0; r8 < RB; ++r8) {
+        const int ml = rl + 8 * (rb + r8);
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(smem + ml * CROWF + c8 * 32 + 16);
+        const bool ok = r0 + h * 128 + ml < Mo && ncol;
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        uint16_t pre[8], out[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = v[e];
+          if constexpr (GEN) {
+            x += bv[e];
+            if constexpr (AX) pre[e] = Mf<T>::cvt(x);
+            if (epi & EPI_GELU) x = gelu_t(x);
+            else if (epi & EPI_RELU) x = fmaxf(x, 0.f);
+            if constexpr (DG) x *= gelu_t_grad(ld_elem<T>(auxv[r8], e));
+            if (ok) cs[e] += x;
+          }
+          out[e] = Mf<T>::cvt(x);
+        }
+        ov[r8] = *reinterpret_cast<const uint4*>(out);
+        if constexpr (AX) pv[r8] = *reinterpret_cast<const uint4*>(pre);
+      }
+#pragma unroll
+      for (int r8 = 0; r8 < RB; ++r8) {
+        const long m = r0 + h * 128 + rl + 8 * (rb + r8);
+        if (m >= Mo || !ncol || (epi & EPI_NOSTORE)) continue;
+        *reinterpret_cast<uint4*>(C + m * p.ldc + n) = ov[r8];
+        if constexpr (AX) *reinterpret_cast<uint4*>(AUX + m * p.ldaux + n) = pv[r8];
+      }
     }
     __syncthreads();
   }
-  if (epi & EPI_COLSUM) {
+  if (GEN && (epi & EPI_COLSUM)) {
     // reduce the 8 row-lanes (rl) of every column group through LDS, one fp32 row per tile
 #pragma unroll
     for (int e = 0; e < 8; ++e) stg[rl * 264 + c8 * 8 + e] = cs[e];
@@ -530,56 +428,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int r = 0; r < 8; ++r) s += stg[r * 264 + col];
     if (c0 + col < No) p.colsum[(long)rt * No + c0 + col] = s;
   }
-  break;
-  }   // tile loop
 }
 
-inline int num_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
-
-template <typename T, int SCHED, bool P>
-int launch_p(const Args& a, int ako, int bko, unsigned grid, hipStream_t st) {
-  if constexpr (P) {   // persistent builds: the NT layout and the transposed-store NN layout
-    if (a.epi & EPI_TRANS) {
-      if (!(ako && !bko)) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED, true, true>), dim3(grid), dim3(256), 0, st, a);
-    } else if (!ako && !bko) {
-      hipLaunchKernelGGL((gemm4w_kernel<T, false, false, SCHED, false, true>), dim3(grid), dim3(256), 0, st, a);
-    } else {
-      return (int)hipErrorInvalidValue;
-    }
-    return (int)hipGetLastError();
-  } else {
-    if (a.epi & EPI_TRANS) {   // only the layout whose main loop keeps every accumulator in AGPRs
-      if (!(ako && !bko)) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED, true, false>), dim3(grid), dim3(256), 0, st, a);
-      return (int)hipGetLastError();
-    }
-    if (!ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, false, SCHED>), dim3(grid), dim3(256), 0, st, a);
-    else if (!ako && bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, true, SCHED>), dim3(grid), dim3(256), 0, st, a);
-    else if (ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((gemm4w_kernel<T, true, true, SCHED>), dim3(grid), dim3(256), 0, st, a);
+template <typename T, int SCHED, int EK>
+int launch_ek(const Args& a, int ako, int bko, hipStream_t st) {
+  const unsigned grid = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  if (a.epi & EPI_TRANS) {   // only the layout whose main loop keeps every accumulator in AGPRs
+    if (!(ako && !bko)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED, true, EK>), dim3(grid), dim3(256), 0, st, a);
     return (int)hipGetLastError();
   }
+  if constexpr (EK == EK_PLAIN || EK == EK_GEN) {
+    if (!ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, false, SCHED, false, EK>), dim3(grid), dim3(256), 0, st, a);
+    else if (!ako && bko) hipLaunchKernelGGL((gemm4w_kernel<T, false, true, SCHED, false, EK>), dim3(grid), dim3(256), 0, st, a);
+    else if (ako && !bko) hipLaunchKernelGGL((gemm4w_kernel<T, true, false, SCHED, false, EK>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm4w_kernel<T, true, true, SCHED, false, EK>), dim3(grid), dim3(256), 0, st, a);
+  } else {   // the dGELU / pre-activation builds: NT (fc2 dgrad) and the transposed store (fc1 fwd)
+    if (ako || bko) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm4w_kernel<T, false, false, SCHED, false, EK>), dim3(grid), dim3(256), 0, st, a);
+  }
+  return (int)hipGetLastError();
 }
 
 template <typename T, int SCHED>
 int launch(const Args& a, int ako, int bko, hipStream_t st) {
-  const unsigned tiles = (unsigned)(((a.M + 255) / 256) * ((a.N + 255) / 256));
-  if (a.epi & EPI_PERSIST) {   // one workgroup per CU (a multiple of 8: XCD-stable tile runs)
-    const unsigned cus = (unsigned)(num_cus() & ~7);
-    return launch_p<T, SCHED, true>(a, ako, bko, tiles < cus || cus == 0 ? tiles : cus, st);
-  }
-  return launch_p<T, SCHED, false>(a, ako, bko, tiles, st);
+  const bool dg = a.epi & EPI_DGELU, ax = a.epi & EPI_AUXOUT;
+  if (dg && ax) return (int)hipErrorInvalidValue;
+  if (dg) return launch_ek<T, SCHED, EK_DGELU>(a, ako, bko, st);
+  if (ax) return launch_ek<T, SCHED, EK_AUX>(a, ako, bko, st);
+  if (a.epi & (EPI_BIAS | EPI_GELU | EPI_RELU | EPI_COLSUM)) return launch_ek<T, SCHED, EK_GEN>(a, ako, bko, st);
+  return launch_ek<T, SCHED, EK_PLAIN>(a, ako, bko, st);
 }
 
 // colsum partials [rows][N] fp32 -> out[N] (T), one thread per column
@@ -602,8 +480,8 @@ using namespace pha;
 // (else B^T stored [N][ldb]). Requires K % 64 == 0; M, N, lda, ldb, ldc, ldaux % 8 == 0; K-outer
 // operand dims >= 8; every byte offset inside one 256-row / 64-k operand panel < 2^32.
 // epi: see g4w::EPI_*; bias fp32 [N]; aux [M][ldaux] (pre-activation in or out);
-// colsum fp32 [ceil(M/256)][N] partials (finish with pha_colsum_finish); with EPI_PERSIST (one
-// workgroup per CU walking the tiles) [ceil(M/128)][N].
+// colsum fp32 [ceil(M/256)][N] partials (finish with pha_colsum_finish).
+// EPI_DGELU / EPI_AUXOUT (mutually exclusive): NT layout or EPI_TRANS only.
 // EPI_TRANS (a_kouter = 1, b_kouter = 0 only): C (and aux) hold the TRANSPOSED product, [N][ldc];
 // bias is indexed by C's column (the kernel's m), colsum is [ceil(N/256)][M]. The NN product
 // x[M][K] . W[K][N] runs as this with A = W (K-outer) and B^T = x: the direct NN instantiation
@@ -626,7 +504,6 @@ PHA_API int pha_gemm4w(int dt, const void* a, const void* b, void* c, long M, lo
   if (dt == kBF16) {
     switch (sched) {
       case 2: return g4w::launch<bf16_t, 2>(p, a_kouter, b_kouter, stream);
-      case 4: return g4w::launch<bf16_t, 4>(p, a_kouter, b_kouter, stream);
       default: return g4w::launch<bf16_t, 0>(p, a_kouter, b_kouter, stream);
     }
   }

@@ -24,7 +24,6 @@ import torch
 from . import _lib
 
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT, EPI_TRANS = 1, 2, 4, 8, 16, 32, 64
-EPI_PERSIST = 256
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
@@ -75,16 +74,8 @@ def supported(M, N, K, *tensors):
     return _lib.native_available()
 
 
-def persistent_default(a_kouter, b_kouter):
-    """persistent grid (one workgroup per CU walking the tiles, next tile's loads overlapped with
-    this tile's epilogue) for the layouts that have a persistent build: NT and the transposed-store
-    NN; opt-in with PHA_G4W_PERSIST=1 until it measures ahead of the per-tile grid."""
-    ok = (not a_kouter and not b_kouter) or (a_kouter and not b_kouter)
-    return ok and os.environ.get("PHA_G4W_PERSIST", "0") == "1"
-
-
 def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, aux_out=False, colsum=False,
-         out=None, trans_out=False, persistent=None):
+         out=None, trans_out=False):
     """C = epi(op(A) @ op(B)).
 
     trans_out (a_kouter=True, b_kouter=False only): return C^T [N, M] instead — bias is indexed
@@ -123,17 +114,12 @@ def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, au
         if aux is None:
             aux = torch.empty(OM, ON, dtype=a.dtype, device=a.device)
         epi |= EPI_AUXOUT
-    if persistent is None:
-        persistent = persistent_default(a_kouter, b_kouter) and (trans_out or not a_kouter)
     cs = None
     if colsum:
-        rows = (OM + 127) // 128 if persistent else (OM + 255) // 256
-        cs = torch.empty(rows, ON, dtype=torch.float32, device=a.device)
+        cs = torch.empty((OM + 255) // 256, ON, dtype=torch.float32, device=a.device)
         epi |= EPI_COLSUM
     if trans_out:
         epi |= EPI_TRANS
-    if persistent:
-        epi |= EPI_PERSIST
     rc = _L().pha_gemm4w(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), epi, _ptr(bias), _ptr(aux),
                          aux.stride(0) if aux is not None else 0, _ptr(cs), sched_variant(a_kouter, b_kouter), _stream(a))

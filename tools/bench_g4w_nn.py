@@ -37,13 +37,13 @@ def check():
     for (M, N, K) in [(256, 256, 64), (264, 520, 128), (1024, 2048, 512), (4096, 1536, 2048)]:
         x, w = r(M, K), r(K, N)
         ref = x.float() @ w.float()
-        for P in (False, True):
-            c = G.nn(x, w, persistent=P)
+        for P in (False,):
+            c = G.nn(x, w)
             err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
             print(f"check nn M={M} N={N} K={K} persistent={P} rel_err={err:.2e}", flush=True)
             assert c.shape == (M, N) and err < 1e-2, err
             bt = w.t().contiguous()
-            c = G.gemm(x, bt, False, False, persistent=P)
+            c = G.gemm(x, bt, False, False)
             err = (c.float() - ref).abs().max().item() / ref.abs().max().item()
             print(f"check NT M={M} N={N} K={K} persistent={P} rel_err={err:.2e}", flush=True)
             assert err < 1e-2, err
@@ -77,14 +77,15 @@ def bench():
     for name, K, N in [("qkv", 2048, 6144), ("out", 2048, 2048), ("fc1", 2048, 8192), ("fc2", 8192, 2048)]:
         x, w, dy = r(T, K), r(K, N), r(T, N)
         wt = w.t().contiguous()
+        b_ = torch.randn(N, device="cuda")
         fl = 2.0 * T * K * N
         rows = [
             ("fwd", [("lib NN", lambda: x @ w), ("lib NT(Wt)", lambda: x @ wt.t())],
-             [("own nn", lambda: G.nn(x, w, persistent=False)), ("own nn-P", lambda: G.nn(x, w, persistent=True))]),
+             [("own nn", lambda: G.nn(x, w)),
+              ("own nn+bias+gelu", lambda: G.nn(x, w, bias=b_, act="gelu", aux_out=True))]),
             ("dX ", [("lib NT", lambda: dy @ w.t())],
-             [("own NT", lambda: G.gemm(dy, w, False, False, persistent=False)),
-              ("own NT-P", lambda: G.gemm(dy, w, False, False, persistent=True)),
-              ("own nn-P(Wt)", lambda: G.nn(dy, wt, persistent=True))]),
+             [("own NT", lambda: G.gemm(dy, w, False, False)),
+              ("own nn(Wt)", lambda: G.nn(dy, wt))]),
             ("dW ", [("lib TN", lambda: x.t() @ dy)], [("own TN", lambda: G.gemm(x, dy, True, True))]),
         ]
         for lab, libs, owns in rows:
@@ -99,7 +100,6 @@ def bench():
     h, dl = r(T, 2048), r(T, 50304)
     fl = 2.0 * T * 2048 * 50304
     for lab, f_lib, f_own in [("logits h@E^T", lambda: h @ E.t(), lambda: G.gemm(h, E, False, False)),
-                              ("logits np   ", lambda: h @ E.t(), lambda: G.gemm(h, E, False, False, persistent=False)),
                               ("dh dL@E     ", lambda: dl @ E, lambda: G.nn(dl, E)),
                               ("dE dL^T@h   ", lambda: dl.t() @ h, lambda: G.gemm(dl, h, True, True))]:
         tl, to = timeit(f_lib, 5), timeit(f_own, 5)
@@ -112,16 +112,16 @@ def bench():
 
 
 def sweep():
-    """SCHED variants of the persistent NT and transposed-store layouts at the GPT shapes"""
+    """SCHED variants of the NT and transposed-store layouts at the GPT shapes"""
     T = 32768
     for K, N in ((2048, 8192), (2048, 2048), (8192, 2048)):
         x, w, bt = r(T, K), r(K, N), r(N, K)
         fl = 2.0 * T * K * N
         out = []
-        for sc in ("0", "2", "4"):
+        for sc in ("0", "2"):
             os.environ["PHA_G4W_SCHED"] = sc
-            out.append(f"nn-P sched{sc} {fl / timeit(lambda: G.nn(x, w)) / 1e12:6.0f}")
-            out.append(f"NT-P sched{sc} {fl / timeit(lambda: G.gemm(x, bt, False, False)) / 1e12:6.0f}")
+            out.append(f"nn sched{sc} {fl / timeit(lambda: G.nn(x, w)) / 1e12:6.0f}")
+            out.append(f"NT sched{sc} {fl / timeit(lambda: G.gemm(x, bt, False, False)) / 1e12:6.0f}")
         os.environ.pop("PHA_G4W_SCHED", None)
         print(f"nn sweep {T}x{N}x{K}: " + "  ".join(out) + " TF", flush=True)
 

@@ -22,13 +22,13 @@ def timeit(fn, iters=10):
     return best
 
 
-def run(a, b, ako, bko, trans, skip, persist=False):
+def run(a, b, ako, bko, trans, skip, persist=False, extra=0):
     L = G._L()
     M, Ka = (a.shape[1], a.shape[0]) if ako else (a.shape[0], a.shape[1])
     N = b.shape[1] if bko else b.shape[0]
     OM, ON = (N, M) if trans else (M, N)
     c = torch.empty(OM, ON, dtype=a.dtype, device=a.device)
-    epi = (G.EPI_TRANS if trans else 0) | (128 if skip else 0) | (G.EPI_PERSIST if persist else 0)
+    epi = (G.EPI_TRANS if trans else 0) | (128 if skip else 0) | (G.EPI_PERSIST if persist else 0) | extra
 
     def f():
         rc = L.pha_gemm4w(1, G._ptr(a), G._ptr(b), G._ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
@@ -40,7 +40,7 @@ def run(a, b, ako, bko, trans, skip, persist=False):
 
 r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()  # noqa: E731
 M, N = 32768, 8192
-for K in (64, 128, 256, 512, 1024, 2048, 4096):
+for K in (64, 256, 2048):
     x, bt, w, xt = r(M, K), r(N, K), r(K, N), r(K, M)
     fl = 2.0 * M * N * K
     t = {}
@@ -48,8 +48,9 @@ for K in (64, 128, 256, 512, 1024, 2048, 4096):
     t["NT-noepi"] = timeit(run(x, bt, False, False, False, True))
     t["NNt"] = timeit(run(w, x, True, False, True, False))
     t["NNt-noepi"] = timeit(run(w, x, True, False, True, True))
-    t["NT-P"] = timeit(run(x, bt, False, False, False, False, True))
-    t["NNt-P"] = timeit(run(w, x, True, False, True, False, True))
+    t["NT-nostore"] = timeit(run(x, bt, False, False, False, False, extra=512))
+    t["NT-nostage"] = timeit(run(x, bt, False, False, False, False, extra=1024))
+    t["NT-neither"] = timeit(run(x, bt, False, False, False, False, extra=1536))
     t["TN"] = timeit(run(xt, w, True, True, False, False))
     t["lib NT"] = timeit(lambda: x @ bt.t())
     print(f"K={K:5d}: " + "  ".join(f"{k} {v * 1e6:7.1f}us ({fl / v / 1e12:5.0f}TF)" for k, v in t.items()), flush=True)
