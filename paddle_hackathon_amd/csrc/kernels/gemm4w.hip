@@ -49,6 +49,7 @@ enum : int {
   EPI_SKIP = 128,      // measurement only: no epilogue (tools/g4w_fixed.py)
   EPI_NOSTORE = 512,   // measurement only: epilogue without its global stores
   EPI_NOSTAGE = 1024,  // measurement only: epilogue without the LDS staging writes
+  EPI_NTSTORE = 2048,  // output stores with the non-temporal (streaming) hint
 };
 
 // Epilogue builds (a kernel template parameter): the dGELU build loads the stored pre-activation,
@@ -372,8 +373,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // read) waits vmcnt(0) too: row-by-row code paid a full memory round trip per row. The dGELU
     // build loads a batch's aux rows before computing it; the others load nothing.
     constexpr bool DG = EK == EK_DGELU, AX = EK == EK_AUX;
-    constexpr int RB = (DG || AX) ? (OT ? 2 : 4) : 8;   // the aux builds hold twice the registers per row
-#pragma unroll
+    constexpr int RB = (DG || AX) ? 4 : 8;   // the aux builds hold twice the registers per row
+    // the batch loop stays rolled: unrolled, the compiler hoists every row's addresses and bounds
+    // tests (C and aux) ahead of the epilogue and spills them
+#pragma unroll 1
     for (int rb = 0; rb < 16; rb += RB) {
       uint4 ov[RB], pv[AX ? RB : 1], auxv[DG ? RB : 1];
       if constexpr (DG) {
@@ -406,12 +409,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         ov[r8] = *reinterpret_cast<const uint4*>(out);
         if constexpr (AX) pv[r8] = *reinterpret_cast<const uint4*>(pre);
+        // one row's GELU math at a time: interleaving the rows' transcendental chains is what
+        // made the aux builds spill
+        if constexpr (DG || AX) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int r8 = 0; r8 < RB; ++r8) {
         const long m = r0 + h * 128 + rl + 8 * (rb + r8);
         if (m >= Mo || !ncol || (epi & EPI_NOSTORE)) continue;
-        *reinterpret_cast<uint4*>(C + m * p.ldc + n) = ov[r8];
+        if (epi & EPI_NTSTORE) {
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, ov[r8]), reinterpret_cast<u32x4_t*>(C + m * p.ldc + n));
+        }
+        else *reinterpret_cast<uint4*>(C + m * p.ldc + n) = ov[r8];
         if constexpr (AX) *reinterpret_cast<uint4*>(AUX + m * p.ldaux + n) = pv[r8];
       }
     }

@@ -51,6 +51,8 @@ for K in (64, 256, 2048):
     t["NT-nostore"] = timeit(run(x, bt, False, False, False, False, extra=512))
     t["NT-nostage"] = timeit(run(x, bt, False, False, False, False, extra=1024))
     t["NT-neither"] = timeit(run(x, bt, False, False, False, False, extra=1536))
+    t["NT-ntstore"] = timeit(run(x, bt, False, False, False, False, extra=2048))
+    t["NNt-ntstore"] = timeit(run(w, x, True, False, True, False, extra=2048))
     t["TN"] = timeit(run(xt, w, True, True, False, False))
     t["lib NT"] = timeit(lambda: x @ bt.t())
     print(f"K={K:5d}: " + "  ".join(f"{k} {v * 1e6:7.1f}us ({fl / v / 1e12:5.0f}TF)" for k, v in t.items()), flush=True)
