@@ -165,16 +165,60 @@ def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=F
     if isinstance(scale_factor, Tensor):
         scale_factor = scale_factor._t.tolist()
     m = mode.lower()
-    kw = {}
-    if m in ("linear", "bilinear", "bicubic", "trilinear"):
-        kw["align_corners"] = align_corners
-    out = TF.interpolate(t, size=size, scale_factor=scale_factor, mode=m, **kw)
+    linear = m in ("linear", "bilinear", "trilinear")
+    if (m == "nearest" and align_corners) or (linear and align_mode == 1 and not align_corners):
+        # conventions torch's interpolate has no switch for (reference interp kernels /
+        # test_{nearest,bilinear}_interp_v2_op.py oracles): nearest with align_corners rounds
+        # ratio * i; align_mode=1 samples at ratio * i (no half-pixel shift)
+        out = _interp_indexed(t, size, scale_factor, m == "nearest", align_corners)
+    else:
+        kw = {}
+        if m in ("linear", "bilinear", "bicubic", "trilinear"):
+            kw["align_corners"] = align_corners
+        out = TF.interpolate(t, size=size, scale_factor=scale_factor, mode=m, **kw)
     if channels_last:
         out = out.movedim(1, -1)
     return _w(out)
 
 
 upsample = interpolate
+
+
+def _interp_indexed(t, size, scale_factor, nearest, align_corners):
+    """separable nearest / linear resampling of the spatial dims of NC... ``t`` with the
+    reference's source coordinates: ratio = (in-1)/(out-1) with align_corners, else 1/scale or
+    in/out; nearest: round(ratio*i) (align_corners) / floor(ratio*i); linear: src = ratio*i"""
+    sp = t.dim() - 2
+    ins = list(t.shape[2:])
+    if size is not None:
+        outs = list(size) if len(size) == sp else [size[0]] * sp
+        scales = [0.0] * sp
+    else:
+        sf = scale_factor if isinstance(scale_factor, (list, tuple)) else [scale_factor] * sp
+        scales = [float(v) for v in sf]
+        outs = [int(i * v) for i, v in zip(ins, scales)]
+    out = t
+    for d in range(sp):
+        n_in, n_out, dim = ins[d], outs[d], 2 + d
+        if n_out > 1:
+            ratio = (n_in - 1.0) / (n_out - 1.0) if align_corners else \
+                (1.0 / scales[d] if scales[d] > 0 else n_in / n_out)
+        else:
+            ratio = 0.0
+        i = torch.arange(n_out, dtype=torch.float64, device=t.device)
+        src = ratio * i
+        if nearest:
+            idx = (src + 0.5 if align_corners else src).floor().long().clamp(0, n_in - 1)
+            out = out.index_select(dim, idx)
+            continue
+        i0 = src.floor().long().clamp(0, n_in - 1)
+        i1 = (i0 + 1).clamp(max=n_in - 1)
+        lam = (src - i0.double()).to(out.dtype)
+        shape = [1] * out.dim()
+        shape[dim] = n_out
+        lam = lam.reshape(shape)
+        out = out.index_select(dim, i0) * (1 - lam) + out.index_select(dim, i1) * lam
+    return out
 
 
 def bilinear(x1, x2, weight, bias=None, name=None):
