@@ -78,14 +78,41 @@ def _pool(n, kind, x, kernel_size, stride, padding, ceil_mode, exclusive, diviso
             return _w(out), _w(mask)
         out = r
     else:
+        # inclusive (exclusive=False) averages divide by the full kernel volume, also for ceil-mode
+        # windows overhanging the padding (reference pool kernels / avg_pool2D_forward_naive);
+        # torch's count_include_pad divides by the window clipped to the padded input
+        if divisor is None and not exclusive:
+            divisor = 1
+            for v in k:
+                divisor *= v
         if n == 1:
-            out = TF.avg_pool1d(t, k, s, pad, ceil_mode, not exclusive)
+            p1 = pad if isinstance(pad, int) else (pad[0] if isinstance(pad, (list, tuple)) else 0)
+            out = TF.avg_pool2d(t.unsqueeze(2), (1, k[0]), (1, s[0]), (0, p1), ceil_mode, not exclusive,
+                                divisor).squeeze(2)
         else:
             f = TF.avg_pool2d if n == 2 else TF.avg_pool3d
             out = f(t, k, s, pad, ceil_mode, not exclusive, divisor)
+    if ceil_mode and pre is None:
+        out = _ceil_tail(out, t, k, s, pad, n, kind, exclusive)
     if cl:
         out = out.movedim(1, -1)
     return _w(out)
+
+
+def _ceil_tail(out, t, k, s, pad, n, kind, exclusive):
+    """ceil_mode output size as the reference computes it, (in - k + 2p + s - 1) / s + 1, which
+    keeps a last window that starts inside the padding (torch drops it): pad the output with what
+    the reference kernel yields for an empty window (0 inclusive avg, 0/0 exclusive avg, the
+    max-pool initial value)"""
+    pads = pad if isinstance(pad, (list, tuple)) else [pad] * n
+    fl = []
+    for i in reversed(range(n)):
+        want = (t.shape[2 + i] - k[i] + 2 * int(pads[i]) + s[i] - 1) // s[i] + 1
+        fl += [0, max(0, want - out.shape[2 + i])]
+    if not any(fl):
+        return out
+    val = torch.finfo(out.dtype).min if kind == "max" else (float("nan") if exclusive else 0.0)
+    return TF.pad(out, fl, value=val)
 
 
 def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
