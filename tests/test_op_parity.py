@@ -802,3 +802,13 @@ def test_clip_increment_scale_stanh():
     # scale_op: bias_after_scale True: x * s + b, False: (x + b) * s (test_scale_op.py)
     np.testing.assert_allclose(paddle.scale(P(x), 2.0, 0.5, bias_after_scale=True).numpy(), x * 2 + 0.5)
     np.testing.assert_allclose(paddle.scale(P(x), 2.0, 0.5, bias_after_scale=False).numpy(), (x + 0.5) * 2)
+
+
+def test_pairwise_distance():
+    # test_pairwise_distance.py: np.linalg.norm(x - y, ord=p, axis=1, keepdims=keepdim)
+    x, y = U(5, 4), U(5, 4)
+    for p in (1.0, 2.0, 3.0, float("inf"), 0.0):
+        for keep in (False, True):
+            got = paddle.nn.functional.pairwise_distance(P(x), P(y), p=p, keepdim=keep).numpy()
+            np.testing.assert_allclose(got, np.linalg.norm(x - y, ord=p, axis=1, keepdims=keep), rtol=1e-6)
+            np.testing.assert_allclose(paddle.nn.PairwiseDistance(p=p, keepdim=keep)(P(x), P(y)).numpy(), got)
