@@ -45,13 +45,17 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
     axis = axis % x.dim()
     if soft_label:
         logp = TF.log_softmax(_up(x), axis) if use_softmax else torch.log(_up(x))
-        lf = lab.float()
-        loss = -(lf * logp)
+        lf = lab.to(logp.dtype)
+        loss = -(lf * logp).sum(axis, keepdim=True)
         if weight is not None:
+            # reference (test_cross_entropy_loss.py cross_entropy_soft): each sample's loss is
+            # scaled by dot(weight, its soft label) and 'mean' divides by the sum of those weights
             shape = [1] * x.dim()
             shape[axis] = -1
-            loss = loss * _t(weight).float().reshape(shape)
-        loss = loss.sum(axis, keepdim=True)
+            cw = (lf * _t(weight).to(logp.dtype).reshape(shape)).sum(axis, keepdim=True)
+            loss = loss * cw
+            if reduction == "mean":
+                return _w(loss.sum() / cw.sum())
         return _w(_reduce(loss, reduction))
     if lab.dim() == x.dim():
         lab = lab.squeeze(axis)

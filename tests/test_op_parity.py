@@ -812,3 +812,44 @@ def test_pairwise_distance():
             got = paddle.nn.functional.pairwise_distance(P(x), P(y), p=p, keepdim=keep).numpy()
             np.testing.assert_allclose(got, np.linalg.norm(x - y, ord=p, axis=1, keepdims=keep), rtol=1e-6)
             np.testing.assert_allclose(paddle.nn.PairwiseDistance(p=p, keepdim=keep)(P(x), P(y)).numpy(), got)
+
+
+def _log_softmax_np(x, axis=-1):
+    return np.log(softmax_np(x, axis))
+
+
+@pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
+def test_cross_entropy_hard_weighted_ignore(reduction):
+    # test_cross_entropy_loss.py cross_entropy_loss_1d
+    x = U(8, 5)
+    lab = R.randint(0, 5, (8,)).astype("int64")
+    lab[2] = -100
+    w = U(5, lo=0.2, hi=2.0)
+    ls = _log_softmax_np(x)
+    out = np.array([0.0 if lab[i] == -100 else -ls[i, lab[i]] * w[lab[i]] for i in range(8)])
+    tw = sum(w[lab[i]] for i in range(8) if lab[i] != -100)
+    want = out.sum() / tw if reduction == "mean" else out.sum() if reduction == "sum" else out
+    got = paddle.nn.functional.cross_entropy(P(x), P(lab), weight=P(w), reduction=reduction).numpy()
+    np.testing.assert_allclose(got.reshape(np.shape(want)), want, rtol=1e-6)
+
+
+@pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
+def test_cross_entropy_soft_weighted(reduction):
+    # test_cross_entropy_loss.py cross_entropy_soft: per-sample weight = dot(weight, soft label)
+    x = U(6, 4)
+    lab = softmax_np(U(6, 4) * 3)
+    w = U(4, lo=0.2, hi=2.0)
+    loss = (-lab * _log_softmax_np(x)).sum(-1, keepdims=True)
+    cw = lab @ w
+    wl = loss * cw[:, None]
+    want = wl.sum() / cw.sum() if reduction == "mean" else wl.sum() if reduction == "sum" else wl
+    got = paddle.nn.functional.cross_entropy(P(x), P(lab), soft_label=True, weight=P(w), reduction=reduction).numpy()
+    np.testing.assert_allclose(got.reshape(np.shape(want)), want, rtol=1e-6)
+
+
+def test_cross_entropy_soft_unweighted_none_keeps_dim():
+    x = U(6, 4)
+    lab = softmax_np(U(6, 4))
+    want = (-lab * _log_softmax_np(x)).sum(-1, keepdims=True)
+    got = paddle.nn.functional.cross_entropy(P(x), P(lab), soft_label=True, reduction="none").numpy()
+    np.testing.assert_allclose(got.reshape(want.shape), want, rtol=1e-6)
