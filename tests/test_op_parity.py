@@ -853,3 +853,15 @@ def test_cross_entropy_soft_unweighted_none_keeps_dim():
     want = (-lab * _log_softmax_np(x)).sum(-1, keepdims=True)
     got = paddle.nn.functional.cross_entropy(P(x), P(lab), soft_label=True, reduction="none").numpy()
     np.testing.assert_allclose(got.reshape(want.shape), want, rtol=1e-6)
+
+
+@pytest.mark.parametrize("reduction", ["batchmean", "mean", "sum", "none"])
+def test_kl_div_negative_targets_masked(reduction):
+    # test_kldiv_loss_op.py kldiv_loss: elements with target < 0 contribute 0
+    x = U(5, 6, lo=-10, hi=10)
+    t = U(5, 6, lo=-10, hi=10)
+    with np.errstate(invalid="ignore"):
+        out = np.where(t >= 0, t * (np.log(t) - x), 0.0)
+    want = {"batchmean": out.sum() / 5, "mean": out.mean(), "sum": out.sum(), "none": out}[reduction]
+    got = paddle.nn.functional.kl_div(P(x), P(t), reduction=reduction).numpy()
+    np.testing.assert_allclose(got.reshape(np.shape(want)), want, rtol=1e-6)
