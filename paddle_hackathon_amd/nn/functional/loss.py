@@ -239,18 +239,65 @@ def cosine_embedding_loss(input1, input2, label, margin=0, reduction="mean", nam
     return _w(TF.cosine_embedding_loss(input1._t, input2._t, label._t, margin, reduction=reduction))
 
 
+class _ReplicatedSum(torch.autograd.Function):
+    """all-reduce SUM whose backward is the identity: every rank goes on with the same replicated
+    value and backpropagates it, so each rank's local partial receives the gradient once (the
+    model-parallel reduce rule; torch's autograd all_reduce would sum the replicas' gradients)"""
+
+    @staticmethod
+    def forward(ctx, x, pg):
+        import torch.distributed as tdist
+        y = x.clone()
+        tdist.all_reduce(y, op=tdist.ReduceOp.SUM, group=pg)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
 def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, scale=64.0, group=None,
                          return_softmax=False, reduction="mean"):
+    """ArcFace-style margin softmax cross-entropy (reference nn/functional/loss.py
+    margin_cross_entropy + the margin_cross_entropy kernel). Class-parallel like the reference:
+    with a distributed job (``group`` None = the default group, or a Group; ``group=False`` forces
+    the single-rank form) every rank holds its shard of the class dimension, labels are global
+    class ids, and the softmax normaliser is reduced over the group (max, then sum of exp) —
+    the returned softmax is this rank's shard of the global one."""
+    import torch.distributed as tdist
     x = _up(logits._t)
     lab = label._t.reshape(-1).long()
+    pg, nranks = None, 1
+    if group is not False and tdist.is_available() and tdist.is_initialized():
+        pg = getattr(group, "process_group", None) if group is not None else None
+        nranks = tdist.get_world_size(pg) if (group is None or pg is not None) else 1
+    C = x.shape[-1]
+    start = 0
+    if nranks > 1:
+        counts = [torch.zeros(1, dtype=torch.int64, device=x.device) for _ in range(nranks)]
+        tdist.all_gather(counts, torch.tensor([C], dtype=torch.int64, device=x.device), group=pg)
+        me = tdist.get_rank(pg)
+        start = int(sum(int(c.item()) for c in counts[:me]))
+    local = lab - start
+    own = (local >= 0) & (local < C)
     theta = torch.acos(x.clamp(-1 + 1e-7, 1 - 1e-7))
     tgt = torch.cos(margin1 * theta + margin2) - margin3
-    oh = TF.one_hot(lab, x.shape[-1]).bool()
+    oh = TF.one_hot(local.clamp(0, C - 1), C).bool() & own[:, None]
     adj = torch.where(oh, tgt, x) * scale
-    loss = TF.cross_entropy(adj, lab, reduction="none").unsqueeze(-1)
+    if nranks == 1:
+        loss = TF.cross_entropy(adj, lab, reduction="none").unsqueeze(-1)
+        sm = torch.softmax(adj, -1) if return_softmax else None
+    else:
+        m = adj.detach().max(-1, keepdim=True).values
+        tdist.all_reduce(m, op=tdist.ReduceOp.MAX, group=pg)
+        e = torch.exp(adj - m)
+        ssum = _ReplicatedSum.apply(e.sum(-1, keepdim=True), pg)
+        t = _ReplicatedSum.apply((adj - m).masked_fill(~oh, 0.0).sum(-1, keepdim=True), pg)
+        loss = torch.log(ssum) - t
+        sm = e / ssum if return_softmax else None
     loss = _reduce(loss, reduction) if reduction else loss
     if return_softmax:
-        return _w(loss), _w(torch.softmax(adj, -1))
+        return _w(loss), _w(sm)
     return _w(loss)
 
 

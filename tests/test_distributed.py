@@ -551,3 +551,36 @@ def test_tensor_parallel_chunked_overlap_matches_serial():
         np.testing.assert_allclose(out["dx"], xt.grad.numpy(), rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(out["dw1"], W1.grad.numpy()[:, r * 16:(r + 1) * 16], rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(out["dw2"], W2.grad.numpy()[r * 16:(r + 1) * 16], rtol=1e-4, atol=1e-6)
+
+
+def _margin_ce_class_parallel(rank, world):
+    import numpy as np
+    import torch
+    import paddle_hackathon_amd as paddle
+    F = paddle.nn.functional
+    rng = np.random.RandomState(0)
+    N, C = 6, 10
+    feat = rng.uniform(-0.9, 0.9, (N, C))
+    lab = rng.randint(0, C, (N,))
+    # full problem on every rank (group=False), then this rank's class shard
+    xf = paddle.to_tensor(feat, stop_gradient=False)
+    lf, sf = F.margin_cross_entropy(xf, paddle.to_tensor(lab), margin2=0.3, scale=8.0, group=False,
+                                    return_softmax=True, reduction="mean")
+    lf.backward()
+    shard = np.array_split(np.arange(C), world)[rank]
+    xs = paddle.to_tensor(feat[:, shard], stop_gradient=False)
+    ls, ss = F.margin_cross_entropy(xs, paddle.to_tensor(lab), margin2=0.3, scale=8.0, return_softmax=True,
+                                    reduction="mean")
+    ls.backward()
+    return {"full": float(lf.numpy().reshape(-1)[0]), "shard": float(ls.numpy().reshape(-1)[0]),
+            "sm_ok": bool(np.allclose(ss.numpy(), sf.numpy()[:, shard], atol=1e-6)),
+            "grad_ok": bool(np.allclose(xs.grad.numpy(), xf.grad.numpy()[:, shard], atol=1e-6))}
+
+
+def test_margin_cross_entropy_class_parallel():
+    """class dimension sharded over 2 ranks == the single-process loss, softmax shard and gradient
+    (reference: margin_cross_entropy with a model-parallel group)"""
+    r = run_dist(_margin_ce_class_parallel, 2)
+    for x in r:
+        assert abs(x["full"] - x["shard"]) < 1e-6, x
+        assert x["sm_ok"] and x["grad_ok"], x
