@@ -51,6 +51,10 @@ def _args():
                          "tune: benchmark solutions for new shapes and write the database; off: library heuristics")
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="ResNet-50: replay the whole training step (fwd + bwd + Momentum) as one hipGraph "
+                         "(paddle.device.cuda.graphs.wrap_cuda_graph); auto = on for one rank with >= 2 warmup steps "
+                         "(the eager warmup and the capture stay out of the timed steps)")
     ap.add_argument("--no-resnet", action="store_true",
                     help="GPT-3 1.3B run: skip the ResNet-50 half of the headline metric (by default it runs after "
                          "the GPT timing, same --steps/--warmup, and lands in config.resnet50_*)")
@@ -187,7 +191,8 @@ def main():
             out["config"].update({"resnet50_samples_per_sec": r["value"],
                                   "resnet50_samples_per_sec_per_gpu": r["config"]["samples_per_sec_per_gpu"],
                                   "resnet50_ms_per_step": r["ms_per_step"],
-                                  "resnet50_global_batch": r["config"]["global_batch"]})
+                                  "resnet50_global_batch": r["config"]["global_batch"],
+                                  "resnet50_hip_graph": r["config"]["hip_graph"]})
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -293,6 +298,13 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
         opt.clear_grad(set_to_zero=False)
         return loss
 
+    graphed = a.graph == "on" or (a.graph == "auto" and world == 1)
+    graphed = graphed and a.warmup >= 2
+    if graphed:
+        # warmup call 1 runs eagerly (GEMM picks, allocator growth), call 2 captures and replays:
+        # every timed step is one replay of the full forward + backward + optimizer kernels
+        from paddle_hackathon_amd.device.cuda.graphs import wrap_cuda_graph
+        step = wrap_cuda_graph(step)
     elapsed, loss = _timed(a, step, world, rank, dist)
     value = B * world * a.steps / elapsed
     res = {
@@ -301,7 +313,8 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
             "ms_per_step": round(elapsed / a.steps * 1000, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic ImageNet-shaped, random-init weights",
             "config": {"model": "ResNet-50", "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
-                       "layout": "NHWC", "samples_per_sec_per_gpu": round(value / world, 2)}}
+                       "layout": "NHWC", "samples_per_sec_per_gpu": round(value / world, 2),
+                       "hip_graph": bool(graphed)}}
     if emit and rank == 0:
         print(json.dumps(res), flush=True)
     return res

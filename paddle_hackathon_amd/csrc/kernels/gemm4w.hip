@@ -50,6 +50,9 @@ enum : int {
   EPI_NOSTORE = 512,   // measurement only: epilogue without its global stores
   EPI_NOSTAGE = 1024,  // measurement only: epilogue without the LDS staging writes
   EPI_NTSTORE = 2048,  // output stores with the non-temporal (streaming) hint
+  EPI_STAGGER = 4096,  // first-round workgroups start in G = (epi >> 24) & 15 phase groups, group g
+                       // after g * ((epi >> 16) & 255) s_sleep(127) — the tiles' output bursts then
+                       // fall on different CUs at different times instead of all at once
 };
 
 // Epilogue builds (a kernel template parameter): the dGELU build loads the stored pre-activation,
@@ -270,6 +273,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
+
+  if ((p.epi & EPI_STAGGER) && bid < 256) {
+    const int groups = max((p.epi >> 24) & 15, 1);
+    const int n = ((bid >> 3) % groups) * ((p.epi >> 16) & 255);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
 
   // prologue
   stage_all(0);

@@ -11,6 +11,8 @@ __all__ = ["Stream", "Event", "current_stream", "synchronize", "device_count", "
            "max_memory_allocated", "max_memory_reserved", "memory_allocated", "memory_reserved",
            "stream_guard", "get_device_properties", "get_device_name", "get_device_capability"]
 
+from . import graphs  # noqa: E402,F401  (hipGraph capture: paddle.device.cuda.graphs)
+
 
 def _dev(device):
     if device is None:

@@ -1,0 +1,261 @@
+"""``paddle.device.cuda.graphs`` on hipGraph (reference: python/paddle/device/cuda/graphs.py:38-118,
+paddle/fluid/platform/cuda_graph_with_memory_pool.cc).
+
+The reference records the kernels of a dygraph region (``CUDAGraph.capture_begin`` /
+``capture_end`` / ``replay``) or of a to_static function (``wrap_cuda_graph``) into a CUDA graph
+with its own memory pool. On MI355X the same object is a hipGraph (``torch.cuda.CUDAGraph`` is
+hipGraph on ROCm): every HIP kernel of this framework launches on the current stream, so a whole
+training step — forward, backward and the fused optimizer kernels, ~700 launches for ResNet-50 —
+replays as ONE graph launch and the host's per-op dispatch cost leaves the step.
+
+What a replay does and does not do (same contract as the reference's CUDA graphs):
+  * it re-runs the captured device work on the captured buffers: inputs must be copied into the
+    tensors the capture read (``wrap_cuda_graph`` does that), outputs land in the same tensors
+    every time;
+  * host-side values read during the capture are frozen into the graph (a Python-float learning
+    rate, an optimizer step counter used on the host): schedule them on the device or recapture;
+  * no host synchronisation may happen inside the captured region (``.item()``, ``.numpy()``).
+
+Capture modes map to ``hipStreamCaptureMode``: ``global`` / ``thread_local`` / ``relaxed``.
+Memory pools: ``"default"`` gives each graph a private pool, ``"new"`` a fresh shared handle,
+and passing a wrapped function or Layer shares that graph's pool (reference ``memory_pool``).
+"""
+from __future__ import annotations
+
+import gc
+import os
+
+import torch
+
+__all__ = ["CUDAGraph", "wrap_cuda_graph", "is_cuda_graph_supported"]
+
+ALL_MODES = ["global", "thread_local", "relaxed"]
+
+
+def is_cuda_graph_supported():
+    """hipGraph capture needs a visible GPU"""
+    return torch.cuda.is_available()
+
+
+class CUDAGraph:
+    """One captured hipGraph. ``capture_begin`` moves the calling thread onto a private side
+    stream (graph capture cannot run on the legacy default stream) that waits for the current
+    stream; ``capture_end`` instantiates the graph and joins the side stream back."""
+
+    _next_id = 0
+
+    def __init__(self, place=None, mode="thread_local", pool=None):
+        if mode not in ALL_MODES:
+            raise ValueError(f"mode must be one of {ALL_MODES}, got {mode!r}")
+        if not is_cuda_graph_supported():
+            raise RuntimeError("CUDAGraph needs a HIP device (no GPU visible)")
+        dev = None
+        if place is not None:
+            dev = place.get_device_id() if hasattr(place, "get_device_id") else int(place)
+        self._device = torch.cuda.current_device() if dev is None else dev
+        self._mode = mode
+        self._pool = pool
+        self._graph = None
+        self._stream = None
+        self._stream_ctx = None
+        self._prev_stream = None
+        self.id = CUDAGraph._next_id
+        CUDAGraph._next_id += 1
+
+    def capture_begin(self):
+        if self._graph is not None:
+            raise RuntimeError("graph already captured; call reset() before capturing again")
+        torch.cuda.synchronize(self._device)
+        gc.collect()
+        self._graph = torch.cuda.CUDAGraph()
+        self._graph.enable_debug_mode()   # keeps the graph template for print_to_dot_files
+        self._prev_stream = torch.cuda.current_stream(self._device)
+        self._stream = torch.cuda.Stream(device=self._device)
+        self._stream.wait_stream(self._prev_stream)
+        self._stream_ctx = torch.cuda.stream(self._stream)
+        self._stream_ctx.__enter__()
+        try:
+            self._graph.capture_begin(pool=self._pool, capture_error_mode=self._mode)
+        except Exception:
+            self._stream_ctx.__exit__(None, None, None)
+            self._stream_ctx = None
+            self._graph = None
+            raise
+
+    def capture_end(self):
+        if self._stream_ctx is None:
+            raise RuntimeError("capture_end() without capture_begin()")
+        try:
+            self._graph.capture_end()
+        finally:
+            self._stream_ctx.__exit__(None, None, None)
+            self._stream_ctx = None
+            self._prev_stream.wait_stream(self._stream)
+
+    def replay(self):
+        if self._graph is None or self._stream_ctx is not None:
+            raise RuntimeError("replay() needs a finished capture")
+        self._graph.replay()
+
+    def reset(self):
+        if self._graph is not None:
+            self._graph.reset()
+        self._graph = None
+
+    def pool(self):
+        """memory-pool handle of this graph (share it with another capture)"""
+        return self._graph.pool() if self._graph is not None else self._pool
+
+    def print_to_dot_files(self, dirname, flags=None):
+        """write the captured graph as Graphviz ``.dot`` (hipGraphDebugDotPrint); ``flags`` is
+        accepted for parity — the HIP runtime prints its full description"""
+        if self._graph is None:
+            raise RuntimeError("nothing captured")
+        if not isinstance(dirname, (str, bytes)):
+            dirname = dirname.name
+        os.makedirs(dirname, exist_ok=True)
+        path = os.path.join(dirname, f"graph_{self.id}.dot")
+        self._graph.debug_dump(path)
+        return path
+
+
+def _tensors_of(obj, out):
+    from ...framework.core import Tensor
+    if isinstance(obj, Tensor):
+        out.append(obj._t)
+    elif isinstance(obj, torch.Tensor):
+        out.append(obj)
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            _tensors_of(o, out)
+    elif isinstance(obj, dict):
+        for k in sorted(obj):
+            _tensors_of(obj[k], out)
+    return out
+
+
+def _signature(obj):
+    """hashable description of the non-tensor structure of the arguments (shape / dtype of
+    tensors, value of everything else): a different signature gets its own graph"""
+    from ...framework.core import Tensor
+    if isinstance(obj, Tensor):
+        obj = obj._t
+    if isinstance(obj, torch.Tensor):
+        return ("T", tuple(obj.shape), str(obj.dtype), str(obj.device))
+    if isinstance(obj, (list, tuple)):
+        return (type(obj).__name__,) + tuple(_signature(o) for o in obj)
+    if isinstance(obj, dict):
+        return ("dict",) + tuple((k, _signature(obj[k])) for k in sorted(obj))
+    return ("V", repr(obj))
+
+
+class GraphedFunction:
+    """``wrap_cuda_graph`` result in dygraph mode. Call 1..warmup: eager, on a side stream (lazy
+    initialisation, per-shape GEMM picks and allocator growth happen outside the capture). The
+    next call captures and then replays once, so every call performs the work exactly once; later
+    calls copy the tensor arguments into the captured inputs and replay. Returns the captured
+    outputs (the same tensors every replay)."""
+
+    def __init__(self, function, mode="thread_local", memory_pool="default", warmup=1):
+        if mode not in ALL_MODES:
+            raise ValueError(f"mode must be one of {ALL_MODES}, got {mode!r}")
+        self._fn = function
+        self._mode = mode
+        self._warmup = warmup
+        if memory_pool == "default":
+            self._pool = None
+        elif memory_pool == "new":
+            self._pool = torch.cuda.graph_pool_handle() if is_cuda_graph_supported() else None
+        elif isinstance(memory_pool, GraphedFunction):
+            self._pool = memory_pool._pool if memory_pool._pool is not None else memory_pool._first_pool()
+        elif hasattr(memory_pool, "_cuda_graph") and isinstance(memory_pool._cuda_graph, GraphedFunction):
+            self._pool = memory_pool._cuda_graph._first_pool()
+        else:
+            raise ValueError("memory_pool must be 'default', 'new', or a wrapped function / Layer")
+        self._entries = {}
+        self._calls = {}
+
+    def _first_pool(self):
+        for ent in self._entries.values():
+            return ent[0].pool()
+        return None
+
+    def __call__(self, *args, **kwargs):
+        if not is_cuda_graph_supported():
+            return self._fn(*args, **kwargs)
+        key = _signature((args, kwargs))
+        ent = self._entries.get(key)
+        if ent is None:
+            n = self._calls.get(key, 0)
+            self._calls[key] = n + 1
+            if n < self._warmup:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    out = self._fn(*args, **kwargs)
+                torch.cuda.current_stream().wait_stream(s)
+                return out
+            g = CUDAGraph(mode=self._mode, pool=self._pool)
+            g.capture_begin()
+            try:
+                out = self._fn(*args, **kwargs)
+            finally:
+                g.capture_end()
+            ent = (g, _tensors_of((args, kwargs), []), out)
+            self._entries[key] = ent
+            g.replay()   # the capture itself ran nothing
+            return out
+        g, static_in, out = ent
+        for dst, src in zip(static_in, _tensors_of((args, kwargs), [])):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+        g.replay()
+        return out
+
+    def reset(self):
+        for g, _, _ in self._entries.values():
+            g.reset()
+        self._entries.clear()
+        self._calls.clear()
+
+
+def wrap_cuda_graph(function, mode="thread_local", memory_pool="default", warmup=1):
+    """Reference ``wrap_cuda_graph``. Dygraph: a :class:`GraphedFunction` around ``function``
+    (a Layer's forward is wrapped in place and the Layer returned). Static mode: the ops the
+    function records are tagged ``_cuda_graph_attr`` = "mode;pool;id" like the reference's
+    ``_cuda_graph_guard`` (carried in the Program IR; ``CompiledProgram`` with
+    ``build_strategy.use_hip_graph`` replays a program as one hipGraph)."""
+    from ...framework import core as _core
+    from ...nn import Layer
+    if mode not in ALL_MODES:
+        raise ValueError(f"mode must be one of {ALL_MODES}, got {mode!r}")
+    if not _core.in_dynamic_mode():
+        return _static_guard(function, mode, memory_pool)
+    if isinstance(function, Layer):
+        layer = function
+        gf = GraphedFunction(layer.forward, mode, memory_pool, warmup)
+        layer._cuda_graph = gf
+        layer.forward = gf
+        return layer
+    return GraphedFunction(function, mode, memory_pool, warmup)
+
+
+_static_ids = [0]
+
+
+def _static_guard(function, mode, memory_pool):
+    if memory_pool not in ("default", "new"):
+        raise ValueError("memory_pool should be 'default' or 'new' under static mode")
+    gid = _static_ids[0]
+    _static_ids[0] += 1
+    attr = f"{mode};{0 if memory_pool == 'default' else gid + 1};{gid}"
+
+    def run(*args, **kwargs):
+        from ...static import default_main_program
+        block = default_main_program().global_block()
+        n0 = len(block.ops)
+        out = function(*args, **kwargs)
+        for op in block.ops[n0:]:
+            op.attrs["_cuda_graph_attr"] = attr
+        return out
+    return run

@@ -165,7 +165,9 @@ def conv_bwd_data(dy, weight, x_shape, stride, padding, dilation):
             nh, nw = len(khs), len(kws)
             # phase output i' reads dY row i' + bh - j for tap j  ==  stride-1 conv with taps
             # reversed (t = nh-1-j) and pad = nh-1-bh
-            sub = weight[:, :, khs[::-1], :][:, :, :, kws[::-1]]  # [Co][Ci][nh][nw]
+            # taps kh0, kh0 + sh, ... reversed: slices + flip (no host index tensor, so this
+            # also runs inside a hipGraph capture)
+            sub = weight[:, :, kh0::sh, :][:, :, :, kw0::sw].flip((2, 3))  # [Co][Ci][nh][nw]
             wt = sub.permute(1, 2, 3, 0).contiguous()  # [Ci][nh][nw][Co]
             PH, PW = len(hs), len(ws_)
             tmp = torch.empty(N, PH, PW, Ci, dtype=dy.dtype, device=dy.device)
@@ -430,8 +432,8 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None):
         # khs[j]: a stride-1 conv over the reversed taps with top padding nh - 1 - bh
         bh, bw = (rh + ph - kh0) // sh, (rw + pw - kw0) // sw
         nh, nw = len(khs), len(kws)
-        wt = _wlayout(w, ("phase", rh, rw, sh, sw, ph, pw), lambda t, khs=khs, kws=kws:
-                      t[:, :, khs[::-1], :][:, :, :, kws[::-1]].permute(1, 2, 3, 0).contiguous())   # [Ci][nh][nw][Co]
+        wt = _wlayout(w, ("phase", rh, rw, sh, sw, ph, pw), lambda t, kh0=kh0, kw0=kw0:   # reversed taps
+                      t[:, :, kh0::sh, :][:, :, :, kw0::sw].flip((2, 3)).permute(1, 2, 3, 0).contiguous())   # [Ci][nh][nw][Co]
         _run(dy, wt, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
              remap=(rh, rw, sh, sw, PH, PW, zero_rest))
     return _done(dx)

@@ -365,8 +365,56 @@ def _chunk():
     return _L().pha_chunk_size()
 
 
+class _CaptureStaging:
+    """Page-locked host staging for pointer tables built while a hipGraph is being captured.
+    torch's pinned caching allocator records an event on the capturing stream, which HIP refuses,
+    so a table uploaded during capture is written into a block of this hipHostMalloc arena
+    (allocated on the first eager upload, i.e. before any capture) and copied by a
+    hipMemcpyAsync that the graph records as a memcpy node. Blocks are never reused: the graph
+    re-reads them on every replay."""
+    SIZE = 8 << 20
+
+    def __init__(self):
+        import ctypes
+        self._ct = ctypes
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        self._hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.c_void_p]
+        p = ctypes.c_void_p()
+        rc = self._hip.hipHostMalloc(ctypes.byref(p), self.SIZE, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipHostMalloc failed ({rc})")
+        self._base, self._used = p.value, 0
+
+    def upload(self, raw, device):
+        n = raw.nbytes
+        off = (self._used + 255) & ~255
+        if off + n > self.SIZE:
+            raise RuntimeError("hipGraph capture staging exhausted (pointer tables of too many captures)")
+        self._used = off + n
+        self._ct.memmove(self._base + off, raw.ctypes.data, n)
+        dst = torch.empty(n, dtype=torch.uint8, device=device)
+        rc = self._hip.hipMemcpyAsync(dst.data_ptr(), self._base + off, n, 1,
+                                      torch.cuda.current_stream(device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"hipMemcpyAsync failed during capture ({rc})")
+        return dst
+
+
+_staging = None
+
+
 def _upload(arr, device):
-    host = torch.from_numpy(arr.view(np.uint8).copy()).pin_memory()
+    global _staging
+    raw = np.ascontiguousarray(arr.view(np.uint8))
+    if torch.cuda.is_current_stream_capturing():
+        if _staging is None:
+            raise RuntimeError("pointer tables built during a hipGraph capture need one eager step first")
+        return _staging.upload(raw, device)
+    if _staging is None and torch.cuda.is_available():
+        _staging = _CaptureStaging()
+    host = torch.from_numpy(raw.copy()).pin_memory()
     return host.to(device, non_blocking=True)
 
 

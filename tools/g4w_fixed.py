@@ -40,7 +40,10 @@ def run(a, b, ako, bko, trans, skip, persist=False, extra=0):
 
 r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()  # noqa: E731
 M, N = 32768, 8192
-for K in (64, 256, 2048):
+SHAPES = [(M, N, K) for K in (64, 256, 2048)]
+if len(sys.argv) > 1:   # M,N,K triples
+    SHAPES = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+for M, N, K in SHAPES:
     x, bt, w, xt = r(M, K), r(N, K), r(K, N), r(K, M)
     fl = 2.0 * M * N * K
     t = {}
@@ -55,4 +58,4 @@ for K in (64, 256, 2048):
     t["NNt-ntstore"] = timeit(run(w, x, True, False, True, False, extra=2048))
     t["TN"] = timeit(run(xt, w, True, True, False, False))
     t["lib NT"] = timeit(lambda: x @ bt.t())
-    print(f"K={K:5d}: " + "  ".join(f"{k} {v * 1e6:7.1f}us ({fl / v / 1e12:5.0f}TF)" for k, v in t.items()), flush=True)
+    print(f"M={M} N={N} K={K:5d}: " + "  ".join(f"{k} {v * 1e6:7.1f}us ({fl / v / 1e12:5.0f}TF)" for k, v in t.items()), flush=True)
