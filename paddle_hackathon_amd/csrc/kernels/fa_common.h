@@ -16,6 +16,11 @@ typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 constexpr float kLog2e = 1.4426950408889634f;
+
+// 2^x as the bare v_exp_f32. exp2f() wraps it in a denormal-range fixup (compare, scale by 2^64,
+// v_ldexp, select: 4 extra VALU ops per element, 128 per backward tile at one wave per SIMD);
+// softmax probabilities below 2^-126 are zero for every use here (-inf masks give exactly 0)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 constexpr float kLn2 = 0.6931471805599453f;
 
 template <typename T> struct MF;

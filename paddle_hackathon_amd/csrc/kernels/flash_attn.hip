@@ -19,6 +19,7 @@
 // Backward: a key-parallel dK/dV kernel and a query-parallel dQ kernel (see below) — no
 // atomics and no cross-workgroup reduction; both prefetch their next tile into registers.
 #include "fa_common.h"
+#include <type_traits>
 #include <cstdlib>
 
 using namespace pha;
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
     if (!__all(tmax <= m_run + kThr)) {
       const float m_new = fmaxf(m_run, tmax);
       const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      const float alpha = fexp2(m_run - m_use);
       l_run *= alpha;
 #pragma unroll
       for (int i = 0; i < ND; ++i)
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[kb][r] - m_use);
+        const float p = fexp2(s[kb][r] - m_use);
         s[kb][r] = p;
         psum += p;
       }
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
       if (!__all(tmax <= m_run + kThr)) {
         const float m_new = fmaxf(m_run, tmax);
         const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-        const float alpha = exp2f(m_run - m_use);
+        const float alpha = fexp2(m_run - m_use);
         l_run *= alpha;
 #pragma unroll
         for (int i = 0; i < ND; ++i)
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kb][r] - m_use);
+          const float p = fexp2(s[kb][r] - m_use);
           s[kb][r] = p;
           psum += p;
         }
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
           if constexpr (EXT & 1) {
             if (bcol) sv += bcol[(long)qq * ex.sq] * kLog2e;
           }
-          p = exp2f(sv - lse_lds[ql] * kLog2e);
+          p = fexp2(sv - lse_lds[ql] * kLog2e);
           float dpv = dpacc[r];
           if constexpr (EXT & 2) {   // dV sees the dropped P; dS = P (Z dP / (1-rate) - delta)
             const bool kp = fa_keep(fa_row(dstream, qq), key, ex.thresh);
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = acc_row(r, h);
-        const float p = exp2f(sacc[r] * scale_log2 - lse_lds[ql] * kLog2e);
+        const float p = fexp2(sacc[r] * scale_log2 - lse_lds[ql] * kLog2e);
         sacc[r] = p;
         dpacc[r] = p * (dpacc[r] - del_lds[ql]);
       }
@@ -815,7 +816,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
           if constexpr (EXT & 1) {
             if (ok && brow) sv += brow[kk] * kLog2e;
           }
-          const float p = ok ? exp2f(sv - lse2) : 0.f;
+          const float p = ok ? fexp2(sv - lse2) : 0.f;
           float dpv = dp[kb][r];
           if constexpr (EXT & 2) dpv = fa_keep(drow, kk, ex.thresh) ? dpv * ex.keep_scale : 0.f;
           s[kb][r] = p * (dpv - dlt);   // dS^T
@@ -824,7 +825,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = exp2f(s[kb][r] * scale_log2 - lse2) * (dp[kb][r] - dlt);
+        for (int r = 0; r < 16; ++r) s[kb][r] = fexp2(s[kb][r] * scale_log2 - lse2) * (dp[kb][r] - dlt);
     }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -878,6 +879,14 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
 // 4 waves (128 keys) with one wave per SIMD: the per-wave state (K/V fragments 64 regs, dK^T/dV^T
 // 128, S/dP 32, staging 32) exceeds the 256-register share two waves per SIMD would leave.
 constexpr int NTKV = 256;
+
+// A/B-measured code-shape switches (tools/bench_fa.py, B=8 S=2048 H=16 D=128 causal, backward):
+// a separate unmasked probability loop for the interior tiles pays in dK/dV (0.938 -> 0.811 ms with
+// the bare exp) but not in dQ (0.945 -> 1.105 ms: the dQ loop's schedule degrades); the bare
+// v_exp_f32 pays in dQ too (0.848 -> 0.811 ms). profiles/flash_attn_exp_mask_ab_r2.log
+constexpr bool kSplitMaskDkdv = true;
+constexpr bool kSplitMaskDq = false;
+constexpr bool kDqBareExp = true;
 
 template <typename T, bool CAUSAL, bool ILP2>
 __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v2(const T* __restrict__ Q, const T* __restrict__ K,
@@ -987,15 +996,23 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
         dpacc = MF<T>::mma(as_frag<frag>(ga), vf[kk], dpacc);
       }
       const bool need_mask = (qh + 32 > S) || (wk0 + 32 > Sk) || (CAUSAL && wk0 + 31 > qh);
+      // the mask test is wave-uniform: the unmasked version (all but the diagonal / ragged
+      // tiles) carries no per-element compares and selects
+      auto probs = [&](auto masked_c) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = half * 32 + acc_row(r, h);
-        const int qq = qt + ql;
-        float p = exp2f(sacc[r] * scale_log2 - lse_l[ql]);
-        if (need_mask && (qq >= S || key >= Sk || (CAUSAL && key > qq))) p = 0.f;
-        sacc[r] = p;
-        dpacc[r] = p * (dpacc[r] - del_l[ql]);
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int ql = half * 32 + acc_row(r, h);
+          float p = fexp2(sacc[r] * scale_log2 - lse_l[ql]);
+          if constexpr (decltype(masked_c)::value) {
+            const int qq = qt + ql;
+            if (qq >= S || key >= Sk || (CAUSAL && key > qq)) p = 0.f;
+          }
+          sacc[r] = p;
+          dpacc[r] = p * (dpacc[r] - del_l[ql]);
+        }
+      };
+      if (!kSplitMaskDkdv || need_mask) probs(std::true_type{});
+      else probs(std::false_type{});
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         u32x4 pw, dw;
@@ -1129,13 +1146,19 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
           st = MF<T>::mma(as_frag<frag>(ka), qf[kk], st);
           dpt = MF<T>::mma(as_frag<frag>(va), gf[kk], dpt);
         }
+        auto probs = [&](auto masked_c) {   // wave-uniform mask test, as in fa_bwd_dkdv_v2
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kk = k0 + kb * 32 + acc_row(r, h);
-          float p = exp2f(st[r] * scale_log2 - lse2);
-          if (need_mask && (kk >= Sk || (CAUSAL && kk > q))) p = 0.f;
-          dpt[r] = p * (dpt[r] - dlt);
-        }
+          for (int r = 0; r < 16; ++r) {
+            float p = kDqBareExp ? fexp2(st[r] * scale_log2 - lse2) : exp2f(st[r] * scale_log2 - lse2);
+            if constexpr (decltype(masked_c)::value) {
+              const int kk = k0 + kb * 32 + acc_row(r, h);
+              if (kk >= Sk || (CAUSAL && kk > q)) p = 0.f;
+            }
+            dpt[r] = p * (dpt[r] - dlt);
+          }
+        };
+        if (!kSplitMaskDq || need_mask) probs(std::true_type{});
+        else probs(std::false_type{});
         // dQ^T[d][q] += K^T[d][key] dS^T[key][q] for this block's two 16-key steps
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {

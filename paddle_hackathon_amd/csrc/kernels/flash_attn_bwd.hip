@@ -171,7 +171,7 @@ void fa_bwd_fused(const T* __restrict__ Q, const T* __restrict__ K, const T* __r
       const int key = k0 + krow;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(sacc[r] * scale_log2);
+        float p = fexp2(sacc[r] * scale_log2);
         if (need_mask && (key >= Sk || (CAUSAL && key > q0 + acc_row(r, h)))) p = 0.f;
         sacc[r] = p;
         dpacc[r] *= p;   // dS (softmax scale applied at the outputs)

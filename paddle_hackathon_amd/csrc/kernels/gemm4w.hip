@@ -131,7 +131,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int bid = blockIdx.x;
   const int q8 = total >> 3, r8 = total & 7, xcd = bid & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  constexpr int GROUP_M = 8;
+  // GROUP_M-row panels (4: measured best or tied at every GPT NT / NN / TN shape against 2..32,
+  // profiles/gemm4w_group_m_r2.log); measurement override: (epi >> 28) & 7 = log2(GROUP_M)
+  const int GROUP_M = ((p.epi >> 28) & 7) ? (1 << ((p.epi >> 28) & 7)) : 4;
   const int group = lin / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);

@@ -12,6 +12,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_C", "libpha_kernels.so")
+if os.environ.get("PHA_KERNELS_LIB"):   # A/B measurements against another in-tree build
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "_C", os.environ["PHA_KERNELS_LIB"])
 
 lib = None
 _load_error = None

@@ -12,7 +12,9 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0] if not name.startswith("void ") else name[5:].split("(")[0]
+    n = name[5:] if name.startswith("void ") else name
+    n = n.replace("(anonymous namespace)::", "")
+    n = n.split("(")[0]
     return n[:90]
 
 
