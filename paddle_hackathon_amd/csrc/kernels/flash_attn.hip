@@ -323,10 +323,11 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + NT2 * i;
-      const int key = k0 + (c >> 4), ch = c & 15;
-      const bool ok = key < Sk;
-      kreg[i] = ok ? *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
-      vreg[i] = ok ? *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+      // keys past Sk read row Sk - 1 (finite; their scores are masked to -inf, P = 0): no exec
+      // branch per load, no zero-fill of the prefetch registers
+      const int key = min(k0 + (c >> 4), Sk - 1), ch = c & 15;
+      kreg[i] = *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8);
+      vreg[i] = *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + ch * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -561,17 +562,19 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
   const float* bcol = ((EXT & 1) && key < Sk) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + key : nullptr;
   const unsigned dstream = (EXT & 2) ? fa_stream(ex.seed, b * H + head) : 0u;
 
+  // keys past Sk read row Sk - 1 (finite; their P and dS are masked to 0 and their dK / dV rows
+  // are not stored): unconditional loads, no exec branch per load
+  const int keyc = min(key, Sk - 1);
   frag kf[NK], vf[NK];
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
-    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
-    if (key < Sk) {
-      a = *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + 16 * kk + 8 * h);
-      c = *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + 16 * kk + 8 * h);
-    }
-    kf[kk] = as_frag<frag>(a);
-    vf[kk] = as_frag<frag>(c);
+    kf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Kb + (long)keyc * kstride + 16 * kk + 8 * h));
+    vf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Vb + (long)keyc * kstride + 16 * kk + 8 * h));
   }
+  // retire the fragment loads here, through the builtin (the waitcnt pass tracks it; inline asm
+  // it does not): otherwise the loop's MFMAs carry counted waits for them that, in steady state,
+  // drain most of the next tile's prefetch (vmcnt counts in issue order)
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt / lgkmcnt untouched
   f32x16 dvt[ND], dkt[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
@@ -918,17 +921,19 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   const float* del_b = DELTA + ((long)b * H + head) * S;
   const float scale_log2 = scale * kLog2e;
 
+  // keys past Sk read row Sk - 1 (finite; their P and dS are masked to 0 and their dK / dV rows
+  // are not stored): unconditional loads, no exec branch per load
+  const int keyc = min(key, Sk - 1);
   frag kf[NK], vf[NK];
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
-    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
-    if (key < Sk) {
-      a = *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + 16 * kk + 8 * h);
-      c = *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + 16 * kk + 8 * h);
-    }
-    kf[kk] = as_frag<frag>(a);
-    vf[kk] = as_frag<frag>(c);
+    kf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Kb + (long)keyc * kstride + 16 * kk + 8 * h));
+    vf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Vb + (long)keyc * kstride + 16 * kk + 8 * h));
   }
+  // retire the fragment loads here, through the builtin (the waitcnt pass tracks it; inline asm
+  // it does not): otherwise the loop's MFMAs carry counted waits for them that, in steady state,
+  // drain most of the next tile's prefetch (vmcnt counts in issue order)
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt / lgkmcnt untouched
   f32x16 dvt[ND], dkt[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
@@ -943,15 +948,15 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       const int c = tid + NTKV * i;              // [0, 2048): first 1024 Q, then dO
       const int which = c >> 10, cc = c & 1023;
       const int row = cc >> 4, ch = cc & 15;
-      const int qq = qt + row;
+      // rows past S read row S - 1 (finite, and masked to P = 0): no exec branch per load
+      const int qq = min(qt + row, S - 1);
       const T* src = which ? dOb : Qb;
       const long rs = which ? fs.o_tok : fs.q_tok;
-      sreg[i] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * rs + ch * 8) : u32x4{0, 0, 0, 0};
+      sreg[i] = *reinterpret_cast<const u32x4*>(src + (long)qq * rs + ch * 8);
     }
-    if (tid < 2 * BQ) {
-      const int qq = qt + (tid & (BQ - 1));
-      srow = (qq < S) ? (tid < BQ ? lse_b[qq] * kLog2e : del_b[qq]) : 0.f;
-    }
+    // raw value: any arithmetic on it here would wait (in-order vmcnt) for the whole prefetch
+    // issued just above; the log2(e) scaling happens in store_tile, after the tile's MFMAs
+    if (tid < 2 * BQ) srow = (tid < BQ ? lse_b : del_b)[min(qt + (tid & (BQ - 1)), S - 1)];
   };
   auto store_tile = [&](int buf) {
     unsigned char* base = smem + buf * BUF;
@@ -961,7 +966,7 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
       const int which = c >> 10, cc = c & 1023;
       *reinterpret_cast<u32x4*>(base + which * IMG + dual_off(cc >> 4, cc & 15)) = sreg[i];
     }
-    if (tid < 2 * BQ) reinterpret_cast<float*>(base + 2 * IMG)[tid] = srow;
+    if (tid < 2 * BQ) reinterpret_cast<float*>(base + 2 * IMG)[tid] = tid < BQ ? srow * kLog2e : srow;
   };
 
   const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
@@ -1002,11 +1007,16 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ql = half * 32 + acc_row(r, h);
-          float p = fexp2(sacc[r] * scale_log2 - lse_l[ql]);
+          float x = sacc[r] * scale_log2 - lse_l[ql];
           if constexpr (decltype(masked_c)::value) {
+            // select on the exponent (2^-inf = 0): a select after the exp became an exec
+            // branch per element
             const int qq = qt + ql;
-            if (qq >= S || key >= Sk || (CAUSAL && key > qq)) p = 0.f;
+            // bitwise, not short-circuit: || became branches around the lse read
+            const bool out = (qq >= S) | (key >= Sk) | (CAUSAL & (key > qq));
+            x = out ? -INFINITY : x;
           }
+          const float p = fexp2(x);
           sacc[r] = p;
           dpacc[r] = p * (dpacc[r] - del_l[ql]);
         }
@@ -1103,10 +1113,10 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + NT2 * i;
-      const int kk = k0 + (c >> 4), ch = c & 15;
-      const bool ok = kk < Sk;
-      kreg[i] = ok ? *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + ch * 8) : u32x4{0, 0, 0, 0};
-      vreg[i] = ok ? *reinterpret_cast<const u32x4*>(Vb + (long)kk * kstride + ch * 8) : u32x4{0, 0, 0, 0};
+      // keys past Sk read row Sk - 1 (finite; masked to P = 0): no exec branch per load
+      const int kk = min(k0 + (c >> 4), Sk - 1), ch = c & 15;
+      kreg[i] = *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + ch * 8);
+      vreg[i] = *reinterpret_cast<const u32x4*>(Vb + (long)kk * kstride + ch * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -1149,11 +1159,12 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, con
         auto probs = [&](auto masked_c) {   // wave-uniform mask test, as in fa_bwd_dkdv_v2
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            float p = kDqBareExp ? fexp2(st[r] * scale_log2 - lse2) : exp2f(st[r] * scale_log2 - lse2);
-            if constexpr (decltype(masked_c)::value) {
+            float x = st[r] * scale_log2 - lse2;
+            if constexpr (decltype(masked_c)::value) {   // select on the exponent, bitwise test
               const int kk = k0 + kb * 32 + acc_row(r, h);
-              if (kk >= Sk || (CAUSAL && kk > q)) p = 0.f;
+              x = ((kk >= Sk) | (CAUSAL & (kk > q))) ? -INFINITY : x;
             }
+            const float p = kDqBareExp ? fexp2(x) : exp2f(x);
             dpt[r] = p * (dpt[r] - dlt);
           }
         };
