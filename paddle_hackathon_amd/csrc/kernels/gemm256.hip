@@ -61,9 +61,19 @@ struct Args {
   const float* bn_aff;
   float* bn_part;     // [bn_row0 + tiles_m][2][N]
   int bn_row0;
+  // optional C += addend (same layout and ldc as C, after the bias / activation): a conv dgrad
+  // that also receives the residual branch's gradient stores the sum, no separate add pass
+  const void* addend = nullptr;
 };
 
 
+
+// one 16-bit element (bf16 / fp16 bits) as float
+template <typename T>
+__device__ __forceinline__ float u16f(uint16_t u) {
+  if constexpr (std::is_same<T, bf16_t>::value) return __uint_as_float((unsigned)u << 16);
+  else return (float)__builtin_bit_cast(_Float16, u);
+}
 
 // per-lane row state of the A gather for one of the wave's A instructions
 struct ARow {
@@ -265,10 +275,22 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
       }
     }
     if (full_n) {
-      *reinterpret_cast<uint4*>(C + m * p.ldc + n) = v;
+      uint4 o = v;
+      if (p.addend) {
+        const uint4 r = *reinterpret_cast<const uint4*>(static_cast<const T*>(p.addend) + m * p.ldc + n);
+        const uint16_t* ev = reinterpret_cast<const uint16_t*>(&v);
+        const uint16_t* er = reinterpret_cast<const uint16_t*>(&r);
+        uint16_t* eo = reinterpret_cast<uint16_t*>(&o);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) eo[t] = Mf<T>::cvt(u16f<T>(ev[t]) + u16f<T>(er[t]));
+      }
+      *reinterpret_cast<uint4*>(C + m * p.ldc + n) = o;
     } else {
       const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
-      for (int t = 0; t < 8 && n + t < N; ++t) reinterpret_cast<uint16_t*>(C)[m * p.ldc + n + t] = e[t];
+      const uint16_t* ad = static_cast<const uint16_t*>(p.addend);
+      for (int t = 0; t < 8 && n + t < N; ++t)
+        reinterpret_cast<uint16_t*>(C)[m * p.ldc + n + t] =
+            ad ? Mf<T>::cvt(u16f<T>(e[t]) + u16f<T>(ad[m * p.ldc + n + t])) : e[t];
     }
   }
   if (p.bn_part) {
@@ -701,8 +723,9 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
                             int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh, int dw, int act,
                             const void* zero16, int tile, int bk, const int* oremap, float* stats, int* stats_rows,
                             const void* bn_x, const float* bn_mean, const float* bn_aff, float* bn_part, int bn_row0,
-                            hipStream_t stream) {
+                            const void* addend, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (addend && (stats || bn_part || (oremap && oremap[8]))) return (int)hipErrorInvalidValue;
   g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
                   KH, KW, sh, sw, ph, pw, dh, dw, 0, 0, 0, 0, 0, 0, 0};
   if (oremap) {   // {OHF, OWF, oh0, ow0, osh, osw, OH, OW, ozero}: phase output size given explicitly
@@ -713,7 +736,7 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
   if (stats && (oremap || bn_part)) return (int)hipErrorInvalidValue;
   if (bn_part && (!bn_x || !bn_mean || Cout % 8)) return (int)hipErrorInvalidValue;
   g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g, stats,
-               bn_x, bn_mean, bn_aff, bn_part, bn_row0};
+               bn_x, bn_mean, bn_aff, bn_part, bn_row0, addend};
   if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, stats_rows);
   if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, stats_rows);
   return (int)hipErrorInvalidValue;

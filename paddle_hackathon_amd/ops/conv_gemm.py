@@ -226,7 +226,7 @@ def _L256():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm256_nt.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, I, P]
         L.pha_gemm256_nt.restype = c_int
-        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P, P, P, P, I, P]
+        L.pha_conv256_fwd.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P, P, P, P, P, P, I, P, P]
         L.pha_gemm8p.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, I, P, P]
         L.pha_gemm8p.restype = c_int
         L.pha_gemm256_tn.argtypes = [I, P, P, P, P, LG, LG, LG, LG, LG, I, I, P, I, I, P]
@@ -316,7 +316,7 @@ def gemm256_nt(a, bt, bias=None, act=None, out=None):
 
 
 def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=None, remap=None, bn_stats=False,
-                bn_bwd=None):
+                bn_bwd=None, addend=None):
     """NHWC conv forward: x [N, H, W, C] (C % 8 == 0), w [Cout, KH, KW, C] -> y [N, OH, OW, Cout].
 
     ``remap = (oh0, ow0, osh, osw, OH, OW[, zero_rest])`` computes an OH x OW output and stores pixel
@@ -326,7 +326,9 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
     as ``y._pha_bn_stats = (partials, rows, y._version)`` for the batch norm that consumes y.
     ``bn_bwd = (bn_x, mean, affine|None, partials, row0)``: y is the output gradient of that batch
     norm; the epilogue writes the BN backward's per-tile sums into partials from row row0 on and
-    the call returns the number of rows written (with y in ``out``)."""
+    the call returns the number of rows written (with y in ``out``).
+    ``addend``: a tensor shaped like y (not aliasing it) added in the epilogue after the activation
+    — a dgrad that also receives the residual branch's gradient (no bn_stats / bn_bwd with it)."""
     assert x.dtype in _DT and w_okkc.dtype == x.dtype and x.is_contiguous() and w_okkc.is_contiguous()
     N, H, W, C = x.shape
     Co, KH, KW, Cw = w_okkc.shape
@@ -355,12 +357,16 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
     if bn_stats and rm is None and bn_bwd is None:
         part = torch.empty(-(-(N * OH * OW) // 128) * 2 * Co, dtype=torch.float32, device=x.device)
     bx, bmean, baff, bpart, brow0 = bn_bwd if bn_bwd is not None else (None, None, None, None, 0)
+    if addend is not None:
+        assert part is None and bpart is None and (rm is None or rm[8] == 0)
+        assert addend.shape == y.shape and addend.dtype == y.dtype and addend.is_contiguous()
+        assert addend.data_ptr() != y.data_ptr()
 
     def run(tile, bk):
         rc = L.pha_conv256_fwd(_DT[x.dtype], _ptr(x), _ptr(w_okkc), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
                                sh, sw, ph, pw, dh, dw, _ACT[act], z, tile, bk, rm, _ptr(part),
                                byref(rows) if (part is not None or bpart is not None) else None,
-                               _ptr(bx), _ptr(bmean), _ptr(baff), _ptr(bpart), int(brow0), st)
+                               _ptr(bx), _ptr(bmean), _ptr(baff), _ptr(bpart), int(brow0), _ptr(addend), st)
         if rc != 0:
             raise RuntimeError(f"pha_conv256_fwd failed ({rc})")
     run(*_autotune(("conv", x.dtype, N, H, W, C, Co, KH, KW, sh, sw, ph, pw, dh, dw, OH, OW), run))
@@ -371,14 +377,16 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
     return y
 
 
-def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None):
+def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend=None):
     """dx [N, H, W, Ci] of an NHWC conv from dy [N, OH, OW, Co] and w [Co, Ci, KH, KW], on the forward
     kernel: stride 1 is the conv of dy with the flipped, transposed filter (pad' = d*(K-1) - p);
     stride s splits dx into s*s phases, each a stride-1 conv over the taps that reach it, stored
     in place through the kernel's output remap (no scatter copy).
 
     ``bn_src = (bn_x, mean, affine|None, token)``: dx is the output gradient of that batch norm;
-    its backward sums are reduced in the epilogue and attached as ``dx._pha_bn_bwd``."""
+    its backward sums are reduced in the epilogue and attached as ``dx._pha_bn_bwd``.
+    ``addend``: another gradient of x (the residual branch's), summed into dx — in the stride-1
+    epilogue, else by one add after the phases."""
     N, H, W, Ci = x_shape
     Co, _, KH, KW = w.shape
     sh, sw = stride
@@ -386,6 +394,10 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None):
     dh, dw = dilation
     _, OH, OW, _ = dy.shape
     dy = dy.contiguous()
+    assert addend is None or (tuple(addend.shape) == (N, H, W, Ci) and addend.dtype == dy.dtype), x_shape
+    if addend is not None:
+        addend = addend.contiguous()
+        bn_src = None   # the BN-backward epilogue sums would miss the addend
     bn = None
     if bn_src is not None and Ci % 8 == 0 and bn_src[0].shape == (N, H, W, Ci) and bn_src[0].is_contiguous():
         # rows: every launch below writes <= ceil(rows / 128) partial rows
@@ -409,7 +421,9 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None):
         wt = _wlayout(w, "dgrad", lambda t: t.flip(2, 3).permute(1, 2, 3, 0).contiguous())   # [Ci][KH][KW][Co]
         dx = torch.empty(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
         return _done(_run(dy, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
-                          remap=(0, 0, 1, 1, H, W)))
+                          remap=(0, 0, 1, 1, H, W), addend=addend))
+    if addend is not None:
+        return conv256_dgrad(dy, w, x_shape, stride, padding, dilation).add_(addend)
     if (dh, dw) != (1, 1):
         raise NotImplementedError("strided + dilated conv dgrad")
     phases = []
@@ -586,12 +600,43 @@ def _bn_bwd_on():
     return _bn_stats_on() and os.environ.get("PHA_CONV_BN_BWD", "0") == "1"
 
 
+def res_route_begin(x):
+    """Residual-gradient route for a residual block whose input ``x`` (torch tensor) feeds exactly
+    two ops: the block's first convolution and, as ``residual``, the fused BN-add-ReLU that ends the
+    block. Autograd would add the two gradients of x in a separate pass; with the route, the BN's
+    backward hands its residual gradient over and the convolution's dgrad epilogue adds it (one
+    fewer read + write of the activation gradient per block). Returns the route token (or None
+    when not applicable); call ``res_route_end`` after the block's forward."""
+    import os
+    if os.environ.get("PHA_RES_ROUTE", "1") == "0" or not torch.is_grad_enabled() or not x.requires_grad \
+            or not x.is_cuda or x.dtype not in _DT or x.dim() != 4:
+        return None
+    route = {"armed": False}
+    x._pha_res_route = route
+    return route
+
+
+def res_route_end(x, route):
+    if route is not None:
+        try:
+            del x._pha_res_route
+        except AttributeError:
+            pass
+        if route.get("armed") and not route.get("sink"):
+            route["armed"] = False   # no fused BN took the residual: nothing is handed over
+
+
 class Conv2dNHWC256(torch.autograd.Function):
     """NHWC conv2d with forward, dgrad and wgrad all on the 256-tile MFMA kernels."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation):
         ctx.save_for_backward(x)
+        route = getattr(x, "_pha_res_route", None)   # first conv of a routed residual block
+        ctx.route = None
+        if route is not None and not route.get("armed"):
+            route["armed"] = True
+            ctx.route = route
         ctx.weight = weight   # the parameter object itself (a leaf input): its layout cache entries match
         ctx.conf = (stride, padding, dilation, bias is not None)
         src = getattr(x, "_pha_bn_src", None)   # x is a batch norm's output: fuse its backward sums
@@ -608,8 +653,11 @@ class Conv2dNHWC256(torch.autograd.Function):
         weight = ctx.weight
         stride, padding, dilation, has_bias = ctx.conf
         gy = gy.contiguous()
+        route = ctx.route
+        addend = route.pop("g", None) if route is not None and route.get("sink") else None
         dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation,
-                           bn_src=ctx.bn_src if _bn_bwd_on() else None) if ctx.needs_input_grad[0] else None
+                           bn_src=ctx.bn_src if _bn_bwd_on() else None,
+                           addend=addend) if ctx.needs_input_grad[0] else None
         dw = conv256_wgrad(gy, x, weight.shape, stride, padding, dilation) if ctx.needs_input_grad[1] else None
         db = gy.float().sum((0, 1, 2)).to(gy.dtype) if has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None

@@ -404,6 +404,13 @@ class _BatchNormNHWC(torch.autograd.Function):
             ctx.bn_token = object()
             y._pha_bn_src = (x, mean, aff if relu else None, ctx.bn_token)
         ctx.relu, ctx.has_res = relu, residual is not None
+        # residual-gradient route (conv_gemm.res_route_begin): the residual is a block input whose
+        # other consumer, an armed conv, adds this gradient in its dgrad epilogue
+        route = getattr(residual, "_pha_res_route", None) if residual is not None else None
+        ctx.route = None
+        if route is not None and route.get("armed") and not route.get("sink"):
+            route["sink"] = True
+            ctx.route = route
         ctx.wdt = None if weight is None else weight.dtype
         ctx.bdt = None if bias is None else bias.dtype
         return y
@@ -416,6 +423,9 @@ class _BatchNormNHWC(torch.autograd.Function):
             ext = None
         dx, dw, db, dres = _hip.bn_bwd(gy.contiguous(), x, y, w32, mean, istd, ctx.relu, ctx.has_res, affine=aff,
                                        ext_part=None if ext is None else (ext[0], ext[1]))
+        if ctx.route is not None and dres is not None:
+            ctx.route["g"] = dres   # handed to the armed conv's dgrad epilogue
+            dres = None
         return (dx, None if ctx.wdt is None else dw.to(ctx.wdt), None if ctx.bdt is None else db.to(ctx.bdt),
                 None, None, dres, None, None, None)
 

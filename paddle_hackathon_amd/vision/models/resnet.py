@@ -11,6 +11,7 @@ from ... import nn
 from ...nn import functional as F
 from ...nn.layer.conv_norm_pool import _BatchNormBase
 from ...tensor import flatten
+from ...ops import conv_gemm as _conv_gemm
 
 
 def _bn_act(bn, x, residual=None, relu=True):
@@ -76,11 +77,16 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_act(self.bn1, self.conv1(x))
-        out = _bn_act(self.bn2, self.conv2(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        return _bn_act(self.bn3, self.conv3(out), residual=identity)
+        # identity block: conv1 adds the residual gradient in its dgrad epilogue (conv_gemm.res_route_begin)
+        route = _conv_gemm.res_route_begin(x._t) if self.downsample is None and self.training else None
+        try:
+            out = _bn_act(self.bn1, self.conv1(x))
+            out = _bn_act(self.bn2, self.conv2(out))
+            if self.downsample is not None:
+                identity = self.downsample(x)
+            return _bn_act(self.bn3, self.conv3(out), residual=identity)
+        finally:
+            _conv_gemm.res_route_end(x._t, route)
 
 
 class ResNet(nn.Layer):

@@ -1013,3 +1013,55 @@ def test_bias_dropout_residual_layer_norm_kernel(dtype):
     hs = keep.float() / (1 - p)
     torch.testing.assert_close(y1.float(), TF.layer_norm(hs, (H,), w.detach(), b.detach(), 1e-5), atol=5e-2, rtol=3e-2)
 
+
+
+def test_resnet_residual_grad_route(monkeypatch):
+    """identity bottleneck: the fused BN-add-ReLU hands its residual gradient to conv1, whose dgrad
+    epilogue adds it (conv_gemm.res_route_begin); gradients equal the unrouted autograd sum"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import conv_gemm
+    from paddle_hackathon_amd.vision.models.resnet import BottleneckBlock
+    paddle.set_device("gpu:0")
+    seen = []
+    orig = conv_gemm.conv256_dgrad
+
+    def spy(*a, **k):
+        seen.append(k.get("addend") is not None)
+        return orig(*a, **k)
+    monkeypatch.setattr(conv_gemm, "conv256_dgrad", spy)
+    results = []
+    for route in ("1", "0"):
+        monkeypatch.setenv("PHA_RES_ROUTE", route)
+        seen.clear()
+        paddle.seed(5)
+        blk = BottleneckBlock(64, 16, data_format="NHWC")
+        blk = paddle.amp.decorate(blk, level="O2", dtype="bfloat16")
+        blk.train()
+        g = torch.Generator("cuda").manual_seed(9)
+        xt = torch.randn(4, 14, 14, 64, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        x = paddle.Tensor(xt)
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            y = blk(x)
+        (y.astype("float32") ** 2).mean().backward()
+        results.append([xt.grad.float().clone()] + [p._t.grad.float().clone() for p in blk.parameters()
+                                                     if p._t.grad is not None])
+        if route == "1":
+            assert any(seen), "conv1's dgrad did not receive the residual gradient"
+        else:
+            assert not any(seen)
+    for a, b in zip(*results):
+        assert (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-6
+
+
+def test_conv_dgrad_addend():
+    """the conv epilogue addend: dgrad(dy) + r in one launch equals dgrad(dy) + r"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    g = torch.Generator("cuda").manual_seed(1)
+    dy = torch.randn(2, 9, 9, 32, device="cuda", generator=g).bfloat16()
+    w = torch.randn(32, 24, 1, 1, device="cuda", generator=g).bfloat16()
+    r = torch.randn(2, 9, 9, 24, device="cuda", generator=g).bfloat16()
+    base = conv_gemm.conv256_dgrad(dy, w, (2, 9, 9, 24), (1, 1), (0, 0), (1, 1))
+    fused = conv_gemm.conv256_dgrad(dy, w, (2, 9, 9, 24), (1, 1), (0, 0), (1, 1), addend=r)
+    ref = base.float() + r.float()
+    # both sides round to bf16 (the epilogue after the add): within one bf16 ulp of the largest value
+    assert (fused.float() - ref).abs().max() <= 8e-3 * ref.abs().max()
