@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
   const float* del_b = DELTA + ((long)b * H + head) * S;
   const float scale_log2 = scale * kLog2e;
   // extensions (key on the lane): bias column of this key, dropout stream of the (b, h)
-  const float* bcol = ((EXT & 1) && key < Sk) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + key : nullptr;
+  const float* bcol = (EXT & 1) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + min(key, Sk - 1) : nullptr;
   const unsigned dstream = (EXT & 2) ? fa_stream(ex.seed, b * H + head) : 0u;
 
   // keys past Sk read row Sk - 1 (finite; their P and dS are masked to 0 and their dK / dV rows
@@ -591,15 +591,12 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
     if (is_q || is_do) {
       const T* src = is_q ? Qb : dOb;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int qq = qt + rg * 4 + j;
-        sreg[j] = (qq < S) ? *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8) : u32x4{0, 0, 0, 0};
+      for (int j = 0; j < 4; ++j) {   // rows past S read row S - 1 (finite, masked to P = 0)
+        const int qq = min(qt + rg * 4 + j, S - 1);
+        sreg[j] = *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8);
       }
     }
-    if (tid < 2 * BQ) {
-      const int qq = qt + (tid & (BQ - 1));
-      srow = (qq < S) ? (tid < BQ ? lse_b[qq] : del_b[qq]) : 0.f;
-    }
+    if (tid < 2 * BQ) srow = (tid < BQ ? lse_b : del_b)[min(qt + (tid & (BQ - 1)), S - 1)];
   };
   auto store_tile = [&]() {
     if (is_q || is_do) {
@@ -630,26 +627,25 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
     }
     const bool need_mask = EXT || (qt + BQ > S) || (k0 + 128 > Sk) || (CAUSAL && k0 + wid * 32 + 31 > qt);
     if (need_mask) {
+      // branch-free: out-of-range / causal-masked elements become 2^-inf = 0 through a select on the
+      // exponent, the bias read is clamped and unconditional (an exec branch per element around
+      // it serialised its load latency)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ql = acc_row(r, h);
         const int qq = qt + ql;
-        float p = 0.f, ds = 0.f;
-        if (qq < S && key < Sk && !(CAUSAL && key > qq)) {
-          float sv = sacc[r] * scale_log2;
-          if constexpr (EXT & 1) {
-            if (bcol) sv += bcol[(long)qq * ex.sq] * kLog2e;
-          }
-          p = fexp2(sv - lse_lds[ql] * kLog2e);
-          float dpv = dpacc[r];
-          if constexpr (EXT & 2) {   // dV sees the dropped P; dS = P (Z dP / (1-rate) - delta)
-            const bool kp = fa_keep(fa_row(dstream, qq), key, ex.thresh);
-            dpv = kp ? dpv * ex.keep_scale : 0.f;
-            ds = p * (dpv - del_lds[ql]);
-            p = kp ? p * ex.keep_scale : 0.f;
-          } else {
-            ds = p * (dpv - del_lds[ql]);
-          }
+        const bool valid = (qq < S) & (key < Sk) & !(CAUSAL & (key > qq));
+        float sv = sacc[r] * scale_log2;
+        if constexpr (EXT & 1) sv += bcol[(long)min(qq, S - 1) * ex.sq] * kLog2e;
+        float p = fexp2(valid ? sv - lse_lds[ql] * kLog2e : -INFINITY), ds;
+        float dpv = dpacc[r];
+        if constexpr (EXT & 2) {   // dV sees the dropped P; dS = P (Z dP / (1-rate) - delta)
+          const bool kp = fa_keep(fa_row(dstream, qq), key, ex.thresh);
+          dpv = kp ? dpv * ex.keep_scale : 0.f;
+          ds = p * (dpv - del_lds[ql]);
+          p = kp ? p * ex.keep_scale : 0.f;
+        } else {
+          ds = p * (dpv - del_lds[ql]);
         }
         sacc[r] = p;
         dpacc[r] = ds;
@@ -732,7 +728,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
   const float scale_log2 = scale * kLog2e;
   const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
   const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
-  const float* brow = ((EXT & 1) && q < S) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)q * ex.sq : nullptr;
+  // clamped row (q past S reads row S - 1; its probabilities are masked): read unconditionally
+  const float* brow = (EXT & 1) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)min(q, S - 1) * ex.sq : nullptr;
   const unsigned drow = (EXT & 2) ? fa_row(fa_stream(ex.seed, b * H + head), q) : 0u;
 
   frag qf[NK], gf[NK];
@@ -814,12 +811,11 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int kk = k0 + kb * 32 + acc_row(r, h);
-          const bool ok = (kk < Sk) && !(CAUSAL && kk > q);
+          // branch-free (select on the exponent, clamped unconditional bias read)
+          const bool ok = (kk < Sk) & !(CAUSAL & (kk > q));
           float sv = s[kb][r] * scale_log2;
-          if constexpr (EXT & 1) {
-            if (ok && brow) sv += brow[kk] * kLog2e;
-          }
-          const float p = ok ? fexp2(sv - lse2) : 0.f;
+          if constexpr (EXT & 1) sv += brow[min(kk, Sk - 1)] * kLog2e;
+          const float p = fexp2(ok ? sv - lse2 : -INFINITY);
           float dpv = dp[kb][r];
           if constexpr (EXT & 2) dpv = fa_keep(drow, kk, ex.thresh) ? dpv * ex.keep_scale : 0.f;
           s[kb][r] = p * (dpv - dlt);   // dS^T
