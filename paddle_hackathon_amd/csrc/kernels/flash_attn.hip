@@ -368,6 +368,8 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
         }
       }
       const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wave_q0);
+      // scores stay unscaled: max(c s) = c max(s) for c = scale * log2(e) > 0 (the launcher
+      // requires scale > 0), and the exponent below is one fma(s, c, -m) per element
       float tmax = -INFINITY;
       if (need_mask) {
 #pragma unroll
@@ -375,8 +377,8 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kb * 32 + acc_row(r, h);
-            const bool masked = (key >= Sk) || (CAUSAL && key > q);
-            const float v = masked ? -INFINITY : s[kb][r] * scale_log2;
+            const bool masked = (key >= Sk) | (CAUSAL & (key > q));
+            const float v = masked ? -INFINITY : s[kb][r];
             s[kb][r] = v;
             tmax = fmaxf(tmax, v);
           }
@@ -384,13 +386,9 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = s[kb][r] * scale_log2;
-            s[kb][r] = v;
-            tmax = fmaxf(tmax, v);
-          }
+          for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kb][r]);
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
       constexpr float kThr = 8.f;
       if (!__all(tmax <= m_run + kThr)) {
         const float m_new = fmaxf(m_run, tmax);
@@ -409,7 +407,7 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(s[kb][r] - m_use);
+          const float p = fexp2(fmaf(s[kb][r], scale_log2, -m_use));
           s[kb][r] = p;
           psum += p;
         }
@@ -1230,8 +1228,9 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
   const float sl = scale * kLog2e;
   FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   fs.order_g = fa_order_g();
-  if (fsp && !(D == 128 && fwd_v2_enabled())) return (int)hipErrorInvalidValue;
-  if (D == 128 && fwd_v2_enabled()) {
+  const bool v2 = D == 128 && fwd_v2_enabled() && scale > 0.f;   // v2 folds the scale into max / exp
+  if (fsp && !v2) return (int)hipErrorInvalidValue;
+  if (v2) {
     const dim3 g2(B * H, (S + BM2 - 1) / BM2), b2(NT2);
     if (causal)
       hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
