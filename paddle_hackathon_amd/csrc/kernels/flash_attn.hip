@@ -1384,7 +1384,8 @@ PHA_API int pha_flash_attn_bwd_preprocess(int dt, const void* o, const void* dou
 PHA_API int pha_flash_attn_bwd(int dt, const void* q, const void* k, const void* v, const void* dout, const float* lse,
                                const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
                                int D, float scale, int causal, hipStream_t stream) {
-  if (H % Hk || (D != 64 && D != 128)) return (int)hipErrorInvalidValue;
+  // S, Sk >= 1: the kernels clamp out-of-range rows to S - 1 / Sk - 1
+  if (H % Hk || (D != 64 && D != 128) || B <= 0 || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_bwd<bf16_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   if (dt == kF16) return launch_bwd<half_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   return (int)hipErrorInvalidValue;

@@ -290,6 +290,7 @@ def flash_attention_qkvpacked(qkv, num_heads, causal=False, dropout_p=0.0, scale
     B, S = qkv.shape[0], qkv.shape[1]
     q4 = qkv.reshape(B, S, num_heads, -1)
     if (_use_hip(q4) and not (training and dropout_p > 0) and q4.is_contiguous()
+            and (scale is None or scale > 0)   # the packed forward folds a positive scale into its max
             and _hip.flash_attn_packed_supported(q4, num_heads)):
         return _hip.FlashAttentionPacked.apply(q4, bool(causal), scale)
     D = q4.shape[-1] // 3

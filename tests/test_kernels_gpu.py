@@ -1065,3 +1065,29 @@ def test_conv_dgrad_addend():
     ref = base.float() + r.float()
     # both sides round to bf16 (the epilogue after the add): within one bf16 ulp of the largest value
     assert (fused.float() - ref).abs().max() <= 8e-3 * ref.abs().max()
+
+
+def test_flash_attn_nonpositive_scale_and_ragged():
+    """a negative softmax scale takes the forward without the folded-scale max (v1) and still
+    matches the fp32 reference; ragged S / Sk (clamped prefetch rows) match too"""
+    from paddle_hackathon_amd.ops import hip
+    g = torch.Generator("cuda").manual_seed(3)
+    for (S, Sk, scale, causal) in ((200, 200, -0.05, False), (130, 70, None, False), (77, 77, None, True)):
+        q = torch.randn(2, S, 4, 128, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        k = torch.randn(2, Sk, 4, 128, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        v = torch.randn(2, Sk, 4, 128, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        o = hip.FlashAttention.apply(q, k, v, causal, scale)
+        do = torch.randn_like(o)
+        dq, dk, dv = torch.autograd.grad(o, (q, k, v), do)
+        # plain fp32 attention as the oracle (torch SDPA's fp32 backward returned NaN here)
+        qr, kr, vr = (t.detach().float().transpose(1, 2).requires_grad_(True) for t in (q, k, v))
+        sc = scale if scale is not None else 128 ** -0.5
+        att = (qr @ kr.transpose(-1, -2)) * sc
+        if causal:
+            att = att.masked_fill(torch.ones(S, Sk, device="cuda", dtype=torch.bool).triu(1), float("-inf"))
+        orf = att.softmax(-1) @ vr
+        gr = torch.autograd.grad(orf, (qr, kr, vr), do.float().transpose(1, 2))
+        assert (o.float() - orf.transpose(1, 2)).abs().max() < 3e-2
+        for a, r in zip((dq, dk, dv), gr):
+            r = r.transpose(1, 2)
+            assert (a.float() - r).abs().max() <= 3e-2 * max(1.0, r.abs().max().item())
