@@ -70,6 +70,9 @@ def pick_mode(x2d, w1, b1, w2):
     if (os.environ.get("PHA_FUSED_MLP", "1") == "0" or not _own_ok(x2d, w1, w2)
             or torch.cuda.is_current_stream_capturing()):
         return 0
+    if os.environ.get("PHA_FUSED_MLP") == "force":   # A/B measurements: the own fused chain always
+        _modes[key] = 1
+        return 1
     gy = torch.randn(M, H, device=x2d.device, dtype=x2d.dtype)
     times = []
     for m in (0, 1):
