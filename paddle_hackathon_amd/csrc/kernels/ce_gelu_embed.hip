@@ -350,6 +350,98 @@ __global__ __launch_bounds__(256) void embedding_fwd_kernel(const int64_t* __res
   for (int c = lane; c < row_vecs; c += 64) dst[c] = src[c];
 }
 
+// Embedding backward, deterministic and sort-free (reference: phi/kernels/gpu/embedding_grad_kernel.cu:246,
+// whose default path is an atomicAdd scatter and whose deterministic path sorts the ids):
+//   gw[v][:] = sum of gy[r][:] over tokens r with ids[r] == v, in increasing r
+// One workgroup owns an output block of EB_ROWS vocabulary rows x EB_DCH columns, accumulated in
+// fp32 in LDS (128 KB). It scans the whole id vector (4 bytes per token per block, L2-resident),
+// compacts the matching token positions into an LDS list in token order (wave ballots + ordered
+// wave offsets), and adds those gradient rows in list order: every output element is summed in
+// token order by one thread, so results are bitwise reproducible, with no atomics and no sort.
+// Rows nobody looked up (and padding_idx) come out zero; the block writes its whole region.
+constexpr int EB_ROWS = 32, EB_DCH = 1024, EB_CAP = 4096;
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float (&o)[4]);
+template <> __device__ __forceinline__ void ld4<bf16_t>(const bf16_t* p, float (&o)[4]) {
+  const uint2 r = *reinterpret_cast<const uint2*>(p);
+  o[0] = __uint_as_float(r.x << 16); o[1] = __uint_as_float(r.x & 0xffff0000u);
+  o[2] = __uint_as_float(r.y << 16); o[3] = __uint_as_float(r.y & 0xffff0000u);
+}
+template <> __device__ __forceinline__ void ld4<half_t>(const half_t* p, float (&o)[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 r = *reinterpret_cast<const h4*>(p);
+  for (int e = 0; e < 4; ++e) o[e] = (float)r[e];
+}
+template <> __device__ __forceinline__ void ld4<float>(const float* p, float (&o)[4]) {
+  const float4 r = *reinterpret_cast<const float4*>(p);
+  o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = r.w;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __restrict__ ids, const T* __restrict__ gy,
+                                                            T* __restrict__ gw, long n, int D, long V, long pad) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char eb_smem[];
+  float* acc = reinterpret_cast<float*>(eb_smem);                       // [EB_ROWS][EB_DCH]
+  int* list = reinterpret_cast<int*>(eb_smem + EB_ROWS * EB_DCH * 4);   // [EB_CAP]
+  int* wcnt = list + EB_CAP;                                            // [4]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const long v0 = (long)blockIdx.x * EB_ROWS;
+  const int d0 = blockIdx.y * EB_DCH;
+  const int dn = min(EB_DCH, D - d0);
+  for (int i = tid; i < EB_ROWS * EB_DCH / 4; i += 256) reinterpret_cast<float4*>(acc)[i] = make_float4(0, 0, 0, 0);
+  int cnt = 0;
+  auto flush = [&]() {   // add the listed gradient rows, in list (= token) order
+    __syncthreads();
+    const int c = tid * 4;
+    if (c < dn) {
+      for (int k = 0; k < cnt; ++k) {
+        const int e = list[k];
+        const long r = e >> 5;
+        float g[4];
+        ld4<T>(gy + r * D + d0 + c, g);
+        float* a = acc + (e & 31) * EB_DCH + c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] += g[q];
+      }
+    }
+    __syncthreads();
+    cnt = 0;
+  };
+  for (long base = 0; base < n; base += 256) {
+    const long r = base + tid;
+    const long id = r < n ? ids[r] : -1;
+    const bool m = id >= v0 && id < v0 + EB_ROWS && id < V && id != pad;
+    const unsigned long long bal = __ballot(m);
+    const int pre = __popcll(bal & ((1ULL << lane) - 1ULL));
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    __syncthreads();
+    int off = cnt, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int cw = wcnt[w];
+      if (w < wid) off += cw;
+      tot += cw;
+    }
+    if (m) list[off + pre] = (int)(r << 5) | (int)(id - v0);
+    cnt += tot;
+    __syncthreads();
+    if (cnt > EB_CAP - 256) flush();
+  }
+  flush();
+  const int c = tid * 4;
+  if (c < dn) {
+    for (int row = 0; row < EB_ROWS; ++row) {
+      const long v = v0 + row;
+      if (v >= V) break;
+      const float* a = acc + row * EB_DCH + c;
+      T* o = gw + v * D + d0 + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Cvt<T>::st(o, q, a[q]);
+    }
+  }
+}
+
 inline int grid_for(long n, int per_block) {
   long g = (n + per_block - 1) / per_block;
   if (g > 256L * 16) g = 256L * 16;   // grid-stride beyond ~16 blocks per CU
@@ -448,6 +540,24 @@ PHA_API int pha_maxpool2d_nhwc_bwd(int dt, const void* gy, const uint8_t* idx, v
   const unsigned grid = (unsigned)std::min((total + 255) / 256, 8192L);
   PHA_DISPATCH_T(dt, T, {
     hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(grid), dim3(256), 0, stream, (const T*)gy, idx, (T*)gx, g);
+  });
+  return (int)hipGetLastError();
+}
+
+// gw [V][D] (T) = embedding gradient of gy [n][D] (T) for ids [n] (int64); padding row pad (or -1)
+PHA_API int pha_embedding_bwd(int dt, const int64_t* ids, const void* gy, void* gw, long n, int D, long V, long pad,
+                              hipStream_t stream) {
+  if (n <= 0 || D <= 0 || V <= 0) return (int)hipErrorInvalidValue;
+  if (D % 4 || n >= (1L << 26)) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((V + EB_ROWS - 1) / EB_ROWS), (unsigned)((D + EB_DCH - 1) / EB_DCH));
+  const size_t lds = (size_t)EB_ROWS * EB_DCH * 4 + EB_CAP * 4 + 16;
+  PHA_DISPATCH_T(dt, T, {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)embedding_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr = true;
+    }
+    hipLaunchKernelGGL(embedding_bwd_kernel<T>, grid, dim3(256), lds, stream, ids, (const T*)gy, (T*)gw, n, D, V, pad);
   });
   return (int)hipGetLastError();
 }

@@ -1,0 +1,492 @@
+// Persistent 256 x 256 x 64 bf16/fp16 MFMA GEMM for gfx950, one wave per SIMD, whose epilogue runs
+// UNDER the next tile's MFMAs. Reference behaviour: the cuBLAS GEMMs behind
+// phi/kernels/impl/matmul_kernel_impl.h:88 (matmul / linear forward and both gradients) and the
+// bias epilogue of fused_gemm_epilogue_op.cu:29.
+//
+//   C[M, N] = sum_k A(m, k) B(k, n) (+ bias[n]),  fp32 accumulate, bf16/fp16 out
+//
+// Why. gemm4w.hip's main loop runs at ~1.6 PF/s, but every tile then stages its 256 x 256 fp32
+// result through LDS and issues a 128 KB store burst while the MFMA pipe idles: ~10 us per tile,
+// 15-25 % of a GPT-sized GEMM (profiles/README.md, round 2 session 3/4). Here each workgroup walks a
+// sequence of tiles as ONE continuous stream of K-tiles (the LDS-DMA prefetch of the next tile's
+// first K-tiles is issued during the current tile's last two, exactly like any other prefetch), and
+// the finished accumulators are written out from registers while the next tile's first k-half
+// multiplies: before MFMA (i, j) first overwrites acc[i][j] (with a zero C operand), the old value is
+// converted to bf16, paired with its neighbour tile through v_permlane16_swap into 16-byte rows, and
+// stored with a bounds-checked buffer store. No LDS staging, no barrier, no idle MFMA pipe.
+//
+// Stores and LDS-DMA share the wave's vmcnt counter (in issue order). The stores of the epilogue
+// phase are the youngest operations when that phase ends, so its wait is vmcnt(#stores): the
+// prefetch it needs has landed, the stores stay in flight.
+//
+// Layouts (template AKO / BKO / OT):
+//   NT  A[m][k],  B^T[n][k]                 forward on the cached W^T, dX = dY W
+//   TN  A[k][m],  B[k][n]                   weight gradients X^T dY
+//   NN  as (W^T X^T)^T: A = W [k][m'] (K-outer), B^T = X [n'][k], transposed store (OT)
+#include "mfma_tile.h"
+#include <type_traits>
+
+namespace pha {
+namespace g4p {
+
+using namespace g256;
+
+enum : int {
+  EPI_BIAS = 1,       // + bias[output column] (fp32)
+  EPI_NOSTORE = 512,  // measurement only: stores dropped by the buffer bounds check (tools/bench_g4p.py)
+  EPI_SKIP = 128,     // measurement only: no epilogue at all (fresh tiles just start at C = 0)
+  EPI_NT = 2048,      // stores with the streaming (non-temporal) cache policy
+  EPI_STAGGER = 4096, // measurement only: workgroup w starts after (w & 7) * ((epi >> 16) & 255) s_sleep(16)
+};
+
+struct Args {
+  const void* a;
+  const void* b;
+  void* c;
+  const float* bias;
+  int M, N, K;
+  int lda, ldb, ldc;
+  int epi;
+  int group_m;
+};
+
+constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
+constexpr int STAGE = 2 * OPB;      // A image, B image
+constexpr int BIAS_OFF = 2 * STAGE; // 4 bias slots of 256 fp32 after the two stages
+constexpr int SMEM = 2 * STAGE + 4 * 1024;
+
+__device__ __forceinline__ unsigned lds_u32(const unsigned char* p) {
+  return (unsigned)(size_t)(__attribute__((address_space(3))) const unsigned char*)p;
+}
+
+// LDS-DMA 16 B per lane: global (sbase + voff) -> LDS m0 + lane * 16
+__device__ __forceinline__ void glds_sv(unsigned voff, const void* sbase, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+// LDS-DMA 4 B per lane (the bias slot)
+__device__ __forceinline__ void glds4(const void* src, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off"
+               :: "v"(src), "s"(m0) : "memory", "m0");
+}
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ unsigned pk(float lo, float hi) {
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, bf2{(__bf16)lo, (__bf16)hi});
+  } else {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, h2{(_Float16)lo, (_Float16)hi});
+  }
+}
+
+// d = a . b (C = 0) written over d's registers (see the fresh-tile phase). The leading s_nop 1 is
+// the VALU-write -> MFMA-operand wait the compiler cannot insert inside an asm statement.
+template <typename T>
+__device__ __forceinline__ void mma0(f32x4& d, const uint4& a, const uint4& b) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u va = __builtin_bit_cast(v4u, a), vb = __builtin_bit_cast(v4u, b);
+  if constexpr (std::is_same<T, bf16_t>::value)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "+a"(d) : "v"(va), "v"(vb));
+  else
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "+a"(d) : "v"(va), "v"(vb));
+}
+
+// tile schedule of one workgroup: round r handles lin = r * G + pos (XCD-bijective pos), lin ->
+// (tm, tn) in GROUP_M-row panels
+struct Sched {
+  int tiles_m, tiles_n, total, G, pos, gm;
+  __device__ __forceinline__ bool valid(int r) const { return r * G + pos < total; }
+  __device__ __forceinline__ void tile(int r, int& tm, int& tn) const {
+    const int lin = r * G + pos;
+    const int group = lin / (gm * tiles_n);
+    const int first_m = group * gm;
+    const int gsize = min(tiles_m - first_m, gm);
+    const int in = lin - group * gm * tiles_n;
+    // wave-uniform by construction; readfirstlane tells the compiler (the integer divisions run
+    // on the VALU), so the DMA bases and store descriptors stay scalar — no waterfall loops
+    tm = __builtin_amdgcn_readfirstlane(first_m + in % gsize);
+    tn = __builtin_amdgcn_readfirstlane(in / gsize);
+  }
+};
+
+template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nk = K >> 6;
+
+  Sched sc;
+  sc.tiles_m = (M + 255) >> 8;
+  sc.tiles_n = (N + 255) >> 8;
+  sc.total = sc.tiles_m * sc.tiles_n;
+  sc.G = gridDim.x;
+  sc.gm = p.group_m;
+  {
+    const int bid = blockIdx.x, G = gridDim.x;
+    const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7;
+    sc.pos = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  }
+  if (!sc.valid(0)) return;
+  if (p.epi & EPI_STAGGER) {
+    const int n = (blockIdx.x & 7) * ((p.epi >> 16) & 255);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(16);
+  }
+
+  // ---- staging cursor: (round rs, k-tile ks); per-lane DMA offsets of the cursor's tile --------
+  unsigned aoff[8], boff[8];
+  const char* abase;
+  const char* bbase;
+  int rs = 0, ks = 0;
+  const size_t astep = AKO ? (size_t)64 * p.lda * 2 : 128, bstep = BKO ? (size_t)64 * p.ldb * 2 : 128;
+  const unsigned lds0 = lds_u32(smem);
+
+  auto set_tile = [&](int r) {   // DMA offsets + bases of round r's tile
+    int tm, tn;
+    sc.tile(r, tm, tn);
+    const int m0 = tm << 8, n0 = tn << 8;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int g = wid * 8 + u;
+#pragma unroll
+      for (int op = 0; op < 2; ++op) {
+        const bool ko = op == 0 ? AKO : BKO;
+        const int dim = op == 0 ? M : N, base = op == 0 ? m0 : n0, ld = op == 0 ? p.lda : p.ldb;
+        unsigned off;
+        if (!ko) {
+          const int row = g * 8 + (lane >> 3);
+          const int grow = min(base + row, dim - 1) - base;
+          off = ((unsigned)grow * (unsigned)ld + (unsigned)(((lane & 7) ^ (row & 7)) * 8)) * 2u;
+        } else {
+          const int half = g >> 4, krow = (g & 15) * 4 + (lane >> 4);
+          const int src = (lane & 15) ^ tn_mask(krow, 256);
+          const int idx = min(half * 128 + src * 8, dim - base - 8);
+          off = ((unsigned)krow * (unsigned)ld + (unsigned)idx) * 2u;
+        }
+        if (op == 0) aoff[u] = off; else boff[u] = off;
+      }
+    }
+    abase = static_cast<const char*>(p.a) + (AKO ? (size_t)m0 * 2 : (size_t)m0 * p.lda * 2);
+    bbase = static_cast<const char*>(p.b) + (BKO ? (size_t)n0 * 2 : (size_t)n0 * p.ldb * 2);
+    if constexpr (BIAS) {   // the tile's 256 output-column biases -> slot r & 3 (wave w: 64 of them)
+      const int c0 = OT ? m0 : n0, No = OT ? M : N;
+      const int col = min(c0 + wid * 64 + lane, No - 1);
+      glds4(p.bias + col, lds0 + BIAS_OFF + (r & 3) * 1024 + wid * 256);
+    }
+  };
+  // the cursor's K-tile goes into LDS buffer st_buf as 16 DMAs per wave, one per MFMA group of a
+  // phase (a burst of them ahead of the MFMAs stalls the pipe: each costs ~60 issue cycles)
+  const char* st_a = nullptr;
+  const char* st_b = nullptr;
+  bool st_on = false;
+  int st_buf = 0;
+  auto stage_begin = [&](int buf) {
+    st_on = sc.valid(rs);
+    st_a = abase + (size_t)ks * astep;
+    st_b = bbase + (size_t)ks * bstep;
+    st_buf = buf;
+  };
+  auto stage_one = [&](int gi) {   // DMA gi (0..15): u = gi >> 1, operand gi & 1
+    if (!st_on) return;
+    const int u = gi >> 1;
+    const unsigned dst = lds0 + st_buf * STAGE + (wid * 8 + u) * 1024 + (gi & 1) * OPB;
+    if (gi & 1) glds_sv(boff[u], st_b, dst);
+    else glds_sv(aoff[u], st_a, dst);
+  };
+  auto stage_end = [&]() {   // advance the cursor; a new tile's offsets + bias DMA
+    if (!st_on) return;
+    if (++ks == nk) {
+      ks = 0;
+      ++rs;
+      if (sc.valid(rs)) set_tile(rs);
+    }
+  };
+
+  const int fr = lane & 15, fk = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  auto readA = [&](int buf, int kh, int i) -> uint4 {
+    const unsigned char* img = smem + buf * STAGE;
+    if constexpr (!AKO) {
+      const int row = wr * 128 + i * 16 + fr;
+      return *reinterpret_cast<const uint4*>(img + row * 128 + (((kh * 4 + fk) ^ (fr & 7)) << 4));
+    } else {
+      return tn_frag<256>(img + wr * 16384, kh * 32 + 8 * fk, i * 16, tq, tp);
+    }
+  };
+  auto readB = [&](int buf, int kh, int j) -> uint4 {
+    const unsigned char* img = smem + buf * STAGE + OPB;
+    if constexpr (!BKO) {
+      const int row = wc * 128 + j * 16 + fr;
+      return *reinterpret_cast<const uint4*>(img + row * 128 + (((kh * 4 + fk) ^ (fr & 7)) << 4));
+    } else {
+      return tn_frag<256>(img + wc * 16384, kh * 32 + 8 * fk, j * 16, tq, tp);
+    }
+  };
+
+  // ---- epilogue geometry (output coordinates; OT swaps the kernel's rows and columns) ----------
+  // Non-OT: acc[i][j][e] = C[wr*128 + i*16 + fr][wc*128 + j*16 + 4fk + e]; tiles j, j+1 pair.
+  // OT:     acc[i][j][e] = C_out[wc*128 + j*16 + fr][wr*128 + i*16 + 4fk + e]; tiles i, i+1 pair.
+  // After the pair swap a lane holds 8 consecutive output columns starting at
+  // (pair base)*16 + (fk & 1) * 16 + (fk >> 1) * 8 of output row (row base) + fr.
+  const int Mo = OT ? N : M, No = OT ? M : N;
+  const int ldc2 = p.ldc * 2;
+  const int wrow = (OT ? wc : wr) * 128;                                  // wave's first output row
+  const int lcol = (OT ? wr : wc) * 128 + (fk & 1) * 16 + (fk >> 1) * 8;   // + pair base * 16
+  const unsigned lane_voff = (unsigned)(fr * ldc2 + lcol * 2);
+  // the tile being written out: output origin (bytes), valid rows / columns from the wave's origin,
+  // bias slot
+  const char* e_base = static_cast<const char*>(p.c);
+  int e_rows = 0, e_cols = 0, e_slot = 0;
+  auto set_epi = [&](int r) {
+    int tm, tn;
+    sc.tile(r, tm, tn);
+    const int r0 = OT ? tn << 8 : tm << 8, c0 = OT ? tm << 8 : tn << 8;
+    e_slot = r & 3;
+    e_base = static_cast<const char*>(p.c) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    // (EPI_NOSTORE, measurement only: zero rows, every store is issued and dropped)
+    e_rows = (p.epi & EPI_NOSTORE) ? 0 : Mo - r0 - wrow;
+    e_cols = No - c0;
+  };
+  // pair (t0, t0 + 1) of the wave's output-row block rb: one 16-B store of the lane's 8 columns.
+  // Bounds: the buffer's base is the block's first row and its size the rows left, so rows past
+  // the output are dropped by the buffer range check; a lane whose 8 columns (multiples of 8,
+  // No % 8 == 0) start past the last column gets an offset past any size. Only the lane's
+  // column offset is a VGPR; row block and pair go to the scalar base / the immediate offset.
+  auto store_pair = [&](const f32x4& x0, const f32x4& x1, int rb, int cb) {
+    // AGPR -> VGPR reads as asm: as plain C++ uses, the register allocator answered the
+    // epilogue's reads by splitting every accumulator's live range into VGPR copies at the tile
+    // boundary (60-150 spilled VGPRs); opaque, it keeps them in place (0 spills). The last MFMA
+    // writing any of these registers is >= 60 MFMAs back (no hazard wait states needed).
+    float v0[4], v1[4];
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v0[0]), "=v"(v0[1]), "=v"(v0[2]), "=v"(v0[3]) : "a"(x0[0]), "a"(x0[1]), "a"(x0[2]), "a"(x0[3]));
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v1[0]), "=v"(v1[1]), "=v"(v1[2]), "=v"(v1[3]) : "a"(x1[0]), "a"(x1[1]), "a"(x1[2]), "a"(x1[3]));
+    if constexpr (BIAS) {   // bias of the lane's pre-swap columns cb*16 + 4fk .. +3 and (cb+1)*16 + ...
+      const unsigned char* bs = smem + BIAS_OFF + e_slot * 1024 + (OT ? wr : wc) * 512 + 16 * fk;
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bs + cb * 64);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bs + cb * 64 + 64);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] += b0[e];
+        v1[e] += b1[e];
+      }
+    }
+    unsigned q00 = pk<T>(v0[0], v0[1]), q01 = pk<T>(v0[2], v0[3]);
+    unsigned q10 = pk<T>(v1[0], v1[1]), q11 = pk<T>(v1[2], v1[3]);
+    // lanes of odd 16-lane rows trade their tile-t0 half for the even rows' tile-(t0+1) half
+    const auto s0 = __builtin_amdgcn_permlane16_swap(q00, q10, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(q01, q11, false, false);
+    q00 = s0[0];
+    q10 = s0[1];
+    q01 = s1[0];
+    q11 = s1[1];
+    // descriptor inputs readfirstlane'd: provably uniform, so the descriptor lives in SGPRs
+    // (no per-store waterfall loop, cdna_hip_programming.md T20)
+    const size_t bp = (size_t)(e_base + (size_t)rb * 16 * ldc2);
+    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes, 0x00020000);
+    const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    if (p.epi & EPI_NT) __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 2);
+    else __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 0);
+  };
+
+  f32x4 acc[8][8];
+  uint4 fa0[8], fb0[8], fa1[8], fb1[8];
+  constexpr int SCHED = AKO ? 0 : 2;   // read placement, as gemm4w's per-layout winners
+
+  // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
+  // into (na, nb). MODE 0: accumulate; 1: fresh tile (C = 0); 2: fresh tile with the previous
+  // tile's accumulators written out right before the MFMA that overwrites them.
+  auto phase = [&](auto rd_c, auto mode_c, auto st_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8],
+                   uint4 (&nb)[8], int rbuf, int rkh) {
+    constexpr bool RD = decltype(rd_c)::value;
+    constexpr int MODE = decltype(mode_c)::value;
+    constexpr bool ST = decltype(st_c)::value;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if constexpr (RD && (SCHED & 2)) {
+        if (s & 1) nb[s >> 1] = readB(rbuf, rkh, s >> 1);
+        else na[s >> 1] = readA(rbuf, rkh, s >> 1);
+      } else if constexpr (RD) {
+        if (s < 8) {
+#pragma unroll
+          for (int r = 2 * s; r < 2 * s + 2; ++r) {
+            if (r == 0) na[0] = readA(rbuf, rkh, 0);
+            else if (r <= 8) nb[r - 1] = readB(rbuf, rkh, r - 1);
+            else na[r - 8] = readA(rbuf, rkh, r - 8);
+          }
+        }
+      }
+      if constexpr (ST) stage_one(s);
+      const int i = s >> 1, jb = (s & 1) * 4;
+      if constexpr (MODE == 2) {
+        if constexpr (!OT) {   // pairs (j, j+1) of row block i
+          store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+          store_pair(acc[i][jb + 2], acc[i][jb + 3], i, jb + 2);
+        } else if ((i & 1) == 0) {   // pairs (i, i+1) of output-row block j
+#pragma unroll
+          for (int q = 0; q < 4; ++q) store_pair(acc[i][jb + q], acc[i + 1][jb + q], jb + q, i);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = jb + q;
+        if constexpr (MODE == 0) {
+          if constexpr (OT) acc[i][j] = Mf<T>::mma(ca[i], cb[j], acc[i][j]);
+          else acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
+        } else {
+          // fresh tile, C = 0, result IN PLACE of the old accumulator: as a builtin with a zero C
+          // the register allocator gives the new value other AGPRs and copies every old
+          // accumulator still waiting for its store into VGPRs (spills); tied "+a" it cannot.
+          // The next reader is the following k-half's MFMA taking it whole as C (no wait states).
+          if constexpr (OT) mma0<T>(acc[i][j], ca[i], cb[j]);
+          else mma0<T>(acc[i][j], cb[j], ca[i]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using yes = std::true_type;
+  using no = std::false_type;
+  using M0 = std::integral_constant<int, 0>;
+  using M1 = std::integral_constant<int, 1>;
+  using M2 = std::integral_constant<int, 2>;
+  // stores one epilogue phase issues per lane: 32 pairs
+  constexpr int NST = 32;
+
+  // ---- prologue ----------------------------------------------------------------------------------
+  set_tile(0);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    stage_begin(b);
+#pragma unroll
+    for (int gi = 0; gi < 16; ++gi) stage_one(gi);
+    stage_end();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa0[i] = readA(0, 0, i);
+    fb0[i] = readB(0, 0, i);
+  }
+
+  // the first epilogue phase has no previous tile: zero rows, its stores are dropped
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int s = 0;   // global K-tile step; buffer s & 1
+  for (int r = 0; sc.valid(r); ++r) {
+    {   // K-tile 0 of tile r: the previous tile is written out under its k-half-0 MFMAs
+      const int buf = s & 1;
+      if constexpr (SKIPEPI) phase(yes{}, M1{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
+      else phase(yes{}, M2{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
+      static_assert(NST == 32, "vmcnt literal");
+      asm volatile("s_waitcnt vmcnt(32)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bar();
+      set_epi(r);   // the next epilogue phase writes this tile
+      stage_begin(buf);
+      phase(yes{}, M0{}, yes{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
+      stage_end();
+      ++s;
+    }
+    for (int k = 1; k < nk; ++k, ++s) {
+      const int buf = s & 1;
+      // phase A: F1 reads of this K-tile | MFMAs on F0 (k-half 0)
+      phase(yes{}, M0{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bar();
+      // phase B: stage the cursor into this buffer, F0 reads of the next K-tile (after the last
+      // K-tile they read a stale buffer, unused) | MFMAs on F1
+      stage_begin(buf);
+      phase(yes{}, M0{}, yes{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
+      stage_end();
+    }
+  }
+  // last tile: stores only
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int jb = 0; jb < 8; jb += 2) {
+      if constexpr (!OT) store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+      else if ((i & 1) == 0) {
+        store_pair(acc[i][jb], acc[i + 1][jb], jb, i);
+        store_pair(acc[i][jb + 1], acc[i + 1][jb + 1], jb + 1, i);
+      }
+    }
+  }
+}
+
+template <typename T, bool BIAS>
+int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
+  if constexpr (std::is_same<T, bf16_t>::value && !BIAS) {   // measurement build (EPI_SKIP)
+    if ((a.epi & EPI_SKIP) && !ako && !bko && !trans) {
+      hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if (!ako && !bko && !trans)
+    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
+  else if (ako && bko && !trans)
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
+  else if (ako && !bko && trans)
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, false, true, BIAS>), dim3(grid), dim3(256), 0, st, a);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+}  // namespace g4p
+}  // namespace pha
+
+using namespace pha;
+
+// C = A . B (+ bias[output column]) on the persistent epilogue-overlapped kernel.
+// Layouts: (a_kouter, b_kouter, trans) = (0,0,0) NT, (1,1,0) TN, (1,0,1) NN as (W^T X^T)^T with the
+// transposed store (C is then [N][ldc]). Requires K % 64 == 0; M, N, lda, ldb, ldc % 8 == 0; 16-B
+// aligned base pointers; K-outer operand dims >= 8; per-panel byte offsets < 2^32; 256 output rows
+// x ldc x 2 bytes < 2^31. grid: workgroups (<= tiles; the caller passes the CU count).
+PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
+                       long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
+                       int group_m, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8)
+    return (int)hipErrorInvalidValue;
+  if ((a_kouter && M < 8) || (b_kouter && N < 8)) return (int)hipErrorInvalidValue;
+  if (M > (1L << 30) || N > (1L << 30) || K > (1L << 30) || lda > (1L << 30) || ldb > (1L << 30))
+    return (int)hipErrorInvalidValue;
+  if ((a_kouter ? 64.0 * lda : 256.0 * lda) * 2 >= 4294967295.0 || (b_kouter ? 64.0 * ldb : 256.0 * ldb) * 2 >= 4294967295.0)
+    return (int)hipErrorInvalidValue;
+  if (256.0 * ldc * 2 >= 2147483647.0) return (int)hipErrorInvalidValue;
+  if (((size_t)a | (size_t)b | (size_t)c) & 15) return (int)hipErrorInvalidValue;
+  if ((epi & g4p::EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
+  const long tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  if (grid <= 0 || grid > tiles) grid = (int)tiles;
+  if (group_m <= 0) group_m = 4;
+  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m};
+  const bool bs = epi & g4p::EPI_BIAS;
+  if (dt == kBF16) return bs ? g4p::launch<bf16_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
+                             : g4p::launch<bf16_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
+  if (dt == kF16) return bs ? g4p::launch<half_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
+                            : g4p::launch<half_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
+  return (int)hipErrorInvalidValue;
+}

@@ -21,6 +21,7 @@ using namespace pha;
 namespace {
 
 constexpr unsigned long long kEmpty = ~0ULL;
+constexpr unsigned long long kTomb = ~0ULL - 1;   // a slot claimed by an insert that found no free row
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
   x ^= x >> 30;
@@ -36,8 +37,9 @@ __device__ __forceinline__ float init_val(unsigned long long key, int j, unsigne
   return (2.f * u - 1.f) * range;
 }
 
-// keys[n] (unique) -> rows[n]; create = 0: missing keys give -1; create = 1: insert (row counter
-// in *next_row, capped at max_rows: overflow gives -2)
+// keys[n] (unique; never ~0 or ~0 - 1, the empty / tombstone markers) -> rows[n]; create = 0:
+// missing keys give -1; create = 1: insert (row counter in *next_row, capped at max_rows: overflow
+// gives -2 and leaves a tombstone)
 __global__ __launch_bounds__(256) void ps_find_insert_kernel(const unsigned long long* __restrict__ keys,
                                                              int* __restrict__ rows_out, long n,
                                                              unsigned long long* __restrict__ tkeys,
@@ -64,7 +66,12 @@ __global__ __launch_bounds__(256) void ps_find_insert_kernel(const unsigned long
       if (prev == kEmpty) {
         const int r = atomicAdd(next_row, 1);
         if (r >= max_rows) {
+          // give the row number back (next_row settles at max_rows) and leave a tombstone: the
+          // slot stays occupied for probing (keys placed past it stay reachable) but matches no
+          // key and is not exported
+          atomicSub(next_row, 1);
           trow[s] = -2;
+          tkeys[s] = kTomb;
           rows_out[i] = -2;
           return;
         }

@@ -31,6 +31,12 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, bc1, bc2, grad_scale;
   int decoupled;
   const float* gscale;   // optional device scalar multiplying every gradient (global-norm clip factor)
+  // optional device scalars for a graph-captured step (replays must not freeze host values): the
+  // learning rate, and beta1^t / beta2^t (the reference's beta1_pow_acc / beta2_pow_acc before
+  // this update) from which the bias corrections are formed
+  const float* lr_dev;
+  const float* pow1;
+  const float* pow2;
 };
 
 template <typename P, typename G>
@@ -39,9 +45,11 @@ __global__ __launch_bounds__(256) void adam_kernel(const TensorMeta* __restrict_
   const TensorMeta mt = metas[ch.x];
   const long start = (long)ch.y * kChunk;
   const long end = min(start + (long)kChunk, mt.n);
-  const float lr = a.lr * mt.lr_ratio;
-  const float sbc2 = sqrtf(a.bc2);
-  const float step = lr * sbc2 / a.bc1;
+  const float lr = (a.lr_dev ? *a.lr_dev : a.lr) * mt.lr_ratio;
+  const float bc1 = a.pow1 ? 1.f - *a.pow1 : a.bc1;
+  const float bc2 = a.pow2 ? 1.f - *a.pow2 : a.bc2;
+  const float sbc2 = sqrtf(bc2);
+  const float step = lr * sbc2 / bc1;
   const float eps_hat = a.eps * sbc2;
   P* p = (P*)mt.p;
   const G* g = (const G*)mt.g;
@@ -164,9 +172,10 @@ PHA_API int pha_tensor_meta_size() { return (int)sizeof(TensorMeta); }
 
 PHA_API int pha_multi_tensor_adam(int pdt, int gdt, const void* metas, const void* chunks, int nchunks, float lr,
                                   float beta1, float beta2, float eps, float bc1, float bc2, float grad_scale,
-                                  int decoupled, const float* gscale, hipStream_t stream) {
+                                  int decoupled, const float* gscale, const float* lr_dev, const float* pow1,
+                                  const float* pow2, hipStream_t stream) {
   if (nchunks <= 0) return 0;
-  AdamArgs a{lr, beta1, beta2, eps, bc1, bc2, grad_scale, decoupled, gscale};
+  AdamArgs a{lr, beta1, beta2, eps, bc1, bc2, grad_scale, decoupled, gscale, lr_dev, pow1, pow2};
   PHA_DISPATCH_T(pdt, P, {
     PHA_DISPATCH_T(gdt, G, {
       hipLaunchKernelGGL((adam_kernel<P, G>), dim3(nchunks), dim3(256), 0, stream, (const TensorMeta*)metas, (const int2*)chunks, a);

@@ -44,7 +44,7 @@ class CUDAGraph:
 
     _next_id = 0
 
-    def __init__(self, place=None, mode="thread_local", pool=None):
+    def __init__(self, place=None, mode="thread_local", pool=None, _stream=None):
         if mode not in ALL_MODES:
             raise ValueError(f"mode must be one of {ALL_MODES}, got {mode!r}")
         if not is_cuda_graph_supported():
@@ -57,6 +57,7 @@ class CUDAGraph:
         self._pool = pool
         self._graph = None
         self._stream = None
+        self._fixed_stream = _stream   # captures that must share one stream (forward + backward)
         self._stream_ctx = None
         self._prev_stream = None
         self.id = CUDAGraph._next_id
@@ -70,7 +71,7 @@ class CUDAGraph:
         self._graph = torch.cuda.CUDAGraph()
         self._graph.enable_debug_mode()   # keeps the graph template for print_to_dot_files
         self._prev_stream = torch.cuda.current_stream(self._device)
-        self._stream = torch.cuda.Stream(device=self._device)
+        self._stream = self._fixed_stream or torch.cuda.Stream(device=self._device)
         self._stream.wait_stream(self._prev_stream)
         self._stream_ctx = torch.cuda.stream(self._stream)
         self._stream_ctx.__enter__()
@@ -149,14 +150,124 @@ def _signature(obj):
     return ("V", repr(obj))
 
 
+def _rebuild(obj, it):
+    """``obj`` with every tensor replaced by the next one of ``it`` (wrapped like the original)"""
+    from ...framework.core import Tensor, _wrap
+    if isinstance(obj, Tensor):
+        return _wrap(next(it))
+    if isinstance(obj, torch.Tensor):
+        return next(it)
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_rebuild(o, it) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _rebuild(obj[k], it) for k in sorted(obj)}
+    return obj
+
+
+class _AutogradGraphs:
+    """Forward and backward of a differentiable call, each captured once as a hipGraph — the
+    reference's ``run_program`` op keeps a forward and a backward program for a wrapped Layer
+    (python/paddle/fluid/dygraph/dygraph_to_static/partial_program.py). Every call replays the
+    forward through an autograd Function whose backward replays the captured backward, so the
+    eager tape around it (``loss.backward()`` of the caller, gradient accumulation into the
+    Layer's parameters) works like an un-graphed call."""
+
+    def __init__(self, fn, args, kwargs, params, mode, pool):
+        ins = _tensors_of((args, kwargs), [])
+        self.static_in = [t.detach().clone().requires_grad_(t.requires_grad) for t in ins]
+        self.params = [p for p in params if p.requires_grad]
+        sargs, skw = _rebuild((args, kwargs), iter(self.static_in))
+        diff = [t for t in self.static_in if t.requires_grad] + self.params
+        stream = torch.cuda.Stream()
+        stream.wait_stream(torch.cuda.current_stream())
+        # warm the autograd path on the capture stream (lazy init, allocator growth)
+        with torch.cuda.stream(stream):
+            outs = _tensors_of(fn(*sargs, **skw), [])
+            req = [o for o in outs if o.requires_grad]
+            if req:
+                torch.autograd.grad(req, diff, [torch.ones_like(o) for o in req], allow_unused=True)
+            del outs, req
+        torch.cuda.current_stream().wait_stream(stream)
+        self.fwd = CUDAGraph(mode=mode, pool=pool, _stream=stream)
+        self.fwd.capture_begin()
+        try:
+            out_obj = fn(*sargs, **skw)
+        finally:
+            self.fwd.capture_end()
+        self.out_obj = out_obj
+        self.static_out = _tensors_of(out_obj, [])
+        self.out_req = [o.requires_grad for o in self.static_out]
+        self.static_gout = [torch.empty_like(o) for o, r in zip(self.static_out, self.out_req) if r]
+        self.bwd = CUDAGraph(mode=mode, pool=self.fwd.pool(), _stream=stream)
+        self.bwd.capture_begin()
+        try:
+            grads = torch.autograd.grad([o for o, r in zip(self.static_out, self.out_req) if r], diff,
+                                        self.static_gout, allow_unused=True)
+        finally:
+            self.bwd.capture_end()
+        self.static_grad = list(grads)
+        self.in_req = [t.requires_grad for t in self.static_in]
+
+    def __call__(self, args, kwargs):
+        ins = _tensors_of((args, kwargs), [])
+        outs = _GraphedCall.apply(self, len(ins), *ins, *self.params)
+        return _rebuild(self.out_obj, iter(outs))
+
+
+class _GraphedCall(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, n_in, *tensors):
+        for dst, src in zip(g.static_in, tensors[:n_in]):
+            if dst.data_ptr() != src.data_ptr():
+                dst.detach().copy_(src)
+        g.fwd.replay()
+        ctx.g, ctx.n_in = g, n_in
+        outs = tuple(o.detach() for o in g.static_out)
+        ctx.mark_non_differentiable(*[o for o, r in zip(outs, g.out_req) if not r])
+        return outs
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        g = ctx.g
+        k = 0
+        for go, r in zip(gouts, g.out_req):
+            if r:
+                if go is None:
+                    g.static_gout[k].zero_()
+                else:
+                    g.static_gout[k].copy_(go)
+                k += 1
+        g.bwd.replay()
+        grads, k = [], 0
+        for r in g.in_req:
+            if r:
+                gr = g.static_grad[k]
+                grads.append(None if gr is None else gr.clone())
+                k += 1
+            else:
+                grads.append(None)
+        for gr in g.static_grad[k:]:
+            grads.append(None if gr is None else gr.clone())
+        return (None, None) + tuple(grads)
+
+
 class GraphedFunction:
     """``wrap_cuda_graph`` result in dygraph mode. Call 1..warmup: eager, on a side stream (lazy
-    initialisation, per-shape GEMM picks and allocator growth happen outside the capture). The
-    next call captures and then replays once, so every call performs the work exactly once; later
-    calls copy the tensor arguments into the captured inputs and replay. Returns the captured
-    outputs (the same tensors every replay)."""
+    initialisation, per-shape GEMM picks and allocator growth happen outside the capture).
 
-    def __init__(self, function, mode="thread_local", memory_pool="default", warmup=1):
+    * A differentiable call (grad enabled and an input or, for a wrapped Layer, a parameter
+      requires grad) captures the forward and the backward as two hipGraphs
+      (:class:`_AutogradGraphs`): the caller backpropagates through the result as through an eager
+      call and the parameters accumulate their gradients.
+    * Anything else — e.g. a whole training step that calls ``backward()`` and the optimizer
+      itself — is captured as one graph: the next call captures and then replays once, so every
+      call performs the work exactly once; later calls copy the tensor arguments into the
+      captured inputs and replay.
+
+    Outputs are the captured tensors (overwritten by the next call), as in the reference."""
+
+    def __init__(self, function, mode="thread_local", memory_pool="default", warmup=1, params=None):
+        self._params = params   # a wrapped Layer's parameters (torch tensors), called lazily
         if mode not in ALL_MODES:
             raise ValueError(f"mode must be one of {ALL_MODES}, got {mode!r}")
         self._fn = function
@@ -177,14 +288,32 @@ class GraphedFunction:
 
     def _first_pool(self):
         for ent in self._entries.values():
-            return ent[0].pool()
+            return ent.fwd.pool() if isinstance(ent, _AutogradGraphs) else ent[0].pool()
         return None
+
+    def _differentiable(self, args, kwargs):
+        if not torch.is_grad_enabled():
+            return False
+        if any(t.requires_grad for t in _tensors_of((args, kwargs), [])):
+            return True
+        return self._params is not None and any(p.requires_grad for p in self._params())
 
     def __call__(self, *args, **kwargs):
         if not is_cuda_graph_supported():
             return self._fn(*args, **kwargs)
-        key = _signature((args, kwargs))
+        diff = self._differentiable(args, kwargs)
+        key = (diff, _signature((args, kwargs)))
         ent = self._entries.get(key)
+        if diff:
+            if ent is None:
+                n = self._calls.get(key, 0)
+                self._calls[key] = n + 1
+                if n < self._warmup:
+                    return self._fn(*args, **kwargs)
+                ent = _AutogradGraphs(self._fn, args, kwargs, self._params() if self._params else [], self._mode,
+                                      self._pool)
+                self._entries[key] = ent
+            return ent(args, kwargs)
         if ent is None:
             n = self._calls.get(key, 0)
             self._calls[key] = n + 1
@@ -213,8 +342,12 @@ class GraphedFunction:
         return out
 
     def reset(self):
-        for g, _, _ in self._entries.values():
-            g.reset()
+        for ent in self._entries.values():
+            if isinstance(ent, _AutogradGraphs):
+                ent.fwd.reset()
+                ent.bwd.reset()
+            else:
+                ent[0].reset()
         self._entries.clear()
         self._calls.clear()
 
@@ -233,7 +366,8 @@ def wrap_cuda_graph(function, mode="thread_local", memory_pool="default", warmup
         return _static_guard(function, mode, memory_pool)
     if isinstance(function, Layer):
         layer = function
-        gf = GraphedFunction(layer.forward, mode, memory_pool, warmup)
+        gf = GraphedFunction(layer.forward, mode, memory_pool, warmup,
+                             params=lambda: [p._t for p in layer.parameters()])
         layer._cuda_graph = gf
         layer.forward = gf
         return layer

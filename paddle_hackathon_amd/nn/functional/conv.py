@@ -102,6 +102,9 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
         pad, pre = _padding(padding, 2, list(w.shape[2:]), st, dl, list(t.shape[1:3]))
         if pre is None and (st == [1, 1] or dl == [1, 1]):
             return _w(_hip_conv2d(t.contiguous(), w, None if bias is None else bias._t, st, pad, dl, groups))
+    if t.is_cuda and n == 2:
+        from ...ops import fallback
+        fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)
     stride = _tup(stride, n)
     dilation = _tup(dilation, n)
@@ -136,6 +139,9 @@ def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
 def _convnd_t(n, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format):
     t = x._t
     w = weight._t
+    if t.is_cuda and n == 2:
+        from ...ops import fallback
+        fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)
     stride = _tup(stride, n)
     dilation = _tup(dilation, n)

@@ -257,6 +257,10 @@ class _Embedding(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         (ids,) = ctx.saved_tensors
+        if _hip.embedding_bwd_supported(gy, ids.numel()):
+            return None, _hip.embedding_bwd(ids, gy, ctx.num, ctx.padding_idx), None
+        from . import fallback
+        fallback.note("embedding_grad", f"{gy.dtype} D={gy.shape[-1]} -> aten")
         gw = torch.ops.aten.embedding_dense_backward(gy, ids, ctx.num, ctx.padding_idx if ctx.padding_idx is not None else -1, False)
         return None, gw, None
 
@@ -264,6 +268,9 @@ class _Embedding(torch.autograd.Function):
 def embedding(ids, weight, padding_idx=None, sparse=False):
     if _use_hip(weight) and weight.is_contiguous() and (weight.shape[1] * weight.element_size()) % 16 == 0 and weight.dtype in (torch.bfloat16, torch.float32, torch.float16):
         return _Embedding.apply(ids.contiguous(), weight, padding_idx)
+    if weight.is_cuda:
+        from . import fallback
+        fallback.note("embedding", f"{weight.dtype} {tuple(weight.shape)} -> torch")
     return TF.embedding(ids, weight, padding_idx)
 
 
@@ -276,6 +283,9 @@ def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=T
     drop = dropout_p if training else 0.0
     if _use_hip(q) and _hip.flash_attn_supported(q, k, v, drop, mask):
         return _hip.flash_attention_any(q, k, v, causal, scale, mask, drop)
+    if q.is_cuda:
+        from . import fallback
+        fallback.note("attention", f"{q.dtype} D={q.shape[-1]} mask={mask is not None} -> torch SDPA")
     qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
     m = mask
     if m is not None and m.dtype != torch.bool:

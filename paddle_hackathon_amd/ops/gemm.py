@@ -35,6 +35,8 @@ def _L():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm4w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P, LG, P, I, P]
         L.pha_gemm4w.restype = c_int
+        L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P]
+        L.pha_gemm4p.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
         L.pha_colsum_finish.restype = c_int
         L._g4w_sig = True
@@ -131,6 +133,42 @@ def gemm(a, b, a_kouter=False, b_kouter=False, bias=None, act=None, aux=None, au
     if colsum:
         res.append(cs)
     return res[0] if len(res) == 1 else tuple(res)
+
+
+def _num_cus(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=False, epi_extra=0, grid=0,
+           group_m=0):
+    """C = op(A) @ op(B) (+ bias[output column]) on the persistent epilogue-overlapped kernel
+    (csrc/kernels/gemm4p.hip). Layouts: NT (False, False), TN (True, True), and with trans_out
+    (True, False) the transposed product C^T [N, M] (``nn_p`` runs x @ W through it)."""
+    assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
+    assert a.stride(1) == 1 and b.stride(1) == 1
+    M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[1], b.shape[0]) if b_kouter else (b.shape[0], b.shape[1])
+    assert Ka == Kb, (a.shape, b.shape, a_kouter, b_kouter)
+    assert (a_kouter, b_kouter, trans_out) in ((False, False, False), (True, True, False), (True, False, True))
+    OM, ON = (N, M) if trans_out else (M, N)
+    c = out if out is not None else torch.empty(OM, ON, dtype=a.dtype, device=a.device)
+    assert c.shape == (OM, ON) and c.stride(1) == 1
+    epi = epi_extra
+    if bias is not None:
+        bias = bias.float().contiguous()
+        assert bias.numel() == ON
+        epi |= EPI_BIAS
+    rc = _L().pha_gemm4p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
+                         int(a_kouter), int(b_kouter), int(trans_out), epi, _ptr(bias), grid or _num_cus(a.device),
+                         group_m, _stream(a))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm4p failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
+    return c
+
+
+def nn_p(a, b, bias=None, **kw):
+    """a [M, K] @ b [K, N] (+ bias) on the persistent kernel as (b^T a^T)^T"""
+    return gemm_p(b, a, True, False, bias=bias, trans_out=True, **kw)
 
 
 def colsum_finish(part, dtype):

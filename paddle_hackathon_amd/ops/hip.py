@@ -41,7 +41,8 @@ def _L():
             "pha_bias_gelu_fwd": [I, P, P, P, LG, I, I, P],
             "pha_bias_gelu_bwd": [I, P, P, P, P, LG, I, I, P],
             "pha_embedding_fwd": [P, P, P, LG, I, LG, P],
-            "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P, P],
+            "pha_embedding_bwd": [I, P, P, P, LG, I, LG, LG, P],
+            "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P, P, P, P, P],
             "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
             "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
             "pha_bn_num_blocks": [LG, I],
@@ -353,6 +354,22 @@ def embedding_fwd(ids, w):
     return out
 
 
+def embedding_bwd(ids, gy, vocab, padding_idx=None):
+    """dW [vocab, D] of an embedding lookup: deterministic (token-order sums, no atomics, no sort)"""
+    ids = ids.reshape(-1).to(torch.int64).contiguous()
+    D = gy.shape[-1]
+    gy2 = gy.reshape(-1, D).contiguous()
+    gw = torch.empty(vocab, D, dtype=gy.dtype, device=gy.device)
+    pad = -1 if padding_idx is None else int(padding_idx) % vocab
+    _check(_L().pha_embedding_bwd(_DT[gy.dtype], _ptr(ids), _ptr(gy2), _ptr(gw), ids.numel(), D, vocab, pad,
+                                  _stream(gy)), "embedding_bwd")
+    return gw
+
+
+def embedding_bwd_supported(gy, n):
+    return gy.dtype in _DT and gy.shape[-1] % 4 == 0 and n < (1 << 26) and n > 0
+
+
 # ----------------------------------------------------------------------------
 # multi-tensor optimizers
 # ----------------------------------------------------------------------------
@@ -460,9 +477,11 @@ def _tables_cached(tag, recs, device):
 
 
 def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, step, weight_decay, decoupled,
-                      lr_ratios, grad_scale, wds=None, gscale_dev=None):
+                      lr_ratios, grad_scale, wds=None, gscale_dev=None, lr_dev=None, pow_dev=None):
     """gscale_dev: optional fp32 device scalar multiplied into every gradient as it is read (the
-    global-norm clip factor — no separate pass over the gradients)."""
+    global-norm clip factor — no separate pass over the gradients). lr_dev / pow_dev: fp32 device
+    scalars (learning rate; (beta1^t, beta2^t) before this update) read by the kernel instead of
+    the host values — what a hipGraph-captured step needs so that replays advance."""
     L = _L()
     dev = params[0].device
     items = []
@@ -482,7 +501,8 @@ def multi_tensor_adam(params, grads, ms, vs, masters, lr, beta1, beta2, eps, ste
         metas, chunks, n = _tables_cached(("adam", pdt, gdt), [t[2] for t in its], dev)
         _check(L.pha_multi_tensor_adam(_DT[pdt], _DT[gdt], _ptr(metas), _ptr(chunks), n, float(lr), float(beta1), float(beta2),
                                        float(eps), float(bc1), float(bc2), float(grad_scale), int(bool(decoupled)),
-                                       _ptr(gscale_dev), stream),
+                                       _ptr(gscale_dev), _ptr(lr_dev), _ptr(None if pow_dev is None else pow_dev[0]),
+                                       _ptr(None if pow_dev is None else pow_dev[1]), stream),
                "multi_tensor_adam")
     _bump([p for p, g in zip(params, grads) if g is not None])
 

@@ -35,6 +35,19 @@ class LRScheduler:
             self.last_lr = self._get_closed_form_lr() if hasattr(self, "_get_closed_form_lr") else self.get_lr()
         if self.verbose:
             print(f"Epoch {self.last_epoch}: {type(self).__name__} set learning rate to {self.last_lr}.")
+        self._push_device_lr()
+
+    # device copies of the current LR that hipGraph-captured optimizer steps read (optimizer
+    # _lr_device): refreshed here, on the host, between replays
+    def _register_device_lr(self, t):
+        import weakref
+        self.__dict__.setdefault("_dev_lrs", []).append(weakref.ref(t))
+
+    def _push_device_lr(self):
+        for r in self.__dict__.get("_dev_lrs", ()):
+            t = r()
+            if t is not None:
+                t.fill_(float(self.last_lr))
 
     def state_keys(self):
         self.keys = ["last_epoch", "last_lr"]
@@ -244,6 +257,7 @@ class ReduceOnPlateau(LRScheduler):
                     self.last_lr = new_lr
                     if self.verbose:
                         print(f"Epoch {self.last_epoch}: ReduceOnPlateau set learning rate to {self.last_lr}.")
+                    self._push_device_lr()
 
     def _is_better(self, current, best):
         if self.mode == "min" and self.threshold_mode == "rel":

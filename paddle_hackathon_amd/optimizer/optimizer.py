@@ -73,6 +73,8 @@ class Optimizer:
         if isinstance(self._learning_rate, LRScheduler):
             raise RuntimeError("optimizer's learning rate can't be LRScheduler when invoke this API")
         self._learning_rate = float(value)
+        for t in self.__dict__.get("_lr_devs", {}).values():   # graph-captured steps read these
+            t.fill_(float(value))
 
     def set_lr_scheduler(self, scheduler):
         self._learning_rate = scheduler
@@ -353,13 +355,26 @@ class Adam(Optimizer):
         groups = {}
         for i, st in enumerate(steps):   # one launch per (update index, device): host-offloaded and
             groups.setdefault((st, params[i].device), []).append(i)   # device parameters may mix
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         for (step, dev), idx in groups.items():
             sel = (lambda xs: [xs[i] for i in idx]) if len(groups) > 1 else (lambda xs: xs)
             if dev.type == "cuda":
                 from ..ops import hip
+                lr_dev = pow_dev = None
+                if not capturing:
+                    self._lr_device(dev, lr)   # exists before any capture (its creation is no graph node)
+                else:
+                    # a hipGraph replays this launch: learning rate and bias corrections come from
+                    # device scalars (the scheduler refreshes the former, the beta-pow accumulators
+                    # advance in-graph), as the reference's adam kernel reads LearningRate /
+                    # Beta1Pow / Beta2Pow tensors
+                    lr_dev = self._lr_device(dev, lr)
+                    b1p, b2p = step_pows[idx[0]]
+                    pow_dev = (b1p._t, b2p._t)
                 hip.multi_tensor_adam(sel(params), sel(grads), sel(m1), sel(m2), sel(masters), lr, self._beta1,
                                       self._beta2, self._epsilon, step, 0.0, self._decoupled, sel(ratios),
-                                      self._grad_scale, sel(wds), gscale_dev=getattr(self, "_gscale_dev", None))
+                                      self._grad_scale, sel(wds), gscale_dev=getattr(self, "_gscale_dev", None),
+                                      lr_dev=lr_dev, pow_dev=pow_dev)
             else:
                 for i in idx:
                     _ops.fused_adam_([params[i]], [grads[i]], [m1[i]], [m2[i]], [masters[i]], lr, self._beta1,
@@ -367,6 +382,18 @@ class Adam(Optimizer):
                                      self._grad_scale)
         torch._foreach_mul_([b[0]._t for b in step_pows], self._beta1)
         torch._foreach_mul_([b[1]._t for b in step_pows], self._beta2)
+
+    def _lr_device(self, dev, lr):
+        """fp32 device scalar holding the learning rate, refreshed by the LR scheduler's step() /
+        set_lr() outside any capture (a replayed graph reads it)"""
+        cache = self.__dict__.setdefault("_lr_devs", {})
+        t = cache.get(dev)
+        if t is None:
+            t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+            cache[dev] = t
+            if isinstance(self._learning_rate, LRScheduler):
+                self._learning_rate._register_device_lr(t)
+        return t
 
     def _param_steps(self, params, pows):
         """1-based update index of every parameter for this step (host counters). A count not seen

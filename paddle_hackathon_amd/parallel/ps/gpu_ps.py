@@ -24,6 +24,7 @@ from ...framework.core import Tensor, _wrap
 __all__ = ["GpuPsTable", "GpuPsEmbedding"]
 
 _EMPTY = -1     # int64 bit pattern of the kernel's ~0 key
+_TOMB = -2      # ~0 - 1: a slot whose insert overflowed the row budget
 
 
 def _mix64_np(x):
@@ -95,6 +96,8 @@ class GpuPsTable:
                 L.pha_ps_gpu_adagrad.restype = c_int
                 L._gps_sig = True
             keys = keys.contiguous()
+            if bool(((keys == _EMPTY) | (keys == _TOMB)).any()):
+                raise ValueError("GPU-PS keys -1 and -2 are reserved (empty / tombstone slot markers)")
             rows = torch.empty(n, dtype=torch.int32, device=self.device)
             rc = L.pha_ps_gpu_find(_ptr(keys), _ptr(rows), n, _ptr(self.keys), _ptr(self.rows), self.capacity,
                                    _ptr(self.next_row), self.max_rows, int(create), _ptr(self.W), _ptr(self.g2),
@@ -196,7 +199,7 @@ class GpuPsTable:
         self._update(keys_in, g_in)
 
     def local_size(self):
-        return int(self.next_row.item()) if self.gpu else len(self._map)
+        return min(int(self.next_row.item()), self.max_rows) if self.gpu else len(self._map)
 
     def size(self):
         n = torch.tensor([self.local_size()], dtype=torch.int64)
@@ -208,7 +211,7 @@ class GpuPsTable:
     def state_dict(self):
         """this rank's shard: {"keys": int64 [n], "values": float32 [n, dim], "g2sum": [n]}"""
         if self.gpu:
-            live = self.keys != _EMPTY
+            live = (self.keys != _EMPTY) & (self.keys != _TOMB) & (self.rows >= 0)
             keys, rows = self.keys[live], self.rows[live].long()
         else:
             keys = torch.tensor(list(self._map.keys()), dtype=torch.int64)

@@ -522,7 +522,10 @@ def _record_reshape(r, y, extra):
     # a helper op in the program itself (the trailing-ones reshape of an axis-broadcast operand)
     fn = _fn("tensor.manipulation.unsqueeze")
     out = Variable(r.prog.global_block(), torch.empty(0, device="meta"))
-    op = OpDesc(f"{fn.__module__}.unsqueeze", fn, (), {"x": y, "axis": [-1 - k for k in range(extra)][::-1]}, out)
+    # positive, ascending axes: unsqueeze inserts them one at a time, so [yr, ..., yr + extra - 1]
+    # appends exactly ``extra`` trailing ones ([-2, -1] would put the first one in front)
+    yr = len(y.shape)
+    op = OpDesc(f"{fn.__module__}.unsqueeze", fn, (), {"x": y, "axis": list(range(yr, yr + extra))}, out)
     out.op = op
     r.prog.global_block().append_op(op)
     return out

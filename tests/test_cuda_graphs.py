@@ -117,3 +117,89 @@ def test_graphed_training_step_matches_eager():
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (le, lg)
     for a, b in zip(pe, pg):
         assert torch.allclose(a, b, atol=1e-2, rtol=1e-2), (a - b).abs().max()
+
+
+@pytest.mark.gpu
+def test_wrapped_layer_backward_matches_eager():
+    """port of the reference's test_cuda_graph_partial_graph.py: a wrapped Layer inside an eager
+    computation, ``func(x * x + 100).mean().backward()`` for 10 steps; the input gradient equals
+    the eager run's with the default, a new and a shared memory pool (dropout left out: a graph's
+    Philox offsets advance differently from eager draws, so masks differ by construction)"""
+    import numpy as np
+    paddle.set_device("gpu:0")
+
+    class SimpleModel(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.linear = paddle.nn.Linear(10, 20)
+            self.relu = paddle.nn.ReLU()
+            self.gelu = paddle.nn.GELU()
+
+        def forward(self, x):
+            return self.gelu(self.relu(self.linear(x)))
+
+    def run(func, graphed, pool="default"):
+        paddle.seed(10)
+        if graphed:
+            func = graphs.wrap_cuda_graph(func, memory_pool=pool)
+        for _ in range(10):
+            x = paddle.randn([3, 10], dtype="float32")
+            x.stop_gradient = False
+            loss = func(x * x + 100).mean()
+            loss.backward()
+            w_grad = func.linear.weight.grad.numpy().copy()
+            func.clear_gradients()
+        return func, x.grad.numpy(), w_grad
+
+    paddle.seed(0)
+    model = SimpleModel()
+    state = {k: v.numpy().copy() for k, v in model.state_dict().items()}
+    _, g1, w1 = run(model, False)
+    for pool in ("default", "new"):
+        m = SimpleModel()
+        m.set_state_dict(state)
+        layer, g2, w2 = run(m, True, pool)
+        np.testing.assert_allclose(g1, g2, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(w1, w2, rtol=1e-6, atol=1e-7)
+    m = SimpleModel()
+    m.set_state_dict(state)
+    _, g3, _ = run(m, True, layer)
+    np.testing.assert_allclose(g1, g3, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_graphed_adamw_step_matches_eager():
+    """AdamW inside a captured step: learning rate (stepped by a scheduler between replays) and
+    bias corrections come from device scalars, so replays track the eager run"""
+    paddle.set_device("gpu:0")
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    xs = [torch.randn(32, 16, device="cuda", generator=gen) for _ in range(6)]
+
+    def run(graphed):
+        paddle.seed(11)
+        net = paddle.nn.Sequential(paddle.nn.Linear(16, 32), paddle.nn.GELU(), paddle.nn.Linear(32, 4))
+        sched = paddle.optimizer.lr.StepDecay(learning_rate=1e-2, step_size=2, gamma=0.5)
+        opt = paddle.optimizer.AdamW(learning_rate=sched, parameters=net.parameters(), weight_decay=0.01)
+        x = paddle.to_tensor(xs[0].clone())
+
+        def step(x):
+            loss = (net(x) ** 2).mean()
+            loss.backward()
+            opt.step()
+            opt.clear_grad(set_to_zero=False)
+            return loss
+        f = graphs.wrap_cuda_graph(step) if graphed else step
+        losses = []
+        for i in range(6):
+            x._t.copy_(xs[i])
+            losses.append(float(f(x)._t.item()))
+            sched.step()
+        torch.cuda.synchronize()
+        return losses, [p._t.float().clone() for p in net.parameters()]
+
+    le, pe = run(False)
+    lg, pg = run(True)
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (le, lg)
+    for a, b in zip(pe, pg):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), (a - b).abs().max()

@@ -223,6 +223,30 @@ def test_reference_style_transformer_ops(tmp_path):
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
 
 
+def test_axis_broadcast_of_a_program_variable(tmp_path):
+    """elementwise_mul(X=[N,C,H,W], Y=[N,C], axis=0) with Y computed in the program (the
+    squeeze-excitation pattern): Y must become [N,C,1,1], not [1,N,C,1]"""
+    desc = pb.ProgramDesc()
+    g = desc.blocks.add()
+    g.idx, g.parent_idx = 0, -1
+    _var(g, "x", [-1, 3, 4, 5])
+    _var(g, "p", [-1, 3, 1, 1])
+    _var(g, "f", [-1, 3])
+    _var(g, "o", [-1, 3, 4, 5])
+    _op(g, "feed", {"X": ["feed"]}, {"Out": ["x"]}, col=0)
+    _op(g, "pool2d", {"X": ["x"]}, {"Out": ["p"]}, pooling_type="avg", ksize=[1, 1], global_pooling=True)
+    _op(g, "flatten_contiguous_range", {"X": ["p"]}, {"Out": ["f"]}, start_axis=1, stop_axis=3)
+    _op(g, "elementwise_mul", {"X": ["x"], "Y": ["f"]}, {"Out": ["o"]}, axis=0)
+    _op(g, "fetch", {"X": ["o"]}, {"Out": ["fetch"]}, col=0)
+    prefix = str(tmp_path / "se")
+    open(prefix + ".pdmodel", "wb").write(desc.SerializeToString())
+    pb.save_combine([], prefix + ".pdiparams")
+    prog, feeds, fetches = paddle.static.load_inference_model(prefix)
+    x = np.random.RandomState(3).randn(2, 3, 4, 5).astype("float32")
+    got, = paddle.static.Executor().run(prog, feed={"x": x}, fetch_list=fetches)
+    np.testing.assert_allclose(got, x * x.mean(axis=(2, 3), keepdims=True), rtol=1e-5, atol=1e-6)
+
+
 def test_static_save_writes_program_desc(static_mode, tmp_path):
     x = paddle.static.data("x", [None, 4], "float32")
     paddle.nn.Linear(4, 2)(x)

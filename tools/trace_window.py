@@ -1,7 +1,11 @@
 """Per-kernel totals over the LAST `ms` milliseconds of a rocprofv3 kernel trace (the timed
 steps), so warm-up / autotuning kernels are excluded. usage: trace_window.py trace.csv ms steps"""
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kernel_classes import classify  # noqa: E402
 
 path, ms, steps = sys.argv[1], float(sys.argv[2]), float(sys.argv[3])
 rows = list(csv.DictReader(open(path)))
@@ -20,11 +24,9 @@ for r in rows:
 print(f"window {ms} ms, kernel busy {busy / 1e6:.2f} ms = {busy / 1e6 / steps:.2f} ms/step")
 cats = {}
 for n, (d, c) in agg.items():
-    k = ("conv(MIOpen/CK)" if ("conv" in n or "igemm" in n or "gemm" in n.lower()) else
-         "batchnorm(MIOpen)" if "BatchNorm" in n else "torch elementwise" if "at::native" in n else
-         "pha" if "pha" in n or "anonymous namespace)::" in n else "other")
+    k = classify(n)
     cats[k] = cats.get(k, 0) + d
 for k, v in sorted(cats.items(), key=lambda x: -x[1]):
-    print(f"  {k:22s} {v / 1e6 / steps:8.2f} ms/step {100 * v / busy:5.1f}%")
+    print(f"  {k:40s} {v / 1e6 / steps:8.2f} ms/step {100 * v / busy:5.1f}%")
 for n, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:30]:
     print(f"{d / 1e6 / steps:8.3f} ms/step {c / steps:6.1f}/step  {n[:120]}")
