@@ -35,8 +35,9 @@ enum : int {
   EPI_BIAS = 1,       // + bias[output column] (fp32)
   EPI_NOSTORE = 512,  // measurement only: stores dropped by the buffer bounds check (tools/bench_g4p.py)
   EPI_SKIP = 128,     // measurement only: no epilogue at all (fresh tiles just start at C = 0)
-  EPI_NT = 2048,      // stores with the streaming (non-temporal) cache policy
   EPI_STAGGER = 4096, // measurement only: workgroup w starts after (w & 7) * ((epi >> 16) & 255) s_sleep(16)
+  EPI_ROUNDS = 8192,  // measurement only: round-robin tile order (lin = r * G + pos) instead of XCD chunks
+  EPI_TEMPORAL = 16384,  // stores with the default cache policy (else non-temporal)
 };
 
 struct Args {
@@ -48,6 +49,8 @@ struct Args {
   int lda, ldb, ldc;
   int epi;
   int group_m;
+  float* ws;    // split-K: fp32 partial slabs [splits][M][N] (C unused)
+  int splits;
 };
 
 constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
@@ -76,6 +79,8 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
 template <typename T>
 __device__ __forceinline__ unsigned pk(float lo, float hi) {
   if constexpr (std::is_same<T, bf16_t>::value) {
@@ -99,13 +104,20 @@ __device__ __forceinline__ void mma0(f32x4& d, const uint4& a, const uint4& b) {
     asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "+a"(d) : "v"(va), "v"(vb));
 }
 
-// tile schedule of one workgroup: round r handles lin = r * G + pos (XCD-bijective pos), lin ->
-// (tm, tn) in GROUP_M-row panels
+// tile schedule of one workgroup. With G % 8 == 0 (G / 8 workgroups per XCD under round-robin
+// placement) every XCD owns a contiguous chunk of the linear tile order and its workgroups walk it
+// together: lin = chunk_start + r * (G / 8) + slot, so the 8 XCDs work on far-apart panels (their
+// HBM / MALL reads spread over the channels) while the 32 CUs of an XCD share panels in its L2.
+// Otherwise lin = r * G + pos. lin -> (tm, tn) in GROUP_M-row panels.
 struct Sched {
-  int tiles_m, tiles_n, total, G, pos, gm;
-  __device__ __forceinline__ bool valid(int r) const { return r * G + pos < total; }
-  __device__ __forceinline__ void tile(int r, int& tm, int& tn) const {
-    const int lin = r * G + pos;
+  int tiles_m, tiles_n, total, G, pos, gm, splits;
+  int c0, c1, step;   // this workgroup's chunk [c0, c1) and stride
+  __device__ __forceinline__ bool valid(int r) const { return c0 + r * step < c1; }
+  // work item of round r: tile (tm, tn) and K slice (the slices of a tile are adjacent items)
+  __device__ __forceinline__ void tile(int r, int& tm, int& tn, int& slice) const {
+    const int item = c0 + r * step;
+    const int lin = item / splits;
+    slice = __builtin_amdgcn_readfirstlane(item - lin * splits);
     const int group = lin / (gm * tiles_n);
     const int first_m = group * gm;
     const int gsize = min(tiles_m - first_m, gm);
@@ -117,25 +129,40 @@ struct Sched {
   }
 };
 
-template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false>
+// SPLIT: the K range of every tile is cut into p.splits slices (separate work items, for problems
+// with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
+// pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
+template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
   const int M = p.M, N = p.N, K = p.K;
-  const int nk = K >> 6;
+  const int nsplit = SPLIT ? p.splits : 1;
+  const int nk = (K >> 6) / nsplit;   // K-tiles per work item
 
   Sched sc;
   sc.tiles_m = (M + 255) >> 8;
   sc.tiles_n = (N + 255) >> 8;
-  sc.total = sc.tiles_m * sc.tiles_n;
+  sc.splits = nsplit;
+  sc.total = sc.tiles_m * sc.tiles_n * nsplit;
   sc.G = gridDim.x;
   sc.gm = p.group_m;
   {
     const int bid = blockIdx.x, G = gridDim.x;
     const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7;
     sc.pos = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (r8 == 0 && !(p.epi & EPI_ROUNDS)) {
+      const int qt = sc.total >> 3, rt = sc.total & 7;
+      sc.c0 = (xcd < rt ? xcd * (qt + 1) : rt * (qt + 1) + (xcd - rt) * qt) + (bid >> 3);
+      sc.c1 = sc.c0 - (bid >> 3) + qt + (xcd < rt ? 1 : 0);
+      sc.step = q8;
+    } else {
+      sc.c0 = sc.pos;
+      sc.c1 = sc.total;
+      sc.step = G;
+    }
   }
   if (!sc.valid(0)) return;
   if (p.epi & EPI_STAGGER) {
@@ -152,8 +179,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const unsigned lds0 = lds_u32(smem);
 
   auto set_tile = [&](int r) {   // DMA offsets + bases of round r's tile
-    int tm, tn;
-    sc.tile(r, tm, tn);
+    int tm, tn, slice;
+    sc.tile(r, tm, tn, slice);
+    const size_t k0 = (size_t)slice * nk * 64;   // first K of the item
     const int m0 = tm << 8, n0 = tn << 8;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -176,9 +204,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (op == 0) aoff[u] = off; else boff[u] = off;
       }
     }
-    abase = static_cast<const char*>(p.a) + (AKO ? (size_t)m0 * 2 : (size_t)m0 * p.lda * 2);
-    bbase = static_cast<const char*>(p.b) + (BKO ? (size_t)n0 * 2 : (size_t)n0 * p.ldb * 2);
-    if constexpr (BIAS) {   // the tile's 256 output-column biases -> slot r & 3 (wave w: 64 of them)
+    abase = static_cast<const char*>(p.a) + (AKO ? (size_t)m0 * 2 + k0 * p.lda * 2 : (size_t)m0 * p.lda * 2 + k0 * 2);
+    bbase = static_cast<const char*>(p.b) + (BKO ? (size_t)n0 * 2 + k0 * p.ldb * 2 : (size_t)n0 * p.ldb * 2 + k0 * 2);
+    if constexpr (BIAS && !SPLIT) {   // the tile's 256 output-column biases -> slot r & 3 (wave w: 64 of them)
       const int c0 = OT ? m0 : n0, No = OT ? M : N;
       const int col = min(c0 + wid * 64 + lane, No - 1);
       glds4(p.bias + col, lds0 + BIAS_OFF + (r & 3) * 1024 + wid * 256);
@@ -190,14 +218,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const char* st_b = nullptr;
   bool st_on = false;
   int st_buf = 0;
+  // Past the last tile the cursor stays on the last K-tile: those DMAs land in a buffer nothing
+  // reads any more (no branch in the MFMA stream); the kernel drains them before it exits.
   auto stage_begin = [&](int buf) {
     st_on = sc.valid(rs);
-    st_a = abase + (size_t)ks * astep;
-    st_b = bbase + (size_t)ks * bstep;
+    st_a = abase + (size_t)(st_on ? ks : nk - 1) * astep;
+    st_b = bbase + (size_t)(st_on ? ks : nk - 1) * bstep;
     st_buf = buf;
   };
   auto stage_one = [&](int gi) {   // DMA gi (0..15): u = gi >> 1, operand gi & 1
-    if (!st_on) return;
     const int u = gi >> 1;
     const unsigned dst = lds0 + st_buf * STAGE + (wid * 8 + u) * 1024 + (gi & 1) * OPB;
     if (gi & 1) glds_sv(boff[u], st_b, dst);
@@ -238,20 +267,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // After the pair swap a lane holds 8 consecutive output columns starting at
   // (pair base)*16 + (fk & 1) * 16 + (fk >> 1) * 8 of output row (row base) + fr.
   const int Mo = OT ? N : M, No = OT ? M : N;
-  const int ldc2 = p.ldc * 2;
+  const int ldc2 = SPLIT ? No * 4 : p.ldc * 2;   // output row bytes (split-K: the fp32 slab)
   const int wrow = (OT ? wc : wr) * 128;                                  // wave's first output row
   const int lcol = (OT ? wr : wc) * 128 + (fk & 1) * 16 + (fk >> 1) * 8;   // + pair base * 16
   const unsigned lane_voff = (unsigned)(fr * ldc2 + lcol * 2);
+  // split-K (non-OT only): a lane's 4 fp32 of tile j sit at columns wc*128 + j*16 + 4fk
+  const int lcol4 = wc * 128 + 4 * fk;
+  const unsigned lane_voff4 = (unsigned)(fr * ldc2 + lcol4 * 4);
   // the tile being written out: output origin (bytes), valid rows / columns from the wave's origin,
   // bias slot
   const char* e_base = static_cast<const char*>(p.c);
   int e_rows = 0, e_cols = 0, e_slot = 0;
   auto set_epi = [&](int r) {
-    int tm, tn;
-    sc.tile(r, tm, tn);
+    int tm, tn, slice;
+    sc.tile(r, tm, tn, slice);
     const int r0 = OT ? tn << 8 : tm << 8, c0 = OT ? tm << 8 : tn << 8;
     e_slot = r & 3;
-    e_base = static_cast<const char*>(p.c) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    if constexpr (SPLIT)
+      e_base = reinterpret_cast<const char*>(p.ws) + (size_t)slice * Mo * No * 4 +
+               ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 4);
+    else
+      e_base = static_cast<const char*>(p.c) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
     // (EPI_NOSTORE, measurement only: zero rows, every store is issued and dropped)
     e_rows = (p.epi & EPI_NOSTORE) ? 0 : Mo - r0 - wrow;
     e_cols = No - c0;
@@ -302,8 +338,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes, 0x00020000);
     const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    if (p.epi & EPI_NT) __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 2);
-    else __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 0);
+    // non-temporal by default (the output is not re-read by this kernel; 3 % faster measured,
+    // profiles/gemm4p_store_ab_r3.log)
+    if (p.epi & EPI_TEMPORAL) __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 2);
+  };
+
+  // split-K: acc tile (rb, cb) of the wave as fp32, one 16-B store per lane
+  auto store_f32 = [&](const f32x4& x, int rb, int cb) {
+    float v[4];
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3]) : "a"(x[0]), "a"(x[1]), "a"(x[2]), "a"(x[3]));
+    const size_t bp = (size_t)(e_base + (size_t)rb * 16 * ldc2);
+    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes, 0x00020000);
+    const unsigned voff = (lcol4 + cb * 16 < e_cols) ? lane_voff4 : 0x80000000u;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f4{v[0], v[1], v[2], v[3]}), rs, voff + cb * 64, 0, 2);
   };
 
   f32x4 acc[8][8];
@@ -335,7 +390,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       if constexpr (ST) stage_one(s);
       const int i = s >> 1, jb = (s & 1) * 4;
-      if constexpr (MODE == 2) {
+      if constexpr (MODE == 2 && SPLIT) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) store_f32(acc[i][jb + q], i, jb + q);
+      } else if constexpr (MODE == 2) {
         if constexpr (!OT) {   // pairs (j, j+1) of row block i
           store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
           store_pair(acc[i][jb + 2], acc[i][jb + 3], i, jb + 2);
@@ -400,7 +458,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if constexpr (SKIPEPI) phase(yes{}, M1{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
       else phase(yes{}, M2{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
       static_assert(NST == 32, "vmcnt literal");
-      asm volatile("s_waitcnt vmcnt(32)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (SPLIT) asm volatile("s_waitcnt vmcnt(63)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(32)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       bar();
       set_epi(r);   // the next epilogue phase writes this tile
@@ -423,12 +482,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       stage_end();
     }
   }
-  // last tile: stores only
+  // last tile: stores only (after the cursor's trailing DMAs have landed)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int jb = 0; jb < 8; jb += 2) {
-      if constexpr (!OT) store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+      if constexpr (SPLIT) {
+        store_f32(acc[i][jb], i, jb);
+        store_f32(acc[i][jb + 1], i, jb + 1);
+      } else if constexpr (!OT) store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
       else if ((i & 1) == 0) {
         store_pair(acc[i][jb], acc[i + 1][jb], jb, i);
         store_pair(acc[i][jb + 1], acc[i + 1][jb + 1], jb + 1, i);
@@ -437,8 +500,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// C[m][n] = sum_s ws[s][m][n] (+ bias[n]), slices summed in order; 8 columns per thread
+template <typename T, bool BIAS>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, T* __restrict__ c,
+                                                            const float* __restrict__ bias, int M, int N, int ldc,
+                                                            int splits) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= (long)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (long)m * N);
+  float acc[8];
+  {
+    const float4 a = *reinterpret_cast<const float4*>(ws + i), b = *reinterpret_cast<const float4*>(ws + i + 4);
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w; acc[4] = b.x; acc[5] = b.y; acc[6] = b.z; acc[7] = b.w;
+  }
+  for (int s = 1; s < splits; ++s) {
+    const float* w = ws + (size_t)s * M * N + i;
+    const float4 a = *reinterpret_cast<const float4*>(w), b = *reinterpret_cast<const float4*>(w + 4);
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w; acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  }
+  if constexpr (BIAS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += bias[n + e];
+  }
+  Vec8<T>::st(c + (long)m * ldc + n, acc);
+}
+
 template <typename T, bool BIAS>
 int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
+  if (a.splits > 1) {   // TN only (weight gradients)
+    if (!(ako && bko && !trans)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+    const long elems = (long)a.M * a.N;
+    hipLaunchKernelGGL((splitk_reduce_kernel<T, BIAS>), dim3((unsigned)((elems / 8 + 255) / 256)), dim3(256), 0, st,
+                       a.ws, static_cast<T*>(a.c), a.bias, a.M, a.N, a.ldc, a.splits);
+    return (int)hipGetLastError();
+  }
   if constexpr (std::is_same<T, bf16_t>::value && !BIAS) {   // measurement build (EPI_SKIP)
     if ((a.epi & EPI_SKIP) && !ako && !bko && !trans) {
       hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
@@ -468,7 +564,7 @@ using namespace pha;
 // x ldc x 2 bytes < 2^31. grid: workgroups (<= tiles; the caller passes the CU count).
 PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
                        long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
-                       int group_m, hipStream_t stream) {
+                       int group_m, float* ws, int splits, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8)
     return (int)hipErrorInvalidValue;
   if ((a_kouter && M < 8) || (b_kouter && N < 8)) return (int)hipErrorInvalidValue;
@@ -479,10 +575,13 @@ PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, lo
   if (256.0 * ldc * 2 >= 2147483647.0) return (int)hipErrorInvalidValue;
   if (((size_t)a | (size_t)b | (size_t)c) & 15) return (int)hipErrorInvalidValue;
   if ((epi & g4p::EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
-  const long tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  if (splits < 1) splits = 1;
+  if (splits > 1 && (!ws || (K / 64) % splits || !a_kouter || !b_kouter || trans || (size_t)ws & 15))
+    return (int)hipErrorInvalidValue;
+  const long tiles = ((M + 255) / 256) * ((N + 255) / 256) * splits;
   if (grid <= 0 || grid > tiles) grid = (int)tiles;
   if (group_m <= 0) group_m = 4;
-  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m};
+  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits};
   const bool bs = epi & g4p::EPI_BIAS;
   if (dt == kBF16) return bs ? g4p::launch<bf16_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                              : g4p::launch<bf16_t, false>(p, a_kouter, b_kouter, trans, grid, stream);

@@ -150,6 +150,19 @@ def _signature(obj):
     return ("V", repr(obj))
 
 
+def _detach_any(obj):
+    from ...framework.core import Tensor, _wrap
+    if isinstance(obj, Tensor):
+        return _wrap(obj._t.detach())
+    if isinstance(obj, torch.Tensor):
+        return obj.detach()
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_detach_any(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _detach_any(v) for k, v in obj.items()}
+    return obj
+
+
 def _rebuild(obj, it):
     """``obj`` with every tensor replaced by the next one of ``it`` (wrapped like the original)"""
     from ...framework.core import Tensor, _wrap
@@ -291,6 +304,11 @@ class GraphedFunction:
             return ent.fwd.pool() if isinstance(ent, _AutogradGraphs) else ent[0].pool()
         return None
 
+    def _side_stream(self):
+        if getattr(self, "_stream", None) is None:
+            self._stream = torch.cuda.Stream()
+        return self._stream
+
     def _differentiable(self, args, kwargs):
         if not torch.is_grad_enabled():
             return False
@@ -318,13 +336,16 @@ class GraphedFunction:
             n = self._calls.get(key, 0)
             self._calls[key] = n + 1
             if n < self._warmup:
-                s = torch.cuda.Stream()
+                # on the stream the capture will use, and the result detached: the warmup's
+                # autograd graph (its AccumulateGrad nodes) must be gone before the capture, or
+                # autograd syncs the capture against the stale nodes' stream
+                s = self._side_stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
                     out = self._fn(*args, **kwargs)
                 torch.cuda.current_stream().wait_stream(s)
-                return out
-            g = CUDAGraph(mode=self._mode, pool=self._pool)
+                return _detach_any(out)
+            g = CUDAGraph(mode=self._mode, pool=self._pool, _stream=self._side_stream())
             g.capture_begin()
             try:
                 out = self._fn(*args, **kwargs)

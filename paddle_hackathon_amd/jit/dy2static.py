@@ -13,6 +13,15 @@ loop_transformer.py:475, return_transformer.py, logical_transformer.py, convert_
     ``names = __pha_jst__.convert_while_loop(cond_fn, body_fn, (current values))``
   * ``for i in range(a, b, s): body``  ->  an index ``while`` loop (then as above)
   * ``a and b`` / ``a or b`` / ``not a`` in tests  ->  ``convert_logical_*`` (tensor-aware, lazy)
+  * ``for x in <seq>`` (tensor, list, tuple, ``enumerate(...)``, ``zip(...)``, any iterable)  ->  an
+    index ``while`` over ``convert_len(seq)`` reading ``convert_getitem(seq, i)``: a Python-length
+    sequence unrolls at trace time, a tensor with a dynamic leading dim becomes a ``while`` op
+    (reference loop_transformer.py:475)
+  * every call ``f(...)``  ->  ``convert_call(f)(...)``: user functions and the ``forward`` of
+    user Layers are converted recursively on first call (cached per code object), framework /
+    library callables pass through (reference convert_call_func.py:113, call_transformer.py:26)
+  * ``print`` / ``len`` / ``assert``  ->  ``convert_print`` / ``convert_len`` / ``convert_assert``
+    (reference print_transformer.py:23, assert_transformer.py, tensor_shape_transformer.py:24)
 
 At run time the ``convert_*`` helpers look at the predicate: a static ``Variable`` (tracing under
 ``jit.to_static``) records ``static.nn.cond`` / ``while_loop`` sub-blocks, so the traced Program
@@ -146,7 +155,122 @@ def convert_numpy(x):
     return x if _is_static_var(x) else x.numpy()
 
 
+def _is_tensorish(x):
+    return isinstance(x, Tensor) or _is_static_var(x)
+
+
+def convert_len(x):
+    """``len(x)``: a Python int whenever the leading dim is known (dygraph tensors, static
+    Variables with a fixed dim 0, Python sequences), else a 1-element int64 shape Variable"""
+    if _is_static_var(x):
+        d = x.shape[0] if len(x.shape) else None
+        if d is not None and d >= 0:
+            return int(d)
+        from .. import tensor as _T
+        return _T.shape(x)[0]
+    if isinstance(x, Tensor):
+        return int(x.shape[0])
+    return len(x)
+
+
+def as_sequence(x):
+    """the iterable of a ``for`` loop, indexable: tensors and sequences as they are, every other
+    iterable (enumerate / zip / generators / dict views) materialised as a list"""
+    if _is_tensorish(x) or isinstance(x, (list, tuple, range, str)):
+        return x
+    return list(x)
+
+
+def convert_getitem(seq, i):
+    if _is_static_var(i) and _is_static_var(seq):
+        from .. import tensor as _T
+        return _T.gather(seq, _T.reshape(i, [1]), axis=0).squeeze(0)
+    if _is_static_var(i):
+        raise ValueError("dy2static: a Python sequence indexed by a tensor-valued loop index (its length "
+                         "must be a Python int)")
+    return seq[i]
+
+
+def convert_print(*args, **kwargs):
+    """``print`` in converted code: static Variables are printed when the program RUNS (a Print op,
+    reference print_transformer.py), everything else right away"""
+    if any(_is_static_var(a) for a in args):
+        from .. import static as _static
+        for a in args:
+            if _is_static_var(a):
+                _static.Print(a)
+            else:
+                print(a, **{k: v for k, v in kwargs.items() if k in ("sep", "end", "file", "flush")})
+        return None
+    return print(*args, **kwargs)
+
+
+def convert_assert(cond, msg=None):
+    """``assert`` in converted code: on a static Variable an op that raises when the program runs
+    with a false condition (reference assert_transformer.py -> Assert op)"""
+    if _is_static_var(cond):
+        from ..framework.dispatch import static_op
+
+        def _check(c):
+            import torch
+            t = torch.as_tensor(c._t if isinstance(c, Tensor) else c)
+            if t.is_meta:   # shape inference while recording
+                return c
+            if not bool(t.all()):
+                raise AssertionError(msg if msg is not None else "dy2static assert failed")
+            return c
+        static_op(_check, "assert")(cond)
+        return None
+    if isinstance(cond, Tensor):
+        cond = bool(cond._t.all())
+    assert cond, msg
+
+
+_PASS_MODULES = ("paddle_hackathon_amd", "torch", "numpy", "builtins", "functools", "itertools", "math",
+                 "collections", "typing", "logging", "inspect", "abc", "copy", "warnings")
+
+
+def _framework_callable(f):
+    mod = getattr(f, "__module__", None) or ""
+    return mod.split(".")[0] in _PASS_MODULES
+
+
+def convert_call(f):
+    """the converted form of a callable met inside converted code (reference convert_call_func.py):
+    user functions / methods are transcribed (cached per code object); a user Layer gets its
+    ``forward`` transcribed in place once (hooks and ``__call__`` unchanged); builtins, classes,
+    framework and library callables, and anything marked ``not_to_static`` pass through"""
+    if getattr(f, "_not_to_static", False) or getattr(f, "__pha_converted__", False):
+        return f
+    from ..nn.layer.layers import Layer
+    if isinstance(f, Layer):
+        if _framework_callable(type(f)):
+            return f
+        fwd = f.forward
+        if not getattr(fwd, "__pha_converted__", False) and not getattr(fwd, "_not_to_static", False):
+            conv = convert_function(fwd)
+            if conv is not fwd:
+                f.__dict__["_pha_original_forward"] = fwd
+                f.forward = conv
+        return f
+    if inspect.ismethod(f):
+        if _framework_callable(f.__func__):
+            return f
+        return convert_function(f)
+    if inspect.isfunction(f):
+        if _framework_callable(f) or f.__name__ == "<lambda>":
+            return f
+        return convert_function(f)
+    return f
+
+
 class _JstNamespace:
+    convert_call = staticmethod(convert_call)
+    convert_len = staticmethod(convert_len)
+    convert_print = staticmethod(convert_print)
+    convert_assert = staticmethod(convert_assert)
+    convert_getitem = staticmethod(convert_getitem)
+    as_sequence = staticmethod(as_sequence)
     UNDEFINED = UNDEFINED
     convert_numpy = staticmethod(convert_numpy)
     ld = staticmethod(ld)
@@ -388,13 +512,31 @@ class _Transformer(ast.NodeTransformer):
         return [cdef, bdef, ast.Expr(value=call)]
 
     # ---- for i in range(...) -------------------------------------------------------------------
+    def _for_sequence(self, node):
+        """``for T in ITER: body``  ->  seq = as_sequence(ITER); index while over convert_len(seq)"""
+        k = self._next()
+        seq, idx, n = f"__pha_seq_{k}", f"__pha_idx_{k}", f"__pha_len_{k}"
+        pre = [ast.Assign(targets=[_name(seq, ast.Store())], value=_call(_jst_attr("as_sequence"), [node.iter])),
+               ast.Assign(targets=[_name(n, ast.Store())], value=_call(_jst_attr("convert_len"), [_name(seq)])),
+               ast.Assign(targets=[_name(idx, ast.Store())], value=ast.Constant(value=0))]
+        incr = ast.Assign(targets=[_name(idx, ast.Store())],
+                          value=ast.BinOp(left=_name(idx), op=ast.Add(), right=ast.Constant(value=1)))
+        test = _call(_jst_attr("range_cond"), [_name(idx), _name(n), ast.Constant(value=1)])
+        get = ast.Assign(targets=[node.target], value=_call(_jst_attr("convert_getitem"), [_name(seq), _name(idx)]))
+        fpre, body, test = self._lower_loop([get] + node.body, test, [incr])
+        loop = ast.While(test=test, body=body, orelse=[])
+        res = self.visit_While(loop)
+        return pre + fpre + (res if isinstance(res, list) else [res])
+
     def visit_For(self, node):
         it = node.iter
-        if not (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"
-                and not it.keywords and 1 <= len(it.args) <= 3 and isinstance(node.target, ast.Name)
-                and not node.orelse):
+        if node.orelse or isinstance(node, ast.AsyncFor) or _contains(node.body, (ast.Return,), stop_at_loops=True):
             self.generic_visit(node)
             return node
+        if not (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"
+                and not it.keywords and 1 <= len(it.args) <= 3 and isinstance(node.target, ast.Name)):
+            node.iter = self.visit(node.iter)
+            return self._for_sequence(node)
         if _contains(node.body, (ast.Return,), stop_at_loops=True):
             self.generic_visit(node)
             return node
@@ -423,7 +565,24 @@ class _Transformer(ast.NodeTransformer):
         f = node.func
         if isinstance(f, ast.Attribute) and f.attr == "numpy" and not node.args and not node.keywords:
             return _call(_jst_attr("convert_numpy"), [f.value])
+        if isinstance(f, ast.Attribute) and isinstance(f.value, ast.Name) and f.value.id == JST:
+            return node   # a helper call this transformer emitted
+        if isinstance(f, ast.Name):
+            if f.id == "print":
+                node.func = _jst_attr("convert_print")
+                return node
+            if f.id == "len" and len(node.args) == 1 and not node.keywords:
+                return _call(_jst_attr("convert_len"), node.args)
+            if f.id in ("super", "locals", "globals", "vars", "eval", "exec", "isinstance", "issubclass",
+                        "range", "enumerate", "zip", "getattr", "setattr", "hasattr", "type", "id"):
+                return node
+        node.func = _call(_jst_attr("convert_call"), [f])
         return node
+
+    def visit_Assert(self, node):
+        self.generic_visit(node)
+        args = [node.test] + ([node.msg] if node.msg is not None else [])
+        return ast.Expr(value=_call(_jst_attr("convert_assert"), args))
 
     def visit_FunctionDef(self, node):
         if node.name.startswith("__pha_"):
@@ -440,6 +599,9 @@ def _transform_source(fn):
     if not isinstance(fdef, (ast.FunctionDef, ast.AsyncFunctionDef)):
         raise TypeError("not a function definition")
     fdef.decorator_list = []
+    for n in ast.walk(fdef):   # zero-argument super() needs the class cell of the original
+        if isinstance(n, ast.Call) and isinstance(n.func, ast.Name) and n.func.id == "super" and not n.args:
+            raise TypeError("uses zero-argument super()")
     _Transformer().visit(fdef)
     ast.fix_missing_locations(tree)
     return tree, fdef.name

@@ -35,7 +35,7 @@ def _L():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm4w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P, LG, P, I, P]
         L.pha_gemm4w.restype = c_int
-        L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P]
+        L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P]
         L.pha_gemm4p.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
         L.pha_colsum_finish.restype = c_int
@@ -140,10 +140,11 @@ def _num_cus(dev):
 
 
 def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=False, epi_extra=0, grid=0,
-           group_m=0):
+           group_m=0, splits=1):
     """C = op(A) @ op(B) (+ bias[output column]) on the persistent epilogue-overlapped kernel
     (csrc/kernels/gemm4p.hip). Layouts: NT (False, False), TN (True, True), and with trans_out
-    (True, False) the transposed product C^T [N, M] (``nn_p`` runs x @ W through it)."""
+    (True, False) the transposed product C^T [N, M] (``nn_p`` runs x @ W through it).
+    splits > 1 (TN only): split-K into fp32 slabs + an in-order reduce (few-tile weight gradients)."""
     assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
     assert a.stride(1) == 1 and b.stride(1) == 1
     M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
@@ -158,9 +159,12 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
         bias = bias.float().contiguous()
         assert bias.numel() == ON
         epi |= EPI_BIAS
+    ws = None
+    if splits > 1:
+        ws = torch.empty(splits * OM * ON, dtype=torch.float32, device=a.device)
     rc = _L().pha_gemm4p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), int(trans_out), epi, _ptr(bias), grid or _num_cus(a.device),
-                         group_m, _stream(a))
+                         group_m, _ptr(ws), splits, _stream(a))
     if rc != 0:
         raise RuntimeError(f"pha_gemm4p failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
     return c

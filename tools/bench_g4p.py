@@ -62,6 +62,16 @@ def check():
                 print(f"check {lay} M={M} N={N} K={K} grid={grid or 'cu'} rel_err={err:.2e} bias_err={errb:.2e}",
                       flush=True)
                 assert err < 1e-2 and errb < 1e-2, (err, errb)
+    # split-K weight gradients (fp32 slabs + in-order reduce), with bias
+    for (M, N, K, sp) in [(2048, 2048, 4096, 4), (264, 520, 1024, 2), (2048, 6144, 2048, 2)]:
+        a, b = r(K, M), r(K, N)
+        bias = torch.randn(N, device="cuda")
+        ref = a.float().t() @ b.float() + bias
+        c = G.gemm_p(a, b, True, True, bias=bias, splits=sp)
+        err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
+        print(f"check tn split-K M={M} N={N} K={K} splits={sp} rel_err={err:.2e}", flush=True)
+        assert err < 1e-2, err
+        assert torch.equal(c, G.gemm_p(a, b, True, True, bias=bias, splits=sp))
     # out-of-place strided output (ldc > N): the columns past N must stay untouched
     a, b = r(520, 256), r(264, 256)
     big = torch.full((520, 512), 7.0, device="cuda", dtype=torch.bfloat16)

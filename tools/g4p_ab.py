@@ -43,8 +43,12 @@ for M, N, K in shapes:
         "g4p": lambda: G.gemm_p(x, wt, out=c),
         "g4p-nostore": lambda: G.gemm_p(x, wt, out=c, epi_extra=512),
         "g4p-noepi": lambda: G.gemm_p(x, wt, out=c, epi_extra=128),
+        "g4p-rounds": lambda: G.gemm_p(x, wt, out=c, epi_extra=8192),
+        "g4p-rounds-noepi": lambda: G.gemm_p(x, wt, out=c, epi_extra=8192 | 128),
+        "g4p-temporal": lambda: G.gemm_p(x, wt, out=c, epi_extra=16384),
+        "g4p-1tile/wg-noepi": lambda: G.gemm_p(x, wt, out=c, epi_extra=128, grid=(M // 256) * (N // 256)),
     }
-    for gm in (1, 2, 8, 16):
+    for gm in (2, 8):
         var[f"g4p-gm{gm}"] = (lambda g: lambda: G.gemm_p(x, wt, out=c, group_m=g))(gm)
     times = {k: [] for k in var}
     for f in var.values():
