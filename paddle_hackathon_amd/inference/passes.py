@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 
 from ..framework.core import Parameter, Tensor, _wrap
+from ..static import program as P
 from ..static.program import OpDesc, Variable, _iter_vars, prune_ops
 from . import fused_ops as FO
 
@@ -161,7 +162,7 @@ class ConstantFoldingPass(Pass):
     def apply_block(self, blk, fetches):
         n = 0
         for op in list(blk.ops):
-            if op.exec is not None or op.fn is None or op.type.startswith("@"):
+            if op.exec is not None or op.fn is None or P.is_train_op(op):
                 continue
             ins = list(_iter_vars((op.args, op.kwargs)))
             tens = [t for t in _iter_tensors_all((op.args, op.kwargs))]

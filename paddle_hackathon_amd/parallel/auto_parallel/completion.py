@@ -16,6 +16,7 @@ partial on m). Ops without a rule run replicated.
 from __future__ import annotations
 
 from ...framework.core import Tensor
+from ...static import program as P
 from ...static.program import Variable, _iter_vars
 
 _PKG = "paddle_hackathon_amd."
@@ -104,7 +105,7 @@ class Completer:
 
     def complete(self, program):
         for op in program.global_block().ops:
-            if op.type.startswith("@") or op.exec is not None:
+            if P.is_train_op(op) or op.exec is not None:
                 continue
             d = self.rule(op)
             self.ops[id(op)] = d

@@ -227,7 +227,7 @@ class Partitioner:
                 self.cur[id(loc)] = list(dm)
                 self.data_dims |= {m for m in dm if m >= 0}
         for op in src_blk.ops:
-            if op.type.startswith("@") or op.exec is not None:
+            if P.is_train_op(op) or op.exec is not None:
                 continue
             self._op(op)
         return self.dst, [self.map.get(id(f), f) for f in fetches]

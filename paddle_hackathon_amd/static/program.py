@@ -239,7 +239,7 @@ class Program:
         blk = p.global_block()
         blk.vars = dict(self.global_block().vars)
         for op in self.global_block().ops:
-            if for_test and op.type.startswith("@"):
+            if for_test and is_train_op(op):
                 continue   # drop backward / optimizer ops
             kwargs = dict(op.kwargs)
             if for_test:
@@ -428,8 +428,20 @@ def _grad_var(block, like, name):
     return v
 
 
+def is_train_op(op):
+    """a backward / loss-grad / optimizer op (not part of an inference program)"""
+    return op.type.startswith("@") or op.attrs.get("op_role") in ("backward", "optimize", "loss")
+
+
 def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None, checkpoints=None,
                     distop_context=None):
+    """per-op backward (static/backward.py)"""
+    from .backward import append_backward as _ab
+    return _ab(loss, parameter_list, no_grad_set, callbacks, checkpoints, distop_context)
+
+
+def _append_backward_opaque(loss, parameter_list=None, no_grad_set=None, callbacks=None, checkpoints=None,
+                            distop_context=None):
     prog = default_main_program()
     blk = prog.global_block()
     params = parameter_list if parameter_list is not None else [p for p in prog.all_parameters() if p.trainable]
@@ -448,6 +460,11 @@ def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None,
 
 
 def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
+    from .backward import gradients as _g
+    return _g(targets, inputs, target_gradients, no_grad_set)
+
+
+def _gradients_opaque(targets, inputs, target_gradients=None, no_grad_set=None):
     prog = default_main_program()
     blk = prog.global_block()
     targets = [targets] if isinstance(targets, Tensor) else list(targets)
@@ -469,6 +486,11 @@ def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
 
 
 def minimize_static(optimizer, loss, parameters=None, no_grad_set=None):
+    from .backward import minimize as _m
+    return _m(optimizer, loss, parameters, no_grad_set)
+
+
+def _minimize_opaque(optimizer, loss, parameters=None, no_grad_set=None):
     prog = default_main_program()
     blk = prog.global_block()
     params = parameters if parameters is not None else [p for p in prog.all_parameters() if p.trainable]
@@ -700,15 +722,64 @@ def run_program(program, feed, fetch_list):
     return res
 
 
+def _cut_inputs(op, env):
+    """A forward op that has a grad op (static/backward.py) reads its non-leaf inputs as fresh
+    autograd leaves (detached views), kept in ``env`` under ("leaf", id(op), id(var)): the grad
+    op's vector-Jacobian product then covers exactly this op's own computation — without the cut,
+    an input that also reaches the op through another input (y = f(x) + x) would be differentiated
+    along both paths here and again in f's grad op."""
+    saved = {}
+    for v in _iter_vars((op.args, op.kwargs)):
+        val = env.get(id(v))
+        if isinstance(val, Tensor) and val._t.requires_grad and val._t.grad_fn is not None and id(v) not in saved:
+            leaf = _wrap(val._t.detach().requires_grad_(True))
+            saved[id(v)] = val
+            env[id(v)] = leaf
+            env[("leaf", id(op), id(v))] = leaf
+    return saved
+
+
+def _grad_env(op, env):
+    """the value environment a grad op reads: its forward op's cut leaves in place of the inputs"""
+    fid = op.attrs.get("_fwd_id")
+    if fid is None:
+        return env
+    ins = op.kwargs.get("ins", ())
+    over = {}
+    for v in _iter_vars(ins):
+        leaf = env.get(("leaf", fid, id(v)))
+        if leaf is not None:
+            over[id(v)] = leaf
+    if not over:
+        return env
+    e2 = dict(env)
+    e2.update(over)
+    return e2
+
+
 def run_block(program, blk, env, free=None):
     """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor);
     ``free``: op index -> Variable ids to drop after that op (eager deletion)"""
+    cut_ids = program.__dict__.get("_cut_ops") or ()
     for i, op in enumerate(blk.ops):
+        saved = _cut_inputs(op, env) if id(op) in cut_ids else None
         if op.exec is not None:
             op.exec(program, env, op)
-        else:
-            out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
+        elif op.attrs.get("no_grad"):   # recompute segments: no autograd state kept in forward
+            with torch.no_grad():
+                out = op.fn(*_subst(op.args, env), **_subst(op.kwargs, env))
+            # the values leave the segment as gradient-requiring leaves: ops after the last
+            # checkpoint build their graph on them and their grad ops reach them
+            for t in _iter_tensors(out if isinstance(out, (list, tuple)) else [out]):
+                if t._t.is_floating_point() and not t._t.requires_grad:
+                    t._t.requires_grad_(True)
             _bind_outputs(op.outputs, out, env)
+        else:
+            e = _grad_env(op, env) if "_fwd_id" in op.attrs else env
+            out = op.fn(*_subst(op.args, e), **_subst(op.kwargs, e))
+            _bind_outputs(op.outputs, out, env)
+        if saved:   # later readers see the original values (and their graph)
+            env.update(saved)
         if free:
             for vid in free.get(i, ()):
                 env.pop(vid, None)
@@ -790,7 +861,7 @@ class CompiledProgram:
         return self
 
     def _run(self, feed, fetch_list):
-        has_opt = any(op.type.startswith("@") for op in self._program.global_block().ops)
+        has_opt = any(is_train_op(op) for op in self._program.global_block().ops)
         if not self._build_strategy.use_hip_graph or has_opt or not torch.cuda.is_available() \
                 or has_control_flow(self._program):   # data-dependent branches cannot be captured
             return run_program(self._program, feed, fetch_list)

@@ -36,7 +36,7 @@ import torch
 from ..framework import core as _core
 from ..framework.core import Parameter, Tensor, _wrap, convert_dtype, dtype_to_str
 from . import proto as pb
-from .program import OpDesc, Program, Variable, _iter_tensors, _iter_vars, _resolve_fn, prune_ops
+from .program import OpDesc, Program, Variable, _iter_tensors, _iter_vars, _resolve_fn, is_train_op, prune_ops
 
 _PKG = "paddle_hackathon_amd."
 
@@ -336,7 +336,7 @@ def program_to_desc(program, feed_vars, fetch_vars):
         if b.idx == 0:
             ops = prune_ops(ops, [v for v in fetch_vars if isinstance(v, Variable)])
         for op in ops:
-            if op.type.startswith("@"):
+            if is_train_op(op):
                 continue   # backward / optimizer steps are not part of a saved program
             w.op(op, blocks[b.idx].ops.add())
             for v in _iter_vars(op.outputs):
