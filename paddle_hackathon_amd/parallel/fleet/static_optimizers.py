@@ -10,11 +10,17 @@ c_broadcast collective ops (paddle/fluid/operators/collective/).
 
 ``minimize(loss)`` in static mode lays the step out as separate ops of the main Program:
 
-    @backward(loss, params) -> grad Variables
-    c_allreduce_coalesced(grads)              (DP: one RCCL call per bucket of <= bucket_mb)
+    <op>_grad ... (one grad op per forward op, static/backward.py; recompute segments when
+                   strategy.recompute gives checkpoints)
+    c_allreduce_start(bucket)                 (DP: inserted right AFTER the last grad op of each
+                                               bucket, async on the RCCL stream: the all-reduce of
+                                               the late layers runs while the early layers' grad
+                                               ops still compute — backward overlap)
   | c_reduce_coalesced(grads, owner)          (sharding: per owner, grads of its parameters)
+    c_allreduce_wait(bucket)                  (before the update)
+    [AMP: check_finite_and_unscale, update_loss_scaling; the update skipped on overflow]
     [gradient merge: accumulate; conditional_block every k steps around the update]
-    @update(params, grads)                    (the inner optimizer on the given gradients)
+    <optimizer>(params, grads)                (the inner optimizer on the given gradients)
     c_broadcast_coalesced(params, owner)      (sharding: owners send their updated slice)
 
 so the communication is visible in the Program (``[op.type for op in prog.global_block().ops]``),
@@ -95,14 +101,47 @@ def c_broadcast_coalesced(xs, root=0, ring_id=0):
     return tuple(xs)
 
 
+_ASYNC = {}   # id(start op) -> (work handle, flat buffer, tensors)
+
+
+class _HostCounter:
+    """a step counter the program carries by reference (the executor copies lists / dicts)"""
+    __slots__ = ("n",)
+
+    def __init__(self):
+        self.n = 0
+
+
+def c_allreduce_start(xs, ring_id=0, scale=1.0, key=0):
+    """launch the sum-all-reduce of a bucket asynchronously (RCCL stream); c_allreduce_wait
+    finishes it. Returns the bucket's tensors unchanged (the wait op produces the reduced ones)."""
+    ts = [x._t.detach() for x in xs]
+    buf = _flat(ts)
+    work = None
+    if tdist.is_available() and tdist.is_initialized():
+        work = tdist.all_reduce(buf, group=_group(ring_id), async_op=True)
+    _ASYNC[key] = (work, buf, ts, scale)
+    return _wrap(torch.zeros(()))
+
+
+def c_allreduce_wait(token, key=0):
+    work, buf, ts, scale = _ASYNC.pop(key)
+    if work is not None:
+        work.wait()
+    if scale != 1.0:
+        buf.mul_(scale)
+    return tuple(_wrap(t) for t in _unflat(buf, ts))
+
+
 def gradient_merge_accumulate(grads, accs, step, k_steps=1, avg=True):
     """acc += g; returns (merged grads, take-update flag); the merged grads are acc (/k) on the
-    k-th step (accumulators reset after use by ``gradient_merge_reset``)"""
+    k-th step (accumulators reset after use by ``gradient_merge_reset``). ``step`` is a host
+    counter (the step count is known on the host: no device read, no sync)."""
     with torch.no_grad():
         for g, a in zip(grads, accs):
             a._t.add_(g._t.to(a._t.dtype))
-        step._t.add_(1)
-        take = bool(int(step._t.item()) % int(k_steps) == 0)
+    step.n += 1
+    take = step.n % int(k_steps) == 0
     merged = tuple(_wrap(a._t / k_steps if avg else a._t.clone()) for a in accs)
     return merged + (_wrap(torch.tensor(take)),)
 
@@ -125,6 +164,21 @@ def _op(blk, fn, kwargs, outs, type_=None):
 
 def _grad_vars(blk, params, suffix="@GRAD"):
     return tuple(P._grad_var(blk, p, p.name + suffix) for p in params)
+
+
+def _buckets_idx(items, idx, bucket_bytes):
+    """``_buckets`` over ``items`` returning the corresponding entries of ``idx``"""
+    out, cur, size = [], [], 0
+    for it, i in zip(items, idx):
+        nb = it._t.numel() * it._t.element_size()
+        if cur and size + nb > bucket_bytes:
+            out.append(cur)
+            cur, size = [], 0
+        cur.append(i)
+        size += nb
+    if cur:
+        out.append(cur)
+    return out
 
 
 def _buckets(items, bucket_bytes):
@@ -172,23 +226,29 @@ class StaticFleetOptimizer:
         sharding = bool(self._cfg("sharding", False)) and self.world > 1
         gm = bool(self._cfg("gradient_merge", False))
         fuse_mb = float((self._cfg("fuse_grad_size_in_MB", 32) or 32))
-        # 1. backward: one op producing every gradient Variable
-        gvars = _grad_vars(blk, params)
-
-        def _backward(loss_t, *ps):
-            gs = torch.autograd.grad(loss_t._t, [p._t for p in ps], allow_unused=True)
-            return tuple(_wrap(g if g is not None else torch.zeros_like(p._t)) for g, p in zip(gs, ps))
-        bwd = _op(blk, _backward, {}, gvars, "@backward")
-        bwd.args = (loss,) + tuple(params)
+        # 1. backward: per-op grad ops (+ recompute segments)
+        from ...static import backward as B
+        ckpts = None
+        if bool(self._cfg("recompute", False)):
+            ckpts = list((self._cfg("recompute_configs", {}) or {}).get("checkpoints", []) or [])
+        pg = B.append_backward(loss, params, no_grad_set, checkpoints=ckpts or None)
+        gvars = tuple(g for _, g in pg)
         grads = list(gvars)
+        # AMP: loss scaling on the grad-op graph (check_finite_and_unscale + update_loss_scaling)
+        self._found_inf = None
+        if bool(self._cfg("amp", False)):
+            from ...static import passes
+            cfg = dict(self._cfg("amp_configs", {}) or {})
+            pg2, self._found_inf, self._amp_state = passes.insert_loss_scaling(
+                prog, loss, list(zip(params, grads)), init_scale=cfg.get("init_loss_scaling", 2.0 ** 15),
+                incr_every_n_steps=cfg.get("incr_every_n_steps", 1000),
+                decr_every_n_nan_or_inf=cfg.get("decr_every_n_nan_or_inf", 2),
+                incr_ratio=cfg.get("incr_ratio", 2.0), decr_ratio=cfg.get("decr_ratio", 0.5),
+                dynamic=cfg.get("use_dynamic_loss_scaling", True))
+            grads = [g for _, g in pg2]
         # 2. gradient communication
         if self.world > 1 and not sharding:
-            new = []
-            for bucket in _buckets(grads, int(fuse_mb * 2 ** 20)):
-                outs = _grad_vars(blk, [g for g in bucket], "@ALLREDUCE")
-                _op(blk, c_allreduce_coalesced, {"xs": tuple(bucket), "ring_id": 0, "scale": 1.0 / self.world}, outs)
-                new += list(outs)
-            grads = new
+            grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20))
         owned = list(range(len(params)))
         if sharding:
             # greedy size-balanced ownership (reference sharding/shard.py)
@@ -217,9 +277,15 @@ class StaticFleetOptimizer:
         own_p = tuple(params[i] for i in owned)
         own_g = tuple(grads[i] for i in owned)
 
+        found_inf = self._found_inf
+
         def _update(*pg):
             n = len(pg) // 2
             ps, gs = pg[:n], pg[n:]
+            if found_inf is not None and len(pg) % 2 == 1:   # AMP overflow: skip this update
+                if bool(pg[-1]._t):
+                    return None
+                ps, gs = pg[:(len(pg) - 1) // 2], pg[(len(pg) - 1) // 2:-1]
             for p, g in zip(ps, gs):
                 p._t.grad = g._t.detach().to(p._t.dtype)
             with P._core_dynamic():
@@ -228,14 +294,15 @@ class StaticFleetOptimizer:
             return None
 
         def append_update():
-            u = _op(prog.current_block(), _update, {}, None, "@update")
-            u.args = own_p + own_g
+            u = _op(prog.current_block(), _update, {}, None, type(opt).__name__.lower())
+            u.args = own_p + own_g + ((found_inf,) if found_inf is not None else ())
+            u.attrs["op_role"] = "optimize"
 
         if gm:
             k = int((self._cfg("gradient_merge_configs", {}) or {}).get("k_steps", 1))
             avg = bool((self._cfg("gradient_merge_configs", {}) or {}).get("avg", True))
             accs = tuple(_wrap(torch.zeros_like(p._t, dtype=torch.float32)) for p in own_p)
-            step = _wrap(torch.zeros((), dtype=torch.int64))
+            step = _HostCounter()
             outs = tuple(P._grad_var(blk, p, p.name + "@MERGED") for p in own_p)
             flag = P.Variable(blk, torch.empty((), dtype=torch.bool, device="meta"))
             blk.vars[flag.name] = flag
@@ -258,7 +325,38 @@ class StaticFleetOptimizer:
                 for bucket in _buckets([params[i] for i in idx], int(fuse_mb * 2 ** 20)):
                     outs = tuple(P.Variable(blk, p._t.to("meta")) for p in bucket)
                     _op(blk, c_broadcast_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": 0}, outs)
-        return [op for op in blk.ops if op.type.startswith("@")], list(zip(params, gvars))
+        return [op for op in blk.ops if P.is_train_op(op)], list(zip(params, gvars))
+
+    def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes):
+        """buckets in gradient-ready order (position of each grad's producing op); each bucket's
+        async all-reduce starts right after its last grad op, and is waited for before the update"""
+        pos = {id(op): i for i, op in enumerate(blk.ops)}
+        ready = sorted(range(len(grads)), key=lambda i: pos.get(id(getattr(grads[i], "op", None)), len(blk.ops)))
+        new = list(grads)
+        inserts, waits = [], []
+        for k, bucket_idx in enumerate(_buckets_idx([grads[i] for i in ready], ready, bucket_bytes)):
+            bucket = tuple(grads[i] for i in bucket_idx)
+            after = max(pos.get(id(getattr(g, "op", None)), len(blk.ops) - 1) for g in bucket)
+            key = id(self) * 1000 + k
+            tok = P.Variable(blk, torch.empty((), device="meta"))
+            blk.vars[tok.name] = tok
+            start = P.OpDesc("c_allreduce_start", c_allreduce_start, (),
+                             {"xs": bucket, "ring_id": 0, "scale": 1.0 / self.world, "key": key}, tok,
+                             attrs={"op_role": "backward", "bucket": k})
+            tok.op = start
+            inserts.append((after, start))
+            outs = _grad_vars(blk, list(bucket), "@ALLREDUCE")
+            wait = P.OpDesc("c_allreduce_wait", c_allreduce_wait, (), {"token": tok, "key": key}, outs,
+                            attrs={"op_role": "backward", "bucket": k})
+            for o in outs:
+                o.op = wait
+            waits.append(wait)
+            for i, o in zip(bucket_idx, outs):
+                new[i] = o
+        for after, op in sorted(inserts, key=lambda t: -t[0]):
+            blk.ops.insert(after + 1, op)
+        blk.ops.extend(waits)
+        return new
 
     def step(self):
         raise RuntimeError("static-mode distributed optimizer: use minimize(loss) and Executor.run")
