@@ -45,7 +45,14 @@ def _args():
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
-    ap.add_argument("--tp", type=int, default=1, help="GPT tensor-parallel degree (dp = gpus / tp)")
+    ap.add_argument("--tp", type=int, default=1, help="GPT tensor-parallel degree (dp = gpus / (tp * pp))")
+    ap.add_argument("--pp", type=int, default=1, help="GPT pipeline-parallel degree (1F1B over RCCL p2p)")
+    ap.add_argument("--micro-batches", type=int, default=None,
+                    help="pipeline: micro-batches per step (default: 2 * pp); the per-GPU batch is cut into them")
+    ap.add_argument("--sharding-stage", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="GPT: group-sharded data parallelism over the gpus / (tp * pp) data ranks (1: optimizer "
+                         "state, 2: + gradients, 3: + parameters); composes with --pp (BASELINE config 5: "
+                         "--model gpt3-13b --pp 2 --sharding-stage 3 --recompute on 8 GPUs)")
     ap.add_argument("--gemm-tuning", default="db", choices=["db", "tune", "off"],
                     help="db: load the in-tree hipBLASLt solution database (TunableOp, no tuning); "
                          "tune: benchmark solutions for new shapes and write the database; off: library heuristics")
@@ -103,40 +110,30 @@ def main():
     if a.model.startswith("bert"):
         return bench_bert(a, paddle, dist, world, rank)
 
-    from paddle_hackathon_amd.models import gpt_config, GPTForPretraining
-    tp = max(1, a.tp)
-    if world % tp:
-        raise SystemExit(f"--tp {tp} must divide the world size {world}")
-    dp = world // tp
-    if world > 1:
-        strategy = dist.fleet.DistributedStrategy()
-        strategy.hybrid_configs = {"dp_degree": dp, "mp_degree": tp, "pp_degree": 1}
-        dist.fleet.init(is_collective=True, strategy=strategy)
-    cfg = gpt_config(a.model, max_position_embeddings=max(2048, a.seq_len), recompute=a.recompute,
-                     tensor_parallel_degree=tp)
-    model = GPTForPretraining(cfg)
-    model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
-    opt = paddle.optimizer.AdamW(learning_rate=1e-4, beta1=0.9, beta2=0.95, weight_decay=0.1,
-                                 parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0),
-                                 multi_precision=True)
-    if world > 1:
-        model = dist.fleet.distributed_model(model)
-        opt = dist.fleet.distributed_optimizer(opt)
-    B, S = a.micro_batch or 16, a.seq_len
+    from paddle_hackathon_amd.models.gpt_train import GPTTrainer, Layout
+    tp, pp = max(1, a.tp), max(1, a.pp)
+    if world % (tp * pp):
+        raise SystemExit(f"--tp {tp} x --pp {pp} must divide the world size {world}")
+    B, S = a.micro_batch or (16 if a.model == "gpt3-1.3b" else 2), a.seq_len
+    lo = Layout(world=world, tp=tp, pp=pp, sharding_stage=a.sharding_stage,
+                micro_batches=(a.micro_batches or 2 * pp) if pp > 1 else 1)
+    if pp > 1 and B % lo.micro_batches:
+        raise SystemExit(f"--micro-batch {B} must be a multiple of --micro-batches {lo.micro_batches}")
+    tr = GPTTrainer(a.model, lo, rank, lr=1e-4, amp=True, clip=1.0,
+                    cfg_overrides={"max_position_embeddings": max(2048, S), "recompute": a.recompute})
+    cfg = tr.cfg
+    model = tr.model
+    dp = lo.data_ranks
     gen = torch.Generator(device="cuda")
-    # tensor-parallel peers must see the same tokens: seed by data-parallel rank
-    gen.manual_seed(rank // tp)
+    # tensor / pipeline peers see the same tokens: seed by data rank
+    gen.manual_seed(tr.data_rank())
     ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (B, S + 1), device="cuda", generator=gen))
     inp, lab = ids[:, :-1], ids[:, 1:]
     inp = paddle.Tensor(inp._t.contiguous())
     lab = paddle.Tensor(lab._t.contiguous())
 
     def step():
-        loss = model(inp, lab)
-        loss.backward()
-        opt.step()
-        opt.clear_grad(set_to_zero=False)
-        return loss
+        return tr.step(inp, lab)
 
     for i in range(a.warmup):
         tw = time.perf_counter()
@@ -164,7 +161,7 @@ def main():
     tokens = B * S * dp * a.steps
     value = tokens / elapsed
     if rank == 0:
-        n_params = sum(p._t.numel() for p in (model._layers if hasattr(model, "_layers") else model).parameters())
+        n_params = tr.n_params
         out = {
             "metric": ("tokens/sec GPT-3-1.3B fleet DP (bf16, whole job)" if a.model == "gpt3-1.3b" else
                        f"tokens/sec {a.model} (bf16, whole job)"),
@@ -173,7 +170,7 @@ def main():
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic (random token ids), random-init weights",
             "config": {"model": "GPT-3-1.3B" if a.model == "gpt3-1.3b" else a.model, "global_batch": B * dp,
-                       "seq_len": S, "parallelism": f"dp{dp}" + (f"_tp{tp}" if tp > 1 else ""), "micro_batch_per_gpu": B,
+                       "seq_len": S, "parallelism": lo.name(), "micro_batch_per_gpu": B,
                        "n_params": n_params,
                        "optimizer": "AdamW fp32-master", "final_loss": round(float(loss.item()), 4),
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)},
@@ -181,7 +178,7 @@ def main():
     if a.model == "gpt3-1.3b" and not a.no_resnet:
         # the second half of BASELINE's metric: ResNet-50 samples/s on the same ranks
         final_loss = float(loss.item())
-        del model, opt, loss, ids, inp, lab, step
+        del model, tr, loss, ids, inp, lab, step
         import gc
         gc.collect()
         torch.cuda.empty_cache()

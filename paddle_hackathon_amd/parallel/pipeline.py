@@ -160,6 +160,11 @@ class PipelineLayer(Layer):
                 dist.broadcast(w._t.data, src=g.ranks[0], group=g.pg)
         return groups
 
+    def shared_parameters(self):
+        """the weights tied across stages (SharedLayerDesc): sharding keeps them replicated, so
+        their gradients stay whole for the cross-stage all-reduce"""
+        return [getattr(self.shared_layers[k], self.shared_weight_attrs[k]) for k in self.shared_layers]
+
     def allreduce_shared_weight_gradients(self):
         for key, g in self._shared_groups.items():
             if key not in self.shared_layers:
@@ -437,7 +442,14 @@ class PipelineParallel(Layer):
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         self._layers.train()
-        loss = self.forward_backward_pipeline(data, scaler)
+        flush = getattr(optimizer, "_flush_grads", None)   # group-sharded stage 1/2 optimizer
+        if flush is not None:
+            # gradients accumulate over the micro-batches; reduce-scatter once at the end
+            with optimizer.no_sync():
+                loss = self.forward_backward_pipeline(data, scaler)
+            flush()
+        else:
+            loss = self.forward_backward_pipeline(data, scaler)
         self._dp_allreduce()
         if scaler is not None:
             scaler.step(optimizer)

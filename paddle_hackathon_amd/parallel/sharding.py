@@ -170,8 +170,8 @@ def _sharded_clip(optimizer, group, replicated=()):
         if clip._check_group is None:
             clip._check_group = _pg(group)
             clip._mp_degree = 1
-    for p in replicated:
-        p.is_firstly_shared = group.rank == 0
+    for p in replicated:   # counted once: first rank of the group (and of any tie it already has)
+        p.is_firstly_shared = getattr(p, "is_firstly_shared", True) is not False and group.rank == 0
 
 
 class GroupShardedOptimizer:
@@ -182,7 +182,7 @@ class GroupShardedOptimizer:
     buckets) instead of stage 1 (persistent flat gradient buffers)."""
 
     def __init__(self, optimizer, group, dp_group=None, grads_sharded=False, buffer_max_size=2 ** 25, offload=False,
-                 hooks=True):
+                 hooks=True, replicate=()):
         self._inner = optimizer
         self._group = group
         self._pg = _pg(group)
@@ -192,7 +192,11 @@ class GroupShardedOptimizer:
         self._grads_sharded = grads_sharded
         self._offload = offload
         self._params = [p for p in optimizer._parameter_list]
-        self._train = [p for p in self._params if not p.stop_gradient]
+        rep_ids = {id(p) for p in replicate}
+        # replicated parameters (e.g. weights tied across pipeline stages): whole gradients,
+        # all-reduced over the group, updated on every rank
+        self._rep = [p for p in self._params if id(p) in rep_ids and not p.stop_gradient]
+        self._train = [p for p in self._params if not p.stop_gradient and id(p) not in rep_ids]
         self._buckets = _make_buckets(self._train, self._n, self._rank, max(int(buffer_max_size), 1))
         self._pbucket = {}
         for b in self._buckets:
@@ -207,9 +211,9 @@ class GroupShardedOptimizer:
         for b in self._buckets:
             pieces += b.build_pieces(offload=offload)
         # the inner optimizer now updates the pieces (its state is this rank's shard)
-        optimizer._param_groups = [{"params": pieces}]
-        optimizer._parameter_list = pieces
-        _sharded_clip(optimizer, group)
+        optimizer._param_groups = [{"params": pieces + self._rep}]
+        optimizer._parameter_list = pieces + self._rep
+        _sharded_clip(optimizer, group, replicated=self._rep)
         self._sync = True
         self._queued = False
         self._handles = []
@@ -271,6 +275,28 @@ class GroupShardedOptimizer:
                 comm_stats["all_reduce"] += 1
             if self._grads_sharded:
                 b.flat_grad = None   # the full gradient bucket is gone after the reduce-scatter
+        self._allreduce_replicated()
+
+    def _allreduce_replicated(self):
+        grads = [p._t.grad for p in self._rep if p._t.grad is not None]
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, group=self._pg)
+        comm_stats["all_reduce"] += 1
+        flat.mul_(1.0 / self._n)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+
+    def _flush_grads(self):
+        """reduce every bucket now (after gradients accumulated under ``no_sync``)"""
+        for b in self._buckets:
+            if b.work is None and (b.flat_grad is not None or not self._grads_sharded):
+                self._launch(b)
+                b.ready = len(b.params)
+        self._finish()
 
     def no_sync(self):
         """accumulate gradients locally (gradient merge): no reduce-scatter until the context exits"""
@@ -319,6 +345,12 @@ class GroupShardedOptimizer:
                 b.bind_grads()   # re-attach views a caller may have dropped
             for _, piece, _, _ in b.pieces:
                 piece._t.grad = None
+        for p in self._rep:
+            if p._t.grad is not None:
+                if set_to_zero:
+                    p._t.grad.zero_()
+                else:
+                    p._t.grad = None
 
     clear_gradients = clear_grad
 
@@ -371,7 +403,7 @@ class GroupShardedStage3(Layer):
     """Parameter + gradient + optimizer-state sharding with layer-ahead all-gather prefetch."""
 
     def __init__(self, layer, optimizer, group=None, sync_buffers=False, segment_size=2 ** 20, offload=False,
-                 sync_comm=False):
+                 sync_comm=False, replicate=()):
         super().__init__()
         self._layer = layer
         self._group = group
@@ -389,8 +421,9 @@ class GroupShardedStage3(Layer):
             own = [p for p in sub._parameters.values() if p is not None and id(p) not in seen]
             for p in own:
                 seen.add(id(p))
-            big = [p for p in own if p._t.numel() >= segment_size]
-            self._replicated += [p for p in own if p._t.numel() < segment_size]
+            rep_ids = {id(p) for p in replicate}
+            big = [p for p in own if p._t.numel() >= segment_size and id(p) not in rep_ids]
+            self._replicated += [p for p in own if p._t.numel() < segment_size or id(p) in rep_ids]
             by_dt = {}
             for p in big:
                 by_dt.setdefault(p._t.dtype, []).append(p)
@@ -693,10 +726,11 @@ class _Stage3Optimizer:
 
 
 def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False, sync_buffers=False,
-                           buffer_max_size=2 ** 25, segment_size=2 ** 20, sync_comm=False):
+                           buffer_max_size=2 ** 25, segment_size=2 ** 20, sync_comm=False, replicate=()):
     """reference: python/paddle/distributed/sharding/group_sharded.py:group_sharded_parallel.
     ``buffer_max_size``: elements per flat bucket (stage 1/2); ``segment_size``: parameters with
-    fewer elements stay replicated (stage 3); ``offload``: host fp32 optimizer state (stage 2/3)."""
+    fewer elements stay replicated (stage 3); ``offload``: host fp32 optimizer state (stage 2/3);
+    ``replicate``: parameters kept whole on every rank (weights tied across pipeline stages)."""
     if group is None:
         if not C.is_initialized():
             C.init_parallel_env()
@@ -706,14 +740,16 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
     if level == "os":
         if offload:
             raise ValueError("offload is supported with sharding levels 'os_g' and 'p_g_os' (as the reference)")
-        opt = GroupShardedOptimizer(optimizer, group, grads_sharded=False, buffer_max_size=buffer_max_size)
+        opt = GroupShardedOptimizer(optimizer, group, grads_sharded=False, buffer_max_size=buffer_max_size,
+                                    replicate=replicate)
         return model, opt, scaler
     if level == "os_g":
         opt = GroupShardedOptimizer(optimizer, group, grads_sharded=True, buffer_max_size=buffer_max_size,
-                                    offload=offload)
+                                    offload=offload, replicate=replicate)
         return GroupShardedStage2(model, opt, group, sync_buffers, buffer_max_size), opt, scaler
     if level == "p_g_os":
-        m = GroupShardedStage3(model, optimizer, group, sync_buffers, segment_size, offload, sync_comm)
+        m = GroupShardedStage3(model, optimizer, group, sync_buffers, segment_size, offload, sync_comm,
+                               replicate=replicate)
         return m, _Stage3Optimizer(optimizer, m), scaler
     raise ValueError(f"unknown sharding level {level}")
 
