@@ -59,9 +59,13 @@ def _args():
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="ResNet-50: replay the whole training step (fwd + bwd + Momentum) as one hipGraph "
-                         "(paddle.device.cuda.graphs.wrap_cuda_graph); auto = on for one rank with >= 2 warmup steps "
-                         "(the eager warmup and the capture stay out of the timed steps)")
+                    help="ResNet-50: replay the whole training step (fwd + bwd incl. the DataParallel RCCL "
+                         "all-reduce buckets + Momentum) as one hipGraph (paddle.device.cuda.graphs.wrap_cuda_graph) "
+                         "at EVERY world size, so the 1 -> 8 GPU curve compares like with like; auto = on with >= 2 "
+                         "warmup steps (the eager warmup and the capture stay out of the timed steps)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="ResNet-50: wrap the model in DataParallel (RCCL reducer) even on one rank — checks the "
+                         "graph-captured all-reduce path on a single GPU")
     ap.add_argument("--no-resnet", action="store_true",
                     help="GPT-3 1.3B run: skip the ResNet-50 half of the headline metric (by default it runs after "
                          "the GPT timing, same --steps/--warmup, and lands in config.resnet50_*)")
@@ -85,6 +89,9 @@ def main():
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus > 1:
         sys.exit(_self_launch(a))
+    # RCCL collectives are captured into the ResNet step's hipGraph: the NCCL watchdog must not
+    # poll events of captured work (torch's documented setting for graphed DDP)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
     if env_world is not None and int(env_world) != a.gpus:
         print(f"[bench] WORLD_SIZE={env_world} disagrees with --gpus {a.gpus}", file=sys.stderr, flush=True)
         sys.exit(2)
@@ -280,7 +287,13 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
     model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
     opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
                                     weight_decay=paddle.regularizer.L2Decay(1e-4), multi_precision=True)
-    if world > 1:
+    if world > 1 or a.force_dp:
+        if world == 1 and not torch.distributed.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29555")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            dist.init_parallel_env()
         model = paddle.DataParallel(model)
     B = (a.micro_batch if a.model.startswith("resnet") else None) or 256
     x = paddle.to_tensor(torch.randn(B, 224, 224, 3, device="cuda").to(torch.bfloat16))
@@ -295,8 +308,7 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
         opt.clear_grad(set_to_zero=False)
         return loss
 
-    graphed = a.graph == "on" or (a.graph == "auto" and world == 1)
-    graphed = graphed and a.warmup >= 2
+    graphed = (a.graph in ("on", "auto")) and a.warmup >= 2
     if graphed:
         # warmup call 1 runs eagerly (GEMM picks, allocator growth), call 2 captures and replays:
         # every timed step is one replay of the full forward + backward + optimizer kernels
@@ -311,7 +323,7 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic ImageNet-shaped, random-init weights",
             "config": {"model": "ResNet-50", "global_batch": B * world, "seq_len": None, "parallelism": f"dp{world}",
                        "layout": "NHWC", "samples_per_sec_per_gpu": round(value / world, 2),
-                       "hip_graph": bool(graphed)}}
+                       "hip_graph": bool(graphed), "data_parallel_reducer": bool(world > 1 or a.force_dp)}}
     if emit and rank == 0:
         print(json.dumps(res), flush=True)
     return res

@@ -802,54 +802,11 @@ def nt_forward_ok(x, w):
             and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype)
 
 
-_gemm_pick = {}
-
-
-def _pick(key, fns):
-    """index of the fastest of ``fns`` (zero-arg launchers of the same product), timed once per
-    key on the real operands; the library candidate is fns[0] (used while capturing a graph or
-    with PHA_GEMM_PICK=0)"""
-    import os
-    ch = _gemm_pick.get(key)
-    if ch is not None:
-        return ch
-    if len(fns) == 1 or os.environ.get("PHA_GEMM_PICK", "1") == "0" or torch.cuda.is_current_stream_capturing():
-        return 0
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best, best_t = 0, float("inf")
-    for i, f in enumerate(fns):
-        f()
-        ev0.record()
-        for _ in range(3):
-            f()
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1)
-        if t < best_t:
-            best, best_t = i, t
-    _gemm_pick[key] = best
-    return best
-
-
 def weight_grad(x2d, gy):
-    """dW = x^T @ dY for a linear layer ([in, out]): hipBLASLt or the own 8-phase kernel in its
-    TN layout (split-K when the [in, out] tile grid is too small to fill the chip), whichever
-    measured faster for this shape"""
-    Tk, Kin = x2d.shape
-    N = gy.shape[1]
+    """dW = x^T @ dY for a linear layer ([in, out]) on the own persistent TN kernel (split-K
+    when the [in, out] tile grid is smaller than the chip) — ops/gemm.py mm_tn"""
     from . import gemm as _g4
-    fns = [lambda: x2d.t().mm(gy)]
-    if _g4._own_ok(x2d, gy) and gy.dtype == x2d.dtype and _g4.supported(Kin, N, Tk, x2d, gy):
-        fns.append(lambda: _g4.gemm(x2d, gy, True, True))   # one-wave-per-SIMD kernel, TN layout
-    if (x2d.dtype in (torch.bfloat16, torch.float16) and gy.dtype == x2d.dtype and Kin % 8 == 0 and N % 8 == 0
-            and Tk % 8 == 0 and x2d.is_contiguous() and gy.is_contiguous() and x2d.numel() < 2 ** 32
-            and gy.numel() < 2 ** 32 and _lib.native_available()):
-        tiles = -(-Kin // 256) * -(-N // 256)
-        fns.append(lambda: gemm8p(x2d, gy, True, True))
-        if tiles < 2 * _num_cus(x2d.device):
-            sp = min(8, max(2, -(-2 * _num_cus(x2d.device) // tiles)))
-            fns.append(lambda: gemm8p(x2d, gy, True, True, splits=sp))
-    return fns[_pick(("dw", x2d.dtype, Tk, Kin, N), fns)]()
+    return _g4.mm_tn(x2d, gy)
 
 
 class LinearNT(torch.autograd.Function):

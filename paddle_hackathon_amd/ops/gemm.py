@@ -71,7 +71,7 @@ def supported(M, N, K, *tensors):
         if not t.is_cuda or t.dtype not in (torch.bfloat16, torch.float16) or t.dim() != 2 or t.stride(1) != 1 \
                 or t.stride(0) % 8:
             return False
-        if t.stride(0) * 256 * 2 >= 2 ** 32:
+        if t.stride(0) * 256 * 2 >= 2 ** 32 or t.data_ptr() % 16:
             return False
     return _lib.native_available()
 
@@ -186,85 +186,76 @@ def colsum_finish(part, dtype):
 
 
 # ----------------------------------------------------------------------------------------------
-# per-shape choice between the library GEMM and the own kernels
+# kernel selection: static and deterministic (same choice on every rank and every run)
 # ----------------------------------------------------------------------------------------------
-_picks = {}
-
-
-def _pick(key, fns):
-    """index of the fastest zero-argument launcher (timed once per key on the real operands;
-    fns[0] while capturing a graph or with PHA_GEMM_PICK=0)"""
-    ch = _picks.get(key)
-    if ch is not None:
-        return ch
-    if len(fns) == 1 or os.environ.get("PHA_GEMM_PICK", "1") == "0" or torch.cuda.is_current_stream_capturing():
-        return 0
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best, best_t = 0, float("inf")
-    for i, f in enumerate(fns):
-        f()
-        ev0.record()
-        for _ in range(3):
-            f()
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1)
-        if t < best_t:
-            best, best_t = i, t
-    _picks[key] = best
-    if os.environ.get("PHA_GEMM_PICK_LOG"):
-        import sys
-        print(f"[gemm-pick] {key}: candidate {best} of {len(fns)} ({'library' if best == 0 else 'own'})",
-              file=sys.stderr, flush=True)
-    return best
+# PHA_GEMM_IMPL: "own" (default) — every supported product on the own kernels (gemm4p: persistent,
+# epilogue under the next tile's MFMAs; split-K for weight gradients with fewer tiles than CUs);
+# "library" — hipBLASLt (A/B measurements); unsupported shapes always go to the library and are
+# counted by ops/fallback.py.
+def _impl():
+    return os.environ.get("PHA_GEMM_IMPL", "own")
 
 
 def _own_ok(*ts):
     return all(t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
-               for t in ts) and _lib.native_available() and os.environ.get("PHA_OWN_GEMM", "1") != "0"
+               for t in ts) and _lib.native_available() and _impl() == "own"
+
+
+def _lib_call(name, shape, fn):
+    if _impl() == "own":
+        from . import fallback
+        fallback.note("matmul", f"{name} {shape} unsupported by the own kernels -> library")
+    return fn()
+
+
+def _splits(M, N, K, dev):
+    """split-K factor for a weight gradient whose tile grid is smaller than the chip: the smallest
+    power of two giving >= one tile per CU that divides the K-tiles"""
+    tiles = -(-M // 256) * -(-N // 256)
+    cus = _num_cus(dev)
+    sp = 1
+    while tiles * sp < cus and (K // 64) % (sp * 2) == 0 and sp < 16:
+        sp *= 2
+    return sp
 
 
 def mm_nt(a, bt):
     """a [M, K] @ bt[N, K]^T"""
-    fns = [lambda: a @ bt.t()]
     M, K = a.shape
     N = bt.shape[0]
     if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
-        fns.append(lambda: gemm(a, bt, False, False))
-    return fns[_pick(("nt", a.dtype, M, N, K), fns)]()
+        return gemm_p(a, bt, False, False)
+    return _lib_call("nt", (M, N, K), lambda: a @ bt.t())
 
 
 def mm_nt_bias(a, bt, bias):
     """a [M, K] @ bt[N, K]^T + bias (bias folded into the own kernel's epilogue)"""
-    fns = [lambda: torch.addmm(bias, a, bt.t())]
     M, K = a.shape
     N = bt.shape[0]
     if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
-        fns.append(lambda: gemm(a, bt, False, False, bias=bias))
-    return fns[_pick(("ntb", a.dtype, M, N, K), fns)]()
+        return gemm_p(a, bt, False, False, bias=bias)
+    return _lib_call("nt+bias", (M, N, K), lambda: torch.addmm(bias, a, bt.t()))
 
 
 def nn(a, b, **epi):
-    """a [M, K] @ b [K, N] (+ epilogue) on the own kernel as (b^T a^T)^T: A = b (K-outer),
-    B^T = a, transposed store"""
+    """a [M, K] @ b [K, N] (+ epilogue) on gemm4w as (b^T a^T)^T: A = b (K-outer), B^T = a,
+    transposed store (the fused GELU / dGELU epilogue builds)"""
     return gemm(b, a, True, False, trans_out=True, **epi)
 
 
 def mm_nn(a, b):
     """a [M, K] @ b [K, N]"""
-    fns = [lambda: a @ b]
     M, K = a.shape
     N = b.shape[1]
     if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
-        fns.append(lambda: nn(a, b))
-    return fns[_pick(("nn", a.dtype, M, N, K), fns)]()
+        return nn_p(a, b)
+    return _lib_call("nn", (M, N, K), lambda: a @ b)
 
 
 def mm_tn(a, b):
-    """a [K, M]^T @ b [K, N] (weight gradients: x^T dY)"""
-    fns = [lambda: a.t() @ b]
+    """a [K, M]^T @ b [K, N] (weight gradients: x^T dY), split-K when the tile grid is small"""
     K, M = a.shape
     N = b.shape[1]
     if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
-        fns.append(lambda: gemm(a, b, True, True))
-    return fns[_pick(("tn", a.dtype, M, N, K), fns)]()
+        return gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device))
+    return _lib_call("tn", (M, N, K), lambda: a.t() @ b)

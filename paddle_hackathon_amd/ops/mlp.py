@@ -6,17 +6,16 @@ Reference behaviour: ``fused_feedforward`` / the fused_gemm_epilogue op
 pre-activation kept as "reserve space", :298 dgelu + bias-grad backward), as used by the GPT
 fleet models.
 
-Two chains compute the same thing; the faster one is picked once per shape by timing both on the
-real operands (``PHA_FUSED_MLP=0`` forces the first):
+Two chains compute the same thing (chain 0 is the default, a static choice — the same on every
+rank; ``PHA_FUSED_MLP=force`` selects chain 1 for A/B measurements):
 
-  0  library fc1 GEMM (NT on the cached W1^T) -> HIP bias+GELU pass; backward: library NT dgrad of
-     fc2 -> HIP dGELU+bias-grad pass
+  0  fc1 GEMM (NT on the cached W1^T, ops/gemm.mm_nt) -> HIP bias+GELU pass; backward: NT dgrad
+     of fc2 -> HIP dGELU+bias-grad pass
   1  own fc1 GEMM (ops/gemm.nn: transposed-store gemm4w) with bias + GELU + stored pre-activation
      in its epilogue; backward: own NT dgrad of fc2 with dGELU against the stored pre-activation
      and the fc1 bias-gradient column sums in its epilogue
 
-Everything else (fc2 forward, both weight gradients, fc1 dgrad) runs on the per-shape library /
-own picks of ops/gemm.py and ops/conv_gemm.py in both chains.
+Everything else (fc2 forward, both weight gradients, fc1 dgrad) runs on ops/gemm.py in both chains.
 """
 from __future__ import annotations
 
@@ -26,9 +25,6 @@ import torch
 
 from . import gemm as G
 from . import hip as _hip
-
-_modes = {}
-
 
 def _eligible(x2d, w1, b1, w2, b2):
     return (x2d.is_cuda and x2d.dtype in (torch.bfloat16, torch.float16)
@@ -61,39 +57,12 @@ def _bwd_gelu(mode, gy, w2, pre, b1):
 
 
 def pick_mode(x2d, w1, b1, w2):
-    M, H = x2d.shape
-    F = w1.shape[1]
-    key = (x2d.dtype, M, H, F)
-    mode = _modes.get(key)
-    if mode is not None:
-        return mode
-    if (os.environ.get("PHA_FUSED_MLP", "1") == "0" or not _own_ok(x2d, w1, w2)
-            or torch.cuda.is_current_stream_capturing()):
-        return 0
-    if os.environ.get("PHA_FUSED_MLP") == "force":   # A/B measurements: the own fused chain always
-        _modes[key] = 1
+    """static: chain 0 (own GEMMs + the HIP bias-GELU / dGELU+bias-grad passes) — measured ahead of
+    the fused-epilogue chain on gfx950 (profiles/gpt3_mlp_chain_pick_ab_r2.log; tanh-GELU at one
+    wave per SIMD cannot hide behind the MFMAs); PHA_FUSED_MLP=force selects chain 1 for A/B"""
+    if os.environ.get("PHA_FUSED_MLP") == "force" and _own_ok(x2d, w1, w2):
         return 1
-    gy = torch.randn(M, H, device=x2d.device, dtype=x2d.dtype)
-    times = []
-    for m in (0, 1):
-        def chain():
-            _, pre = _fwd(m, x2d, w1, b1)
-            _bwd_gelu(m, gy, w2, pre, b1)
-        chain()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        for _ in range(3):
-            chain()
-        ev1.record()
-        ev1.synchronize()
-        times.append(ev0.elapsed_time(ev1))
-    mode = int(times[1] < 0.98 * times[0])   # near-ties stay on chain 0 (timing noise flips them)
-    _modes[key] = mode
-    if os.environ.get("PHA_GEMM_PICK_LOG"):
-        import sys
-        print(f"[mlp-pick] {key}: chain {mode} (lib {times[0]:.3f} ms, own-fused {times[1]:.3f} ms for 3)",
-              file=sys.stderr, flush=True)
-    return mode
+    return 0
 
 
 class FusedMLP(torch.autograd.Function):
