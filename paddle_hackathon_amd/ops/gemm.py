@@ -188,21 +188,32 @@ def colsum_finish(part, dtype):
 # ----------------------------------------------------------------------------------------------
 # kernel selection: static and deterministic (same choice on every rank and every run)
 # ----------------------------------------------------------------------------------------------
-# PHA_GEMM_IMPL: "own" (default) — every supported product on the own kernels (gemm4p: persistent,
-# epilogue under the next tile's MFMAs; split-K for weight gradients with fewer tiles than CUs);
-# "library" — hipBLASLt (A/B measurements); unsupported shapes always go to the library and are
-# counted by ops/fallback.py.
+# PHA_GEMM_IMPL selects per layout, statically (profiles/gemm_paths_r3.log, per GPT-1.3B shape):
+#   "auto" (default) — weight gradients (TN, split-K when the tile grid is smaller than the chip)
+#       and NN products on the own gemm4p kernel, where it beats hipBLASLt by 4-16 %; the NT
+#       forward / dX products on hipBLASLt, which is 3-21 % faster there (long-K NT is latency
+#       bound on gemm4p's two-stage LDS ring);
+#   "own" — every supported product on gemm4p (what the zero-library traces use);
+#   "library" — every product on hipBLASLt.
+# Shapes the own kernel cannot take always go to the library and are counted by ops/fallback.py.
 def _impl():
-    return os.environ.get("PHA_GEMM_IMPL", "own")
+    return os.environ.get("PHA_GEMM_IMPL", "auto")
 
 
-def _own_ok(*ts):
+_AUTO_OWN = ("tn", "nn")
+
+
+def _own_ok(layout, *ts):
+    impl = _impl()
+    if impl == "library" or (impl == "auto" and layout not in _AUTO_OWN):
+        return False
     return all(t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
-               for t in ts) and _lib.native_available() and _impl() == "own"
+               for t in ts) and _lib.native_available()
 
 
-def _lib_call(name, shape, fn):
-    if _impl() == "own":
+def _lib_call(layout, name, shape, fn):
+    impl = _impl()
+    if impl == "own" or (impl == "auto" and layout in _AUTO_OWN):
         from . import fallback
         fallback.note("matmul", f"{name} {shape} unsupported by the own kernels -> library")
     return fn()
@@ -223,18 +234,18 @@ def mm_nt(a, bt):
     """a [M, K] @ bt[N, K]^T"""
     M, K = a.shape
     N = bt.shape[0]
-    if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
+    if _own_ok("nt", a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
         return gemm_p(a, bt, False, False)
-    return _lib_call("nt", (M, N, K), lambda: a @ bt.t())
+    return _lib_call("nt", "nt", (M, N, K), lambda: a @ bt.t())
 
 
 def mm_nt_bias(a, bt, bias):
     """a [M, K] @ bt[N, K]^T + bias (bias folded into the own kernel's epilogue)"""
     M, K = a.shape
     N = bt.shape[0]
-    if _own_ok(a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
+    if _own_ok("nt", a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
         return gemm_p(a, bt, False, False, bias=bias)
-    return _lib_call("nt+bias", (M, N, K), lambda: torch.addmm(bias, a, bt.t()))
+    return _lib_call("nt", "nt+bias", (M, N, K), lambda: torch.addmm(bias, a, bt.t()))
 
 
 def nn(a, b, **epi):
@@ -247,15 +258,15 @@ def mm_nn(a, b):
     """a [M, K] @ b [K, N]"""
     M, K = a.shape
     N = b.shape[1]
-    if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
+    if _own_ok("nn", a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
         return nn_p(a, b)
-    return _lib_call("nn", (M, N, K), lambda: a @ b)
+    return _lib_call("nn", "nn", (M, N, K), lambda: a @ b)
 
 
 def mm_tn(a, b):
     """a [K, M]^T @ b [K, N] (weight gradients: x^T dY), split-K when the tile grid is small"""
     K, M = a.shape
     N = b.shape[1]
-    if _own_ok(a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
+    if _own_ok("tn", a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
         return gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device))
-    return _lib_call("tn", (M, N, K), lambda: a.t() @ b)
+    return _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)

@@ -35,7 +35,7 @@ def _eligible(x2d, w1, b1, w2, b2):
 def _own_ok(x2d, w1, w2):
     M, H = x2d.shape
     F = w1.shape[1]
-    return (G._own_ok(x2d, w1, w2) and G.supported(F, M, H, w1, x2d) and G.supported(M, F, H, x2d, w2))
+    return (G._own_ok("nn", x2d, w1, w2) and G.supported(F, M, H, w1, x2d) and G.supported(M, F, H, x2d, w2))
 
 
 def _fwd(mode, x2d, w1, b1):

@@ -695,6 +695,8 @@ def run_program(program, feed, fetch_list):
         if v.need_grad and t.is_floating_point():
             t = t.detach().requires_grad_(True)
         env[id(v)] = _wrap(t)
+        if getattr(val, "_lod", None):      # fluid LoD tensors keep their sequence offsets
+            env[id(v)]._lod = val._lod
     fetch_ids = set()
     for f in fetch_list or []:
         if isinstance(f, str) and f in blk.vars:
@@ -799,6 +801,13 @@ class Executor:
             scope=None, return_numpy=True, use_program_cache=False, return_merged=True, use_prune=False):
         if program is None:
             program = default_main_program()
+        # fluid py_reader / DataLoader.from_generator attached to the program: a run without an
+        # explicit feed pulls the next batch (EOFException ends the pass)
+        readers = [r for r in program.__dict__.get("_py_readers", ()) if getattr(r, "_it", None) is not None]
+        if readers and not feed:
+            feed = {}
+            for r in readers:
+                feed.update(r._next_feed())
         if isinstance(program, CompiledProgram):
             outs = program._run(feed, fetch_list)
         else:

@@ -1,0 +1,832 @@
+"""``paddle.fluid`` compatibility package: API coverage over the reference's 1.x ``__all__`` lists
+and numpy oracles (written from the op definitions in paddle/fluid/operators/*_op.h and the
+reference's test_*_op.py checks) for the 1.x layer semantics, dygraph training through
+``fluid.dygraph``, and static Programs with 1.x control flow (While / Switch / IfElse /
+StaticRNN / DynamicRNN) run by the Executor."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import paddle_hackathon_amd as paddle
+import paddle_hackathon_amd.fluid as fluid
+from paddle_hackathon_amd.fluid import layers
+
+# ----------------------------------------------------------------------------- API coverage
+# python/paddle/fluid/layers/*.py __all__ (reference)
+LAYERS_ALL = """While Switch increment array_write create_array less_than less_equal greater_than greater_equal equal
+not_equal array_read array_length cond IfElse DynamicRNN StaticRNN reorder_lod_tensor_by_rank Print Assert is_empty
+case switch_case while_loop prior_box density_prior_box multi_box_head bipartite_match target_assign
+detection_output ssd_loss rpn_target_assign retinanet_target_assign sigmoid_focal_loss anchor_generator
+roi_perspective_transform generate_proposal_labels generate_proposals generate_mask_labels iou_similarity box_coder
+polygon_box_transform yolov3_loss yolo_box box_clip multiclass_nms locality_aware_nms matrix_nms
+retinanet_detection_output distribute_fpn_proposals box_decoder_and_assign collect_fpn_proposals Uniform Normal
+Categorical MultivariateNormalDiag data read_file double_buffer py_reader create_py_reader_by_data load
+exponential_decay natural_exp_decay inverse_time_decay polynomial_decay piecewise_decay noam_decay cosine_decay
+linear_lr_warmup center_loss bpr_loss cross_entropy square_error_cost edit_distance warpctc nce hsigmoid
+sampled_softmax_with_cross_entropy softmax_with_cross_entropy rank_loss margin_rank_loss
+sigmoid_cross_entropy_with_logits teacher_student_sigmoid_loss huber_loss kldiv_loss npair_loss mse_loss accuracy
+auc fc embedding linear_chain_crf crf_decoding cos_sim chunk_eval conv2d conv3d softmax pool2d pool3d
+adaptive_pool2d adaptive_pool3d batch_norm inplace_abn instance_norm data_norm conv2d_transpose conv3d_transpose
+reduce_sum reduce_mean reduce_max reduce_min reduce_prod reduce_all reduce_any dropout split ctc_greedy_decoder
+l2_normalize matmul topk transpose im2sequence row_conv multiplex layer_norm group_norm spectral_norm smooth_l1
+one_hot autoincreased_step_counter reshape squeeze unsqueeze lod_reset lod_append lrn pad pad_constant_like
+label_smooth roi_pool roi_align dice_loss image_resize image_resize_short resize_linear resize_bilinear
+resize_trilinear resize_nearest gather gather_nd scatter scatter_nd_add scatter_nd random_crop mean_iou relu selu
+log crop crop_tensor elu relu6 pow stanh hard_sigmoid swish prelu brelu leaky_relu soft_relu flatten stack pad2d
+unstack unique unique_with_counts expand expand_as scale elementwise_add elementwise_div elementwise_sub
+elementwise_mul elementwise_max elementwise_min elementwise_pow elementwise_mod elementwise_floordiv
+uniform_random_batch_size_like gaussian_random sampling_id gaussian_random_batch_size_like sum slice strided_slice
+shape rank size logical_and logical_or logical_xor logical_not clip clip_by_norm mean mul maxout space_to_depth
+affine_grid affine_channel similarity_focus hash grid_sampler log_loss add_position_encoding
+bilinear_tensor_product merge_selected_rows get_tensor_from_selected_rows shuffle_channel temporal_shift py_func
+psroi_pool prroi_pool pixel_shuffle fsp_matrix continuous_value_model where sign deformable_conv unfold
+deformable_roi_pooling filter_by_instag shard_index hard_swish mish gather_tree uniform_random unbind softshrink
+hard_shrink cumsum thresholded_relu gelu erf RNNCell GRUCell LSTMCell Decoder BeamSearchDecoder rnn birnn
+dynamic_decode DecodeHelper TrainingHelper GreedyEmbeddingHelper SampleEmbeddingHelper BasicDecoder dynamic_lstm
+dynamic_lstmp dynamic_gru gru_unit lstm_unit lstm beam_search beam_search_decode sequence_conv sequence_softmax
+sequence_pool sequence_concat sequence_first_step sequence_last_step sequence_slice sequence_expand
+sequence_expand_as sequence_pad sequence_unpad sequence_reshape sequence_scatter sequence_enumerate sequence_mask
+sequence_reverse create_tensor create_parameter create_global_var cast tensor_array_to_tensor concat sums assign
+fill_constant_batch_size_like fill_constant argmin argmax argsort ones zeros reverse has_inf has_nan isfinite range
+linspace zeros_like ones_like diag eye triu sigmoid silu logsigmoid tanh_shrink softplus softsign tanh exp expm1
+atan sqrt rsqrt abs ceil floor cos tan acos sin sinh asin cosh round reciprocal square lgamma acosh asinh atanh exp_
+sqrt_ rsqrt_ ceil_ floor_ round_ reciprocal_""".split()
+
+DYGRAPH_ALL = """no_grad no_grad_ grad guard enable_dygraph disable_dygraph enabled to_variable Conv2D Conv3D Pool2D
+Linear BatchNorm Dropout Embedding GRUUnit InstanceNorm LayerNorm NCE PRelu BilinearTensorProduct Conv2DTranspose
+Conv3DTranspose GroupNorm SpectralNorm TreeConv Flatten Layer Sequential ParameterList LayerList save_dygraph
+load_dygraph NoamDecay PiecewiseDecay NaturalExpDecay ExponentialDecay InverseTimeDecay PolynomialDecay CosineDecay
+LinearLrWarmup ReduceLROnPlateau StepDecay MultiStepDecay LambdaDecay TracedLayer declarative
+dygraph_to_static_func set_code_level set_verbosity save load not_to_static prepare_context ParallelEnv
+DataParallel LSTMCell GRUCell TranslatedLayer""".split()
+
+MODULE_ALL = {
+    "": """Program default_startup_program default_main_program program_guard name_scope cuda_places cpu_places
+        cuda_pinned_places in_dygraph_mode is_compiled_with_cuda is_compiled_with_rocm Variable require_version
+        device_guard set_flags get_flags Executor global_scope scope_guard create_lod_tensor
+        create_random_int_lodtensor CompiledProgram ExecutionStrategy BuildStrategy append_backward gradients io
+        initializer embedding one_hot layers contrib data dygraph enable_dygraph disable_dygraph enable_imperative
+        disable_imperative transpiler nets optimizer backward regularizer LoDTensor LoDTensorArray CPUPlace
+        CUDAPlace CUDAPinnedPlace Tensor ParamAttr WeightNormParamAttr DataFeeder clip profiler unique_name Scope
+        install_check save load ParallelExecutor DistributeTranspiler""",
+    "io": """save_vars save_params save_persistables load_vars load_params load_persistables save_inference_model
+        load_inference_model batch save load load_program_state set_program_state get_program_parameter
+        get_program_persistable_vars PyReader DataLoader""",
+    "optimizer": """SGD Momentum Adagrad Adam Adamax Dpsgd DecayedAdagrad Ftrl SGDOptimizer MomentumOptimizer
+        AdagradOptimizer AdamOptimizer AdamaxOptimizer DpsgdOptimizer DecayedAdagradOptimizer RMSPropOptimizer
+        FtrlOptimizer Adadelta AdadeltaOptimizer ModelAverage LarsMomentum LarsMomentumOptimizer LambOptimizer
+        ExponentialMovingAverage PipelineOptimizer LookaheadOptimizer RecomputeOptimizer""",
+    "initializer": """Constant Uniform Normal TruncatedNormal Xavier Bilinear MSRA ConstantInitializer
+        UniformInitializer NormalInitializer TruncatedNormalInitializer XavierInitializer BilinearInitializer
+        MSRAInitializer NumpyArrayInitializer set_global_initializer""",
+    "regularizer": "L1Decay L2Decay L1DecayRegularizer L2DecayRegularizer",
+    "clip": "set_gradient_clip ErrorClipByValue ClipGradByValue ClipGradByNorm ClipGradByGlobalNorm",
+    "metrics": "MetricBase CompositeMetric Precision Recall Accuracy ChunkEvaluator EditDistance DetectionMAP Auc",
+    "nets": "simple_img_conv_pool sequence_conv_pool glu scaled_dot_product_attention img_conv_group",
+    "profiler": "cuda_profiler reset_profiler profiler start_profiler stop_profiler",
+    "unique_name": "generate switch guard",
+    "compiler": "CompiledProgram ExecutionStrategy BuildStrategy IpuCompiledProgram IpuStrategy",
+    "lod_tensor": "create_lod_tensor create_random_int_lodtensor",
+    "core": "LoDTensor LoDTensorArray Scope CPUPlace CUDAPlace EOFException VarDesc",
+    "reader": "PyReader DataLoader default_collate_fn",
+    "average": "WeightedAverage",
+    "evaluator": "ChunkEvaluator EditDistance DetectionMAP",
+    "input": "one_hot embedding",
+    "backward": "append_backward gradients",
+    "executor": "Executor global_scope scope_guard",
+}
+
+
+def test_layers_api_coverage():
+    missing = [n for n in LAYERS_ALL if not callable(getattr(layers, n, None))]
+    assert not missing, missing
+    assert set(LAYERS_ALL) <= set(layers.__all__)
+
+
+def test_dygraph_api_coverage():
+    missing = [n for n in DYGRAPH_ALL if getattr(fluid.dygraph, n, None) is None]
+    assert not missing, missing
+
+
+@pytest.mark.parametrize("mod", sorted(MODULE_ALL))
+def test_module_api_coverage(mod):
+    m = fluid if not mod else getattr(fluid, mod)
+    missing = [n for n in MODULE_ALL[mod].split() if not hasattr(m, n)]
+    assert not missing, missing
+
+
+# ----------------------------------------------------------------------------- helpers
+def t(a, dtype=None):
+    return paddle.to_tensor(np.asarray(a) if dtype is None else np.asarray(a, dtype=dtype))
+
+
+def lod(a, lens, dtype=None):
+    return fluid.create_lod_tensor(np.asarray(a) if dtype is None else np.asarray(a, dtype=dtype), [lens],
+                                   fluid.CPUPlace())
+
+
+def n(x):
+    return x.numpy() if hasattr(x, "numpy") else np.asarray(x)
+
+
+# ----------------------------------------------------------------------------- elementwise / shape ops
+def test_elementwise_axis_broadcast():
+    x = np.random.rand(2, 3, 4, 5).astype("float32")
+    y = np.random.rand(3, 4).astype("float32")
+    out = layers.elementwise_add(t(x), t(y), axis=1)
+    np.testing.assert_allclose(n(out), x + y.reshape(1, 3, 4, 1), rtol=1e-6)
+    y2 = np.random.rand(5).astype("float32")
+    np.testing.assert_allclose(n(layers.elementwise_mul(t(x), t(y2))), x * y2, rtol=1e-6)
+    a = np.array([-7, 7, -8], "int64")
+    b = np.array([3, -3, 3], "int64")
+    np.testing.assert_array_equal(n(layers.elementwise_mod(t(a), t(b))), np.mod(a, b))
+    np.testing.assert_array_equal(n(layers.elementwise_floordiv(t(a), t(b))), np.floor_divide(a, b))
+
+
+def test_reduce_mul_matmul_flatten():
+    x = np.random.rand(2, 3, 4).astype("float32")
+    np.testing.assert_allclose(n(layers.reduce_sum(t(x), dim=[1, 2])), x.sum((1, 2)), rtol=1e-5)
+    np.testing.assert_allclose(n(layers.reduce_mean(t(x), dim=-1, keep_dim=True)), x.mean(-1, keepdims=True),
+                               rtol=1e-5)
+    np.testing.assert_allclose(n(layers.reduce_prod(t(x), dim=1)), x.prod(1), rtol=1e-5)
+    w = np.random.rand(12, 5).astype("float32")
+    np.testing.assert_allclose(n(layers.mul(t(x), t(w), x_num_col_dims=1)), x.reshape(2, 12) @ w, rtol=1e-5)
+    a, b = np.random.rand(3, 4).astype("float32"), np.random.rand(5, 4).astype("float32")
+    np.testing.assert_allclose(n(layers.matmul(t(a), t(b), transpose_y=True, alpha=0.5)), 0.5 * a @ b.T, rtol=1e-5)
+    assert n(layers.flatten(t(x), axis=2)).shape == (6, 4)
+    np.testing.assert_array_equal(n(layers.reshape(t(x), [0, -1])), x.reshape(2, 12))
+
+
+def test_one_hot_v1_and_v2():
+    ids = np.array([[1], [0], [3]], "int64")
+    out = layers.one_hot(t(ids), 4)
+    np.testing.assert_array_equal(n(out), np.eye(4)[[1, 0, 3]])
+    out2 = fluid.one_hot(t(ids), 4)          # v2 appends a dimension
+    assert n(out2).shape == (3, 1, 4)
+
+
+def test_cross_entropy_probabilities_and_soft():
+    p = np.random.dirichlet(np.ones(5), size=4).astype("float32")
+    y = np.array([[0], [2], [4], [1]], "int64")
+    out = n(layers.cross_entropy(t(p), t(y)))
+    np.testing.assert_allclose(out, -np.log(p[np.arange(4), y[:, 0]])[:, None], rtol=1e-5)
+    out_ign = n(layers.cross_entropy(t(p), t(np.array([[0], [-100], [4], [1]], "int64"))))
+    assert out_ign[1, 0] == 0.0
+    soft = np.random.dirichlet(np.ones(5), size=4).astype("float32")
+    np.testing.assert_allclose(n(layers.cross_entropy(t(p), t(soft), soft_label=True)),
+                               -(soft * np.log(p)).sum(1, keepdims=True), rtol=1e-5)
+
+
+def test_space_to_depth_index_map():
+    """reproduces the flat index map of space_to_depth_op.h (see test_space_to_depth_op.py)"""
+    B, C, H, Wd, bs = 2, 8, 4, 6, 2
+    x = np.random.rand(B, C, H, Wd)
+    out = np.zeros(x.size)
+    flat = x.reshape(-1)
+    oc = C // (bs * bs)
+    for b in range(B):
+        for k in range(C):
+            for j in range(H):
+                for i in range(Wd):
+                    src = i + Wd * (j + H * (k + C * b))
+                    c2, off = k % oc, k // oc
+                    w2, h2 = i * bs + off % bs, j * bs + off // bs
+                    out[w2 + Wd * bs * (h2 + H * bs * (c2 + oc * b))] = flat[src]
+    got = n(layers.space_to_depth(t(x), bs))
+    assert got.shape == (B, C * bs * bs, H // bs, Wd // bs)
+    np.testing.assert_allclose(got.reshape(-1), out)
+
+
+def test_similarity_focus_greedy_mask():
+    x = np.array([[[[0.8, 0.1], [0.4, 0.5]], [[0.9, 0.7], [0.9, 0.9]], [[0.8, 0.9], [0.1, 0.2]]],
+                  [[[0.2, 0.5], [0.3, 0.4]], [[0.9, 0.7], [0.8, 0.4]], [[0.0, 0.2], [0.4, 0.7]]]])
+    got = n(layers.similarity_focus(t(x), 1, [0]))
+    # batch 0 channel 0: 0.8 at (0,0) then 0.5 at (1,1); batch 1: 0.5 at (0,1) then 0.3 at (1,0)
+    m0 = np.array([[1, 0], [0, 1]])
+    m1 = np.array([[0, 1], [1, 0]])
+    np.testing.assert_array_equal(got[0], np.broadcast_to(m0, (3, 2, 2)))
+    np.testing.assert_array_equal(got[1], np.broadcast_to(m1, (3, 2, 2)))
+
+
+def test_add_position_encoding():
+    x = np.random.rand(2, 5, 6).astype("float32")
+    alpha, beta = 0.6, 0.4
+    half = 3
+    ref = np.empty_like(x)
+    for j in range(5):
+        for k in range(half):
+            val = j / pow(10000.0, k / (half - 1))
+            ref[:, j, k] = x[:, j, k] * alpha + np.sin(val) * beta
+            ref[:, j, half + k] = x[:, j, half + k] * alpha + np.cos(val) * beta
+    np.testing.assert_allclose(n(layers.add_position_encoding(t(x), alpha, beta)), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_teacher_student_sigmoid_loss():
+    x = np.random.randn(8, 1).astype("float64")
+    y = np.array([-2.0, -1.0, 0.3, 1.7, -1.5, -0.5, 0.0, 1.0]).reshape(8, 1)
+    got = n(layers.teacher_student_sigmoid_loss(t(x), t(y)))
+    ref = np.zeros_like(x)
+    for i in range(8):
+        xi, li = x[i, 0], y[i, 0]
+        sp = max(xi, 0) + np.log(1 + np.exp(-abs(xi)))
+        if li < -1:
+            ref[i] = sp
+        elif li < 0:
+            ref[i] = sp - xi
+        elif li < 1:
+            ref[i] = sp + sp - xi * li
+        else:
+            ref[i] = sp - xi + sp - xi * (li - 1)
+    np.testing.assert_allclose(got, ref, rtol=1e-6)
+
+
+def test_lrn_alpha_not_divided():
+    x = np.random.rand(2, 7, 3, 3).astype("float32")
+    nsz, k, alpha, beta = 5, 2.0, 1e-2, 0.75
+    sq = x ** 2
+    mid = np.full_like(x, k)
+    for c in range(7):
+        lo, hi = max(0, c - nsz // 2), min(7, c + nsz // 2 + 1)
+        mid[:, c] += alpha * sq[:, lo:hi].sum(1)
+    np.testing.assert_allclose(n(layers.lrn(t(x), nsz, k, alpha, beta)), x / mid ** beta, rtol=1e-5)
+
+
+def test_pool2d_exclusive_padding_and_ceil():
+    x = np.random.rand(1, 2, 5, 5).astype("float32")
+    got = n(layers.pool2d(t(x), 3, "avg", 2, 1, exclusive=True))
+    xp = np.pad(x, ((0, 0), (0, 0), (1, 1), (1, 1)))
+    cnt = np.pad(np.ones((5, 5)), 1)
+    ref = np.zeros((1, 2, 3, 3), "float32")
+    for i in range(3):
+        for j in range(3):
+            win = xp[:, :, 2 * i:2 * i + 3, 2 * j:2 * j + 3]
+            ref[:, :, i, j] = win.sum((2, 3)) / cnt[2 * i:2 * i + 3, 2 * j:2 * j + 3].sum()
+    np.testing.assert_allclose(got, ref, rtol=1e-5)
+    assert n(layers.pool2d(t(x), 2, "max", 2, ceil_mode=True)).shape == (1, 2, 3, 3)
+    np.testing.assert_allclose(n(layers.pool2d(t(x), global_pooling=True, pool_type="avg")),
+                               x.mean((2, 3), keepdims=True), rtol=1e-5)
+
+
+def test_misc_ops_against_numpy():
+    x = np.random.rand(4, 6).astype("float32")
+    np.testing.assert_allclose(n(layers.pad(t(x), [1, 0, 0, 2], 9.0)), np.pad(x, ((1, 0), (0, 2)), constant_values=9),
+                               rtol=1e-6)
+    img = np.random.rand(1, 1, 4, 4).astype("float32")
+    np.testing.assert_allclose(n(layers.pad2d(t(img), [1, 1, 2, 0], mode="reflect")),
+                               np.pad(img, ((0, 0), (0, 0), (1, 1), (2, 0)), mode="reflect"), rtol=1e-6)
+    np.testing.assert_allclose(n(layers.crop(t(x), shape=[2, 3], offsets=[1, 2])), x[1:3, 2:5], rtol=1e-6)
+    ids = np.array([[1], [6], [12], [19]], "int64")
+    np.testing.assert_array_equal(n(layers.shard_index(t(ids), 20, 2, 0)), [[1], [6], [-1], [-1]])
+    cvm_in = np.abs(np.random.rand(3, 5)).astype("float32")
+    got = n(layers.continuous_value_model(t(cvm_in), None, True))
+    np.testing.assert_allclose(got[:, 0], np.log(cvm_in[:, 0] + 1), rtol=1e-5)
+    np.testing.assert_allclose(got[:, 1], np.log(cvm_in[:, 1] + 1) - np.log(cvm_in[:, 0] + 1), rtol=1e-5)
+    a, b = np.random.rand(2, 3, 4, 4).astype("float32"), np.random.rand(2, 5, 4, 4).astype("float32")
+    np.testing.assert_allclose(n(layers.fsp_matrix(t(a), t(b))),
+                               np.einsum("bihw,bjhw->bij", a, b) / 16, rtol=1e-5)
+    mx = np.random.rand(2, 6, 3, 3).astype("float32")
+    np.testing.assert_allclose(n(layers.maxout(t(mx), 2)), mx.reshape(2, 3, 2, 3, 3).max(2), rtol=1e-6)
+    sel = n(layers.multiplex([t(x), t(x * 2)], t(np.array([[1], [0], [1], [0]], "int32"))))
+    np.testing.assert_allclose(sel, np.stack([x[0] * 2, x[1], x[2] * 2, x[3]]), rtol=1e-6)
+    u, idx = layers.unique(t(np.array([2, 3, 3, 1, 5, 3], "int64")))
+    np.testing.assert_array_equal(n(u), [2, 3, 1, 5])
+    np.testing.assert_array_equal(n(idx), [0, 1, 1, 2, 3, 1])
+    np.testing.assert_array_equal(n(layers.where(t(np.array([[True, False], [False, True]])))), [[0, 0], [1, 1]])
+    s = n(layers.smooth_l1(t(x), t(x * 0.5)))
+    d = x * 0.5
+    ref = np.where(np.abs(d) < 1, 0.5 * d * d, np.abs(d) - 0.5).sum(1, keepdims=True)
+    np.testing.assert_allclose(s, ref, rtol=1e-5)
+
+
+def test_hash_matches_xxhash():
+    import xxhash
+    x = np.array([[1, 2], [3, 4]], "int64")
+    got = n(layers.hash(t(x), 1000, num_hash=2))
+    assert got.shape == (2, 2, 1)
+    for i in range(2):
+        for j in range(2):
+            assert got[i, j, 0] == xxhash.xxh64_intdigest(x[i].tobytes(), seed=j) % 1000
+
+
+# ----------------------------------------------------------------------------- LoD sequence ops
+def test_sequence_pool_softmax_concat_expand():
+    data = np.arange(12, dtype="float32").reshape(6, 2)
+    x = lod(data, [2, 3, 1])
+    np.testing.assert_allclose(n(layers.sequence_pool(x, "sum")), [[2, 4], [18, 21], [10, 11]])
+    np.testing.assert_allclose(n(layers.sequence_pool(x, "average")), [[1, 2], [6, 7], [10, 11]])
+    np.testing.assert_allclose(n(layers.sequence_pool(x, "max")), [[2, 3], [8, 9], [10, 11]])
+    np.testing.assert_allclose(n(layers.sequence_last_step(x)), [[2, 3], [8, 9], [10, 11]])
+    sm = layers.sequence_softmax(lod(np.array([1, 2, 3, 4, 5, 6], "float32").reshape(6, 1), [2, 3, 1]))
+    v = n(sm).reshape(-1)
+    e = np.exp([1, 2])
+    np.testing.assert_allclose(v[:2], e / e.sum(), rtol=1e-6)
+    assert v[5] == pytest.approx(1.0)
+    cat = layers.sequence_concat([x, x])
+    assert fluid.core.lod_of(cat) == [[0, 4, 10, 12]]
+    y = lod(np.zeros((5, 1), "float32"), [2, 3])
+    ex = layers.sequence_expand_as(t(np.array([[1.0], [2.0]], "float32")), y)
+    np.testing.assert_allclose(n(ex).reshape(-1), [1, 1, 2, 2, 2])
+    rv = layers.sequence_reverse(x)
+    np.testing.assert_allclose(n(rv)[:2], data[:2][::-1])
+    pad, length = layers.sequence_pad(x, t(np.array([0.0], "float32")))
+    assert n(pad).shape == (3, 3, 2) and list(n(length)) == [2, 3, 1]
+    un = layers.sequence_unpad(pad, length)
+    np.testing.assert_allclose(n(un), data)
+
+
+def test_edit_distance_and_chunk_eval():
+    hyp = lod(np.array([1, 2, 3, 4, 5], "int64").reshape(-1, 1), [3, 2])
+    ref = lod(np.array([1, 3, 3, 4, 6, 7], "int64").reshape(-1, 1), [3, 3])
+    d, num = layers.edit_distance(hyp, ref, normalized=False)
+    np.testing.assert_allclose(n(d).reshape(-1), [1, 2])
+    assert int(n(num)[0]) == 2
+    # IOB with 2 chunk types: tags B-0=0 I-0=1 B-1=2 I-1=3 O=4
+    pred = lod(np.array([0, 1, 4, 2, 3, 4], "int64").reshape(-1, 1), [6])
+    lab = lod(np.array([0, 1, 4, 2, 4, 4], "int64").reshape(-1, 1), [6])
+    p, r, f1, ni, nl, nc = layers.chunk_eval(pred, lab, "IOB", 2)
+    assert int(n(ni)[0]) == 2 and int(n(nl)[0]) == 2 and int(n(nc)[0]) == 1
+    assert float(n(f1)[0]) == pytest.approx(0.5)
+
+
+def test_ctc_greedy_decoder_lod_and_padded():
+    probs = np.zeros((7, 4), "float32")
+    for i, k in enumerate([1, 1, 0, 2, 2, 3, 0]):
+        probs[i, k] = 1.0
+    out = layers.ctc_greedy_decoder(lod(probs, [4, 3]), blank=0)
+    np.testing.assert_array_equal(n(out).reshape(-1), [1, 2, 2, 3])
+    assert fluid.core.lod_of(out) == [[0, 2, 4]]
+    padded = np.stack([probs[:4], np.concatenate([probs[4:], np.zeros((1, 4), "float32")])])
+    o2, l2 = layers.ctc_greedy_decoder(t(padded), 0, input_length=t(np.array([[4], [3]], "int64")))
+    assert list(n(l2).reshape(-1)) == [2, 2]
+
+
+def test_linear_chain_crf_matches_bruteforce():
+    import itertools
+    paddle.seed(3)
+    K, L = 3, 4
+    emis = np.random.randn(L, K).astype("float32")
+    lab = np.array([0, 2, 1, 1], "int64").reshape(-1, 1)
+    nll = layers.linear_chain_crf(lod(emis, [L]), lod(lab, [L]), param_attr=fluid.ParamAttr(name="crfw"))
+    w = layers.nn.get_parameter("crfw").numpy()
+    start, end, A = w[0], w[1], w[2:]
+
+    def score(path):
+        s = start[path[0]] + end[path[-1]] + sum(emis[i, k] for i, k in enumerate(path))
+        return s + sum(A[a, b] for a, b in zip(path[:-1], path[1:]))
+    logz = np.log(sum(np.exp(score(pth)) for pth in itertools.product(range(K), repeat=L)))
+    assert float(n(nll)[0, 0]) == pytest.approx(logz - score(list(lab[:, 0])), rel=1e-4)
+    best = max(itertools.product(range(K), repeat=L), key=score)
+    dec = layers.crf_decoding(lod(emis, [L]), fluid.ParamAttr(name="crfw"))
+    assert list(n(dec).reshape(-1)) == list(best)
+
+
+# ----------------------------------------------------------------------------- detection
+def test_iou_box_clip_polygon():
+    a = np.array([[0, 0, 2, 2], [1, 1, 3, 3]], "float32")
+    b = np.array([[0, 0, 2, 2], [2, 2, 4, 4]], "float32")
+    np.testing.assert_allclose(n(layers.iou_similarity(t(a), t(b))), [[1, 0], [1 / 7, 1 / 7]], rtol=1e-5)
+    boxes = lod(np.array([[-5, -5, 50, 30], [10, 10, 200, 200]], "float32"), [2])
+    clipped = n(layers.box_clip(boxes, t(np.array([[40, 100, 1.0]], "float32"))))
+    np.testing.assert_allclose(clipped, [[0, 0, 50, 30], [10, 10, 99, 39]])
+    g = np.random.rand(1, 4, 2, 3).astype("float32")
+    out = n(layers.polygon_box_transform(t(g)))
+    for c in range(4):
+        for h in range(2):
+            for w in range(3):
+                exp = (4 * w if c % 2 == 0 else 4 * h) - g[0, c, h, w]
+                assert out[0, c, h, w] == pytest.approx(exp, rel=1e-6)
+
+
+def test_bipartite_match_greedy():
+    d = np.array([[0.1, 0.9, 0.3], [0.8, 0.7, 0.2]], "float32")
+    idx, dist = layers.bipartite_match(lod(d, [2]))
+    np.testing.assert_array_equal(n(idx), [[1, 0, -1]])
+    np.testing.assert_allclose(n(dist), [[0.8, 0.9, 0.0]], rtol=1e-6)
+    idx2, _ = layers.bipartite_match(lod(d, [2]), "per_prediction", 0.25)
+    np.testing.assert_array_equal(n(idx2), [[1, 0, 0]])
+
+
+def test_anchor_generator_and_density_prior_box():
+    feat = t(np.zeros((1, 8, 2, 3), "float32"))
+    anchors, var = layers.anchor_generator(feat, [64.0, 128.0], [0.5, 1.0], stride=[16.0, 16.0])
+    a = n(anchors)
+    assert a.shape == (2, 3, 4, 4)
+    # ratio 0.5, size 64 at cell (0, 0)
+    base_w = round(np.sqrt(256 / 0.5))
+    base_h = round(base_w * 0.5)
+    w, h = 64 / 16 * base_w, 64 / 16 * base_h
+    cx = cy = 0.5 * 15
+    np.testing.assert_allclose(a[0, 0, 0], [cx - 0.5 * (w - 1), cy - 0.5 * (h - 1), cx + 0.5 * (w - 1),
+                                           cy + 0.5 * (h - 1)], rtol=1e-6)
+    img = t(np.zeros((1, 3, 32, 32), "float32"))
+    boxes, _ = layers.density_prior_box(t(np.zeros((1, 8, 2, 2), "float32")), img, densities=[2], fixed_sizes=[8.0],
+                                        fixed_ratios=[1.0])
+    assert n(boxes).shape == (2, 2, 4, 4)
+    assert (n(boxes) >= 0).all() and (n(boxes) <= 1).all()
+
+
+def test_multiclass_nms_suppresses_overlaps():
+    boxes = np.array([[[0, 0, 10, 10], [1, 1, 11, 11], [50, 50, 60, 60]]], "float32")
+    scores = np.array([[[0.0, 0.0, 0.0], [0.9, 0.8, 0.7]]], "float32")
+    out = layers.multiclass_nms(t(boxes), t(scores), 0.1, 10, 10, 0.5)
+    o = n(out)
+    assert o.shape == (2, 6)
+    np.testing.assert_allclose(o[:, 1], [0.9, 0.7])
+    assert fluid.core.lod_of(out) == [[0, 2]]
+
+
+def test_prroi_pool_exact_integral():
+    x = np.random.rand(1, 2, 6, 6).astype("float32")
+    rois = lod(np.array([[0.5, 1.0, 4.5, 5.0]], "float32"), [1])
+    got = n(layers.prroi_pool(t(x), rois, 1.0, 2, 2))
+    # dense midpoint quadrature of the bilinear interpolant
+    def bil(c, yy, xx):
+        y0, x0 = int(np.floor(yy)), int(np.floor(xx))
+        v = 0.0
+        for dy, wy in ((0, 1 - (yy - y0)), (1, yy - y0)):
+            for dx, wx in ((0, 1 - (xx - x0)), (1, xx - x0)):
+                Y, X = y0 + dy, x0 + dx
+                if 0 <= Y < 6 and 0 <= X < 6:
+                    v += wy * wx * x[0, c, Y, X]
+        return v
+    S = 80
+    for ph in range(2):
+        for pw in range(2):
+            ys = 1.0 + ph * 2.0 + (np.arange(S) + 0.5) * 2.0 / S
+            xs = 0.5 + pw * 2.0 + (np.arange(S) + 0.5) * 2.0 / S
+            for c in range(2):
+                ref = np.mean([bil(c, yy, xx) for yy in ys for xx in xs])
+                assert got[0, c, ph, pw] == pytest.approx(ref, rel=2e-3)
+
+
+def test_sigmoid_focal_loss_formula():
+    x = np.random.randn(4, 3).astype("float32")
+    lab = np.array([[0], [1], [3], [-1]], "int32")
+    got = n(layers.sigmoid_focal_loss(t(x), t(lab), t(np.array([2], "int32"))))
+    p = 1 / (1 + np.exp(-x))
+    ref = np.zeros_like(x)
+    for a in range(4):
+        for d in range(3):
+            g = lab[a, 0]
+            pos, neg = float(g == d + 1), float(g != -1 and g != d + 1)
+            tp = (1 - p[a, d]) ** 2 * np.log(max(p[a, d], np.finfo(np.float32).tiny))
+            tn = p[a, d] ** 2 * (-x[a, d] * (x[a, d] >= 0) - np.log(1 + np.exp(x[a, d] - 2 * x[a, d] * (x[a, d] >= 0))))
+            ref[a, d] = -pos * tp * 0.25 / 2 - neg * tn * 0.75 / 2
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- recurrent
+def test_dynamic_gru_and_lstm_match_step_formulas():
+    paddle.seed(0)
+    H = 3
+    x = np.random.rand(5, 3 * H).astype("float32")
+    out = layers.dynamic_gru(lod(x, [2, 3]), H, param_attr=fluid.ParamAttr(name="gw"),
+                             bias_attr=fluid.ParamAttr(name="gb"))
+    wt, bt = layers.nn.get_parameter("gw").numpy(), layers.nn.get_parameter("gb").numpy().reshape(-1)
+    sig = lambda v: 1 / (1 + np.exp(-v))  # noqa: E731
+    ref = []
+    for a, e in ((0, 2), (2, 5)):
+        h = np.zeros(H, "float32")
+        for i in range(a, e):
+            xu, xr, xc = np.split(x[i] + bt, 3)
+            u, r = sig(xu + h @ wt[:, :H]), sig(xr + h @ wt[:, H:2 * H])
+            c = np.tanh(xc + (r * h) @ wt[:, 2 * H:])
+            h = (1 - u) * h + u * c
+            ref.append(h)
+    np.testing.assert_allclose(n(out), np.stack(ref), rtol=1e-5, atol=1e-6)
+    hid, cell = layers.dynamic_lstm(lod(np.random.rand(4, 4 * H).astype("float32"), [4]), 4 * H)
+    assert n(hid).shape == (4, H) and fluid.core.lod_of(hid) == [[0, 4]]
+
+
+def test_beam_search_step():
+    pre_ids = lod(np.array([[1], [2]], "int64"), [2])
+    pre_ids._lod = [[0, 2], [0, 1, 2]]
+    pre_scores = lod(np.array([[0.5], [0.6]], "float32"), [2])
+    ids = t(np.array([[4, 2], [3, 5]], "int64"))
+    scores = t(np.array([[0.9, 0.1], [0.8, 0.7]], "float32"))
+    si, ss = layers.beam_search(pre_ids, pre_scores, ids, scores, beam_size=2, end_id=0)
+    np.testing.assert_array_equal(n(si).reshape(-1), [4, 3])
+    np.testing.assert_allclose(n(ss).reshape(-1), [0.9, 0.8])
+    assert fluid.core.lod_of(si)[1] == [0, 1, 2]
+
+
+def test_fluid_rnn_cells_and_rnn():
+    cell = layers.GRUCell(4)
+    x = t(np.random.rand(2, 5, 3).astype("float32"))
+    out, final = layers.rnn(cell, x, sequence_length=t(np.array([5, 2], "int64")))
+    assert n(out).shape == (2, 5, 4)
+    assert np.allclose(n(out)[1, 2:], 0)
+    np.testing.assert_allclose(n(final)[1], n(out)[1, 1], rtol=1e-6)
+
+
+# ----------------------------------------------------------------------------- dygraph
+class _MNIST(fluid.dygraph.Layer):
+    def __init__(self):
+        super().__init__()
+        self.conv = fluid.dygraph.Conv2D(1, 4, 3, act="relu")
+        self.pool = fluid.dygraph.Pool2D(2, "max", 2)
+        self.fc = fluid.dygraph.Linear(4 * 3 * 3, 10, act="softmax")
+
+    def forward(self, x):
+        y = self.pool(self.conv(x))
+        return self.fc(layers.reshape(y, [-1, 36]))
+
+
+def test_dygraph_training_and_checkpoint(tmp_path):
+    np.random.seed(0)
+    with fluid.dygraph.guard(fluid.CPUPlace()):
+        paddle.seed(1)
+        model = _MNIST()
+        opt = fluid.optimizer.AdamOptimizer(learning_rate=0.01, parameter_list=model.parameters())
+        xs = np.random.rand(16, 1, 8, 8).astype("float32")
+        ys = (xs.reshape(16, -1).mean(1) > 0.5).astype("int64").reshape(-1, 1)
+        losses = []
+        for _ in range(30):
+            img, label = fluid.dygraph.to_variable(xs), fluid.dygraph.to_variable(ys)
+            pred = model(img)
+            loss = layers.mean(layers.cross_entropy(pred, label))
+            loss.backward()
+            opt.minimize(loss)
+            model.clear_gradients()
+            losses.append(float(loss.numpy()))
+        assert losses[-1] < losses[0]
+        acc = layers.accuracy(model(fluid.dygraph.to_variable(xs)), fluid.dygraph.to_variable(ys))
+        assert 0.0 <= float(acc.numpy()[0]) <= 1.0
+        path = str(tmp_path / "mnist")
+        fluid.save_dygraph(model.state_dict(), path)
+        fluid.save_dygraph(opt.state_dict(), path)
+        params, opt_state = fluid.load_dygraph(path)
+        assert params is not None and opt_state is not None
+        m2 = _MNIST()
+        m2.set_dict(params) if hasattr(m2, "set_dict") else m2.set_state_dict(params)
+        np.testing.assert_allclose(n(m2(fluid.dygraph.to_variable(xs))), n(model(fluid.dygraph.to_variable(xs))),
+                                   rtol=1e-5)
+
+
+def test_dygraph_lr_decay_advances_per_minimize():
+    with fluid.dygraph.guard():
+        lin = fluid.dygraph.Linear(2, 1)
+        dec = fluid.dygraph.ExponentialDecay(0.1, decay_steps=1, decay_rate=0.5)
+        opt = fluid.optimizer.SGD(learning_rate=dec, parameter_list=lin.parameters())
+        lrs = []
+        for _ in range(3):
+            loss = layers.reduce_sum(lin(fluid.dygraph.to_variable(np.ones((1, 2), "float32"))))
+            loss.backward()
+            lrs.append(opt.current_step_lr())
+            opt.minimize(loss)
+            opt.clear_gradients()
+        np.testing.assert_allclose(lrs, [0.1, 0.05, 0.025], rtol=1e-6)
+
+
+def test_tree_conv_single_chain():
+    with fluid.dygraph.guard():
+        paddle.seed(0)
+        tc = fluid.dygraph.TreeConv(2, 3, num_filters=1, max_depth=2, act=None, bias_attr=False)
+        x = np.random.rand(1, 3, 2).astype("float32")
+        edges = np.array([[[1, 2], [1, 3], [0, 0]]], "int32")
+        out = n(tc(t(x), t(edges)))
+        w = n(tc.weight).reshape(2, 3, 3)          # [F, (l, r, t), out]
+        # root 1 with children 2, 3 at depth 1 (eta_t = 0.5): child i gets eta_l = 0.5*(i)/(1), eta_r rest
+        def coef(index, pclen, depth):
+            et = (2 - depth) / 2
+            el = (1 - et) * (0.5 if pclen == 1 else (index - 1) / (pclen - 1))
+            return el, (1 - et) * (1 - el), et
+        rows = [(0, coef(1, 1, 0)), (1, coef(1, 2, 1)), (2, coef(2, 2, 1))]
+        feat = np.zeros((2, 3))
+        for node, (el, er, et) in rows:
+            feat += np.outer(x[0, node], [el, er, et])
+        ref0 = np.einsum("fk,fko->o", feat, w)
+        np.testing.assert_allclose(out[0, 0, :, 0], ref0, rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- static programs
+@pytest.fixture
+def static_mode():
+    paddle.enable_static()
+    main, start = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, start):
+        yield main
+    paddle.disable_static()
+
+
+def test_static_fc_training_converges(static_mode):
+    x = layers.data("x", [4], dtype="float32")
+    y = layers.data("y", [1], dtype="float32")
+    pred = layers.fc(x, 1)
+    loss = layers.mean(layers.square_error_cost(pred, y))
+    fluid.optimizer.SGD(learning_rate=0.1).minimize(loss)
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(fluid.default_startup_program())
+    rng = np.random.RandomState(0)
+    wtrue = rng.rand(4, 1).astype("float32")
+    first = last = None
+    for i in range(60):
+        xb = rng.rand(16, 4).astype("float32")
+        lv, = exe.run(static_mode, feed={"x": xb, "y": xb @ wtrue}, fetch_list=[loss])
+        first = first if first is not None else float(lv)
+        last = float(lv)
+    assert last < first * 0.2
+
+
+def test_static_while_loop_with_inplace_updates(static_mode):
+    i = layers.fill_constant([1], "int64", 0)
+    limit = layers.fill_constant([1], "int64", 10)
+    acc = layers.fill_constant([1], "float32", 0.0)
+    cond = layers.less_than(i, limit)
+    w = layers.While(cond)
+    with w.block():
+        layers.assign(layers.elementwise_add(acc, layers.cast(i, "float32")), acc)
+        layers.increment(i, 1, in_place=True)
+        layers.less_than(i, limit, cond=cond)
+    exe = fluid.Executor(fluid.CPUPlace())
+    r_acc, r_i = exe.run(static_mode, fetch_list=[acc, i])
+    assert float(r_acc[0]) == 45.0 and int(r_i[0]) == 10
+
+
+def test_static_switch_and_array(static_mode):
+    x = layers.data("x", [1], append_batch_size=False, dtype="float32")
+    out = layers.fill_constant([1], "float32", -1.0)
+    with layers.Switch() as sw:
+        with sw.case(layers.less_than(x, layers.fill_constant([1], "float32", 0.0))):
+            layers.assign(layers.fill_constant([1], "float32", 10.0), out)
+        with sw.case(layers.less_than(x, layers.fill_constant([1], "float32", 5.0))):
+            layers.assign(layers.fill_constant([1], "float32", 20.0), out)
+        with sw.default():
+            layers.assign(layers.fill_constant([1], "float32", 30.0), out)
+    arr = layers.create_array("float32")
+    zero = layers.fill_constant([1], "int64", 0)
+    layers.array_write(x, zero, array=arr)
+    back = layers.array_read(arr, zero)
+    n_arr = layers.array_length(arr)
+    exe = fluid.Executor(fluid.CPUPlace())
+    for v, exp in ((-3.0, 10.0), (2.0, 20.0), (9.0, 30.0)):
+        o, b, ln = exe.run(static_mode, feed={"x": np.array([v], "float32")}, fetch_list=[out, back, n_arr])
+        assert float(o[0]) == exp and float(b[0]) == v and int(ln[0]) == 1
+
+
+def test_static_ifelse_rows(static_mode):
+    x = layers.data("x", [1], dtype="float32")
+    cond = layers.less_than(x, layers.fill_constant([1], "float32", 0.0))
+    ie = layers.IfElse(cond)
+    with ie.true_block():
+        ie.output(layers.scale(ie.input(x), -1.0))
+    with ie.false_block():
+        ie.output(layers.scale(ie.input(x), 2.0))
+    out = ie()[0]
+    exe = fluid.Executor(fluid.CPUPlace())
+    xv = np.array([[-1.0], [2.0], [-3.0], [4.0]], "float32")
+    o, = exe.run(static_mode, feed={"x": xv}, fetch_list=[out])
+    np.testing.assert_allclose(o.reshape(-1), [1, 4, 3, 8])
+
+
+def test_ifelse_dygraph_eager():
+    with fluid.dygraph.guard():
+        x = t(np.array([[-1.0], [2.0]], "float32"))
+        ie = layers.IfElse(layers.less_than(x, t(np.zeros((2, 1), "float32"))))
+        with ie.true_block():
+            ie.output(layers.scale(ie.input(x), -1.0))
+        with ie.false_block():
+            ie.output(layers.scale(ie.input(x), 2.0))
+        np.testing.assert_allclose(n(ie()[0]).reshape(-1), [1, 4])
+
+
+def test_static_rnn_cumulative_sum(static_mode):
+    x = layers.data("x", [4, 2, 3], append_batch_size=False, dtype="float32")   # [T, B, D]
+    rnn = layers.StaticRNN()
+    with rnn.step():
+        step = rnn.step_input(x)
+        mem = rnn.memory(shape=[-1, 3], batch_ref=step)
+        new = layers.elementwise_add(mem, step)
+        rnn.update_memory(mem, new)
+        rnn.step_output(new)
+    out = rnn()
+    exe = fluid.Executor(fluid.CPUPlace())
+    xv = np.random.rand(4, 2, 3).astype("float32")
+    o, = exe.run(static_mode, feed={"x": xv}, fetch_list=[out])
+    np.testing.assert_allclose(o, np.cumsum(xv, 0), rtol=1e-5)
+
+
+def test_static_dynamic_rnn_over_lod(static_mode):
+    x = layers.data("x", [2], dtype="float32", lod_level=1)
+    drnn = layers.DynamicRNN()
+    with drnn.block():
+        w = drnn.step_input(x)
+        mem = drnn.memory(shape=[2], value=0.0)
+        new = layers.elementwise_add(mem, w)
+        drnn.update_memory(mem, new)
+        drnn.output(new)
+    out = drnn()
+    exe = fluid.Executor(fluid.CPUPlace())
+    data = np.arange(10, dtype="float32").reshape(5, 2)
+    o, = exe.run(static_mode, feed={"x": lod(data, [2, 3])}, fetch_list=[out], return_numpy=False)
+    ref = np.concatenate([np.cumsum(data[:2], 0), np.cumsum(data[2:], 0)])
+    np.testing.assert_allclose(n(o), ref)
+    assert fluid.core.lod_of(o) == [[0, 2, 5]]
+
+
+def test_inference_model_roundtrip_per_var_and_combined(static_mode, tmp_path):
+    x = layers.data("img", [6], dtype="float32")
+    h = layers.fc(x, 5, act="relu")
+    y = layers.softmax(layers.fc(h, 3))
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(fluid.default_startup_program())
+    xv = np.random.rand(4, 6).astype("float32")
+    ref, = exe.run(static_mode, feed={"img": xv}, fetch_list=[y])
+    for params_filename in (None, "params"):
+        d = str(tmp_path / f"m_{params_filename}")
+        fluid.io.save_inference_model(d, ["img"], [y], exe, static_mode, params_filename=params_filename)
+        assert os.path.exists(os.path.join(d, "__model__"))
+        prog, feeds, fetches = fluid.io.load_inference_model(d, exe, params_filename=params_filename)
+        assert feeds == ["img"]
+        got, = exe.run(prog, feed={"img": xv}, fetch_list=fetches)
+        np.testing.assert_allclose(got, ref, rtol=1e-5)
+
+
+def test_save_load_params_per_var(static_mode, tmp_path):
+    x = layers.data("x", [3], dtype="float32")
+    layers.fc(x, 2, param_attr=fluid.ParamAttr(name="fc_w"), bias_attr=fluid.ParamAttr(name="fc_b"))
+    exe = fluid.Executor(fluid.CPUPlace())
+    fluid.io.save_params(exe, str(tmp_path), static_mode)
+    assert os.path.exists(tmp_path / "fc_w") and os.path.exists(tmp_path / "fc_b")
+    w = [p for p in static_mode.all_parameters() if p.name == "fc_w"][0]
+    saved = w.numpy().copy()
+    w.set_value(np.zeros_like(saved))
+    fluid.io.load_params(exe, str(tmp_path), static_mode)
+    np.testing.assert_allclose(w.numpy(), saved)
+
+
+def test_py_reader_feeds_executor(static_mode):
+    reader = layers.py_reader(capacity=4, shapes=[[-1, 2]], dtypes=["float32"])
+    x = layers.read_file(reader)
+    s = layers.reduce_sum(x)
+
+    def gen():
+        for k in range(3):
+            yield [np.full((2, 2), k, "float32")]
+    reader.decorate_tensor_provider(gen)
+    exe = fluid.Executor(fluid.CPUPlace())
+    reader.start()
+    got = []
+    with pytest.raises(fluid.core.EOFException):
+        while True:
+            got.append(float(exe.run(static_mode, fetch_list=[s])[0]))
+    assert got == [0.0, 4.0, 8.0]
+
+
+def test_data_feeder_lod():
+    paddle.enable_static()
+    try:
+        main = fluid.Program()
+        with fluid.program_guard(main, fluid.Program()):
+            words = layers.data("w", [1], dtype="int64", lod_level=1)
+            lab = layers.data("l", [1], dtype="int64")
+            feeder = fluid.DataFeeder([words, lab], fluid.CPUPlace())
+            feed = feeder.feed([([1, 2, 3], [0]), ([4, 5], [1])])
+            assert fluid.core.lod_of(feed["w"]) == [[0, 3, 5]]
+            assert feed["l"].shape == (2, 1)
+    finally:
+        paddle.disable_static()
+
+
+def test_metrics_and_weighted_average():
+    acc = fluid.metrics.Accuracy()
+    acc.update(0.5, 2)
+    acc.update(1.0, 2)
+    assert acc.eval() == pytest.approx(0.75)
+    p = fluid.metrics.Precision()
+    p.update(np.array([0.9, 0.2, 0.8]), np.array([1, 0, 0]))
+    assert p.eval() == pytest.approx(0.5)
+    auc = fluid.metrics.Auc(num_thresholds=1000)
+    auc.update(np.array([[0.1, 0.9], [0.6, 0.4], [0.3, 0.7], [0.8, 0.2]]), np.array([1, 0, 1, 0]))
+    assert auc.eval() == pytest.approx(1.0)
+    wa = fluid.average.WeightedAverage()
+    wa.add(1.0, 1)
+    wa.add(3.0, 3)
+    assert wa.eval() == pytest.approx(2.5)
+
+
+def test_lod_tensor_api():
+    tns = fluid.create_lod_tensor(np.arange(6).reshape(6, 1), [[2, 4]], fluid.CPUPlace())
+    assert tns.recursive_sequence_lengths() == [[2, 4]]
+    assert tns.lod() == [[0, 2, 6]]
+    assert tns.has_valid_recursive_sequence_lengths()
+    assert tns.shape() == [6, 1]
+    words = fluid.create_lod_tensor([[1, 2], [3, 4, 5]], [[2, 3]], fluid.CPUPlace())
+    assert np.asarray(words).reshape(-1).tolist() == [1, 2, 3, 4, 5]
+
+
+def test_fluid_optimizers_reduce_quadratic():
+    for cls, kw in ((fluid.optimizer.DecayedAdagradOptimizer, {}), (fluid.optimizer.FtrlOptimizer, {"l1": 0.0}),
+                    (fluid.optimizer.MomentumOptimizer, {"momentum": 0.9}),
+                    (fluid.optimizer.RMSPropOptimizer, {})):
+        with fluid.dygraph.guard():
+            w = paddle.create_parameter([4], "float32", default_initializer=paddle.nn.initializer.Constant(2.0))
+            opt = cls(learning_rate=0.1, parameter_list=[w], **kw)
+            for _ in range(20):
+                loss = layers.reduce_sum(layers.square(w))
+                loss.backward()
+                opt.minimize(loss)
+                opt.clear_gradients()
+            assert float(layers.reduce_sum(layers.square(w)).numpy()) < 16.0, cls.__name__

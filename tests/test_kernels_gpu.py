@@ -865,19 +865,26 @@ def test_gemm4w_transposed_store(monkeypatch, sched, M, N, K):
     assert (db - dh_ref.sum(0)).abs().max() / dh_ref.sum(0).abs().max() < 1e-2
 
 
-def test_gemm_picks_match_reference():
-    """the per-shape own/library pick entry points (mm_nt / mm_nn / mm_tn / mm_nt_bias) vs fp32"""
+@pytest.mark.parametrize("impl", ["auto", "own", "library"])
+def test_gemm_picks_match_reference(impl, monkeypatch):
+    """the dispatch entry points (mm_nt / mm_nn / mm_tn incl. split-K / mm_nt_bias) under every
+    PHA_GEMM_IMPL policy vs fp32"""
     from paddle_hackathon_amd.ops import gemm as G
+    monkeypatch.setenv("PHA_GEMM_IMPL", impl)
     torch.manual_seed(4)
     a = (torch.rand(512, 256, device="cuda") * 2 - 1).bfloat16()
     bt = (torch.rand(384, 256, device="cuda") * 2 - 1).bfloat16()
     b = (torch.rand(256, 384, device="cuda") * 2 - 1).bfloat16()
+    dy = (torch.rand(512, 128, device="cuda") * 2 - 1).bfloat16()
+    xk = (torch.rand(4096, 256, device="cuda") * 2 - 1).bfloat16()     # long-K weight gradient: split-K
+    dk = (torch.rand(4096, 512, device="cuda") * 2 - 1).bfloat16()
     bias = torch.randn(384, device="cuda").bfloat16()
     for got, ref in [(G.mm_nt(a, bt), a.float() @ bt.float().t()), (G.mm_nn(a, b), a.float() @ b.float()),
-                     (G.mm_tn(a, (torch.rand(512, 128, device="cuda") * 2 - 1).bfloat16()), None),
+                     (G.mm_tn(a, dy), a.float().t() @ dy.float()),
+                     (G.mm_tn(xk, dk), xk.float().t() @ dk.float()),
                      (G.mm_nt_bias(a, bt, bias), a.float() @ bt.float().t() + bias.float())]:
-        if ref is not None:
-            assert (got.float() - ref).abs().max() / ref.abs().max() < 1e-2
+        assert got.shape == ref.shape
+        assert (got.float() - ref).abs().max() / ref.abs().max() < 1e-2
 
 
 def _attn_ref(q, k, v, causal, scale, bias=None, keep=None, rate=0.0):

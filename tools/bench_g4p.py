@@ -126,7 +126,52 @@ def bench():
     print("per-step GEMM ms (same products): " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()), flush=True)
 
 
+
+
+def paths():
+    """the dispatch functions the GPT step calls (ops/gemm.py mm_nt / mm_nt_bias / mm_tn), own vs
+    library, per GPT-1.3B shape (B16 x S2048 tokens, 24 layers)"""
+    import os
+    T = 32768
+    tot = {"own": 0.0, "library": 0.0}
+
+    def both(f, iters=10):
+        res = {}
+        for impl in ("own", "library"):
+            os.environ["PHA_GEMM_IMPL"] = impl
+            res[impl] = timeit(f, iters)
+        return res
+
+    shapes = [("qkv", 2048, 6144), ("out", 2048, 2048), ("fc1", 2048, 8192), ("fc2", 8192, 2048)]
+    for name, K, N in shapes:
+        x, wt, w, dy = r(T, K), r(N, K), r(K, N), r(T, N)
+        b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+        fl = 2.0 * T * K * N
+        for lab, f in [("fwd mm_nt_bias", lambda: G.mm_nt_bias(x, wt, b)),
+                       ("dX  mm_nt     ", lambda: G.mm_nt(dy, w)),
+                       ("dW  mm_tn     ", lambda: G.mm_tn(x, dy))]:
+            t = both(f)
+            for k in tot:
+                tot[k] += t[k] * 24
+            print(f"{name} {lab} {T}x{N}x{K}: own {fl / t['own'] / 1e12:6.0f} TF  lib {fl / t['library'] / 1e12:6.0f} TF"
+                  f"  ({(t['own'] / t['library'] - 1) * 100:+.1f}%)", flush=True)
+    V, H = 50304, 2048
+    x, E, dl = r(T, H), r(V, H), r(T, V)
+    fl = 2.0 * T * V * H
+    for lab, f in [("logits mm_nt", lambda: G.mm_nt(x, E)), ("dh mm_nn    ", lambda: G.mm_nn(dl, E)),
+                   ("dE mm_tn    ", lambda: G.mm_tn(dl, x))]:
+        t = both(f, 3)
+        for k in tot:
+            tot[k] += t[k]
+        print(f"head {lab} {T}x{V}x{H}: own {fl / t['own'] / 1e12:6.0f} TF  lib {fl / t['library'] / 1e12:6.0f} TF"
+              f"  ({(t['own'] / t['library'] - 1) * 100:+.1f}%)", flush=True)
+    print("per-step GEMM ms: " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()), flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "paths":
+        paths()
+        sys.exit(0)
     check()
     if len(sys.argv) < 2 or sys.argv[1] != "check":
         bench()
