@@ -30,6 +30,7 @@ import torch
 __all__ = ["CUDAGraph", "wrap_cuda_graph", "is_cuda_graph_supported"]
 
 ALL_MODES = ["global", "thread_local", "relaxed"]
+_NO_DEBUG = os.environ.get("PHA_GRAPH_DEBUG", "1") == "0"
 
 
 def is_cuda_graph_supported():
@@ -58,6 +59,7 @@ class CUDAGraph:
         self._graph = None
         self._stream = None
         self._fixed_stream = _stream   # captures that must share one stream (forward + backward)
+        self._no_debug = False
         self._stream_ctx = None
         self._prev_stream = None
         self.id = CUDAGraph._next_id
@@ -69,7 +71,8 @@ class CUDAGraph:
         torch.cuda.synchronize(self._device)
         gc.collect()
         self._graph = torch.cuda.CUDAGraph()
-        self._graph.enable_debug_mode()   # keeps the graph template for print_to_dot_files
+        if not _NO_DEBUG and not self._no_debug:
+            self._graph.enable_debug_mode()   # keeps the graph template for print_to_dot_files
         self._prev_stream = torch.cuda.current_stream(self._device)
         self._stream = self._fixed_stream or torch.cuda.Stream(device=self._device)
         self._stream.wait_stream(self._prev_stream)

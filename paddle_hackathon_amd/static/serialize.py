@@ -418,8 +418,8 @@ class _Reader:
         for bm in d.blocks:
             blk = prog.blocks[bm.idx]
             for vd in bm.vars:
-                if vd.type.type != pb.LOD_TENSOR or vd.persistable:
-                    continue
+                if vd.type.type != pb.LOD_TENSOR or vd.persistable or vd.name in self.vars:
+                    continue   # one Variable per name: sub-block ops update their parent's variables
                 td = vd.type.lod_tensor.tensor
                 dims = list(td.dims)
                 meta = torch.empty([1 if s < 0 else s for s in dims], dtype=pb.dtype_of(td.data_type), device="meta")
@@ -467,17 +467,32 @@ class _Reader:
                     fn = _resolve_fn(attrs["__pha_fn__"])
                     op = OpDesc(attrs["__pha_fn__"], fn, tuple(self.dec(j["args"], slots)),
                                 {k: self.dec(v, slots) for k, v in j["kwargs"].items()}, self.dec(j["outs"], out_slots))
+                elif om.type in _ref.CF:
+                    op = _ref.CF[om.type](self, blk, ins, outs, attrs)
                 else:
                     conv = _CONVERT.get(om.type)
                     if conv is None:
                         raise NotImplementedError(f"ProgramDesc op type {om.type!r} has no converter")
-                    fn, kwargs, out_slot = conv(self, ins, attrs)
-                    o = self.var(outs[out_slot][0], blk)
+                    fn, kwargs, out_spec = conv(self, ins, attrs)
+                    if isinstance(out_spec, str):
+                        o = self.var(outs[out_spec][0], blk)
+                    elif out_spec[0] == "list":
+                        o = [self.var(n, blk) for n in outs[out_spec[1]]]
+                    else:     # one Variable per slot (absent optional slots get a fresh one)
+                        o = tuple(self.var(outs[sl][0], blk) if outs.get(sl) else
+                                  self.var(f"{om.type}.{sl}.{len(self.vars)}", blk) for sl in out_spec)
+                    fn = getattr(fn, "__wrapped_op__", fn)
                     qual = f"{fn.__module__}.{fn.__name__}"
-                    op = OpDesc(qual, getattr(fn, "__wrapped_op__", fn), (), kwargs, o)
+                    op = OpDesc(qual, fn, (), kwargs, o)
                 for v in _iter_vars(op.outputs):
                     v.op = op
                 blk.append_op(op)
+        # reference-layout control flow reads its sub-blocks' free variables: known only now
+        for b in prog.blocks:
+            for op in b.ops:
+                if op.attrs.get("ref_layout"):
+                    extra = [v for v in _iter_vars(op.kwargs.get("Condition", []))]
+                    op.attrs["captured"] = cf._captured([prog.blocks[op.attrs["sub_block"]]]) + extra
         return prog, [feeds[k] for k in sorted(feeds)], [fetches[k] for k in sorted(fetches)]
 
 
@@ -758,6 +773,13 @@ _CONVERT = {
     "reduce_max": _reduce("tensor.math.max"),
     "fill_constant": _conv_fill_constant,
 }
+
+
+from . import ref_ops as _ref  # noqa: E402
+
+for _k, _v in _ref.CONVERT.items():
+    _CONVERT.setdefault(_k, _v)
+_CONVERT.setdefault("depthwise_conv2d", _conv_conv2d)
 
 
 # ------------------------------------------------------------------------------- byte-level API

@@ -269,3 +269,323 @@ def test_unknown_reference_op_is_reported(tmp_path):
     open(prefix + ".pdiparams", "wb").write(b"")
     with pytest.raises(NotImplementedError, match="some_exotic_op"):
         paddle.static.load_inference_model(prefix)
+
+
+# ----------------------------------------------------------------------------- op-type coverage table
+def _single_op_program(tmp_path, op_type, inputs, outputs, attrs, name="m"):
+    """ProgramDesc laid out like the reference's: feed every non-persistable input, run one
+    ``op_type`` op, fetch every output. ``inputs``: {slot: [(var name, array, feed?)]},
+    ``outputs``: {slot: [var names]}. -> (program, feed names, fetch vars)"""
+    import torch
+    desc = pb.ProgramDesc()
+    g = desc.blocks.add()
+    g.idx, g.parent_idx = 0, -1
+    params, feeds = {}, []
+    for slot, lst in inputs.items():
+        for vname, arr, is_feed in lst:
+            code = {np.dtype("float32"): 5, np.dtype("int64"): 3, np.dtype("int32"): 2, np.dtype("bool"): 0,
+                    np.dtype("float64"): 6}[arr.dtype]
+            _var(g, vname, list(arr.shape), dtype=code, persistable=not is_feed)
+            if is_feed:
+                feeds.append(vname)
+            else:
+                params[vname] = arr
+    for i, vname in enumerate(feeds):
+        _op(g, "feed", {"X": ["feed"]}, {"Out": [vname]}, col=i)
+    op = _op(g, op_type, {s: [v for v, _, _ in lst] for s, lst in inputs.items()}, outputs)
+    for k, v in attrs.items():
+        a = op.attrs.add()
+        a.name = k
+        if isinstance(v, bool):
+            a.type, a.b = pb.BOOLEAN, v
+        elif isinstance(v, int):
+            a.type, a.i = pb.INT, v
+        elif isinstance(v, float):
+            a.type, a.f = pb.FLOAT, v
+        elif isinstance(v, str):
+            a.type, a.s = pb.STRING, v
+        elif v and all(isinstance(e, bool) for e in v):
+            a.type = pb.BOOLEANS
+            a.bools.extend(v)
+        elif all(isinstance(e, int) for e in v):
+            a.type = pb.INTS
+            a.ints.extend(v)
+        else:
+            a.type = pb.FLOATS
+            a.floats.extend(float(e) for e in v)
+    fetch = [n for lst in outputs.values() for n in lst]
+    for i, n in enumerate(fetch):
+        _op(g, "fetch", {"X": [n]}, {"Out": ["fetch"]}, col=i)
+    prefix = str(tmp_path / name)
+    open(prefix + ".pdmodel", "wb").write(desc.SerializeToString())
+    pb.save_combine([torch.from_numpy(params[n]) for n in sorted(params)], prefix + ".pdiparams")
+    return paddle.static.load_inference_model(prefix)
+
+
+_R = np.random.RandomState(7)
+_X = _R.randn(2, 3, 4).astype("float32")
+_P = np.abs(_R.randn(2, 3, 4)).astype("float32") + 0.1
+_I = _R.randint(0, 3, (2, 3)).astype("int64")
+_IMG = _R.randn(1, 4, 4, 4).astype("float32")
+
+
+def _u(op, fn, x=_X, **attrs):
+    return (op, {"X": [("x", x, True)]}, {"Out": ["o"]}, attrs, lambda: [fn(x)])
+
+
+def _ui(op, fn, x=_X, **attrs):
+    return (op, {"Input": [("x", x, True)]}, {"Out": ["o"]}, attrs, lambda: [fn(x)])
+
+
+def _np_sigmoid(v):
+    return 1 / (1 + np.exp(-v))
+
+
+COVERAGE = [
+    _u("abs", np.abs), _u("acos", np.arccos, np.clip(_X, -0.9, 0.9)), _u("asin", np.arcsin, np.clip(_X, -0.9, 0.9)),
+    _u("atan", np.arctan), _u("ceil", np.ceil), _u("cos", np.cos), _u("cosh", np.cosh), _u("floor", np.floor),
+    _u("log", np.log, _P), _u("log1p", np.log1p, _P), _u("log2", np.log2, _P), _u("log10", np.log10, _P),
+    _u("reciprocal", lambda v: 1 / v, _P), _u("round", np.round), _u("rsqrt", lambda v: 1 / np.sqrt(v), _P),
+    _u("sin", np.sin), _u("sinh", np.sinh), _u("square", np.square), _u("tan", np.tan),
+    _u("softsign", lambda v: v / (1 + np.abs(v))), _u("expm1", np.expm1), _u("sign", np.sign),
+    _u("logsigmoid", lambda v: np.log(_np_sigmoid(v))), _u("tanh_shrink", lambda v: v - np.tanh(v)),
+    _u("exp", np.exp), _u("sqrt", np.sqrt, _P), _u("tanh", np.tanh), _u("relu", lambda v: np.maximum(v, 0)),
+    _u("sigmoid", _np_sigmoid), _u("silu", lambda v: v * _np_sigmoid(v)),
+    _u("relu6", lambda v: np.clip(v, 0, 0.5), threshold=0.5),
+    _u("leaky_relu", lambda v: np.where(v > 0, v, 0.1 * v), alpha=0.1),
+    _u("elu", lambda v: np.where(v > 0, v, 0.5 * (np.exp(v) - 1)), alpha=0.5),
+    _u("swish", lambda v: v * _np_sigmoid(2.0 * v), beta=2.0),
+    _u("hard_swish", lambda v: v * np.clip(v + 3, 0, 6) / 6, threshold=6.0, scale=6.0, offset=3.0),
+    _u("hard_sigmoid", lambda v: np.clip(0.25 * v + 0.5, 0, 1), slope=0.25, offset=0.5),
+    _u("softshrink", lambda v: np.where(v > 0.3, v - 0.3, np.where(v < -0.3, v + 0.3, 0)), **{"lambda": 0.3}),
+    _u("hard_shrink", lambda v: np.where(np.abs(v) > 0.4, v, 0), threshold=0.4),
+    _u("thresholded_relu", lambda v: np.where(v > 0.2, v, 0), threshold=0.2),
+    _u("brelu", lambda v: np.clip(v, -0.5, 0.5), t_min=-0.5, t_max=0.5),
+    _u("stanh", lambda v: 1.7159 * np.tanh(0.67 * v), scale_a=0.67, scale_b=1.7159),
+    _u("softplus", lambda v: np.log1p(np.exp(v))),
+    _u("mish", lambda v: v * np.tanh(np.log1p(np.exp(v)))),
+    _u("log_softmax", lambda v: v - np.log(np.exp(v).sum(-1, keepdims=True)), axis=-1),
+    _u("softmax", lambda v: np.exp(v) / np.exp(v).sum(-1, keepdims=True), axis=-1),
+    _u("scale", lambda v: 2.0 * v + 1.0, scale=2.0, bias=1.0, bias_after_scale=True),
+    _u("logical_not", np.logical_not, _X > 0), _u("isfinite_v2", np.isfinite), _u("isnan_v2", np.isnan),
+    _u("assign", lambda v: v), _u("fill_zeros_like", np.zeros_like),
+    _u("fill_any_like", lambda v: np.full_like(v, 3.0), value=3.0),
+    _u("mean", lambda v: np.array([v.mean()])), _u("squared_l2_norm", lambda v: np.array([(v * v).sum()])),
+    _u("reduce_sum", lambda v: v.sum(1), dim=[1]), _u("reduce_mean", lambda v: v.mean(2), dim=[2]),
+    _u("reduce_max", lambda v: v.max(1), dim=[1]), _u("reduce_min", lambda v: v.min(1), dim=[1]),
+    _u("reduce_prod", lambda v: v.prod(2), dim=[2]), _u("reduce_all", lambda v: v.all(1), _X > -1, dim=[1]),
+    _u("reduce_any", lambda v: v.any(1), _X > 1, dim=[1]),
+    _u("cumsum", lambda v: np.cumsum(v, 1), axis=1),
+    _u("clip", lambda v: np.clip(v, -0.5, 0.5), min=-0.5, max=0.5),
+    _u("transpose2", lambda v: v.transpose(2, 0, 1), axis=[2, 0, 1]),
+    _u("transpose", lambda v: v.transpose(1, 0, 2), axis=[1, 0, 2]),
+    _u("reshape2", lambda v: v.reshape(2, 12), shape=[0, -1]), _u("reshape", lambda v: v.reshape(6, 4), shape=[6, 4]),
+    _u("flatten_contiguous_range", lambda v: v.reshape(2, 12), start_axis=1, stop_axis=2),
+    _u("flatten2", lambda v: v.reshape(6, 4), axis=2), _u("flatten", lambda v: v.reshape(2, 12), axis=1),
+    _u("unsqueeze2", lambda v: v[:, None], axes=[1]), _u("unsqueeze", lambda v: v[..., None], axes=[3]),
+    _u("squeeze2", lambda v: v[:, 0], _X[:, :1], axes=[1]), _u("squeeze", lambda v: v[:, 0], _X[:, :1], axes=[1]),
+    _u("tile", lambda v: np.tile(v, (1, 2, 1)), repeat_times=[1, 2, 1]),
+    _u("expand_v2", lambda v: np.broadcast_to(v, (2, 3, 4)), _X[:1], shape=[2, -1, -1]),
+    _u("expand", lambda v: np.tile(v, (2, 1, 1)), _X[:1], expand_times=[2, 1, 1]),
+    _u("arg_max", lambda v: v.argmax(1), axis=1, keepdims=False, flatten=False, dtype=3),
+    _u("arg_min", lambda v: v.argmin(2), axis=2),
+    _u("cast", lambda v: v.astype("int64"), np.array([1.5, -2.7, 3.1], "float32"), in_dtype=5, out_dtype=3),
+    _ui("slice", lambda v: v[:, 1:3], axes=[1], starts=[1], ends=[3]),
+    _ui("strided_slice", lambda v: v[:, ::2, 1:], axes=[1, 2], starts=[0, 1], ends=[3, 4], strides=[2, 1]),
+    _u("pad", lambda v: np.pad(v, ((0, 0), (1, 0), (0, 2)), constant_values=1.5), paddings=[0, 0, 1, 0, 0, 2],
+       pad_value=1.5),
+    _u("pad2d", lambda v: np.pad(v, ((0, 0), (0, 0), (1, 1), (0, 2)), mode="reflect"), _IMG,
+       paddings=[1, 1, 0, 2], mode="reflect"),
+    _u("pad3d", lambda v: np.pad(v, ((0, 0), (0, 0), (1, 0), (0, 1), (2, 2))), _IMG[None],
+       paddings=[2, 2, 0, 1, 1, 0], mode="constant", value=0.0),
+    _u("tril_triu", lambda v: np.triu(v), _X[0], diagonal=0, lower=False),
+    _ui("shape", lambda v: np.array(v.shape, "int32")),
+    _u("roll", lambda v: np.roll(v, 1, axis=2), shifts=[1], axis=[2]),
+    _u("flip", lambda v: v[:, ::-1], axis=[1]),
+    _u("p_norm", lambda v: np.sqrt((v * v).sum(-1)), porder=2.0, axis=-1),
+    _u("pixel_shuffle", lambda v: v.reshape(1, 1, 2, 2, 4, 4).transpose(0, 1, 4, 2, 5, 3).reshape(1, 1, 8, 8),
+       _IMG, upscale_factor=2),
+    _u("shuffle_channel", lambda v: v.reshape(1, 2, 2, 4, 4).transpose(0, 2, 1, 3, 4).reshape(1, 4, 4, 4), _IMG,
+       group=2),
+    _u("nearest_interp_v2", lambda v: v.repeat(2, 2).repeat(2, 3), _IMG, out_h=8, out_w=8, interp_method="nearest",
+       align_corners=False),
+    _u("maxout", lambda v: v.reshape(1, 2, 2, 4, 4).max(2), _IMG, groups=2),
+    _u("space_to_depth", lambda v: v.reshape(1, 2, 2, 1, 4, 4).transpose(0, 3, 4, 1, 5, 2).reshape(1, 16, 2, 2),
+       _IMG, blocksize=2),
+    _u("one_hot_v2", lambda v: np.eye(3, dtype="float32")[v], _I, depth=3),
+    _u("one_hot", lambda v: np.eye(3, dtype="float32")[v[:, 0]], _I[:, :1], depth=3),
+    _u("gelu", lambda v: 0.5 * v * (1 + np.vectorize(__import__("math").erf)(v / np.sqrt(2))), approximate=False),
+    # binary
+    *[(op, {"X": [("x", _X, True)], "Y": [("y", _P, True)]}, {"Out": ["o"]}, {}, (lambda f: lambda: [f(_X, _P)])(f))
+      for op, f in [("elementwise_add", np.add), ("elementwise_sub", np.subtract), ("elementwise_mul", np.multiply),
+                    ("elementwise_div", np.divide), ("elementwise_max", np.maximum), ("elementwise_min", np.minimum),
+                    ("elementwise_mod", np.mod), ("elementwise_floordiv", np.floor_divide),
+                    ("less_than", np.less), ("less_equal", np.less_equal), ("greater_than", np.greater),
+                    ("greater_equal", np.greater_equal), ("equal", np.equal), ("not_equal", np.not_equal)]],
+    ("elementwise_pow", {"X": [("x", _P, True)], "Y": [("y", _X, True)]}, {"Out": ["o"]}, {},
+     lambda: [np.power(_P, _X)]),
+    *[(op, {"X": [("x", _X > 0, True)], "Y": [("y", _X > 0.5, True)]}, {"Out": ["o"]}, {},
+       (lambda f: lambda: [f(_X > 0, _X > 0.5)])(f))
+      for op, f in [("logical_and", np.logical_and), ("logical_or", np.logical_or), ("logical_xor", np.logical_xor)]],
+    ("matmul", {"X": [("x", _X, True)], "Y": [("y", _P, True)]}, {"Out": ["o"]},
+     {"transpose_X": False, "transpose_Y": True, "alpha": 0.5}, lambda: [0.5 * _X @ _P.transpose(0, 2, 1)]),
+    ("matmul_v2", {"X": [("x", _X, True)], "Y": [("y", _P, True)]}, {"Out": ["o"]}, {"trans_x": True, "trans_y": False},
+     lambda: [_X.transpose(0, 2, 1) @ _P]),
+    ("bmm", {"X": [("x", _X, True)], "Y": [("y", _P.transpose(0, 2, 1).copy(), True)]}, {"Out": ["o"]}, {},
+     lambda: [_X @ _P.transpose(0, 2, 1)]),
+    ("mul", {"X": [("x", _X, True)], "Y": [("y", _P.reshape(12, 2), False)]}, {"Out": ["o"]},
+     {"x_num_col_dims": 1, "y_num_col_dims": 1}, lambda: [_X.reshape(2, 12) @ _P.reshape(12, 2)]),
+    ("where", {"Condition": [("c", _X > 0, True)], "X": [("x", _X, True)], "Y": [("y", _P, True)]}, {"Out": ["o"]},
+     {}, lambda: [np.where(_X > 0, _X, _P)]),
+    ("where_index", {"Condition": [("c", _X[0] > 0, True)]}, {"Out": ["o"]}, {},
+     lambda: [np.argwhere(_X[0] > 0)]),
+    ("prelu", {"X": [("x", _IMG, True)], "Alpha": [("a", np.full(4, 0.1, "float32"), False)]}, {"Out": ["o"]},
+     {"mode": "channel"}, lambda: [np.where(_IMG > 0, _IMG, 0.1 * _IMG)]),
+    # shape / indexing
+    ("stack", {"X": [("a", _X, True), ("b", _P, True)]}, {"Y": ["o"]}, {"axis": 1}, lambda: [np.stack([_X, _P], 1)]),
+    ("concat", {"X": [("a", _X, True), ("b", _P, True)]}, {"Out": ["o"]}, {"axis": 2},
+     lambda: [np.concatenate([_X, _P], 2)]),
+    ("sum", {"X": [("a", _X, True), ("b", _P, True)]}, {"Out": ["o"]}, {}, lambda: [_X + _P]),
+    ("unstack", {"X": [("x", _X, True)]}, {"Y": ["o0", "o1"]}, {"axis": 0, "num": 2}, lambda: [_X[0], _X[1]]),
+    ("split", {"X": [("x", _X, True)]}, {"Out": ["o0", "o1"]}, {"num": 0, "sections": [1, 3], "axis": 2},
+     lambda: [_X[..., :1], _X[..., 1:]]),
+    ("gather", {"X": [("x", _X, True)], "Index": [("i", np.array([2, 0], "int64"), True)]}, {"Out": ["o"]},
+     {"axis": 1}, lambda: [_X[:, [2, 0]]]),
+    ("gather_nd", {"X": [("x", _X, True)], "Index": [("i", np.array([[1, 2], [0, 1]], "int64"), True)]},
+     {"Out": ["o"]}, {}, lambda: [_X[[1, 0], [2, 1]]]),
+    ("index_select", {"X": [("x", _X, True)], "Index": [("i", np.array([3, 1], "int64"), True)]}, {"Out": ["o"]},
+     {"dim": 2}, lambda: [_X[:, :, [3, 1]]]),
+    ("scatter", {"X": [("x", _X[0], True)], "Ids": [("i", np.array([2], "int64"), True)],
+                 "Updates": [("u", _P[0, :1], True)]}, {"Out": ["o"]}, {"overwrite": True},
+     lambda: [np.concatenate([_X[0, :2], _P[0, :1]])]),
+    ("top_k_v2", {"X": [("x", _X, True)]}, {"Out": ["v"], "Indices": ["i"]}, {"k": 2, "axis": -1},
+     lambda: [-np.sort(-_X, -1)[..., :2], np.argsort(-_X, -1, kind="stable")[..., :2]]),
+    ("top_k", {"X": [("x", _X, True)]}, {"Out": ["v"], "Indices": ["i"]}, {"k": 1},
+     lambda: [_X.max(-1, keepdims=True), _X.argmax(-1)[..., None]]),
+    ("argsort", {"X": [("x", _X, True)]}, {"Out": ["v"], "Indices": ["i"]}, {"axis": 1, "descending": False},
+     lambda: [np.sort(_X, 1), np.argsort(_X, 1, kind="stable")]),
+    ("lookup_table_v2", {"Ids": [("i", _I, True)], "W": [("w", _P[0].T.copy(), False)]}, {"Out": ["o"]},
+     {"padding_idx": -1}, lambda: [_P[0].T[_I]]),
+    ("lookup_table", {"Ids": [("i", _I[:, :1], True)], "W": [("w", _P[0].T.copy(), False)]}, {"Out": ["o"]},
+     {"padding_idx": -1}, lambda: [_P[0].T[_I[:, 0]]]),
+    ("range", {"Start": [("s", np.array([1.0], "float32"), True)], "End": [("e", np.array([7.0], "float32"), True)],
+               "Step": [("st", np.array([2.0], "float32"), True)]}, {"Out": ["o"]}, {},
+     lambda: [np.arange(1.0, 7.0, 2.0)]),
+    ("fill_constant", {}, {"Out": ["o"]}, {"shape": [2, 2], "value": 1.25, "dtype": 5},
+     lambda: [np.full((2, 2), 1.25)]),
+    ("fill_constant_batch_size_like", {"Input": [("x", _X, True)]}, {"Out": ["o"]},
+     {"shape": [-1, 5], "value": 2.0, "dtype": 5, "input_dim_idx": 0, "output_dim_idx": 0},
+     lambda: [np.full((2, 5), 2.0)]),
+    ("assign_value", {}, {"Out": ["o"]}, {"shape": [2], "dtype": 5, "fp32_values": [1.5, 2.5]},
+     lambda: [np.array([1.5, 2.5])]),
+    ("expand_as_v2", {"X": [("x", _X[:1], True)]}, {"Out": ["o"]}, {"target_shape": [2, 3, 4]},
+     lambda: [np.broadcast_to(_X[:1], (2, 3, 4))]),
+    # normalisation / nn
+    ("layer_norm", {"X": [("x", _X, True)], "Scale": [("s", np.ones(4, "float32"), False)],
+                    "Bias": [("b", np.zeros(4, "float32"), False)]}, {"Y": ["o"]}, {"epsilon": 1e-5,
+                                                                                   "begin_norm_axis": 2},
+     lambda: [(_X - _X.mean(-1, keepdims=True)) / np.sqrt(_X.var(-1, keepdims=True) + 1e-5)]),
+    ("instance_norm", {"X": [("x", _IMG, True)]}, {"Y": ["o"]}, {"epsilon": 1e-5},
+     lambda: [(_IMG - _IMG.mean((2, 3), keepdims=True)) / np.sqrt(_IMG.var((2, 3), keepdims=True) + 1e-5)]),
+    ("group_norm", {"X": [("x", _IMG, True)]}, {"Y": ["o"]}, {"epsilon": 1e-5, "groups": 2},
+     lambda: [((_IMG.reshape(1, 2, -1) - _IMG.reshape(1, 2, -1).mean(-1, keepdims=True))
+               / np.sqrt(_IMG.reshape(1, 2, -1).var(-1, keepdims=True) + 1e-5)).reshape(_IMG.shape)]),
+    ("affine_channel", {"X": [("x", _IMG, True)], "Scale": [("s", np.arange(4, dtype="float32"), False)],
+                        "Bias": [("b", np.ones(4, "float32"), False)]}, {"Out": ["o"]}, {},
+     lambda: [_IMG * np.arange(4)[None, :, None, None] + 1]),
+    ("pool2d", {"X": [("x", _IMG, True)]}, {"Out": ["o"]}, {"pooling_type": "max", "ksize": [2, 2],
+                                                            "strides": [2, 2], "paddings": [0, 0]},
+     lambda: [_IMG.reshape(1, 4, 2, 2, 2, 2).max((3, 5))]),
+    ("pool3d", {"X": [("x", _IMG[None], True)]}, {"Out": ["o"]}, {"pooling_type": "avg", "ksize": [1, 2, 2],
+                                                                  "strides": [1, 2, 2], "paddings": [0, 0, 0]},
+     lambda: [_IMG[None].reshape(1, 1, 4, 2, 2, 2, 2).mean((4, 6))]),
+    ("conv2d", {"Input": [("x", _IMG, True)], "Filter": [("w", np.ones((2, 4, 1, 1), "float32"), False)]},
+     {"Output": ["o"]}, {"strides": [1, 1], "paddings": [0, 0], "dilations": [1, 1], "groups": 1},
+     lambda: [np.repeat(_IMG.sum(1, keepdims=True), 2, 1)]),
+    ("depthwise_conv2d", {"Input": [("x", _IMG, True)], "Filter": [("w", np.full((4, 1, 1, 1), 2.0, "float32"),
+                                                                     False)]},
+     {"Output": ["o"]}, {"strides": [1, 1], "paddings": [0, 0], "dilations": [1, 1], "groups": 4},
+     lambda: [2 * _IMG]),
+    ("conv2d_transpose", {"Input": [("x", _IMG, True)], "Filter": [("w", np.ones((4, 1, 1, 1), "float32"), False)]},
+     {"Output": ["o"]}, {"strides": [1, 1], "paddings": [0, 0], "dilations": [1, 1], "groups": 1},
+     lambda: [_IMG.sum(1, keepdims=True)]),
+    ("dropout", {"X": [("x", _X, True)]}, {"Out": ["o"]}, {"dropout_prob": 0.25}, lambda: [0.75 * _X]),
+]
+
+
+def test_op_coverage_table_size():
+    from paddle_hackathon_amd.static import serialize as S
+    types = {c[0] for c in COVERAGE}
+    assert len(types) >= 100, len(types)
+    missing = [t for t in types if t not in S._CONVERT and t not in S._ref.CF]
+    assert not missing, missing
+    assert len(S._CONVERT) + len(S._ref.CF) >= 150
+
+
+@pytest.mark.parametrize("case", COVERAGE, ids=[c[0] for c in COVERAGE])
+def test_reference_op_round_trip(case, tmp_path):
+    op_type, inputs, outputs, attrs, ref = case
+    prog, feeds, fetches = _single_op_program(tmp_path, op_type, inputs, outputs, attrs)
+    feed = {v: a for lst in inputs.values() for v, a, f in lst if f}
+    outs = paddle.static.Executor().run(prog, feed=feed, fetch_list=fetches)
+    for got, want in zip(outs, ref()):
+        want = np.asarray(want)
+        assert tuple(np.shape(got)) == tuple(want.shape), (op_type, np.shape(got), want.shape)
+        np.testing.assert_allclose(np.asarray(got, dtype="float64"), want.astype("float64"), rtol=1e-4, atol=1e-5,
+                                   err_msg=op_type)
+    # written again by the framework and read back: same results
+    if op_type not in ("fill_constant", "assign_value"):
+        prefix = str(tmp_path / "again")
+        feed_vars = [v for v in prog.global_block().vars.values() if getattr(v, "is_data", False)]
+        paddle.static.save_inference_model(prefix, feed_vars, fetches, program=prog)
+        prog2, _, fetches2 = paddle.static.load_inference_model(prefix)
+        outs2 = paddle.static.Executor().run(prog2, feed=feed, fetch_list=fetches2)
+        for a, b in zip(outs, outs2):
+            np.testing.assert_allclose(np.asarray(a, dtype="float64"), np.asarray(b, dtype="float64"), rtol=1e-6)
+
+
+def test_reference_layout_while_and_conditional_block(tmp_path):
+    """1.x While / conditional_block layout: block 1 is the loop body (increments i, accumulates,
+    recomputes the condition into the same variable), block 2 the branch taken when acc > 10"""
+    import torch
+    desc = pb.ProgramDesc()
+    g = desc.blocks.add()
+    g.idx, g.parent_idx = 0, -1
+    body = desc.blocks.add()
+    body.idx, body.parent_idx = 1, 0
+    br = desc.blocks.add()
+    br.idx, br.parent_idx = 2, 0
+    for n, d in (("n", [1]), ("i", [1]), ("acc", [1]), ("c", [1]), ("one", [1]), ("ten", [1]), ("big", [1]),
+                 ("res", [1])):
+        _var(g, n, d, dtype=0 if n in ("c", "big") else 5)
+    _op(g, "feed", {"X": ["feed"]}, {"Out": ["n"]}, col=0)
+    _op(g, "fill_constant", {}, {"Out": ["i"]}, shape=[1], value=0.0, dtype=5)
+    _op(g, "fill_constant", {}, {"Out": ["acc"]}, shape=[1], value=0.0, dtype=5)
+    _op(g, "fill_constant", {}, {"Out": ["one"]}, shape=[1], value=1.0, dtype=5)
+    _op(g, "fill_constant", {}, {"Out": ["ten"]}, shape=[1], value=10.0, dtype=5)
+    _op(g, "fill_constant", {}, {"Out": ["res"]}, shape=[1], value=-1.0, dtype=5)
+    _op(g, "less_than", {"X": ["i"], "Y": ["n"]}, {"Out": ["c"]})
+    w = _op(g, "while", {"X": ["i", "acc", "n"], "Condition": ["c"]}, {"Out": ["i", "acc"], "StepScopes": ["ss"]})
+    a = w.attrs.add()
+    a.name, a.type, a.block_idx = "sub_block", pb.BLOCK, 1
+    _op(body, "elementwise_add", {"X": ["acc"], "Y": ["i"]}, {"Out": ["acc"]}, axis=-1)
+    _op(body, "increment", {"X": ["i"]}, {"Out": ["i"]}, step=1.0)
+    _op(body, "less_than", {"X": ["i"], "Y": ["n"]}, {"Out": ["c"]})
+    _op(g, "greater_than", {"X": ["acc"], "Y": ["ten"]}, {"Out": ["big"]})
+    cb = _op(g, "conditional_block", {"Cond": ["big"], "Input": ["acc"]}, {"Out": ["res"], "Scope": ["sc"]},
+             is_scalar_condition=True)
+    a = cb.attrs.add()
+    a.name, a.type, a.block_idx = "sub_block", pb.BLOCK, 2
+    _op(br, "scale", {"X": ["acc"]}, {"Out": ["res"]}, scale=2.0, bias=0.0, bias_after_scale=True)
+    _op(g, "fetch", {"X": ["acc"]}, {"Out": ["fetch"]}, col=0)
+    _op(g, "fetch", {"X": ["res"]}, {"Out": ["fetch"]}, col=1)
+    prefix = str(tmp_path / "loop")
+    open(prefix + ".pdmodel", "wb").write(desc.SerializeToString())
+    pb.save_combine([], prefix + ".pdiparams")
+    prog, feeds, fetches = paddle.static.load_inference_model(prefix)
+    exe = paddle.static.Executor()
+    acc, res = exe.run(prog, feed={"n": np.array([5.0], "float32")}, fetch_list=fetches)
+    assert float(acc[0]) == 10.0 and float(res[0]) == -1.0       # 0+1+2+3+4, branch not taken
+    acc, res = exe.run(prog, feed={"n": np.array([6.0], "float32")}, fetch_list=fetches)
+    assert float(acc[0]) == 15.0 and float(res[0]) == 30.0
+    _ = torch
