@@ -212,16 +212,20 @@ class RecomputeOptimizer:
 
 
 class PipelineOptimizer:
-    """1.x static pipeline wrapper: ``num_microbatches`` micro-batches per step with gradient
-    accumulation over them (one stage here; multi-stage pipelines run through
-    fleet.meta_parallel.PipelineLayer, parallel/pipeline.py)"""
+    """1.x static pipeline: the program's ``device_guard("gpu:k")`` sections become stages, one
+    per rank, run over ``num_microbatches`` micro-batches with point-to-point activation and
+    gradient transfers (parallel/fleet/static_pipeline.py). Dygraph pipelines use
+    fleet.meta_parallel.PipelineLayer (parallel/pipeline.py)."""
 
     def __init__(self, optimizer, num_microbatches=1, start_cpu_core_id=0):
+        from ..parallel.fleet.static_pipeline import PipelineOptimizer as _P
+        self._impl = _P(optimizer, num_microbatches)
         self._optimizer = optimizer
-        self._num_microbatches = num_microbatches
 
     def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
-        return self._optimizer.minimize(loss, startup_program, parameter_list, no_grad_set)
+        if _core.in_dynamic_mode():
+            return self._optimizer.minimize(loss, startup_program, parameter_list, no_grad_set)
+        return self._impl.minimize(loss, startup_program, parameter_list, no_grad_set)
 
     def __getattr__(self, item):
         return getattr(self._optimizer, item)

@@ -210,7 +210,13 @@ class Fleet:
             self._ps.strategy = self._strategy
             return PSOptimizer(optimizer, self._ps, self._strategy)
         if not _core_in_dynamic():
-            # static graph: meta-optimizers rewrite the Program (static_optimizers.py)
+            # static graph: meta-optimizers rewrite the Program (static_optimizers.py); pipeline
+            # parallelism runs the stage program of this rank (static_pipeline.py)
+            st = self._strategy
+            if st is not None and getattr(st, "pipeline", False):
+                from .static_pipeline import PipelineOptimizer
+                cfg = dict(getattr(st, "pipeline_configs", {}) or {})
+                return PipelineOptimizer(optimizer, int(cfg.get("accumulate_steps", 1)))
             from .static_optimizers import StaticFleetOptimizer
             return StaticFleetOptimizer(optimizer, self._strategy)
         if self._hcg is None:

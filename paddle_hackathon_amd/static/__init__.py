@@ -70,13 +70,22 @@ set_ipu_shard = ipu_shard_guard
 
 
 class device_guard:
+    """ops recorded inside carry ``op_device`` = ``device`` ("gpu:k" names pipeline stage k for
+    the static pipeline pass, parallel/fleet/static_pipeline.py; reference fluid/framework.py
+    device_guard)"""
+
     def __init__(self, device=None):
         self.device = device
 
     def __enter__(self):
+        from .program import _OP_DEVICE
+        self.prev = _OP_DEVICE[0]
+        _OP_DEVICE[0] = self.device
         return self
 
     def __exit__(self, *a):
+        from .program import _OP_DEVICE
+        _OP_DEVICE[0] = self.prev
         return False
 
 

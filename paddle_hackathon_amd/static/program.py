@@ -415,10 +415,15 @@ def record_op(fn, name, args, kwargs):
     blk = default_main_program().current_block()
     outs = _outputs_to_vars(meta_out, blk)
     op = OpDesc(qual, fn, bargs, bkw, outs)
+    if _OP_DEVICE[0] is not None:     # static.device_guard: pipeline stage / placement of the op
+        op.attrs["op_device"] = _OP_DEVICE[0]
     for v in _iter_vars(outs):
         v.op = op
     blk.append_op(op)
     return outs
+
+
+_OP_DEVICE = [None]
 
 
 # ----------------------------------------------------------------------------- backward / optimize ops
@@ -803,6 +808,10 @@ class Executor:
             program = default_main_program()
         # fluid py_reader / DataLoader.from_generator attached to the program: a run without an
         # explicit feed pulls the next batch (EOFException ends the pass)
+        pipe = program.__dict__.get("_pipeline") if not isinstance(program, CompiledProgram) else None
+        if pipe is not None:      # static pipeline parallelism: this rank's stage over micro-batches
+            outs = pipe.run(feed or {}, fetch_list or [])
+            return [o.numpy() if isinstance(o, Tensor) and return_numpy else o for o in outs]
         readers = [r for r in program.__dict__.get("_py_readers", ()) if getattr(r, "_it", None) is not None]
         if readers and not feed:
             feed = {}

@@ -88,6 +88,24 @@ _REF = {
     "nn.functional.pooling.avg_pool2d": ("pool2d", {"x": "X"}, "Out", {"kernel_size": "ksize", "stride": "strides",
                                                                        "padding": "paddings"}),
 }
+_FLUID_SLOTS = {"x": "X", "y": "Y", "input": "X", "label": "Label", "index": "Index", "updates": "Updates",
+                "condition": "Condition", "ids": "Ids"}
+_FLUID_TYPE = {"topk": "top_k", "reshape": "reshape2", "transpose": "transpose2", "squeeze": "squeeze2",
+               "unsqueeze": "unsqueeze2", "flatten": "flatten2", "expand": "expand"}
+
+
+def _fluid_ref(short):
+    """a recorded 1.x layer (fluid.layers.*) whose name is a reference op type: emitted under that
+    type, tensors in the reference slots, scalar arguments as same-named attributes"""
+    if not short.startswith("fluid.layers."):
+        return None
+    name = short.rsplit(".", 1)[-1]
+    typ = _FLUID_TYPE.get(name, name)
+    if typ not in _CONVERT and typ not in ("reduce_prod", "reduce_all", "reduce_any"):
+        return None
+    return (typ, _FLUID_SLOTS, "Out", {})
+
+
 _EXTRA_ATTRS = {
     "nn.functional.pooling.max_pool2d": {"pooling_type": "max"},
     "nn.functional.pooling.avg_pool2d": {"pooling_type": "avg"},
@@ -243,7 +261,7 @@ class _Writer:
         if op.exec is not None:
             self._cf_op(op, msg, ins, outs)
         else:
-            ref = _REF.get(short)
+            ref = _REF.get(short) or _fluid_ref(short)
             slot_of = ref[1] if ref else {}
             msg.type = ref[0] if ref else op.type
             args_j = self.enc(list(op.args), "args", ins) if op.args else []

@@ -589,3 +589,29 @@ def test_reference_layout_while_and_conditional_block(tmp_path):
     acc, res = exe.run(prog, feed={"n": np.array([6.0], "float32")}, fetch_list=fetches)
     assert float(acc[0]) == 15.0 and float(res[0]) == 30.0
     _ = torch
+
+
+def test_fluid_layers_are_written_as_reference_types(tmp_path):
+    from paddle_hackathon_amd import fluid
+    from paddle_hackathon_amd.fluid import layers
+    paddle.enable_static()
+    try:
+        main = fluid.Program()
+        with fluid.program_guard(main, fluid.Program()):
+            x = layers.data("x", [4], dtype="float32")
+            y = layers.hard_swish(layers.elementwise_mul(x, layers.relu6(x), axis=-1))
+            y = layers.reduce_sum(layers.leaky_relu(y, 0.1), dim=[1])
+            exe = fluid.Executor()
+            xv = np.random.RandomState(0).randn(3, 4).astype("float32")
+            ref, = exe.run(main, feed={"x": xv}, fetch_list=[y])
+            fluid.io.save_inference_model(str(tmp_path), ["x"], [y], exe, main)
+    finally:
+        paddle.disable_static()
+    desc = pb.ProgramDesc()
+    desc.ParseFromString(open(str(tmp_path / "__model__"), "rb").read())
+    types = [op.type for op in desc.blocks[0].ops]
+    for t in ("elementwise_mul", "relu6", "hard_swish", "leaky_relu", "reduce_sum"):
+        assert t in types, types
+    prog, feeds, fetches = fluid.io.load_inference_model(str(tmp_path), fluid.Executor())
+    got, = fluid.Executor().run(prog, feed={"x": xv}, fetch_list=fetches)
+    np.testing.assert_allclose(got, ref, rtol=1e-5)
