@@ -191,9 +191,30 @@ class _AutogradGraphs:
     def __init__(self, fn, args, kwargs, params, mode, pool):
         ins = _tensors_of((args, kwargs), [])
         self.static_in = [t.detach().clone().requires_grad_(t.requires_grad) for t in ins]
-        self.params = [p for p in params if p.requires_grad]
+        # a wrapped Layer's parameters (framework Parameters, whose torch tensor is ``_t``): during
+        # warmup and capture the Layer runs on fresh leaf aliases of the same storage. The real
+        # leaves' AccumulateGrad nodes were made by eager calls on another stream and may still be
+        # referenced by the caller's last autograd graph; routing the captured backward through them
+        # makes autograd join the capture with that stream (an invalid capture: the HIP runtime
+        # crashed at instantiation). Replays read the parameters' live storage; _GraphedCall hands
+        # the captured gradients to the real leaves.
+        owners = [p for p in params if getattr(p, "_t", p).requires_grad]
+        self.params = [getattr(p, "_t", p) for p in owners]
+        aliases = [t.detach().requires_grad_(True) for t in self.params]
+        swap = [o for o in owners if hasattr(o, "_t")]
+        for o, a in zip(owners, aliases):
+            if hasattr(o, "_t"):
+                o._t = a
+        try:
+            self._capture(fn, args, kwargs, aliases if swap else self.params, mode, pool)
+        finally:
+            for o, t in zip(owners, self.params):
+                if hasattr(o, "_t"):
+                    o._t = t
+
+    def _capture(self, fn, args, kwargs, params, mode, pool):
         sargs, skw = _rebuild((args, kwargs), iter(self.static_in))
-        diff = [t for t in self.static_in if t.requires_grad] + self.params
+        diff = [t for t in self.static_in if t.requires_grad] + list(params)
         stream = torch.cuda.Stream()
         stream.wait_stream(torch.cuda.current_stream())
         # warm the autograd path on the capture stream (lazy init, allocator growth)
@@ -317,7 +338,7 @@ class GraphedFunction:
             return False
         if any(t.requires_grad for t in _tensors_of((args, kwargs), [])):
             return True
-        return self._params is not None and any(p.requires_grad for p in self._params())
+        return self._params is not None and any(getattr(p, "_t", p).requires_grad for p in self._params())
 
     def __call__(self, *args, **kwargs):
         if not is_cuda_graph_supported():
@@ -390,8 +411,7 @@ def wrap_cuda_graph(function, mode="thread_local", memory_pool="default", warmup
         return _static_guard(function, mode, memory_pool)
     if isinstance(function, Layer):
         layer = function
-        gf = GraphedFunction(layer.forward, mode, memory_pool, warmup,
-                             params=lambda: [p._t for p in layer.parameters()])
+        gf = GraphedFunction(layer.forward, mode, memory_pool, warmup, params=lambda: list(layer.parameters()))
         layer._cuda_graph = gf
         layer.forward = gf
         return layer
