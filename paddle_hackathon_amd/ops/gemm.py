@@ -11,8 +11,9 @@ the epilogues folded in:
   * forward fc1:   h = x @ W1 + b1 stored as pre-activation AND a = gelu(h) in one pass
   * backward fc2-dgrad: dH = (dY @ W2^T) * gelu'(h) with the bias-gradient column sums of dH
 
-Operands need K % 64 == 0 and M, N, row strides % 8 == 0 (``supported``); anything else goes to
-the caller's fallback.
+Operands need K % 64 == 0 and M, N, row strides % 8 == 0 (``supported``); the ``mm_*`` entry
+points zero-pad tails (K to 64, M / N to 8) so odd shapes (vocab 30522, a handful of masked
+tokens, a batch of 8) stay on the own kernels.
 """
 from __future__ import annotations
 
@@ -207,8 +208,12 @@ def _own_ok(layout, *ts):
     impl = _impl()
     if impl == "library" or (impl == "auto" and layout not in _AUTO_OWN):
         return False
-    return all(t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
-               for t in ts) and _lib.native_available()
+    return all(t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 for t in ts) \
+        and _lib.native_available()
+
+
+def _c(t):
+    return t if t.stride(1) == 1 else t.contiguous()
 
 
 def _lib_call(layout, name, shape, fn):
@@ -230,12 +235,33 @@ def _splits(M, N, K, dev):
     return sp
 
 
+def _pad2(t, rm, cm):
+    """zero-padded contiguous copy of 2-D ``t`` with rows % rm == 0 and cols % cm == 0 (t itself
+    when already aligned): K tails must read zeros, and M / N / row strides need 16-B alignment"""
+    R, C = t.shape
+    Rp, Cp = -(-R // rm) * rm, -(-C // cm) * cm
+    if (Rp, Cp) == (R, C) and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0:
+        return t
+    out = torch.zeros(Rp, Cp, dtype=t.dtype, device=t.device)
+    out[:R, :C] = t
+    return out
+
+
+def _own_fits(t):
+    """the padded row stride still fits the kernel's 32-bit tile offsets"""
+    return (t.shape[1] + 64) * 256 * 2 < 2 ** 32
+
+
 def mm_nt(a, bt):
     """a [M, K] @ bt[N, K]^T"""
     M, K = a.shape
     N = bt.shape[0]
-    if _own_ok("nt", a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
-        return gemm_p(a, bt, False, False)
+    if _own_ok("nt", a, bt) and bt.dtype == a.dtype:
+        a, bt = _c(a), _c(bt)
+        if supported(M, N, K, a, bt):
+            return gemm_p(a, bt, False, False)
+        if _own_fits(a) and _own_fits(bt):
+            return gemm_p(_pad2(a, 8, 64), _pad2(bt, 8, 64), False, False)[:M, :N]
     return _lib_call("nt", "nt", (M, N, K), lambda: a @ bt.t())
 
 
@@ -243,8 +269,13 @@ def mm_nt_bias(a, bt, bias):
     """a [M, K] @ bt[N, K]^T + bias (bias folded into the own kernel's epilogue)"""
     M, K = a.shape
     N = bt.shape[0]
-    if _own_ok("nt", a, bt) and bt.dtype == a.dtype and supported(M, N, K, a, bt):
-        return gemm_p(a, bt, False, False, bias=bias)
+    if _own_ok("nt", a, bt) and bt.dtype == a.dtype:
+        a, bt = _c(a), _c(bt)
+        if supported(M, N, K, a, bt):
+            return gemm_p(a, bt, False, False, bias=bias)
+        if _own_fits(a) and _own_fits(bt):
+            bp = bias if N % 8 == 0 else torch.nn.functional.pad(bias.float(), (0, -(-N // 8) * 8 - N))
+            return gemm_p(_pad2(a, 8, 64), _pad2(bt, 8, 64), False, False, bias=bp)[:M, :N]
     return _lib_call("nt", "nt+bias", (M, N, K), lambda: torch.addmm(bias, a, bt.t()))
 
 
@@ -258,8 +289,12 @@ def mm_nn(a, b):
     """a [M, K] @ b [K, N]"""
     M, K = a.shape
     N = b.shape[1]
-    if _own_ok("nn", a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
-        return nn_p(a, b)
+    if _own_ok("nn", a, b) and b.dtype == a.dtype:
+        a, b = _c(a), _c(b)
+        if supported(M, N, K, a, b):
+            return nn_p(a, b)
+        if _own_fits(a) and _own_fits(b):
+            return nn_p(_pad2(a, 8, 64), _pad2(b, 64, 8))[:M, :N]
     return _lib_call("nn", "nn", (M, N, K), lambda: a @ b)
 
 
@@ -267,6 +302,11 @@ def mm_tn(a, b):
     """a [K, M]^T @ b [K, N] (weight gradients: x^T dY), split-K when the tile grid is small"""
     K, M = a.shape
     N = b.shape[1]
-    if _own_ok("tn", a, b) and b.dtype == a.dtype and supported(M, N, K, a, b):
-        return gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device))
+    if _own_ok("tn", a, b) and b.dtype == a.dtype:
+        a, b = _c(a), _c(b)
+        if supported(M, N, K, a, b):
+            return gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device))
+        if _own_fits(a) and _own_fits(b):
+            ap, bp = _pad2(a, 64, 8), _pad2(b, 64, 8)
+            return gemm_p(ap, bp, True, True, splits=_splits(ap.shape[1], bp.shape[1], ap.shape[0], a.device))[:M, :N]
     return _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)

@@ -1132,6 +1132,30 @@ def _train_steps(model, loss_fn, opt, steps=2):
     return float(loss.item())
 
 
+@pytest.mark.parametrize("M,N,K", [(4, 30522, 128), (30522, 128, 4), (8, 1000, 2048), (2048, 1000, 8),
+                                   (100, 72, 200)])
+def test_gemm_tail_padding(M, N, K, monkeypatch):
+    """odd tails (vocab 30522, 4 masked tokens, batch 8) run on the own kernels through the
+    zero-padded entry points, matching an fp32 reference in every layout"""
+    from paddle_hackathon_amd.ops import gemm as G, fallback
+    monkeypatch.setenv("PHA_GEMM_IMPL", "own")
+    fallback.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    bt = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda", generator=g)
+    ref = a.float() @ bt.float().t()
+    outs = {"nt": G.mm_nt(a, bt), "nt_bias": G.mm_nt_bias(a, bt, bias), "nn": G.mm_nn(a, bt.t().contiguous()),
+            "tn": G.mm_tn(a.t().contiguous(), bt.t().contiguous())}
+    torch.cuda.synchronize()
+    assert fallback.total() == 0, fallback.counts()
+    for k, o in outs.items():
+        r = ref + bias if k == "nt_bias" else ref
+        assert o.shape == (M, N), (k, o.shape)
+        err = (o.float() - r).abs().max().item()
+        assert err <= 2e-2 * max(1.0, r.abs().max().item()), (k, err)
+
+
 @pytest.mark.parametrize("impl", ["auto", "own"])
 def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     """GPT (fleet bench model), BERT (vocab 30522, not a multiple of 8) and ResNet-50 (NHWC)
@@ -1144,6 +1168,7 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
         BertPretrainingCriterion
     from paddle_hackathon_amd.vision.models import resnet50
     monkeypatch.setenv("PHA_GEMM_IMPL", impl)
+    monkeypatch.setenv("PHA_FALLBACK_LOG", "1")
     paddle.set_device("gpu")
     paddle.seed(0)
     results = {}
