@@ -168,7 +168,37 @@ def paths():
     print("per-step GEMM ms: " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()), flush=True)
 
 
+def nnform():
+    """x @ W and dY @ W^T as the NN-form kernel (K-outer weight operand, transposed store) vs the
+    own NT kernel vs hipBLASLt NT, per GPT-1.3B shape"""
+    T = 32768
+    tot = {"lib": 0.0, "nt": 0.0, "nn": 0.0}
+    for name, K, N in [("qkv", 2048, 6144), ("out", 2048, 2048), ("fc1", 2048, 8192), ("fc2", 8192, 2048),
+                       ("head", 2048, 50304)]:
+        x, wt, dy = r(T, K), r(N, K), r(T, N)
+        w = wt.t().contiguous()
+        b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+        fl = 2.0 * T * K * N
+        ref = (x.float() @ w.float() + b.float())
+        err = ((G.nn_p(x, w, bias=b).float() - ref).abs().max() / ref.abs().max()).item()
+        n = 24 if name != "head" else 1
+        for lab, fs in [("fwd", {"lib": lambda: torch.addmm(b, x, wt.t()), "nt": lambda: G.gemm_p(x, wt, False, False, bias=b),
+                                 "nn": lambda: G.nn_p(x, w, bias=b)}),
+                        ("dX ", {"lib": lambda: dy @ wt, "nt": lambda: G.gemm_p(dy, w, False, False),
+                                 "nn": lambda: G.nn_p(dy, wt)})]:
+            t = {k: timeit(f, 10 if n > 1 else 3) for k, f in fs.items()}
+            for k in tot:
+                tot[k] += t[k] * n
+            print(f"{name} {lab} {T}x{N if lab == 'fwd' else K}x{K if lab == 'fwd' else N}: "
+                  + "  ".join(f"{k} {fl / v / 1e12:6.0f} TF" for k, v in t.items())
+                  + f"  (nn vs lib {(t['nn'] / t['lib'] - 1) * 100:+.1f}%)  fwd err {err:.1e}", flush=True)
+    print("per-step ms: " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()), flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "nnform":
+        nnform()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "paths":
         paths()
         sys.exit(0)
