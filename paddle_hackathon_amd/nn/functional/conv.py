@@ -1,9 +1,9 @@
 """Convolutions (reference: python/paddle/nn/functional/conv.py, phi/kernels/gpu/conv_*).
 
 Paddle layouts: weight [C_out, C_in/groups, *k] (transpose conv: [C_in, C_out/groups, *k]);
-``data_format`` NCHW or NHWC. NHWC inputs are viewed as NCHW tensors in
-channels-last memory format (no copies), which is the layout gfx950 conv
-kernels want.
+``data_format`` NCHW or NHWC. 2-D convolutions run on the own kernels in NHWC memory for both
+formats (``_own_conv2d``); what they do not take (fp32 dense, 1-D / 3-D, transposed) goes to
+MIOpen and is counted by ops/fallback.py.
 """
 from __future__ import annotations
 
@@ -94,14 +94,62 @@ def _hip_conv_ok(t_nhwc, w, groups):
             and w.dtype == t_nhwc.dtype and groups == 1 and w.shape[0] % 8 == 0 and _lib.require_native())
 
 
+def _own_conv2d(t, w, bias, stride, padding, dilation, groups, data_format):
+    """2-D convolution on the own HIP kernels, or None when they do not take it.
+
+    Physical layout is NHWC either way: an NCHW input is viewed through ``permute(0, 2, 3, 1)``
+    (free when it is already channels-last in memory, one transpose otherwise — typically only the
+    network's input) and the NHWC result is returned as an NCHW view (channels-last memory), so a
+    whole NCHW network stays channels-last after its first layer: BN, pooling and the following
+    convolutions see NHWC memory again (``nhwc_view``).
+    Dense bf16 / fp16 convolutions run on the implicit-GEMM MFMA kernels (ops/conv_gemm.py);
+    grouped / depthwise, dilated + strided and fp32 grouped ones on the direct kernels
+    (ops/grouped_conv.py)."""
+    import os
+    if os.environ.get("PHA_CONV_IMPL", "hip") != "hip" or not t.is_cuda or t.dim() != 4:
+        return None
+    nchw = data_format == "NCHW"
+    x = t.permute(0, 2, 3, 1) if nchw else t
+    st, dl = _tup(stride, 2), _tup(dilation, 2)
+    pad, pre = _padding(padding, 2, list(w.shape[2:]), st, dl, list(x.shape[1:3]))
+    from ...ops import grouped_conv as _gc
+    CO = w.shape[0]
+    wp, bp = w, bias
+    if groups == 1 and CO % 8:   # output channels padded to 8 with zero filters, sliced off below
+        wp = TF.pad(w, [0, 0, 0, 0, 0, 0, 0, -CO % 8])
+        bp = None if bias is None else TF.pad(bias, [0, -CO % 8])
+    dense = _hip_conv_ok(x, wp, groups) and (st == [1, 1] or dl == [1, 1])
+    if not dense and not _gc.ok(x, w, groups):
+        return None
+    x = x.contiguous()
+    if pre is not None:   # asymmetric ("SAME") padding: explicit zero rows / columns
+        x = TF.pad(x, [0, 0, pre[1][0], pre[1][1], pre[0][0], pre[0][1]])
+        pad = [0, 0]
+    if dense:
+        out = _hip_conv2d(x, wp, bp, st, pad, dl, groups)
+        if out.shape[-1] != CO:
+            out = out[..., :CO]
+    else:
+        out = _gc.conv2d_nhwc(x, w, bias, st, pad, dl, groups)
+    return out.permute(0, 3, 1, 2) if nchw else out
+
+
+def nhwc_view(t):
+    """the NHWC tensor whose permute is the 4-D NCHW tensor ``t`` when ``t`` is channels-last in
+    memory (what the own convolutions return), else None"""
+    if t.dim() != 4:
+        return None
+    v = t.permute(0, 2, 3, 1)
+    return v if v.is_contiguous() else None
+
+
 def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     t = x._t
     w = weight._t
-    if n == 2 and data_format == "NHWC" and _hip_conv_ok(t, w, groups):
-        st, dl = _tup(stride, 2), _tup(dilation, 2)
-        pad, pre = _padding(padding, 2, list(w.shape[2:]), st, dl, list(t.shape[1:3]))
-        if pre is None and (st == [1, 1] or dl == [1, 1]):
-            return _w(_hip_conv2d(t.contiguous(), w, None if bias is None else bias._t, st, pad, dl, groups))
+    if n == 2 and data_format in ("NCHW", "NHWC"):
+        out = _own_conv2d(t, w, None if bias is None else bias._t, stride, padding, dilation, groups, data_format)
+        if out is not None:
+            return _w(out)
     if t.is_cuda and n == 2:
         from ...ops import fallback
         fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")

@@ -21,8 +21,9 @@ def _t(x):
 
 def batch_norm(x, running_mean, running_var, weight, bias, training=False, momentum=0.9, epsilon=1e-05,
                data_format="NCHW", use_global_stats=None, name=None):
-    """Channels-last inputs (NHWC/NLC/NDHWC) run the fused HIP BN kernels; channels-first
-    falls back to the library kernel (reference: nn/functional/norm.py:batch_norm)."""
+    """Channels-last inputs (NHWC/NLC/NDHWC, and NCHW tensors whose memory is channels-last — the
+    own convolutions' outputs) run the fused HIP BN kernels; other channels-first tensors use the
+    library kernel (reference: nn/functional/norm.py:batch_norm)."""
     return batch_norm_act(x, running_mean, running_var, weight, bias, training, momentum, epsilon, data_format,
                           use_global_stats)
 
@@ -38,14 +39,26 @@ def batch_norm_act(x, running_mean, running_var, weight, bias, training=False, m
     use_batch = training and not use_global_stats
     rm, rv = _t(running_mean), _t(running_var)
     res = _t(residual)
+    back = False
+    if not cl and t.is_cuda and t.dim() == 4:
+        # NCHW tensor in channels-last memory (what the own convolutions return): the NHWC kernels
+        # on the NHWC view, the result viewed back as NCHW
+        from .conv import nhwc_view
+        v = nhwc_view(t)
+        if v is not None:
+            t, cl, back = v, True, True
+            if res is not None:
+                res = res.permute(0, 2, 3, 1)
     if cl:
+        if res is not None:
+            res = res.contiguous()
         if use_batch:
             out = _ops.fused.batch_norm_train(t.contiguous(), _t(weight), _t(bias), rm, rv, momentum, epsilon, -1,
                                               residual=res, relu=act == "relu")
         else:
             out = _ops.fused.batch_norm_infer(t.contiguous(), _t(weight), _t(bias), rm, rv, epsilon, -1, residual=res,
                                               relu=act == "relu")
-        return _w(out)
+        return _w(out.permute(0, 3, 1, 2) if back else out)
     out = TF.batch_norm(t, rm, rv, _t(weight), _t(bias), use_batch, 1.0 - momentum, epsilon)
     if res is not None:
         out = out + res

@@ -56,13 +56,15 @@ def _pool(n, kind, x, kernel_size, stride, padding, ceil_mode, exclusive, diviso
     k = _tup(kernel_size, n)
     s = _tup(stride, n) if stride is not None else k
     pad, pre = _pad_arg(padding, n, t, k, s, ceil_mode)
-    if n == 2 and kind == "max" and cl and pre is None and not ceil_mode and not return_mask:
+    if n == 2 and kind == "max" and pre is None and not ceil_mode and not return_mask:
         from ...ops import hip as _hip, fused as _fused
-        xt = x._t
+        from .conv import nhwc_view
+        xt = x._t if cl else nhwc_view(x._t)   # NCHW in channels-last memory: its NHWC view
         p2 = list(_tup(pad, 2)) if not isinstance(pad, (list, tuple)) else list(pad)
-        if len(p2) == 2 and _fused._use_hip(xt) and _hip.maxpool_nhwc_ok(xt, k, s, p2):
+        if xt is not None and len(p2) == 2 and _fused._use_hip(xt) and _hip.maxpool_nhwc_ok(xt, k, s, p2):
             # NHWC max pool on the HIP kernels (byte window index, gather backward)
-            return _w(_hip.MaxPool2dNHWC.apply(xt, tuple(k), tuple(s), tuple(p2)))
+            y = _hip.MaxPool2dNHWC.apply(xt, tuple(k), tuple(s), tuple(p2))
+            return _w(y if cl else y.permute(0, 3, 1, 2))
     if pre is not None:
         fl = []
         for a, b in reversed(pre):
