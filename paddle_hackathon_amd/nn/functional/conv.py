@@ -184,9 +184,54 @@ def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
     return _convnd(3, x, weight, bias, stride, padding, dilation, groups, data_format)
 
 
+def _own_conv2d_t(t, w, bias, stride, padding, output_padding, groups, dilation, output_size, data_format):
+    """2-D transposed convolution on the own kernels (NHWC memory, as ``_own_conv2d``), or None.
+    Dense bf16 / fp16: the input gradient of the convolution with the same weight on the 256-tile
+    implicit-GEMM kernels; grouped / depthwise / dilated + strided: the direct kernels."""
+    import os
+    if os.environ.get("PHA_CONV_IMPL", "hip") != "hip" or not t.is_cuda or t.dim() != 4:
+        return None
+    nchw = data_format == "NCHW"
+    x = t.permute(0, 2, 3, 1) if nchw else t
+    st, dl = _tup(stride, 2), _tup(dilation, 2)
+    k = list(w.shape[2:])
+    if isinstance(padding, str):
+        pad = [0, 0] if padding.upper() == "VALID" else [((k[i] - 1) * dl[i]) // 2 for i in range(2)]
+    else:
+        pad, pre = _padding(padding, 2, k, st, dl, list(x.shape[1:3]))
+        if pre is not None:
+            return None
+    opad = _tup(output_padding, 2)
+    H, W = x.shape[1], x.shape[2]
+    base = [(H - 1) * st[0] - 2 * pad[0] + dl[0] * (k[0] - 1) + 1, (W - 1) * st[1] - 2 * pad[1] + dl[1] * (k[1] - 1) + 1]
+    if output_size is not None:
+        osz = _tup(output_size if not isinstance(output_size, Tensor) else output_size._t.tolist(), 2)
+    else:
+        osz = [base[0] + opad[0], base[1] + opad[1]]
+    if any(o < b or o >= b + s for o, b, s in zip(osz, base, st)):
+        return None
+    from ...ops import grouped_conv as _gc, conv_gemm as _cg
+    Cout = w.shape[1] * groups
+    dense = (groups == 1 and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
+             and x.shape[-1] % 8 == 0 and Cout % 8 == 0 and (st == [1, 1] or dl == [1, 1])
+             and _hip_conv_ok(x, w, 1))
+    if dense:
+        out = _cg.conv_transpose2d_nhwc256(x.contiguous(), w, bias, st, pad, dl, osz)
+    elif _gc.transpose_ok(x, w, groups) and (groups > 1 or x.dtype != torch.float32):
+        out = _gc.conv_transpose2d_nhwc(x, w, bias, st, pad, dl, groups, osz)
+    else:
+        return None
+    return out.permute(0, 3, 1, 2) if nchw else out
+
+
 def _convnd_t(n, x, weight, bias, stride, padding, output_padding, groups, dilation, output_size, data_format):
     t = x._t
     w = weight._t
+    if n == 2 and data_format in ("NCHW", "NHWC"):
+        out = _own_conv2d_t(t, w, None if bias is None else bias._t, stride, padding, output_padding, groups,
+                            dilation, output_size, data_format)
+        if out is not None:
+            return _w(out)
     if t.is_cuda and n == 2:
         from ...ops import fallback
         fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")

@@ -667,6 +667,46 @@ def conv2d_nhwc256(x, weight, bias, stride, padding, dilation):
     return Conv2dNHWC256.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))
 
 
+class ConvTranspose2dNHWC256(torch.autograd.Function):
+    """y = conv_transpose(x, w), w [C_in, C_out, KH, KW]: the input gradient of the convolution F
+    with weight w (F maps C_out -> C_in channels) applied to x, on the 256-tile kernels (conv256_dgrad:
+    stride phases stored in place); dx = F(dy) (conv256_fwd), dw = F's filter gradient with input dy
+    and output gradient x (conv256_wgrad)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation, out_hw):
+        x = x.contiguous()
+        N = x.shape[0]
+        Cout = weight.shape[1]
+        y = conv256_dgrad(x, weight, (N, out_hw[0], out_hw[1], Cout), stride, padding, dilation)
+        if bias is not None:
+            y += bias.to(y.dtype)
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        ctx.conf = (stride, padding, dilation, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        weight = ctx.weight
+        stride, padding, dilation, has_bias = ctx.conf
+        gy = gy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            w_okkc = _wlayout(weight, "fwd", lambda t: t.permute(0, 2, 3, 1).contiguous())
+            dx = conv256_fwd(gy, w_okkc, stride, padding, dilation)
+        if ctx.needs_input_grad[1]:
+            dw = conv256_wgrad(x, gy, weight.shape, stride, padding, dilation)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = gy.float().sum((0, 1, 2)).to(gy.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+def conv_transpose2d_nhwc256(x, weight, bias, stride, padding, dilation, out_hw):
+    return ConvTranspose2dNHWC256.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation), tuple(out_hw))
+
+
 class LinearHip(torch.autograd.Function):
     """y = x @ W (+ b), Paddle [in, out] weight, on the 8-phase MFMA GEMM for all three products:
     forward NN (W k-outer), dX = dY W^T (NT), dW = X^T dY (both operands k-outer)."""

@@ -118,6 +118,65 @@ class GroupedConv2dNHWC(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class GroupedConvTranspose2dNHWC(torch.autograd.Function):
+    """y = conv_transpose(x, w): the input gradient of the convolution F whose weight is w
+    ([C_in, C_out / groups, KH, KW] read as F's [C_out', C_in' / groups, KH, KW]) applied to x;
+    dx = F(dy), dw = F's filter gradient with (input dy, output gradient x)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, pad, dil, groups, out_hw):
+        x = x.contiguous()
+        N, H, W, Cin = x.shape
+        Cout = w.shape[1] * groups
+        OH, OW = out_hw
+        d = [N, OH, OW, Cout, H, W, Cin, w.shape[2], w.shape[3], stride[0], stride[1], pad[0], pad[1], dil[0], dil[1],
+             groups]
+        dims = torch.tensor(d, dtype=torch.int32)
+        depthwise = w.shape[1] == 1 and w.shape[0] == groups
+        w2 = w.permute(2, 3, 1, 0).contiguous() if depthwise else w.permute(2, 3, 0, 1).contiguous()
+        y = torch.empty(N, OH, OW, Cout, dtype=x.dtype, device=x.device)
+        _check(_L().pha_gconv_dgrad(_DT[x.dtype], _p(dims), _p(x), _p(w2), _p(y), _stream(x)), "dgrad")
+        if bias is not None:
+            y += bias.to(y.dtype)
+        ctx.save_for_backward(x, w)
+        ctx.dims, ctx.has_b = dims, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        dims = ctx.dims
+        gy = gy.contiguous()
+        L = _L()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wr = w.permute(2, 3, 1, 0).contiguous()
+            dx = torch.empty_like(x)
+            _check(L.pha_gconv_fwd(_DT[x.dtype], _p(dims), _p(gy), _p(wr), None, _p(dx), _stream(x)), "fwd")
+        if ctx.needs_input_grad[1]:
+            base = L.pha_gconv_wgrad_items(_p(dims))
+            npix = x.shape[0] * x.shape[1] * x.shape[2]
+            chunks = max(1, min(-(-2048 // base), -(-npix // 256)))
+            ws = torch.empty(L.pha_gconv_wgrad_ws(_p(dims), chunks), dtype=torch.float32, device=x.device)
+            dw = torch.empty_like(w)
+            _check(L.pha_gconv_wgrad(_DT[x.dtype], _p(dims), _p(gy), _p(x), _p(dw), _p(ws), chunks, _stream(x)),
+                   "wgrad")
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = gy.reshape(-1, gy.shape[-1]).float().sum(0).to(gy.dtype)
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv_transpose2d_nhwc(x, w, bias, stride, pad, dil, groups, out_hw):
+    """NHWC transposed convolution on the direct kernels (channel counts multiples of 8)"""
+    return GroupedConvTranspose2dNHWC.apply(x, w, bias, tuple(stride), tuple(pad), tuple(dil), groups, tuple(out_hw))
+
+
+def transpose_ok(x, w, groups):
+    return (x.is_cuda and x.dim() == 4 and w.dim() == 4 and x.dtype in _DT and w.dtype == x.dtype
+            and x.shape[-1] == w.shape[0] and x.shape[-1] % 8 == 0 and (w.shape[1] * groups) % 8 == 0
+            and x.shape[-1] % groups == 0 and _lib.native_available())
+
+
 def conv2d_nhwc(x, w, bias, stride, pad, dil, groups):
     """NHWC direct convolution; a dense one whose channel counts are not multiples of 8 is
     zero-padded (input channels of x and w, output channels of w, sliced off the result)"""

@@ -135,3 +135,48 @@ def test_zoo_models_nchw_no_conv_fallback(name):
     y = paddle.to_tensor(torch.randint(0, 1000, (4,), device="cuda"))
     counts = _no_conv_fallback_step(model, x, y)
     assert counts.get("conv2d", 0) == 0, counts
+
+
+# (N, Cin, H, W, Cout, k, stride, pad, out_pad, dil, groups, dtype)
+TCASES = [
+    (2, 32, 8, 9, 16, 4, 2, 1, 0, 1, 1, torch.bfloat16),    # DCGAN-style 4x4 stride-2 upsample
+    (2, 16, 7, 7, 32, 3, 2, 1, 1, 1, 1, torch.bfloat16),    # output_padding 1
+    (2, 24, 6, 6, 40, 3, 1, 1, 0, 1, 1, torch.float16),     # stride 1
+    (2, 32, 6, 6, 32, 3, 2, 2, 1, 2, 1, torch.bfloat16),    # dilated + strided (direct)
+    (2, 64, 5, 5, 64, 3, 2, 1, 1, 1, 64, torch.bfloat16),   # depthwise (direct)
+    (2, 32, 6, 6, 64, 3, 1, 1, 0, 1, 4, torch.float32),     # grouped fp32 (direct)
+]
+
+
+@pytest.mark.parametrize("fmt", ["NCHW", "NHWC"])
+@pytest.mark.parametrize("case", TCASES)
+def test_conv2d_transpose_own_kernels(case, fmt):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    N, Cin, H, W, Cout, k, s, p, op, d, g, dt = case
+    paddle.set_device("gpu")
+    torch.manual_seed(0)
+    x = torch.randn(N, Cin, H, W, device="cuda").to(dt)
+    w = (torch.randn(Cin, Cout // g, k, k, device="cuda") / (Cin * k * k / s / s) ** 0.5).to(dt)
+    b = torch.randn(Cout, device="cuda").to(dt)
+    xr, wr, br = (t.float().detach().requires_grad_(True) for t in (x, w, b))
+    ref = TF.conv_transpose2d(xr, wr, br, s, p, op, g, d)
+    xin = x if fmt == "NCHW" else x.permute(0, 2, 3, 1).contiguous()
+    xa, wa, ba = (paddle.to_tensor(t) for t in (xin, w, b))
+    for t in (xa, wa, ba):
+        t.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.conv2d_transpose(xa, wa, ba, stride=s, padding=p, output_padding=op, dilation=d,
+                                              groups=g, data_format=fmt)
+    assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
+    yt = y._t if fmt == "NCHW" else y._t.permute(0, 3, 1, 2)
+    assert yt.shape == ref.shape
+    _close(yt, ref, dt, "fwd")
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    gin = gy.to(dt) if fmt == "NCHW" else gy.to(dt).permute(0, 2, 3, 1).contiguous()
+    y._t.backward(gin)
+    gx = xa._t.grad if fmt == "NCHW" else xa._t.grad.permute(0, 3, 1, 2)
+    _close(gx, xr.grad, dt, "dx")
+    _close(wa._t.grad, wr.grad, dt, "dw")
+    _close(ba._t.grad, br.grad, dt, "db")
