@@ -1,6 +1,7 @@
 """paddle.incubate.autotune.set_config (reference: python/paddle/incubate/autotune.py).
 
-kernel.enable → let MIOpen/hipBLASLt benchmark algorithms (torch.backends.cudnn.benchmark);
+kernel.enable → time the own conv kernels' tile candidates for shapes missing from the in-tree
+table (ops/conv_gemm.py) and let MIOpen benchmark algorithms (torch.backends.cudnn.benchmark);
 layout.enable → prefer channels-last (NHWC) convolution layouts, the fast path on MI355X;
 dataloader.enable → let the DataLoader tune its worker count on first use.
 
@@ -62,6 +63,8 @@ def set_config(config=None):
             continue
         _config[k].update(v)
     torch.backends.cudnn.benchmark = bool(_config["kernel"]["enable"])
+    from ..ops import conv_gemm
+    conv_gemm.set_timing_autotune(_config["kernel"]["enable"])
     from ..framework import flags
     flags.set_flags({"FLAGS_use_autotune": bool(_config["kernel"]["enable"]),
                      "FLAGS_conv_prefer_nhwc": bool(_config["layout"]["enable"])})
