@@ -33,6 +33,8 @@ using namespace g256;
 
 enum : int {
   EPI_BIAS = 1,       // + bias[output column] (fp32)
+  EPI_GELU = 2,       // NT only: C = gelu_tanh(acc + bias), and aux = acc (the pre-activation before
+                      // the bias, what the HIP dGELU + bias-grad pass reads back)
   EPI_NOSTORE = 512,  // measurement only: stores dropped by the buffer bounds check (tools/bench_g4p.py)
   EPI_SKIP = 128,     // measurement only: no epilogue at all (fresh tiles just start at C = 0)
   EPI_STAGGER = 4096, // measurement only: workgroup w starts after (w & 7) * ((epi >> 16) & 255) s_sleep(16)
@@ -51,6 +53,7 @@ struct Args {
   int group_m;
   float* ws;    // split-K: fp32 partial slabs [splits][M][N] (C unused)
   int splits;
+  void* aux;    // EPI_GELU: pre-activation output, same shape and row stride as C
 };
 
 constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
@@ -80,6 +83,13 @@ __device__ __forceinline__ void bar() {
 }
 
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+// tanh-GELU on one exp + one reciprocal (the HIP bias-GELU pass's math)
+__device__ __forceinline__ float gelu_t(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
+  return 0.5f * x * (1.f + t);
+}
 
 template <typename T>
 __device__ __forceinline__ unsigned pk(float lo, float hi) {
@@ -132,7 +142,8 @@ struct Sched {
 // SPLIT: the K range of every tile is cut into p.splits slices (separate work items, for problems
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
-template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false>
+template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
+          bool GELU = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -277,6 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the tile being written out: output origin (bytes), valid rows / columns from the wave's origin,
   // bias slot
   const char* e_base = static_cast<const char*>(p.c);
+  const char* e_aux = static_cast<const char*>(p.aux);
   int e_rows = 0, e_cols = 0, e_slot = 0;
   auto set_epi = [&](int r) {
     int tm, tn, slice;
@@ -288,6 +300,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 4);
     else
       e_base = static_cast<const char*>(p.c) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    if constexpr (GELU) e_aux = static_cast<const char*>(p.aux) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
     // (EPI_NOSTORE, measurement only: zero rows, every store is issued and dropped)
     e_rows = (p.epi & EPI_NOSTORE) ? 0 : Mo - r0 - wrow;
     e_cols = No - c0;
@@ -309,6 +322,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
                  "v_accvgpr_read_b32 %3, %7"
                  : "=v"(v1[0]), "=v"(v1[1]), "=v"(v1[2]), "=v"(v1[3]) : "a"(x1[0]), "a"(x1[1]), "a"(x1[2]), "a"(x1[3]));
+    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
+    const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    // 8 values -> the lane's 16-B row segment: pack, then lanes of odd 16-lane rows trade their
+    // tile-t0 half for the even rows' tile-(t0+1) half
+    auto pack_swap = [&](const float (&a)[4], const float (&b)[4]) {
+      unsigned q00 = pk<T>(a[0], a[1]), q01 = pk<T>(a[2], a[3]);
+      unsigned q10 = pk<T>(b[0], b[1]), q11 = pk<T>(b[2], b[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(q00, q10, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(q01, q11, false, false);
+      return u32x4{s0[0], s1[0], s0[1], s1[1]};
+    };
+    // descriptor inputs readfirstlane'd: provably uniform, so the descriptor lives in SGPRs
+    // (no per-store waterfall loop, cdna_hip_programming.md T20)
+    auto rsrc = [&](const char* base) {
+      const size_t bp = (size_t)(base + (size_t)rb * 16 * ldc2);
+      const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+      const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+      return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes,
+                                               0x00020000);
+    };
+    if constexpr (GELU)   // the pre-activation (before the bias) for the backward pass
+      __builtin_amdgcn_raw_buffer_store_b128(pack_swap(v0, v1), rsrc(e_aux), voff + cb * 32, 0, 2);
     if constexpr (BIAS) {   // bias of the lane's pre-swap columns cb*16 + 4fk .. +3 and (cb+1)*16 + ...
       const unsigned char* bs = smem + BIAS_OFF + e_slot * 1024 + (OT ? wr : wc) * 512 + 16 * fk;
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(bs + cb * 64);
@@ -319,29 +355,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         v1[e] += b1[e];
       }
     }
-    unsigned q00 = pk<T>(v0[0], v0[1]), q01 = pk<T>(v0[2], v0[3]);
-    unsigned q10 = pk<T>(v1[0], v1[1]), q11 = pk<T>(v1[2], v1[3]);
-    // lanes of odd 16-lane rows trade their tile-t0 half for the even rows' tile-(t0+1) half
-    const auto s0 = __builtin_amdgcn_permlane16_swap(q00, q10, false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(q01, q11, false, false);
-    q00 = s0[0];
-    q10 = s0[1];
-    q01 = s1[0];
-    q11 = s1[1];
-    // descriptor inputs readfirstlane'd: provably uniform, so the descriptor lives in SGPRs
-    // (no per-store waterfall loop, cdna_hip_programming.md T20)
-    const size_t bp = (size_t)(e_base + (size_t)rb * 16 * ldc2);
-    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
-    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
-    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes, 0x00020000);
-    const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] = gelu_t(v0[e]);
+        v1[e] = gelu_t(v1[e]);
+      }
+    }
+    const auto rs = rsrc(e_base);
+    const u32x4 q = pack_swap(v0, v1);
     // non-temporal by default (the output is not re-read by this kernel; 3 % faster measured,
     // profiles/gemm4p_store_ab_r3.log)
-    if (p.epi & EPI_TEMPORAL) __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 0);
-    else __builtin_amdgcn_raw_buffer_store_b128(u32x4{q00, q01, q10, q11}, rs, voff + cb * 32, 0, 2);
+    if (p.epi & EPI_TEMPORAL) __builtin_amdgcn_raw_buffer_store_b128(q, rs, voff + cb * 32, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(q, rs, voff + cb * 32, 0, 2);
   };
 
   // split-K: acc tile (rb, cb) of the wave as fp32, one 16-B store per lane
@@ -458,7 +484,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if constexpr (SKIPEPI) phase(yes{}, M1{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
       else phase(yes{}, M2{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
       static_assert(NST == 32, "vmcnt literal");
-      if constexpr (SPLIT) asm volatile("s_waitcnt vmcnt(63)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      // GELU builds store twice per pair (64 > the counter's 63): wait to 63, one store retired
+      if constexpr (SPLIT || GELU) asm volatile("s_waitcnt vmcnt(63)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(32)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       bar();
@@ -541,7 +568,11 @@ int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st)
       return (int)hipGetLastError();
     }
   }
-  if (!ako && !bko && !trans)
+  if ((a.epi & EPI_GELU) && !ako && !bko && !trans)
+    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+  else if (a.epi & EPI_GELU)
+    return (int)hipErrorInvalidValue;
+  else if (!ako && !bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
@@ -564,7 +595,7 @@ using namespace pha;
 // x ldc x 2 bytes < 2^31. grid: workgroups (<= tiles; the caller passes the CU count).
 PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
                        long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
-                       int group_m, float* ws, int splits, hipStream_t stream) {
+                       int group_m, float* ws, int splits, hipStream_t stream, void* aux) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8)
     return (int)hipErrorInvalidValue;
   if ((a_kouter && M < 8) || (b_kouter && N < 8)) return (int)hipErrorInvalidValue;
@@ -575,13 +606,14 @@ PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, lo
   if (256.0 * ldc * 2 >= 2147483647.0) return (int)hipErrorInvalidValue;
   if (((size_t)a | (size_t)b | (size_t)c) & 15) return (int)hipErrorInvalidValue;
   if ((epi & g4p::EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
+  if ((epi & g4p::EPI_GELU) && (!aux || ((size_t)aux & 15) || splits > 1)) return (int)hipErrorInvalidValue;
   if (splits < 1) splits = 1;
   if (splits > 1 && (!ws || (K / 64) % splits || !a_kouter || !b_kouter || trans || (size_t)ws & 15))
     return (int)hipErrorInvalidValue;
   const long tiles = ((M + 255) / 256) * ((N + 255) / 256) * splits;
   if (grid <= 0 || grid > tiles) grid = (int)tiles;
   if (group_m <= 0) group_m = 4;
-  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits};
+  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits, aux};
   const bool bs = epi & g4p::EPI_BIAS;
   if (dt == kBF16) return bs ? g4p::launch<bf16_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                              : g4p::launch<bf16_t, false>(p, a_kouter, b_kouter, trans, grid, stream);

@@ -36,7 +36,7 @@ def _L():
         P, I, LG = c_void_p, c_int, c_long
         L.pha_gemm4w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, P, LG, P, I, P]
         L.pha_gemm4w.restype = c_int
-        L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P]
+        L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P, P]
         L.pha_gemm4p.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
         L.pha_colsum_finish.restype = c_int
@@ -141,11 +141,13 @@ def _num_cus(dev):
 
 
 def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=False, epi_extra=0, grid=0,
-           group_m=0, splits=1):
+           group_m=0, splits=1, gelu_aux=None):
     """C = op(A) @ op(B) (+ bias[output column]) on the persistent epilogue-overlapped kernel
     (csrc/kernels/gemm4p.hip). Layouts: NT (False, False), TN (True, True), and with trans_out
     (True, False) the transposed product C^T [N, M] (``nn_p`` runs x @ W through it).
-    splits > 1 (TN only): split-K into fp32 slabs + an in-order reduce (few-tile weight gradients)."""
+    splits > 1 (TN only): split-K into fp32 slabs + an in-order reduce (few-tile weight gradients).
+    gelu_aux (NT only): C = gelu_tanh(A B^T + bias) and gelu_aux <- A B^T (the pre-activation
+    without the bias, shaped and strided like C) from the same epilogue."""
     assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
     assert a.stride(1) == 1 and b.stride(1) == 1
     M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
@@ -163,9 +165,13 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
     ws = None
     if splits > 1:
         ws = torch.empty(splits * OM * ON, dtype=torch.float32, device=a.device)
+    if gelu_aux is not None:
+        assert (a_kouter, b_kouter, trans_out, splits) == (False, False, False, 1)
+        assert gelu_aux.shape == c.shape and gelu_aux.stride() == c.stride() and gelu_aux.dtype == c.dtype
+        epi |= EPI_GELU
     rc = _L().pha_gemm4p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), int(trans_out), epi, _ptr(bias), grid or _num_cus(a.device),
-                         group_m, _ptr(ws), splits, _stream(a))
+                         group_m, _ptr(ws), splits, _stream(a), _ptr(gelu_aux))
     if rc != 0:
         raise RuntimeError(f"pha_gemm4p failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
     return c
@@ -283,6 +289,19 @@ def nn(a, b, **epi):
     """a [M, K] @ b [K, N] (+ epilogue) on gemm4w as (b^T a^T)^T: A = b (K-outer), B^T = a,
     transposed store (the fused GELU / dGELU epilogue builds)"""
     return gemm(b, a, True, False, trans_out=True, **epi)
+
+
+def mm_nt_bias_gelu(a, bt, bias):
+    """(gelu_tanh(a bt^T + bias), a bt^T) in one own-kernel pass (the MLP's fc1 forward), or None
+    when the own kernel does not take the operands"""
+    M, K = a.shape
+    N = bt.shape[0]
+    if not (_impl() != "library" and a.is_cuda and bt.dtype == a.dtype and a.dtype in (torch.bfloat16, torch.float16)
+            and supported(M, N, K, a, bt) and bias is not None and bias.numel() == N):
+        return None
+    pre = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    act = gemm_p(a, bt, False, False, bias=bias, gelu_aux=pre)
+    return act, pre
 
 
 def mm_nn(a, b):

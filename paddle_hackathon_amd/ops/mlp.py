@@ -6,14 +6,15 @@ Reference behaviour: ``fused_feedforward`` / the fused_gemm_epilogue op
 pre-activation kept as "reserve space", :298 dgelu + bias-grad backward), as used by the GPT
 fleet models.
 
-Two chains compute the same thing (chain 0 is the default, a static choice — the same on every
-rank; ``PHA_FUSED_MLP=force`` selects chain 1 for A/B measurements):
+Three chains compute the same thing (a static choice, ``pick_mode``):
 
   0  fc1 GEMM (NT on the cached W1^T, ops/gemm.mm_nt) -> HIP bias+GELU pass; backward: NT dgrad
      of fc2 -> HIP dGELU+bias-grad pass
   1  own fc1 GEMM (ops/gemm.nn: transposed-store gemm4w) with bias + GELU + stored pre-activation
      in its epilogue; backward: own NT dgrad of fc2 with dGELU against the stored pre-activation
      and the fc1 bias-gradient column sums in its epilogue
+  2  own fc1 GEMM (persistent gemm4p, NT) with bias + GELU + the stored pre-activation in its
+     overlapped epilogue; backward as chain 0
 
 Everything else (fc2 forward, both weight gradients, fc1 dgrad) runs on ops/gemm.py in both chains.
 """
@@ -39,10 +40,14 @@ def _own_ok(x2d, w1, w2):
 
 
 def _fwd(mode, x2d, w1, b1):
-    """-> (activation, saved pre-activation); mode 0 saves x W1 (bias not added), mode 1 x W1 + b1"""
+    """-> (activation, saved pre-activation); modes 0 / 2 save x W1 (bias not added), mode 1 x W1 + b1"""
     if mode == 1:
         return G.nn(x2d, w1, bias=b1, act="gelu", aux_out=True)
     from .conv_gemm import weight_t
+    if mode == 2:
+        r = G.mm_nt_bias_gelu(x2d, weight_t(w1), b1)
+        if r is not None:
+            return r
     h = G.mm_nt(x2d, weight_t(w1))
     return _hip.bias_gelu_fwd(h, b1, True), h
 
@@ -56,13 +61,24 @@ def _bwd_gelu(mode, gy, w2, pre, b1):
     return _hip.bias_gelu_bwd(ga, pre, b1, True)
 
 
+_MODES = {"pass": 0, "force": 1, "epi": 2}
+
+
 def pick_mode(x2d, w1, b1, w2):
-    """static: chain 0 (own GEMMs + the HIP bias-GELU / dGELU+bias-grad passes) — measured ahead of
-    the fused-epilogue chain on gfx950 (profiles/gpt3_mlp_chain_pick_ab_r2.log; tanh-GELU at one
-    wave per SIMD cannot hide behind the MFMAs); PHA_FUSED_MLP=force selects chain 1 for A/B"""
-    if os.environ.get("PHA_FUSED_MLP") == "force" and _own_ok(x2d, w1, w2):
-        return 1
-    return 0
+    """static (the same on every rank): PHA_FUSED_MLP = "pass" (chain 0), "epi" (chain 2: fc1 on the
+    persistent gemm4p with bias + GELU + pre-activation in its epilogue, backward as chain 0) or
+    "force" (chain 1, the gemm4w fused chain, measured behind chain 0 in round 2:
+    profiles/gpt3_mlp_chain_pick_ab_r2.log)"""
+    mode = _MODES.get(os.environ.get("PHA_FUSED_MLP", _DEFAULT), 0)
+    if mode == 1 and not _own_ok(x2d, w1, w2):
+        return 0
+    return mode
+
+
+# chain 2 by default: fc1's bias + GELU live in the GEMM that produces them (882 vs 967 us per
+# layer for library GEMM + pass, profiles/mlp_epi_ab_r3/gelu_epi.log; full GPT step within noise
+# of chain 0 in an alternating A/B, ab_*.log)
+_DEFAULT = "epi"
 
 
 class FusedMLP(torch.autograd.Function):

@@ -195,7 +195,42 @@ def nnform():
     print("per-step ms: " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in tot.items()), flush=True)
 
 
+def gelu():
+    """fc1 forward of the GPT-1.3B MLP: library NT + HIP bias-GELU pass, own NT + pass, and the own
+    NT with bias + GELU + pre-activation in the overlapped epilogue (ops/gemm.mm_nt_bias_gelu)"""
+    import os
+    from paddle_hackathon_amd.ops import hip
+    T, K, N = 32768, 2048, 8192
+    x, wt = r(T, K), r(N, K)
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    act, pre = G.mm_nt_bias_gelu(x, wt, b)
+    ref_pre = x.float() @ wt.float().t()
+    ref_act = torch.nn.functional.gelu(ref_pre + b.float(), approximate="tanh")
+    e1 = ((pre.float() - ref_pre).abs().max() / ref_pre.abs().max()).item()
+    e2 = ((act.float() - ref_act).abs().max() / ref_act.abs().max()).item()
+    print(f"fused gelu epilogue: pre rel_err {e1:.2e}  act rel_err {e2:.2e}", flush=True)
+    fl = 2.0 * T * K * N
+
+    def lib():
+        os.environ["PHA_GEMM_IMPL"] = "library"
+        h = G.mm_nt(x, wt)
+        os.environ.pop("PHA_GEMM_IMPL")
+        return hip.bias_gelu_fwd(h, b, True)
+
+    def own_pass():
+        h = G.gemm_p(x, wt, False, False)
+        return hip.bias_gelu_fwd(h, b, True)
+    res = {"lib+pass": timeit(lib), "own+pass": timeit(own_pass), "own fused": timeit(lambda: G.mm_nt_bias_gelu(x, wt, b)),
+           "own gemm only": timeit(lambda: G.gemm_p(x, wt, False, False, bias=b))}
+    os.environ.pop("PHA_GEMM_IMPL", None)
+    for k, v in res.items():
+        print(f"fc1 fwd {k:14s}: {v * 1e6:7.1f} us  {fl / v / 1e12:6.0f} TF  (x24 layers: {v * 24e3:.2f} ms)", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "gelu":
+        gelu()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "nnform":
         nnform()
         sys.exit(0)
