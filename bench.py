@@ -102,7 +102,8 @@ def main():
     if world > 1:
         dist.init_parallel_env()
     rank = dist.get_rank()
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    # ranks beyond the visible GPUs share them (only the one-GPU multi-rank rehearsal, PHA_DIST_BACKEND=gloo)
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     paddle.set_device(f"gpu:{torch.cuda.current_device()}")
     paddle.seed(1234 + rank)
     if a.gemm_tuning != "off":

@@ -135,8 +135,8 @@ def init_parallel_env(backend=None, timeout_s=1800):
     os.environ.setdefault("MASTER_PORT", os.environ.get("PADDLE_MASTER_PORT", "29500"))
     os.environ.setdefault("RANK", str(env.rank))
     os.environ.setdefault("WORLD_SIZE", str(env.world_size))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:   # PHA_DIST_BACKEND=gloo: host collectives even with GPUs (multi-rank rehearsal on one GPU)
+        backend = os.environ.get("PHA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend in ("nccl", "rccl") and torch.cuda.is_available():
         torch.cuda.set_device(env.device_id % max(1, torch.cuda.device_count()))
         from ..framework import core

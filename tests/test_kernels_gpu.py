@@ -1209,3 +1209,20 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     _train_steps(rn, lambda m: paddle.nn.functional.cross_entropy(m(x), y), ropt)
     results["resnet50"] = fallback.counts()
     assert all(not v for v in results.values()), results
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (264, 520, 128), (4096, 8192, 2048)])
+def test_gemm4p_gelu_epilogue(M, N, K):
+    """gemm4p EPI_GELU (the MLP fc1 forward): act = gelu_tanh(x W^T + b) and the pre-activation
+    x W^T from one epilogue, against fp32"""
+    from paddle_hackathon_amd.ops import gemm as G
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
+    wt = (torch.rand(N, K, device="cuda", generator=g) * 2 - 1).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g).bfloat16()
+    act, pre = G.mm_nt_bias_gelu(x, wt, b)
+    ref_pre = x.float() @ wt.float().t()
+    ref_act = TF.gelu(ref_pre + b.float(), approximate="tanh")
+    for got, ref, what in ((pre, ref_pre, "pre"), (act, ref_act, "act")):
+        err = ((got.float() - ref).abs().max() / ref.abs().max()).item()
+        assert err < 1e-2, (what, err)
