@@ -96,6 +96,10 @@ class Fleet:
         ws = C.get_world_size()
         hc = dict(self._strategy.hybrid_configs)
         mp = max(1, int(hc.get("mp_degree", 1)))
+        if mp == 1 and getattr(self._strategy, "tensor_parallel", False):
+            # static-graph tensor parallelism (reference tensor_parallel_optimizer.py): the model
+            # groups are tensor_parallel_degree consecutive ranks, data parallel across them
+            mp = max(1, int((self._strategy.tensor_parallel_configs or {}).get("tensor_parallel_degree", 1)))
         pp = max(1, int(hc.get("pp_degree", 1)))
         sh = max(1, int(hc.get("sharding_degree", 1)))
         dp = int(hc.get("dp_degree", -1))

@@ -246,9 +246,14 @@ class StaticFleetOptimizer:
                 incr_ratio=cfg.get("incr_ratio", 2.0), decr_ratio=cfg.get("decr_ratio", 0.5),
                 dynamic=cfg.get("use_dynamic_loss_scaling", True))
             grads = [g for _, g in pg2]
-        # 2. gradient communication
-        if self.world > 1 and not sharding:
-            grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20))
+        # 2. gradient communication (tensor parallel: over the data-parallel group only, after the
+        #    startup broadcasts that make replicated parameters equal — tensor_parallel_optimizer.py)
+        ring, comm_world = 0, self.world
+        tp = self._tensor_parallel(prog)
+        if tp is not None:
+            ring, comm_world = tp
+        if comm_world > 1 and not sharding:
+            grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20), ring, comm_world)
         owned = list(range(len(params)))
         if sharding:
             # greedy size-balanced ownership (reference sharding/shard.py)
@@ -327,7 +332,29 @@ class StaticFleetOptimizer:
                     _op(blk, c_broadcast_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": 0}, outs)
         return [op for op in blk.ops if P.is_train_op(op)], list(zip(params, gvars))
 
-    def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes):
+    def _tensor_parallel(self, prog):
+        """strategy.tensor_parallel: broadcast every replicated parameter (not ``is_distributed``) from
+        the first rank of its model-parallel group and every parameter from the first rank of its
+        data-parallel group (the reference's startup c_broadcast ops), register the data-parallel
+        group as ring 2. -> (ring id, data-parallel degree) or None"""
+        if not bool(self._cfg("tensor_parallel", False)) or not tdist.is_initialized():
+            return None
+        from .. import fleet as _fleet
+        hcg = _fleet.fleet._hcg
+        if hcg is None or hcg.get_model_parallel_world_size() <= 1:
+            return None
+        from .. import collective as C
+        mp_g, dp_g = hcg.get_model_parallel_group(), hcg.get_data_parallel_group()
+        with torch.no_grad():
+            for p in prog.all_parameters():
+                if not getattr(p, "is_distributed", False):
+                    tdist.broadcast(p._t.data, src=mp_g.ranks[0], group=C._resolve_group(mp_g))
+                if dp_g.nranks > 1:
+                    tdist.broadcast(p._t.data, src=dp_g.ranks[0], group=C._resolve_group(dp_g))
+        register_ring(2, C._resolve_group(dp_g))
+        return 2, dp_g.nranks
+
+    def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes, ring=0, world=None):
         """buckets in gradient-ready order (position of each grad's producing op); each bucket's
         async all-reduce starts right after its last grad op, and is waited for before the update"""
         pos = {id(op): i for i, op in enumerate(blk.ops)}
@@ -341,7 +368,7 @@ class StaticFleetOptimizer:
             tok = P.Variable(blk, torch.empty((), device="meta"))
             blk.vars[tok.name] = tok
             start = P.OpDesc("c_allreduce_start", c_allreduce_start, (),
-                             {"xs": bucket, "ring_id": 0, "scale": 1.0 / self.world, "key": key}, tok,
+                             {"xs": bucket, "ring_id": ring, "scale": 1.0 / (world or self.world), "key": key}, tok,
                              attrs={"op_role": "backward", "bucket": k})
             tok.op = start
             inserts.append((after, start))

@@ -51,6 +51,67 @@ def _rk(group):
     return group.rank if isinstance(group, C.Group) else dist.get_rank(group)
 
 
+def _static_var(x):
+    """x is a static-graph Variable: the TP layer records ONE op (static TP, reference
+    fleet/meta_optimizers/tensor_parallel_optimizer.py over paddle.distributed.split)"""
+    from ..static import program as P
+    return isinstance(x, P.Variable)
+
+
+def _record(fn, name, args, kwargs):
+    from ..static import program as P
+    return P.record_op(fn, name, args, kwargs)
+
+
+def _meta(x, last):
+    return _wrap(torch.empty(*x._t.shape[:-1], last, dtype=x._t.dtype, device="meta"))
+
+
+def column_parallel_linear(x, weight, bias=None, gather_output=True):
+    """the op a static ColumnParallelLinear records: x @ W_shard (+ b_shard), optionally gathered"""
+    group = _mp_group()
+    if x._t.is_meta:
+        return _meta(x, weight.shape[1] * (_ws(group) if gather_output else 1))
+    xt = x._t
+    if _ws(group) > 1 and xt.dim() >= 2:
+        y = _wrap(_ColumnParallelMatmul.apply(xt, weight._t, None if bias is None else bias._t, _pg(group),
+                                              _tp_chunks(xt.numel() // xt.shape[-1])))
+    else:
+        y = F.linear(_c_identity(x, group), weight, bias)
+    return _c_concat(y, group) if gather_output and _ws(group) > 1 else y
+
+
+def row_parallel_linear(x, weight, bias=None, input_is_parallel=False):
+    """the op a static RowParallelLinear records: all_reduce(x_shard @ W_shard) (+ b)"""
+    group = _mp_group()
+    if x._t.is_meta:
+        return _meta(x, weight.shape[1])
+    if not input_is_parallel and _ws(group) > 1:
+        x = _c_split(x, group)
+    xt = x._t
+    if _ws(group) > 1 and xt.dim() >= 2:
+        y = _wrap(_RowParallelMatmul.apply(xt, weight._t, _pg(group), _tp_chunks(xt.numel() // xt.shape[-1])))
+    else:
+        y = _mp_allreduce(F.linear(x, weight, None), group)
+    return y + bias if bias is not None else y
+
+
+def vocab_parallel_embedding(x, weight, vocab_start=0):
+    """the op a static VocabParallelEmbedding records: masked local lookup + all_reduce"""
+    group = _mp_group()
+    if x._t.is_meta:
+        return _wrap(torch.empty(*x._t.shape, weight.shape[1], dtype=weight._t.dtype, device="meta"))
+    if _ws(group) == 1:
+        return F.embedding(x, weight)
+    ids = x._t
+    per = weight.shape[0]
+    mask = (ids < vocab_start) | (ids >= vocab_start + per)
+    local = torch.where(mask, torch.zeros_like(ids), ids - vocab_start)
+    out = F.embedding(_wrap(local), weight)._t
+    out = out.masked_fill(mask.unsqueeze(-1), 0.0)
+    return _mp_allreduce(_wrap(out), group)
+
+
 class _Identity(torch.autograd.Function):
     """c_identity: forward identity, backward all-reduce over the TP group."""
 
@@ -231,6 +292,9 @@ class VocabParallelEmbedding(Layer):
         self.weight.is_distributed = self.world_size > 1
 
     def forward(self, x):
+        if _static_var(x):
+            return _record(vocab_parallel_embedding, "vocab_parallel_embedding", (x, self.weight),
+                           {"vocab_start": int(self.vocab_start_index)})
         if self.world_size == 1:
             return F.embedding(x, self.weight)
         ids = x._t
@@ -262,6 +326,9 @@ class ColumnParallelLinear(Layer):
             self.bias = None
 
     def forward(self, x):
+        if _static_var(x):
+            return _record(column_parallel_linear, "column_parallel_linear", (x, self.weight, self.bias),
+                           {"gather_output": bool(self.gather_output)})
         xt = x._t if isinstance(x, Tensor) else x
         if self.world_size > 1 and type(xt).__name__ != "DTensor" and xt.dim() >= 2:
             rows = xt.numel() // xt.shape[-1]
@@ -290,6 +357,9 @@ class RowParallelLinear(Layer):
         self.bias = self.create_parameter([out_features], is_bias=True) if has_bias else None
 
     def forward(self, x):
+        if _static_var(x):
+            return _record(row_parallel_linear, "row_parallel_linear", (x, self.weight, self.bias),
+                           {"input_is_parallel": bool(self.input_is_parallel)})
         if not self.input_is_parallel and self.world_size > 1:
             x = _c_split(x, self.model_parallel_group)
         xt = x._t if isinstance(x, Tensor) else x
