@@ -27,9 +27,10 @@ from .engine import Engine  # noqa: F401
 
 
 def parallelize(program, fetches, process_mesh, rank=None, optimizer=None, loss=None, auto=False, mesh_dim=0,
-                memory_limit=None):
+                memory_limit=None, strategy=None):
     """Static-graph semi-/fully-automatic parallelism: (optionally plan) -> complete -> partition
-    [-> backward + gradient sync + optimizer]. Returns (local Program, local fetch Variables,
+    [-> per-op backward + the strategy's passes (recompute / amp / sharding / gradient merge) + gradient
+    sync + optimizer]. Returns (local Program, local fetch Variables,
     Parallelizer). Feeds split along a mesh dim (annotated data) are fed as this rank's slice."""
     from .planner import plan
     from .partitioner import Parallelizer
@@ -40,7 +41,7 @@ def parallelize(program, fetches, process_mesh, rank=None, optimizer=None, loss=
     lidx = next((i for i, f in enumerate(fetches) if f is loss), len(fetches))
     prog, outs = par.parallelize(fetches + ([loss] if loss is not None and lidx == len(fetches) else []))
     if optimizer is not None:
-        par.minimize(optimizer, outs[lidx])
+        par.minimize(optimizer, outs[lidx], strategy)
     return prog, outs[:len(fetches)], par
 
 

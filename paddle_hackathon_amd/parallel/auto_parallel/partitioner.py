@@ -299,9 +299,39 @@ class Parallelizer:
     def local_parameters(self):
         return [p for p in self.part.params.values() if isinstance(p, Parameter) and not p.stop_gradient]
 
-    def minimize(self, optimizer, loss):
-        """append @backward, per-parameter gradient all-reduce over the data-parallel mesh dims
-        (the dims the feeds are split on and the parameter is replicated on) and @update"""
+    def minimize(self, optimizer, loss, strategy=None):
+        """training on the partitioned Program through the static fleet optimizer
+        (parallel/fleet/static_optimizers.py): per-op grad ops on the local program, then the passes
+        the reference runs on an auto-parallel program (distributed/passes/auto_parallel_*.py) —
+        ``strategy.recompute`` (checkpoints), ``strategy.amp`` (loss scaling), gradient sync over the
+        data-parallel mesh dim as bucketed all-reduces overlapped with the backward,
+        ``strategy.sharding`` (optimizer-state owners along that dim) and
+        ``strategy.gradient_merge`` — then the inner optimizer. The loss is already the global mean,
+        so the data-parallel sync sums."""
+        from ..fleet.static_optimizers import StaticFleetOptimizer, register_ring
+        from ..strategy import DistributedStrategy
+        params = self.local_parameters()
+        dims = [m for m in sorted(self.part.data_dims) if self.mesh.topology[m] > 1]
+        if len(dims) > 1 or any(m in p.dist_attr["dims_mapping"] for p in params for m in dims):
+            return self._minimize_per_param(optimizer, loss)
+        st = strategy if strategy is not None else DistributedStrategy()
+        if dims:
+            m = dims[0]
+            ring = 100 + m
+            register_ring(ring, _GROUPS.get(m))
+            coord = _coord(self.mesh, self.rank)
+            sfo = StaticFleetOptimizer(optimizer, st, world_size=self.mesh.topology[m], rank=coord[m],
+                                       comm=(ring, self.mesh.topology[m], 1.0))
+        else:
+            sfo = StaticFleetOptimizer(optimizer, st, world_size=1, rank=0, comm=(0, 1, 1.0))
+        with P.program_guard(self.program):
+            sfo.minimize(loss, parameter_list=params)
+        self.fleet_optimizer = sfo
+        return params
+
+    def _minimize_per_param(self, optimizer, loss):
+        """several data-parallel mesh dims (or parameters split along one): @backward, one
+        all-reduce per parameter over each data dim it is replicated on, @update"""
         from ..fleet.static_optimizers import _grad_vars, _op
         blk = self.program.global_block()
         params = self.local_parameters()

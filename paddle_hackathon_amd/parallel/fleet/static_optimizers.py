@@ -198,11 +198,15 @@ def _buckets(items, bucket_bytes):
 class StaticFleetOptimizer:
     """``fleet.distributed_optimizer(opt, strategy)`` in static mode."""
 
-    def __init__(self, inner, strategy=None, world_size=None, rank=None):
+    def __init__(self, inner, strategy=None, world_size=None, rank=None, comm=None):
+        """comm = (ring id, group size, gradient scale): the data-parallel communication runs over that
+        registered ring instead of the global group (auto_parallel's data mesh dim; world_size /
+        rank are then the group's)"""
         self.inner = inner
         self.strategy = strategy
         self.world = world_size if world_size is not None else (tdist.get_world_size() if tdist.is_initialized() else 1)
         self.rank = rank if rank is not None else (tdist.get_rank() if tdist.is_initialized() else 0)
+        self.comm = comm
         self.owner = {}
 
     def __getattr__(self, item):
@@ -248,12 +252,15 @@ class StaticFleetOptimizer:
             grads = [g for _, g in pg2]
         # 2. gradient communication (tensor parallel: over the data-parallel group only, after the
         #    startup broadcasts that make replicated parameters equal — tensor_parallel_optimizer.py)
-        ring, comm_world = 0, self.world
+        ring, comm_world, scale = 0, self.world, 1.0 / max(1, self.world)
         tp = self._tensor_parallel(prog)
         if tp is not None:
             ring, comm_world = tp
+            scale = 1.0 / comm_world
+        if self.comm is not None:
+            ring, comm_world, scale = self.comm
         if comm_world > 1 and not sharding:
-            grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20), ring, comm_world)
+            grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20), ring, comm_world, scale)
         owned = list(range(len(params)))
         if sharding:
             # greedy size-balanced ownership (reference sharding/shard.py)
@@ -268,8 +275,8 @@ class StaticFleetOptimizer:
                 pos = {id(grads[i]): i for i in idx}
                 for bucket in _buckets([grads[i] for i in idx], int(fuse_mb * 2 ** 20)):
                     outs = _grad_vars(blk, bucket, "@REDUCE")
-                    _op(blk, c_reduce_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": 0,
-                                                  "scale": 1.0 / self.world}, outs)
+                    _op(blk, c_reduce_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": ring,
+                                                  "scale": scale}, outs)
                     for g, o in zip(bucket, outs):
                         new[pos[id(g)]] = o
             grads = new
@@ -329,7 +336,7 @@ class StaticFleetOptimizer:
                 idx = [i for i in range(len(params)) if self.owner[i] == r]
                 for bucket in _buckets([params[i] for i in idx], int(fuse_mb * 2 ** 20)):
                     outs = tuple(P.Variable(blk, p._t.to("meta")) for p in bucket)
-                    _op(blk, c_broadcast_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": 0}, outs)
+                    _op(blk, c_broadcast_coalesced, {"xs": tuple(bucket), "root": r, "ring_id": ring}, outs)
         return [op for op in blk.ops if P.is_train_op(op)], list(zip(params, gvars))
 
     def _tensor_parallel(self, prog):
@@ -354,7 +361,7 @@ class StaticFleetOptimizer:
         register_ring(2, C._resolve_group(dp_g))
         return 2, dp_g.nranks
 
-    def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes, ring=0, world=None):
+    def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes, ring=0, world=None, scale=None):
         """buckets in gradient-ready order (position of each grad's producing op); each bucket's
         async all-reduce starts right after its last grad op, and is waited for before the update"""
         pos = {id(op): i for i, op in enumerate(blk.ops)}
@@ -368,7 +375,8 @@ class StaticFleetOptimizer:
             tok = P.Variable(blk, torch.empty((), device="meta"))
             blk.vars[tok.name] = tok
             start = P.OpDesc("c_allreduce_start", c_allreduce_start, (),
-                             {"xs": bucket, "ring_id": ring, "scale": 1.0 / (world or self.world), "key": key}, tok,
+                             {"xs": bucket, "ring_id": ring,
+                              "scale": scale if scale is not None else 1.0 / (world or self.world), "key": key}, tok,
                              attrs={"op_role": "backward", "bucket": k})
             tok.op = start
             inserts.append((after, start))
