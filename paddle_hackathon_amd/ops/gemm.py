@@ -231,12 +231,21 @@ def _lib_call(layout, name, shape, fn):
 
 
 def _splits(M, N, K, dev):
-    """split-K factor for a weight gradient whose tile grid is smaller than the chip: the smallest
-    power of two giving >= one tile per CU that divides the K-tiles"""
+    """split-K factor for a weight gradient: the smallest power of two (<= 16, dividing the K-tiles)
+    whose work items fill the chip's rounds to >= 95 % (tiles x splits over whole multiples of the
+    CU count: GPT-1.3B's qkv dW has 192 tiles — split 2 would run 384 items in two rounds, 75 %
+    busy; split 4 runs 768 in three full rounds); grids of >= 2 rounds already stay unsplit"""
     tiles = -(-M // 256) * -(-N // 256)
     cus = _num_cus(dev)
+    ktiles = K // 64
+
+    def eff(sp):
+        items = tiles * sp
+        return items / (-(-items // cus) * cus)
+    if tiles >= 2 * cus:
+        return 1
     sp = 1
-    while tiles * sp < cus and (K // 64) % (sp * 2) == 0 and sp < 16:
+    while (tiles * sp < cus or eff(sp) < 0.95) and sp < 16 and ktiles % (sp * 2) == 0 and ktiles // (sp * 2) >= 4:
         sp *= 2
     return sp
 
