@@ -91,10 +91,9 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
   //      written with 8 ds_write_b64 (4 keys each) instead of 32 ds_write_b16.
   constexpr int KCH = (BN * CH) / 256;          // K chunks per thread
   constexpr int VITEMS = (BN / 4) * CH;          // (4-key group, d chunk) items
+  constexpr int VIT = (VITEMS + 255) / 256;      // V items per thread (2 at D = 256)
   u32x4 kreg[KCH];
-  u32x4 vreg[4];
-  const int v_item = tid;                        // valid when tid < VITEMS
-  const int v_kg = v_item / CH, v_ch = v_item % CH;
+  u32x4 vreg[VIT][4];
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
@@ -103,11 +102,16 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
       const int key = k0 + row;
       kreg[i] = (key < Sk) ? *reinterpret_cast<const u32x4*>(Kb + (long)key * kstride + ch * 8) : u32x4{0, 0, 0, 0};
     }
-    if (v_item < VITEMS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = k0 + v_kg * 4 + j;
-        vreg[j] = (key < Sk) ? *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + v_ch * 8) : u32x4{0, 0, 0, 0};
+    for (int it = 0; it < VIT; ++it) {
+      const int v_item = tid + 256 * it;
+      if (v_item < VITEMS) {
+        const int v_kg = v_item / CH, v_ch = v_item % CH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = k0 + v_kg * 4 + j;
+          vreg[it][j] = (key < Sk) ? *reinterpret_cast<const u32x4*>(Vb + (long)key * kstride + v_ch * 8) : u32x4{0, 0, 0, 0};
+        }
       }
     }
   };
@@ -117,17 +121,22 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
       const int c = tid + 256 * i;
       *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(c / CH, c % CH)) = kreg[i];
     }
-    if (v_item < VITEMS) {
-      const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&vreg[0]);
-      const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&vreg[1]);
-      const uint16_t* e2 = reinterpret_cast<const uint16_t*>(&vreg[2]);
-      const uint16_t* e3 = reinterpret_cast<const uint16_t*>(&vreg[3]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        u32x2 w;
-        w[0] = (uint32_t)e0[e] | ((uint32_t)e1[e] << 16);
-        w[1] = (uint32_t)e2[e] | ((uint32_t)e3[e] << 16);
-        *reinterpret_cast<u32x2*>(vt_lds + (v_ch * 8 + e) * VT_STRIDE + v_kg * 8) = w;
+    for (int it = 0; it < VIT; ++it) {
+      const int v_item = tid + 256 * it;
+      if (v_item < VITEMS) {
+        const int v_kg = v_item / CH, v_ch = v_item % CH;
+        const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&vreg[it][0]);
+        const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&vreg[it][1]);
+        const uint16_t* e2 = reinterpret_cast<const uint16_t*>(&vreg[it][2]);
+        const uint16_t* e3 = reinterpret_cast<const uint16_t*>(&vreg[it][3]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          u32x2 w;
+          w[0] = (uint32_t)e0[e] | ((uint32_t)e1[e] << 16);
+          w[1] = (uint32_t)e2[e] | ((uint32_t)e3[e] << 16);
+          *reinterpret_cast<u32x2*>(vt_lds + (v_ch * 8 + e) * VT_STRIDE + v_kg * 8) = w;
+        }
       }
     }
   };
@@ -577,31 +586,43 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
 
-  // staging item: threads [0, 8*CH) own (4-row group, chunk) of Q, the next 8*CH of dO
+  // staging items: [0, ITEMS) are (4-row group, chunk) of Q, [ITEMS, 2 ITEMS) of dO; thread tid owns
+  // items tid + 256 i (one each up to D = 128, two at D = 256)
   constexpr int ITEMS = (BQ / 4) * CH;        // per tensor (D=128: 128, D=64: 64)
-  const bool is_q = tid < ITEMS;
-  const bool is_do = tid >= ITEMS && tid < 2 * ITEMS;
-  const int it = is_q ? tid : tid - ITEMS;
-  const int rg = it / CH, ch = it % CH;
-  u32x4 sreg[4];
+  constexpr int SIT = (2 * ITEMS + 255) / 256;
+  u32x4 sreg[SIT][4];
   float srow = 0.f;
   auto load_tile = [&](int qt) {
-    if (is_q || is_do) {
-      const T* src = is_q ? Qb : dOb;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {   // rows past S read row S - 1 (finite, masked to P = 0)
-        const int qq = min(qt + rg * 4 + j, S - 1);
-        sreg[j] = *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8);
+    for (int i = 0; i < SIT; ++i) {
+      const int item = tid + 256 * i;
+      if (item < 2 * ITEMS) {
+        const bool is_q = item < ITEMS;
+        const int it = is_q ? item : item - ITEMS;
+        const int rg = it / CH, ch = it % CH;
+        const T* src = is_q ? Qb : dOb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // rows past S read row S - 1 (finite, masked to P = 0)
+          const int qq = min(qt + rg * 4 + j, S - 1);
+          sreg[i][j] = *reinterpret_cast<const u32x4*>(src + (long)qq * qstride + ch * 8);
+        }
       }
     }
     if (tid < 2 * BQ) srow = (tid < BQ ? lse_b : del_b)[min(qt + (tid & (BQ - 1)), S - 1)];
   };
   auto store_tile = [&]() {
-    if (is_q || is_do) {
-      unsigned char* rows = is_q ? q_lds : do_lds;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(rows + (rg * 4 + j) * ROWB + ch * 16) = sreg[j];
-      write_t4(is_q ? qt_lds : dot_lds, TB, ch, rg * 4, sreg);
+    for (int i = 0; i < SIT; ++i) {
+      const int item = tid + 256 * i;
+      if (item < 2 * ITEMS) {
+        const bool is_q = item < ITEMS;
+        const int it = is_q ? item : item - ITEMS;
+        const int rg = it / CH, ch = it % CH;
+        unsigned char* rows = is_q ? q_lds : do_lds;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(rows + (rg * 4 + j) * ROWB + ch * 16) = sreg[i][j];
+        write_t4(is_q ? qt_lds : dot_lds, TB, ch, rg * 4, sreg[i]);
+      }
     }
     if (tid < 2 * BQ) (tid < BQ ? lse_lds : del_lds)[tid & (BQ - 1)] = srow;
   };
@@ -747,16 +768,21 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
 
   // staging: K as (4-key group, chunk) items -> K rows + K^T image; V as 16-B row chunks
   constexpr int KITEMS = (BN / 4) * CH;
+  constexpr int KIT = (KITEMS + 255) / 256;     // K items per thread (2 at D = 256)
   constexpr int VCH = (BN * CH) / 256;
-  const int kg = tid / CH, kch = tid % CH;
-  u32x4 kreg[4];
+  u32x4 kreg[KIT][4];
   u32x4 vreg[VCH];
   auto load_tile = [&](int k0) {
-    if (tid < KITEMS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kk = k0 + kg * 4 + j;
-        kreg[j] = (kk < Sk) ? *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + kch * 8) : u32x4{0, 0, 0, 0};
+    for (int i = 0; i < KIT; ++i) {
+      const int item = tid + 256 * i;
+      if (item < KITEMS) {
+        const int kg = item / CH, kch = item % CH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kk = k0 + kg * 4 + j;
+          kreg[i][j] = (kk < Sk) ? *reinterpret_cast<const u32x4*>(Kb + (long)kk * kstride + kch * 8) : u32x4{0, 0, 0, 0};
+        }
       }
     }
 #pragma unroll
@@ -767,10 +793,15 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
     }
   };
   auto store_tile = [&]() {
-    if (tid < KITEMS) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(kg * 4 + j, kch)) = kreg[j];
-      write_t4(kt_lds, KT_STRIDE, kch, kg * 4, kreg);
+    for (int i = 0; i < KIT; ++i) {
+      const int item = tid + 256 * i;
+      if (item < KITEMS) {
+        const int kg = item / CH, kch = item % CH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(k_lds + k_lds_off<D>(kg * 4 + j, kch)) = kreg[i][j];
+        write_t4(kt_lds, KT_STRIDE, kch, kg * 4, kreg[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
@@ -1242,6 +1273,7 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
 #define FA_L(DD, CC) hipLaunchKernelGGL((fa_fwd_kernel<T, DD, CC>), grid, block, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, FaExt{})
   if (D == 128) { if (causal) FA_L(128, true); else FA_L(128, false); }
   else if (D == 64) { if (causal) FA_L(64, true); else FA_L(64, false); }
+  else if (D == 256) { if (causal) FA_L(256, true); else FA_L(256, false); }
   else return (int)hipErrorInvalidValue;
 #undef FA_L
   return (int)hipGetLastError();
@@ -1277,6 +1309,7 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
                      (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, FaExt{})
   if (D == 128) { if (causal) { FB_L(128, true); } else { FB_L(128, false); } }
   else if (D == 64) { if (causal) { FB_L(64, true); } else { FB_L(64, false); } }
+  else if (D == 256) { if (causal) { FB_L(256, true); } else { FB_L(256, false); } }
   else return (int)hipErrorInvalidValue;
 #undef FB_L
   return (int)hipGetLastError();
@@ -1301,6 +1334,7 @@ int launch_ext(bool bwd, const void* q, const void* k, const void* v, void* o, f
   if (D == 128) { FX(128) }
   else if (D == 64) { FX(64) }
   else if (D == 32) { FX(32) }
+  else if (D == 256) { FX(256) }
   else return (int)hipErrorInvalidValue;
 #undef FX
 #undef FX_B
@@ -1326,11 +1360,11 @@ int dispatch_ext(bool bwd, const void* q, const void* k, const void* v, void* o,
 // Attention with an additive fp32 bias (natural-log units, key stride 1; element strides sb / sh /
 // sq of batch / head / query, 0 = broadcast: a key-padding mask [B,1,1,Sk] has sh = sq = 0) and/or
 // dropout of the probabilities (rate in [0, 1): 16-bit threshold; seed selects the stream, the
-// backward regenerates the same mask from it). Head dims 32 / 64 / 128.
+// backward regenerates the same mask from it). Head dims 32 / 64 / 128 / 256.
 PHA_API int pha_flash_attn_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                                    int S, int Sk, int H, int Hk, int D, float scale, int causal, const float* bias,
                                    long sb, long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
-  if (H % Hk || (D != 32 && D != 64 && D != 128) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
+  if (H % Hk || (D != 32 && D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
     return (int)hipErrorInvalidValue;
   FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
@@ -1343,7 +1377,7 @@ PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const v
                                    const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int S,
                                    int Sk, int H, int Hk, int D, float scale, int causal, const float* bias, long sb,
                                    long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
-  if (H % Hk || (D != 32 && D != 64 && D != 128) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
+  if (H % Hk || (D != 32 && D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
     return (int)hipErrorInvalidValue;
   FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
@@ -1354,7 +1388,7 @@ PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const v
 
 PHA_API int pha_flash_attn_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S,
                                int Sk, int H, int Hk, int D, float scale, int causal, hipStream_t stream) {
-  if (H % Hk || (D != 64 && D != 128) || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
+  if (H % Hk || (D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_fwd<bf16_t>(q, k, v, o, lse, B, S, Sk, H, Hk, D, scale, causal, stream);
   if (dt == kF16) return launch_fwd<half_t>(q, k, v, o, lse, B, S, Sk, H, Hk, D, scale, causal, stream);
   return (int)hipErrorInvalidValue;
@@ -1368,10 +1402,12 @@ PHA_API int pha_flash_attn_bwd_preprocess(int dt, const void* o, const void* dou
   if (dt == kBF16) {
     if (D == 128) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 128>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
     else if (D == 32) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 32>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
+    else if (D == 256) hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 256>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
     else hipLaunchKernelGGL((fa_bwd_pre_kernel<bf16_t, 64>), grid, block, 0, stream, (const bf16_t*)o, (const bf16_t*)dout, delta, B, S, H);
   } else if (dt == kF16) {
     if (D == 128) hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 128>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
     else if (D == 32) hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 32>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
+    else if (D == 256) hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 256>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
     else hipLaunchKernelGGL((fa_bwd_pre_kernel<half_t, 64>), grid, block, 0, stream, (const half_t*)o, (const half_t*)dout, delta, B, S, H);
   } else {
     return (int)hipErrorInvalidValue;
@@ -1385,7 +1421,7 @@ PHA_API int pha_flash_attn_bwd(int dt, const void* q, const void* k, const void*
                                const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
                                int D, float scale, int causal, hipStream_t stream) {
   // S, Sk >= 1: the kernels clamp out-of-range rows to S - 1 / Sk - 1
-  if (H % Hk || (D != 64 && D != 128) || B <= 0 || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
+  if (H % Hk || (D != 64 && D != 128 && D != 256) || B <= 0 || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_bwd<bf16_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   if (dt == kF16) return launch_bwd<half_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   return (int)hipErrorInvalidValue;

@@ -564,8 +564,8 @@ def multi_tensor_l2norm_sq(tensors):
 # flash attention (csrc/kernels/flash_attn.hip)
 # ----------------------------------------------------------------------------
 def flash_attn_supported(q, k, v, dropout_p, mask=None):
-    """shapes the own kernels take: bf16/fp16 [B, S, H, D] with D <= 128 (32 / 64 / 128 natively,
-    other multiples of 8 zero-padded up), GQA (H % Hk == 0); optional additive / boolean mask
+    """shapes the own kernels take: bf16/fp16 [B, S, H, D] with D <= 256 (32 / 64 / 128 / 256
+    natively, other multiples of 8 zero-padded up; 256 on the generic 4-wave kernels), GQA (H % Hk == 0); optional additive / boolean mask
     broadcastable to [B, H, S, Sk] that needs no gradient; optional dropout"""
     import os
     if os.environ.get("PHA_DISABLE_FLASH") == "1":
@@ -578,7 +578,7 @@ def flash_attn_supported(q, k, v, dropout_p, mask=None):
     if q.dim() != 4 or k.dim() != 4 or v.dim() != 4:
         return False
     B, S, H, D = q.shape
-    if D > 128 or D % 8 or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
+    if D > 256 or D % 8 or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
         return False
     if H % k.shape[2] != 0:
         return False
@@ -595,7 +595,7 @@ def flash_attn_supported(q, k, v, dropout_p, mask=None):
 
 
 def _fa_head_dim(D):
-    return D if D in (32, 64, 128) else (64 if D < 64 else 128)
+    return D if D in (32, 64, 128, 256) else (64 if D < 64 else 128 if D < 128 else 256)
 
 
 def _fa_bias(mask, B, H, S, Sk, device):

@@ -905,12 +905,12 @@ def _attn_ref(q, k, v, causal, scale, bias=None, keep=None, rate=0.0):
     return (p @ vt).transpose(1, 2)
 
 
-@pytest.mark.parametrize("D", [32, 64, 80, 96, 128])
+@pytest.mark.parametrize("D", [32, 64, 80, 96, 128, 192, 256])
 @pytest.mark.parametrize("mask_kind", ["keypad", "full", "bool"])
 @pytest.mark.parametrize("causal", [False, True])
 def test_flash_attention_mask_and_head_dims(D, mask_kind, causal):
-    """additive key-padding [B,1,1,Sk], full [B,H,S,Sk] and boolean masks, head dims 32..128
-    (80/96 zero-padded), forward + all input gradients vs fp32"""
+    """additive key-padding [B,1,1,Sk], full [B,H,S,Sk] and boolean masks, head dims 32..256
+    (80/96/192 zero-padded), forward + all input gradients vs fp32"""
     from paddle_hackathon_amd import ops
     torch.manual_seed(11)
     B, S, H = 2, 200, 3
@@ -936,6 +936,30 @@ def test_flash_attention_mask_and_head_dims(D, mask_kind, causal):
     g = torch.autograd.grad(o, (q, k, v), do)
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     gr = torch.autograd.grad(_attn_ref(qr, kr, vr, causal, scale, bias), (qr, kr, vr), do.float())
+    for a, b in zip(g, gr):
+        assert (a.float() - b).abs().max() / b.abs().max() < 3e-2
+
+
+@pytest.mark.parametrize("D", [160, 256])
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_attention_head_dim_256(D, causal):
+    """head dims above 128 (no mask): the own generic kernels at D = 256, forward + gradients vs
+    fp32, and no fallback to torch SDPA"""
+    from paddle_hackathon_amd import ops
+    from paddle_hackathon_amd.ops import fallback
+    torch.manual_seed(5)
+    B, S, H = 2, 300, 4
+    q, k, v = (torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_() for _ in range(3))
+    fallback.reset()
+    o = ops.flash_attention(q, k, v, causal=causal)
+    assert fallback.total() == 0, fallback.counts()
+    scale = 1.0 / math.sqrt(D)
+    ref = _attn_ref(q, k, v, causal, scale, None)
+    assert (o.float() - ref).abs().max() < 3e-2
+    do = torch.randn_like(o)
+    g = torch.autograd.grad(o, (q, k, v), do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    gr = torch.autograd.grad(_attn_ref(qr, kr, vr, causal, scale, None), (qr, kr, vr), do.float())
     for a, b in zip(g, gr):
         assert (a.float() - b).abs().max() / b.abs().max() < 3e-2
 
