@@ -580,6 +580,11 @@ def flash_attn_supported(q, k, v, dropout_p, mask=None):
     B, S, H, D = q.shape
     if D > 256 or D % 8 or k.shape != v.shape or k.shape[0] != B or k.shape[3] != D:
         return False
+    if D > 128 and os.environ.get("PHA_FA_WIDE", "sdpa") != "own":
+        # head dims 129-256 run on the generic 4-wave kernels at one wave per SIMD (the backward
+        # spills): correct and tested, but 2.5x slower than torch SDPA at D = 256
+        # (profiles/fa_d256_r3.log) — opt in with PHA_FA_WIDE=own
+        return False
     if H % k.shape[2] != 0:
         return False
     if dropout_p and not (0.0 < dropout_p < 1.0):

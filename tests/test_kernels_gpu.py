@@ -908,10 +908,11 @@ def _attn_ref(q, k, v, causal, scale, bias=None, keep=None, rate=0.0):
 @pytest.mark.parametrize("D", [32, 64, 80, 96, 128, 192, 256])
 @pytest.mark.parametrize("mask_kind", ["keypad", "full", "bool"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_flash_attention_mask_and_head_dims(D, mask_kind, causal):
+def test_flash_attention_mask_and_head_dims(D, mask_kind, causal, monkeypatch):
     """additive key-padding [B,1,1,Sk], full [B,H,S,Sk] and boolean masks, head dims 32..256
     (80/96/192 zero-padded), forward + all input gradients vs fp32"""
     from paddle_hackathon_amd import ops
+    monkeypatch.setenv("PHA_FA_WIDE", "own")
     torch.manual_seed(11)
     B, S, H = 2, 200, 3
     q = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_()
@@ -942,10 +943,11 @@ def test_flash_attention_mask_and_head_dims(D, mask_kind, causal):
 
 @pytest.mark.parametrize("D", [160, 256])
 @pytest.mark.parametrize("causal", [False, True])
-def test_flash_attention_head_dim_256(D, causal):
-    """head dims above 128 (no mask): the own generic kernels at D = 256, forward + gradients vs
-    fp32, and no fallback to torch SDPA"""
+def test_flash_attention_head_dim_256(D, causal, monkeypatch):
+    """head dims above 128 (no mask): the own generic kernels at D = 256 (PHA_FA_WIDE=own),
+    forward + gradients vs fp32, and no fallback to torch SDPA"""
     from paddle_hackathon_amd import ops
+    monkeypatch.setenv("PHA_FA_WIDE", "own")
     from paddle_hackathon_amd.ops import fallback
     torch.manual_seed(5)
     B, S, H = 2, 300, 4
