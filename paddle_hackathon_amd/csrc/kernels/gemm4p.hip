@@ -40,6 +40,7 @@ enum : int {
   EPI_STAGGER = 4096, // measurement only: workgroup w starts after (w & 7) * ((epi >> 16) & 255) s_sleep(16)
   EPI_ROUNDS = 8192,  // measurement only: round-robin tile order (lin = r * G + pos) instead of XCD chunks
   EPI_TEMPORAL = 16384,  // stores with the default cache policy (else non-temporal)
+  EPI_RSTAGE = 32768,    // NT: register-staged operands (global_load -> VGPR -> ds_write) instead of LDS-DMA
 };
 
 struct Args {
@@ -143,7 +144,7 @@ struct Sched {
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
 template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
-          bool GELU = false>
+          bool GELU = false, bool RS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -242,6 +243,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const unsigned dst = lds0 + st_buf * STAGE + (wid * 8 + u) * 1024 + (gi & 1) * OPB;
     if (gi & 1) glds_sv(boff[u], st_b, dst);
     else glds_sv(aoff[u], st_a, dst);
+  };
+  // RS (register staging, NT): the cursor's K-tile is loaded into 16 x 16 B of VGPRs per lane
+  // (global_load_dwordx4) one K-tile ahead and written to its LDS slots (ds_write_b128, the same
+  // swizzled image the DMA produces) during the next K-tile's phase B. Each load then has a whole
+  // K-tile of latency cover and no wait drains the prefetch at the phase boundary.
+  typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+  u32x4s sreg[RS ? 16 : 1];
+  auto stage_load = [&](int gi) {
+    const int u = gi >> 1;
+    if (gi & 1) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(sreg[RS ? gi : 0]) : "v"(boff[u]), "s"(st_b) : "memory");
+    else asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(sreg[RS ? gi : 0]) : "v"(aoff[u]), "s"(st_a) : "memory");
+  };
+  auto stage_write = [&](int gi) {
+    const int u = gi >> 1;
+    const unsigned dst = lds0 + st_buf * STAGE + (wid * 8 + u) * 1024 + (gi & 1) * OPB + lane * 16;
+    asm volatile("ds_write_b128 %0, %1" :: "v"(dst), "v"(sreg[RS ? gi : 0]) : "memory");
   };
   auto stage_end = [&]() {   // advance the cursor; a new tile's offsets + bias DMA
     if (!st_on) return;
@@ -398,7 +415,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                    uint4 (&nb)[8], int rbuf, int rkh) {
     constexpr bool RD = decltype(rd_c)::value;
     constexpr int MODE = decltype(mode_c)::value;
-    constexpr bool ST = decltype(st_c)::value;
+    constexpr int STV = decltype(st_c)::value;   // 0: no staging; else staging (RS: vmcnt STV - 1)
+    constexpr bool ST = STV != 0;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if constexpr (RD && (SCHED & 2)) {
@@ -414,7 +432,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         }
       }
-      if constexpr (ST) stage_one(s);
+      if constexpr (ST && RS) {
+        // the previous set's load s has landed (STV - 1 younger ops: its 15 later loads + this
+        // set's s earlier ones [+ the epilogue's stores]), then it is written and reloaded
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(STV - 1) : "memory");
+        stage_write(s);
+        stage_load(s);
+      } else if constexpr (ST) {
+        stage_one(s);
+      }
       const int i = s >> 1, jb = (s & 1) * 4;
       if constexpr (MODE == 2 && SPLIT) {
 #pragma unroll
@@ -463,6 +489,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int gi = 0; gi < 16; ++gi) stage_one(gi);
     stage_end();
   }
+  if constexpr (RS) {   // the register stage starts one K-tile ahead of the two LDS buffers
+    stage_begin(0);
+#pragma unroll
+    for (int gi = 0; gi < 16; ++gi) stage_load(gi);
+    stage_end();
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
 #pragma unroll
@@ -478,34 +510,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int s = 0;   // global K-tile step; buffer s & 1
+  using ST1 = std::integral_constant<int, 1>;
+  using STB = std::integral_constant<int, RS ? 16 : 1>;         // phase B staging (RS: vmcnt(15))
+  using STB2 = std::integral_constant<int, RS ? 16 + 32 : 1>;   // after an epilogue phase's stores
+  (void)sizeof(ST1);
   for (int r = 0; sc.valid(r); ++r) {
     {   // K-tile 0 of tile r: the previous tile is written out under its k-half-0 MFMAs
       const int buf = s & 1;
-      if constexpr (SKIPEPI) phase(yes{}, M1{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
-      else phase(yes{}, M2{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
+      if constexpr (SKIPEPI) phase(yes{}, M1{}, M0{}, fa0, fb0, fa1, fb1, buf, 1);
+      else phase(yes{}, M2{}, M0{}, fa0, fb0, fa1, fb1, buf, 1);
       static_assert(NST == 32, "vmcnt literal");
       // GELU builds store twice per pair (64 > the counter's 63): wait to 63, one store retired
-      if constexpr (SPLIT || GELU) asm volatile("s_waitcnt vmcnt(63)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (RS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else if constexpr (SPLIT || GELU) asm volatile("s_waitcnt vmcnt(63)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(32)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       bar();
       set_epi(r);   // the next epilogue phase writes this tile
       stage_begin(buf);
-      phase(yes{}, M0{}, yes{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
+      phase(yes{}, M0{}, STB2{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
       stage_end();
       ++s;
     }
     for (int k = 1; k < nk; ++k, ++s) {
       const int buf = s & 1;
       // phase A: F1 reads of this K-tile | MFMAs on F0 (k-half 0)
-      phase(yes{}, M0{}, no{}, fa0, fb0, fa1, fb1, buf, 1);
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      phase(yes{}, M0{}, M0{}, fa0, fb0, fa1, fb1, buf, 1);
+      if constexpr (RS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       bar();
       // phase B: stage the cursor into this buffer, F0 reads of the next K-tile (after the last
       // K-tile they read a stale buffer, unused) | MFMAs on F1
       stage_begin(buf);
-      phase(yes{}, M0{}, yes{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
+      phase(yes{}, M0{}, STB{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
       stage_end();
     }
   }
@@ -568,7 +606,12 @@ int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st)
       return (int)hipGetLastError();
     }
   }
-  if ((a.epi & EPI_GELU) && !ako && !bko && !trans)
+  if ((a.epi & EPI_RSTAGE) && !ako && !bko && !trans) {
+    if (a.epi & EPI_GELU)
+      hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true, true>), dim3(grid), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+  } else if ((a.epi & EPI_GELU) && !ako && !bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true>), dim3(grid), dim3(256), 0, st, a);
   else if (a.epi & EPI_GELU)
     return (int)hipErrorInvalidValue;

@@ -25,6 +25,7 @@ import torch
 from . import _lib
 
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT, EPI_TRANS = 1, 2, 4, 8, 16, 32, 64
+EPI_RSTAGE = 32768   # gemm4p NT: register-staged operands
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 

@@ -227,7 +227,42 @@ def gelu():
         print(f"fc1 fwd {k:14s}: {v * 1e6:7.1f} us  {fl / v / 1e12:6.0f} TF  (x24 layers: {v * 24e3:.2f} ms)", flush=True)
 
 
+def rstage():
+    """NT on gemm4p: LDS-DMA staging vs register staging (EPI_RSTAGE) vs hipBLASLt — numerics
+    (bitwise equal outputs expected: same MFMA order) and speed at the GPT NT shapes"""
+    torch.manual_seed(0)
+    for (M, N, K) in [(264, 520, 128), (1032, 2056, 512), (4096, 4096, 1024), (296, 8, 64)]:
+        a, b = r(M, K), r(N, K)
+        bias = torch.randn(N, device="cuda")
+        for bb in (None, bias):
+            c0 = G.gemm_p(a, b, False, False, bias=bb)
+            c1 = G.gemm_p(a, b, False, False, bias=bb, epi_extra=G.EPI_RSTAGE)
+            torch.cuda.synchronize()
+            print(f"rstage check M={M} N={N} K={K} bias={bb is not None}: equal={torch.equal(c0, c1)} "
+                  f"max_diff={(c0.float() - c1.float()).abs().max().item():.2e}", flush=True)
+    a, b = r(4096, 2048), r(8192, 2048)
+    bias = torch.randn(8192, device="cuda", dtype=torch.bfloat16)
+    pre0 = torch.empty(4096, 8192, device="cuda", dtype=torch.bfloat16)
+    pre1 = torch.empty_like(pre0)
+    g0 = G.gemm_p(a, b, False, False, bias=bias, gelu_aux=pre0)
+    g1 = G.gemm_p(a, b, False, False, bias=bias, gelu_aux=pre1, epi_extra=G.EPI_RSTAGE)
+    print(f"rstage gelu: equal={torch.equal(g0, g1) and torch.equal(pre0, pre1)}", flush=True)
+    T = 32768
+    for name, N, K in [("qkv fwd", 6144, 2048), ("qkv dX", 2048, 6144), ("out", 2048, 2048), ("fc1 fwd", 8192, 2048),
+                       ("fc1 dX", 2048, 8192), ("fc2 fwd", 2048, 8192), ("fc2 dX", 8192, 2048)]:
+        a, b = r(T, K), r(N, K)
+        fl = 2.0 * T * N * K
+        t0 = timeit(lambda: G.gemm_p(a, b, False, False))
+        t1 = timeit(lambda: G.gemm_p(a, b, False, False, epi_extra=G.EPI_RSTAGE))
+        tl = timeit(lambda: a @ b.t())
+        print(f"{name:8s} {T}x{N}x{K}: dma {fl / t0 / 1e12:6.0f} TF  rstage {fl / t1 / 1e12:6.0f} TF  "
+              f"lib {fl / tl / 1e12:6.0f} TF", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "rstage":
+        rstage()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "gelu":
         gelu()
         sys.exit(0)
