@@ -915,6 +915,11 @@ constexpr int NTKV = 256;
 constexpr bool kSplitMaskDkdv = true;
 constexpr bool kSplitMaskDq = false;
 constexpr bool kDqBareExp = true;
+constexpr bool kDkdvGroups = true;   // fa_bwd_dkdv_v3's sched_group_barrier interleave
+#ifndef PHA_DKDV_AHEAD
+#define PHA_DKDV_AHEAD 16
+#endif
+constexpr int kDkdvAhead = PHA_DKDV_AHEAD;   // operand reads issued before the first S / dP MFMA
 
 template <typename T, bool CAUSAL, bool ILP2>
 __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v2(const T* __restrict__ Q, const T* __restrict__ K,
@@ -1088,6 +1093,270 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   }
 }
 
+// LDS-DMA 16 B per lane: global (sbase + voff) -> LDS m0 + lane * 16 (issued from asm so the
+// compiler's waitcnt pass does not drain it at the first LDS read; the kernel waits explicitly)
+__device__ __forceinline__ void fa_glds16(unsigned voff, const void* sbase, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+
+// ============================================================================================
+// Backward v3 dK/dV (D = 128, default): fa_bwd_dkdv_v2's geometry (4 waves, 32 keys per wave on
+// the lane, K/V fragments and dK^T/dV^T in registers, 64-query tiles as two 32-row halves) with
+//  * the row constants as the initial accumulators (CDNA guide App. B "Attention backward"): the
+//    S chain starts from -lse/scale and the dP chain from -delta (4 + 4 ds_read_b128 per half
+//    instead of 32 scalar reads), so p = exp2(c S') and dS = p dP' need no subtractions;
+//  * a software pipeline over halves: step j issues half j's S/dP MFMAs (16) in the same basic
+//    block as half j-1's probabilities (VALU) and its dV/dK MFMAs (16), so one wave per SIMD
+//    always has independent MFMAs to cover the exp / pack work and the LDS latencies;
+//  * a 3-deep Q/dO ring (99 KB): the half pending from the previous tile still reads its buffer
+//    while the next tile is written, so one barrier per tile stays enough.
+// ============================================================================================
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v3(const T* __restrict__ Q, const T* __restrict__ K,
+                                                      const T* __restrict__ V, const T* __restrict__ dO,
+                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                      T* __restrict__ dK, T* __restrict__ dV, int S, int Sk, int H,
+                                                      int Hk, float scale, FaStrides fs) {
+  typedef typename MF<T>::frag frag;
+  constexpr int NK = 8, ND = 4, BQ = 64;
+  constexpr int IMG = BQ * 256;                         // 16 KiB per operand image
+  constexpr int BUF = 2 * IMG + 2 * BQ * 4;             // Q, dO, -lse/scale, -delta
+  __shared__ __attribute__((aligned(16))) unsigned char smem[3 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5, lr = lane & 31;
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / ((Sk + NTKV / 2 - 1) / (NTKV / 2)), (Sk + NTKV / 2 - 1) / (NTKV / 2), fs.order_g, bh, rank);
+  const int head = bh % H, b = bh / H;
+  const int hk = head / (H / Hk);
+  const int k0 = rank * (NTKV / 2);
+  const int wk0 = k0 + wid * 32;
+  const int key = wk0 + lr;
+  const long kstride = fs.kv_tok;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const float* lse_b = LSE + ((long)b * H + head) * S;
+  const float* del_b = DELTA + ((long)b * H + head) * S;
+  const float c2 = scale * kLog2e, nis = -1.f / scale;
+
+  const int keyc = min(key, Sk - 1);
+  frag kf[NK], vf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    kf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Kb + (long)keyc * kstride + 16 * kk + 8 * h));
+    vf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Vb + (long)keyc * kstride + 16 * kk + 8 * h));
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): see fa_bwd_dkdv_v2
+  f32x16 dvt[ND], dkt[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
+
+  // Q / dO tiles by LDS-DMA (no staging registers): wave w issues the 1-KiB pieces w*8 .. w*8+7
+  // (piece = 4 rows of one operand); lane l writes physical chunk l & 15 of row l >> 4, so it
+  // fetches the logical chunk (l & 15) ^ swizzle(row) of dual_off's image
+  float srow = 0.f;
+  auto load_tile = [&](int qt, int buf) {
+    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)(smem + buf * BUF);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int gidx = wid * 8 + u, which = gidx >> 4;
+      const int row = (gidx & 15) * 4 + (lane >> 4);
+      const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const long rs = which ? fs.o_tok : fs.q_tok;
+      const T* base = (which ? dOb : Qb) + (long)qt * rs;
+      const unsigned voff = (unsigned)(((long)(min(qt + row, S - 1) - qt) * rs + ch * 8) * 2);
+      fa_glds16(voff, base, __builtin_amdgcn_readfirstlane(lds + which * IMG + (gidx & 15) * 1024));
+    }
+    if (tid < 2 * BQ) srow = (tid < BQ ? lse_b : del_b)[min(qt + (tid & (BQ - 1)), S - 1)];
+  };
+  auto store_rc = [&](int buf) {   // row constants (the DMA'd images need no store)
+    if (tid < 2 * BQ) reinterpret_cast<float*>(smem + buf * BUF + 2 * IMG)[tid] = tid < BQ ? srow * nis : -srow;
+  };
+
+  // step of half j (parity P): A = its S / dP chains (row constants as the initial accumulators;
+  // masked scores start at -inf, so no per-element select is left after the MFMAs), C = the
+  // dV / dK MFMAs of the pending half j-1 (packed P / dS in pw[P^1], dw[P^1], its image pimg),
+  // then B = half j's probabilities packed into pw[P], dw[P]. C's 16 MFMAs cover B's VALU (B
+  // waits only for A's results), and only the packed half (16 registers) crosses steps. One code
+  // path per half (the mask is a branch around the initial values only): step variants behind
+  // branches made the register allocator spill the K / V fragments.
+  u32x4 pw[2][2], dw[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { pw[i][j] = u32x4{0, 0, 0, 0}; dw[i][j] = u32x4{0, 0, 0, 0}; }
+  // lane parts of the LDS read addresses; the parity / 16-row block / buffer parts are immediates
+  // or one scalar base (dual_off's swizzle reduces to these for rows 32P + lr and the transposed
+  // rows 32Q + 16 s2 + 4h + tq (+8))
+  int aoff[NK], troff[ND][2];
+  {
+    const int fr = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) aoff[kk] = lr * 256 + 16 * ((2 * kk + h) ^ fr);
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+        troff[db][hi] = (4 * h + tq) * 256 + hi * 2048 +
+                        16 * (4 * (db ^ tq) + ((2 * (g & 1) + (tp >> 1)) ^ ((h + 2 * hi) & 3))) + 8 * (tp & 1);
+  }
+  const int rcoff = 4 * h * 4;
+  auto lds_b128 = [&](const unsigned char* base, int off) { return *reinterpret_cast<const u32x4*>(base + off); };
+  auto trf = [&](const unsigned char* base, int db) {
+    const u32x2 lo = ds_read_tr16(base + troff[db][0]);
+    const u32x2 hi = ds_read_tr16(base + troff[db][1]);
+    return u32x4{lo[0], lo[1], hi[0], hi[1]};
+  };
+  auto step = [&](auto par_c, auto a_c, const unsigned char* img, int qh, bool msk, const unsigned char* pimg) {
+    constexpr int P = decltype(par_c)::value, Q = P ^ 1;
+    constexpr bool DA = decltype(a_c)::value;
+    f32x16 sa, da;
+    if constexpr (DA) {
+      const unsigned char* rc = img + 2 * IMG + rcoff + P * 128;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float4 l4 = *reinterpret_cast<const float4*>(rc + 32 * jj);
+        const float4 d4 = *reinterpret_cast<const float4*>(rc + BQ * 4 + 32 * jj);
+        sa[4 * jj + 0] = l4.x; sa[4 * jj + 1] = l4.y; sa[4 * jj + 2] = l4.z; sa[4 * jj + 3] = l4.w;
+        da[4 * jj + 0] = d4.x; da[4 * jj + 1] = d4.y; da[4 * jj + 2] = d4.z; da[4 * jj + 3] = d4.w;
+      }
+      if (msk) {
+        // query qh + 4h + rowb(r): masked when past S, when the key is past Sk, or (causal) when
+        // the key is after the query
+        const int lim = key >= Sk ? 32 : (CAUSAL ? key - qh - 4 * h : -1);
+        const int lim2 = S - qh - 4 * h;
+        const float mval = c2 > 0.f ? -INFINITY : INFINITY;   // exp2(c2 * mval) = 0 for either sign
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rb = (r & 3) + 8 * (r >> 2);
+          sa[r] = ((rb < lim) | (rb >= lim2)) ? mval : sa[r];
+        }
+      }
+      const unsigned char* do_img = img + IMG;
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const u32x4 qa = lds_b128(img + P * 8192, aoff[kk]);
+        const u32x4 ga = lds_b128(do_img + P * 8192, aoff[kk]);
+        sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
+        da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
+      }
+    }
+    // C's transposed operand reads, issued under A's MFMAs
+    u32x4 cav[2][ND], cbv[2][ND];
+    {
+      const unsigned char* pdo = pimg + IMG;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          cav[s2][db] = trf(pdo + Q * 8192 + s2 * 4096, db);
+          cbv[s2][db] = trf(pimg + Q * 8192 + s2 * 4096, db);
+        }
+    }
+    if constexpr (DA && kDkdvGroups) {
+      // region 1 (CDNA guide T19): all 16 A operand reads first (one LDS latency per step, not
+      // one per MFMA pair), then A's 16 MFMAs each with two of C's 32 transposed reads
+      __builtin_amdgcn_sched_group_barrier(0x100, kDkdvAhead, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, (48 - kDkdvAhead + 15) / 16, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // region 2: C's MFMAs with B's VALU (B waits only for A's last MFMAs)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int db = 0; db < ND; ++db) {
+        dvt[db] = MF<T>::mma(as_frag<frag>(cav[s2][db]), as_frag<frag>(pw[Q][s2]), dvt[db]);
+        dkt[db] = MF<T>::mma(as_frag<frag>(cbv[s2][db]), as_frag<frag>(dw[Q][s2]), dkt[db]);
+      }
+    if constexpr (DA) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(sa[r] * c2);
+        sa[r] = p;
+        da[r] = p * da[r];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pw[P][s2][j] = MF<T>::pack(sa[8 * s2 + 2 * j], sa[8 * s2 + 2 * j + 1]);
+          dw[P][s2][j] = MF<T>::pack(da[8 * s2 + 2 * j], da[8 * s2 + 2 * j + 1]);
+        }
+      if constexpr (kDkdvGroups) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        }
+      }
+    }
+  };
+  using yes = std::true_type;
+  using no = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  auto needm = [&](int qh) { return (qh + 32 > S) || (wk0 + 32 > Sk) || (CAUSAL && wk0 + 31 > qh); };
+
+  const int qstart = CAUSAL ? (k0 / BQ) * BQ : 0;
+  const int ntile = qstart < S ? (S - qstart + BQ - 1) / BQ : 0;
+  if (ntile > 0) {
+    load_tile(qstart, 0);
+    store_rc(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // halves whose keys all follow all their queries are skipped (causal, at the start only); the
+  // first step's C then multiplies the zero-initialised pw / dw (adds nothing)
+  bool pend = false;
+  const unsigned char* pimg = smem;
+  int buf = 0;
+  for (int t = 0; t < ntile; ++t) {
+    const int qt = qstart + t * BQ;
+    const int nbuf = buf == 2 ? 0 : buf + 1;
+    if (t + 1 < ntile) load_tile(qt + BQ, nbuf);
+    const unsigned char* img = smem + buf * BUF;
+    if (!(CAUSAL && wk0 > qt + 31)) {
+      step(P0{}, yes{}, img, qt, needm(qt), pimg);
+      pend = true;
+      pimg = img;
+    }
+    if (!(CAUSAL && wk0 > qt + 63)) {
+      step(P1{}, yes{}, img, qt + 32, needm(qt + 32), pimg);
+      pend = true;
+      pimg = img;
+    }
+    buf = nbuf;
+    if (t + 1 < ntile) store_rc(buf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile has landed (asm: untracked)
+    __syncthreads();
+  }
+  if (pend) step(P0{}, no{}, smem, 0, false, pimg);   // C of the last half (parity 1)
+  if (key < Sk) {
+    T* dkr = dK + ((long)b * Sk + key) * fs.dkv_tok + (long)head * fs.dkv_head;
+    T* dvr = dV + ((long)b * Sk + key) * fs.dkv_tok + (long)head * fs.dkv_head;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 wk, wv;
+        wk[0] = MF<T>::pack(dkt[db][4 * gg + 0] * scale, dkt[db][4 * gg + 1] * scale);
+        wk[1] = MF<T>::pack(dkt[db][4 * gg + 2] * scale, dkt[db][4 * gg + 3] * scale);
+        wv[0] = MF<T>::pack(dvt[db][4 * gg + 0], dvt[db][4 * gg + 1]);
+        wv[1] = MF<T>::pack(dvt[db][4 * gg + 2], dvt[db][4 * gg + 3]);
+        *reinterpret_cast<u32x2*>(dkr + d) = wk;
+        *reinterpret_cast<u32x2*>(dvr + d) = wv;
+      }
+  }
+}
+
 template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, const T* __restrict__ K,
                                                     const T* __restrict__ V, const T* __restrict__ dO,
@@ -1237,6 +1506,11 @@ bool dkdv_ilp2() {  // PHA_FA_DKDV_ILP=0 serialises the two 32-row halves (A/B c
   return !(e && e[0] == '0');
 }
 
+bool dkdv_v3() {  // PHA_FA_DKDV=v2 selects the unpipelined dK/dV kernel (A/B comparisons)
+  const char* e = getenv("PHA_FA_DKDV");
+  return !(e && e[0] == 'v' && e[1] == '2');
+}
+
 bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comparisons)
   const char* e = getenv("PHA_FA_BWD_V1");
   return !(e && e[0] == '1');
@@ -1289,7 +1563,10 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
   if (D == 128 && bwd_v2_enabled()) {
     const dim3 gk2(B * H, (Sk + NTKV / 2 - 1) / (NTKV / 2)), gq2(B * H, (S + BM2 - 1) / BM2), b2(NT2), bk(NTKV);
 #define FB2(CC)                                                                                                    \
-    if (dkdv_ilp2())                                                                                               \
+    if (dkdv_v3())                                                                                                 \
+      hipLaunchKernelGGL((fa_bwd_dkdv_v3<T, CC>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,          \
+                         (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                     \
+    else if (dkdv_ilp2())                                                                                          \
       hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, true>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,    \
                          (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                     \
     else                                                                                                           \

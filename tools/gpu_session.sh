@@ -126,6 +126,12 @@ for s in "$@"; do
       if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g4w/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g4w_prof.py > $OUT/prof_g4w/pmc2.log 2>&1; rc=$?; fi
       if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d $OUT/prof_g4w/pmc3 -o run --output-format csv -- python3 $ROOT/tools/g4w_prof.py > $OUT/prof_g4w/pmc3.log 2>&1; rc=$?; fi
       tail -2 $OUT/prof_g4w/*.log ;;
+    fa_bwd)
+      timeout -k 10 300 python tools/bench_fa_bwd.py > $OUT/fa_bwd.log 2>&1; rc=$?
+      cat $OUT/fa_bwd.log | tail -12 ;;
+    tests_flash)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "flash" > $OUT/pytest_flash.log 2>&1; rc=$?
+      tail -5 $OUT/pytest_flash.log ;;
     tests_all)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method thread > $OUT/pytest_gpu_all.log 2>&1; rc=$?
       tail -5 $OUT/pytest_gpu_all.log ;;
