@@ -920,6 +920,11 @@ constexpr bool kDkdvGroups = true;   // fa_bwd_dkdv_v3's sched_group_barrier int
 #define PHA_DKDV_AHEAD 16
 #endif
 constexpr int kDkdvAhead = PHA_DKDV_AHEAD;   // operand reads issued before the first S / dP MFMA
+constexpr bool kDqGroups = true;   // fa_bwd_dq_v3's read-ahead interleave
+#ifndef PHA_DQ_AHEAD
+#define PHA_DQ_AHEAD 8
+#endif
+constexpr int kDqAhead = PHA_DQ_AHEAD;
 
 template <typename T, bool CAUSAL, bool ILP2>
 __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) void fa_bwd_dkdv_v2(const T* __restrict__ Q, const T* __restrict__ K,
@@ -1357,6 +1362,176 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   }
 }
 
+// dQ v3 (default): fa_bwd_dq_v2's geometry with K / V tiles by LDS-DMA (no staging registers, no
+// ds_write), the mask folded into the S^T chain's initial accumulator (-inf where masked, so the
+// probability loop is one code path with no selects), and each 32-key block's 16 row reads issued
+// ahead of its MFMAs (one LDS latency per block).
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NT2) void fa_bwd_dq_v3(const T* __restrict__ Q, const T* __restrict__ K,
+                                                    const T* __restrict__ V, const T* __restrict__ dO,
+                                                    const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale, FaStrides fs) {
+  typedef typename MF<T>::frag frag;
+  constexpr int NK = 8, ND = 4;
+  constexpr int IMG = BN * 256;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            lr = lane & 31;
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  const int nqb = (S + BM2 - 1) / BM2;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / nqb, nqb, fs.order_g, bh, rank);
+  const int qb = CAUSAL ? (nqb - 1 - rank) : rank;
+  const int head = bh % H, b = bh / H;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM2;
+  const int wq0 = q0 + wid * 32;
+  const int q = wq0 + lr;
+  const long kstride = fs.kv_tok;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * kstride + (long)hk * fs.kv_head;
+  const float scale_log2 = scale * kLog2e;
+  const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
+  const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
+
+  frag qf[NK], gf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (q < S) {
+      a = *reinterpret_cast<const u32x4*>(Qb + (long)q * fs.q_tok + 16 * kk + 8 * h);
+      c = *reinterpret_cast<const u32x4*>(dOb + (long)q * fs.o_tok + 16 * kk + 8 * h);
+    }
+    qf[kk] = as_frag<frag>(a);
+    gf[kk] = as_frag<frag>(c);
+  }
+  f32x16 dq[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dq[i] = zero16();
+
+  // K / V tile (64 keys) by LDS-DMA: 32 1-KiB pieces (4 rows of one operand), 4 per wave
+  auto load_tile = [&](int k0, int buf) {
+    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)(smem + buf * 2 * IMG);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gidx = wid * 4 + u, which = gidx >> 4;
+      const int row = (gidx & 15) * 4 + (lane >> 4);
+      const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const T* base = (which ? Vb : Kb) + (long)k0 * kstride;
+      const unsigned voff = (unsigned)(((long)(min(k0 + row, Sk - 1) - k0) * kstride + ch * 8) * 2);
+      fa_glds16(voff, base, __builtin_amdgcn_readfirstlane(lds + which * IMG + (gidx & 15) * 1024));
+    }
+  };
+
+  // lane parts of the LDS addresses (see fa_bwd_dkdv_v3): key rows kb*32 + lr, transposed rows
+  // kb*32 + 16 s2 + 4h + tq (+8)
+  int aoff[NK], troff[ND][2];
+  {
+    const int fr = ((lr & 3) << 2) | ((lr >> 2) & 3);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) aoff[kk] = lr * 256 + 16 * ((2 * kk + h) ^ fr);
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+        troff[db][hi] = (4 * h + tq) * 256 + hi * 2048 +
+                        16 * (4 * (db ^ tq) + ((2 * (g & 1) + (tp >> 1)) ^ ((h + 2 * hi) & 3))) + 8 * (tp & 1);
+  }
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM2);
+  const int ntile = (kend + BN - 1) / BN;
+  if (ntile > 0) {
+    load_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const float mval = scale_log2 > 0.f ? -INFINITY : INFINITY;   // exp2(mval * c) = 0 for either sign
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * BN;
+    const int cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + BN, cur ^ 1);
+    const unsigned char* k_img = smem + cur * 2 * IMG;
+    const unsigned char* v_img = k_img + IMG;
+    if (!(CAUSAL && k0 > wq0 + 31)) {
+      const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wq0);
+#pragma unroll 1
+      for (int kb = 0; kb < 2; ++kb) {
+        if (CAUSAL && k0 + kb * 32 > wq0 + 31) break;   // every key of the block after every query
+        f32x16 st = zero16(), dpt = zero16();
+        if (need_mask) {
+          // key k0 + 32kb + 4h + rowb(r): masked past Sk or (causal) after the lane's query
+          const int base = k0 + kb * 32 + 4 * h;
+          const int lim1 = CAUSAL ? q - base : 1 << 20, lim2 = Sk - base;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rb = (r & 3) + 8 * (r >> 2);
+            st[r] = ((rb > lim1) | (rb >= lim2)) ? mval : 0.f;
+          }
+        }
+        const unsigned char* kbi = k_img + kb * 8192;
+        const unsigned char* vbi = v_img + kb * 8192;
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const u32x4 ka = *reinterpret_cast<const u32x4*>(kbi + aoff[kk]);
+          const u32x4 va = *reinterpret_cast<const u32x4*>(vbi + aoff[kk]);
+          st = MF<T>::mma(as_frag<frag>(ka), qf[kk], st);
+          dpt = MF<T>::mma(as_frag<frag>(va), gf[kk], dpt);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(st[r], scale_log2, -lse2));
+          dpt[r] = p * (dpt[r] - dlt);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int s8 = s2 * 8;
+          u32x4 pw;
+          pw[0] = MF<T>::pack(dpt[s8 + 0], dpt[s8 + 1]);
+          pw[1] = MF<T>::pack(dpt[s8 + 2], dpt[s8 + 3]);
+          pw[2] = MF<T>::pack(dpt[s8 + 4], dpt[s8 + 5]);
+          pw[3] = MF<T>::pack(dpt[s8 + 6], dpt[s8 + 7]);
+          const frag pf = as_frag<frag>(pw);
+#pragma unroll
+          for (int db = 0; db < ND; ++db) {
+            const unsigned char* tb = kbi + s2 * 4096;
+            const u32x2 lo = ds_read_tr16(tb + troff[db][0]);
+            const u32x2 hi = ds_read_tr16(tb + troff[db][1]);
+            dq[db] = MF<T>::mma(as_frag<frag>(u32x4{lo[0], lo[1], hi[0], hi[1]}), pf, dq[db]);
+          }
+        }
+        if constexpr (kDqGroups) {
+          // the 16 row reads ahead of the S^T / dP^T MFMAs, the 16 transposed reads under them
+          __builtin_amdgcn_sched_group_barrier(0x100, kDqAhead, 0);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, (32 - kDqAhead + 15) / 16, 0);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile has landed (asm: untracked)
+    __syncthreads();
+  }
+  if (q < S) {
+    T* qrow = dQ + ((long)b * S + q) * fs.dq_tok + (long)head * fs.dq_head;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(dq[db][4 * gg + 0] * scale, dq[db][4 * gg + 1] * scale);
+        w[1] = MF<T>::pack(dq[db][4 * gg + 2] * scale, dq[db][4 * gg + 3] * scale);
+        *reinterpret_cast<u32x2*>(qrow + d) = w;
+      }
+  }
+}
+
 template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(NT2) void fa_bwd_dq_v2(const T* __restrict__ Q, const T* __restrict__ K,
                                                     const T* __restrict__ V, const T* __restrict__ dO,
@@ -1511,6 +1686,11 @@ bool dkdv_v3() {  // PHA_FA_DKDV=v2 selects the unpipelined dK/dV kernel (A/B co
   return !(e && e[0] == 'v' && e[1] == '2');
 }
 
+bool dq_v3() {  // PHA_FA_DQ=v2 selects the register-staged dQ kernel (A/B comparisons)
+  const char* e = getenv("PHA_FA_DQ");
+  return !(e && e[0] == 'v' && e[1] == '2');
+}
+
 bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comparisons)
   const char* e = getenv("PHA_FA_BWD_V1");
   return !(e && e[0] == '1');
@@ -1572,8 +1752,12 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
     else                                                                                                           \
     hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, false>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
                        (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                       \
-    hipLaunchKernelGGL((fa_bwd_dq_v2<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,              \
-                       (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs)
+    if (dq_v3())                                                                                                   \
+      hipLaunchKernelGGL((fa_bwd_dq_v3<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
+                         (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs);                             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((fa_bwd_dq_v2<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
+                         (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs)
     if (causal) { FB2(true); } else { FB2(false); }
 #undef FB2
     return (int)hipGetLastError();

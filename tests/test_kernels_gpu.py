@@ -270,7 +270,7 @@ def test_flash_attention_fwd_bwd(dt, D, causal, S):
         assert err < 3e-2 * max(1.0, scale), (name, err, scale)
 
 
-@pytest.mark.parametrize("mode", ["v2", "v2dkdv", "fused"])
+@pytest.mark.parametrize("mode", ["v2", "v2dkdv", "v2dq", "fused"])
 @pytest.mark.parametrize("causal,S,Sk", [(True, 300, 300), (True, 1024, 1024), (False, 200, 520), (True, 520, 200),
                                          (False, 64, 1000)])
 def test_flash_attention_bwd_paths_gqa(mode, causal, S, Sk, monkeypatch):
@@ -278,8 +278,9 @@ def test_flash_attention_bwd_paths_gqa(mode, causal, S, Sk, monkeypatch):
     v2 dK/dV kernel, single-kernel with atomic fp32 dQ) against fp32, with GQA (8 query heads on 2
     kv heads), ragged lengths and cross attention."""
     from paddle_hackathon_amd.ops import hip
-    monkeypatch.setenv("PHA_FA_BWD", "v2" if mode == "v2dkdv" else mode)
+    monkeypatch.setenv("PHA_FA_BWD", "v2" if mode in ("v2dkdv", "v2dq") else mode)
     monkeypatch.setenv("PHA_FA_DKDV", "v2" if mode == "v2dkdv" else "v3")
+    monkeypatch.setenv("PHA_FA_DQ", "v2" if mode == "v2dq" else "v3")
     torch.manual_seed(1)
     B, H, Hk, D = 2, 8, 2, 128
     q = torch.randn(B, S, H, D, device="cuda").bfloat16().requires_grad_(True)

@@ -37,11 +37,12 @@ def main():
     o = hip.FlashAttention.apply(q, k, v, causal, None)
     do = torch.randn_like(o)
     grads = {}
-    for name, env in (("v2", "v2"), ("v3", "v3")):
+    for name, env, dqe in (("v2", "v2", "v2"), ("v3dkdv", "v3", "v2"), ("v3", "v3", "v3")):
         os.environ["PHA_FA_DKDV"] = env
+        os.environ["PHA_FA_DQ"] = dqe
         grads[name] = torch.autograd.grad(o, (q, k, v), do, retain_graph=True)
         t = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True), 5)
-        print(f"bwd dkdv {name}: {t * 1e3:.3f} ms  {2.5 * fl / t / 1e12:.1f} TF (useful flops)", flush=True)
+        print(f"bwd {name}: {t * 1e3:.3f} ms  {2.5 * fl / t / 1e12:.1f} TF (useful flops)", flush=True)
     for n, a, b in zip("qkv", grads["v2"], grads["v3"]):
         print(f"  d{n} v3 vs v2 max diff {(a.float() - b.float()).abs().max().item():.5f} "
               f"(scale {a.float().abs().max().item():.3f})", flush=True)
