@@ -279,6 +279,18 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
 //  * everything else (swapped S^T = K Q^T, lane-local online softmax, deferred rescale,
 //    accumulator-as-B-operand P^T) as in fa_fwd_kernel.
 // ============================================================================================
+// LDS-DMA 16 B per lane: global (sbase + voff) -> LDS m0 + lane * 16 (issued from asm so the
+// compiler's waitcnt pass does not drain it at the first LDS read; the kernel waits explicitly)
+__device__ __forceinline__ void fa_glds16(unsigned voff, const void* sbase, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+
+constexpr bool kFwdGroups = true;   // fa_fwd_v3_kernel's read-ahead interleave
+#ifndef PHA_FWD_AHEAD
+#define PHA_FWD_AHEAD 8
+#endif
+constexpr int kFwdAhead = PHA_FWD_AHEAD;
 constexpr int BM2 = 256;
 constexpr int NT2 = 512;
 
@@ -446,6 +458,195 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v2_kernel(const T* __restrict__ Q,
       }
     }
     if (t + 1 < ntile) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (q < S) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    T* orow = O + ((long)b * S + q) * fs.o_tok + (long)head * fs.o_head;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(o[db][4 * gg + 0] * inv, o[db][4 * gg + 1] * inv);
+        w[1] = MF<T>::pack(o[db][4 * gg + 2] * inv, o[db][4 * gg + 3] * inv);
+        *reinterpret_cast<u32x2*>(orow + d) = w;
+      }
+    if (h == 0) {
+      const float lse = (l_run > 0.f) ? (m_run + log2f(l_run)) * kLn2 : INFINITY;
+      LSE[((long)b * H + head) * S + q] = lse;
+    }
+  }
+}
+
+// Forward v3 (D = 128, default): fa_fwd_v2's geometry with K / V tiles by LDS-DMA (no staging
+// registers, no ds_write), the mask folded into the score accumulators' initial values (-inf where
+// masked: the max / exp loops have no selects), lane-offset + immediate LDS addressing and the
+// K-row reads issued ahead of the QK^T MFMAs.
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q, const T* __restrict__ K,
+                                                        const T* __restrict__ V, T* __restrict__ O,
+                                                        float* __restrict__ LSE, int S, int Sk, int H, int Hk,
+                                                        float scale_log2, FaStrides fs) {
+  typedef typename MF<T>::frag frag;
+  constexpr int ND = 4, NK = 8;
+  constexpr int TILE = BN * 128 * 2;                 // 16 KiB per K or V tile
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * 2 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            lr = lane & 31;
+  const int nqb = (S + BM2 - 1) / BM2;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / nqb, nqb, fs.order_g, bh, rank);
+  const int qb = CAUSAL ? (nqb - 1 - rank) : rank;
+  const int head = bh % H, b = bh / H;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM2;
+  const int q = q0 + wid * 32 + lr;
+  const long qstride = fs.q_tok, kstride = fs.kv_tok;
+  const T* Qb = Q + ((long)b * S) * qstride + (long)head * fs.q_head;
+  const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
+
+  frag qf[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 v = {0, 0, 0, 0};
+    if (q < S) v = *reinterpret_cast<const u32x4*>(Qb + (long)q * qstride + 16 * kk + 8 * h);
+    qf[kk] = as_frag<frag>(v);
+  }
+  f32x16 o[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) o[i] = zero16();
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM2);
+  const int ntile = (kend + BN - 1) / BN;
+  const int wave_q0 = q0 + wid * 32, wave_qmax = wave_q0 + 31;
+
+  // K / V tile by LDS-DMA: 32 1-KiB pieces (4 rows of one operand), 4 per wave; K rows swizzled as
+  // k_lds_off (chunk ^ row & 15), V rows as v_lds_off (the tr-read image)
+  auto load_tile = [&](int k0, int buf) {
+    const unsigned lds = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)(smem + buf * 2 * TILE);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gidx = wid * 4 + u, which = gidx >> 4;
+      const int row = (gidx & 15) * 4 + (lane >> 4);
+      const int ch = (lane & 15) ^ (which ? (((row & 3) << 2) | ((row >> 2) & 3)) : (row & 15));
+      const T* base = (which ? Vb : Kb) + (long)k0 * kstride;
+      const unsigned voff = (unsigned)(((long)(min(k0 + row, Sk - 1) - k0) * kstride + ch * 8) * 2);
+      fa_glds16(voff, base, __builtin_amdgcn_readfirstlane(lds + which * TILE + (gidx & 15) * 1024));
+    }
+  };
+
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  int koff[NK], troff[ND][2];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) koff[kk] = lr * 256 + 16 * ((2 * kk + h) ^ (lr & 15));
+#pragma unroll
+  for (int db = 0; db < ND; ++db)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi)
+      troff[db][hi] = (4 * h + tq) * 256 + hi * 2048 +
+                      16 * (4 * (db ^ tq) + ((2 * (g & 1) + (tp >> 1)) ^ ((h + 2 * hi) & 3))) + 8 * (tp & 1);
+
+  if (ntile > 0) {
+    load_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * BN;
+    const int cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + BN, cur ^ 1);
+    const unsigned char* kl = smem + cur * 2 * TILE;
+    const unsigned char* vl = kl + TILE;
+    if (!(CAUSAL && k0 > wave_qmax)) {
+      const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wave_q0);
+      f32x16 s[2];
+      s[0] = zero16();
+      s[1] = zero16();
+      if (need_mask) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int base = k0 + kb * 32 + 4 * h;
+          const int lim1 = CAUSAL ? q - base : 1 << 20, lim2 = Sk - base;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rb = (r & 3) + 8 * (r >> 2);
+            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(kl + kb * 8192 + koff[kk]);
+          s[kb] = MF<T>::mma(as_frag<frag>(a), qf[kk], s[kb]);
+        }
+      if constexpr (kFwdGroups) {
+        __builtin_amdgcn_sched_group_barrier(0x100, kFwdAhead, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // scores unscaled (scale > 0: max(c s) = c max(s)); masked scores are -inf already
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kb][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
+      constexpr float kThr = 8.f;
+      if (!__all(tmax <= m_run + kThr)) {
+        const float m_new = fmaxf(m_run, tmax);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = fexp2(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        m_run = m_new;
+      }
+      const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(s[kb][r], scale_log2, -m_use));
+          s[kb][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 32, 64);
+      l_run += psum;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f32x16& sv = s[ks >> 1];
+        const int s8 = (ks & 1) * 8;
+        u32x4 pw;
+        pw[0] = MF<T>::pack(sv[s8 + 0], sv[s8 + 1]);
+        pw[1] = MF<T>::pack(sv[s8 + 2], sv[s8 + 3]);
+        pw[2] = MF<T>::pack(sv[s8 + 4], sv[s8 + 5]);
+        pw[3] = MF<T>::pack(sv[s8 + 6], sv[s8 + 7]);
+        const frag pf = as_frag<frag>(pw);
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          const u32x2 lo = ds_read_tr16(vl + ks * 4096 + troff[db][0]);
+          const u32x2 hi = ds_read_tr16(vl + ks * 4096 + troff[db][1]);
+          o[db] = MF<T>::mma(as_frag<frag>(u32x4{lo[0], lo[1], hi[0], hi[1]}), pf, o[db]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile has landed (asm: untracked)
     __syncthreads();
   }
 
@@ -1098,12 +1299,6 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
   }
 }
 
-// LDS-DMA 16 B per lane: global (sbase + voff) -> LDS m0 + lane * 16 (issued from asm so the
-// compiler's waitcnt pass does not drain it at the first LDS read; the kernel waits explicitly)
-__device__ __forceinline__ void fa_glds16(unsigned voff, const void* sbase, unsigned m0) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
-}
 
 // ============================================================================================
 // Backward v3 dK/dV (D = 128, default): fa_bwd_dkdv_v2's geometry (4 waves, 32 keys per wave on
@@ -1686,6 +1881,11 @@ bool dkdv_v3() {  // PHA_FA_DKDV=v2 selects the unpipelined dK/dV kernel (A/B co
   return !(e && e[0] == 'v' && e[1] == '2');
 }
 
+bool fwd_v3() {  // PHA_FA_FWD=v2 selects the register-staged forward kernel (A/B comparisons)
+  const char* e = getenv("PHA_FA_FWD");
+  return !(e && e[0] == 'v' && e[1] == '2');
+}
+
 bool dq_v3() {  // PHA_FA_DQ=v2 selects the register-staged dQ kernel (A/B comparisons)
   const char* e = getenv("PHA_FA_DQ");
   return !(e && e[0] == 'v' && e[1] == '2');
@@ -1717,7 +1917,11 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
   if (fsp && !v2) return (int)hipErrorInvalidValue;
   if (v2) {
     const dim3 g2(B * H, (S + BM2 - 1) / BM2), b2(NT2);
-    if (causal)
+    if (fwd_v3() && causal)
+      hipLaunchKernelGGL((fa_fwd_v3_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
+    else if (fwd_v3())
+      hipLaunchKernelGGL((fa_fwd_v3_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
+    else if (causal)
       hipLaunchKernelGGL((fa_fwd_v2_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
     else
       hipLaunchKernelGGL((fa_fwd_v2_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);

@@ -298,6 +298,23 @@ def test_flash_attention_bwd_paths_gqa(mode, causal, S, Sk, monkeypatch):
         assert err < 3e-2 * max(1.0, scale), (mode, name, err, scale)
 
 
+@pytest.mark.parametrize("causal,S,Sk", [(True, 300, 300), (False, 200, 520), (True, 520, 200), (False, 64, 1000)])
+def test_flash_attention_fwd_v2_v3(causal, S, Sk, monkeypatch):
+    """The LDS-DMA forward (v3, default) and the register-staged one (v2) against fp32, GQA and
+    ragged / cross-attention lengths."""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(2)
+    B, H, Hk, D = 2, 8, 2, 128
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    k = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16()
+    v = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16()
+    ref = _ref_attn(q, k, v, causal)
+    for mode in ("v2", "v3"):
+        monkeypatch.setenv("PHA_FA_FWD", mode)
+        o = hip.FlashAttention.apply(q, k, v, causal, None)
+        assert (o.float() - ref).abs().max().item() < 2e-2, mode
+
+
 def test_flash_attention_gqa():
     from paddle_hackathon_amd.ops import hip
     torch.manual_seed(0)

@@ -31,9 +31,14 @@ def main():
     torch.manual_seed(0)
     q, k, v = (torch.randn(B, S, H, D, device="cuda").to(torch.bfloat16).requires_grad_(True) for _ in range(3))
     fl = 4 * B * H * S * S * D / (2 if causal else 1)
-    with torch.no_grad():
-        t = timeit(lambda: hip.FlashAttention.apply(q, k, v, causal, None))
-    print(f"fwd: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF", flush=True)
+    outs = {}
+    for name in ("v2", "v3"):
+        os.environ["PHA_FA_FWD"] = name
+        with torch.no_grad():
+            outs[name] = hip.FlashAttention.apply(q, k, v, causal, None)
+            t = timeit(lambda: hip.FlashAttention.apply(q, k, v, causal, None))
+        print(f"fwd {name}: {t * 1e3:.3f} ms  {fl / t / 1e12:.1f} TF", flush=True)
+    print(f"  fwd v3 vs v2 max diff {(outs['v2'].float() - outs['v3'].float()).abs().max().item():.5f}", flush=True)
     o = hip.FlashAttention.apply(q, k, v, causal, None)
     do = torch.randn_like(o)
     grads = {}
