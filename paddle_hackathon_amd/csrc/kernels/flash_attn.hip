@@ -286,7 +286,10 @@ __device__ __forceinline__ void fa_glds16(unsigned voff, const void* sbase, unsi
                :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
 }
 
-constexpr bool kFwdGroups = true;   // fa_fwd_v3_kernel's read-ahead interleave
+#ifndef PHA_FA_GROUPS
+#define PHA_FA_GROUPS 7   // sched_group_barrier interleaves on: bit 0 dK/dV v3, bit 1 dQ v3, bit 2 forward v3
+#endif
+constexpr bool kFwdGroups = (PHA_FA_GROUPS >> 2) & 1;   // fa_fwd_v3_kernel's read-ahead interleave
 #ifndef PHA_FWD_AHEAD
 #define PHA_FWD_AHEAD 8
 #endif
@@ -1116,12 +1119,12 @@ constexpr int NTKV = 256;
 constexpr bool kSplitMaskDkdv = true;
 constexpr bool kSplitMaskDq = false;
 constexpr bool kDqBareExp = true;
-constexpr bool kDkdvGroups = true;   // fa_bwd_dkdv_v3's sched_group_barrier interleave
+constexpr bool kDkdvGroups = PHA_FA_GROUPS & 1;   // fa_bwd_dkdv_v3's sched_group_barrier interleave
 #ifndef PHA_DKDV_AHEAD
 #define PHA_DKDV_AHEAD 16
 #endif
 constexpr int kDkdvAhead = PHA_DKDV_AHEAD;   // operand reads issued before the first S / dP MFMA
-constexpr bool kDqGroups = true;   // fa_bwd_dq_v3's read-ahead interleave
+constexpr bool kDqGroups = (PHA_FA_GROUPS >> 1) & 1;   // fa_bwd_dq_v3's read-ahead interleave
 #ifndef PHA_DQ_AHEAD
 #define PHA_DQ_AHEAD 8
 #endif

@@ -129,6 +129,9 @@ for s in "$@"; do
     fa_bwd)
       timeout -k 10 300 python tools/bench_fa_bwd.py > $OUT/fa_bwd.log 2>&1; rc=$?
       cat $OUT/fa_bwd.log | tail -12 ;;
+    fa_variants)
+      rc=0; for lib in ${FA_LIBS:-libpha_kernels.so}; do echo "--- $lib"; PHA_KERNELS_LIB=$lib FA_QUICK=1 timeout -k 10 120 python tools/bench_fa_bwd.py 2>&1 | grep -E "fwd|bwd" || { rc=1; break; }; done > $OUT/fa_variants.log 2>&1
+      cat $OUT/fa_variants.log ;;
     tests_flash)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "flash" > $OUT/pytest_flash.log 2>&1; rc=$?
       tail -5 $OUT/pytest_flash.log ;;
