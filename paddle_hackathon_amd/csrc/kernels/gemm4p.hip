@@ -41,6 +41,7 @@ enum : int {
   EPI_ROUNDS = 8192,  // measurement only: round-robin tile order (lin = r * G + pos) instead of XCD chunks
   EPI_TEMPORAL = 16384,  // stores with the default cache policy (else non-temporal)
   EPI_RSTAGE = 32768,    // NT: register-staged operands (global_load -> VGPR -> ds_write) instead of LDS-DMA
+  EPI_EARLY = 65536,     // early-release schedule (see the EARLY main loop)
 };
 
 struct Args {
@@ -144,7 +145,7 @@ struct Sched {
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
 template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
-          bool GELU = false, bool RS = false>
+          bool GELU = false, bool RS = false, bool EARLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -480,6 +481,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // stores one epilogue phase issues per lane: 32 pairs
   constexpr int NST = 32;
 
+  // EARLY schedule (the buffer-release pattern of hipBLASLt's gfx950 NT kernel, profiles/README.md
+  // round 3): phase A reads its 16 next-k-half fragments in a burst (groups 0-3), then
+  // lgkmcnt(0) + barrier releases the K-tile's LDS buffer at group 4, so the next-next K-tile's 16
+  // DMAs go out in A's groups 4-15 and B's groups 0-3 — one K-tile ahead of where the plain
+  // schedule can issue them; the A/B boundary waits with a counted vmcnt for the previous set only.
+  // Each DMA gets >= 112 MFMAs of latency cover instead of >= 64.
+  auto phaseE = [&](auto mode_c, auto rel_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8], uint4 (&nb)[8],
+                    int rbuf, int rkh, int stbuf) {
+    constexpr int MODE = decltype(mode_c)::value;
+    constexpr bool REL = decltype(rel_c)::value;   // phase A: read burst, release barrier, DMAs 0-11
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if constexpr (REL) {
+        if (s < 4) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int r = 4 * s + q;
+            if (r & 1) nb[r >> 1] = readB(rbuf, rkh, r >> 1);
+            else na[r >> 1] = readA(rbuf, rkh, r >> 1);
+          }
+        }
+        if (s == 4) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          bar();
+          stage_begin(stbuf);
+        }
+        if (s >= 4) stage_one(s - 4);
+      } else {
+        if constexpr (SCHED & 2) {
+          if (s & 1) nb[s >> 1] = readB(rbuf, rkh, s >> 1);
+          else na[s >> 1] = readA(rbuf, rkh, s >> 1);
+        } else if (s < 8) {
+#pragma unroll
+          for (int r = 2 * s; r < 2 * s + 2; ++r) {
+            if (r == 0) na[0] = readA(rbuf, rkh, 0);
+            else if (r <= 8) nb[r - 1] = readB(rbuf, rkh, r - 1);
+            else na[r - 8] = readA(rbuf, rkh, r - 8);
+          }
+        }
+        if (s < 4) stage_one(12 + s);
+      }
+      const int i = s >> 1, jb = (s & 1) * 4;
+      if constexpr (MODE == 2 && SPLIT) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) store_f32(acc[i][jb + q], i, jb + q);
+      } else if constexpr (MODE == 2) {
+        if constexpr (!OT) {
+          store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+          store_pair(acc[i][jb + 2], acc[i][jb + 3], i, jb + 2);
+        } else if ((i & 1) == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) store_pair(acc[i][jb + q], acc[i + 1][jb + q], jb + q, i);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = jb + q;
+        if constexpr (MODE == 0) {
+          if constexpr (OT) acc[i][j] = Mf<T>::mma(ca[i], cb[j], acc[i][j]);
+          else acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
+        } else {
+          if constexpr (OT) mma0<T>(acc[i][j], ca[i], cb[j]);
+          else mma0<T>(acc[i][j], cb[j], ca[i]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   // ---- prologue ----------------------------------------------------------------------------------
   set_tile(0);
 #pragma unroll
@@ -510,6 +581,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int s = 0;   // global K-tile step; buffer s & 1
+  if constexpr (EARLY && !SKIPEPI && !RS) {
+    using yes = std::true_type;
+    using no = std::false_type;
+    using M0 = std::integral_constant<int, 0>;
+    using M2 = std::integral_constant<int, 2>;
+    // VMEM ops younger than the previous K-tile's DMAs at the A/B boundary: phase A's 12 DMAs, plus
+    // an epilogue phase's stores (capped at the counter's 63)
+    constexpr int NSTE = (SPLIT || GELU) ? 64 : 32;
+    constexpr int VB2 = 12 + NSTE > 63 ? 63 : 12 + NSTE;
+    for (int r = 0; sc.valid(r); ++r) {
+      {
+        const int buf = s & 1;
+        phaseE(M2{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(VB2) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        bar();
+        set_epi(r);
+        phaseE(M0{}, no{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        stage_end();
+        ++s;
+      }
+      for (int k = 1; k < nk; ++k, ++s) {
+        const int buf = s & 1;
+        phaseE(M0{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        bar();
+        phaseE(M0{}, no{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        stage_end();
+      }
+    }
+  } else {
   using ST1 = std::integral_constant<int, 1>;
   using STB = std::integral_constant<int, RS ? 16 : 1>;         // phase B staging (RS: vmcnt(15))
   using STB2 = std::integral_constant<int, RS ? 16 + 32 : 1>;   // after an epilogue phase's stores
@@ -546,6 +649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       phase(yes{}, M0{}, STB{}, fa1, fb1, fa0, fb0, buf ^ 1, 0);
       stage_end();
     }
+  }
   }
   // last tile: stores only (after the cursor's trailing DMAs have landed)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -590,40 +694,46 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   Vec8<T>::st(c + (long)m * ldc + n, acc);
 }
 
-template <typename T, bool BIAS>
-int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
+template <typename T, bool BIAS, bool E>
+int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
   if (a.splits > 1) {   // TN only (weight gradients)
     if (!(ako && bko && !trans)) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E>), dim3(grid), dim3(256), 0, st, a);
     const long elems = (long)a.M * a.N;
     hipLaunchKernelGGL((splitk_reduce_kernel<T, BIAS>), dim3((unsigned)((elems / 8 + 255) / 256)), dim3(256), 0, st,
                        a.ws, static_cast<T*>(a.c), a.bias, a.M, a.N, a.ldc, a.splits);
     return (int)hipGetLastError();
   }
-  if constexpr (std::is_same<T, bf16_t>::value && !BIAS) {   // measurement build (EPI_SKIP)
+  if constexpr (std::is_same<T, bf16_t>::value && !BIAS && !E) {   // measurement build (EPI_SKIP)
     if ((a.epi & EPI_SKIP) && !ako && !bko && !trans) {
       hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
       return (int)hipGetLastError();
     }
   }
-  if ((a.epi & EPI_RSTAGE) && !ako && !bko && !trans) {
+  if (!E && (a.epi & EPI_RSTAGE) && !ako && !bko && !trans) {
     if (a.epi & EPI_GELU)
       hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true, true>), dim3(grid), dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
   } else if ((a.epi & EPI_GELU) && !ako && !bko && !trans)
-    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (a.epi & EPI_GELU)
     return (int)hipErrorInvalidValue;
   else if (!ako && !bko && !trans)
-    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && bko && !trans)
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && !bko && trans)
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, false, true, BIAS>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, false, true, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
+}
+
+template <typename T, bool BIAS>
+int launch(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
+  if (a.epi & EPI_EARLY) return launch_e<T, BIAS, true>(a, ako, bko, trans, grid, st);
+  return launch_e<T, BIAS, false>(a, ako, bko, trans, grid, st);
 }
 
 }  // namespace g4p

@@ -1273,3 +1273,42 @@ def test_gemm4p_gelu_epilogue(M, N, K):
     for got, ref, what in ((pre, ref_pre, "pre"), (act, ref_act, "act")):
         err = ((got.float() - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-2, (what, err)
+
+
+@pytest.mark.parametrize("layout", ["nt", "nt_bias", "nt_gelu", "tn", "tn_split", "nn"])
+@pytest.mark.parametrize("M,N,K", [(264, 520, 128), (1032, 2056, 512), (2048, 1024, 1024), (296, 8, 64)])
+def test_gemm4p_early_schedule_bitwise(layout, M, N, K):
+    """the early-release main loop (EPI_EARLY) changes only when operands are staged and waited for:
+    outputs equal the default schedule's bit for bit (ragged tiles, bias, GELU aux, split-K, NN)"""
+    from paddle_hackathon_amd.ops import gemm as G
+    torch.manual_seed(5)
+    r = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1).bfloat16()   # noqa: E731
+    if layout.startswith("nt"):
+        a, bt, bias = r(M, K), r(N, K), torch.randn(N, device="cuda")
+        if layout == "nt_gelu":
+            pre0, pre1 = (torch.empty(M, N, dtype=torch.bfloat16, device="cuda") for _ in range(2))
+            c0 = G.gemm_p(a, bt, bias=bias, gelu_aux=pre0)
+            c1 = G.gemm_p(a, bt, bias=bias, gelu_aux=pre1, epi_extra=G.EPI_EARLY)
+            assert torch.equal(pre0, pre1)
+        else:
+            b = bias if layout == "nt_bias" else None
+            c0 = G.gemm_p(a, bt, bias=b)
+            c1 = G.gemm_p(a, bt, bias=b, epi_extra=G.EPI_EARLY)
+        ref = a.float() @ bt.float().t() + (bias if layout != "nt" else 0)
+        if layout == "nt_gelu":
+            ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif layout.startswith("tn"):
+        if K < 256 and layout == "tn_split":
+            pytest.skip("split-K needs >= 4 K-tiles per slice")
+        a, b = r(K, M), r(K, N)
+        sp = 2 if layout == "tn_split" else 1
+        c0 = G.gemm_p(a, b, True, True, splits=sp)
+        c1 = G.gemm_p(a, b, True, True, splits=sp, epi_extra=G.EPI_EARLY)
+        ref = a.float().t() @ b.float()
+    else:
+        a, b = r(M, K), r(K, N)
+        c0 = G.nn_p(a, b)
+        c1 = G.nn_p(a, b, epi_extra=G.EPI_EARLY)
+        ref = a.float() @ b.float()
+    assert torch.equal(c0, c1), (c0.float() - c1.float()).abs().max().item()
+    assert (c1.float() - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())

@@ -132,6 +132,18 @@ for s in "$@"; do
     fa_variants)
       rc=0; for lib in ${FA_LIBS:-libpha_kernels.so}; do echo "--- $lib"; PHA_KERNELS_LIB=$lib FA_QUICK=1 timeout -k 10 120 python tools/bench_fa_bwd.py 2>&1 | grep -E "fwd|bwd" || { rc=1; break; }; done > $OUT/fa_variants.log 2>&1
       cat $OUT/fa_variants.log ;;
+    bench_ab)
+      # alternating default / variant (BENCH_AB_ENV, e.g. PHA_GEMM_AUTO_NT=1) runs of the GPT bench on one box
+      rc=0; for i in 1 2; do for v in default variant; do if [ $v = variant ]; then E="$BENCH_AB_ENV"; else E=""; fi; env $E timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-resnet > $OUT/bench_ab_$v$i.log 2>&1 || { rc=1; break 2; }; echo "$v $i $(tail -1 $OUT/bench_ab_$v$i.log | cut -c100-200)"; done; done ;;
+    bench_own)
+      PHA_GEMM_IMPL=own timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} --no-resnet > $OUT/bench_own.log 2>&1; rc=$?
+      tail -1 $OUT/bench_own.log | cut -c1-400 ;;
+    g4p_early)
+      timeout -k 10 300 python tools/g4p_early_ab.py > $OUT/g4p_early.log 2>&1; rc=$?
+      cat $OUT/g4p_early.log | tail -16 ;;
+    tests_gemm)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "gemm or linear or mlp" > $OUT/pytest_gemm.log 2>&1; rc=$?
+      tail -5 $OUT/pytest_gemm.log ;;
     tests_flash)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "flash" > $OUT/pytest_flash.log 2>&1; rc=$?
       tail -5 $OUT/pytest_flash.log ;;
