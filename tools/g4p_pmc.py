@@ -14,8 +14,10 @@ def main():
     for (M, N, K) in ((32768, 2048, 8192), (32768, 8192, 2048)):
         a = torch.randn(M, K, device="cuda").bfloat16()
         b = torch.randn(N, K, device="cuda").bfloat16()
-        for _ in range(3):
-            G.gemm_p(a, b, False, False)
+        for sched in ("0", "1"):   # plain / early-release schedule (dispatch order: 3 + 3, then library)
+            os.environ["PHA_G4P_EARLY"] = sched
+            for _ in range(3):
+                G.gemm_p(a, b, False, False)
         for _ in range(3):
             a @ b.t()
         torch.cuda.synchronize()

@@ -132,12 +132,21 @@ for s in "$@"; do
     fa_variants)
       rc=0; for lib in ${FA_LIBS:-libpha_kernels.so}; do echo "--- $lib"; PHA_KERNELS_LIB=$lib FA_QUICK=1 timeout -k 10 120 python tools/bench_fa_bwd.py 2>&1 | grep -E "fwd|bwd" || { rc=1; break; }; done > $OUT/fa_variants.log 2>&1
       cat $OUT/fa_variants.log ;;
+    prof_g4p)
+      export TMPDIR=/tmp
+      rm -rf $OUT/prof_g4p; mkdir -p $OUT/prof_g4p
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_g4p/pmc1 -o run --output-format csv -- python3 $ROOT/tools/g4p_pmc.py > $OUT/prof_g4p/pmc1.log 2>&1; rc=$?
+      if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g4p/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g4p_pmc.py > $OUT/prof_g4p/pmc2.log 2>&1; rc=$?; fi
+      tail -2 $OUT/prof_g4p/*.log ;;
     bench_ab)
       # alternating default / variant (BENCH_AB_ENV, e.g. PHA_GEMM_AUTO_NT=1) runs of the GPT bench on one box
       rc=0; for i in 1 2; do for v in default variant; do if [ $v = variant ]; then E="$BENCH_AB_ENV"; else E=""; fi; env $E timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-resnet > $OUT/bench_ab_$v$i.log 2>&1 || { rc=1; break 2; }; echo "$v $i $(tail -1 $OUT/bench_ab_$v$i.log | cut -c100-200)"; done; done ;;
     bench_own)
       PHA_GEMM_IMPL=own timeout -k 10 400 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} --no-resnet > $OUT/bench_own.log 2>&1; rc=$?
       tail -1 $OUT/bench_own.log | cut -c1-400 ;;
+    g4p_libs)
+      rc=0; for lib in ${G4P_LIBS:-libpha_kernels.so}; do echo "--- $lib"; PHA_KERNELS_LIB=$lib G4P_QUICK=1 timeout -k 10 200 python tools/g4p_early_ab.py 2>&1 | grep -E "TF|sum" || { rc=1; break; }; done > $OUT/g4p_libs.log 2>&1
+      cat $OUT/g4p_libs.log ;;
     g4p_early)
       timeout -k 10 300 python tools/g4p_early_ab.py > $OUT/g4p_early.log 2>&1; rc=$?
       cat $OUT/g4p_early.log | tail -16 ;;
