@@ -1124,6 +1124,10 @@ constexpr bool kDkdvGroups = PHA_FA_GROUPS & 1;   // fa_bwd_dkdv_v3's sched_grou
 #define PHA_DKDV_AHEAD 16
 #endif
 constexpr int kDkdvAhead = PHA_DKDV_AHEAD;   // operand reads issued before the first S / dP MFMA
+#ifndef PHA_DKDV_ASM_SP
+#define PHA_DKDV_ASM_SP 1
+#endif
+constexpr bool kDkdvAsmSP = PHA_DKDV_ASM_SP;   // fa_bwd_dkdv_v3: S / dP chains as asm MFMAs into VGPRs
 constexpr bool kDqGroups = (PHA_FA_GROUPS >> 1) & 1;   // fa_bwd_dq_v3's read-ahead interleave
 #ifndef PHA_DQ_AHEAD
 #define PHA_DQ_AHEAD 8
@@ -1303,6 +1307,17 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 }
 
 
+// D (VGPR) += A (VGPR) * B (AGPR) on the 32x32x16 MFMA, D tied in place
+template <typename T>
+__device__ __forceinline__ void mma_vva(f32x16& d, const u32x4& a, const typename MF<T>::frag& b) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u va = __builtin_bit_cast(v4u, a), vb = __builtin_bit_cast(v4u, b);
+  if constexpr (std::is_same<T, bf16_t>::value)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(va), "a"(vb));
+  else
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(va), "a"(vb));
+}
+
 // ============================================================================================
 // Backward v3 dK/dV (D = 128, default): fa_bwd_dkdv_v2's geometry (4 waves, 32 keys per wave on
 // the lane, K/V fragments and dK^T/dV^T in registers, 64-query tiles as two 32-row halves) with
@@ -1417,6 +1432,18 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
     constexpr int P = decltype(par_c)::value, Q = P ^ 1;
     constexpr bool DA = decltype(a_c)::value;
     f32x16 sa, da;
+    // C's transposed operand reads (issued under A's MFMAs)
+    u32x4 cav[2][ND], cbv[2][ND];
+    auto read_c = [&]() {
+      const unsigned char* pdo = pimg + IMG;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          cav[s2][db] = trf(pdo + Q * 8192 + s2 * 4096, db);
+          cbv[s2][db] = trf(pimg + Q * 8192 + s2 * 4096, db);
+        }
+    };
     if constexpr (DA) {
       const unsigned char* rc = img + 2 * IMG + rcoff + P * 128;
 #pragma unroll
@@ -1439,27 +1466,41 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
         }
       }
       const unsigned char* do_img = img + IMG;
+      if constexpr (kDkdvAsmSP) {
+        // all 16 operand reads, then C's 32 transposed reads, then the S / dP chains as asm MFMAs
+        // accumulating in VGPRs (the probability VALU reads them with no accvgpr copies; K / V
+        // fragments come from AGPRs). Inline asm is opaque to the scheduler's grouping, so the
+        // order is fixed in the source: reads first, one LDS latency per step.
+        u32x4 qa[NK], ga[NK];
 #pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const u32x4 qa = lds_b128(img + P * 8192, aoff[kk]);
-        const u32x4 ga = lds_b128(do_img + P * 8192, aoff[kk]);
-        sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
-        da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
+        for (int kk = 0; kk < NK; ++kk) {
+          qa[kk] = lds_b128(img + P * 8192, aoff[kk]);
+          ga[kk] = lds_b128(do_img + P * 8192, aoff[kk]);
+        }
+        read_c();
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 1" ::: "memory");   // a VALU write of the initial values (mask select)
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          mma_vva<T>(sa, qa[kk], kf[kk]);
+          mma_vva<T>(da, ga[kk], vf[kk]);
+        }
+        // an MFMA's VGPR result read by VALU needs 18 wait states after its issue (16-pass
+        // 32x32x16); the compiler does not insert them behind inline asm
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const u32x4 qa = lds_b128(img + P * 8192, aoff[kk]);
+          const u32x4 ga = lds_b128(do_img + P * 8192, aoff[kk]);
+          sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
+          da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
+        }
       }
     }
-    // C's transposed operand reads, issued under A's MFMAs
-    u32x4 cav[2][ND], cbv[2][ND];
-    {
-      const unsigned char* pdo = pimg + IMG;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int db = 0; db < ND; ++db) {
-          cav[s2][db] = trf(pdo + Q * 8192 + s2 * 4096, db);
-          cbv[s2][db] = trf(pimg + Q * 8192 + s2 * 4096, db);
-        }
-    }
-    if constexpr (DA && kDkdvGroups) {
+    if constexpr (!(DA && kDkdvAsmSP)) read_c();
+    if constexpr (DA && kDkdvGroups && !kDkdvAsmSP) {
       // region 1 (CDNA guide T19): all 16 A operand reads first (one LDS latency per step, not
       // one per MFMA pair), then A's 16 MFMAs each with two of C's 32 transposed reads
       __builtin_amdgcn_sched_group_barrier(0x100, kDkdvAhead, 0);

@@ -129,6 +129,9 @@ for s in "$@"; do
     fa_bwd)
       timeout -k 10 300 python tools/bench_fa_bwd.py > $OUT/fa_bwd.log 2>&1; rc=$?
       cat $OUT/fa_bwd.log | tail -12 ;;
+    fa_libcmp)
+      PHA_KERNELS_LIB=libpha_kernels.so timeout -k 10 120 python tools/fa_lib_compare.py save $OUT/fa_a.pt && PHA_KERNELS_LIB=${FA_LIB_B} timeout -k 10 120 python tools/fa_lib_compare.py save $OUT/fa_b.pt && python tools/fa_lib_compare.py cmp $OUT/fa_a.pt $OUT/fa_b.pt > $OUT/fa_libcmp.log 2>&1; rc=$?
+      rm -f $OUT/fa_a.pt $OUT/fa_b.pt; tail -14 $OUT/fa_libcmp.log ;;
     fa_variants)
       rc=0; for lib in ${FA_LIBS:-libpha_kernels.so}; do echo "--- $lib"; PHA_KERNELS_LIB=$lib FA_QUICK=1 timeout -k 10 120 python tools/bench_fa_bwd.py 2>&1 | grep -E "fwd|bwd" || { rc=1; break; }; done > $OUT/fa_variants.log 2>&1
       cat $OUT/fa_variants.log ;;
@@ -153,6 +156,9 @@ for s in "$@"; do
     tests_gemm)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "gemm or linear or mlp" > $OUT/pytest_gemm.log 2>&1; rc=$?
       tail -5 $OUT/pytest_gemm.log ;;
+    fa_stagger)
+      rc=0; for i in 1 2; do for v in 0 1; do echo "--- stagger=$v"; PHA_FA_FWD_STAGGER=$v FA_QUICK=1 timeout -k 10 120 python tools/bench_fa_bwd.py 2>&1 | grep -E "fwd" || { rc=1; break 2; }; done; done > $OUT/fa_stagger.log 2>&1
+      cat $OUT/fa_stagger.log ;;
     tests_flash)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "flash" > $OUT/pytest_flash.log 2>&1; rc=$?
       tail -5 $OUT/pytest_flash.log ;;
