@@ -59,10 +59,12 @@ def _args():
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="ResNet-50: replay the whole training step (fwd + bwd incl. the DataParallel RCCL "
-                         "all-reduce buckets + Momentum) as one hipGraph (paddle.device.cuda.graphs.wrap_cuda_graph) "
-                         "at EVERY world size, so the 1 -> 8 GPU curve compares like with like; auto = on with >= 2 "
-                         "warmup steps (the eager warmup and the capture stay out of the timed steps)")
+                    help="ResNet-50: replay the whole training step (fwd + bwd + Momentum) as one hipGraph "
+                         "(paddle.device.cuda.graphs.wrap_cuda_graph). auto = on for a single rank (also with "
+                         "--force-dp) and off for multi-rank jobs: capturing the DataParallel RCCL all-reduce "
+                         "across ranks is unverified (only one GPU per test box; the gloo rehearsal cannot "
+                         "capture collectives), so multi-rank ResNet timing is eager unless --graph on, which "
+                         "builds the model and reducer on the capture stream and captures the all-reduce")
     ap.add_argument("--force-dp", action="store_true",
                     help="ResNet-50: wrap the model in DataParallel (RCCL reducer) even on one rank — checks the "
                          "graph-captured all-reduce path on a single GPU")
@@ -281,7 +283,25 @@ def bench_bert(a, paddle, dist, world, rank):
                        "final_loss": round(float(loss.item()), 4)}}), flush=True)
 
 
+def _resnet_graphed(a, world):
+    """whether the ResNet step is replayed as one hipGraph (see --graph)"""
+    if a.warmup < 2 or a.graph == "off":
+        return False
+    from paddle_hackathon_amd.parallel import collective
+    if world > 1 and collective.get_backend() != "nccl":
+        return False   # host (gloo) collectives cannot be captured
+    return a.graph == "on" or world == 1
+
+
 def bench_resnet(a, paddle, dist, world, rank, emit=True):
+    import torch
+    # model, reducer hooks and every step run on one stream: the capture stream when graphed
+    cap_stream = torch.cuda.Stream() if _resnet_graphed(a, world) else torch.cuda.current_stream()
+    with torch.cuda.stream(cap_stream):
+        return _bench_resnet(a, paddle, dist, world, rank, emit, cap_stream)
+
+
+def _bench_resnet(a, paddle, dist, world, rank, emit, cap_stream):
     import torch
     from paddle_hackathon_amd.vision.models import resnet50
     model = resnet50(data_format="NHWC")
@@ -309,25 +329,16 @@ def bench_resnet(a, paddle, dist, world, rank, emit=True):
         opt.clear_grad(set_to_zero=False)
         return loss
 
-    graphed = (a.graph in ("on", "auto")) and a.warmup >= 2
-    eager_step = step
+    graphed = _resnet_graphed(a, world)
     if graphed:
         # warmup call 1 runs eagerly (GEMM picks, allocator growth), call 2 captures and replays:
-        # every timed step is one replay of the full forward + backward + optimizer kernels
+        # every timed step is one replay of the full forward + backward + optimizer kernels, on the
+        # stream the model and reducer were built on (autograd's AccumulateGrad nodes then match
+        # the capture stream)
         from paddle_hackathon_amd.device.cuda.graphs import wrap_cuda_graph
         step = wrap_cuda_graph(step)
-    try:
-        elapsed, loss = _timed(a, step, world, rank, dist)
-    except RuntimeError as e:
-        # safety net for the multi-rank capture of the RCCL all-reduce (exercised on one GPU only):
-        # every rank runs the same capture and fails at the same point, so all fall back together
-        if not graphed or a.graph == "on":
-            raise
-        print(f"[bench] rank {rank}: ResNet step capture failed ({str(e).splitlines()[0][:200]}); timing it eagerly",
-              file=sys.stderr, flush=True)
-        torch.cuda.synchronize()
-        graphed = False
-        elapsed, loss = _timed(a, eager_step, world, rank, dist)
+        step._stream = cap_stream
+    elapsed, loss = _timed(a, step, world, rank, dist)
     value = B * world * a.steps / elapsed
     res = {
             "metric": "samples/sec ResNet-50 bf16 (whole job)", "baseline_metric": BASELINE_METRIC,

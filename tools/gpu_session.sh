@@ -141,6 +141,14 @@ for s in "$@"; do
       timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $OUT/prof_g4p/pmc1 -o run --output-format csv -- python3 $ROOT/tools/g4p_pmc.py > $OUT/prof_g4p/pmc1.log 2>&1; rc=$?
       if [ $rc = 0 ]; then timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE -d $OUT/prof_g4p/pmc2 -o run --output-format csv -- python3 $ROOT/tools/g4p_pmc.py > $OUT/prof_g4p/pmc2.log 2>&1; rc=$?; fi
       tail -2 $OUT/prof_g4p/*.log ;;
+    rehearse2)
+      # two ranks sharing the one GPU over gloo: the multi-rank DP path of bench.py (GPT + ResNet; the
+      # multi-rank ResNet step is timed eagerly)
+      PHA_DIST_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 2 > $OUT/rehearse2.log 2>&1; rc=$?
+      grep -E "metric|capture|Error|error" $OUT/rehearse2.log | cut -c1-300 | tail -6 ;;
+    bench_forcedp)
+      timeout -k 10 400 python bench.py --model resnet50 --force-dp --steps 5 --warmup 3 > $OUT/bench_forcedp.log 2>&1; rc=$?
+      tail -1 $OUT/bench_forcedp.log | cut -c1-300 ;;
     bench_ab)
       # alternating default / variant (BENCH_AB_ENV, e.g. PHA_GEMM_AUTO_NT=1) runs of the GPT bench on one box
       rc=0; for i in 1 2; do for v in default variant; do if [ $v = variant ]; then E="$BENCH_AB_ENV"; else E=""; fi; env $E timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-resnet > $OUT/bench_ab_$v$i.log 2>&1 || { rc=1; break 2; }; echo "$v $i $(tail -1 $OUT/bench_ab_$v$i.log | cut -c100-200)"; done; done ;;
