@@ -31,6 +31,13 @@ namespace g4p {
 
 using namespace g256;
 
+#ifndef PHA_G4P_RELG_NT
+#define PHA_G4P_RELG_NT 8
+#endif
+#ifndef PHA_G4P_RELG_TN
+#define PHA_G4P_RELG_TN 8
+#endif
+
 enum : int {
   EPI_BIAS = 1,       // + bias[output column] (fp32)
   EPI_GELU = 2,       // NT only: C = gelu_tanh(acc + bias), and aux = acc (the pre-activation before
@@ -408,6 +415,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   f32x4 acc[8][8];
   uint4 fa0[8], fb0[8], fa1[8], fb1[8];
   constexpr int SCHED = AKO ? 0 : 2;   // read placement, as gemm4w's per-layout winners
+  // EARLY: MFMA group at which phase A's fragment-read burst ends and the buffer is released
+  constexpr int RELG = AKO ? PHA_G4P_RELG_TN : PHA_G4P_RELG_NT;
 
   // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
   // into (na, nb). MODE 0: accumulate; 1: fresh tile (C = 0); 2: fresh tile with the previous
@@ -494,21 +503,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if constexpr (REL) {
-        if (s < 4) {
+        if (s < RELG) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int r = 4 * s + q;
+          for (int q = 0; q < 16 / RELG; ++q) {
+            const int r = (16 / RELG) * s + q;
             if (r & 1) nb[r >> 1] = readB(rbuf, rkh, r >> 1);
             else na[r >> 1] = readA(rbuf, rkh, r >> 1);
           }
         }
-        if (s == 4) {
+        if (s == RELG) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_sched_barrier(0);
           bar();
           stage_begin(stbuf);
         }
-        if (s >= 4) stage_one(s - 4);
+        if (s >= RELG) stage_one(s - RELG);
       } else {
         if constexpr (SCHED & 2) {
           if (s & 1) nb[s >> 1] = readB(rbuf, rkh, s >> 1);
@@ -521,7 +530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             else na[r - 8] = readA(rbuf, rkh, r - 8);
           }
         }
-        if (s < 4) stage_one(12 + s);
+        if (s < RELG) stage_one(16 - RELG + s);
       }
       const int i = s >> 1, jb = (s & 1) * 4;
       if constexpr (MODE == 2 && SPLIT) {
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // VMEM ops younger than the previous K-tile's DMAs at the A/B boundary: phase A's 12 DMAs, plus
     // an epilogue phase's stores (capped at the counter's 63)
     constexpr int NSTE = (SPLIT || GELU) ? 64 : 32;
-    constexpr int VB2 = 12 + NSTE > 63 ? 63 : 12 + NSTE;
+    constexpr int VB2 = 16 - RELG + NSTE > 63 ? 63 : 16 - RELG + NSTE;
     for (int r = 0; sc.valid(r); ++r) {
       {
         const int buf = s & 1;
@@ -605,7 +614,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int k = 1; k < nk; ++k, ++s) {
         const int buf = s & 1;
         phaseE(M0{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
-        asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(16 - RELG) : "memory");
         __builtin_amdgcn_sched_barrier(0);
         bar();
         phaseE(M0{}, no{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);

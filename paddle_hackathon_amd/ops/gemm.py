@@ -180,14 +180,13 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
 
 
 def _epi_default(a_kouter, b_kouter, trans_out, K):
-    """gemm4p main-loop schedule, static by layout and K (bitwise-identical results either way):
-    the early-release schedule for NT products with K >= 4096, where it is 8-9 % faster (longer DMA
-    latency cover); the plain schedule elsewhere, 1-2 % faster at K = 2048 and for the TN weight
-    gradients (profiles/gemm4p_early_ab_r3.log). PHA_G4P_EARLY=1 / 0 forces it on / off."""
-    env = os.environ.get("PHA_G4P_EARLY")
-    if env is not None:
-        return EPI_EARLY if env == "1" else 0
-    return EPI_EARLY if (not a_kouter and not b_kouter and not trans_out and K >= 4096) else 0
+    """gemm4p main-loop schedule (bitwise-identical results either way): the early-release schedule
+    on every layout — phase A's fragment reads in a burst over 8 MFMA groups, the LDS buffer
+    released there, the next-next K-tile's DMAs spread over the following 16 groups. 8-9 % faster on
+    long-K NT, ~1 % on the TN weight gradients and K = 2048 NT, +0.3-0.4 % on the whole GPT step
+    (profiles/gemm4p_early_ab_r3.log, gemm4p_relg_ab_r3.log). PHA_G4P_EARLY=0 selects the plain
+    schedule (1 forces the early one)."""
+    return 0 if os.environ.get("PHA_G4P_EARLY", "1") == "0" else EPI_EARLY
 
 
 def nn_p(a, b, bias=None, **kw):
