@@ -417,6 +417,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int SCHED = AKO ? 0 : 2;   // read placement, as gemm4w's per-layout winners
   // EARLY: MFMA group at which phase A's fragment-read burst ends and the buffer is released
   constexpr int RELG = AKO ? PHA_G4P_RELG_TN : PHA_G4P_RELG_NT;
+  static_assert(16 % RELG == 0 && RELG < 16, "the read burst covers the 16 fragment reads in whole groups");
 
   // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
   // into (na, nb). MODE 0: accumulate; 1: fresh tile (C = 0); 2: fresh tile with the previous
