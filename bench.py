@@ -15,7 +15,9 @@ Each step = forward + backward + AdamW update (fp32 master weights) of the full
 bf16 on synthetic token ids; weak scaling (micro-batch per GPU fixed).
 The other half of BASELINE's metric, ResNet-50 bf16 samples/sec (batch 256 per GPU, NHWC,
 Momentum), runs on the same ranks right after the GPT timing and is reported inside the same JSON
-line (``config.resnet50_samples_per_sec``, whole job; ``--no-resnet`` skips it);
+line (``config.resnet50_samples_per_sec``, whole job; ``--no-resnet`` skips it). A single-rank job
+replays that step as one hipGraph and also times it eagerly (``config.resnet50_eager_samples_per_sec``),
+the mode multi-rank jobs use, so the eager numbers form a like-for-like 1 -> N curve;
 ``--model resnet50`` measures only that config.
 Rank 0 prints ONE JSON line.
 """
@@ -193,13 +195,24 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
         r = bench_resnet(a, paddle, dist, world, rank, emit=False)
+        r_eager = r
+        if r["config"]["hip_graph"]:
+            # the same step timed eagerly too, so a 1 -> N curve of the eager numbers compares like
+            # with like (multi-rank jobs time ResNet eagerly unless --graph on)
+            gc.collect()
+            torch.cuda.empty_cache()
+            r_eager = bench_resnet(argparse.Namespace(**{**vars(a), "graph": "off"}), paddle, dist, world, rank,
+                                   emit=False)
         if rank == 0:
             out["config"]["final_loss"] = round(final_loss, 4)
             out["config"].update({"resnet50_samples_per_sec": r["value"],
                                   "resnet50_samples_per_sec_per_gpu": r["config"]["samples_per_sec_per_gpu"],
                                   "resnet50_ms_per_step": r["ms_per_step"],
                                   "resnet50_global_batch": r["config"]["global_batch"],
-                                  "resnet50_hip_graph": r["config"]["hip_graph"]})
+                                  "resnet50_hip_graph": r["config"]["hip_graph"],
+                                  "resnet50_eager_samples_per_sec": r_eager["value"],
+                                  "resnet50_eager_samples_per_sec_per_gpu":
+                                      r_eager["config"]["samples_per_sec_per_gpu"]})
     if rank == 0:
         print(json.dumps(out), flush=True)
 
