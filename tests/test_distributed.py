@@ -452,7 +452,7 @@ def test_gpt_tensor_parallel_matches_single_process():
     loss.backward()
     params = dict(ref.named_parameters())
     for r in res:
-        np.testing.assert_allclose(r["loss"], float(loss.numpy()), rtol=1e-5)
+        np.testing.assert_allclose(r["loss"], float(loss.item()), rtol=1e-5)
         for n in names:
             np.testing.assert_allclose(r[n], params[n]._t.grad.numpy(), rtol=2e-4, atol=2e-6, err_msg=n)
 
