@@ -771,7 +771,7 @@ def test_py_reader_feeds_executor(static_mode):
     got = []
     with pytest.raises(fluid.core.EOFException):
         while True:
-            got.append(float(exe.run(static_mode, fetch_list=[s])[0]))
+            got.append(exe.run(static_mode, fetch_list=[s])[0].item())
     assert got == [0.0, 4.0, 8.0]
 
 
@@ -829,4 +829,4 @@ def test_fluid_optimizers_reduce_quadratic():
                 loss.backward()
                 opt.minimize(loss)
                 opt.clear_gradients()
-            assert float(layers.reduce_sum(layers.square(w)).numpy()) < 16.0, cls.__name__
+            assert layers.reduce_sum(layers.square(w)).item() < 16.0, cls.__name__

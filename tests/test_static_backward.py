@@ -38,7 +38,7 @@ def _dygraph_grads(w1, w2, X, Y):
     h2 = paddle.nn.functional.relu(h1 * 2.0 + h1)
     loss = paddle.mean((paddle.matmul(h2, W2) - paddle.to_tensor(Y)) ** 2)
     loss.backward()
-    out = (float(loss.numpy()), W1.grad.numpy(), W2.grad.numpy())
+    out = (loss.item(), W1.grad.numpy(), W2.grad.numpy())
     paddle.enable_static()
     return out
 
@@ -80,7 +80,7 @@ def test_minimize_with_grad_ops_trains(static_mode):
     assert types[-1] == "adam" and "matmul_grad" in types
     exe = paddle.static.Executor(paddle.CPUPlace())
     exe.run(startup)
-    losses = [float(exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])[0]) for _ in range(40)]
+    losses = [exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])[0].item() for _ in range(40)]
     assert losses[-1] < 0.5 * losses[0]
 
 
@@ -122,4 +122,4 @@ def test_static_amp_loss_scaling(static_mode):
     np.testing.assert_allclose(g2, r2, rtol=1e-5, atol=1e-6)
     assert not bool(inf)
     exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])
-    assert float(state["scale"].numpy()) == 2048.0   # two good steps: scale doubled
+    assert state["scale"].item() == 2048.0   # two good steps: scale doubled

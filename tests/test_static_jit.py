@@ -29,7 +29,7 @@ def test_static_train_clone_and_inference_export(static_mode, tmp_path):
     rng = np.random.RandomState(0)
     X = rng.randn(64, 4).astype("float32")
     Y = X.sum(1, keepdims=True).astype("float32")
-    losses = [float(exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])[0]) for _ in range(60)]
+    losses = [exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])[0].item() for _ in range(60)]
     assert losses[-1] < 0.2 * losses[0]
     (p,) = exe.run(test_prog, feed={"x": X[:5], "y": Y[:5]}, fetch_list=[pred])
     assert p.shape == (5, 1)
