@@ -93,9 +93,12 @@ def main():
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus > 1:
         sys.exit(_self_launch(a))
-    # RCCL collectives are captured into the ResNet step's hipGraph: the NCCL watchdog must not
-    # poll events of captured work (torch's documented setting for graphed DDP)
-    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+    # only when a multi-rank ResNet step captures its RCCL all-reduce into the hipGraph (--graph on)
+    # must the NCCL watchdog stop polling events of captured work (torch's documented setting for
+    # graphed DDP); everywhere else it stays on, so an RCCL fault or desync aborts instead of hanging
+    if int(env_world or 1) > 1 and a.graph == "on" and a.warmup >= 2 and \
+            os.environ.get("PHA_DIST_BACKEND", "nccl") == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
     if env_world is not None and int(env_world) != a.gpus:
         print(f"[bench] WORLD_SIZE={env_world} disagrees with --gpus {a.gpus}", file=sys.stderr, flush=True)
         sys.exit(2)

@@ -244,6 +244,7 @@ class _AutogradGraphs:
             self.bwd.capture_end()
         self.static_grad = list(grads)
         self.in_req = [t.requires_grad for t in self.static_in]
+        self.generation = 0   # forward replays so far: the saved activations belong to the latest
 
     def __call__(self, args, kwargs):
         ins = _tensors_of((args, kwargs), [])
@@ -258,7 +259,8 @@ class _GraphedCall(torch.autograd.Function):
             if dst.data_ptr() != src.data_ptr():
                 dst.detach().copy_(src)
         g.fwd.replay()
-        ctx.g, ctx.n_in = g, n_in
+        g.generation += 1
+        ctx.g, ctx.n_in, ctx.generation = g, n_in, g.generation
         outs = tuple(o.detach() for o in g.static_out)
         ctx.mark_non_differentiable(*[o for o, r in zip(outs, g.out_req) if not r])
         return outs
@@ -266,6 +268,14 @@ class _GraphedCall(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gouts):
         g = ctx.g
+        if ctx.generation != g.generation:
+            # the captured backward reads the static activations of the LATEST forward replay; an
+            # older call's gradients would silently come from the newer call's activations
+            raise RuntimeError(
+                "wrap_cuda_graph: backward of a graphed call after a newer forward replay of the same "
+                "graph (the static activation buffers were overwritten). Run backward before calling "
+                "the graphed Layer again, or wrap each call site (weight sharing, several micro-batches "
+                "per backward) in its own wrap_cuda_graph")
         k = 0
         for go, r in zip(gouts, g.out_req):
             if r:
@@ -402,7 +412,12 @@ def wrap_cuda_graph(function, mode="thread_local", memory_pool="default", warmup
     (a Layer's forward is wrapped in place and the Layer returned). Static mode: the ops the
     function records are tagged ``_cuda_graph_attr`` = "mode;pool;id" like the reference's
     ``_cuda_graph_guard`` (carried in the Program IR; ``CompiledProgram`` with
-    ``build_strategy.use_hip_graph`` replays a program as one hipGraph)."""
+    ``build_strategy.use_hip_graph`` replays a program as one hipGraph).
+
+    Limitation of a differentiable graphed call: its outputs and saved activations are the
+    captured static buffers, so only the LATEST call can be backpropagated. Calling the graphed
+    Layer twice before backward (a weight-shared block, several micro-batches, several losses)
+    makes the older call's backward raise instead of silently using the newer activations."""
     from ...framework import core as _core
     from ...nn import Layer
     if mode not in ALL_MODES:

@@ -1,6 +1,7 @@
 """``fluid.contrib`` (reference: python/paddle/fluid/contrib): the mixed-precision decorator
-(``contrib.mixed_precision.decorate``) and ``BasicGRUUnit`` / ``BasicLSTMUnit``."""
+(``contrib.mixed_precision.decorate``), the 1.x ``BasicGRUUnit`` / ``BasicLSTMUnit`` and the
+slim quantization passes (``contrib.slim``)."""
 from . import mixed_precision  # noqa: F401
-from ..layers.rnn import GRUCell as BasicGRUUnit, LSTMCell as BasicLSTMUnit  # noqa: F401
+from .rnn_impl import BasicGRUUnit, BasicLSTMUnit  # noqa: F401
 
 __all__ = ["mixed_precision", "BasicGRUUnit", "BasicLSTMUnit"]

@@ -30,16 +30,21 @@ class _AMPOptimizer:
         self._scaler = None
 
     def get_loss_scaling(self):
-        return self._cfg["init_loss_scaling"]
+        """the current loss scale (a Variable-backed tensor after a static minimize)"""
+        st = getattr(self, "_state", None)
+        return st["scale"] if st is not None else self._cfg["init_loss_scaling"]
 
     def minimize(self, loss, startup_program=None, parameter_list=None, no_grad_set=None):
         if not _core.in_dynamic_mode():
             from ...static.backward import append_backward, append_optimize_op
             from ...static import passes
             pg = append_backward(loss, parameter_list, no_grad_set)
-            pg, found = passes.insert_loss_scaling(pg, **self._cfg) if hasattr(passes, "insert_loss_scaling") \
-                else (pg, None)
-            return append_optimize_op(self._optimizer, pg), pg
+            c = self._cfg
+            pg, found, self._state = passes.insert_loss_scaling(
+                loss.block.program, loss, pg, init_scale=c["init_loss_scaling"],
+                incr_every_n_steps=c["incr_every_n_steps"], decr_every_n_nan_or_inf=c["decr_every_n_nan_or_inf"],
+                incr_ratio=c["incr_ratio"], decr_ratio=c["decr_ratio"], dynamic=c["use_dynamic_loss_scaling"])
+            return [append_optimize_op(self._optimizer, pg, found_inf=found)], pg
         from ...amp import GradScaler
         if self._scaler is None:
             c = self._cfg

@@ -101,6 +101,16 @@ def c_broadcast_coalesced(xs, root=0, ring_id=0):
     return tuple(xs)
 
 
+def c_allreduce_max(x, ring_id=0):
+    """max-all-reduce of a scalar flag / tensor (the AMP found_infinite sync)"""
+    t = x._t.detach()
+    buf = t.reshape(-1).to(torch.float32).clone()
+    if tdist.is_available() and tdist.is_initialized():
+        tdist.all_reduce(buf, op=tdist.ReduceOp.MAX, group=_group(ring_id))
+    out = buf.reshape(t.shape)
+    return _wrap(out > 0 if t.dtype == torch.bool else out.to(t.dtype))
+
+
 _ASYNC = {}   # id(start op) -> (work handle, flat buffer, tensors)
 
 
@@ -261,6 +271,8 @@ class StaticFleetOptimizer:
             ring, comm_world, scale = self.comm
         if comm_world > 1 and not sharding:
             grads = self._insert_overlapped_allreduce(blk, grads, int(fuse_mb * 2 ** 20), ring, comm_world, scale)
+        if self._found_inf is not None and (comm_world > 1 or sharding):
+            self._sync_found_inf(blk, ring)
         owned = list(range(len(params)))
         if sharding:
             # greedy size-balanced ownership (reference sharding/shard.py)
@@ -360,6 +372,23 @@ class StaticFleetOptimizer:
                     tdist.broadcast(p._t.data, src=dp_g.ranks[0], group=C._resolve_group(dp_g))
         register_ring(2, C._resolve_group(dp_g))
         return 2, dp_g.nranks
+
+    def _sync_found_inf(self, blk, ring):
+        """every rank checked only its LOCAL gradients for inf/nan, before the all-reduce; an
+        overflow on one rank reaches all of them through the sum. Max-all-reduce the flag over the
+        gradient ring (the reference's c_allreduce_max on found_infinite,
+        fleet/meta_optimizers/amp_optimizer.py + sharding's check group) and move
+        update_loss_scaling behind it, so every rank skips the same step and keeps the same scale."""
+        flag = self._found_inf
+        synced = P.Variable(blk, torch.empty((), dtype=torch.bool, device="meta"), flag.name + "@GLOBAL")
+        blk.vars[synced.name] = synced
+        _op(blk, c_allreduce_max, {"x": flag, "ring_id": ring}, synced, "c_allreduce_max")
+        upd = [op for op in blk.ops if op.type == "update_loss_scaling" and op.kwargs.get("found_inf") is flag]
+        for op in upd:
+            blk.ops.remove(op)
+            op.kwargs = dict(op.kwargs, found_inf=synced)
+            blk.append_op(op)
+        self._found_inf = synced
 
     def _insert_overlapped_allreduce(self, blk, grads, bucket_bytes, ring=0, world=None, scale=None):
         """buckets in gradient-ready order (position of each grad's producing op); each bucket's

@@ -13,8 +13,9 @@ first consumer. One rank runs one stage (rank = stage index within the pipeline 
 
 Schedule. ``Executor.run`` on a pipelined program splits the feed along the batch dimension into
 ``accumulate_steps`` micro-batches, runs every micro-batch's forward section, then every
-micro-batch's backward section (GPipe order; all ranks walk the same op sequence, so message
-tags match and the non-blocking sends cannot deadlock), averages each parameter gradient over
+micro-batch's backward section (GPipe order; all ranks walk the same op sequence; receives are
+posted in each sender's send order — RCCL matches point-to-point messages by order, not tag — and
+the non-blocking sends cannot deadlock), averages each parameter gradient over
 the micro-batches and applies the inner optimizer to the stage's own parameters. Fetches of a
 variable computed on this stage return the mean over micro-batches (None on other stages).
 """
@@ -160,18 +161,44 @@ class PipelineRunner:
                 ps = self.producer_stage.get(id(v))
                 if ps is not None and ps != st:
                     self.consumers.setdefault(id(v), set()).add(st)
-        self.tags = {}
-        for op in self.fwd_ops + self.bwd_ops:
-            for v in P._iter_vars(op.outputs):
-                self.tags.setdefault(id(v), len(self.tags))
+        # Message order. RCCL pairs point-to-point messages by posting order, not by tag, so the
+        # receiver must post its receives in exactly the order the sender posts its sends. Each
+        # (src -> dst) stream is laid out statically: every section in run order (forward of micro-
+        # batches 0..k-1, then their backward), the producer stage's ops in program order, each
+        # op's outputs that dst reads. A receive that needs the n-th message of a stream first
+        # takes messages 0..n-1 (buffered into their micro-batch's environment) — always safe, as
+        # the sender posted them before the n-th.
+        self.streams = {}
+        sections = [(self.fwd_ops, m) for m in range(self.k)] + [(self.bwd_ops, m) for m in range(self.k)]
+        for ops, m in sections:
+            for op in ops:
+                src = self.op_stage[id(op)]
+                for v in P._iter_vars(op.outputs):
+                    for dst in sorted(self.consumers.get(id(v), ())):
+                        if dst != src:
+                            self.streams.setdefault((src, dst), []).append((m, id(v)))
 
     def _inputs(self, op):
         return [v for v in B._op_inputs(self.prog, op) if isinstance(v, P.Variable)]
 
-    def _section(self, ops, env, m, xfer):
+    def _recv_until(self, src, m, vid, envs, xfer):
+        seq = self.streams.get((src, self.stage), [])
+        cur = self._cursor.get(src, 0)
+        while vid not in envs[m]:
+            if cur >= len(seq):
+                raise RuntimeError(f"static pipeline: stage {self.stage} needs a variable stage {src} never sends")
+            mm, want = seq[cur]
+            t = xfer.recv(src, cur, self.device)
+            if t.is_floating_point():
+                t.requires_grad_(True)
+            envs[mm][want] = _wrap(t)
+            cur += 1
+        self._cursor[src] = cur
+
+    def _section(self, ops, envs, m, xfer):
         """run this stage's ops of ``ops`` for micro-batch m, with the transfers around them"""
-        nvars = max(1, len(self.tags))
         me = self.stage
+        env = envs[m]
         fake = P.Block(self.prog)
         for op in ops:
             st = self.op_stage[id(op)]
@@ -179,16 +206,17 @@ class PipelineRunner:
                 for v in self._inputs(op):
                     ps = self.producer_stage.get(id(v))
                     if ps is not None and ps != me and id(v) not in env:
-                        t = xfer.recv(ps, m * nvars + self.tags[id(v)], self.device)
-                        if t.is_floating_point():
-                            t.requires_grad_(True)
-                        env[id(v)] = _wrap(t)
+                        self._recv_until(ps, m, id(v), envs, xfer)
                 fake.ops = [op]
                 P.run_block(self.prog, fake, env)
                 for v in P._iter_vars(op.outputs):
                     for cs in sorted(self.consumers.get(id(v), ())):
-                        if cs != me and id(v) in env:
-                            xfer.send(env[id(v)]._t, cs, m * nvars + self.tags[id(v)])
+                        if cs != me:
+                            if id(v) not in env:
+                                raise RuntimeError(f"static pipeline: {v.name} was not produced on stage {me}")
+                            n = self._sent.get(cs, 0)
+                            xfer.send(env[id(v)]._t, cs, n)
+                            self._sent[cs] = n + 1
 
     @property
     def device(self):
@@ -201,8 +229,9 @@ class PipelineRunner:
         for name, val in feed.items():
             a = val.numpy() if isinstance(val, Tensor) else np.asarray(val)
             parts[name] = np.array_split(a, self.k, axis=0)
-        envs = []
         xfer = _Transfer(self)
+        self._cursor, self._sent = {}, {}
+        envs = []
         for m in range(self.k):
             env = {}
             for name, chunks in parts.items():
@@ -215,10 +244,11 @@ class PipelineRunner:
                 if getattr(v, "need_grad", False) and t.is_floating_point():
                     t.requires_grad_(True)
                 env[id(v)] = _wrap(t)
-            self._section(self.fwd_ops, env, m, xfer)
             envs.append(env)
         for m in range(self.k):
-            self._section(self.bwd_ops, envs[m], self.k + m, xfer)
+            self._section(self.fwd_ops, envs, m, xfer)
+        for m in range(self.k):
+            self._section(self.bwd_ops, envs, m, xfer)
         xfer.wait()
         # average the parameter gradients over the micro-batches, then the inner optimizer
         with torch.no_grad():

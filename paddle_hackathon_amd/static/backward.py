@@ -303,15 +303,22 @@ def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
     return out
 
 
-def append_optimize_op(optimizer, params_grads, program=None, block=None):
+def append_optimize_op(optimizer, params_grads, program=None, block=None, found_inf=None):
     """one fused optimizer op over (param, grad) pairs (reference: the per-parameter optimizer ops
-    fused by fuse_optimizer_ops_pass); type = the optimizer's name (``adamw``, ``momentum`` ...)"""
+    fused by fuse_optimizer_ops_pass); type = the optimizer's name (``adamw``, ``momentum`` ...).
+    found_inf (AMP): a bool Variable; the update is skipped on the steps where it is true (the
+    reference's optimizer ops read it as their SkipUpdate input)."""
     prog = program or P.default_main_program()
     blk = block or prog.current_block()
     ps = tuple(p for p, _ in params_grads)
     gs = tuple(g for _, g in params_grads)
+    if optimizer._parameter_list is None:
+        optimizer._add_param_group({"params": list(ps)})
+        optimizer._parameter_list = list(ps)
 
-    def _update(params, grads):
+    def _update(params, grads, found_inf=None):
+        if found_inf is not None and bool(found_inf._t):
+            return None
         for p, g in zip(params, grads):
             p._t.grad = g._t.detach().to(p._t.dtype)
         with P._core_dynamic():
@@ -319,7 +326,10 @@ def append_optimize_op(optimizer, params_grads, program=None, block=None):
         optimizer.clear_grad(set_to_zero=False)
         return None
 
-    op = P.OpDesc(type(optimizer).__name__.lower(), _update, (), {"params": ps, "grads": gs}, None,
+    kw = {"params": ps, "grads": gs}
+    if found_inf is not None:
+        kw["found_inf"] = found_inf
+    op = P.OpDesc(type(optimizer).__name__.lower(), _update, (), kw, None,
                   attrs={"op_role": OPTIMIZE, "op_role_var": [p.name for p in ps]})
     blk.append_op(op)
     return op

@@ -203,3 +203,22 @@ def test_graphed_adamw_step_matches_eager():
         assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (le, lg)
     for a, b in zip(pe, pg):
         assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), (a - b).abs().max()
+
+
+@pytest.mark.gpu
+def test_graphed_layer_two_live_calls_raise():
+    """two forward replays of one graphed Layer before backward — the older call's
+    backward must refuse (its activations were overwritten), the latest call's still works"""
+    paddle.set_device("gpu:0")
+    lin = graphs.wrap_cuda_graph(paddle.nn.Linear(8, 8))
+    for _ in range(3):   # warmup + capture
+        x = paddle.randn([4, 8])
+        x.stop_gradient = False
+        lin(x).mean().backward()
+    x1, x2 = paddle.randn([4, 8]), paddle.randn([4, 8])
+    x1.stop_gradient = x2.stop_gradient = False
+    y1 = lin(x1)
+    y2 = lin(x2)
+    y2.mean().backward()
+    with pytest.raises(RuntimeError, match="newer forward replay"):
+        y1.mean().backward()

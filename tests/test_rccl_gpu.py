@@ -64,7 +64,7 @@ def _train(paddle, model, opt, steps=3):
         loss.backward()
         opt.step()
         opt.clear_grad()
-        losses.append(float(loss.numpy()))
+        losses.append(float(loss.item()))
     return losses
 
 

@@ -151,3 +151,44 @@ def test_static_amp_matches_single_process():
     assert "check_finite_and_unscale" in out["types"] and "update_loss_scaling" in out["types"]
     import paddle_hackathon_amd as paddle
     paddle.disable_static()
+
+
+def _static_amp_overflow(rank, world):
+    """rank 1 feeds an inf on step 1 only: its local gradients overflow, rank 0's do not"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    paddle.enable_static()
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        loss = _build(paddle)
+        strategy = fleet.DistributedStrategy()
+        strategy.amp = True
+        strategy.amp_configs = {"init_loss_scaling": 256.0, "decr_every_n_nan_or_inf": 1}
+        opt = fleet.distributed_optimizer(paddle.optimizer.SGD(0.1), strategy)
+        opt.minimize(loss)
+    exe = paddle.static.Executor()
+    exe.run(start)
+    half = 8 // world
+    for step in range(3):
+        x = X[rank * half:(rank + 1) * half].copy()
+        if step == 1 and rank == 1:
+            x[0, 0] = np.inf
+        exe.run(main, feed={"x": x, "y": Y[rank * half:(rank + 1) * half]}, fetch_list=[loss])
+    types = [op.type for op in main.global_block().ops]
+    return {"params": [p.numpy() for p in main.all_parameters()], "types": types,
+            "scale": float(opt._amp_state["scale"]._t.item())}
+
+
+def test_static_amp_overflow_on_one_rank_skips_everywhere():
+    """the found_inf flag is max-all-reduced over the data-parallel ring before
+    update_loss_scaling and the update — an overflow on one rank skips the step on every rank,
+    both ranks halve the scale and keep identical, finite parameters"""
+    res = run_dist(_static_amp_overflow, 2)
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        assert np.isfinite(a).all() and np.isfinite(b).all()
+        np.testing.assert_allclose(a, b, rtol=0, atol=0)
+    assert res[0]["scale"] == res[1]["scale"] < 256.0   # decreased once, equally
+    types = res[0]["types"]
+    assert "c_allreduce_max" in types
+    assert types.index("c_allreduce_max") < types.index("update_loss_scaling")
+    assert types.index("c_allreduce_max") > types.index("c_allreduce_wait")

@@ -122,3 +122,60 @@ def test_stage_assignment_and_transfers():
                 assert st[id(op)] == st[id(f)]
     finally:
         paddle.disable_static()
+
+
+def _order_worker(rank, world):
+    """stage 0 produces a (8 wide) THEN b (5 wide); stage 1 reads b first. Every message goes
+    with tag 0, so the gloo pairing is by posting order — RCCL's semantics."""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd import fluid
+    from paddle_hackathon_amd.fluid import layers
+    from paddle_hackathon_amd.parallel.fleet import static_pipeline as SP
+    import torch.distributed as tdist
+
+    class _NoTag:
+        def __getattr__(self, k):
+            return getattr(tdist, k)
+
+        @staticmethod
+        def isend(t, dst, group=None, tag=0):
+            return tdist.isend(t, dst, group=group, tag=0)
+
+        @staticmethod
+        def recv(t, src, group=None, tag=0):
+            return tdist.recv(t, src, group=group, tag=0)
+    SP.tdist = _NoTag()
+    g = np.random.RandomState(3)
+    init = {"wa": g.randn(6, 8).astype("float32") * 0.4, "wb": g.randn(6, 5).astype("float32") * 0.4,
+            "wo1": g.randn(5, 3).astype("float32") * 0.4, "wo2": g.randn(8, 3).astype("float32") * 0.4}
+    paddle.enable_static()
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        x = paddle.static.data("x", [None, 6], "float32")
+        y = paddle.static.data("y", [None, 3], "float32")
+        with paddle.static.device_guard("gpu:0"):
+            a = layers.fc(x, 8, param_attr=fluid.ParamAttr(name="wa"), bias_attr=False, act="tanh")
+            b = layers.fc(x, 5, param_attr=fluid.ParamAttr(name="wb"), bias_attr=False)
+        with paddle.static.device_guard("gpu:1"):
+            o = layers.fc(b, 3, param_attr=fluid.ParamAttr(name="wo1"), bias_attr=False) + \
+                layers.fc(a, 3, param_attr=fluid.ParamAttr(name="wo2"), bias_attr=False)
+            loss = layers.mean(layers.square_error_cost(o, y))
+        params = {p.name: p for p in main.all_parameters()}
+        for k, v in init.items():
+            params[k].set_value(v)
+        fluid.optimizer.PipelineOptimizer(paddle.optimizer.SGD(learning_rate=0.1), num_microbatches=2).minimize(loss)
+    exe = paddle.static.Executor()
+    xv, yv = _data(0)
+    lv, = exe.run(main, feed={"x": xv, "y": yv}, fetch_list=[loss])
+    paddle.disable_static()
+    return None if lv is None else float(np.asarray(lv).reshape(-1)[0]), init, xv, yv
+
+
+def test_pp_receives_follow_send_order_without_tags():
+    res = run_dist(_order_worker, 2)
+    loss1, init, xv, yv = res[1]
+    x, y = torch.tensor(xv), torch.tensor(yv)
+    w = {k: torch.tensor(v) for k, v in init.items()}
+    ref = ((((x @ w["wb"]) @ w["wo1"] + torch.tanh(x @ w["wa"]) @ w["wo2"]) - y) ** 2).mean()
+    assert res[0][0] is None
+    np.testing.assert_allclose(loss1, float(ref), rtol=1e-5)
