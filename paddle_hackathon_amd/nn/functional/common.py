@@ -60,7 +60,13 @@ def linear(x, weight, bias=None, name=None):
         else:
             out = torch.addmm(b, x2d, wt)
         return _w(out.reshape(list(xt.shape[:-1]) + [wt.shape[-1]]))
-    out = torch.matmul(xt, wt)
+    if bias is None and xt.dim() >= 2 and _cg.nt_forward_ok(xt, wt):
+        return _w(_cg.linear_nt(xt, wt))   # the NT product on the cached W^T, like the biased path
+    if xt.is_cuda:
+        from ...ops import gemm as _gemm
+        out = _gemm.matmul(xt, wt)
+    else:
+        out = torch.matmul(xt, wt)
     if bias is not None:
         out = out + bias._t
     return _w(out)

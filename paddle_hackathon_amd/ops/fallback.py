@@ -12,6 +12,7 @@ import os
 import sys
 
 _counts = collections.Counter()
+_lib_counts = collections.Counter()
 _seen = set()
 
 
@@ -25,6 +26,23 @@ def note(op, reason):
         print(f"[pha-fallback] {op}: {reason}", file=sys.stderr, flush=True)
 
 
+def library(op, reason):
+    """a GPU ``op`` ran on a vendor-library kernel BY POLICY (the static GEMM policy of ops/gemm.py
+    keeps the plain NT forward / dX products on hipBLASLt under PHA_GEMM_IMPL=auto): counted apart
+    from the fallbacks so a trace-free run still reports how much of the step left the own kernels.
+    PHA_STRICT_LIBRARY=1 raises."""
+    _lib_counts[op] += 1
+    if os.environ.get("PHA_STRICT_LIBRARY") == "1":
+        raise RuntimeError(f"library kernel: {op} ({reason})")
+    if os.environ.get("PHA_FALLBACK_LOG") and ("lib", op, reason) not in _seen:
+        _seen.add(("lib", op, reason))
+        print(f"[pha-library] {op}: {reason}", file=sys.stderr, flush=True)
+
+
+def library_counts():
+    return dict(_lib_counts)
+
+
 def counts():
     return dict(_counts)
 
@@ -35,4 +53,5 @@ def total():
 
 def reset():
     _counts.clear()
+    _lib_counts.clear()
     _seen.clear()

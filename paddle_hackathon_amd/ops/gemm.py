@@ -40,6 +40,8 @@ def _L():
         L.pha_gemm4w.restype = c_int
         L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P, P]
         L.pha_gemm4p.restype = c_int
+        L.pha_gemm8w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, P]
+        L.pha_gemm8w.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
         L.pha_colsum_finish.restype = c_int
         L._g4w_sig = True
@@ -179,6 +181,27 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
     return c
 
 
+def gemm_8w(a, bt, bias=None, out=None, epi_extra=0, group_m=0):
+    """C = a [M, K] @ bt [N, K]^T (+ bias) on the 8-wave (two waves per SIMD) NT kernel
+    (csrc/kernels/gemm8w.hip)"""
+    assert a.dtype in (torch.bfloat16, torch.float16) and bt.dtype == a.dtype and a.dim() == 2 and bt.dim() == 2
+    assert a.stride(1) == 1 and bt.stride(1) == 1 and a.shape[1] == bt.shape[1]
+    M, K = a.shape
+    N = bt.shape[0]
+    c = out if out is not None else torch.empty(M, N, dtype=a.dtype, device=a.device)
+    assert c.shape == (M, N) and c.stride(1) == 1
+    epi = epi_extra
+    if bias is not None:
+        bias = bias.float().contiguous()
+        assert bias.numel() == N
+        epi |= 1
+    rc = _L().pha_gemm8w(_DT[a.dtype], _ptr(a), _ptr(bt), _ptr(c), M, N, K, a.stride(0), bt.stride(0), c.stride(0),
+                         epi, _ptr(bias), group_m, _stream(a))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm8w failed ({rc}) M={M} N={N} K={K}")
+    return c
+
+
 def _epi_default(a_kouter, b_kouter, trans_out, K):
     """gemm4p main-loop schedule (bitwise-identical results either way): the early-release schedule
     on every layout — phase A's fragment reads in a burst over 8 MFMA groups, the LDS buffer
@@ -244,10 +267,15 @@ def _c(t):
 
 
 def _lib_call(layout, name, shape, fn):
+    """every product that leaves the own kernels is counted: as a fallback when the policy wanted
+    the own kernel (unsupported operands), as a planned library product otherwise (``auto`` NT,
+    ``library``) — ops/fallback.py keeps the two apart"""
+    from . import fallback
     impl = _impl()
     if impl == "own" or (impl == "auto" and layout in _AUTO_OWN):
-        from . import fallback
         fallback.note("matmul", f"{name} {shape} unsupported by the own kernels -> library")
+    else:
+        fallback.library("matmul", f"{name} {shape} on hipBLASLt (PHA_GEMM_IMPL={impl})")
     return fn()
 
 
@@ -359,3 +387,88 @@ def mm_tn(a, b):
             ap, bp = _pad2(a, 64, 8), _pad2(b, 64, 8)
             return gemm_p(ap, bp, True, True, splits=_splits(ap.shape[1], bp.shape[1], ap.shape[0], a.device))[:M, :N]
     return _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)
+
+
+# ----------------------------------------------------------------------------------------------
+# generic products (paddle.matmul / mm / bmm, bias-less F.linear): every bf16 / fp16 GPU product
+# goes through the layouts above (own kernels under PHA_GEMM_IMPL=own, the static per-layout
+# policy under auto); what cannot (fp32, batched with per-batch right operands, both operands
+# transposed) is counted by ops/fallback.py. Reference: phi/kernels/impl/matmul_kernel_impl.h:88
+# (MatMulFunction: 2-D, broadcast-batched and transposed forms) and :489 (MatmulGradKernel).
+# ----------------------------------------------------------------------------------------------
+class _NN(torch.autograd.Function):
+    """C = A [M, K] @ B [K, N]; dA = dC B^T (NT on B), dB = A^T dC (TN)"""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return mm_nn(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = _c(g)
+        return (mm_nt(g, b) if ctx.needs_input_grad[0] else None,
+                mm_tn(a, g) if ctx.needs_input_grad[1] else None)
+
+
+class _NT(torch.autograd.Function):
+    """C = A [M, K] @ Bt [N, K]^T; dA = dC Bt (NN), dBt = dC^T A (TN)"""
+
+    @staticmethod
+    def forward(ctx, a, bt):
+        ctx.save_for_backward(a, bt)
+        return mm_nt(a, bt)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, bt = ctx.saved_tensors
+        g = _c(g)
+        return (mm_nn(g, bt) if ctx.needs_input_grad[0] else None,
+                mm_tn(g, a) if ctx.needs_input_grad[1] else None)
+
+
+class _TN(torch.autograd.Function):
+    """C = At [K, M]^T @ B [K, N]; dAt = B dC^T (NT), dB = At dC (NN)"""
+
+    @staticmethod
+    def forward(ctx, at, b):
+        ctx.save_for_backward(at, b)
+        return mm_tn(at, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        at, b = ctx.saved_tensors
+        g = _c(g)
+        return (mm_nt(b, g) if ctx.needs_input_grad[0] else None,
+                mm_nn(at, g) if ctx.needs_input_grad[1] else None)
+
+
+def _gemm_dtype_ok(a, b):
+    return (a.is_cuda and b.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype
+            and type(a).__name__ != "DTensor" and type(b).__name__ != "DTensor" and _lib.native_available())
+
+
+def matmul(a, b, transpose_a=False, transpose_b=False):
+    """torch.matmul semantics (vectors, broadcast batches, optional transposes of the last two dims);
+    2-D products — and batched left operands against a shared 2-D right operand, flattened into M —
+    run on the own GEMM layouts"""
+    if not (a.is_cuda or b.is_cuda):
+        x = a.transpose(-1, -2) if transpose_a and a.dim() > 1 else a
+        y = b.transpose(-1, -2) if transpose_b and b.dim() > 1 else b
+        return torch.matmul(x, y)
+    if _gemm_dtype_ok(a, b) and a.dim() >= 2 and b.dim() == 2 and not (transpose_a and transpose_b) \
+            and (a.dim() == 2 or not transpose_a):
+        if transpose_a:                       # a [K, M]
+            return _TN.apply(_c(a), _c(b)) if not transpose_b else None
+        lead = a.shape[:-1]
+        a2 = _c(a.reshape(-1, a.shape[-1]))
+        out = _NT.apply(a2, _c(b)) if transpose_b else _NN.apply(a2, _c(b))
+        return out.reshape(*lead, out.shape[-1])
+    from . import fallback
+    why = (f"{a.dtype} product" if not _gemm_dtype_ok(a, b) else
+           f"batched product {tuple(a.shape)} x {tuple(b.shape)}")
+    fallback.note("matmul", why + " on the library")
+    x = a.transpose(-1, -2) if transpose_a and a.dim() > 1 else a
+    y = b.transpose(-1, -2) if transpose_b and b.dim() > 1 else b
+    return torch.matmul(x, y)

@@ -1,0 +1,296 @@
+"""Emit side of the ProgramDesc converters: recorded API calls whose reference op needs attributes
+computed from the call (not a 1:1 renaming, see serialize._REF) — indexing, comparisons, shape
+ops, search ops and the fake-quantization ops. Each emitter returns
+
+    (reference op type, {kwarg: input slot}, output slot(s), {attr: value}, {slot: extra tensor})
+
+or None when the call has no single-op reference form (the op is then written under its own
+qualified type). Output slots: one name, a tuple of names (one output each), or one name for a
+list output. Attribute names and defaults follow paddle/fluid/operators/*_op.cc:
+slice_op.cc / strided_slice_op.cc (axes, starts, ends, strides, decrease_axis, infer_flags),
+compare_op.cc (axis, force_cpu), expand_v2_op.cc (shape), split_op.cc (num, sections, axis),
+stack_op.cc (axis), tile_op.cc (repeat_times), clip_op.cc (min, max), cum_op.cc (axis, flatten,
+exclusive, reverse), arg_min_max_op_base.h (axis, keepdims, flatten, dtype), top_k_v2_op.cc
+(k, axis, largest, sorted), scale_op.cc, fake_quantize_op.cc / fake_dequantize_op.cc /
+quantize_linear_op.cc (bit_length, round_type, quant_axis, moving_rate, is_test, max_range)."""
+from __future__ import annotations
+
+import torch
+
+from ..framework.core import Tensor, _wrap
+from . import proto as pb
+
+_INT_MAX = 2 ** 31 - 1
+
+
+def _is_t(v):
+    return isinstance(v, Tensor)
+
+
+def _const(v, like=None):
+    dt = like._t.dtype if isinstance(like, Tensor) and like._t.is_floating_point() else None
+    return _wrap(torch.tensor(v, dtype=dt if dt is not None and isinstance(v, float) else None))
+
+
+def _ints(v):
+    return isinstance(v, (list, tuple)) and all(isinstance(x, int) and not isinstance(x, bool) for x in v)
+
+
+def _cmp(typ):
+    def emit(kw):
+        x, y = kw.get("x"), kw.get("y")
+        if not _is_t(x):
+            return None
+        extra = {} if _is_t(y) else {"Y": _const(y, x)}
+        return typ, {"x": "X", "y": "Y"}, "Out", {"axis": -1, "force_cpu": False}, extra
+    return emit
+
+
+def _getitem(kw):
+    x, idx = kw.get("x"), kw.get("idx")
+    if not _is_t(x):
+        return None
+    rank = x._t.dim()
+    items = list(idx) if isinstance(idx, tuple) else [idx]
+    if sum(1 for i in items if i is Ellipsis) > 1:
+        return None
+    if any(i is Ellipsis for i in items):
+        k = items.index(Ellipsis)
+        items = items[:k] + [slice(None)] * (rank - len(items) + 1) + items[k + 1:]
+    if len(items) > rank or not all(isinstance(i, (int, slice)) and not isinstance(i, bool) for i in items):
+        return None
+    axes, starts, ends, strides, dec = [], [], [], [], []
+    for ax, it in enumerate(items):
+        if isinstance(it, int):
+            axes.append(ax)
+            starts.append(it)
+            ends.append(it + 1 if it != -1 else _INT_MAX)
+            strides.append(1)
+            dec.append(ax)
+            continue
+        if not all(v is None or (isinstance(v, int) and not isinstance(v, bool)) for v in (it.start, it.stop, it.step)):
+            return None
+        if it.start is None and it.stop is None and it.step in (None, 1):
+            continue
+        step = 1 if it.step is None else it.step
+        axes.append(ax)
+        strides.append(step)
+        if step > 0:
+            starts.append(0 if it.start is None else it.start)
+            ends.append(_INT_MAX if it.stop is None else it.stop)
+        else:
+            starts.append(-1 if it.start is None else it.start)
+            ends.append(-_INT_MAX if it.stop is None else it.stop)
+    if not axes:   # x[:] / x[...]: a copy
+        return "assign", {"x": "X"}, "Out", {}, {}
+    if all(s == 1 for s in strides):
+        return "slice", {"x": "Input"}, "Out", {"axes": axes, "starts": starts, "ends": ends, "decrease_axis": dec,
+                                                "infer_flags": [1] * len(axes)}, {}
+    return "strided_slice", {"x": "Input"}, "Out", {"axes": axes, "starts": starts, "ends": ends, "strides": strides,
+                                                    "decrease_axis": dec, "infer_flags": [1] * len(axes)}, {}
+
+
+def _expand(kw):
+    s = kw.get("shape")
+    if not _ints(s):
+        return None
+    return "expand_v2", {"x": "X"}, "Out", {"shape": list(s)}, {}
+
+
+def _split(kw):
+    n, ax = kw.get("num_or_sections"), kw.get("axis", 0)
+    if not isinstance(ax, int):
+        return None
+    if isinstance(n, int):
+        return "split", {"x": "X"}, "Out", {"num": n, "axis": ax}, {}
+    if _ints(n):
+        return "split", {"x": "X"}, "Out", {"num": 0, "sections": list(n), "axis": ax}, {}
+    return None
+
+
+def _stack(kw):
+    return "stack", {"x": "X"}, "Y", {"axis": int(kw.get("axis", 0))}, {}
+
+
+def _tile(kw):
+    r = kw.get("repeat_times")
+    if not _ints(r):
+        return None
+    return "tile", {"x": "X"}, "Out", {"repeat_times": list(r)}, {}
+
+
+def _where(kw):
+    c, x, y = kw.get("condition"), kw.get("x"), kw.get("y")
+    if x is None and y is None:
+        return "where_index", {"condition": "Condition"}, "Out", {}, {}
+    extra = {}
+    if not _is_t(x):
+        extra["X"] = _const(x, y)
+    if not _is_t(y):
+        extra["Y"] = _const(y, x)
+    return "where", {"condition": "Condition", "x": "X", "y": "Y"}, "Out", {}, extra
+
+
+def _clip(kw):
+    lo, hi = kw.get("min"), kw.get("max")
+    at, extra = {}, {}
+    for name, v, d in (("min", lo, -3.4028234663852886e38), ("max", hi, 3.4028234663852886e38)):
+        if v is None:
+            at[name] = d
+        elif _is_t(v):
+            at[name] = d   # the tensor goes to the Min / Max slot
+        else:
+            at[name] = float(v)
+    return "clip", {"x": "X", "min": "Min", "max": "Max"}, "Out", at, extra
+
+
+def _cumsum(kw):
+    ax = kw.get("axis")
+    return "cumsum", {"x": "X"}, "Out", {"axis": -1 if ax is None else int(ax), "flatten": ax is None,
+                                         "exclusive": False, "reverse": False}, {}
+
+
+def _arg(typ):
+    def emit(kw):
+        ax = kw.get("axis")
+        from ..framework.core import convert_dtype
+        dt = pb.vartype_of(convert_dtype(kw.get("dtype", "int64")))
+        return typ, {"x": "X"}, "Out", {"axis": 0 if ax is None else int(ax), "keepdims": bool(kw.get("keepdim")),
+                                        "flatten": ax is None, "dtype": dt}, {}
+    return emit
+
+
+def _topk(kw):
+    k = kw.get("k")
+    if not isinstance(k, int):
+        return None
+    ax = kw.get("axis")
+    return "top_k_v2", {"x": "X"}, ("Out", "Indices"), {"k": k, "axis": -1 if ax is None else int(ax),
+                                                         "largest": bool(kw.get("largest", True)),
+                                                         "sorted": bool(kw.get("sorted", True))}, {}
+
+
+def _neg(kw):
+    return "scale", {"x": "X"}, "Out", {"scale": -1.0, "bias": 0.0, "bias_after_scale": True}, {}
+
+
+def _cast(kw):
+    x, dt = kw.get("x"), kw.get("dtype")
+    if not _is_t(x):
+        return None
+    from ..framework.core import convert_dtype
+    return "cast", {"x": "X"}, "Out", {"in_dtype": pb.vartype_of(x._t.dtype),
+                                       "out_dtype": pb.vartype_of(convert_dtype(dt))}, {}
+
+
+# ------------------------------------------------------------------------------- quantization
+def _qdq_abs_max(kw):
+    return "fake_quantize_dequantize_abs_max", {"x": "X"}, ("Out", "OutScale"), \
+        {"bit_length": int(kw.get("bit_length", 8)), "round_type": int(kw.get("round_type", 1))}, {}
+
+
+def _q_abs_max(kw):
+    return "fake_quantize_abs_max", {"x": "X"}, ("Out", "OutScale"), \
+        {"bit_length": int(kw.get("bit_length", 8)), "round_type": int(kw.get("round_type", 1))}, {}
+
+
+def _qdq_channel(typ):
+    def emit(kw):
+        return typ, {"x": "X"}, ("Out", "OutScale"), {"bit_length": int(kw.get("bit_length", 8)),
+                                                       "quant_axis": int(kw.get("quant_axis", 0)),
+                                                       "round_type": int(kw.get("round_type", 1))}, {}
+    return emit
+
+
+def _qdq_moving(typ):
+    def emit(kw):
+        return typ, {"x": "X", "in_scale": "InScale", "in_state": "InState", "in_accum": "InAccum"}, "Out", \
+            {"bit_length": int(kw.get("bit_length", 8)), "moving_rate": float(kw.get("moving_rate", 0.9)),
+             "is_test": bool(kw.get("is_test", False)), "round_type": int(kw.get("round_type", 1))}, \
+            {"@out:OutScale": kw.get("in_scale"), "@out:OutState": kw.get("in_state"),
+             "@out:OutAccum": kw.get("in_accum")}
+    return emit
+
+
+def _ma_scale(kw):
+    return "moving_average_abs_max_scale", {"x": "X", "in_scale": "InScale", "in_state": "InState",
+                                            "in_accum": "InAccum"}, "Out", \
+        {"moving_rate": float(kw.get("moving_rate", 0.9)), "is_test": bool(kw.get("is_test", False))}, \
+        {"@out:OutScale": kw.get("in_scale"), "@out:OutState": kw.get("in_state"),
+         "@out:OutAccum": kw.get("in_accum")}
+
+
+def _qdq_fixed(kw):
+    """a frozen (calibrated) quant-dequant: the reference writes it as the moving-average op with
+    is_test = True reading the stored scale (per tensor), or the channel-wise op (per channel)"""
+    s = kw.get("scale")
+    if _is_t(s) and s._t.numel() > 1:
+        return "fake_channel_wise_quantize_dequantize_abs_max", {"x": "X", "scale": "InScale"}, "Out", \
+            {"bit_length": int(kw.get("bit_length", 8)), "quant_axis": int(kw.get("quant_axis") or 0),
+             "round_type": int(kw.get("round_type", 1))}, {}
+    return "fake_quantize_dequantize_moving_average_abs_max", {"x": "X", "scale": "InScale"}, "Out", \
+        {"bit_length": int(kw.get("bit_length", 8)), "moving_rate": 0.9, "is_test": True,
+         "round_type": int(kw.get("round_type", 1))}, {}
+
+
+def _q_linear(typ):
+    def emit(kw):
+        at = {"bit_length": int(kw.get("bit_length", 8)), "quant_axis": int(kw.get("quant_axis", -1))}
+        if typ == "quantize_linear":
+            at["round_type"] = int(kw.get("round_type", 0))
+        return typ, {"x": "X", "scale": "Scale", "zero_point": "ZeroPoint"}, "Y", at, {}
+    return emit
+
+
+def _deq_max_abs(kw):
+    return "fake_dequantize_max_abs", {"x": "X", "scale": "Scale"}, "Out", \
+        {"max_range": float(kw.get("max_range", 127.0))}, {}
+
+
+def _ch_deq(kw):
+    return "fake_channel_wise_dequantize_max_abs", {"x": "X", "scales": "Scales"}, "Out", \
+        {"quant_bits": [int(b) for b in kw.get("quant_bits", (8,))], "quant_axis": int(kw.get("quant_axis", 0))}, {}
+
+
+_Q = "nn.quant.ops."
+EMIT = {
+    **{f"tensor.logic.{n}": _cmp(n) for n in ("greater_than", "greater_equal", "less_than", "less_equal", "equal",
+                                               "not_equal")},
+    "tensor.getitem": _getitem,
+    "tensor.manipulation.expand": _expand,
+    "tensor.manipulation.broadcast_to": _expand,
+    "tensor.manipulation.split": _split,
+    "tensor.manipulation.stack": _stack,
+    "tensor.manipulation.tile": _tile,
+    "tensor.manipulation.where": _where,
+    "tensor.math.clip": _clip,
+    "tensor.math.cumsum": _cumsum,
+    "tensor.search.argmax": _arg("arg_max"),
+    "tensor.search.argmin": _arg("arg_min"),
+    "tensor.search.topk": _topk,
+    "tensor.math.neg": _neg,
+    "tensor.manipulation.cast": _cast,
+    _Q + "fake_quantize_dequantize_abs_max": _qdq_abs_max,
+    _Q + "fake_quantize_abs_max": _q_abs_max,
+    _Q + "fake_channel_wise_quantize_dequantize_abs_max": _qdq_channel("fake_channel_wise_quantize_dequantize_abs_max"),
+    _Q + "fake_channel_wise_quantize_abs_max": _qdq_channel("fake_channel_wise_quantize_abs_max"),
+    _Q + "fake_quantize_dequantize_moving_average_abs_max":
+        _qdq_moving("fake_quantize_dequantize_moving_average_abs_max"),
+    _Q + "fake_quantize_moving_average_abs_max": _qdq_moving("fake_quantize_moving_average_abs_max"),
+    _Q + "moving_average_abs_max_scale": _ma_scale,
+    _Q + "fake_quantize_dequantize_fixed_scale": _qdq_fixed,
+    _Q + "quantize_linear": _q_linear("quantize_linear"),
+    _Q + "dequantize_linear": _q_linear("dequantize_linear"),
+    _Q + "fake_dequantize_max_abs": _deq_max_abs,
+    _Q + "fake_channel_wise_dequantize_max_abs": _ch_deq,
+}
+
+
+def spec(short, op):
+    f = EMIT.get(short)
+    if f is None or op.args:
+        return None
+    try:
+        return f(op.kwargs)
+    except (TypeError, ValueError):
+        return None

@@ -297,14 +297,10 @@ def pad_nd_op(x, paddings, mode="constant", value=0.0, data_format="NCHW"):
 def strided_slice_op(x, axes, starts, ends, strides, decrease_axis=()):
     t = _t(x)
     for a, s, e, st in zip(axes, starts, ends, strides):
-        n = t.shape[a]
-        if st > 0:
-            s = max(s + n, 0) if s < 0 else min(s, n)
-            e = max(e + n, 0) if e < 0 else min(e, n)
-        else:
-            s = s + n if s < 0 else min(s, n - 1)
-            e = e + n if e < -1 else e
-        t = t.index_select(a, torch.arange(s, e, st, device=t.device))
+        # the reference clamps start / end into the dim like Python slicing (negative values count
+        # from the end; an end past the front with a negative stride runs through index 0)
+        idx = list(range(*slice(s, e, st).indices(t.shape[a])))
+        t = t.index_select(a, torch.tensor(idx, dtype=torch.long, device=t.device))
     if decrease_axis:
         t = t.squeeze(tuple(decrease_axis))
     return _wrap(t)
@@ -624,7 +620,77 @@ def _conv_fluid(name, slots, attrs, out):
     return conv
 
 
+def _quant(name):
+    from ..nn.quant import ops as QO
+    return getattr(QO, name)
+
+
+def _conv_q_absmax(typ):
+    def conv(r, ins, at):
+        return _quant(typ), {"x": _one(r, ins, "X"), "bit_length": at.get("bit_length", 8),
+                             "round_type": at.get("round_type", 1)}, ("Out", "OutScale")
+    return conv
+
+
+def _conv_q_channel(typ):
+    def conv(r, ins, at):
+        return _quant(typ), {"x": _one(r, ins, "X"), "bit_length": at.get("bit_length", 8),
+                             "quant_axis": at.get("quant_axis", 0), "round_type": at.get("round_type", 1)}, \
+            ("Out", "OutScale")
+    return conv
+
+
+def _conv_q_channel_frozen(r, ins, at):
+    """the channel-wise quant-dequant with a stored per-channel scale (our frozen weight form)"""
+    if not ins.get("InScale"):
+        return _conv_q_channel("fake_channel_wise_quantize_dequantize_abs_max")(r, ins, at)
+    return _quant("fake_quantize_dequantize_fixed_scale"), {
+        "x": _one(r, ins, "X"), "scale": _one(r, ins, "InScale"), "bit_length": at.get("bit_length", 8),
+        "round_type": at.get("round_type", 1), "quant_axis": at.get("quant_axis", 0)}, "Out"
+
+
+def _conv_q_moving(typ):
+    def conv(r, ins, at):
+        return _quant(typ), {"x": _one(r, ins, "X"), "in_scale": _one(r, ins, "InScale"),
+                             "in_state": _one(r, ins, "InState"), "in_accum": _one(r, ins, "InAccum"),
+                             "bit_length": at.get("bit_length", 8), "moving_rate": at.get("moving_rate", 0.9),
+                             "is_test": at.get("is_test", True), "round_type": at.get("round_type", 1)}, "Out"
+    return conv
+
+
+def _conv_ma_scale(r, ins, at):
+    return _quant("moving_average_abs_max_scale"), {
+        "x": _one(r, ins, "X"), "in_scale": _one(r, ins, "InScale") or r.var(ins.get("OutScale", ["_"])[0]),
+        "in_state": _one(r, ins, "InState"), "in_accum": _one(r, ins, "InAccum"),
+        "moving_rate": at.get("moving_rate", 0.9), "is_test": at.get("is_test", True)}, "Out"
+
+
+def _conv_q_linear(typ):
+    def conv(r, ins, at):
+        kw = {"x": _one(r, ins, "X"), "scale": _one(r, ins, "Scale"), "zero_point": _one(r, ins, "ZeroPoint"),
+              "bit_length": at.get("bit_length", 8), "quant_axis": at.get("quant_axis", -1)}
+        if typ == "quantize_linear":
+            kw["round_type"] = at.get("round_type", 0)
+        return _quant(typ), kw, "Y"
+    return conv
+
+
 CONVERT = {
+    # fake quantization (fake_quantize_op.cc, fake_dequantize_op.cc, quantize_linear_op.cc)
+    "fake_quantize_dequantize_abs_max": _conv_q_absmax("fake_quantize_dequantize_abs_max"),
+    "fake_quantize_abs_max": _conv_q_absmax("fake_quantize_abs_max"),
+    "fake_channel_wise_quantize_dequantize_abs_max": _conv_q_channel_frozen,
+    "fake_channel_wise_quantize_abs_max": _conv_q_channel("fake_channel_wise_quantize_abs_max"),
+    "fake_quantize_dequantize_moving_average_abs_max": _conv_q_moving("fake_quantize_dequantize_moving_average_abs_max"),
+    "fake_quantize_moving_average_abs_max": _conv_q_moving("fake_quantize_moving_average_abs_max"),
+    "moving_average_abs_max_scale": _conv_ma_scale,
+    "quantize_linear": _conv_q_linear("quantize_linear"),
+    "dequantize_linear": _conv_q_linear("dequantize_linear"),
+    "fake_dequantize_max_abs": lambda r, ins, at: (_quant("fake_dequantize_max_abs"), {
+        "x": _one(r, ins, "X"), "scale": _one(r, ins, "Scale"), "max_range": at.get("max_range", 127.0)}, "Out"),
+    "fake_channel_wise_dequantize_max_abs": lambda r, ins, at: (_quant("fake_channel_wise_dequantize_max_abs"), {
+        "x": _one(r, ins, "X"), "scales": _one(r, ins, "Scales"), "quant_bits": at.get("quant_bits", [8]),
+        "quant_axis": at.get("quant_axis", 0)}, "Out"),
     # activations / unary
     **{op: _unary(op) for op in ("abs", "acos", "asin", "atan", "ceil", "cos", "cosh", "floor", "log", "log1p", "log2",
                                  "log10", "reciprocal", "round", "rsqrt", "sin", "sinh", "square", "tan", "softsign",

@@ -260,6 +260,17 @@ class _Writer:
         short = _qual_short(op.type)
         if op.exec is not None:
             self._cf_op(op, msg, ins, outs)
+        elif op.attrs.get("ref_op") is not None:
+            typ, r_ins, r_outs, r_attrs = op.attrs["ref_op"]
+            msg.type = typ
+            for slot, ts in r_ins.items():
+                ins[slot] = [self.tensor_name(t) for t in ts]
+            for slot, ts in r_outs.items():
+                outs[slot] = [self.tensor_name(t) for t in ts]
+            for k, v in r_attrs.items():
+                _set_attr(msg, k, v)
+        elif self._emit_ref(op, msg, short, ins, outs):
+            pass
         else:
             ref = _REF.get(short) or _fluid_ref(short)
             slot_of = ref[1] if ref else {}
@@ -285,6 +296,35 @@ class _Writer:
             v = msg.outputs.add()
             v.parameter = slot
             v.arguments.extend(names)
+
+    def _emit_ref(self, op, msg, short, ins, outs):
+        """calls whose reference op needs computed attributes (static/ref_emit.py); False when the
+        call has no single-op reference form"""
+        from . import ref_emit
+        spec = ref_emit.spec(short, op)
+        if spec is None:
+            return False
+        typ, slot_of, out_slots, attrs, extra = spec
+        msg.type = typ
+        args_j = self.enc(list(op.args), "args", ins) if op.args else []
+        kw_j = {k: self.enc(v, slot_of.get(k, k), ins) for k, v in op.kwargs.items()}
+        for name, val in attrs.items():
+            _set_attr(msg, name, val)
+        if isinstance(out_slots, tuple) and isinstance(op.outputs, (tuple, list)) and len(op.outputs) == len(out_slots):
+            parts = [self.enc(o, s, outs) for o, s in zip(op.outputs, out_slots)]
+            out_j = {"@tuple": parts} if isinstance(op.outputs, tuple) else parts
+        else:
+            out_j = self.enc(op.outputs, out_slots if isinstance(out_slots, str) else out_slots[0], outs)
+        for slot, t in extra.items():   # constant operands of scalar arguments, in-place state outputs
+            if t is None:
+                continue
+            if slot.startswith("@out:"):
+                outs.setdefault(slot[5:], []).append(self.tensor_name(t))
+            else:
+                ins.setdefault(slot, []).append(self.tensor_name(t))
+        _set_attr(msg, "__pha_fn__", op.type)
+        _set_attr(msg, "__pha_args__", json.dumps({"args": args_j, "kwargs": kw_j, "outs": out_j}))
+        return True
 
     def _cf_op(self, op, msg, ins, outs):
         a = op.attrs
@@ -502,6 +542,11 @@ class _Reader:
                     fn = getattr(fn, "__wrapped_op__", fn)
                     qual = f"{fn.__module__}.{fn.__name__}"
                     op = OpDesc(qual, fn, (), kwargs, o)
+                    # the reference op as read: written back under the same type, slots and
+                    # attributes (a loaded reference model saves as a reference model)
+                    op.attrs["ref_op"] = (om.type, {sl: [self.var(n, blk) for n in ns] for sl, ns in ins.items()},
+                                          {sl: [self.var(n, blk) for n in ns] for sl, ns in outs.items()},
+                                          {k: v for k, v in attrs.items() if k not in _PRIVATE})
                 for v in _iter_vars(op.outputs):
                     v.op = op
                 blk.append_op(op)

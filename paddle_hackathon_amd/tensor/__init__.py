@@ -47,7 +47,46 @@ def getitem(x, idx):
         i = idx._t.reshape(1).to(torch.int64)
         i = torch.where(i < 0, i + t.shape[0], i)
         return _wrap(torch.index_select(t, 0, i.to(t.device)).squeeze(0))
+    items = idx if isinstance(idx, tuple) else (idx,)
+    import builtins
+    if builtins.any(isinstance(i, builtins.slice) and isinstance(i.step, int) and i.step < 0 for i in items):
+        return _wrap(_neg_step_getitem(t, items))
     return _wrap(t[_index(idx)])
+
+
+def _neg_step_getitem(t, items):
+    """basic indexing with negative slice steps (x[::-1], x[5:1:-2]; torch has no negative
+    strides): the negative-step slices are taken as full dims, then gathered by index_select
+    (differentiable) with Python's slice arithmetic"""
+    import builtins
+    if builtins.any(i is Ellipsis for i in items):
+        k = list(items).index(Ellipsis)
+        n_real = builtins.sum(1 for i in items if i is not None and i is not Ellipsis)
+        items = items[:k] + (builtins.slice(None),) * (t.dim() - n_real) + items[k + 1:]
+    first, picks, out_dim, in_dim = [], [], 0, 0
+    for it in items:
+        if it is None:
+            first.append(None)
+            out_dim += 1
+        elif isinstance(it, builtins.slice) and it.step is not None and it.step < 0:
+            first.append(builtins.slice(None))
+            idx = builtins.range(*it.indices(t.shape[in_dim]))
+            picks.append((out_dim, torch.tensor(list(idx), dtype=torch.long, device=t.device)))
+            out_dim += 1
+            in_dim += 1
+        elif isinstance(it, builtins.slice):
+            first.append(it)
+            out_dim += 1
+            in_dim += 1
+        else:
+            first.append(_index(it))
+            in_dim += 1
+            if not isinstance(it, int):
+                out_dim += 1
+    out = t[tuple(first)]
+    for d, ix in picks:
+        out = torch.index_select(out, d, ix)
+    return out
 
 
 def setitem(x, idx, value):

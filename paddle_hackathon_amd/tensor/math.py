@@ -664,6 +664,9 @@ def numel(x, name=None):
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
     a = x._t if isinstance(x, Tensor) else torch.as_tensor(x)
     b = y._t if isinstance(y, Tensor) else torch.as_tensor(y)
+    if a.is_cuda or b.is_cuda:   # GPU products: the own GEMM layouts (ops/gemm.py matmul)
+        from ..ops import gemm as _gemm
+        return _w(_gemm.matmul(a, b, transpose_x and a.dim() > 1, transpose_y and b.dim() > 1))
     if transpose_x:
         a = a.transpose(-1, -2) if a.dim() > 1 else a
     if transpose_y:
@@ -673,12 +676,20 @@ def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
 
 @_export
 def mm(input, mat2, name=None):
-    return _w(torch.matmul(_u(input), _u(mat2)))
+    a, b = _u(input), _u(mat2)
+    if a.is_cuda:
+        from ..ops import gemm as _gemm
+        return _w(_gemm.matmul(a, b))
+    return _w(torch.matmul(a, b))
 
 
 @_export
 def bmm(x, y, name=None):
-    return _w(torch.bmm(_u(x), _u(y)))
+    a, b = _u(x), _u(y)
+    if a.is_cuda:
+        from ..ops import gemm as _gemm
+        return _w(_gemm.matmul(a, b))
+    return _w(torch.bmm(a, b))
 
 
 @_export

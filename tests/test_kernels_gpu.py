@@ -1208,7 +1208,9 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     """GPT (fleet bench model), BERT (vocab 30522, not a multiple of 8) and ResNet-50 (NHWC)
     training steps record no hot-path fallback (ops/fallback.py): every matmul / conv /
     attention / embedding ran on the own kernels or — under the "auto" GEMM policy — on the
-    library kernels chosen for the NT layout by measurement, never as an unsupported-shape escape."""
+    library kernels chosen for the NT layout by measurement, never as an unsupported-shape escape.
+    Library products are counted apart (fallback.library_counts): none under PHA_GEMM_IMPL=own, and
+    under auto only the planned NT matmuls."""
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.ops import fallback
     from paddle_hackathon_amd.models import gpt_config, GPTForPretraining, bert_config, BertForPretraining, \
@@ -1218,7 +1220,7 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     monkeypatch.setenv("PHA_FALLBACK_LOG", "1")
     paddle.set_device("gpu")
     paddle.seed(0)
-    results = {}
+    results, libs = {}, {}
 
     fallback.reset()
     cfg = gpt_config("gpt-tiny", hidden_size=256, num_heads=4, ffn_hidden_size=1024, vocab_size=1024,
@@ -1228,6 +1230,7 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     ids = paddle.to_tensor(torch.randint(0, 1024, (2, 256), device="cuda"))
     _train_steps(gpt, lambda m: m(ids, ids), opt)
     results["gpt"] = fallback.counts()
+    libs["gpt"] = fallback.library_counts()
 
     fallback.reset()
     bcfg = bert_config("bert-tiny", vocab_size=30522, hidden_size=128, num_heads=2, intermediate_size=512,
@@ -1246,6 +1249,7 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
         return crit(mlm, nsp, mlab, nlab)
     _train_steps(bert, bert_loss, bopt)
     results["bert"] = fallback.counts()
+    libs["bert"] = fallback.library_counts()
 
     fallback.reset()
     rn = paddle.amp.decorate(resnet50(data_format="NHWC"), level="O2", dtype="bfloat16")
@@ -1255,7 +1259,13 @@ def test_headline_paths_have_no_fallbacks(impl, monkeypatch):
     y = paddle.to_tensor(torch.randint(0, 1000, (8,), device="cuda"))
     _train_steps(rn, lambda m: paddle.nn.functional.cross_entropy(m(x), y), ropt)
     results["resnet50"] = fallback.counts()
+    libs["resnet50"] = fallback.library_counts()
     assert all(not v for v in results.values()), results
+    if impl == "own":
+        assert all(not v for v in libs.values()), libs
+    else:
+        assert all(set(v) <= {"matmul"} for v in libs.values()), libs
+        assert not libs["resnet50"], libs
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (264, 520, 128), (4096, 8192, 2048)])

@@ -1,0 +1,8 @@
+set -e
+cd /tmp && export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/g8w_pmc
+mkdir -p $O
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d $O/p1 -o run --output-format csv -- python3 tools/g8w_pmc.py > $O/p1.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE -d $O/p2 -o run --output-format csv -- python3 tools/g8w_pmc.py > $O/p2.log 2>&1
+find $O -name "*counter_collection.csv" | head
