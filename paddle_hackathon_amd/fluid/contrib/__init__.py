@@ -3,5 +3,6 @@
 slim quantization passes (``contrib.slim``)."""
 from . import mixed_precision  # noqa: F401
 from .rnn_impl import BasicGRUUnit, BasicLSTMUnit  # noqa: F401
+from . import slim  # noqa: F401
 
 __all__ = ["mixed_precision", "BasicGRUUnit", "BasicLSTMUnit"]

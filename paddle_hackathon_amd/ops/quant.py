@@ -229,10 +229,30 @@ def fake_channel_wise_dequantize_max_abs(x, scales, quant_bits=(8,), quant_axis=
     return (x.float().reshape(-1, C, inner) * s).reshape(x.shape).to(x.dtype)
 
 
+class _ScaledSTE(torch.autograd.Function):
+    """forward: y (computed without autograd); backward: dX = dY * factor (the quantize step's
+    straight-through derivative bin / s)"""
+
+    @staticmethod
+    def forward(ctx, x, y, factor):
+        ctx.save_for_backward(factor)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        f, = ctx.saved_tensors
+        return g * f.to(g.dtype), None, None
+
+
 def quantize_linear(x, scale, zero_point=None, bit_length=8, quant_axis=-1, round_type=0):
     """the 2.4 export op: q = clip(round(x / s * bin) + zp) (integer levels, x's float dtype)"""
     per_ch = scale.numel() > 1
     q = quant_dequant(x, scale, bit_length, round_type, dequant=False, quant_axis=quant_axis if per_ch else None)
+    if torch.is_grad_enabled() and x.requires_grad and x.is_floating_point():
+        s = scale.detach().float()
+        if per_ch:
+            s = s.reshape([-1 if i == quant_axis % x.dim() else 1 for i in range(x.dim())])
+        q = _ScaledSTE.apply(x, q.to(x.dtype), bin_cnt(bit_length) / torch.where(s <= 1e-30, s + 1e-6, s))
     if zero_point is not None and bool((zero_point != 0).any()):
         q = q + zero_point.to(q.dtype).reshape([-1 if i == quant_axis % x.dim() else 1 for i in range(x.dim())]
                                                 if per_ch else [])

@@ -111,6 +111,8 @@ _EXTRA_ATTRS = {
     "nn.functional.pooling.avg_pool2d": {"pooling_type": "avg"},
 }
 _PRIVATE = ("__pha_fn__", "__pha_args__", "__pha_cf__")
+# op annotations carried through save / load (the quantization tools' output thresholds)
+_ANNOTATIONS = ("out_threshold", "with_quant_attr", "Input_scale", "skip_quant")
 
 
 # ------------------------------------------------------------------------------------- helpers
@@ -268,7 +270,8 @@ class _Writer:
             for slot, ts in r_outs.items():
                 outs[slot] = [self.tensor_name(t) for t in ts]
             for k, v in r_attrs.items():
-                _set_attr(msg, k, v)
+                if k not in (op.attrs.get("extra_attrs") or {}):
+                    _set_attr(msg, k, v)
         elif self._emit_ref(op, msg, short, ins, outs):
             pass
         else:
@@ -288,6 +291,8 @@ class _Writer:
             out_j = self.enc(op.outputs, out_slot, outs)
             _set_attr(msg, "__pha_fn__", op.type)
             _set_attr(msg, "__pha_args__", json.dumps({"args": args_j, "kwargs": kw_j, "outs": out_j}))
+        for k, v in (op.attrs.get("extra_attrs") or {}).items():   # annotations (out_threshold ...)
+            _set_attr(msg, k, v)
         for slot, names in ins.items():
             v = msg.inputs.add()
             v.parameter = slot
@@ -547,6 +552,9 @@ class _Reader:
                     op.attrs["ref_op"] = (om.type, {sl: [self.var(n, blk) for n in ns] for sl, ns in ins.items()},
                                           {sl: [self.var(n, blk) for n in ns] for sl, ns in outs.items()},
                                           {k: v for k, v in attrs.items() if k not in _PRIVATE})
+                ann = {k: attrs[k] for k in _ANNOTATIONS if k in attrs}
+                if ann:
+                    op.attrs["extra_attrs"] = ann
                 for v in _iter_vars(op.outputs):
                     v.op = op
                 blk.append_op(op)
@@ -878,3 +886,28 @@ def load_persistables(desc, data):
     if off != len(data):
         raise ValueError("persistables stream has trailing bytes (program / params mismatch)")
     return out
+
+
+def op_reference(op):
+    """(reference op type, {input slot: kwarg name}) of a recorded or loaded op, the way the
+    writer would emit it — None for ops written under their own qualified type (the static
+    quantization passes find quantizable ops and their activation / weight operands with this)"""
+    if op.exec is not None:
+        return None
+    r = op.attrs.get("ref_op")
+    if r is not None:
+        slots = {}
+        for slot, ts in r[1].items():
+            for k, v in op.kwargs.items():
+                if ts and v is ts[0]:
+                    slots[slot] = k
+        return r[0], slots
+    short = _qual_short(op.type)
+    from . import ref_emit
+    sp = ref_emit.spec(short, op)
+    if sp is not None:
+        return sp[0], {s: k for k, s in sp[1].items()}
+    ref = _REF.get(short) or _fluid_ref(short)
+    if ref is None:
+        return None
+    return ref[0], {s: k for k, s in ref[1].items()}
