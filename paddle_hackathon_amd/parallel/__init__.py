@@ -12,6 +12,7 @@ try:  # optional subsystems (filled in progressively)
     from .sharding import group_sharded_parallel, save_group_sharded_model  # noqa: F401
     from . import ps  # noqa: F401
     from . import auto_parallel  # noqa: F401
+    from . import passes  # noqa: F401
     from .auto_parallel import shard_tensor, shard_op, ProcessMesh  # noqa: F401
 except ImportError:  # pragma: no cover
     pass

@@ -1,5 +1,6 @@
 """fleet.utils (reference: python/paddle/distributed/fleet/utils/__init__.py)."""
-from ..recompute import recompute, recompute_sequential  # noqa: F401
+from ...recompute import recompute, recompute_sequential  # noqa: F401
+from . import hybrid_parallel_util  # noqa: F401
 
 
 class LocalFS:
