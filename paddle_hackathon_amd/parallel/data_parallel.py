@@ -102,16 +102,34 @@ class _Reducer:
                 self._launch(b)
         return hook
 
+    @staticmethod
+    def _grads_in_buf(b):
+        """every gradient of the bucket is already its slice of the flat buffer (the steady state:
+        after the first step the parameters' .grad ARE views of the bucket, so backward accumulates
+        straight into the buffer RCCL reduces — no concatenation, no copy back)"""
+        if b.buf is None or b.buf.dtype != b.dtype:
+            return False
+        base, es, off = b.buf.data_ptr(), b.buf.element_size(), 0
+        for p in b.params:
+            g = p._t.grad
+            if g is None or g.data_ptr() != base + off * es or not g.is_contiguous():
+                return False
+            off += g.numel()
+        return off == b.buf.numel()
+
     def _launch(self, b):
         grads = [p._t.grad for p in b.params]
         n = sum(g.numel() for g in grads)
         cdt = self.comm_dtype if self.comm_dtype is not None and b.dtype == torch.float32 else b.dtype
-        if b.buf is None or b.buf.numel() != n or b.buf.device != grads[0].device or b.buf.dtype != cdt:
-            b.buf = torch.empty(n, dtype=cdt, device=grads[0].device)
-        if cdt == b.dtype:
-            torch.cat([g.reshape(-1) for g in grads], out=b.buf)
+        if cdt == b.dtype and self._grads_in_buf(b):
+            pass
         else:
-            b.buf.copy_(torch.cat([g.reshape(-1) for g in grads]))
+            if b.buf is None or b.buf.numel() != n or b.buf.device != grads[0].device or b.buf.dtype != cdt:
+                b.buf = torch.empty(n, dtype=cdt, device=grads[0].device)
+            if cdt == b.dtype:
+                torch.cat([g.reshape(-1) for g in grads], out=b.buf)
+            else:
+                b.buf.copy_(torch.cat([g.reshape(-1) for g in grads]))
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         b.work = dist.all_reduce(b.buf, op=op, group=self.pg, async_op=True)
 
@@ -136,13 +154,22 @@ class _Reducer:
             if not self.avg_native:
                 b.buf.div_(self.nranks)
             off = 0
+            if b.buf.dtype == b.dtype:
+                # the parameters adopt their bucket slices as .grad (first step, or after a
+                # clear_grad that dropped the gradients): later steps accumulate into the bucket
+                base, es = b.buf.data_ptr(), b.buf.element_size()
+                for p in b.params:
+                    n = p._t.numel()
+                    if p._t.grad.data_ptr() != base + off * es:
+                        p._t.grad = b.buf[off:off + n].view_as(p._t)
+                    off += n
+                continue
             grads = [p._t.grad for p in b.params]
             views = []
             for g in grads:
                 views.append(b.buf[off:off + g.numel()].view_as(g))
                 off += g.numel()
-            if views and views[0].dtype != grads[0].dtype:
-                views = [v.to(grads[0].dtype) for v in views]
+            views = [v.to(grads[0].dtype) for v in views]   # comm dtype (fp16_allreduce) back to fp32
             torch._foreach_copy_(grads, views)
 
     def remove(self):

