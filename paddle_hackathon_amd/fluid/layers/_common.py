@@ -135,6 +135,8 @@ def to_padded(x, length=None, pad_value=0.0):
 
 def from_padded(p, lens, like_lod=None):
     """flat LoD tensor [sum(len), ...] from padded rows"""
+    if lens.device.type == "meta" or p.device.type == "meta":   # static build: shapes only
+        return _wrap(p.reshape(-1, *p.shape[2:]))
     ls = [int(n) for n in lens.tolist()]
     parts = [p[i, :n] for i, n in enumerate(ls)]
     flat = torch.cat(parts, 0) if parts else p.new_zeros([0] + list(p.shape[2:]))

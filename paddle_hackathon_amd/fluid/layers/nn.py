@@ -1520,4 +1520,5 @@ def gather_tree(ids, parents):
 
 
 register(globals(), __all__, skip=_BUILDERS)
+register(globals(), ["_lookup_v1"])   # embedding's recorded op (lookup_table in a saved ProgramDesc)
 _ = (dt, Tensor)

@@ -1,13 +1,21 @@
 """``fluid.layers`` sequence (LoD) ops (reference: python/paddle/fluid/layers/sequence_lod.py;
 kernels paddle/fluid/operators/sequence_ops/*). Inputs are LoD tensors (flat [sum(len), ...]
 rows with a ``_lod`` offset table, see fluid/core.py); each op pads to [B, Tmax, ...], computes
-with length masks, and returns LoD rows again. Padded tensors plus explicit lengths work too."""
+with length masks, and returns LoD rows again. Padded tensors plus explicit lengths work too.
+
+Static Programs. Every op records ONE op (``sequence_pool`` ... typed by the reference op name in a
+saved ProgramDesc, static/ref_emit.py) whose LoD is resolved when the Executor runs it: fed LoD
+tensors keep their offsets, ops that keep the row count share their input's LoD (the reference's
+ShareLoD, static/program.py run_block), and the sequence ops read / write the offsets at run
+time. At build time (meta tensors, no LoD yet) a LoD input is taken as one sequence, which gives
+the outputs their static shapes (batch dim 1 = the -1 of the declared shape).
+``sequence_conv`` creates its filter at build time and records the pure ``sequence_conv_op``."""
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as TF
 
-from ._common import T, W, dev, to_padded, from_padded, mask_of
+from ._common import T, W, dev, to_padded, from_padded, mask_of, register
 from .. import core as fcore
 
 __all__ = ["sequence_conv", "sequence_softmax", "sequence_pool", "sequence_concat", "sequence_first_step",
@@ -20,11 +28,25 @@ def _lod(x):
     return fcore.lod_of(x)
 
 
+def _meta(x):
+    return T(x).device.type == "meta"
+
+
 def _seq_offsets(x):
     lod = _lod(x)
     if not lod:
+        if _meta(x):                       # build time: one sequence of all rows
+            return [0, T(x).shape[0]]
         raise ValueError("sequence op: input has no LoD (build it with fluid.create_lod_tensor or set _lod)")
     return lod[-1]
+
+
+def _padded(x):
+    """(padded [B, Tmax, ...], lengths, had_lod); a build-time (meta) LoD input is one sequence"""
+    if not _lod(x) and _meta(x):
+        t = T(x)
+        return t[None], torch.full((1,), t.shape[0], dtype=torch.long, device=t.device), True
+    return to_padded(x)
 
 
 def _out(t, lens, like):
@@ -40,36 +62,45 @@ def sequence_conv(input, num_filters, filter_size=3, filter_stride=1, padding=Tr
     filter (sequence_conv_op.h)"""
     from ._common import fparam as _create_parameter
     from ._common import act as _act
-    x = T(input)
-    D = x.shape[1]
-    w = _create_parameter([filter_size * D, num_filters], x.dtype, param_attr)
+    D = T(input).shape[1]
+    w = _create_parameter([filter_size * D, num_filters], T(input).dtype, param_attr)
+    b = _create_parameter([num_filters], T(input).dtype, bias_attr, is_bias=True) if bias_attr is not False else None
     start = -(filter_size // 2) if padding_start is None else padding_start
-    off = _seq_offsets(input)
-    p, lens, _ = to_padded(input)
-    B, Tm = p.shape[:2]
+    conv = sequence_conv_op(input, w, None, filter_size, start, filter_stride)
+    out = conv
+    if b is not None:   # the bias is its own elementwise_add op, as in the reference builder
+        from ...tensor import math as _m
+        out = _m.add(out, b)
+    out = _act(out, act)
+    if out is not conv and _lod(conv):   # dygraph: the elementwise ops keep the rows (ShareLoD)
+        out._lod = _lod(conv)
+    return out
+
+
+def sequence_conv_op(input, filter, bias=None, context_length=3, context_start=-1, context_stride=1):
+    """the recorded sequence_conv op (Input, Filter [, Bias]; contextLength / contextStart /
+    contextStride)"""
+    p, lens, _ = _padded(input)
+    Tm = p.shape[1]
     m = mask_of(lens, Tm, p.device)
     p = p * m[..., None]
     cols = []
-    for k in range(filter_size):
-        s = start + k
+    for k in range(context_length):
+        s = context_start + k
         sh = torch.zeros_like(p)
         if s >= 0:
             sh[:, :Tm - s] = p[:, s:] if s < Tm else sh[:, :0]
         else:
             sh[:, -s:] = p[:, :Tm + s] if -s < Tm else sh[:, :0]
         cols.append(sh)
-    ctx = torch.cat(cols, -1)
-    y = ctx @ T(w)
-    if bias_attr is not False:
-        b = _create_parameter([num_filters], x.dtype, bias_attr, is_bias=True)
-        y = y + T(b)
-    out = from_padded(y, lens, _lod(input))
-    _ = off
-    return _act(out, act)
+    y = torch.cat(cols, -1) @ T(filter)
+    if bias is not None:
+        y = y + T(bias)
+    return from_padded(y, lens, _lod(input))
 
 
 def sequence_softmax(input, use_cudnn=False, name=None):
-    p, lens, _ = to_padded(input)
+    p, lens, _ = _padded(input)
     v = p.reshape(p.shape[0], p.shape[1])
     m = mask_of(lens, v.shape[1], v.device)
     s = torch.softmax(v.masked_fill(~m, float("-inf")), 1).nan_to_num(0.0)
@@ -79,7 +110,7 @@ def sequence_softmax(input, use_cudnn=False, name=None):
 def sequence_pool(input, pool_type, is_test=False, pad_value=0.0):
     """sum / average / sqrt / max / last / first per sequence -> [B, D]; empty sequences give
     ``pad_value``"""
-    p, lens, _ = to_padded(input)
+    p, lens, _ = _padded(input)
     B, Tm = p.shape[:2]
     m = mask_of(lens, Tm, p.device)
     mf = m.reshape(B, Tm, *([1] * (p.dim() - 2))).to(p.dtype)
@@ -100,7 +131,10 @@ def sequence_pool(input, pool_type, is_test=False, pad_value=0.0):
     else:
         raise ValueError(f"sequence_pool: pool_type {pool_type!r}")
     empty = (lens == 0).reshape(B, *([1] * (r.dim() - 1)))
-    return W(torch.where(empty, torch.full_like(r, pad_value), r))
+    out = W(torch.where(empty, torch.full_like(r, pad_value), r))
+    if len(_lod(input)) > 1:              # a 2-level input keeps its outer level
+        out._lod = _lod(input)[:-1]
+    return out
 
 
 def sequence_first_step(input):
@@ -113,6 +147,8 @@ def sequence_last_step(input):
 
 def sequence_concat(input, name=None):
     """concatenate the i-th sequences of every input, for each i"""
+    if not _lod(input[0]) and _meta(input[0]):
+        return W(torch.cat([T(x) for x in input], 0))
     offs = [_seq_offsets(x) for x in input]
     ts = [T(x) for x in input]
     parts, lens = [], []
@@ -126,6 +162,8 @@ def sequence_concat(input, name=None):
 
 
 def sequence_slice(input, offset, length, name=None):
+    if not _lod(input) and _meta(input):
+        return W(T(input).clone())
     off = _seq_offsets(input)
     t = T(input)
     so = T(offset).reshape(-1).tolist()
@@ -137,9 +175,13 @@ def sequence_slice(input, offset, length, name=None):
 def sequence_expand(x, y, ref_level=-1, name=None):
     """repeat each sequence (or row) of ``x`` as many times as ``y``'s ``ref_level`` LoD says"""
     ylod = _lod(y)
+    t = T(x)
+    if not ylod:
+        if _meta(y) or _meta(x):           # build time: the output has x's row layout
+            return W(t.clone())
+        raise ValueError("sequence_expand: y has no LoD")
     ref = ylod[ref_level]
     reps = fcore._lengths_from_offsets(ref)
-    t = T(x)
     xoff = _lod(x)[0] if _lod(x) else list(range(t.shape[0] + 1))
     parts, lens = [], []
     for i, r in enumerate(reps):
@@ -154,8 +196,10 @@ def sequence_expand(x, y, ref_level=-1, name=None):
 
 def sequence_expand_as(x, y, name=None):
     """row i of ``x`` repeated to the length of ``y``'s i-th sequence"""
-    lens = fcore._lengths_from_offsets(_seq_offsets(y))
     t = T(x)
+    if not _lod(y) and _meta(y):
+        return W(t.expand(T(y).shape[0], *t.shape[1:]).clone() if t.shape[0] == 1 else t.clone())
+    lens = fcore._lengths_from_offsets(_seq_offsets(y))
     out = W(torch.repeat_interleave(t, torch.tensor(lens, device=t.device), 0))
     out._lod = [fcore._offsets_from_lengths(lens)]
     return out
@@ -163,7 +207,7 @@ def sequence_expand_as(x, y, name=None):
 
 def sequence_pad(x, pad_value, maxlen=None, name=None):
     """-> (padded [B, maxlen, ...], lengths [B] int64)"""
-    p, lens, _ = to_padded(x)
+    p, lens, _ = _padded(x)
     pv = T(pad_value).reshape(-1)
     Tm = maxlen if maxlen is not None else p.shape[1]
     fill = pv.to(p.dtype).reshape(p.shape[2:]) if pv.numel() > 1 else pv.to(p.dtype).reshape(())
@@ -175,12 +219,17 @@ def sequence_pad(x, pad_value, maxlen=None, name=None):
 
 
 def sequence_unpad(x, length, name=None):
+    t = T(x)
+    if _meta(x):
+        return W(t.reshape(-1, *t.shape[2:]))
     lens = T(length).reshape(-1).long()
-    return from_padded(T(x), lens)
+    return from_padded(t, lens)
 
 
 def sequence_reshape(input, new_dim):
     t = T(input)
+    if not _lod(input) and _meta(input):
+        return W(t.reshape(-1, new_dim))
     D = t.shape[1]
     lens = [n * D // new_dim for n in fcore._lengths_from_offsets(_seq_offsets(input))]
     return _out(t.reshape(-1, new_dim), lens, input)
@@ -189,6 +238,8 @@ def sequence_reshape(input, new_dim):
 def sequence_scatter(input, index, updates, name=None):
     """out = input; out[i, index_j] += updates_j for the j-th row of the i-th update sequence"""
     t = T(input).clone()
+    if _meta(input):
+        return W(t)
     idx = T(index).reshape(-1).long()
     u = T(updates)
     uoff = _seq_offsets(updates)
@@ -202,6 +253,8 @@ def sequence_enumerate(input, win_size, pad_value=0, name=None):
     """every length-``win_size`` window starting at each position of each sequence (padded past
     the end)"""
     t = T(input).reshape(-1)
+    if _meta(input):
+        return W(t.new_zeros(t.shape[0], win_size))
     off = _seq_offsets(input)
     rows = []
     for i in range(len(off) - 1):
@@ -218,13 +271,18 @@ def sequence_enumerate(input, win_size, pad_value=0, name=None):
 
 def sequence_mask(x, maxlen=None, dtype="int64", name=None):
     lens = T(x)
-    m = int(T(maxlen).item()) if hasattr(maxlen, "_t") else (maxlen if maxlen is not None else int(lens.max()))
+    if hasattr(maxlen, "_t"):
+        m = 1 if _meta(maxlen) else int(T(maxlen).item())
+    else:
+        m = maxlen if maxlen is not None else (1 if lens.device.type == "meta" else int(lens.max()))
     r = torch.arange(m, device=lens.device)
     return W((r < lens[..., None]).to(fcore.convert_dtype(dtype)))
 
 
 def sequence_reverse(x, name=None):
     t = T(x)
+    if not _lod(x) and _meta(x):
+        return W(t.flip(0))
     off = _seq_offsets(x)
     parts = [t[off[i]:off[i + 1]].flip(0) for i in range(len(off) - 1)]
     out = W(torch.cat(parts, 0))
@@ -233,3 +291,5 @@ def sequence_reverse(x, name=None):
 
 
 _ = (dev, TF)
+# every op records one static op (sequence_conv records sequence_conv_op after creating its filter)
+register(globals(), [n for n in __all__ if n != "sequence_conv"] + ["sequence_conv_op"])

@@ -326,6 +326,7 @@ def data(name, shape, dtype=None, lod_level=0):
     meta = torch.empty([1 if s == -1 else s for s in shape], dtype=dt, device="meta")
     blk = default_main_program().global_block()
     v = Variable(blk, meta, name, declared_shape=shape, is_data=True)
+    v.lod_level = int(lod_level or 0)
     blk.vars[name] = v
     return v
 
@@ -702,6 +703,7 @@ def run_program(program, feed, fetch_list):
         env[id(v)] = _wrap(t)
         if getattr(val, "_lod", None):      # fluid LoD tensors keep their sequence offsets
             env[id(v)]._lod = val._lod
+            program.__dict__["_lod_run"] = True   # outputs share their inputs' LoD (_share_lod)
     fetch_ids = set()
     for f in fetch_list or []:
         if isinstance(f, str) and f in blk.vars:
@@ -740,6 +742,8 @@ def _cut_inputs(op, env):
         val = env.get(id(v))
         if isinstance(val, Tensor) and val._t.requires_grad and val._t.grad_fn is not None and id(v) not in saved:
             leaf = _wrap(val._t.detach().requires_grad_(True))
+            if getattr(val, "_lod", None):
+                leaf._lod = val._lod
             saved[id(v)] = val
             env[id(v)] = leaf
             env[("leaf", id(op), id(v))] = leaf
@@ -764,6 +768,24 @@ def _grad_env(op, env):
     return e2
 
 
+def _share_lod(op, out, env):
+    """the reference's ShareLoD (InferShape ctx->ShareLoD("X", "Out")): an output that has no LoD
+    of its own and keeps the row count of a LoD input carries that input's sequence offsets (fc,
+    embedding, activations ... on fluid LoD tensors); the sequence ops set theirs themselves"""
+    src = None
+    for v in _iter_vars((op.args, op.kwargs)):
+        val = env.get(id(v))
+        lod = getattr(val, "_lod", None)
+        if lod:
+            src = (val._t.shape[0] if val._t.dim() else None, lod)
+            break
+    if src is None:
+        return
+    for t in _iter_tensors(out if isinstance(out, (list, tuple)) else [out]):
+        if not getattr(t, "_lod", None) and t._t.dim() and t._t.shape[0] == src[0]:
+            t._lod = src[1]
+
+
 def run_block(program, blk, env, free=None):
     """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor);
     ``free``: op index -> Variable ids to drop after that op (eager deletion)"""
@@ -785,6 +807,8 @@ def run_block(program, blk, env, free=None):
             e = _grad_env(op, env) if "_fwd_id" in op.attrs else env
             out = op.fn(*_subst(op.args, e), **_subst(op.kwargs, e))
             _bind_outputs(op.outputs, out, env)
+            if program.__dict__.get("_lod_run"):
+                _share_lod(op, out, e)
         if saved:   # later readers see the original values (and their graph)
             env.update(saved)
         if free:

@@ -46,6 +46,21 @@ def _cmp(typ):
     return emit
 
 
+def _elt(typ):
+    """elementwise binary op; a Python-scalar operand becomes a constant input tensor"""
+    def emit(kw):
+        x, y = kw.get("x"), kw.get("y")
+        if not (_is_t(x) or _is_t(y)):
+            return None
+        extra = {}
+        if not _is_t(y):
+            extra["Y"] = _const(y, x)
+        if not _is_t(x):
+            extra["X"] = _const(x, y)
+        return typ, {"x": "X", "y": "Y"}, "Out", {"axis": -1}, extra
+    return emit
+
+
 def _getitem(kw):
     x, idx = kw.get("x"), kw.get("idx")
     if not _is_t(x):
@@ -252,10 +267,121 @@ def _ch_deq(kw):
         {"quant_bits": [int(b) for b in kw.get("quant_bits", (8,))], "quant_axis": int(kw.get("quant_axis", 0))}, {}
 
 
+# ------------------------------------------------------------------------------- LoD sequence ops
+# (sequence_ops/sequence_*_op.cc: slot and attribute names)
+def _seq_pool(pooltype=None):
+    def emit(kw):
+        pt = (pooltype or kw.get("pool_type", "average")).upper()
+        return "sequence_pool", {"input": "X"}, "Out", {"pooltype": pt, "is_test": bool(kw.get("is_test", False)),
+                                                        "pad_value": float(kw.get("pad_value", 0.0))}, {}
+    return emit
+
+
+def _seq_conv(kw):
+    if kw.get("bias") is not None:
+        return None
+    return "sequence_conv", {"input": "X", "filter": "Filter"}, "Out", \
+        {"contextLength": int(kw.get("context_length", 3)), "contextStart": int(kw.get("context_start", -1)),
+         "contextStride": int(kw.get("context_stride", 1)), "paddingTrainable": False}, {}
+
+
+def _seq_pad(kw):
+    pv = kw.get("pad_value")
+    ml = kw.get("maxlen")
+    return "sequence_pad", {"x": "X", "pad_value": "PadValue"}, ("Out", "Length"), \
+        {"padded_length": -1 if ml is None else int(ml)}, ({} if _is_t(pv) else {"PadValue": _const(pv)})
+
+
+def _seq_mask(kw):
+    from ..framework.core import convert_dtype
+    ml = kw.get("maxlen")
+    if _is_t(ml):
+        return None
+    return "sequence_mask", {"x": "X"}, "Y", {"maxlen": -1 if ml is None else int(ml),
+                                              "out_dtype": pb.vartype_of(convert_dtype(kw.get("dtype", "int64")))}, {}
+
+
+def _lookup_v1(kw):
+    pad = kw.get("padding_idx")
+    return "lookup_table", {"input": "Ids", "w": "W"}, "Out", \
+        {"padding_idx": -1 if pad is None else int(pad), "is_sparse": False, "is_distributed": False}, {}
+
+
+_S = "fluid.layers.sequence_lod."
+_SEQ = {
+    _S + "sequence_pool": _seq_pool(),
+    _S + "sequence_first_step": _seq_pool("FIRST"),
+    _S + "sequence_last_step": _seq_pool("LAST"),
+    _S + "sequence_conv_op": _seq_conv,
+    _S + "sequence_softmax": lambda kw: ("sequence_softmax", {"input": "X"}, "Out", {}, {}),
+    _S + "sequence_expand": lambda kw: ("sequence_expand", {"x": "X", "y": "Y"}, "Out",
+                                        {"ref_level": int(kw.get("ref_level", -1))}, {}),
+    _S + "sequence_expand_as": lambda kw: ("sequence_expand_as", {"x": "X", "y": "Y"}, "Out", {}, {}),
+    _S + "sequence_pad": _seq_pad,
+    _S + "sequence_unpad": lambda kw: ("sequence_unpad", {"x": "X", "length": "Length"}, "Out", {}, {}),
+    _S + "sequence_reverse": lambda kw: ("sequence_reverse", {"x": "X"}, "Y", {}, {}),
+    _S + "sequence_concat": lambda kw: ("sequence_concat", {"input": "X"}, "Out", {}, {}),
+    _S + "sequence_reshape": lambda kw: ("sequence_reshape", {"input": "X"}, "Out",
+                                         {"new_dim": int(kw.get("new_dim"))}, {}),
+    _S + "sequence_mask": _seq_mask,
+    _S + "sequence_enumerate": lambda kw: ("sequence_enumerate", {"input": "X"}, "Out",
+                                           {"win_size": int(kw.get("win_size")),
+                                            "pad_value": int(kw.get("pad_value", 0))}, {}),
+    _S + "sequence_slice": lambda kw: ("sequence_slice", {"input": "X", "offset": "Offset", "length": "Length"},
+                                       "Out", {}, {}),
+    _S + "sequence_scatter": lambda kw: ("sequence_scatter", {"input": "X", "index": "Ids", "updates": "Updates"},
+                                         "Out", {}, {}),
+    "fluid.layers.nn._lookup_v1": _lookup_v1,
+}
+
+# ------------------------------------------------------------------------------- activations
+# (activation_op.cc: the 2.x function's arguments renamed to the 1.x op's attributes)
+def _act(typ, **attrs):
+    """``attrs``: reference attr -> (our kwarg, default) or a constant"""
+    def emit(kw):
+        if kw.get("dtype") is not None:
+            return None
+        at = {a: (float(kw.get(v[0], v[1])) if isinstance(v, tuple) else v) for a, v in attrs.items()}
+        return typ, {"x": "X"}, "Out", at, {}
+    return emit
+
+
+_A = "nn.functional.activation."
+_ACT = {
+    _A + "tanh": _act("tanh"),
+    _A + "leaky_relu": _act("leaky_relu", alpha=("negative_slope", 0.01)),
+    _A + "elu": _act("elu", alpha=("alpha", 1.0)),
+    _A + "relu6": _act("relu6", threshold=6.0),
+    _A + "hardswish": _act("hard_swish", threshold=6.0, scale=6.0, offset=3.0),
+    _A + "hardsigmoid": _act("hard_sigmoid", slope=("slope", 0.1666667), offset=("offset", 0.5)),
+    _A + "softplus": _act("softplus", beta=("beta", 1.0), threshold=("threshold", 20.0)),
+    _A + "softshrink": _act("softshrink", **{"lambda": ("threshold", 0.5)}),
+    _A + "hardshrink": _act("hard_shrink", threshold=("threshold", 0.5)),
+    _A + "thresholded_relu": _act("thresholded_relu", threshold=("threshold", 1.0)),
+    _A + "swish": _act("swish", beta=1.0),
+    _A + "mish": _act("mish"),
+    _A + "selu": _act("selu", scale=("scale", 1.0507009873554805), alpha=("alpha", 1.6732632423543772)),
+    _A + "tanhshrink": _act("tanh_shrink"),
+    _A + "log_sigmoid": _act("logsigmoid"),
+    _A + "softsign": _act("softsign"),
+    _A + "hardtanh": _act("brelu", t_min=("min", -1.0), t_max=("max", 1.0)),
+    _A + "log_softmax": lambda kw: None if kw.get("dtype") is not None else
+    ("log_softmax", {"x": "X"}, "Out", {"axis": int(kw.get("axis", -1))}, {}),
+    **{"tensor.math." + n: _act(n) for n in ("log", "abs", "sin", "cos", "tan", "floor", "ceil", "rsqrt", "square",
+                                             "reciprocal", "sign", "erf", "round", "log2", "log10", "log1p", "expm1",
+                                             "atan", "asin", "acos", "sinh", "cosh")},
+}
+
 _Q = "nn.quant.ops."
 EMIT = {
+    **_SEQ,
+    **_ACT,
     **{f"tensor.logic.{n}": _cmp(n) for n in ("greater_than", "greater_equal", "less_than", "less_equal", "equal",
                                                "not_equal")},
+    **{f"tensor.math.{n}": _elt(t) for n, t in (("add", "elementwise_add"), ("subtract", "elementwise_sub"),
+                                                ("multiply", "elementwise_mul"), ("divide", "elementwise_div"),
+                                                ("maximum", "elementwise_max"), ("minimum", "elementwise_min"),
+                                                ("pow", "elementwise_pow"))},
     "tensor.getitem": _getitem,
     "tensor.manipulation.expand": _expand,
     "tensor.manipulation.broadcast_to": _expand,

@@ -675,7 +675,64 @@ def _conv_q_linear(typ):
     return conv
 
 
+# LoD sequence ops (sequence_ops/sequence_*_op.cc), run by fluid.layers.sequence_lod at run time
+def _seq(name):
+    from ..fluid.layers import sequence_lod as S
+    f = getattr(S, name)
+    return getattr(f, "__wrapped_op__", f)
+
+
+def _conv_seq_pool(r, ins, at):
+    return _seq("sequence_pool"), {"input": _one(r, ins, "X"), "pool_type": at.get("pooltype", "AVERAGE").lower(),
+                                   "is_test": at.get("is_test", False), "pad_value": at.get("pad_value", 0.0)}, "Out"
+
+
+def _conv_seq_conv(r, ins, at):
+    return _seq("sequence_conv_op"), {"input": _one(r, ins, "X"), "filter": _one(r, ins, "Filter"),
+                                      "context_length": at.get("contextLength", 3),
+                                      "context_start": at.get("contextStart", -1),
+                                      "context_stride": at.get("contextStride", 1)}, "Out"
+
+
+def _conv_seq_pad(r, ins, at):
+    pl = at.get("padded_length", -1)
+    return _seq("sequence_pad"), {"x": _one(r, ins, "X"), "pad_value": _one(r, ins, "PadValue"),
+                                  "maxlen": None if pl == -1 else pl}, ("Out", "Length")
+
+
+def _conv_seq_mask(r, ins, at):
+    ml = at.get("maxlen", -1)
+    return _seq("sequence_mask"), {"x": _one(r, ins, "X"), "maxlen": None if ml == -1 else ml,
+                                   "dtype": pb.dtype_of(at.get("out_dtype", 3))}, "Y"
+
+
+_SEQ_CONVERT = {
+    "sequence_pool": _conv_seq_pool,
+    "sequence_conv": _conv_seq_conv,
+    "sequence_softmax": lambda r, ins, at: (_seq("sequence_softmax"), {"input": _one(r, ins, "X")}, "Out"),
+    "sequence_expand": lambda r, ins, at: (_seq("sequence_expand"), {"x": _one(r, ins, "X"), "y": _one(r, ins, "Y"),
+                                                                     "ref_level": at.get("ref_level", -1)}, "Out"),
+    "sequence_expand_as": lambda r, ins, at: (_seq("sequence_expand_as"), {"x": _one(r, ins, "X"),
+                                                                           "y": _one(r, ins, "Y")}, "Out"),
+    "sequence_pad": _conv_seq_pad,
+    "sequence_unpad": lambda r, ins, at: (_seq("sequence_unpad"), {"x": _one(r, ins, "X"),
+                                                                   "length": _one(r, ins, "Length")}, "Out"),
+    "sequence_reverse": lambda r, ins, at: (_seq("sequence_reverse"), {"x": _one(r, ins, "X")}, "Y"),
+    "sequence_concat": lambda r, ins, at: (_seq("sequence_concat"), {"input": _many(r, ins, "X")}, "Out"),
+    "sequence_reshape": lambda r, ins, at: (_seq("sequence_reshape"), {"input": _one(r, ins, "X"),
+                                                                       "new_dim": at["new_dim"]}, "Out"),
+    "sequence_mask": _conv_seq_mask,
+    "sequence_enumerate": lambda r, ins, at: (_seq("sequence_enumerate"), {
+        "input": _one(r, ins, "X"), "win_size": at["win_size"], "pad_value": at.get("pad_value", 0)}, "Out"),
+    "sequence_slice": lambda r, ins, at: (_seq("sequence_slice"), {
+        "input": _one(r, ins, "X"), "offset": _one(r, ins, "Offset"), "length": _one(r, ins, "Length")}, "Out"),
+    "sequence_scatter": lambda r, ins, at: (_seq("sequence_scatter"), {
+        "input": _one(r, ins, "X"), "index": _one(r, ins, "Ids"), "updates": _one(r, ins, "Updates")}, "Out"),
+}
+
+
 CONVERT = {
+    **_SEQ_CONVERT,
     # fake quantization (fake_quantize_op.cc, fake_dequantize_op.cc, quantize_linear_op.cc)
     "fake_quantize_dequantize_abs_max": _conv_q_absmax("fake_quantize_dequantize_abs_max"),
     "fake_quantize_abs_max": _conv_q_absmax("fake_quantize_abs_max"),

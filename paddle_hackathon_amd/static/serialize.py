@@ -357,11 +357,13 @@ class _Writer:
 
 
 def _var_desc(blk_msg, name, t, persistable=False, is_param=False, shape=None, need_check_feed=False,
-              stop_gradient=True):
+              stop_gradient=True, lod_level=0):
     vd = blk_msg.vars.add()
     vd.name = name
     vd.type.type = pb.LOD_TENSOR
     vd.type.lod_tensor.tensor.data_type = pb.vartype_of(t.dtype)
+    if lod_level:
+        vd.type.lod_tensor.lod_level = int(lod_level)
     vd.type.lod_tensor.tensor.dims.extend(int(s) for s in (shape if shape is not None else t.shape))
     vd.persistable = persistable
     vd.is_parameter = is_param
@@ -416,7 +418,8 @@ def program_to_desc(program, feed_vars, fetch_vars):
     for bidx, v in sorted(w.var_block.values(), key=lambda p: (p[0], p[1].name)):
         shape = v.declared_shape if v.declared_shape is not None else list(v._t.shape)
         _var_desc(blocks[bidx], v.name, v._t, shape=[-1 if s is None else s for s in shape],
-                  need_check_feed=id(v) in feed_ids, stop_gradient=not getattr(v, "need_grad", False))
+                  need_check_feed=id(v) in feed_ids, stop_gradient=not getattr(v, "need_grad", False),
+                  lod_level=getattr(v, "lod_level", 0))
     for name in sorted(w.persist):
         t = w.persist[name]
         _var_desc(g, name, t._t, persistable=True, is_param=isinstance(t, Parameter),
@@ -488,6 +491,8 @@ class _Reader:
                 meta = torch.empty([1 if s < 0 else s for s in dims], dtype=pb.dtype_of(td.data_type), device="meta")
                 v = Variable(blk, meta, vd.name, declared_shape=dims if any(s < 0 for s in dims) else None)
                 v.need_grad = not vd.stop_gradient
+                if vd.type.lod_tensor.lod_level:
+                    v.lod_level = int(vd.type.lod_tensor.lod_level)
                 blk.vars[vd.name] = v
                 self.vars[vd.name] = v
         feeds, fetches = {}, {}
