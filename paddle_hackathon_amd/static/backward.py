@@ -330,7 +330,7 @@ def append_optimize_op(optimizer, params_grads, program=None, block=None, found_
     if found_inf is not None:
         kw["found_inf"] = found_inf
     op = P.OpDesc(type(optimizer).__name__.lower(), _update, (), kw, None,
-                  attrs={"op_role": OPTIMIZE, "op_role_var": [p.name for p in ps]})
+                  attrs={"op_role": OPTIMIZE, "op_role_var": [p.name for p in ps], "optimizer": optimizer})
     blk.append_op(op)
     return op
 

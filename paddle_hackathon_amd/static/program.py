@@ -822,6 +822,14 @@ def has_control_flow(program):
     return len(program.blocks) > 1 or any(op.exec is not None for op in program.global_block().ops)
 
 
+_CLOSE_HOOKS = []
+
+
+def register_close_hook(fn):
+    """``fn()`` runs at the next ``Executor.close()`` (once)"""
+    _CLOSE_HOOKS.append(fn)
+
+
 class Executor:
     def __init__(self, place=None):
         self.place = place
@@ -852,7 +860,10 @@ class Executor:
         return outs
 
     def close(self):
-        pass
+        """end this process' part in a distributed job: the close hooks registered by the
+        transpiled programs run (a DistributeTranspiler trainer leaves the parameter servers)"""
+        while _CLOSE_HOOKS:
+            _CLOSE_HOOKS.pop(0)()
 
     def train_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
                            fetch_info=None, print_period=100, fetch_handler=None):

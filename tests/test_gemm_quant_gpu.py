@@ -31,7 +31,7 @@ def test_paddle_matmul_own_layouts(ta, tb, M, N, K, monkeypatch):
     out.backward(paddle.to_tensor(gout))
     torch.cuda.synchronize()
     assert fallback.total() == 0 and not fallback.library_counts(), (fallback.counts(), fallback.library_counts())
-    af, bf = a.float().requires_grad_(), b.float().requires_grad_()
+    af, bf = a.detach().float().requires_grad_(), b.detach().float().requires_grad_()
     ref = (af.t() if ta else af) @ (bf.t() if tb else bf)
     ref.backward(gout.float())
     scale = K ** 0.5

@@ -1,0 +1,215 @@
+"""fluid DistributeTranspiler (reference: python/paddle/fluid/transpiler/distribute_transpiler.py,
+tests test_dist_transpiler.py / test_dist_mnist*.py: parameter blocks, send / recv insertion,
+pserver programs; sync training equals full-batch local training)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import paddle_hackathon_amd as paddle  # noqa: E402
+import paddle_hackathon_amd.fluid as fluid  # noqa: E402
+from paddle_hackathon_amd.utils import native  # noqa: E402
+from dist_helper import run_dist  # noqa: E402
+
+_MODEL = '''
+def build(seed):
+    paddle.seed(seed)
+    main, start = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, start):
+        x = fluid.data("x", [None, 16], "float32")
+        y = fluid.data("y", [None, 1], "float32")
+        h = fluid.layers.fc(x, 64, act="tanh")
+        pred = fluid.layers.fc(h, 1)
+        loss = fluid.layers.mean(fluid.layers.square_error_cost(pred, y))
+        fluid.optimizer.SGD(0.1).minimize(loss)
+    return main, start, loss
+
+
+def batches(n):
+    rs = np.random.RandomState(0)
+    wt = rs.randn(16, 1).astype("float32")
+    for _ in range(n):
+        xb = rs.randn(32, 16).astype("float32")
+        yield xb, np.tanh(xb @ wt)
+'''
+
+_JOB = textwrap.dedent('''
+    import json, sys
+    sys.path.insert(0, {root!r})
+    import numpy as np
+    import paddle_hackathon_amd as paddle
+    import paddle_hackathon_amd.fluid as fluid
+''') + _MODEL + textwrap.dedent('''
+    role, idx, eps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    paddle.enable_static()
+    main, start, loss = build(100 + idx)   # different local inits: the servers' copy of trainer 0's wins
+    cfg = fluid.DistributeTranspilerConfig()
+    cfg.min_block_size = 256
+    t = fluid.DistributeTranspiler(cfg)
+    t.transpile(idx if role == "trainer" else 0, program=main, pservers=eps, trainers=2, startup_program=start)
+    exe = fluid.Executor(fluid.CPUPlace())
+    if role == "pserver":
+        ps_main, ps_start = t.get_pserver_programs(eps.split(",")[idx])
+        exe.run(ps_start)
+        exe.run(ps_main)          # serves until both trainers closed
+        sys.exit(0)
+    prog = t.get_trainer_program()
+    exe.run(start)
+    losses = []
+    for xb, yb in batches(12):
+        mine = slice(idx * 16, idx * 16 + 16)
+        l, = exe.run(prog, feed={{"x": xb[mine], "y": yb[mine]}}, fetch_list=[loss])
+        losses.append(float(np.asarray(l).ravel()[0]))
+    params = {{p.name: p.numpy().tolist() for p in main.all_parameters()}}
+    exe.close()
+    json.dump({{"losses": losses, "params": params, "blocks": [repr(b) for b in t.blocks],
+               "types": [op.type for op in prog.global_block().ops]}}, open(out, "w"))
+''')
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _local_reference(n_steps):
+    """the same model trained in one process on the full 32-row batches from trainer 0's init"""
+    ns = {"paddle": paddle, "fluid": fluid, "np": np}
+    exec(_MODEL, ns)
+    paddle.enable_static()
+    try:
+        main, start, loss = ns["build"](100)
+        exe = fluid.Executor(fluid.CPUPlace())
+        exe.run(start)
+        for xb, yb in ns["batches"](n_steps):
+            exe.run(main, feed={"x": xb, "y": yb}, fetch_list=[loss])
+        return {p.name: p.numpy() for p in main.all_parameters()}
+    finally:
+        paddle.disable_static()
+
+
+def test_slice_variable_and_dispatch():
+    from paddle_hackathon_amd.fluid.transpiler import slice_variable
+
+    class V:
+        def __init__(self, name, shape):
+            self.name, self.shape = name, shape
+    blocks = slice_variable(V("w", [1000, 64]), 3, 8192)
+    assert [(b.row0, b.row1) for b in blocks] == [(0, 334), (334, 668), (668, 1000)]
+    assert sum(b.numel for b in blocks) == 64000 and blocks[1].offset == 334 * 64
+    assert len(slice_variable(V("b", [64]), 3, 8192)) == 1          # below min_block_size: one block
+    eps = ["a:1", "b:2"]
+    assert fluid.RoundRobin(eps).dispatch(blocks) == ["a:1", "b:2", "a:1"]
+    h = fluid.HashName(eps).dispatch(blocks)
+    assert h == fluid.HashName(eps).dispatch(blocks) and set(h) <= set(eps)
+
+
+@pytest.mark.skipif(not native.available(), reason="native runtime (parameter server) not built")
+def test_transpiled_pserver_training_equals_full_batch(tmp_path):
+    """2 pservers + 2 trainers (separate processes): the trainer program sends gradient blocks and
+    receives parameter blocks; after 12 sync steps both trainers hold the parameters of one
+    process trained on the full batches (mean of the two half-batch gradients)"""
+    script = tmp_path / "job.py"
+    script.write_text(_JOB.format(root=ROOT))
+    eps = f"127.0.0.1:{_port()},127.0.0.1:{_port()}"
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    procs = [subprocess.Popen([sys.executable, str(script), "pserver", str(i), eps, "-"], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for i in range(2)]
+    procs += [subprocess.Popen([sys.executable, str(script), "trainer", str(i), eps, str(tmp_path / f"t{i}.json")],
+                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+              for i in range(2)]
+    logs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=180)
+            logs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    res = [json.load(open(tmp_path / f"t{i}.json")) for i in range(2)]
+    types = res[0]["types"]
+    assert "sgd" not in types
+    assert types.count("send") == 4 and types.count("recv") == 4
+    assert types.index("send_barrier") < types.index("recv") < types.index("fetch_barrier")
+    assert sum("block1" in b for b in res[0]["blocks"]) == 1      # the 16x64 weight is cut in two
+    assert res[0]["losses"][-1] < res[0]["losses"][0]
+    ref = _local_reference(12)
+    for name, v in ref.items():
+        for r in res:
+            np.testing.assert_allclose(np.asarray(r["params"][name]).reshape(v.shape), v, rtol=2e-4, atol=2e-5)
+
+
+def test_pserver_program_structure():
+    paddle.enable_static()
+    try:
+        main, start = fluid.Program(), fluid.Program()
+        with fluid.program_guard(main, start):
+            x = fluid.data("x", [None, 8], "float32")
+            loss = fluid.layers.mean(fluid.layers.fc(x, 4))
+            fluid.optimizer.Adam(0.01).minimize(loss)
+        t = fluid.DistributeTranspiler()
+        t.transpile(0, program=main, pservers="127.0.0.1:7001,127.0.0.1:7002", trainers=2, startup_program=start)
+        ps = t.get_pserver_program("127.0.0.1:7002")
+        ops = ps.global_block().ops
+        assert [o.type for o in ops] == ["listen_and_serv"]
+        assert ops[0].attrs["rule"] == "adam" and ops[0].attrs["Fanin"] == 2
+        assert ops[0].attrs["optimize_blocks"] == [b.name for b in t.blocks if b.endpoint == "127.0.0.1:7002"]
+        with pytest.raises(ValueError):
+            t.get_pserver_program("127.0.0.1:9999")
+        main2, start2 = fluid.Program(), fluid.Program()
+        with fluid.program_guard(main2, start2):
+            x = fluid.data("x", [None, 8], "float32")
+            loss = fluid.layers.mean(fluid.layers.fc(x, 4))
+            fluid.optimizer.Momentum(0.01, 0.9).minimize(loss)
+        with pytest.raises(NotImplementedError):
+            fluid.DistributeTranspiler().transpile(0, program=main2, pservers="127.0.0.1:7001", trainers=1,
+                                                   startup_program=start2)
+    finally:
+        paddle.disable_static()
+
+
+def _nccl2_body(rank, world):
+    import numpy as np
+    import paddle_hackathon_amd as paddle
+    import paddle_hackathon_amd.fluid as fluid
+    paddle.enable_static()
+    paddle.seed(7 + rank)             # different inits: the startup broadcast makes them equal
+    main, start = fluid.Program(), fluid.Program()
+    with fluid.program_guard(main, start):
+        x = fluid.data("x", [None, 8], "float32")
+        y = fluid.data("y", [None, 1], "float32")
+        loss = fluid.layers.mean(fluid.layers.square_error_cost(fluid.layers.fc(x, 1), y))
+        fluid.optimizer.SGD(0.2).minimize(loss)
+    cfg = fluid.DistributeTranspilerConfig()
+    cfg.mode = "nccl2"
+    t = fluid.DistributeTranspiler(cfg)
+    t.transpile(rank, program=main, pservers="", trainers="127.0.0.1:1,127.0.0.1:2", startup_program=start,
+                current_endpoint=f"127.0.0.1:{rank + 1}")
+    exe = fluid.Executor(fluid.CPUPlace())
+    exe.run(start)
+    rs = np.random.RandomState(rank)
+    for _ in range(5):
+        xb = rs.randn(8, 8).astype("float32")
+        exe.run(t.get_trainer_program(), feed={"x": xb, "y": xb.sum(1, keepdims=True)}, fetch_list=[loss])
+    types = [o.type for o in t.get_trainer_program().global_block().ops]
+    return {p.name: p.numpy() for p in main.all_parameters()}, types
+
+
+def test_transpiler_nccl2_mode_allreduces_gradients():
+    a, b = run_dist(_nccl2_body, world=2)
+    assert "c_allreduce_coalesced" in a[1]
+    for k in a[0]:
+        np.testing.assert_allclose(a[0][k], b[0][k], rtol=1e-6)
