@@ -49,6 +49,23 @@ class Layout:
         return s
 
 
+def _tp_slice(state, model, rank, tp):
+    """the slices of a full state dict that tensor-parallel rank ``rank`` of ``tp`` holds: each
+    tensor whose shape differs from the model's parameter is split along the differing dim"""
+    import numpy as np
+    params = dict(model.named_parameters())
+    out = {}
+    for name, v in state.items():
+        p = params.get(name)
+        v = np.asarray(v)
+        if p is None or tuple(p.shape) == v.shape:
+            out[name] = v
+            continue
+        d = [i for i in range(v.ndim) if v.shape[i] != p.shape[i]][0]
+        out[name] = np.ascontiguousarray(np.split(v, tp, axis=d)[rank % tp])
+    return out
+
+
 class GPTTrainer:
     """``step(inp, lab) -> loss`` for one rank of the layout (inp / lab: this rank's token block,
     [batch, seq] int64; with pipeline parallelism the batch is cut into ``micro_batches``)."""
@@ -81,6 +98,8 @@ class GPTTrainer:
         else:
             model = GPTForPretraining(cfg)
             if state is not None:
+                if lo.tp > 1:   # a full (single-card) state: this rank's tensor-parallel slices
+                    state = _tp_slice(state, model, hcg.get_model_parallel_rank(), lo.tp)
                 model.set_state_dict({k: paddle.to_tensor(v) for k, v in state.items()})
         if amp:
             model = paddle.amp.decorate(model, level="O2", dtype="bfloat16")
