@@ -12,6 +12,8 @@ from . import asp  # noqa: F401
 from . import checkpoint  # noqa: F401
 from . import distributed  # noqa: F401
 from . import autotune  # noqa: F401
+from . import operators  # noqa: F401
+from . import passes  # noqa: F401
 from .. import sparse  # noqa: F401
 
 __all__ = ["LookAhead", "ModelAverage", "softmax_mask_fuse_upper_triangle", "softmax_mask_fuse", "graph_send_recv",

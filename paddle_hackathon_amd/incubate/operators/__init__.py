@@ -9,9 +9,9 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..framework.core import Tensor, _wrap
-from ..framework.dispatch import register_ops
-from .. import ops as _ops
+from ...framework.core import Tensor, _wrap
+from ...framework.dispatch import register_ops
+from ... import ops as _ops
 
 __all__ = ["graph_send_recv", "graph_khop_sampler", "graph_reindex", "graph_sample_neighbors", "segment_sum",
            "segment_mean", "segment_max", "segment_min", "softmax_mask_fuse", "softmax_mask_fuse_upper_triangle",
@@ -185,3 +185,8 @@ def identity_loss(x, reduction="none"):
 
 
 register_ops(globals(), __all__)
+
+
+from .resnet_unit import ResNetUnit, resnet_unit  # noqa: E402,F401
+
+__all__ += ["ResNetUnit", "resnet_unit"]
