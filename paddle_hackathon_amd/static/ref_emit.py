@@ -372,8 +372,27 @@ _ACT = {
                                              "atan", "asin", "acos", "sinh", "cosh")},
 }
 
+_RU_SLOTS = {"x": "X", "filter_x": "FilterX", "scale_x": "ScaleX", "bias_x": "BiasX", "mean_x": "MeanX",
+             "var_x": "VarX", "z": "Z", "filter_z": "FilterZ", "scale_z": "ScaleZ", "bias_z": "BiasZ",
+             "mean_z": "MeanZ", "var_z": "VarZ"}
+
+
+def _resnet_unit(kw):
+    """resnet_unit_op.cc: the reference filter layout only (OHWI for NHWC, OIHW for NCHW)"""
+    fmt = kw.get("data_format", "NHWC")
+    if kw.get("filter_layout") not in (None, "OHWI" if fmt == "NHWC" else "OIHW"):
+        return None
+    return "resnet_unit", dict(_RU_SLOTS), "Y", {
+        "stride": int(kw["stride"]), "stride_z": int(kw["stride_z"]), "padding": int(kw["padding"]),
+        "dilation": int(kw["dilation"]), "group": int(kw["groups"]), "momentum": float(kw["momentum"]),
+        "epsilon": float(kw["eps"]), "data_format": fmt, "fuse_add": bool(kw["fuse_add"]),
+        "has_shortcut": bool(kw["has_shortcut"]), "use_global_stats": bool(kw["use_global_stats"]),
+        "is_test": bool(kw["is_test"]), "act_type": kw.get("act") or "identity"}, {}
+
+
 _Q = "nn.quant.ops."
 EMIT = {
+    "incubate.operators.resnet_unit.resnet_unit": _resnet_unit,
     **_SEQ,
     **_ACT,
     **{f"tensor.logic.{n}": _cmp(n) for n in ("greater_than", "greater_equal", "less_than", "less_equal", "equal",

@@ -567,6 +567,21 @@ def _kw(fn, slots, attrs, out, **fixed):
     return conv
 
 
+def _conv_resnet_unit(r, ins, at):
+    from ..incubate.operators.resnet_unit import resnet_unit
+    slots = {"x": "X", "filter_x": "FilterX", "scale_x": "ScaleX", "bias_x": "BiasX", "mean_x": "MeanX",
+             "var_x": "VarX", "z": "Z", "filter_z": "FilterZ", "scale_z": "ScaleZ", "bias_z": "BiasZ",
+             "mean_z": "MeanZ", "var_z": "VarZ"}
+    kw = {k: _one(r, ins, s) for k, s in slots.items()}
+    kw.update(stride=at.get("stride", 1), stride_z=at.get("stride_z", 1), padding=at.get("padding", 0),
+              dilation=at.get("dilation", 1), groups=at.get("group", 1), momentum=at.get("momentum", 0.9),
+              eps=at.get("epsilon", 1e-5), data_format=at.get("data_format", "NHWC"),
+              fuse_add=at.get("fuse_add", False), has_shortcut=at.get("has_shortcut", False),
+              use_global_stats=at.get("use_global_stats", False), is_test=at.get("is_test", False),
+              act=at.get("act_type", "relu"))
+    return resnet_unit, kw, "Y"
+
+
 def _conv_stack(r, ins, at):
     return stack_op, {"xs": _many(r, ins, "X"), "axis": at.get("axis", 0)}, "Y"
 
@@ -780,6 +795,7 @@ CONVERT = {
                   "Out"),
     # shape / indexing
     "stack": _conv_stack,
+    "resnet_unit": _conv_resnet_unit,
     "unstack": _conv_unstack,
     "split": _conv_split,
     "gather": _conv_gather,

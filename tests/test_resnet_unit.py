@@ -119,3 +119,35 @@ def test_resnet_unit_gpu_bf16_nhwc(mode):
         torch.testing.assert_close(x.grad._t.double(), gx.to(y._t.device), atol=0.08, rtol=0.05)
     finally:
         paddle.set_device("cpu")
+
+
+def test_resnet_unit_saves_as_reference_op(tmp_path):
+    """a program with a ResNetUnit (NHWC, reference filter layout) is written as one resnet_unit op
+    with the reference slots / attributes and computes the same after loading (inference)"""
+    import sys
+    sys.path.insert(0, __file__.rsplit("/", 1)[0])
+    from test_program_desc import _strip_private
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [2, 6, 6, 8], "float32")
+            u = ResNetUnit(8, 16, 3, is_test=True)
+            y = u(x)
+        exe = paddle.static.Executor()
+        xv = np.random.RandomState(0).randn(2, 6, 6, 8).astype("float32")
+        ref, = exe.run(main, feed={"x": xv}, fetch_list=[y])
+        prefix = str(tmp_path / "ru")
+        paddle.static.save_inference_model(prefix, [x], [y], exe, program=main)
+        desc = _strip_private(prefix + ".pdmodel")
+        ops = [o for o in desc.blocks[0].ops if o.type not in ("feed", "fetch")]
+        assert [o.type for o in ops] == ["resnet_unit"]
+        slots = {v.parameter for v in ops[0].inputs}
+        assert {"X", "FilterX", "ScaleX", "BiasX", "MeanX", "VarX"} <= slots
+        attrs = {a.name for a in ops[0].attrs}
+        assert {"stride", "padding", "epsilon", "data_format", "act_type", "has_shortcut"} <= attrs
+        prog, _, fetches = paddle.static.load_inference_model(prefix, exe)
+        got, = exe.run(prog, feed={"x": xv}, fetch_list=fetches)
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+    finally:
+        paddle.disable_static()
