@@ -64,6 +64,9 @@ struct Args {
   // optional C += addend (same layout and ldc as C, after the bias / activation): a conv dgrad
   // that also receives the residual branch's gradient stores the sum, no separate add pass
   const void* addend = nullptr;
+  // C is fp32 (ldc in floats): the accumulators are stored directly (bias / activation / output
+  // remap applied; no stats, bn_part or addend) — the fp32 products split into three bf16 terms
+  int out_f32 = 0;
 };
 
 
@@ -82,7 +85,7 @@ struct ARow {
   bool ok;
 };
 
-template <typename T, int BM, int BN, int BK, bool CONV>
+template <typename T, int BM, int BN, int BK, bool CONV, bool F32OUT = false>
 __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   constexpr int NSTAGE = BK == 64 ? 2 : 4;   // BK 64: one tile in flight; BK 32: three
   constexpr int WN = BN / 64, WM = 8 / WN;          // wave grid
@@ -229,6 +232,43 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
     }
   }
   __builtin_amdgcn_s_barrier();   // all fragment reads done: the LDS is reused for the C tile
+
+  // ---- fp32 output: straight from the accumulators (16 lanes store 64 contiguous bytes of a row)
+  if constexpr (F32OUT) {
+    float* Cf = static_cast<float*>(p.c);
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const long n = n0 + wn * 64 + j * 16 + fr;
+      if (n >= N) continue;
+      const float bv = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          long m = m0 + wm * WTM + i * 16 + 4 * fk + e;
+          if (m >= M) continue;
+          float v = acc[i][j][e] + bv;
+          if (p.act == ACT_RELU) v = fmaxf(v, 0.f);
+          else if (p.act == ACT_GELU) v = gelu_tanh(v);
+          if constexpr (CONV) {
+            const ConvGeo& g = p.g;
+            if (g.osh > 0) {
+              const int hw = g.OH * g.OW;
+              const int b = (int)(m / hw), rem = (int)(m - (long)b * hw);
+              const int oh = rem / g.OW, ow = rem - oh * g.OW;
+              const int fh = g.oh0 + oh * g.osh, fw = g.ow0 + ow * g.osw;
+              m = ((long)b * g.OHF + fh) * g.OWF + fw;
+              if (g.ozero)
+                for (int a = 0; a < g.osh; ++a)
+                  for (int c = 0; c < g.osw; ++c)
+                    if ((a | c) && fh + a < g.OHF && fw + c < g.OWF) Cf[(m + (long)a * g.OWF + c) * p.ldc + n] = 0.f;
+            }
+          }
+          Cf[m * p.ldc + n] = v;
+        }
+    }
+    return;
+  }
 
   // ---- epilogue: bias / activation, C tile staged through LDS so every lane stores 16 B --------
   // acc[i][j] register e = C[row 4*(lane>>4) + e][col lane&15] of 16x16 block (i, j)
@@ -413,6 +453,11 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_
   if (tile >= 0 && tile < 6) best = tile;
   const int bm = cands[best][0], bn = cands[best][1];
   if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);   // row tiles with stats / bn_part rows
+  if (a.out_f32) {   // fp32 products (three-term bf16 split): one 128 x 128 x 32 instantiation
+    const long tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    hipLaunchKernelGGL((gemm256_kernel<T, 128, 128, 32, CONV, true>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    return (int)hipGetLastError();
+  }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;
     const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
@@ -739,6 +784,27 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
                bn_x, bn_mean, bn_aff, bn_part, bn_row0, addend};
   if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, stats_rows);
   if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, stats_rows);
+  return (int)hipErrorInvalidValue;
+}
+
+// pha_conv256_fwd with an fp32 y (ldc = Cout floats): bias / act / output remap only (the fp32
+// convolution as one bf16 implicit GEMM over the [hi, hi, lo] x [hi, lo, hi] channel split)
+PHA_API int pha_conv256_fwd_f32out(int dt, const void* x, const void* w, float* y, const float* bias, int N, int H,
+                                   int W, int C, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int dh,
+                                   int dw, int act, const void* zero16, int tile, int bk, const int* oremap,
+                                   hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  g256::ConvGeo g{N, H, W, C, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
+                  KH, KW, sh, sw, ph, pw, dh, dw, 0, 0, 0, 0, 0, 0, 0};
+  if (oremap) {
+    g.OHF = oremap[0]; g.OWF = oremap[1]; g.oh0 = oremap[2]; g.ow0 = oremap[3]; g.osh = oremap[4]; g.osw = oremap[5];
+    g.OH = oremap[6]; g.OW = oremap[7]; g.ozero = oremap[8];
+  }
+  const long M = (long)N * g.OH * g.OW, K = (long)KH * KW * C;
+  g256::Args p{x, w, y, bias, M, (long)Cout, K, 0, K, (long)Cout, act, zero16, g, nullptr,
+               nullptr, nullptr, nullptr, nullptr, 0, nullptr, 1};
+  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk);
+  if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk);
   return (int)hipErrorInvalidValue;
 }
 

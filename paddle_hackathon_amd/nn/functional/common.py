@@ -57,6 +57,9 @@ def linear(x, weight, bias=None, name=None):
         elif _ops.fused._use_hip(xt) and xt.dtype in (torch.bfloat16, torch.float16) and b.dtype == xt.dtype \
                 and wt.dtype == xt.dtype and wt.shape[-1] % 8 == 0:
             out = _LinearBias.apply(x2d, wt, b)
+        elif xt.is_cuda:   # fp32 / mixed products: ops/gemm.py (three-term bf16 split for fp32)
+            from ...ops import gemm as _gemm
+            out = _gemm.matmul(x2d, wt) + b
         else:
             out = torch.addmm(b, x2d, wt)
         return _w(out.reshape(list(xt.shape[:-1]) + [wt.shape[-1]]))

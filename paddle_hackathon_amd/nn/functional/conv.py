@@ -2,8 +2,9 @@
 
 Paddle layouts: weight [C_out, C_in/groups, *k] (transpose conv: [C_in, C_out/groups, *k]);
 ``data_format`` NCHW or NHWC. 2-D convolutions run on the own kernels in NHWC memory for both
-formats (``_own_conv2d``); what they do not take (fp32 dense, 1-D / 3-D, transposed) goes to
-MIOpen and is counted by ops/fallback.py.
+formats (``_own_conv2d``), fp32 ones included (a three-term bf16 split on the same MFMA kernels,
+ops/conv_gemm.py split3); 1-D convolutions run as height-1 2-D ones. What they do not take (3-D,
+some transposed / grouped forms) goes to MIOpen and is counted by ops/fallback.py (3-D: not counted).
 """
 from __future__ import annotations
 
@@ -78,6 +79,8 @@ def _hip_conv2d(x, w, bias, stride, pad, dilation, groups):
         cp = (c + 7) // 8 * 8
         x = TF.pad(x, [0, cp - c])
         w = TF.pad(w, [0, 0, 0, 0, 0, cp - c])
+    if x.dtype == torch.float32:   # fp32: three-term bf16 split on the same MFMA kernels
+        return conv_gemm.conv2d_nhwc256_f32(x, w, bias, stride, pad, dilation)
     if os.environ.get("PHA_CONV_KERNEL", "256") == "v1":
         return conv_gemm.conv2d_nhwc(x, w, bias, stride, pad, dilation)
     return conv_gemm.conv2d_nhwc256(x, w, bias, stride, pad, dilation)
@@ -90,7 +93,10 @@ def _hip_conv_ok(t_nhwc, w, groups):
     if os.environ.get("PHA_CONV_IMPL", "hip") != "hip":
         return False
     from ...ops import conv_gemm, _lib
-    return (t_nhwc.is_cuda and t_nhwc.dim() == 4 and t_nhwc.dtype in (torch.bfloat16, torch.float16)
+    # fp32 dense convs: the same kernels over a three-term bf16 split (conv_gemm.split3); PHA_CONV_F32=library
+    # keeps them on MIOpen
+    f32 = t_nhwc.dtype == torch.float32 and os.environ.get("PHA_CONV_F32", "hip") == "hip"
+    return (t_nhwc.is_cuda and t_nhwc.dim() == 4 and (t_nhwc.dtype in (torch.bfloat16, torch.float16) or f32)
             and w.dtype == t_nhwc.dtype and groups == 1 and w.shape[0] % 8 == 0 and _lib.require_native())
 
 
@@ -143,6 +149,30 @@ def nhwc_view(t):
     return v if v.is_contiguous() else None
 
 
+def _conv1d_as_2d(t, w, bias, stride, padding, dilation, groups, data_format):
+    """a 1-D convolution as the 2-D one over a height-1 image (the own kernels), or None"""
+    if data_format not in ("NCL", "NLC") or t.dim() != 3:
+        return None
+    if isinstance(padding, str):
+        pad2 = padding
+    else:
+        p = padding if isinstance(padding, (list, tuple)) else [padding]
+        p = [int(v) for v in p]
+        if len(p) == 1:
+            pad2 = [0, p[0]]
+        elif len(p) == 2:
+            pad2 = [0, 0, p[0], p[1]]
+        else:
+            return None
+    nchw = data_format == "NCL"
+    x4 = t.unsqueeze(2) if nchw else t.unsqueeze(1)
+    out = _own_conv2d(x4, w.unsqueeze(2), bias, [1, _tup(stride, 1)[0]], pad2, [1, _tup(dilation, 1)[0]], groups,
+                      "NCHW" if nchw else "NHWC")
+    if out is None:
+        return None
+    return out.squeeze(2) if nchw else out.squeeze(1)
+
+
 def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     t = x._t
     w = weight._t
@@ -150,9 +180,13 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
         out = _own_conv2d(t, w, None if bias is None else bias._t, stride, padding, dilation, groups, data_format)
         if out is not None:
             return _w(out)
-    if t.is_cuda and n == 2:
+    if n == 1 and t.is_cuda:
+        out = _conv1d_as_2d(t, w, None if bias is None else bias._t, stride, padding, dilation, groups, data_format)
+        if out is not None:
+            return _w(out)
+    if t.is_cuda and n in (1, 2):
         from ...ops import fallback
-        fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
+        fallback.note(f"conv{n}d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)
     stride = _tup(stride, n)
     dilation = _tup(dilation, n)
@@ -232,9 +266,9 @@ def _convnd_t(n, x, weight, bias, stride, padding, output_padding, groups, dilat
                             dilation, output_size, data_format)
         if out is not None:
             return _w(out)
-    if t.is_cuda and n == 2:
+    if t.is_cuda and n in (1, 2):
         from ...ops import fallback
-        fallback.note("conv2d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
+        fallback.note(f"conv{n}d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)
     stride = _tup(stride, n)
     dilation = _tup(dilation, n)

@@ -237,6 +237,8 @@ def _L256():
         L.pha_conv256_wgrad.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P]
         L.pha_conv256_wgrad.restype = c_int
         L.pha_conv256_fwd.restype = c_int
+        L.pha_conv256_fwd_f32out.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
+        L.pha_conv256_fwd_f32out.restype = c_int
         L._g256_sig = True
     return L
 
@@ -438,7 +440,7 @@ def conv256_fwd(x, w_okkc, stride, padding, dilation, bias=None, act=None, out=N
     return y
 
 
-def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend=None):
+def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend=None, f32=False):
     """dx [N, H, W, Ci] of an NHWC conv from dy [N, OH, OW, Co] and w [Co, Ci, KH, KW], on the forward
     kernel: stride 1 is the conv of dy with the flipped, transposed filter (pad' = d*(K-1) - p);
     stride s splits dx into s*s phases, each a stride-1 conv over the taps that reach it, stored
@@ -447,7 +449,9 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend
     ``bn_src = (bn_x, mean, affine|None, token)``: dx is the output gradient of that batch norm;
     its backward sums are reduced in the epilogue and attached as ``dx._pha_bn_bwd``.
     ``addend``: another gradient of x (the residual branch's), summed into dx — in the stride-1
-    epilogue, else by one add after the phases."""
+    epilogue, else by one add after the phases.
+    ``f32``: fp32 dy / w / dx through the three-term bf16 split (``split3``): dy's channels
+    [hi, hi, lo] against filters [hi, lo, hi] along Co, fp32 epilogue stores."""
     N, H, W, Ci = x_shape
     Co, _, KH, KW = w.shape
     sh, sw = stride
@@ -455,6 +459,8 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend
     dh, dw = dilation
     _, OH, OW, _ = dy.shape
     dy = dy.contiguous()
+    if f32:
+        return _dgrad_f32(dy, w, x_shape, stride, padding, dilation)
     assert addend is None or (tuple(addend.shape) == (N, H, W, Ci) and addend.dtype == dy.dtype), x_shape
     if addend is not None:
         addend = addend.contiguous()
@@ -515,6 +521,123 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend
 
 
 _wlayouts = {}
+
+
+# ----------------------------------------------------------------------------------------------
+# fp32 convolutions on the bf16 MFMA kernels: x = xh + xl, w = wh + wl (bf16 hi / lo parts), and
+# x.w ~= xh.wh + xh.wl + xl.wh — the lo.lo term is below fp32 rounding of most products (2^-16
+# relative). The three products are ONE implicit GEMM over concatenated channels [xh, xh, xl] x
+# [wh, wl, wh] with an fp32 epilogue, so Paddle's default-dtype convolutions run on the matrix
+# cores at ~5x the fp32 MFMA rate instead of on MIOpen (reference: phi/kernels/gpudnn/
+# conv_kernel.cu, cuDNN's fp32 / TF32 paths).
+# ----------------------------------------------------------------------------------------------
+def split3(t, dim, order="hhl"):
+    """fp32 t -> bf16 parts concatenated along ``dim`` in ``order`` (h = hi, l = lo)"""
+    hi = t.to(torch.bfloat16)
+    lo = (t - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi if c == "h" else lo for c in order], dim)
+
+
+def conv256_fwd_f32(x3, w3, stride, padding, dilation, bias=None, act=None, out=None, remap=None):
+    """NHWC conv with an fp32 output from pre-split bf16 operands: x3 [N, H, W, 3C] ([hi, hi, lo]),
+    w3 [Co, KH, KW, 3C] ([hi, lo, hi])"""
+    assert x3.dtype == torch.bfloat16 and w3.dtype == x3.dtype and x3.is_contiguous() and w3.is_contiguous()
+    N, H, W, C = x3.shape
+    Co, KH, KW, Cw = w3.shape
+    assert C == Cw and C % 8 == 0
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    rm = None
+    if remap is not None:
+        assert out is not None and out.is_contiguous() and out.dtype == torch.float32
+        oh0, ow0, osh, osw, OH, OW = remap[:6]
+        zr = int(len(remap) > 6 and bool(remap[6]))
+        rm = (c_int * 9)(out.shape[1], out.shape[2], oh0, ow0, osh, osw, OH, OW, zr)
+        y = out
+    else:
+        OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+        OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+        y = out if out is not None else torch.empty((N, OH, OW, Co), dtype=torch.float32, device=x3.device)
+        assert y.shape == (N, OH, OW, Co) and y.is_contiguous() and y.dtype == torch.float32
+    if bias is not None:
+        bias = bias.float().contiguous()
+    L, z, st = _L256(), _ptr(_zero_page(x3.device)), c_void_p(torch.cuda.current_stream(x3.device).cuda_stream)
+    rc = L.pha_conv256_fwd_f32out(_DT[x3.dtype], _ptr(x3), _ptr(w3), _ptr(y), _ptr(bias), N, H, W, C, Co, KH, KW,
+                                  sh, sw, ph, pw, dh, dw, _ACT[act], z, -1, 0, rm, st)
+    if rc != 0:
+        raise RuntimeError(f"pha_conv256_fwd_f32out failed ({rc})")
+    return y
+
+
+def _dgrad_f32(dy, w, x_shape, stride, padding, dilation):
+    """fp32 dx of an NHWC conv (see conv256_dgrad): dy split along Co as [hi, hi, lo], the dgrad
+    filter layouts (Co last) split as [hi, lo, hi]"""
+    N, H, W, Ci = x_shape
+    Co, _, KH, KW = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    dy3 = split3(dy, 3, "hhl")
+    if (sh, sw) == (1, 1):
+        wt = _wlayout(w, "dgrad_f32", lambda t: split3(t.flip(2, 3).permute(1, 2, 3, 0).contiguous(), 3, "hlh"))
+        dx = torch.empty(N, H, W, Ci, dtype=torch.float32, device=dy.device)
+        return conv256_fwd_f32(dy3, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
+                               remap=(0, 0, 1, 1, H, W))
+    if (dh, dw) != (1, 1):
+        raise NotImplementedError("strided + dilated conv dgrad")
+    phases = []
+    for rh in range(sh):
+        for rw in range(sw):
+            PH, PW = len(range(rh, H, sh)), len(range(rw, W, sw))
+            kh0, kw0 = (rh + ph) % sh, (rw + pw) % sw
+            khs, kws = list(range(kh0, KH, sh)), list(range(kw0, KW, sw))
+            phases.append((rh, rw, PH, PW, khs, kws, kh0, kw0))
+    live = [p for p in phases if p[2] and p[3] and p[4] and p[5]]
+    zero_rest = len(live) == 1 and live[0][:2] == (0, 0) and live[0][2] * sh >= H and live[0][3] * sw >= W
+    full = len(live) == len(phases) or zero_rest
+    dx = (torch.empty if full else torch.zeros)(N, H, W, Ci, dtype=torch.float32, device=dy.device)
+    for rh, rw, PH, PW, khs, kws, kh0, kw0 in live:
+        bh, bw = (rh + ph - kh0) // sh, (rw + pw - kw0) // sw
+        nh, nw = len(khs), len(kws)
+        wt = _wlayout(w, ("phase_f32", rh, rw, sh, sw, ph, pw), lambda t, kh0=kh0, kw0=kw0: split3(
+            t[:, :, kh0::sh, :][:, :, :, kw0::sw].flip((2, 3)).permute(1, 2, 3, 0).contiguous(), 3, "hlh"))
+        conv256_fwd_f32(dy3, wt, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
+                        remap=(rh, rw, sh, sw, PH, PW, zero_rest))
+    return dx
+
+
+class Conv2dNHWC256F32(torch.autograd.Function):
+    """fp32 NHWC conv2d: forward, dgrad and wgrad as three-term bf16 MFMA products (split3)"""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation):
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        ctx.conf = (stride, padding, dilation, bias is not None)
+        w3 = _wlayout(weight, "fwd_f32", lambda t: split3(t.permute(0, 2, 3, 1).contiguous(), 3, "hlh"))
+        return conv256_fwd_f32(split3(x.contiguous(), 3, "hhl"), w3, stride, padding, dilation, bias=bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        weight = ctx.weight
+        stride, padding, dilation, has_bias = ctx.conf
+        gy = gy.contiguous().float()
+        dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation, f32=True) \
+            if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            # the reduction runs over pixels: stack the split along the batch ([dy_h; dy_h; dy_l] x
+            # [x_h; x_l; x_h]) and let the weight-gradient GEMM sum the three terms in fp32
+            dw = conv256_wgrad(split3(gy, 0, "hhl"), split3(x.contiguous(), 0, "hlh"), weight.shape, stride, padding,
+                               dilation, out_dtype=torch.float32)
+        db = gy.sum((0, 1, 2)) if has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+def conv2d_nhwc256_f32(x, weight, bias, stride, padding, dilation):
+    return Conv2dNHWC256F32.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))
 
 
 def _wlayout(w, kind, make):

@@ -444,6 +444,46 @@ class _TN(torch.autograd.Function):
                 mm_nn(at, g) if ctx.needs_input_grad[1] else None)
 
 
+class _F32MM(torch.autograd.Function):
+    """fp32 C = A [M, K] @ B [K, N] on the bf16 MFMA kernels: A = Ah + Al, B = Bh + Bl and
+    A B ~= Ah Bh + Ah Bl + Al Bh as ONE K-outer product over 3K ([Ah; Ah; Al]^T [Bh; Bl; Bh]) with
+    fp32 split-K partials (gemm256_tn); dA = dC B^T and dB = A^T dC the same way. The dropped
+    Al Bl term is ~2^-16 of each product: near-fp32 results at the bf16 matrix rate."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return mm_f32(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.float()
+        return (mm_f32(g, b.t()) if ctx.needs_input_grad[0] else None,
+                mm_f32(a.t(), g) if ctx.needs_input_grad[1] else None)
+
+
+def mm_f32(a, b):
+    """fp32 a [M, K] @ b [K, N] (any strides) as a three-term bf16 product, fp32 out"""
+    from .conv_gemm import split3, gemm256_tn
+    M, K = a.shape
+    N = b.shape[1]
+    at3 = split3(a.t(), 0, "hhl")        # [3K, M]
+    b3 = split3(b, 0, "hlh")             # [3K, N]
+    pm, pn = -M % 8, -N % 8
+    if pm:
+        at3 = torch.nn.functional.pad(at3, [0, pm])
+    if pn:
+        b3 = torch.nn.functional.pad(b3, [0, pn])
+    out = gemm256_tn(at3.contiguous(), b3.contiguous(), out_dtype=torch.float32)
+    return out[:M, :N] if (pm or pn) else out
+
+
+def _f32_ok(a, b):
+    return (a.is_cuda and b.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
+            and os.environ.get("PHA_MATMUL_F32", "hip") == "hip" and _lib.native_available())
+
+
 def _gemm_dtype_ok(a, b):
     return (a.is_cuda and b.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype
             and type(a).__name__ != "DTensor" and type(b).__name__ != "DTensor" and _lib.native_available())
@@ -464,6 +504,12 @@ def matmul(a, b, transpose_a=False, transpose_b=False):
         lead = a.shape[:-1]
         a2 = _c(a.reshape(-1, a.shape[-1]))
         out = _NT.apply(a2, _c(b)) if transpose_b else _NN.apply(a2, _c(b))
+        return out.reshape(*lead, out.shape[-1])
+    if _f32_ok(a, b) and a.dim() >= 2 and b.dim() == 2 and (a.dim() == 2 or not transpose_a):
+        x = a.transpose(-1, -2) if transpose_a else a
+        y = b.transpose(-1, -2) if transpose_b else b
+        lead = x.shape[:-1]
+        out = _F32MM.apply(x.reshape(-1, x.shape[-1]), y)
         return out.reshape(*lead, out.shape[-1])
     from . import fallback
     why = (f"{a.dtype} product" if not _gemm_dtype_ok(a, b) else

@@ -1,0 +1,113 @@
+"""fp32 (Paddle's default dtype) convolutions and matmuls on the own MFMA kernels through the
+three-term bf16 split (ops/conv_gemm.py split3, ops/gemm.py mm_f32; reference: the cuDNN / cuBLAS
+fp32 kernels behind phi/kernels/gpudnn/conv_kernel.cu and matmul_kernel_impl.h). Oracle: fp64 torch
+of the same op; the split keeps ~2^-16 relative error per product, fp32 accumulation."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("cfg", [
+    # N, C, H, W, Co, k, stride, pad
+    (2, 16, 14, 14, 32, 3, 1, 1),
+    (2, 32, 15, 15, 16, 3, 2, 1),
+    (2, 64, 8, 8, 64, 1, 2, 0),
+    (2, 3, 32, 32, 24, 7, 2, 3),      # RGB stem: channels padded to 8
+    (1, 8, 9, 9, 12, 3, 1, 1),        # Cout % 8 != 0
+])
+@pytest.mark.parametrize("fmt", ["NCHW", "NHWC"])
+def test_fp32_conv2d_own_kernels(cfg, fmt):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    N, C, H, W, Co, k, s, p = cfg
+    paddle.set_device("gpu")
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda")
+    w = torch.randn(Co, C, k, k, device="cuda") * (2.0 / (C * k * k)) ** 0.5
+    b = torch.randn(Co, device="cuda")
+    xin = x.permute(0, 2, 3, 1).contiguous() if fmt == "NHWC" else x
+    px, pw, pb = paddle.to_tensor(xin), paddle.to_tensor(w), paddle.to_tensor(b)
+    for t in (px, pw, pb):
+        t.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.conv2d(px, pw, pb, stride=s, padding=p, data_format=fmt)
+    gy = torch.randn(tuple(y.shape), device="cuda")
+    y.backward(paddle.to_tensor(gy))
+    torch.cuda.synchronize()
+    assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
+    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    ref = torch.nn.functional.conv2d(xd, wd, bd, stride=s, padding=p)
+    gref = gy.double().permute(0, 3, 1, 2) if fmt == "NHWC" else gy.double()
+    ref.backward(gref)
+    out = y._t.permute(0, 3, 1, 2) if fmt == "NHWC" else y._t
+    assert y._t.dtype == torch.float32
+    assert _rel(out, ref) < 2e-5
+    gx = px.grad._t.permute(0, 3, 1, 2) if fmt == "NHWC" else px.grad._t
+    assert _rel(gx, xd.grad) < 2e-5
+    assert _rel(pw.grad._t, wd.grad) < 2e-5
+    assert _rel(pb.grad._t, bd.grad) < 1e-5
+
+
+def test_fp32_conv1d_runs_as_2d():
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    paddle.set_device("gpu")
+    torch.manual_seed(1)
+    x = torch.randn(4, 16, 50, device="cuda")
+    w = torch.randn(24, 16, 5, device="cuda") * 0.1
+    fallback.reset()
+    y = paddle.nn.functional.conv1d(paddle.to_tensor(x), paddle.to_tensor(w), padding=2, stride=2)
+    assert fallback.total() == 0, fallback.counts()
+    ref = torch.nn.functional.conv1d(x.double(), w.double(), padding=2, stride=2)
+    assert _rel(y._t, ref) < 2e-5
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 512, 384), (100, 72, 40), (7, 300, 5)])
+def test_fp32_matmul_and_linear(M, K, N):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    paddle.set_device("gpu")
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device="cuda")
+    b = torch.randn(K, N, device="cuda")
+    bias = torch.randn(N, device="cuda")
+    pa, pb, pbias = paddle.to_tensor(a), paddle.to_tensor(b), paddle.to_tensor(bias)
+    pa.stop_gradient = pb.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.linear(pa, pb, pbias)
+    g = torch.randn(M, N, device="cuda")
+    y.backward(paddle.to_tensor(g))
+    torch.cuda.synchronize()
+    assert fallback.total() == 0 and not fallback.library_counts(), (fallback.counts(), fallback.library_counts())
+    ad, bd = a.double().requires_grad_(), b.double().requires_grad_()
+    ref = ad @ bd + bias.double()
+    ref.backward(g.double())
+    assert _rel(y._t, ref) < 2e-5
+    assert _rel(pa.grad._t, ad.grad) < 2e-5
+    assert _rel(pb.grad._t, bd.grad) < 2e-5
+    z = paddle.matmul(pa, paddle.to_tensor(b.t().contiguous()), transpose_y=True)
+    assert _rel(z._t, (a.double() @ b.double())) < 2e-5
+
+
+def test_fp32_resnet_block_no_miopen():
+    """an fp32 ResNet bottleneck (conv / BN / ReLU / residual) forward + backward without a library
+    convolution"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    from paddle_hackathon_amd.vision.models.resnet import BottleneckBlock
+    paddle.set_device("gpu")
+    paddle.seed(0)
+    blk = BottleneckBlock(64, 16, stride=1)
+    x = paddle.randn([4, 64, 16, 16])
+    x.stop_gradient = False
+    fallback.reset()
+    y = blk(x)
+    y.sum().backward()
+    torch.cuda.synchronize()
+    assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
+    assert y._t.dtype == torch.float32 and torch.isfinite(x.grad._t).all()

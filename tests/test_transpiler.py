@@ -68,7 +68,7 @@ _JOB = textwrap.dedent('''
         mine = slice(idx * 16, idx * 16 + 16)
         l, = exe.run(prog, feed={{"x": xb[mine], "y": yb[mine]}}, fetch_list=[loss])
         losses.append(float(np.asarray(l).ravel()[0]))
-    params = {{p.name: p.numpy().tolist() for p in main.all_parameters()}}
+    params = [p.numpy().tolist() for p in main.all_parameters()]   # creation order (names are per-process)
     exe.close()
     json.dump({{"losses": losses, "params": params, "blocks": [repr(b) for b in t.blocks],
                "types": [op.type for op in prog.global_block().ops]}}, open(out, "w"))
@@ -94,7 +94,7 @@ def _local_reference(n_steps):
         exe.run(start)
         for xb, yb in ns["batches"](n_steps):
             exe.run(main, feed={"x": xb, "y": yb}, fetch_list=[loss])
-        return {p.name: p.numpy() for p in main.all_parameters()}
+        return [p.numpy() for p in main.all_parameters()]
     finally:
         paddle.disable_static()
 
@@ -147,9 +147,10 @@ def test_transpiled_pserver_training_equals_full_batch(tmp_path):
     assert sum("block1" in b for b in res[0]["blocks"]) == 1      # the 16x64 weight is cut in two
     assert res[0]["losses"][-1] < res[0]["losses"][0]
     ref = _local_reference(12)
-    for name, v in ref.items():
+    assert len(ref) == len(res[0]["params"]) == 4
+    for i, v in enumerate(ref):
         for r in res:
-            np.testing.assert_allclose(np.asarray(r["params"][name]).reshape(v.shape), v, rtol=2e-4, atol=2e-5)
+            np.testing.assert_allclose(np.asarray(r["params"][i]).reshape(v.shape), v, rtol=2e-4, atol=2e-5)
 
 
 def test_pserver_program_structure():
