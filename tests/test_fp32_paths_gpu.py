@@ -40,7 +40,7 @@ def test_fp32_conv2d_own_kernels(cfg, fmt):
     y.backward(paddle.to_tensor(gy))
     torch.cuda.synchronize()
     assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
-    xd, wd, bd = (t.double().requires_grad_() for t in (x, w, b))
+    xd, wd, bd = (t.detach().double().requires_grad_() for t in (x, w, b))
     ref = torch.nn.functional.conv2d(xd, wd, bd, stride=s, padding=p)
     gref = gy.double().permute(0, 3, 1, 2) if fmt == "NHWC" else gy.double()
     ref.backward(gref)
@@ -84,14 +84,14 @@ def test_fp32_matmul_and_linear(M, K, N):
     y.backward(paddle.to_tensor(g))
     torch.cuda.synchronize()
     assert fallback.total() == 0 and not fallback.library_counts(), (fallback.counts(), fallback.library_counts())
-    ad, bd = a.double().requires_grad_(), b.double().requires_grad_()
+    ad, bd = a.detach().double().requires_grad_(), b.detach().double().requires_grad_()
     ref = ad @ bd + bias.double()
     ref.backward(g.double())
     assert _rel(y._t, ref) < 2e-5
     assert _rel(pa.grad._t, ad.grad) < 2e-5
     assert _rel(pb.grad._t, bd.grad) < 2e-5
     z = paddle.matmul(pa, paddle.to_tensor(b.t().contiguous()), transpose_y=True)
-    assert _rel(z._t, (a.double() @ b.double())) < 2e-5
+    assert _rel(z._t, (a.detach().double() @ b.detach().double())) < 2e-5
 
 
 def test_fp32_resnet_block_no_miopen():
