@@ -53,6 +53,14 @@ template <> __device__ __forceinline__ float round_to<half_t>(float v) { return 
 // ---- 8-wide vector load/store (16 B for 2-byte types, 2x16 B for fp32) -----------
 template <typename T> struct Vec8;
 template <> struct Vec8<bf16_t> {
+  static __device__ __forceinline__ void unpack(const uint4& r, float (&o)[8]) {
+    uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = __uint_as_float(w[i] << 16);
+      o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
   static __device__ __forceinline__ void ld(const bf16_t* p, float (&o)[8]) {
     uint4 r = *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {r.x, r.y, r.z, r.w};
@@ -72,6 +80,11 @@ template <> struct Vec8<bf16_t> {
 };
 template <> struct Vec8<half_t> {
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ void unpack(const uint4& r, float (&o)[8]) {
+    const h8 v = __builtin_bit_cast(h8, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
   static __device__ __forceinline__ void ld(const half_t* p, float (&o)[8]) {
     h8 r = *reinterpret_cast<const h8*>(p);
 #pragma unroll

@@ -110,10 +110,29 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 }
 
 // dx per row + per-block partial column sums of dy*xhat (dw) and dy (db).
+// 8 elements held as their raw vector(s) (16 B for bf16 / fp16, 32 B for fp32), unpacked on use
+template <typename T>
+struct Raw8 {
+  uint4 v;
+  __device__ __forceinline__ void ld(const T* p) { v = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void unpack(float (&o)[8]) const { Vec8<T>::unpack(v, o); }
+};
+template <>
+struct Raw8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void ld(const float* p) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void unpack(float (&o)[8]) const {
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  }
+};
+
 // BW waves per block (16 -> 1024 threads): a grid of one block per CU then still gives 4
 // waves per SIMD to hide HBM latency, while the dw/db partials stay one [H] row per block.
 template <typename T, typename W, int NCH, int BW>
-__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 4 ? 4 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+__global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 4 : NCH <= 4 ? 2 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const W* __restrict__ w, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, T* __restrict__ dx,
                                                          float* __restrict__ part_w, float* __restrict__ part_b,
@@ -126,6 +145,71 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
 #pragma unroll
     for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; }
 
+  // H = 1537..2048 (NCH 4, the GPT-1.3B width): one HBM round trip per row with x / dy / dres held
+  // raw in registers (2 waves per SIMD, no spills); other widths re-read x and dy in pass 2
+  if constexpr (NCH == 4) {
+  for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
+    const float mu = mean[row], rs = rstd[row];
+    const T* xr = x + (long)row * H;
+    const T* gr = dy + (long)row * H;
+    // one HBM round trip per row: x, dy (and the residual gradient) are loaded once, kept as raw
+    // 16-B vectors and unpacked again for pass 2 (no second read, no dependent dres load)
+    Raw8<T> rx[NCH], rg[NCH], rr[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        rx[c].ld(xr + col);
+        rg[c].ld(gr + col);
+        if (dres) rr[c].ld(dres + (long)row * H + col);
+      }
+    }
+    // pass 1: row statistics of g = dy*w
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        float xv[8], gv[8], wv[8];
+        rx[c].unpack(xv);
+        rg[c].unpack(gv);
+        Vec8<W>::ld(w + col, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float g = gv[i] * wv[i];
+          s1 += g * (xv[i] - mu) * rs;
+          s2 += g;
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / H, c2 = wave_sum(s2) / H;
+    T* dr = dx + (long)row * H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (col < H) {
+        float xv[8], gv[8], wv[8], o[8];
+        rx[c].unpack(xv);
+        rg[c].unpack(gv);
+        Vec8<W>::ld(w + col, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xh = (xv[i] - mu) * rs;
+          o[i] = rs * (gv[i] * wv[i] - xh * c1 - c2);
+          aw[c][i] += gv[i] * xh;
+          ab[c][i] += gv[i];
+        }
+        if (dres) {  // fused residual branch: dx += d(sum output)
+          float rv[8];
+          rr[c].unpack(rv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += rv[i];
+        }
+        Vec8<T>::st(dr + col, o);
+      }
+    }
+  }
+  } else {
   for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
     const float mu = mean[row], rs = rstd[row];
     const T* xr = x + (long)row * H;
@@ -175,6 +259,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
         Vec8<T>::st(dr + col, o);
       }
     }
+  }
   }
   // block reduction of the BW waves' partial column sums through LDS, one column chunk at a time
   __shared__ float red[BW][512];
