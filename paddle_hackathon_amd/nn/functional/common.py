@@ -25,21 +25,31 @@ def _t(x):
 
 
 class _LinearBias(torch.autograd.Function):
-    """addmm (hipBLASLt, bias in the epilogue) whose bias gradient is the HIP column-sum kernel
-    instead of a generic reduction; dx / dW stay on hipBLASLt."""
+    """x @ W + b on the own GEMM layouts (ops/gemm.py: NN forward, NT dX, TN dW with the bias
+    gradient reduced in the same TN pass); products the own kernels cannot take are counted
+    library calls there"""
 
     @staticmethod
     def forward(ctx, x2d, w, b):
+        from ...ops import gemm as _gemm
         ctx.save_for_backward(x2d, w)
-        return torch.addmm(b, x2d, w)
+        out = _gemm.mm_nn(x2d.contiguous(), w)
+        return out.add_(b)
 
     @staticmethod
     def backward(ctx, gy):
+        from ...ops import gemm as _gemm
+        from ...ops.conv_gemm import weight_grad
         x2d, w = ctx.saved_tensors
         gy = gy.contiguous()
-        dx = gy.mm(w.t()) if ctx.needs_input_grad[0] else None
-        dw = x2d.t().mm(gy) if ctx.needs_input_grad[1] else None
-        db = _ops.hip.col_sum(gy) if ctx.needs_input_grad[2] else None
+        dx = _gemm.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            dw, db = weight_grad(x2d.contiguous(), gy, bias_dtype=gy.dtype)
+        elif ctx.needs_input_grad[1]:
+            dw = weight_grad(x2d.contiguous(), gy)
+        elif ctx.needs_input_grad[2]:
+            db = _ops.hip.col_sum(gy)
         return dx, dw, db
 
 
