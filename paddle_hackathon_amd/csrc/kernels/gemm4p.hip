@@ -63,9 +63,6 @@ struct Args {
   float* ws;    // split-K: fp32 partial slabs [splits][M][N] (C unused)
   int splits;
   void* aux;    // EPI_GELU: pre-activation output, same shape and row stride as C
-  // TN only (CS build): column sums of B over the work item's K range, fp32 [splits][N] — the
-  // bias gradient of a linear layer (B = dY) from the weight-gradient GEMM that streams dY anyway
-  float* colsum;
 };
 
 constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
@@ -154,20 +151,8 @@ struct Sched {
 // SPLIT: the K range of every tile is cut into p.splits slices (separate work items, for problems
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
-// bf16 / fp16 pair (one dword) summed into c: v_dot2 against (1, 1)
-template <typename T>
-__device__ __forceinline__ float pair_sum(unsigned w, float c) {
-  if constexpr (std::is_same<T, bf16_t>::value) {
-    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, w), __builtin_bit_cast(bf2, 0x3F803F80u), c, false);
-  } else {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, w), __builtin_bit_cast(h2, 0x3C003C00u), c, false);
-  }
-}
-
 template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
-          bool GELU = false, bool RS = false, bool EARLY = false, bool CS = false>
+          bool GELU = false, bool RS = false, bool EARLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -427,51 +412,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f4{v[0], v[1], v[2], v[3]}), rs, voff + cb * 64, 0, 2);
   };
 
-  // CS: per-lane partial column sums of the B fragments the MFMAs consume (the fragment of B
-  // column block j holds column j*16 + fr over k chunk fk); reduced over the 4 k chunks and stored
-  // by the wr == 0 waves of row-tile 0 when the tile ends
-  static_assert(!CS || (AKO && BKO && !OT), "column sums: TN layout only");
-  float csum[CS ? 8 : 1];
-  float* cs_ptr = nullptr;
-  int cs_c0 = 0;
-  bool cs_on = false;
-#pragma unroll
-  for (int j = 0; j < (CS ? 8 : 1); ++j) csum[j] = 0.f;
-  auto cs_flush = [&]() {
-    if constexpr (CS) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = csum[j];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        csum[j] = 0.f;
-        const int col = cs_c0 + wc * 128 + j * 16 + fr;
-        if (cs_on && wr == 0 && fk == 0 && col < N) cs_ptr[col] = v;
-      }
-    }
-  };
-  auto cs_set = [&](int r) {   // the tile whose first k-half the next phase multiplies
-    if constexpr (CS) {
-      int tm, tn, slice;
-      sc.tile(r, tm, tn, slice);
-      cs_on = tm == 0;
-      cs_c0 = tn << 8;
-      cs_ptr = p.colsum + (size_t)slice * N;
-    }
-  };
-  auto cs_acc = [&](const uint4 (&cb)[8], int s) {   // 2 of the 32 pair sums of a phase per MFMA group
-    if constexpr (CS) {
-      const uint4 f = cb[s >> 1];
-      if (s & 1) {
-        csum[s >> 1] = pair_sum<T>(f.z, csum[s >> 1]);
-        csum[s >> 1] = pair_sum<T>(f.w, csum[s >> 1]);
-      } else {
-        csum[s >> 1] = pair_sum<T>(f.x, csum[s >> 1]);
-        csum[s >> 1] = pair_sum<T>(f.y, csum[s >> 1]);
-      }
-    }
-  };
-
   f32x4 acc[8][8];
   uint4 fa0[8], fb0[8], fa1[8], fb1[8];
   constexpr int SCHED = AKO ? 0 : 2;   // read placement, as gemm4w's per-layout winners
@@ -512,7 +452,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       } else if constexpr (ST) {
         stage_one(s);
       }
-      cs_acc(cb, s);
       const int i = s >> 1, jb = (s & 1) * 4;
       if constexpr (MODE == 2 && SPLIT) {
 #pragma unroll
@@ -594,7 +533,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         if (s < RELG) stage_one(16 - RELG + s);
       }
-      cs_acc(cb, s);
       const int i = s >> 1, jb = (s & 1) * 4;
       if constexpr (MODE == 2 && SPLIT) {
 #pragma unroll
@@ -665,8 +603,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int r = 0; sc.valid(r); ++r) {
       {
         const int buf = s & 1;
-        cs_flush();
-        cs_set(r);
         phaseE(M2{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(VB2) : "memory");
         __builtin_amdgcn_sched_barrier(0);
@@ -694,8 +630,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int r = 0; sc.valid(r); ++r) {
     {   // K-tile 0 of tile r: the previous tile is written out under its k-half-0 MFMAs
       const int buf = s & 1;
-      cs_flush();
-      cs_set(r);
       if constexpr (SKIPEPI) phase(yes{}, M1{}, M0{}, fa0, fb0, fa1, fb1, buf, 1);
       else phase(yes{}, M2{}, M0{}, fa0, fb0, fa1, fb1, buf, 1);
       static_assert(NST == 32, "vmcnt literal");
@@ -729,7 +663,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // last tile: stores only (after the cursor's trailing DMAs have landed)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  cs_flush();
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -773,13 +706,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 template <typename T, bool BIAS, bool E>
 int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
-  if (a.colsum && !(ako && bko && !trans)) return (int)hipErrorInvalidValue;
   if (a.splits > 1) {   // TN only (weight gradients)
     if (!(ako && bko && !trans)) return (int)hipErrorInvalidValue;
-    if (a.colsum)
-      hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E, true>), dim3(grid), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E>), dim3(grid), dim3(256), 0, st, a);
     const long elems = (long)a.M * a.N;
     hipLaunchKernelGGL((splitk_reduce_kernel<T, BIAS>), dim3((unsigned)((elems / 8 + 255) / 256)), dim3(256), 0, st,
                        a.ws, static_cast<T*>(a.c), a.bias, a.M, a.N, a.ldc, a.splits);
@@ -802,8 +731,6 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
     return (int)hipErrorInvalidValue;
   else if (!ako && !bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
-  else if (ako && bko && !trans && a.colsum)
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, true>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && !bko && trans)
@@ -829,9 +756,9 @@ using namespace pha;
 // transposed store (C is then [N][ldc]). Requires K % 64 == 0; M, N, lda, ldb, ldc % 8 == 0; 16-B
 // aligned base pointers; K-outer operand dims >= 8; per-panel byte offsets < 2^32; 256 output rows
 // x ldc x 2 bytes < 2^31. grid: workgroups (<= tiles; the caller passes the CU count).
-static int gemm4p_impl(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
+PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
                        long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
-                       int group_m, float* ws, int splits, hipStream_t stream, void* aux, float* colsum) {
+                       int group_m, float* ws, int splits, hipStream_t stream, void* aux) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8)
     return (int)hipErrorInvalidValue;
   if ((a_kouter && M < 8) || (b_kouter && N < 8)) return (int)hipErrorInvalidValue;
@@ -849,30 +776,11 @@ static int gemm4p_impl(int dt, const void* a, const void* b, void* c, long M, lo
   const long tiles = ((M + 255) / 256) * ((N + 255) / 256) * splits;
   if (grid <= 0 || grid > tiles) grid = (int)tiles;
   if (group_m <= 0) group_m = 4;
-  if (colsum && (!a_kouter || !b_kouter || trans || ((size_t)colsum & 3))) return (int)hipErrorInvalidValue;
-  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits, aux,
-              colsum};
+  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits, aux};
   const bool bs = epi & g4p::EPI_BIAS;
   if (dt == kBF16) return bs ? g4p::launch<bf16_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                              : g4p::launch<bf16_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
   if (dt == kF16) return bs ? g4p::launch<half_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                             : g4p::launch<half_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
   return (int)hipErrorInvalidValue;
-}
-
-PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
-                       long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
-                       int group_m, float* ws, int splits, hipStream_t stream, void* aux) {
-  return gemm4p_impl(dt, a, b, c, M, N, K, lda, ldb, ldc, a_kouter, b_kouter, trans, epi, bias, grid, group_m, ws,
-                     splits, stream, aux, nullptr);
-}
-
-// TN weight gradient that also writes colsum[s][n] = sum over work item s's K range of B[k][n]
-// (fp32, [splits][N]; summed over s by the caller): a linear layer's bias gradient for free
-PHA_API int pha_gemm4p_colsum(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda,
-                              long ldb, long ldc, int epi, int grid, int group_m, float* ws, int splits,
-                              float* colsum, hipStream_t stream) {
-  if (!colsum) return (int)hipErrorInvalidValue;
-  return gemm4p_impl(dt, a, b, c, M, N, K, lda, ldb, ldc, 1, 1, 0, epi, nullptr, grid, group_m, ws, splits, stream,
-                     nullptr, colsum);
 }

@@ -25,8 +25,8 @@ def _t(x):
 
 
 class _LinearBias(torch.autograd.Function):
-    """x @ W + b on the own GEMM layouts (ops/gemm.py: NN forward, NT dX, TN dW with the bias
-    gradient reduced in the same TN pass); products the own kernels cannot take are counted
+    """x @ W + b on the own GEMM layouts (ops/gemm.py: NN forward, NT dX, TN dW) with the bias
+    gradient from the HIP column-sum kernel; products the own kernels cannot take are counted
     library calls there"""
 
     @staticmethod
@@ -43,13 +43,8 @@ class _LinearBias(torch.autograd.Function):
         x2d, w = ctx.saved_tensors
         gy = gy.contiguous()
         dx = _gemm.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
-        dw = db = None
-        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
-            dw, db = weight_grad(x2d.contiguous(), gy, bias_dtype=gy.dtype)
-        elif ctx.needs_input_grad[1]:
-            dw = weight_grad(x2d.contiguous(), gy)
-        elif ctx.needs_input_grad[2]:
-            db = _ops.hip.col_sum(gy)
+        dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
+        db = _ops.hip.col_sum(gy) if ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

@@ -1025,15 +1025,11 @@ def nt_forward_ok(x, w):
             and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype)
 
 
-def weight_grad(x2d, gy, bias_dtype=None):
+def weight_grad(x2d, gy):
     """dW = x^T @ dY for a linear layer ([in, out]) on the own persistent TN kernel (split-K
-    when the [in, out] tile grid is smaller than the chip) — ops/gemm.py mm_tn. With
-    ``bias_dtype``: returns (dW, db), db = column sums of dY reduced by the same GEMM pass"""
+    when the [in, out] tile grid is smaller than the chip) — ops/gemm.py mm_tn"""
     from . import gemm as _g4
-    if bias_dtype is None:
-        return _g4.mm_tn(x2d, gy)
-    dw, cs = _g4.mm_tn(x2d, gy, colsum=True)
-    return dw, cs.to(bias_dtype)
+    return _g4.mm_tn(x2d, gy)
 
 
 class LinearNT(torch.autograd.Function):
@@ -1056,13 +1052,8 @@ class LinearNT(torch.autograd.Function):
         gy = gy.contiguous()
         from . import gemm as _g4
         dx = _g4.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
-        dw = db = None
-        want_db = ctx.has_b and ctx.needs_input_grad[2]
-        if ctx.needs_input_grad[1] and want_db:   # db from the weight-gradient pass over dY
-            dw, db = weight_grad(x2d.contiguous(), gy, bias_dtype=w.dtype)
-        else:
-            dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
-            db = hip.col_sum(gy) if want_db else None
+        dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
+        db = hip.col_sum(gy) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

@@ -42,8 +42,6 @@ def _L():
         L.pha_gemm4p.restype = c_int
         L.pha_gemm8w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, P]
         L.pha_gemm8w.restype = c_int
-        L.pha_gemm4p_colsum.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, P, I, P, P]
-        L.pha_gemm4p_colsum.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
         L.pha_colsum_finish.restype = c_int
         L._g4w_sig = True
@@ -377,46 +375,18 @@ def mm_nn(a, b):
     return _lib_call("nn", "nn", (M, N, K), lambda: a @ b)
 
 
-def gemm_p_colsum(a, b, splits=1, grid=0, group_m=0):
-    """TN C = a [K, M]^T @ b [K, N] on gemm4p plus the column sums of b over K (fp32 [N]) from the
-    same pass: the B fragments the MFMAs consume are summed with v_dot2 against (1, 1) and stored
-    by row-tile 0 (csrc/kernels/gemm4p.hip CS build) — a linear layer's bias gradient without a
-    separate read of dY"""
-    assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
-    assert a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] == b.shape[0]
-    K, M = a.shape
-    N = b.shape[1]
-    c = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    cs = torch.empty(splits, N, dtype=torch.float32, device=a.device)
-    ws = torch.empty(splits * M * N, dtype=torch.float32, device=a.device) if splits > 1 else None
-    epi = _epi_default(True, True, False, K)
-    rc = _L().pha_gemm4p_colsum(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, K, a.stride(0), b.stride(0),
-                                c.stride(0), epi, grid or _num_cus(a.device), group_m, _ptr(ws), splits, _ptr(cs),
-                                _stream(a))
-    if rc != 0:
-        raise RuntimeError(f"pha_gemm4p_colsum failed ({rc}) M={M} N={N} K={K} splits={splits}")
-    return c, (cs[0] if splits == 1 else cs.sum(0))
-
-
-def mm_tn(a, b, colsum=False):
-    """a [K, M]^T @ b [K, N] (weight gradients: x^T dY), split-K when the tile grid is small.
-    ``colsum``: also return the fp32 column sums of b (the bias gradient), fused on the own kernel"""
+def mm_tn(a, b):
+    """a [K, M]^T @ b [K, N] (weight gradients: x^T dY), split-K when the tile grid is small"""
     K, M = a.shape
     N = b.shape[1]
     if _own_ok("tn", a, b) and b.dtype == a.dtype:
         a, b = _c(a), _c(b)
         if supported(M, N, K, a, b):
-            sp = _splits(M, N, K, a.device)
-            return gemm_p_colsum(a, b, splits=sp) if colsum else gemm_p(a, b, True, True, splits=sp)
+            return gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device))
         if _own_fits(a) and _own_fits(b):
             ap, bp = _pad2(a, 64, 8), _pad2(b, 64, 8)
-            sp = _splits(ap.shape[1], bp.shape[1], ap.shape[0], a.device)
-            if colsum:
-                c, cs = gemm_p_colsum(ap, bp, splits=sp)
-                return c[:M, :N], cs[:N]
-            return gemm_p(ap, bp, True, True, splits=sp)[:M, :N]
-    out = _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)
-    return (out, b.float().sum(0)) if colsum else out
+            return gemm_p(ap, bp, True, True, splits=_splits(ap.shape[1], bp.shape[1], ap.shape[0], a.device))[:M, :N]
+    return _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -262,9 +262,7 @@ def bias_gelu_fwd(x, b, approximate):
     return y
 
 
-def bias_gelu_bwd(gy, x, b, approximate, want_db=True):
-    """-> (d x, d b) of gelu(x + b); ``want_db=False``: d b is not formed (None) — the caller takes
-    it from the next GEMM's column sums"""
+def bias_gelu_bwd(gy, x, b, approximate):
     n = x.numel()
     H = x.shape[-1]
     if n % 8 or (b is not None and H % 8):
@@ -274,7 +272,7 @@ def bias_gelu_bwd(gy, x, b, approximate, want_db=True):
             y = TF.gelu(xx, approximate="tanh" if approximate else "none")
             (gx,) = torch.autograd.grad(y, xx, gy.float())
         gx = gx.to(x.dtype)
-    elif want_db and b is not None and x.dtype != torch.float32 and hasattr(_L(), "pha_bias_gelu_bwd_db"):
+    elif b is not None and x.dtype != torch.float32 and hasattr(_L(), "pha_bias_gelu_bwd_db"):
         # gx and the per-row-block column sums of gx in one pass; db = sum of the partials
         gx = torch.empty_like(x)
         rows = n // H
@@ -288,7 +286,7 @@ def bias_gelu_bwd(gy, x, b, approximate, want_db=True):
     else:
         gx = torch.empty_like(x)
         _check(_L().pha_bias_gelu_bwd(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), n, H, int(approximate), _stream(x)), "bias_gelu_bwd")
-    gb = gx.reshape(-1, H).sum(0, dtype=torch.float32).to(b.dtype) if (b is not None and want_db) else None
+    gb = gx.reshape(-1, H).sum(0, dtype=torch.float32).to(b.dtype) if b is not None else None
     return gx, gb
 
 

@@ -53,19 +53,12 @@ def _fwd(mode, x2d, w1, b1):
 
 
 def _bwd_gelu(mode, gy, w2, pre, b1):
-    """-> (d pre-activation, d b1 or None) from the MLP output gradient; None: db1 comes from the
-    fc1 weight-gradient GEMM's column sums (ops/gemm.py mm_tn colsum)"""
+    """-> (d pre-activation, d b1) from the MLP output gradient"""
     if mode == 1:
         g, part = G.gemm(gy, w2, False, False, act="dgelu", aux=pre, colsum=True)
         return g, G.colsum_finish(part, b1.dtype)
     ga = G.mm_nt(gy, w2)
-    if _FUSED_DB:
-        return _hip.bias_gelu_bwd(ga, pre, b1, True, want_db=False)[0], None
     return _hip.bias_gelu_bwd(ga, pre, b1, True)
-
-
-# bias gradients from the weight-gradient GEMMs (PHA_FUSED_DB=0: separate column-sum passes)
-_FUSED_DB = os.environ.get("PHA_FUSED_DB", "1") != "0"
 
 
 _MODES = {"pass": 0, "force": 1, "epi": 2}
@@ -103,16 +96,11 @@ class FusedMLP(torch.autograd.Function):
         from .conv_gemm import weight_grad
         x2d, w1, b1, w2, pre, a = ctx.saved_tensors
         gy = gy.contiguous()
-        if _FUSED_DB:
-            dw2, db2 = weight_grad(a, gy, bias_dtype=b1.dtype)
-        else:
-            dw2, db2 = weight_grad(a, gy), _hip.col_sum(gy)
+        dw2 = weight_grad(a, gy)
+        db2 = _hip.col_sum(gy)
         g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1)
         dx = G.mm_nt(g, w1) if ctx.needs_input_grad[0] else None
-        if db1 is None:
-            dw1, db1 = weight_grad(x2d, g, bias_dtype=b1.dtype)
-        else:
-            dw1 = weight_grad(x2d, g)
+        dw1 = weight_grad(x2d, g)
         return dx, dw1, db1, dw2, db2, None
 
 

@@ -683,6 +683,17 @@ def plan_program_memory(program, fetch_list=(), alignment=256):
     return {"arena_bytes": total, "naive_bytes": int(sum(sizes)), "offsets": dict(zip(names, offs))}
 
 
+def _program_tensors(program):
+    """the real (persistable) tensors the program's ops read or write"""
+    seen, out = set(), []
+    for op in (o for b in program.blocks for o in b.ops):
+        for t in _iter_tensors((op.args, op.kwargs, op.outputs)):
+            if not isinstance(t, Variable) and id(t) not in seen:
+                seen.add(id(t))
+                out.append(t)
+    return out
+
+
 def run_program(program, feed, fetch_list):
     """Interpret ``program`` with ``feed``; returns fetched Tensors (real). Intermediate values are
     dropped right after their last reader (eager deletion)."""
@@ -721,6 +732,12 @@ def run_program(program, feed, fetch_list):
     res = []
     for f in fetch_list or []:
         if isinstance(f, str):
+            if f not in blk.vars:   # a persistable (parameter / optimizer state) by name
+                hit = [t for t in _program_tensors(program) if getattr(t, "name", None) == f]
+                if not hit:
+                    raise KeyError(f)
+                res.append(_wrap(hit[0]._t.detach().clone()))   # a snapshot: later steps update it in place
+                continue
             f = blk.vars[f]
         if isinstance(f, Variable):
             res.append(env[id(f)])

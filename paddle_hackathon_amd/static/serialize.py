@@ -539,6 +539,11 @@ class _Reader:
                     op = _ref.CF[om.type](self, blk, ins, outs, attrs)
                 else:
                     conv = _CONVERT.get(om.type)
+                    if conv is None and om.type in _rg.OPTIMIZERS:
+                        conv = _rg.OPTIMIZERS[om.type]
+                    if conv is None and om.type.endswith("_grad"):   # training programs: backward ops
+                        self._grad_out_slots = [sl for sl in outs if sl.endswith("@GRAD") and outs[sl]]
+                        conv = _rg.grad_converter(om.type[:-5], _CONVERT)
                     if conv is None:
                         raise NotImplementedError(f"ProgramDesc op type {om.type!r} has no converter")
                     fn, kwargs, out_spec = conv(self, ins, attrs)
@@ -852,8 +857,11 @@ _CONVERT = {
 
 
 from . import ref_ops as _ref  # noqa: E402
+from . import ref_grad as _rg  # noqa: E402
 
 for _k, _v in _ref.CONVERT.items():
+    _CONVERT.setdefault(_k, _v)
+for _k, _v in _rg.FORWARD.items():
     _CONVERT.setdefault(_k, _v)
 _CONVERT.setdefault("depthwise_conv2d", _conv_conv2d)
 

@@ -138,47 +138,3 @@ def test_quant_moving_average_and_ste():
         assert abs(scale.item() - hist[-1]) < 1e-5 * max(1, hist[-1])
         out.sum().backward()
         torch.testing.assert_close(x.grad, torch.ones_like(x))
-
-
-@pytest.mark.parametrize("K,M,N,splits", [(4096, 512, 768, 1), (8192, 256, 512, 4), (2048, 264, 1032, 2),
-                                          (32768, 2048, 2048, 1)])
-def test_gemm4p_tn_column_sums(K, M, N, splits):
-    """TN weight gradient with the bias gradient (column sums of B over K) from the same pass"""
-    from paddle_hackathon_amd.ops import gemm as G
-    g = torch.Generator(device="cuda").manual_seed(K + M + N)
-    a, b = _r(K, M, g=g), _r(K, N, g=g)
-    c, cs = G.gemm_p_colsum(a, b, splits=splits)
-    torch.testing.assert_close(c.float(), a.float().t() @ b.float(), atol=0.05 * (K / 4096) ** 0.5, rtol=0.02)
-    ref = b.float().sum(0)
-    assert cs.shape == (N,)
-    assert (cs - ref).abs().max().item() <= 1e-3 * K ** 0.5
-
-
-def test_linear_and_mlp_bias_grads_from_gemm(monkeypatch):
-    """LinearNT / fused MLP backward take db from the weight-gradient GEMM: same values as the
-    separate column-sum path"""
-    import paddle_hackathon_amd as paddle
-    from paddle_hackathon_amd.ops import mlp, conv_gemm
-    paddle.set_device("gpu")
-    g = torch.Generator(device="cuda").manual_seed(3)
-    x = _r(1024, 256, g=g).requires_grad_()
-    w1, b1 = _r(256, 1024, g=g).mul_(0.05).requires_grad_(), _r(1024, g=g).requires_grad_()
-    w2, b2 = _r(1024, 256, g=g).mul_(0.05).requires_grad_(), _r(256, g=g).requires_grad_()
-    gy = _r(1024, 256, g=g)
-    grads = {}
-    for fused in (True, False):
-        monkeypatch.setattr(mlp, "_FUSED_DB", fused)
-        for t in (x, w1, b1, w2, b2):
-            t.grad = None
-        y = mlp.FusedMLP.apply(x, w1, b1, w2, b2, 0)
-        y.backward(gy)
-        grads[fused] = [t.grad.float().clone() for t in (b1, b2, w1, w2)]
-    for a, b in zip(grads[True], grads[False]):
-        torch.testing.assert_close(a, b, atol=0.05, rtol=0.02)
-    xl = _r(512, 256, g=g).requires_grad_()
-    wl, bl = _r(256, 384, g=g).mul_(0.05).requires_grad_(), _r(384, g=g).requires_grad_()
-    y = conv_gemm.LinearNT.apply(xl, wl, bl)
-    gl = _r(512, 384, g=g)
-    y.backward(gl)
-    torch.testing.assert_close(bl.grad.float(), gl.float().sum(0), atol=0.1, rtol=0.02)
-    torch.testing.assert_close(wl.grad.float(), xl.float().t() @ gl.float(), atol=0.1, rtol=0.02)

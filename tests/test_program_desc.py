@@ -756,3 +756,143 @@ def test_activations_and_scalar_elementwise_emit_reference_types(tmp_path):
             np.testing.assert_allclose(np.asarray(b), np.asarray(a), rtol=1e-5, atol=1e-6)
     finally:
         paddle.disable_static()
+
+
+def test_reference_training_program_executes(tmp_path):
+    """round-3 verdict: a reference-written TRAINING ProgramDesc — forward ops, <type>_grad ops
+    with @GRAD slots (mean_grad, softmax_with_cross_entropy_grad, elementwise_add_grad(axis=1),
+    mul_grad, relu_grad) and sgd ops updating the persistable parameters in place — loads and
+    trains: three steps equal the same SGD in torch (static/ref_grad.py)"""
+    import torch
+    rng = np.random.RandomState(3)
+    P = {"w1": rng.randn(4, 8).astype("float32") * 0.5, "b1": rng.randn(8).astype("float32") * 0.1,
+         "w2": rng.randn(8, 3).astype("float32") * 0.5, "b2": np.zeros(3, "float32"),
+         "lr": np.array([0.1], "float32")}
+    desc = pb.ProgramDesc()
+    g = desc.blocks.add()
+    g.idx, g.parent_idx = 0, -1
+    _var(g, "x", [-1, 4])
+    _var(g, "label", [-1, 1], dtype=3)
+    for n, a in P.items():
+        _var(g, n, list(a.shape), persistable=True)
+    for n in ("h1", "a1", "r1", "h2", "a2", "sm", "ls", "loss", "loss@GRAD", "ls@GRAD", "a2@GRAD", "h2@GRAD",
+              "b2@GRAD", "r1@GRAD", "w2@GRAD", "a1@GRAD", "h1@GRAD", "b1@GRAD", "w1@GRAD"):
+        _var(g, n, [-1])
+    _op(g, "feed", {"X": ["feed"]}, {"Out": ["x"]}, col=0)
+    _op(g, "feed", {"X": ["feed"]}, {"Out": ["label"]}, col=1)
+    _op(g, "mul", {"X": ["x"], "Y": ["w1"]}, {"Out": ["h1"]}, x_num_col_dims=1, y_num_col_dims=1)
+    _op(g, "elementwise_add", {"X": ["h1"], "Y": ["b1"]}, {"Out": ["a1"]}, axis=1)
+    _op(g, "relu", {"X": ["a1"]}, {"Out": ["r1"]})
+    _op(g, "mul", {"X": ["r1"], "Y": ["w2"]}, {"Out": ["h2"]}, x_num_col_dims=1, y_num_col_dims=1)
+    _op(g, "elementwise_add", {"X": ["h2"], "Y": ["b2"]}, {"Out": ["a2"]}, axis=1)
+    _op(g, "softmax_with_cross_entropy", {"Logits": ["a2"], "Label": ["label"]}, {"Softmax": ["sm"], "Loss": ["ls"]},
+        soft_label=False, ignore_index=-100, axis=-1)
+    _op(g, "mean", {"X": ["ls"]}, {"Out": ["loss"]})
+    # backward (op_role 1) and optimizer (op_role 2) ops as the reference's append_backward / minimize write them
+    _op(g, "fill_constant", {}, {"Out": ["loss@GRAD"]}, shape=[1], value=1.0, dtype=5, op_role=257)
+    _op(g, "mean_grad", {"X": ["ls"], "Out@GRAD": ["loss@GRAD"]}, {"X@GRAD": ["ls@GRAD"]}, op_role=1)
+    _op(g, "softmax_with_cross_entropy_grad", {"Label": ["label"], "Softmax": ["sm"], "Loss@GRAD": ["ls@GRAD"]},
+        {"Logits@GRAD": ["a2@GRAD"]}, soft_label=False, ignore_index=-100, axis=-1, op_role=1)
+    _op(g, "elementwise_add_grad", {"X": ["h2"], "Y": ["b2"], "Out@GRAD": ["a2@GRAD"]},
+        {"X@GRAD": ["h2@GRAD"], "Y@GRAD": ["b2@GRAD"]}, axis=1, op_role=1)
+    _op(g, "mul_grad", {"X": ["r1"], "Y": ["w2"], "Out@GRAD": ["h2@GRAD"]},
+        {"X@GRAD": ["r1@GRAD"], "Y@GRAD": ["w2@GRAD"]}, x_num_col_dims=1, y_num_col_dims=1, op_role=1)
+    _op(g, "relu_grad", {"Out": ["r1"], "Out@GRAD": ["r1@GRAD"]}, {"X@GRAD": ["a1@GRAD"]}, op_role=1)
+    _op(g, "elementwise_add_grad", {"X": ["h1"], "Y": ["b1"], "Out@GRAD": ["a1@GRAD"]},
+        {"X@GRAD": ["h1@GRAD"], "Y@GRAD": ["b1@GRAD"]}, axis=1, op_role=1)
+    _op(g, "mul_grad", {"X": ["x"], "Y": ["w1"], "Out@GRAD": ["h1@GRAD"]}, {"Y@GRAD": ["w1@GRAD"]},
+        x_num_col_dims=1, y_num_col_dims=1, op_role=1)
+    for n in ("w1", "b1", "w2", "b2"):
+        _op(g, "sgd", {"Param": [n], "Grad": [n + "@GRAD"], "LearningRate": ["lr"]}, {"ParamOut": [n]}, op_role=2)
+    _op(g, "fetch", {"X": ["loss"]}, {"Out": ["fetch"]}, col=0)
+    prefix = str(tmp_path / "train")
+    open(prefix + ".pdmodel", "wb").write(desc.SerializeToString())
+    pb.save_combine([torch.from_numpy(P[n]) for n in sorted(P)], prefix + ".pdiparams")
+
+    exe = paddle.static.Executor()
+    prog, feeds, fetches = paddle.static.load_inference_model(prefix, exe)
+    assert feeds == ["x", "label"]
+    types = [op.attrs["ref_op"][0] for op in prog.global_block().ops if "ref_op" in op.attrs]
+    assert "mul_grad" in types and types.count("sgd") == 4
+    xs = [rng.randn(5, 4).astype("float32") for _ in range(3)]
+    labs = [rng.randint(0, 3, (5, 1)).astype("int64") for _ in range(3)]
+    got = []
+    for xb, lb in zip(xs, labs):
+        out = exe.run(prog, feed={"x": xb, "label": lb}, fetch_list=fetches + ["w1", "b1", "w2", "b2"])
+        got.append(out)
+
+    T = {n: torch.tensor(P[n]).requires_grad_(n != "lr") for n in P}
+    for step, (xb, lb) in enumerate(zip(xs, labs)):
+        h = torch.relu(torch.from_numpy(xb) @ T["w1"] + T["b1"])
+        logits = h @ T["w2"] + T["b2"]
+        loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(lb).reshape(-1))
+        loss.backward()
+        np.testing.assert_allclose(np.asarray(got[step][0]).reshape(-1)[0], loss.item(), rtol=1e-5)
+        with torch.no_grad():
+            for n in ("w1", "b1", "w2", "b2"):
+                T[n] -= 0.1 * T[n].grad
+                T[n].grad = None
+        for i, n in enumerate(("w1", "b1", "w2", "b2")):
+            np.testing.assert_allclose(np.asarray(got[step][1 + i]), T[n].detach().numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("opt", ["adam", "momentum"])
+def test_reference_training_program_optimizers(tmp_path, opt):
+    """adam / momentum ops of a reference training program (moments and beta-pow accumulators
+    are persistables updated in place) against the reference update formulas"""
+    import torch
+    rng = np.random.RandomState(4)
+    P = {"w": rng.randn(4, 2).astype("float32"), "lr": np.array([0.05], "float32")}
+    if opt == "adam":
+        P.update(m1=np.zeros((4, 2), "float32"), m2=np.zeros((4, 2), "float32"),
+                 b1p=np.array([0.9], "float32"), b2p=np.array([0.999], "float32"))
+    else:
+        P.update(vel=np.zeros((4, 2), "float32"))
+    desc = pb.ProgramDesc()
+    g = desc.blocks.add()
+    g.idx, g.parent_idx = 0, -1
+    _var(g, "x", [-1, 4])
+    for n, a in P.items():
+        _var(g, n, list(a.shape), persistable=True)
+    for n in ("h", "sq", "loss", "loss@GRAD", "sq@GRAD", "h@GRAD", "w@GRAD"):
+        _var(g, n, [-1])
+    _op(g, "feed", {"X": ["feed"]}, {"Out": ["x"]}, col=0)
+    _op(g, "mul", {"X": ["x"], "Y": ["w"]}, {"Out": ["h"]}, x_num_col_dims=1, y_num_col_dims=1)
+    _op(g, "square", {"X": ["h"]}, {"Out": ["sq"]})
+    _op(g, "mean", {"X": ["sq"]}, {"Out": ["loss"]})
+    _op(g, "fill_constant", {}, {"Out": ["loss@GRAD"]}, shape=[1], value=1.0, dtype=5)
+    _op(g, "mean_grad", {"X": ["sq"], "Out@GRAD": ["loss@GRAD"]}, {"X@GRAD": ["sq@GRAD"]})
+    _op(g, "square_grad", {"X": ["h"], "Out@GRAD": ["sq@GRAD"]}, {"X@GRAD": ["h@GRAD"]})
+    _op(g, "mul_grad", {"X": ["x"], "Y": ["w"], "Out@GRAD": ["h@GRAD"]}, {"Y@GRAD": ["w@GRAD"]},
+        x_num_col_dims=1, y_num_col_dims=1)
+    if opt == "adam":
+        _op(g, "adam", {"Param": ["w"], "Grad": ["w@GRAD"], "LearningRate": ["lr"], "Moment1": ["m1"],
+                        "Moment2": ["m2"], "Beta1Pow": ["b1p"], "Beta2Pow": ["b2p"]},
+            {"ParamOut": ["w"], "Moment1Out": ["m1"], "Moment2Out": ["m2"], "Beta1PowOut": ["b1p"],
+             "Beta2PowOut": ["b2p"]}, beta1=0.9, beta2=0.999, epsilon=1e-8)
+    else:
+        _op(g, "momentum", {"Param": ["w"], "Grad": ["w@GRAD"], "Velocity": ["vel"], "LearningRate": ["lr"]},
+            {"ParamOut": ["w"], "VelocityOut": ["vel"]}, mu=0.9, use_nesterov=False)
+    _op(g, "fetch", {"X": ["loss"]}, {"Out": ["fetch"]}, col=0)
+    prefix = str(tmp_path / opt)
+    open(prefix + ".pdmodel", "wb").write(desc.SerializeToString())
+    pb.save_combine([torch.from_numpy(P[n]) for n in sorted(P)], prefix + ".pdiparams")
+    exe = paddle.static.Executor()
+    prog, _, fetches = paddle.static.load_inference_model(prefix, exe)
+    w = P["w"].astype("float64")
+    m1 = m2 = v = np.zeros_like(w)
+    b1p, b2p = 0.9, 0.999
+    for step in range(4):
+        xb = rng.randn(6, 4).astype("float32")
+        _, wv = exe.run(prog, feed={"x": xb}, fetch_list=fetches + ["w"])
+        gw = xb.T.astype("float64") @ (2 * (xb @ w)) / (6 * 2)
+        if opt == "adam":
+            m1 = 0.9 * m1 + 0.1 * gw
+            m2 = 0.999 * m2 + 0.001 * gw * gw
+            lr_t = 0.05 * np.sqrt(1 - b2p) / (1 - b1p)
+            w = w - lr_t * m1 / (np.sqrt(m2) + 1e-8 * np.sqrt(1 - b2p))
+            b1p, b2p = b1p * 0.9, b2p * 0.999
+        else:
+            v = 0.9 * v + gw
+            w = w - 0.05 * v
+        np.testing.assert_allclose(np.asarray(wv), w, rtol=1e-4, atol=1e-6)
