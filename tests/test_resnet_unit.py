@@ -14,7 +14,7 @@ def _bn(c):
     return (c - c.mean((0, 2, 3), keepdim=True)) / torch.sqrt(c.var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5)
 
 
-def _ref(u, x, z, fmt, mode):
+def _ref(u, x, z, fmt, mode, gy=None):
     def conv(t, w, s):
         if fmt == "NHWC":
             t, w = t.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2)
@@ -31,7 +31,7 @@ def _ref(u, x, z, fmt, mode):
     out = torch.relu(out)
     if fmt == "NHWC":
         out = out.permute(0, 2, 3, 1)
-    out.sum().backward()
+    out.backward(torch.ones_like(out) if gy is None else gy.double())
     return out, xt.grad, fx.grad, c.detach().mean((0, 2, 3))
 
 
@@ -112,13 +112,16 @@ def test_resnet_unit_gpu_bf16_nhwc(mode):
         x.stop_gradient = False
         z = paddle.randn([4, 14, 14, 64]).astype("bfloat16") if short else None
         y = u(x, z)
-        y.astype("float32").sum().backward()
-        ref, gx, gw, _ = _ref(u, x, z, "NHWC", mode)
+        gy = torch.randn(tuple(y.shape), device="cuda")   # a random upstream gradient (a sum loss makes
+        y.backward(paddle.to_tensor(gy.to(torch.bfloat16)))   # BN's backward a cancellation test)
+        ref, gx, gw, _ = _ref(u, x, z, "NHWC", mode, gy.to(torch.bfloat16).cpu())
         assert y._t.dtype == torch.bfloat16
         torch.testing.assert_close(y._t.double(), ref.detach().to(y._t.device), atol=0.06, rtol=0.05)
-        # the input gradient passes BN's backward (cancellations) in bf16: compare in norm
+        # the input gradient passes BN's backward (cancellations) in bf16: compare in norm. With the
+        # shortcut branch the bf16-rounded residual moves the ReLU mask: the CPU torch bf16 run of the
+        # same unit lands at 2.1 % from the fp64 oracle too (plain: 0.2 %)
         gxd = gx.to(y._t.device)
-        assert ((x.grad._t.double() - gxd).norm() / gxd.norm()).item() < 2e-2
+        assert ((x.grad._t.double() - gxd).norm() / gxd.norm()).item() < (4e-2 if short else 1e-2)
     finally:
         paddle.set_device("cpu")
 
