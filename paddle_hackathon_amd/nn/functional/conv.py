@@ -3,8 +3,9 @@
 Paddle layouts: weight [C_out, C_in/groups, *k] (transpose conv: [C_in, C_out/groups, *k]);
 ``data_format`` NCHW or NHWC. 2-D convolutions run on the own kernels in NHWC memory for both
 formats (``_own_conv2d``), fp32 ones included (a three-term bf16 split on the same MFMA kernels,
-ops/conv_gemm.py split3); 1-D convolutions run as height-1 2-D ones. What they do not take (3-D,
-some transposed / grouped forms) goes to MIOpen and is counted by ops/fallback.py (3-D: not counted).
+ops/conv_gemm.py split3); 1-D convolutions run as height-1 2-D ones, 3-D ones as one 2-D
+convolution per depth tap (``_conv3d_as_2d``). What they do not take (some transposed / grouped /
+"SAME"-padded forms) goes to MIOpen and is counted by ops/fallback.py.
 """
 from __future__ import annotations
 
@@ -173,6 +174,41 @@ def _conv1d_as_2d(t, w, bias, stride, padding, dilation, groups, data_format):
     return out.squeeze(2) if nchw else out.squeeze(1)
 
 
+def _conv3d_as_2d(t, w, bias, stride, padding, dilation, groups, data_format):
+    """3-D convolution on the own 2-D kernels: out[:, od] = sum_kd conv2d(x[:, od*sd - pd + kd*dd],
+    w[:, :, kd]) — one height x width convolution per depth tap over all (batch, output-depth)
+    planes at once, summed in fp32 (autograd runs through the 2-D convolutions). None when the
+    2-D kernels do not take the planes."""
+    if data_format not in ("NCDHW", "NDHWC") or t.dim() != 5 or isinstance(padding, str):
+        return None
+    st, dl = _tup(stride, 3), _tup(dilation, 3)
+    k = list(w.shape[2:])
+    pad, pre = _padding(padding, 3, k, st, dl, [0, 0, 0])
+    if pre is not None:
+        return None
+    x = t.permute(0, 2, 3, 4, 1) if data_format == "NCDHW" else t     # N, D, H, W, C
+    N, D, H, W, C = x.shape
+    KD = k[0]
+    OD = (D + 2 * pad[0] - dl[0] * (KD - 1) - 1) // st[0] + 1
+    if OD <= 0:
+        return None
+    xp = TF.pad(x, [0, 0, 0, 0, 0, 0, pad[0], pad[0]]) if pad[0] else x
+    acc = None
+    for kd in range(KD):
+        d0 = kd * dl[0]
+        planes = xp[:, d0:d0 + (OD - 1) * st[0] + 1:st[0]].reshape(N * OD, H, W, C)
+        o = _own_conv2d(planes, w[:, :, kd], None, st[1:], pad[1:], dl[1:], groups, "NHWC")
+        if o is None:
+            return None
+        o = o.float() if o.dtype in (torch.bfloat16, torch.float16) else o   # fp32 sum of the taps
+        acc = o if acc is None else acc + o
+    out = acc.to(t.dtype)
+    out = out.reshape(N, OD, out.shape[1], out.shape[2], out.shape[3])
+    if bias is not None:
+        out = out + bias
+    return out.permute(0, 4, 1, 2, 3) if data_format == "NCDHW" else out
+
+
 def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     t = x._t
     w = weight._t
@@ -184,7 +220,11 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
         out = _conv1d_as_2d(t, w, None if bias is None else bias._t, stride, padding, dilation, groups, data_format)
         if out is not None:
             return _w(out)
-    if t.is_cuda and n in (1, 2):
+    if n == 3 and t.is_cuda:
+        out = _conv3d_as_2d(t, w, None if bias is None else bias._t, stride, padding, dilation, groups, data_format)
+        if out is not None:
+            return _w(out)
+    if t.is_cuda:
         from ...ops import fallback
         fallback.note(f"conv{n}d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)
@@ -266,7 +306,7 @@ def _convnd_t(n, x, weight, bias, stride, padding, output_padding, groups, dilat
                             dilation, output_size, data_format)
         if out is not None:
             return _w(out)
-    if t.is_cuda and n in (1, 2):
+    if t.is_cuda:
         from ...ops import fallback
         fallback.note(f"conv{n}d", f"{data_format} {t.dtype} groups={groups} -> MIOpen")
     t, cl = _to_ncx(t, data_format)

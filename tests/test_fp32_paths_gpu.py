@@ -111,3 +111,33 @@ def test_fp32_resnet_block_no_miopen():
     torch.cuda.synchronize()
     assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
     assert y._t.dtype == torch.float32 and torch.isfinite(x.grad._t).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("fmt", ["NCDHW", "NDHWC"])
+def test_conv3d_own_kernels(dtype, fmt):
+    """3-D convolution as per-depth-tap 2-D convolutions on the own kernels (forward + backward)"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    paddle.set_device("gpu")
+    torch.manual_seed(5)
+    x = torch.randn(2, 8, 6, 10, 10, device="cuda")
+    w = torch.randn(16, 8, 3, 3, 3, device="cuda") * 0.1
+    b = torch.randn(16, device="cuda")
+    xin = x.permute(0, 2, 3, 4, 1).contiguous() if fmt == "NDHWC" else x
+    px, pw, pb = (paddle.to_tensor(v.to(dtype)) for v in (xin, w, b))
+    for t in (px, pw, pb):
+        t.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.conv3d(px, pw, pb, stride=[2, 1, 1], padding=1, data_format=fmt)
+    y.astype("float32").sum().backward()
+    assert fallback.counts().get("conv3d", 0) == 0, fallback.counts()
+    xd, wd = x.to(dtype).double().requires_grad_(), w.to(dtype).double().requires_grad_()
+    ref = torch.nn.functional.conv3d(xd, wd, b.to(dtype).double(), stride=[2, 1, 1], padding=1)
+    ref.sum().backward()
+    out = y._t.permute(0, 4, 1, 2, 3) if fmt == "NDHWC" else y._t
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ref) < tol
+    gx = px.grad._t.permute(0, 4, 1, 2, 3) if fmt == "NDHWC" else px.grad._t
+    assert _rel(gx, xd.grad) < tol
+    assert _rel(pw.grad._t, wd.grad) < tol

@@ -865,3 +865,29 @@ def test_kl_div_negative_targets_masked(reduction):
     want = {"batchmean": out.sum() / 5, "mean": out.mean(), "sum": out.sum(), "none": out}[reduction]
     got = paddle.nn.functional.kl_div(P(x), P(t), reduction=reduction).numpy()
     np.testing.assert_allclose(got.reshape(np.shape(want)), want, rtol=1e-6)
+
+
+def test_conv3d_depth_tap_decomposition(monkeypatch):
+    """the GPU route of conv3d (one 2-D convolution per depth tap, nn/functional/conv.py
+    _conv3d_as_2d) checked on CPU with a plain NHWC 2-D convolution standing in for the own kernel"""
+    import torch
+    import torch.nn.functional as TF
+    from paddle_hackathon_amd.nn.functional import conv as C
+
+    def fake_own(t, w, bias, stride, padding, dilation, groups, data_format):
+        y = TF.conv2d(t.permute(0, 3, 1, 2), w, None, stride, padding, dilation, groups)
+        return y.permute(0, 2, 3, 1)
+    monkeypatch.setattr(C, "_own_conv2d", fake_own)
+    torch.manual_seed(0)
+    x = torch.randn(2, 4, 7, 6, 5, dtype=torch.float64)
+    w = torch.randn(6, 4, 3, 2, 3, dtype=torch.float64)
+    b = torch.randn(6, dtype=torch.float64)
+    for fmt in ("NCDHW", "NDHWC"):
+        xin = x.permute(0, 2, 3, 4, 1) if fmt == "NDHWC" else x
+        out = C._conv3d_as_2d(xin, w, b, [2, 1, 2], [1, 0, 1], [1, 1, 1], 1, fmt)
+        ref = TF.conv3d(x, w, b, [2, 1, 2], [1, 0, 1])
+        if fmt == "NDHWC":
+            out = out.permute(0, 4, 1, 2, 3)
+        torch.testing.assert_close(out, ref)
+    out = C._conv3d_as_2d(x, w, None, 1, 2, [2, 1, 1], 1, "NCDHW")
+    torch.testing.assert_close(out, TF.conv3d(x, w, None, 1, 2, [2, 1, 1]))
