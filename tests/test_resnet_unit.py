@@ -31,7 +31,7 @@ def _ref(u, x, z, fmt, mode, gy=None):
     out = torch.relu(out)
     if fmt == "NHWC":
         out = out.permute(0, 2, 3, 1)
-    out.backward(torch.ones_like(out) if gy is None else gy.double())
+    out.backward(torch.ones_like(out) if gy is None else gy.double().to(out.device))
     return out, xt.grad, fx.grad, c.detach().mean((0, 2, 3))
 
 
@@ -114,7 +114,7 @@ def test_resnet_unit_gpu_bf16_nhwc(mode):
         y = u(x, z)
         gy = torch.randn(tuple(y.shape), device="cuda")   # a random upstream gradient (a sum loss makes
         y.backward(paddle.to_tensor(gy.to(torch.bfloat16)))   # BN's backward a cancellation test)
-        ref, gx, gw, _ = _ref(u, x, z, "NHWC", mode, gy.to(torch.bfloat16).cpu())
+        ref, gx, gw, _ = _ref(u, x, z, "NHWC", mode, gy.to(torch.bfloat16))
         assert y._t.dtype == torch.bfloat16
         torch.testing.assert_close(y._t.double(), ref.detach().to(y._t.device), atol=0.06, rtol=0.05)
         # the input gradient passes BN's backward (cancellations) in bf16: compare in norm. With the
