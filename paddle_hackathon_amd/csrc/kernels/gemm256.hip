@@ -40,6 +40,11 @@ struct ConvGeo {
   // (n * OHF + oh0 + oh * osh) * OWF + ow0 + ow * osw — one phase of a strided conv's dgrad
   int OHF, OWF, oh0, ow0, osh, osw;
   int ozero;   // also store zeros at the osh x osw - 1 other pixels of the output's stride cell
+  // grouped convolution (blockIdx.y = group): the image's pixel stride in channels (0: C) and the
+  // per-group element offsets of the image channels (ga), the filter / A rows (gb) and the output
+  // columns (gc); C, the GEMM N and K are the ONE group's
+  int cs = 0;
+  long ga = 0, gb = 0, gc = 0;
 };
 
 struct Args {
@@ -125,6 +130,15 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
   const T* A = static_cast<const T*>(p.a);
   const T* Bt = static_cast<const T*>(p.b);
   const char* zero = static_cast<const char*>(p.zero);
+  long goff_c = 0;   // grouped conv: this group's output column offset
+  int CS = 0;        // conv: image pixel stride in channels
+  if constexpr (CONV) {
+    const int grp = blockIdx.y;
+    A += grp * p.g.ga;
+    Bt += grp * p.g.gb;
+    goff_c = grp * p.g.gc;
+    CS = p.g.cs ? p.g.cs : p.g.C;
+  }
 
   // ---- per-lane source rows of this thread's glds instructions ------------------------------
   // wave-instruction i fills image bytes [i * 1024, +1024) = RPI rows of 2*BK bytes; lane l takes
@@ -146,7 +160,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
       const int oh = rem / g.OW, ow = rem - (rem / g.OW) * g.OW;
       ar[j].ih0 = oh * g.sh - g.ph;
       ar[j].iw0 = ow * g.sw - g.pw;
-      ar[j].base = reinterpret_cast<const char*>(A + (long)n * g.H * g.W * g.C);
+      ar[j].base = reinterpret_cast<const char*>(A + (long)n * g.H * g.W * CS);
     } else {
       ar[j].base = reinterpret_cast<const char*>(A + (ar[j].ok ? m : 0) * p.lda);
       ar[j].ih0 = ar[j].iw0 = 0;
@@ -179,7 +193,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
           const int kh = tap / g.KW, kw = tap - kh * g.KW;
           const int ih = ar[j].ih0 + kh * g.dh, iw = ar[j].iw0 + kw * g.dw;
           if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-            src = ar[j].base + (((long)ih * g.W + iw) * g.C + cin) * sizeof(T);
+            src = ar[j].base + (((long)ih * g.W + iw) * CS + cin) * sizeof(T);
         } else {
           src = ar[j].base + k * sizeof(T);
         }
@@ -235,7 +249,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 
   // ---- fp32 output: straight from the accumulators (16 lanes store 64 contiguous bytes of a row)
   if constexpr (F32OUT) {
-    float* Cf = static_cast<float*>(p.c);
+    float* Cf = static_cast<float*>(p.c) + goff_c;
 #pragma unroll
     for (int j = 0; j < CB; ++j) {
       const long n = n0 + wn * 64 + j * 16 + fr;
@@ -289,7 +303,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
       }
   }
   __syncthreads();
-  T* C = static_cast<T*>(p.c);
+  T* C = static_cast<T*>(p.c) + goff_c;
   constexpr int CH = BN / 8;                          // 16-B chunks per C row
   const bool full_n = n0 + BN <= N && (p.ldc % 8) == 0;
   for (int idx = tid; idx < BM * CH; idx += NT) {
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
 // tile: index into cands (-1 = heuristic), bk: 32 | 64 (0 = heuristic); the host autotuner
 // (ops/conv_gemm.py) times the candidates once per shape and passes its choice
 template <typename T, bool CONV>
-int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_rows = nullptr) {
+int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_rows = nullptr, int groups_ = 1) {
   if (bk != 32 && bk != 64) bk = (CONV || a.K <= 1024) ? 32 : 64;
   // tile shape: the fewest "CU rounds x tile work / tile efficiency" (a 784-tile grid on 256 CUs
   // wastes a quarter of the chip in its last round; small tiles pay in operand re-reads)
@@ -453,16 +467,17 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_
   if (tile >= 0 && tile < 6) best = tile;
   const int bm = cands[best][0], bn = cands[best][1];
   if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);   // row tiles with stats / bn_part rows
+  const unsigned groups = (unsigned)std::max(1, groups_);
   if (a.out_f32) {   // fp32 products (three-term bf16 split): one 128 x 128 x 32 instantiation
     const long tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    hipLaunchKernelGGL((gemm256_kernel<T, 128, 128, 32, CONV, true>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((gemm256_kernel<T, 128, 128, 32, CONV, true>), dim3((unsigned)tiles, groups), dim3(NT), 0, st, a);
     return (int)hipGetLastError();
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;
     const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
-    if (bk == 32) hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 32, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 64, CONV>), dim3((unsigned)tiles), dim3(NT), 0, st, a);
+    if (bk == 32) hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 32, CONV>), dim3((unsigned)tiles, groups), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, 64, CONV>), dim3((unsigned)tiles, groups), dim3(NT), 0, st, a);
   };
 #define G256_CASE(M_, N_) if (bm == M_ && bn == N_) { go(std::integral_constant<int, M_>(), std::integral_constant<int, N_>()); return (int)hipGetLastError(); }
   G256_CASE(256, 256) G256_CASE(256, 128) G256_CASE(256, 64) G256_CASE(128, 256) G256_CASE(128, 128) G256_CASE(128, 64)
@@ -532,6 +547,15 @@ __global__ __launch_bounds__(NT) void gemm256_tn_kernel(TnArgs p) {
   const T* A = static_cast<const T*>(p.a);
   const T* B = static_cast<const T*>(p.b);
   const char* zero = static_cast<const char*>(p.zero);
+  int CS = 0;   // B_CONV: image pixel stride in channels
+  float* wsg = p.ws;
+  if constexpr (BCONV) {   // grouped conv weight gradient: blockIdx.y = group
+    const int grp = blockIdx.y;
+    A += grp * p.g.gc;                       // the group's dY columns
+    B += grp * p.g.ga;                       // the group's input channels
+    wsg += (long)grp * p.splits * M * N;     // the group's partial slabs
+    CS = p.g.cs ? p.g.cs : p.g.C;
+  }
 
   // per-lane source columns (constant over the K loop) and image rows of each glds instruction
   int arow[A_INS];
@@ -587,7 +611,7 @@ __global__ __launch_bounds__(NT) void gemm256_tn_kernel(TnArgs p) {
           const int oh = rem / g.OW, ow = rem - oh * g.OW;
           const int ih = oh * g.sh + bkh[j], iw = ow * g.sw + bkw[j];
           if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-            src = bcol[j] + (((long)b * g.H + ih) * g.W + iw) * g.C * (long)sizeof(T);
+            src = bcol[j] + (((long)b * g.H + ih) * g.W + iw) * CS * (long)sizeof(T);
         } else {
           src = bcol[j] + k * p.ldb * (long)sizeof(T);
         }
@@ -631,7 +655,7 @@ __global__ __launch_bounds__(NT) void gemm256_tn_kernel(TnArgs p) {
 
   // fp32 partials straight from the accumulators: register e of block (i, j) is
   // C[4 * (lane >> 4) + e][lane & 15]; 16 lanes store 64 contiguous bytes of a row
-  float* ws = p.ws + (long)split * M * N;
+  float* ws = wsg + (long)split * M * N;
   const int fr = lane & 15;
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
@@ -666,6 +690,9 @@ template <typename T, bool OUTF32>
 __global__ __launch_bounds__(256) void tn_finalize_kernel(const float* __restrict__ ws, void* out, long M, long N,
                                                            int S, int conv_c, int accumulate) {
   const long total = M * N;
+  // grouped conv weight gradients: blockIdx.y = group, slabs [group][S][M][N] -> out rows of the group
+  ws += (long)blockIdx.y * S * total;
+  out = static_cast<char*>(out) + (long)blockIdx.y * total * (OUTF32 ? sizeof(float) : sizeof(T));
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += ws[s * total + idx];
@@ -689,7 +716,9 @@ __global__ __launch_bounds__(256) void tn_finalize_kernel(const float* __restric
 
 // tile: 0 (256x256) 1 (256x128) 2 (128x256) 3 (128x128) 4 (64x256) 5 (256x64) 6 (128x64) 7 (64x128)
 template <typename T, bool BCONV>
-int launch_tn(TnArgs a, void* out, int out_f32, int conv_c, int accumulate, int tile, int splits, hipStream_t st) {
+int launch_tn(TnArgs a, void* out, int out_f32, int conv_c, int accumulate, int tile, int splits, hipStream_t st,
+              int groups_ = 1) {
+  const unsigned groups = (unsigned)std::max(1, groups_);
   static const int cands[8][2] = {{256, 256}, {256, 128}, {128, 256}, {128, 128},
                                   {64, 256}, {256, 64}, {128, 64}, {64, 128}};
   static int cus = 0;
@@ -717,13 +746,14 @@ int launch_tn(TnArgs a, void* out, int out_f32, int conv_c, int accumulate, int 
   a.splits = (int)((a.K + a.kchunk - 1) / a.kchunk);
   const unsigned grid = (unsigned)(tiles * a.splits);
 #define TN_CASE(M_, N_) \
-  if (bm == M_ && bn == N_) hipLaunchKernelGGL((gemm256_tn_kernel<T, M_, N_, BCONV>), dim3(grid), dim3(NT), 0, st, a);
+  if (bm == M_ && bn == N_) hipLaunchKernelGGL((gemm256_tn_kernel<T, M_, N_, BCONV>), dim3(grid, groups), dim3(NT), 0, st, a);
   TN_CASE(256, 256) TN_CASE(256, 128) TN_CASE(128, 256) TN_CASE(128, 128)
   TN_CASE(64, 256) TN_CASE(256, 64) TN_CASE(128, 64) TN_CASE(64, 128)
 #undef TN_CASE
   const long total = a.M * a.N;
   const float* part = a.ws;
   int S = a.splits;
+  if (S > 32 && groups > 1) return (int)hipErrorInvalidValue;   // (grouped: the caller caps the splits)
   if (S > 32) {   // ws holds (S + ceil(S / 16)) x M x N floats
     float* ws2 = a.ws + (long)S * total;
     const int G = (S + 15) / 16;
@@ -733,9 +763,9 @@ int launch_tn(TnArgs a, void* out, int out_f32, int conv_c, int accumulate, int 
     S = G;
   }
   const unsigned fg = (unsigned)std::min((total + 255) / 256, 8192L);
-  if (out_f32) hipLaunchKernelGGL((tn_finalize_kernel<T, true>), dim3(fg), dim3(256), 0, st, part, out, a.M, a.N,
+  if (out_f32) hipLaunchKernelGGL((tn_finalize_kernel<T, true>), dim3(fg, groups), dim3(256), 0, st, part, out, a.M, a.N,
                                   S, conv_c, accumulate);
-  else hipLaunchKernelGGL((tn_finalize_kernel<T, false>), dim3(fg), dim3(256), 0, st, part, out, a.M, a.N,
+  else hipLaunchKernelGGL((tn_finalize_kernel<T, false>), dim3(fg, groups), dim3(256), 0, st, part, out, a.M, a.N,
                           S, conv_c, accumulate);
   return (int)hipGetLastError();
 }
@@ -784,6 +814,53 @@ PHA_API int pha_conv256_fwd(int dt, const void* x, const void* w, void* y, const
                bn_x, bn_mean, bn_aff, bn_part, bn_row0, addend};
   if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, stats_rows);
   if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, stats_rows);
+  return (int)hipErrorInvalidValue;
+}
+
+// grouped NHWC convolution on the implicit-GEMM kernel: x [N, H, W, groups*cig], w [groups*cog][KH][KW][cig],
+// y [N*OH*OW][ldy] (group g writes columns g*cog.. of y + its own offset); cig % 8 == 0. One launch,
+// blockIdx.y = group. out_f32: fp32 y (bias / act / remap as pha_conv256_fwd_f32out). oremap as
+// pha_conv256_fwd (dgrad phases).
+PHA_API int pha_conv256_fwd_grouped(int dt, const void* x, const void* w, void* y, const float* bias, int N, int H,
+                                    int W, int cig, int cog, int groups, int KH, int KW, int sh, int sw, int ph,
+                                    int pw, int dh, int dw, int act, long ldy, int out_f32, const void* zero16,
+                                    int tile, int bk, const int* oremap, hipStream_t stream) {
+  if (cig % 8 || groups < 1) return (int)hipErrorInvalidValue;
+  g256::ConvGeo g{N, H, W, cig, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1,
+                  KH, KW, sh, sw, ph, pw, dh, dw, 0, 0, 0, 0, 0, 0, 0};
+  if (oremap) {
+    g.OHF = oremap[0]; g.OWF = oremap[1]; g.oh0 = oremap[2]; g.ow0 = oremap[3]; g.osh = oremap[4]; g.osw = oremap[5];
+    g.OH = oremap[6]; g.OW = oremap[7]; g.ozero = oremap[8];
+  }
+  const long K = (long)KH * KW * cig;
+  g.cs = cig * groups;
+  g.ga = cig;
+  g.gb = (long)cog * K;
+  g.gc = cog;
+  const long M = (long)N * g.OH * g.OW;
+  g256::Args p{x, w, y, bias, M, (long)cog, K, 0, K, ldy, act, zero16, g, nullptr,
+               nullptr, nullptr, nullptr, nullptr, 0, nullptr, out_f32 ? 1 : 0};
+  if (dt == kBF16) return g256::launch<bf16_t, true>(p, stream, tile, bk, nullptr, groups);
+  if (dt == kF16) return g256::launch<half_t, true>(p, stream, tile, bk, nullptr, groups);
+  return (int)hipErrorInvalidValue;
+}
+
+// grouped conv weight gradient: dw [groups*cog][cig][KH][KW] from dy [N*OH*OW][groups*cog] and x
+// [N, H, W, groups*cig]; ws >= groups * splits * cog * KH*KW*cig floats, splits <= 32
+PHA_API int pha_conv256_wgrad_grouped(int dt, const void* dy, const void* x, void* dw, float* ws, int N, int H, int W,
+                                      int cig, int cog, int groups, int KH, int KW, int sh, int sw, int ph, int pw,
+                                      int dh, int dw_, int out_f32, const void* zero16, int tile, int splits,
+                                      hipStream_t stream) {
+  if (cig % 8 || cog % 8 || groups < 1 || splits > 32) return (int)hipErrorInvalidValue;
+  g256::ConvGeo g{N, H, W, cig, (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, (W + 2 * pw - dw_ * (KW - 1) - 1) / sw + 1,
+                  KH, KW, sh, sw, ph, pw, dh, dw_, 0, 0, 0, 0, 0, 0, 0};
+  g.cs = cig * groups;
+  g.ga = cig;
+  g.gc = cog;
+  const long K = (long)N * g.OH * g.OW;
+  g256::TnArgs p{dy, x, ws, (long)cog, (long)KH * KW * cig, K, (long)cog * groups, (long)cig, 0, 1, zero16, g};
+  if (dt == kBF16) return g256::launch_tn<bf16_t, true>(p, dw, out_f32, cig, 0, tile, splits, stream, groups);
+  if (dt == kF16) return g256::launch_tn<half_t, true>(p, dw, out_f32, cig, 0, tile, splits, stream, groups);
   return (int)hipErrorInvalidValue;
 }
 

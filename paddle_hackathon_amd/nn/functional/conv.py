@@ -126,7 +126,10 @@ def _own_conv2d(t, w, bias, stride, padding, dilation, groups, data_format):
         wp = TF.pad(w, [0, 0, 0, 0, 0, 0, 0, -CO % 8])
         bp = None if bias is None else TF.pad(bias, [0, -CO % 8])
     dense = _hip_conv_ok(x, wp, groups) and (st == [1, 1] or dl == [1, 1])
-    if not dense and not _gc.ok(x, w, groups):
+    from ...ops import conv_gemm as _cgm
+    gmfma = (not dense and groups > 1 and w.shape[1] != 1
+             and (st == [1, 1] or dl == [1, 1]) and _cgm.grouped_ok(x, w, groups))
+    if not dense and not gmfma and not _gc.ok(x, w, groups):
         return None
     x = x.contiguous()
     if pre is not None:   # asymmetric ("SAME") padding: explicit zero rows / columns
@@ -136,6 +139,8 @@ def _own_conv2d(t, w, bias, stride, padding, dilation, groups, data_format):
         out = _hip_conv2d(x, wp, bp, st, pad, dl, groups)
         if out.shape[-1] != CO:
             out = out[..., :CO]
+    elif gmfma:   # grouped (ResNeXt-style) convs: one grouped implicit GEMM per pass on the matrix cores
+        out = _cgm.conv2d_nhwc256_grouped(x, w, bias, st, pad, dl, groups)
     else:
         out = _gc.conv2d_nhwc(x, w, bias, st, pad, dl, groups)
     return out.permute(0, 3, 1, 2) if nchw else out

@@ -239,6 +239,10 @@ def _L256():
         L.pha_conv256_fwd.restype = c_int
         L.pha_conv256_fwd_f32out.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
         L.pha_conv256_fwd_f32out.restype = c_int
+        L.pha_conv256_fwd_grouped.argtypes = [I, P, P, P, P] + [I] * 16 + [LG, I, P, I, I, P, P]
+        L.pha_conv256_fwd_grouped.restype = c_int
+        L.pha_conv256_wgrad_grouped.argtypes = [I, P, P, P, P] + [I] * 16 + [P, I, I, P]
+        L.pha_conv256_wgrad_grouped.restype = c_int
         L._g256_sig = True
     return L
 
@@ -634,6 +638,174 @@ class Conv2dNHWC256F32(torch.autograd.Function):
                                dilation, out_dtype=torch.float32)
         db = gy.sum((0, 1, 2)) if has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None
+
+
+# ----------------------------------------------------------------------------------------------
+# grouped convolutions (ResNeXt's 3x3 group convs) as ONE grouped implicit GEMM per pass: blockIdx.y
+# = group, each group's GEMM over its own input channels / filter rows / output columns
+# (gemm256.hip ConvGeo cs / ga / gb / gc). Groups narrower than 8 input channels are merged in
+# pairs / quads with block-diagonal zero filters (a few x the FLOPs of those small convs, on the
+# matrix cores instead of the VALU kernels).
+# ----------------------------------------------------------------------------------------------
+def _gfwd(x, w_g, groups, cig, cog, stride, padding, dilation, out=None, remap=None, bias=None):
+    """x [N, H, W, groups*cig], w_g [groups*cog, KH, KW, cig] -> y [N, OH, OW, groups*cog]"""
+    N, H, W, C = x.shape
+    _, KH, KW, _ = w_g.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    rm = None
+    if remap is not None:
+        oh0, ow0, osh, osw, OH, OW = remap[:6]
+        zr = int(len(remap) > 6 and bool(remap[6]))
+        rm = (c_int * 9)(out.shape[1], out.shape[2], oh0, ow0, osh, osw, OH, OW, zr)
+        y = out
+    else:
+        OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+        OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+        y = out if out is not None else torch.empty((N, OH, OW, groups * cog), dtype=x.dtype, device=x.device)
+    L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    rc = L.pha_conv256_fwd_grouped(_DT[x.dtype], _ptr(x), _ptr(w_g), _ptr(y), _ptr(bias), N, H, W, cig, cog, groups,
+                                   KH, KW, sh, sw, ph, pw, dh, dw, _ACT[None], y.shape[-1], 0, z, -1, 0, rm, st)
+    if rc != 0:
+        raise RuntimeError(f"pha_conv256_fwd_grouped failed ({rc})")
+    return y
+
+
+def _merge_groups(w, groups, m):
+    """[Co, cig, KH, KW] grouped filters -> [Co, cig*m, KH, KW] for groups / m groups, each merged
+    group's filter block-diagonal (zeros between the original groups)"""
+    Co, cig, KH, KW = w.shape
+    cog = Co // groups
+    wg = w.reshape(groups // m, m, cog, cig, KH, KW)
+    out = w.new_zeros(groups // m, m, cog, m, cig, KH, KW)
+    for i in range(m):
+        out[:, i, :, i] = wg[:, i]
+    return out.reshape(Co, m * cig, KH, KW)
+
+
+class GroupedConv2dNHWC256(torch.autograd.Function):
+    """grouped NHWC conv2d: forward, dgrad (flipped / phase filters, grouped) and wgrad (grouped TN
+    with per-group split-K slabs) on the 256-tile MFMA kernels"""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation, groups):
+        Co, cig, KH, KW = weight.shape
+        cog = Co // groups
+        ctx.save_for_backward(x)
+        ctx.weight, ctx.conf = weight, (stride, padding, dilation, groups, bias is not None)
+        wg = _wlayout(weight, ("gfwd", groups), lambda t: t.permute(0, 2, 3, 1).contiguous())
+        y = _gfwd(x.contiguous(), wg, groups, cig, cog, stride, padding, dilation)
+        return y.add_(bias.to(y.dtype)) if bias is not None else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, = ctx.saved_tensors
+        w = ctx.weight
+        stride, padding, dilation, groups, has_bias = ctx.conf
+        Co, cig, KH, KW = w.shape
+        cog = Co // groups
+        gy = gy.contiguous()
+        N, H, W, C = x.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _gdgrad(gy, w, (N, H, W, C), stride, padding, dilation, groups)
+        if ctx.needs_input_grad[1]:
+            dw = _gwgrad(gy, x.contiguous(), w.shape, stride, padding, dilation, groups)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = gy.float().sum((0, 1, 2)).to(gy.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+def _gdgrad(dy, w, x_shape, stride, padding, dilation, groups):
+    N, H, W, C = x_shape
+    Co, cig, KH, KW = w.shape
+    cog = Co // groups
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+
+    def gt(t):   # [Co, cig, kh, kw] (taps already selected / flipped) -> [groups*cig, kh, kw, cog]
+        g_, kh, kw = groups, t.shape[2], t.shape[3]
+        return t.reshape(g_, cog, cig, kh, kw).permute(0, 2, 3, 4, 1).reshape(g_ * cig, kh, kw, cog).contiguous()
+    if (sh, sw) == (1, 1):
+        wt = _wlayout(w, ("gdgrad", groups), lambda t: gt(t.flip(2, 3)))
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        return _gfwd(dy, wt, groups, cog, cig, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
+                     remap=(0, 0, 1, 1, H, W))
+    if (dh, dw) != (1, 1):
+        raise NotImplementedError("strided + dilated grouped conv dgrad")
+    phases = []
+    for rh in range(sh):
+        for rw in range(sw):
+            PH, PW = len(range(rh, H, sh)), len(range(rw, W, sw))
+            kh0, kw0 = (rh + ph) % sh, (rw + pw) % sw
+            khs, kws = list(range(kh0, KH, sh)), list(range(kw0, KW, sw))
+            phases.append((rh, rw, PH, PW, khs, kws, kh0, kw0))
+    live = [p for p in phases if p[2] and p[3] and p[4] and p[5]]
+    zero_rest = len(live) == 1 and live[0][:2] == (0, 0) and live[0][2] * sh >= H and live[0][3] * sw >= W \
+        and cig % 8 == 0
+    full = len(live) == len(phases) or zero_rest
+    dx = (torch.empty if full else torch.zeros)(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    for rh, rw, PH, PW, khs, kws, kh0, kw0 in live:
+        bh, bw = (rh + ph - kh0) // sh, (rw + pw - kw0) // sw
+        nh, nw = len(khs), len(kws)
+        wt = _wlayout(w, ("gphase", groups, rh, rw, sh, sw, ph, pw), lambda t, kh0=kh0, kw0=kw0:
+                      gt(t[:, :, kh0::sh, :][:, :, :, kw0::sw].flip((2, 3))))
+        _gfwd(dy, wt, groups, cog, cig, (1, 1), (nh - 1 - bh, nw - 1 - bw), (1, 1), out=dx,
+              remap=(rh, rw, sh, sw, PH, PW, zero_rest))
+    return dx
+
+
+def _gwgrad(dy, x, w_shape, stride, padding, dilation, groups):
+    Co, cig, KH, KW = w_shape
+    cog = Co // groups
+    N, H, W, C = x.shape
+    _, OH, OW, _ = dy.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    out = torch.empty(Co, cig, KH, KW, dtype=dy.dtype, device=dy.device)
+    M, Nn, K = cog, KH * KW * cig, N * OH * OW
+    sp = max(1, min(32, K // 32 // 8, -(-2 * _num_cus(dy.device) // max(1, groups * -(-M // 128) * -(-Nn // 128)))))
+    ws = torch.empty(groups * sp * M * Nn, dtype=torch.float32, device=dy.device)
+    L, z, st = _L256(), _ptr(_zero_page(x.device)), c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    rc = L.pha_conv256_wgrad_grouped(_DT[dy.dtype], _ptr(dy), _ptr(x), _ptr(out), _ptr(ws), N, H, W, cig, cog, groups,
+                                     KH, KW, sh, sw, ph, pw, dh, dw, 0, z, -1, sp, st)
+    if rc != 0:
+        raise RuntimeError(f"pha_conv256_wgrad_grouped failed ({rc})")
+    return out
+
+
+def grouped_ok(x, w, groups):
+    """bf16 / fp16 grouped convs the grouped implicit GEMM takes (after merging narrow groups)"""
+    import os
+    if os.environ.get("PHA_GCONV_MFMA", "1") == "0" or groups <= 1 or w.dtype != x.dtype \
+            or x.dtype not in (torch.bfloat16, torch.float16) or not x.is_cuda:
+        return False
+    Co, cig = w.shape[0], w.shape[1]
+    if Co % groups or cig * groups != x.shape[-1]:
+        return False
+    cog = Co // groups
+    m = _merge_factor(cig, cog, groups)
+    return m is not None and cig * m >= 8
+
+
+def _merge_factor(cig, cog, groups):
+    """smallest m (dividing groups) with cig*m and cog*m multiples of 8"""
+    for m in (1, 2, 4, 8):
+        if groups % m == 0 and (cig * m) % 8 == 0 and (cog * m) % 8 == 0:
+            return m
+    return None
+
+
+def conv2d_nhwc256_grouped(x, weight, bias, stride, padding, dilation, groups):
+    Co, cig = weight.shape[0], weight.shape[1]
+    m = _merge_factor(cig, Co // groups, groups)
+    if m > 1:   # narrow groups: merge m of them with block-diagonal filters (autograd through the merge)
+        weight = _merge_groups(weight, groups, m)
+        groups //= m
+    return GroupedConv2dNHWC256.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation), groups)
 
 
 def conv2d_nhwc256_f32(x, weight, bias, stride, padding, dilation):

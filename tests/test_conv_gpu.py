@@ -180,3 +180,41 @@ def test_conv2d_transpose_own_kernels(case, fmt):
     _close(gx, xr.grad, dt, "dx")
     _close(wa._t.grad, wr.grad, dt, "dw")
     _close(ba._t.grad, br.grad, dt, "db")
+
+
+@pytest.mark.parametrize("cfg", [
+    # N, C, H, W, Co, groups, k, stride, pad
+    (4, 128, 14, 14, 128, 32, 3, 1, 1),    # ResNeXt 32x4d stage 1 (cig 4: groups merged in pairs)
+    (4, 256, 14, 14, 256, 32, 3, 2, 1),    # cig 8, strided
+    (2, 512, 7, 7, 512, 32, 3, 1, 1),      # cig 16
+    (2, 64, 9, 9, 128, 2, 3, 1, 1),        # few wide groups
+])
+def test_grouped_conv_mfma(cfg):
+    """grouped convolutions on the grouped implicit GEMM (forward, dgrad, wgrad) vs fp32 torch"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    N, C, H, W, Co, g, k, s, p = cfg
+    paddle.set_device("gpu")
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Co, C // g, k, k, device="cuda") * (2.0 / (C // g * k * k)) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Co, device="cuda").to(torch.bfloat16)
+    px, pw, pb = paddle.to_tensor(x), paddle.to_tensor(w), paddle.to_tensor(b)
+    for t in (px, pw, pb):
+        t.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.conv2d(px, pw, pb, stride=s, padding=p, groups=g, data_format="NHWC")
+    gy = torch.randn(tuple(y.shape), device="cuda").to(torch.bfloat16)
+    y.backward(paddle.to_tensor(gy))
+    torch.cuda.synchronize()
+    assert fallback.total() == 0, fallback.counts()
+    xd, wd, bd = (t.detach().float().requires_grad_() for t in (x, w, b))
+    ref = torch.nn.functional.conv2d(xd.permute(0, 3, 1, 2), wd, bd, stride=s, padding=p, groups=g).permute(0, 2, 3, 1)
+    ref.backward(gy.float())
+
+    def rel(a, r):
+        return ((a.float() - r).norm() / r.norm()).item()
+    assert rel(y._t, ref) < 1e-2
+    assert rel(px.grad._t, xd.grad) < 1e-2
+    assert rel(pw.grad._t, wd.grad) < 1e-2
+    assert rel(pb.grad._t, bd.grad) < 1e-2

@@ -891,3 +891,20 @@ def test_conv3d_depth_tap_decomposition(monkeypatch):
         torch.testing.assert_close(out, ref)
     out = C._conv3d_as_2d(x, w, None, 1, 2, [2, 1, 1], 1, "NCDHW")
     torch.testing.assert_close(out, TF.conv3d(x, w, None, 1, 2, [2, 1, 1]))
+
+
+def test_grouped_conv_merge_is_block_diagonal():
+    """ops/conv_gemm.py _merge_groups: m narrow groups merged into one with block-diagonal filters
+    compute the same convolution (what lets cig = 4 groups run on the grouped MFMA GEMM)"""
+    import torch
+    import torch.nn.functional as TF
+    from paddle_hackathon_amd.ops.conv_gemm import _merge_groups, _merge_factor
+    torch.manual_seed(0)
+    x = torch.randn(2, 128, 7, 7, dtype=torch.float64)
+    w = torch.randn(128, 4, 3, 3, dtype=torch.float64)
+    m = _merge_factor(4, 4, 32)
+    assert m == 2
+    ref = TF.conv2d(x, w, padding=1, groups=32)
+    got = TF.conv2d(x, _merge_groups(w, 32, m), padding=1, groups=16)
+    torch.testing.assert_close(got, ref)
+    assert _merge_factor(8, 8, 32) == 1 and _merge_factor(2, 2, 32) == 4 and _merge_factor(3, 3, 5) is None
