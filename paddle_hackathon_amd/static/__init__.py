@@ -236,17 +236,21 @@ def _as_list(v):
 
 
 def serialize_program(feed_vars, fetch_vars, **kwargs):
-    """ProgramDesc bytes (framework.proto wire format; static/serialize.py)"""
+    """ProgramDesc bytes (framework.proto wire format; static/serialize.py). ``training=True``: the
+    whole training program (reference <type>_grad and optimizer ops, static/ref_train.py), which
+    loads back with ``deserialize_program`` + ``deserialize_persistables`` and keeps training"""
     from .serialize import serialize_program_bytes
     program = kwargs.get("program") or default_main_program()
-    return serialize_program_bytes(program, _as_list(feed_vars), _as_list(fetch_vars))
+    return serialize_program_bytes(program, _as_list(feed_vars), _as_list(fetch_vars), kwargs.get("training", False))
 
 
 def serialize_persistables(feed_vars, fetch_vars, executor=None, **kwargs):
-    """the persistables the pruned program reads, as one save_combine stream sorted by name"""
+    """the persistables the (pruned) program reads, as one save_combine stream sorted by name;
+    ``training=True``: those of the whole training program, optimizer accumulators included"""
     from .serialize import serialize_persistables_bytes
     program = kwargs.get("program") or default_main_program()
-    return serialize_persistables_bytes(program, _as_list(feed_vars), _as_list(fetch_vars))
+    return serialize_persistables_bytes(program, _as_list(feed_vars), _as_list(fetch_vars),
+                                        kwargs.get("training", False))
 
 
 def deserialize_program(data):

@@ -1,0 +1,212 @@
+"""Writing a TRAINING Program as a reference ProgramDesc (reference: what append_backward and
+Optimizer.minimize leave in ``main_program.desc`` — per-op ``<type>_grad`` ops with the forward's
+input / output slots, ``<slot>@GRAD`` gradients, ``sum`` for gradient fan-in, ``fill_constant`` for
+the loss gradient, and one optimizer op per parameter (sgd / momentum / adam / adamw) whose state
+lives in persistable accumulators named ``{param}_{acc}_0``).
+
+The grad ops carry no kernels of their own here: static/ref_grad.py reads ``<type>_grad`` back by
+recomputing the forward op from its slots and taking the VJP, so a saved training program trains
+after loading (tests/test_program_desc.py)."""
+from __future__ import annotations
+
+import torch
+
+from ..framework.core import Tensor, _wrap
+from . import proto as pb
+
+__all__ = ["is_grad_op", "emit_grad", "emit_sum", "emit_fill_ones", "emit_assign", "emit_optimizer",
+           "is_optimizer_op"]
+
+
+def _bw():
+    from . import backward
+    return backward
+
+
+def is_grad_op(program, op):
+    return op.fn is _bw()._vjp and id(op) in program.__dict__.get("_grad_of", {})
+
+
+def is_optimizer_op(op):
+    return op.attrs.get("op_role") == "optimize" and "params" in op.kwargs and "optimizer" in op.attrs
+
+
+def _tensors(v):
+    if isinstance(v, Tensor):
+        return [v]
+    if isinstance(v, (list, tuple)):
+        out = []
+        for e in v:
+            out += _tensors(e)
+        return out
+    return []
+
+
+def fwd_slots(w, fop):
+    """(type, {slot: [tensors]} inputs, {slot: [Variables]} outputs, {attr: value}) of the forward op as
+    the writer emits it, or None when it has no reference form"""
+    from .serialize import _REF, _fluid_ref, _qual_short, _EXTRA_ATTRS, _iter_vars
+    from . import ref_emit
+    short = _qual_short(fop.type)
+    ref_op = fop.attrs.get("ref_op")
+    if ref_op is not None:
+        typ, r_ins, r_outs, r_attrs = ref_op
+        return typ, {k: list(v) for k, v in r_ins.items()}, {k: list(v) for k, v in r_outs.items()}, dict(r_attrs)
+    outs = list(_iter_vars(fop.outputs))
+    spec = ref_emit.spec(short, fop)
+    if spec is not None:
+        typ, slot_of, out_slots, attrs, extra = spec
+        ins = {}
+        for k, v in fop.kwargs.items():
+            if k in slot_of and _tensors(v):
+                ins.setdefault(slot_of[k], []).extend(_tensors(v))
+        for slot, t in extra.items():
+            if t is not None and not slot.startswith("@out:"):
+                ins.setdefault(slot, []).append(t)
+        if isinstance(out_slots, tuple) and len(out_slots) == len(outs):
+            o = {s: [v] for s, v in zip(out_slots, outs)}
+        else:
+            o = {out_slots if isinstance(out_slots, str) else out_slots[0]: outs}
+        return typ, ins, o, dict(attrs)
+    ref = _REF.get(short) or _fluid_ref(short)
+    if ref is None or fop.args:
+        return None
+    typ, slot_of, out_slot, attr_map = ref
+    ins, attrs = {}, {}
+    for k, v in fop.kwargs.items():
+        ts = _tensors(v)
+        if ts:
+            ins.setdefault(slot_of.get(k, k), []).extend(ts)
+        elif v is not None:
+            attrs[attr_map.get(k, k)] = v
+    attrs.update(_EXTRA_ATTRS.get(short, {}))
+    return typ, ins, {out_slot: outs}, attrs
+
+
+def emit_grad(w, program, op, msg, ins, outs):
+    """the reference <type>_grad op of a recorded grad op (static/backward.py _vjp)"""
+    from .serialize import _set_attr
+    fop = program.__dict__["_grad_of"][id(op)]
+    spec = fwd_slots(w, fop)
+    if spec is None:
+        raise NotImplementedError(f"training program: {fop.type} has no reference op type, so its grad op "
+                                  "cannot be written")
+    typ, f_ins, f_outs, attrs = spec
+    msg.type = typ + "_grad"
+    slot_of_in = {}
+    for slot, ts in f_ins.items():
+        ins[slot] = [w.tensor_name(t) for t in ts]
+        for t in ts:
+            slot_of_in.setdefault(id(t), slot)
+    out_slot_of = {}
+    for slot, vs in f_outs.items():
+        ins[slot] = [w.tensor_name(v) for v in vs]   # Out etc.: the output-based grad makers read it
+        for v in vs:
+            out_slot_of[id(v)] = slot
+    for o, g in zip(op.kwargs["outs"], op.kwargs["gouts"]):
+        if g is None or id(o) not in out_slot_of:
+            continue
+        ins.setdefault(out_slot_of[id(o)] + "@GRAD", []).append(w.tensor_name(g))
+    for v, g in zip(op.kwargs["ins"], op.outputs):
+        slot = slot_of_in.get(id(v))
+        if slot is None:
+            raise NotImplementedError(f"training program: {fop.type}_grad: input {getattr(v, 'name', v)} has no slot")
+        if len(f_ins[slot]) > 1:
+            raise NotImplementedError(f"training program: {typ}_grad of a list slot {slot}")
+        outs[slot + "@GRAD"] = [w.tensor_name(g)]
+    for k, v in attrs.items():
+        _set_attr(msg, k, v)
+    _set_attr(msg, "op_role", 1)
+
+
+def emit_sum(w, op, msg, ins, outs):
+    from .serialize import _set_attr
+    msg.type = "sum"
+    ins["X"] = [w.tensor_name(t) for t in op.kwargs["xs"]]
+    outs["Out"] = [w.tensor_name(op.outputs)]
+    _set_attr(msg, "op_role", 1)
+
+
+def emit_assign(w, op, msg, ins, outs):
+    from .serialize import _set_attr
+    msg.type = "assign"
+    ins["X"] = [w.tensor_name(op.kwargs["x"])]
+    outs["Out"] = [w.tensor_name(op.outputs)]
+    _set_attr(msg, "op_role", 1)
+
+
+def emit_fill_ones(w, op, msg, ins, outs):
+    """the loss gradient: fill_constant of the loss's shape (the reference's op_role 257)"""
+    from .serialize import _set_attr
+    x = op.kwargs["x"]
+    msg.type = "fill_constant"
+    outs["Out"] = [w.tensor_name(op.outputs)]
+    shape = [int(s) for s in (x._t.shape or [1])]
+    _set_attr(msg, "shape", shape)
+    _set_attr(msg, "value", 1.0)
+    _set_attr(msg, "dtype", pb.vartype_of(x._t.dtype))
+    _set_attr(msg, "op_role", 257)
+
+
+def _named(t, name):
+    t.name = name
+    t._pha_persist_name = True
+    return t
+
+
+def emit_optimizer(w, op, block_msg):
+    """one reference optimizer op per parameter; the state tensors are the optimizer's own
+    accumulators (created if the optimizer has not stepped yet), saved as persistables"""
+    from .serialize import _set_attr
+    opt = op.attrs["optimizer"]
+    kind = type(opt).__name__.lower()
+    kind = kind[:-len("optimizer")] if kind.endswith("optimizer") else kind
+    if kind not in ("sgd", "momentum", "adam", "adamw"):
+        raise NotImplementedError(f"training program: optimizer {type(opt).__name__} has no reference op here")
+    if op.kwargs.get("found_inf") is not None:
+        raise NotImplementedError("training program: AMP loss scaling is not written as reference ops")
+    lr_val = float(opt.get_lr()) if hasattr(opt, "get_lr") else 0.01
+    cache = w.__dict__.setdefault("_lr_tensor", {})
+    lr = cache.get(lr_val)
+    if lr is None:
+        lr = cache[lr_val] = _named(_wrap(torch.tensor([lr_val], dtype=torch.float32)),
+                                    f"learning_rate_{len(cache)}")
+    for p, g in zip(op.kwargs["params"], op.kwargs["grads"]):
+        msg = block_msg.ops.add()
+        ins = {"Param": [w.tensor_name(p)], "Grad": [w.tensor_name(g)], "LearningRate": [w.tensor_name(lr)]}
+        outs = {"ParamOut": [w.tensor_name(p)]}
+        if kind == "sgd":
+            msg.type = "sgd"
+        elif kind == "momentum":
+            msg.type = "momentum"
+            vel = opt._acc("velocity", p)
+            ins["Velocity"] = outs["VelocityOut"] = [w.tensor_name(_named(vel, vel.name))]
+            _set_attr(msg, "mu", float(getattr(opt, "_momentum", 0.9)))
+            _set_attr(msg, "use_nesterov", bool(getattr(opt, "_use_nesterov", False)))
+        else:
+            msg.type = kind
+            b1, b2 = float(getattr(opt, "_beta1", 0.9)), float(getattr(opt, "_beta2", 0.999))
+            accs = {"Moment1": opt._acc("moment1", p), "Moment2": opt._acc("moment2", p),
+                    "Beta1Pow": opt._acc("beta1_pow_acc", p, fill=b1, shape=[1]),
+                    "Beta2Pow": opt._acc("beta2_pow_acc", p, fill=b2, shape=[1])}
+            for slot, t in accs.items():
+                ins[slot] = [w.tensor_name(_named(t, t.name))]
+                outs[slot + "Out"] = ins[slot]
+            _set_attr(msg, "beta1", b1)
+            _set_attr(msg, "beta2", b2)
+            _set_attr(msg, "epsilon", float(getattr(opt, "_epsilon", 1e-8)))
+            if kind == "adamw":
+                coeff = getattr(opt, "_coeff", None)
+                if coeff is None:
+                    coeff = getattr(opt, "_weight_decay", 0.01)
+                _set_attr(msg, "coeff", float(coeff if isinstance(coeff, (int, float)) else 0.01))
+                _set_attr(msg, "with_decay", True)
+        _set_attr(msg, "op_role", 2)
+        for slot, names in ins.items():
+            v = msg.inputs.add()
+            v.parameter = slot
+            v.arguments.extend(names)
+        for slot, names in outs.items():
+            v = msg.outputs.add()
+            v.parameter = slot
+            v.arguments.extend(names)

@@ -210,7 +210,8 @@ class _Writer:
             return t.name
         n = self._pname.get(id(t))
         if n is None:
-            n = t.name if isinstance(t, Parameter) and t.name and t.name not in self.persist \
+            named = isinstance(t, Parameter) or getattr(t, "_pha_persist_name", False)   # params, optimizer state
+            n = t.name if named and t.name and t.name not in self.persist \
                 else f"_pha_const_{len(self._pname)}"
             self._pname[id(t)] = n
             self.persist[n] = t
@@ -260,7 +261,16 @@ class _Writer:
     def op(self, op, msg):
         ins, outs = {}, {}
         short = _qual_short(op.type)
-        if op.exec is not None:
+        from . import backward as _bw, ref_train as _rt
+        if getattr(self, "train", False) and _rt.is_grad_op(self.program, op):
+            _rt.emit_grad(self, self.program, op, msg, ins, outs)
+        elif getattr(self, "train", False) and op.fn is _bw._sum:
+            _rt.emit_sum(self, op, msg, ins, outs)
+        elif getattr(self, "train", False) and op.fn is _bw._fill_ones:
+            _rt.emit_fill_ones(self, op, msg, ins, outs)
+        elif getattr(self, "train", False) and op.type == "assign" and op.attrs.get("op_role") == "backward":
+            _rt.emit_assign(self, op, msg, ins, outs)
+        elif op.exec is not None:
             self._cf_op(op, msg, ins, outs)
         elif op.attrs.get("ref_op") is not None:
             typ, r_ins, r_outs, r_attrs = op.attrs["ref_op"]
@@ -372,9 +382,13 @@ def _var_desc(blk_msg, name, t, persistable=False, is_param=False, shape=None, n
     return vd
 
 
-def program_to_desc(program, feed_vars, fetch_vars):
-    """-> (ProgramDesc message, {persistable name: Tensor})"""
+def program_to_desc(program, feed_vars, fetch_vars, train=False):
+    """-> (ProgramDesc message, {persistable name: Tensor}); ``train``: the whole training program —
+    backward ops as reference <type>_grad ops and one reference optimizer op per parameter
+    (static/ref_train.py) — instead of the pruned forward"""
+    from . import ref_train as _rt
     w = _Writer(program)
+    w.train = train
     desc = pb.ProgramDesc()
     desc.version.version = 0
     blocks = []
@@ -398,11 +412,14 @@ def program_to_desc(program, feed_vars, fetch_vars):
         w.var_block[id(v)] = (0, v)
     for b in program.blocks:
         ops = b.ops
-        if b.idx == 0:
+        if b.idx == 0 and not train:
             ops = prune_ops(ops, [v for v in fetch_vars if isinstance(v, Variable)])
         for op in ops:
-            if is_train_op(op):
-                continue   # backward / optimizer steps are not part of a saved program
+            if is_train_op(op) and not train:
+                continue   # backward / optimizer steps are not part of a saved inference program
+            if train and _rt.is_optimizer_op(op):
+                _rt.emit_optimizer(w, op, blocks[b.idx])
+                continue
             w.op(op, blocks[b.idx].ops.add())
             for v in _iter_vars(op.outputs):
                 w.var_block.setdefault(id(v), (b.idx, v))
@@ -867,13 +884,13 @@ _CONVERT.setdefault("depthwise_conv2d", _conv_conv2d)
 
 
 # ------------------------------------------------------------------------------- byte-level API
-def serialize_program_bytes(program, feed_vars, fetch_vars):
-    desc, _ = program_to_desc(program, feed_vars, fetch_vars)
+def serialize_program_bytes(program, feed_vars, fetch_vars, train=False):
+    desc, _ = program_to_desc(program, feed_vars, fetch_vars, train)
     return desc.SerializeToString()
 
 
-def serialize_persistables_bytes(program, feed_vars, fetch_vars):
-    _, persist = program_to_desc(program, feed_vars, fetch_vars)
+def serialize_persistables_bytes(program, feed_vars, fetch_vars, train=False):
+    _, persist = program_to_desc(program, feed_vars, fetch_vars, train)
     return b"".join(pb.tensor_to_stream(persist[n]._t) for n in sorted(persist))
 
 

@@ -896,3 +896,50 @@ def test_reference_training_program_optimizers(tmp_path, opt):
             v = 0.9 * v + gw
             w = w - 0.05 * v
         np.testing.assert_allclose(np.asarray(wv), w, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam", "momentum"])
+def test_training_program_round_trip(opt):
+    """a static training program (fc -> relu -> fc -> square error -> mean; backward; optimizer)
+    serialised WHOLE — backward as reference <type>_grad ops, the optimizer as one reference op per
+    parameter with its accumulators as persistables (static/ref_train.py) — loads back and keeps
+    training exactly like the original program"""
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [-1, 6], "float32")
+            y = paddle.static.data("y", [-1, 1], "float32")
+            h = paddle.nn.functional.relu(paddle.static.nn.fc(x, 8))
+            pred = paddle.static.nn.fc(h, 1)
+            loss = paddle.mean(paddle.square(pred - y))
+            o = {"sgd": lambda: paddle.optimizer.SGD(0.05),
+                 "adam": lambda: paddle.optimizer.Adam(0.01),
+                 "momentum": lambda: paddle.optimizer.Momentum(0.05, 0.9)}[opt]()
+            o.minimize(loss)
+        exe = paddle.static.Executor()
+        exe.run(start)
+        rs = np.random.RandomState(0)
+        batches = [(rs.randn(5, 6).astype("float32"), rs.randn(5, 1).astype("float32")) for _ in range(5)]
+        for xb, yb in batches[:2]:
+            exe.run(main, feed={"x": xb, "y": yb}, fetch_list=[loss])
+        pbytes = paddle.static.serialize_program([x, y], [loss], program=main, training=True)
+        sbytes = paddle.static.serialize_persistables([x, y], [loss], program=main, training=True)
+        desc = pb.ProgramDesc()
+        desc.ParseFromString(pbytes)
+        types = [o_.type for o_ in desc.blocks[0].ops]
+        assert "fc_grad" in types and "relu_grad" in types and types.count(opt) == 4, types
+        assert not [t for t in types if t.startswith("paddle_hackathon_amd.")], types
+        ref = [float(np.asarray(exe.run(main, feed={"x": xb, "y": yb}, fetch_list=[loss])[0]).reshape(-1)[0])
+               for xb, yb in batches[2:]]
+        ref_params = {p.name: p.numpy().copy() for p in main.all_parameters()}
+        stub = paddle.static.deserialize_program(pbytes)
+        prog = paddle.static.deserialize_persistables(stub, sbytes)
+        got = [float(np.asarray(exe.run(prog, feed={"x": xb, "y": yb}, fetch_list=stub.fetches)[0]).reshape(-1)[0])
+               for xb, yb in batches[2:]]
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-7)
+        loaded = {t.name: t for t in prog.all_parameters()}
+        for n, v in ref_params.items():
+            np.testing.assert_allclose(loaded[n].numpy(), v, rtol=1e-5, atol=1e-6)
+    finally:
+        paddle.disable_static()
