@@ -302,6 +302,7 @@ struct GraphTable {
 struct Server {
   int listen_fd = -1, port = 0;
   std::atomic<bool> stopping{false};
+  std::atomic<int> busy{0};   // requests read and not yet answered
   std::thread accept_thr;
   std::mutex conn_mu;
   std::vector<std::thread> conns;
@@ -448,6 +449,7 @@ void handle(Server* s, int fd) {
     if (h.nbytes && !read_full(fd, in.data(), h.nbytes)) break;
     out.clear();
     int32_t status = 0;
+    ++s->busy;
     switch (h.cmd) {
       case PING:
         break;
@@ -788,6 +790,10 @@ void handle(Server* s, int fd) {
         break;
       }
       case STOP: {
+        // let the other connections' in-flight requests answer first (a trainer released from the
+        // final barrier may not have its reply yet; the stop shuts every connection down), bounded
+        // so a trainer stuck in a barrier that can never complete does not hold the server
+        for (int i = 0; i < 10000 && s->busy.load() > 1; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(1));
         s->stopping = true;
         s->wake_all();
         if (s->listen_fd >= 0) ::shutdown(s->listen_fd, SHUT_RDWR);
@@ -799,7 +805,9 @@ void handle(Server* s, int fd) {
         status = -100;
     }
     const RespHdr r{status, 0, out.size()};
-    if (!write_full(fd, &r, sizeof(r)) || (!out.empty() && !write_full(fd, out.data(), out.size()))) break;
+    const bool sent = write_full(fd, &r, sizeof(r)) && (out.empty() || write_full(fd, out.data(), out.size()));
+    --s->busy;
+    if (!sent) break;
   }
   ::close(fd);
 }

@@ -239,9 +239,9 @@ def _L256():
         L.pha_conv256_fwd.restype = c_int
         L.pha_conv256_fwd_f32out.argtypes = [I, P, P, P, P] + [I] * 13 + [I, P, I, I, P, P]
         L.pha_conv256_fwd_f32out.restype = c_int
-        L.pha_conv256_fwd_grouped.argtypes = [I, P, P, P, P] + [I] * 16 + [LG, I, P, I, I, P, P]
+        L.pha_conv256_fwd_grouped.argtypes = [I, P, P, P, P] + [I] * 15 + [LG, I, P, I, I, P, P]
         L.pha_conv256_fwd_grouped.restype = c_int
-        L.pha_conv256_wgrad_grouped.argtypes = [I, P, P, P, P] + [I] * 16 + [P, I, I, P]
+        L.pha_conv256_wgrad_grouped.argtypes = [I, P, P, P, P] + [I] * 15 + [P, I, I, P]
         L.pha_conv256_wgrad_grouped.restype = c_int
         L._g256_sig = True
     return L

@@ -232,6 +232,10 @@ def _launch_ps(a):
                     rc = p.returncode
                     raise KeyboardInterrupt
             time.sleep(0.2)
+        for r, p in enumerate(trn):   # the last trainers may have exited together, some failing
+            if p.returncode not in (None, 0):
+                print(f"[launch] trainer {r} exited with {p.returncode}", file=sys.stderr)
+                rc = rc or p.returncode
         deadline = time.time() + 30
         while any(p.poll() is None for p in srv) and time.time() < deadline:
             time.sleep(0.2)

@@ -132,7 +132,7 @@ def test_conv3d_own_kernels(dtype, fmt):
     y = paddle.nn.functional.conv3d(px, pw, pb, stride=[2, 1, 1], padding=1, data_format=fmt)
     y.astype("float32").sum().backward()
     assert fallback.counts().get("conv3d", 0) == 0, fallback.counts()
-    xd, wd = x.to(dtype).double().requires_grad_(), w.to(dtype).double().requires_grad_()
+    xd, wd = x.detach().to(dtype).double().requires_grad_(), w.detach().to(dtype).double().requires_grad_()
     ref = torch.nn.functional.conv3d(xd, wd, b.to(dtype).double(), stride=[2, 1, 1], padding=1)
     ref.sum().backward()
     out = y._t.permute(0, 4, 1, 2, 3) if fmt == "NDHWC" else y._t

@@ -3,6 +3,7 @@ split3 / ops/gemm.py mm_f32) vs MIOpen / hipBLASLt fp32 (PHA_CONV_F32=library, P
 ResNet-50 NCHW training steps and square fp32 GEMMs.
 
   python tools/bench_fp32.py
+  python tools/bench_fp32.py resnet hip|library     (ResNet-50 only, one side)
 """
 import os
 import sys
@@ -60,6 +61,10 @@ def gemm_tf(impl, n):
 
 def main():
     paddle.set_device("gpu")
+    if len(sys.argv) > 2 and sys.argv[1] == "resnet":   # one side only (for rocprofv3)
+        ms, loss = resnet_ms(sys.argv[2])
+        print(f"resnet50 fp32 NCHW batch 64 conv/matmul={sys.argv[2]}: {ms:7.1f} ms/step loss {loss:.4f}")
+        return
     for n in (2048, 4096, 8192):
         for impl in ("hip", "library"):
             tf, err = gemm_tf(impl, n)
