@@ -243,6 +243,8 @@ def _L256():
         L.pha_conv256_fwd_grouped.restype = c_int
         L.pha_conv256_wgrad_grouped.argtypes = [I, P, P, P, P] + [I] * 15 + [P, I, I, P]
         L.pha_conv256_wgrad_grouped.restype = c_int
+        L.pha_split3_f32.argtypes = [P, P, LG, LG, I, P]
+        L.pha_split3_f32.restype = c_int
         L._g256_sig = True
     return L
 
@@ -536,7 +538,20 @@ _wlayouts = {}
 # conv_kernel.cu, cuDNN's fp32 / TF32 paths).
 # ----------------------------------------------------------------------------------------------
 def split3(t, dim, order="hhl"):
-    """fp32 t -> bf16 parts concatenated along ``dim`` in ``order`` (h = hi, l = lo)"""
+    """fp32 t -> bf16 parts concatenated along ``dim`` in ``order`` (h = hi, l = lo); one pass of
+    csrc/kernels/split.hip on the GPU"""
+    dim = dim % t.dim()
+    inner = t[(0,) * dim].numel() if t.numel() else 0
+    if (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and inner and inner % 8 == 0
+            and t.data_ptr() % 16 == 0 and _lib.native_available()):
+        shape = list(t.shape)
+        shape[dim] *= 3
+        out = torch.empty(shape, dtype=torch.bfloat16, device=t.device)
+        mask = sum(1 << i for i, c in enumerate(order) if c == "l")
+        rc = _L256().pha_split3_f32(_ptr(t), _ptr(out), t.numel() // inner, inner, mask,
+                                     c_void_p(torch.cuda.current_stream(t.device).cuda_stream))
+        if rc == 0:
+            return out
     hi = t.to(torch.bfloat16)
     lo = (t - hi.float()).to(torch.bfloat16)
     return torch.cat([hi if c == "h" else lo for c in order], dim)

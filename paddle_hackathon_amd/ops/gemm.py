@@ -468,8 +468,8 @@ def mm_f32(a, b):
     from .conv_gemm import split3, gemm256_tn
     M, K = a.shape
     N = b.shape[1]
-    at3 = split3(a.t(), 0, "hhl")        # [3K, M]
-    b3 = split3(b, 0, "hlh")             # [3K, N]
+    at3 = split3(a.t().contiguous(), 0, "hhl")        # [3K, M] (one transpose copy, then one split pass)
+    b3 = split3(b.contiguous(), 0, "hlh")             # [3K, N]
     pm, pn = -M % 8, -N % 8
     if pm:
         at3 = torch.nn.functional.pad(at3, [0, pm])

@@ -141,3 +141,18 @@ def test_conv3d_own_kernels(dtype, fmt):
     gx = px.grad._t.permute(0, 4, 1, 2, 3) if fmt == "NDHWC" else px.grad._t
     assert _rel(gx, xd.grad) < tol
     assert _rel(pw.grad._t, wd.grad) < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,dim,order", [((4, 6, 6, 24), 3, "hhl"), ((64, 40), 0, "hlh"), ((3, 5, 16), 1, "lhl")])
+def test_split3_kernel_matches_torch(shape, dim, order):
+    """csrc/kernels/split.hip: the one-pass fp32 -> [hi | lo] bf16 split equals the torch expression
+    bit for bit (round-to-nearest-even for both terms)"""
+    from paddle_hackathon_amd.ops import conv_gemm
+    torch.manual_seed(0)
+    t = torch.randn(*shape, device="cuda") * 100
+    got = conv_gemm.split3(t, dim, order)
+    hi = t.to(torch.bfloat16)
+    lo = (t - hi.float()).to(torch.bfloat16)
+    ref = torch.cat([hi if c == "h" else lo for c in order], dim)
+    assert got.shape == ref.shape and torch.equal(got.view(torch.int16), ref.view(torch.int16))
