@@ -65,6 +65,7 @@ struct FaStrides {
   long q_tok, kv_tok, o_tok, dq_tok, dkv_tok;
   int q_head, kv_head, o_head, dq_head, dkv_head;
   int order_g;   // key/query blocks of one (b, h) kept together on an XCD (see fa_block)
+  int prio = 0;  // 8-wave kernels' wave priorities: 0 none, 1 waves 0-3 high, 2 high while issuing MFMAs
 };
 
 __device__ __forceinline__ int v_lds_off(int row, int chunk) {  // 256-B rows, tr-read friendly XOR

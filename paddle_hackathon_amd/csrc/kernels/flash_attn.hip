@@ -561,6 +561,11 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  // wave priorities (fs.prio): the two waves of a SIMD (w, w + 4) otherwise reach their MFMA and
+  // softmax phases together after every barrier; a priority skew lets one wave's exp / pack VALU
+  // issue under the other's MFMAs
+  if (fs.prio == 1 && wid < 4) __builtin_amdgcn_s_setprio(1);
+  const bool dyn_prio = fs.prio == 2;
   for (int t = 0; t < ntile; ++t) {
     const int k0 = t * BN;
     const int cur = t & 1;
@@ -568,6 +573,7 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
     const unsigned char* kl = smem + cur * 2 * TILE;
     const unsigned char* vl = kl + TILE;
     if (!(CAUSAL && k0 > wave_qmax)) {
+      if (dyn_prio) __builtin_amdgcn_s_setprio(1);
       const bool need_mask = (k0 + BN > Sk) || (CAUSAL && k0 + BN - 1 > wave_q0);
       f32x16 s[2];
       s[0] = zero16();
@@ -600,6 +606,10 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (dyn_prio) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
+      }
       // scores unscaled (scale > 0: max(c s) = c max(s)); masked scores are -inf already
       float tmax = -INFINITY;
 #pragma unroll
@@ -631,6 +641,10 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
         }
       psum += __shfl_xor(psum, 32, 64);
       l_run += psum;
+      if (dyn_prio) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+      }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const f32x16& sv = s[ks >> 1];
@@ -647,6 +661,10 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
           const u32x2 hi = ds_read_tr16(vl + ks * 4096 + troff[db][1]);
           o[db] = MF<T>::mma(as_frag<frag>(u32x4{lo[0], lo[1], hi[0], hi[1]}), pf, o[db]);
         }
+      }
+      if (dyn_prio) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile has landed (asm: untracked)
@@ -1689,6 +1707,7 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v3(const T* __restrict__ Q, con
     __syncthreads();
   }
   const float mval = scale_log2 > 0.f ? -INFINITY : INFINITY;   // exp2(mval * c) = 0 for either sign
+  if (fs.prio != 0 && wid < 4) __builtin_amdgcn_s_setprio(1);   // see fa_fwd_v3_kernel
   for (int t = 0; t < ntile; ++t) {
     const int k0 = t * BN;
     const int cur = t & 1;
@@ -1940,6 +1959,11 @@ bool bwd_v2_enabled() {  // PHA_FA_BWD_V1=1 selects the 4-wave kernels (A/B comp
   return !(e && e[0] == '1');
 }
 
+int fa_prio() {  // PHA_FA_PRIO: 8-wave kernels' wave priorities (FaStrides::prio)
+  const char* e = getenv("PHA_FA_PRIO");
+  return e ? atoi(e) : 0;
+}
+
 int fa_order_g() {  // PHA_FA_ORDER_G: blocks of one (b, h) kept together per XCD (0 = plain order)
   const char* e = getenv("PHA_FA_ORDER_G");
   return e ? atoi(e) : 0;   // measured: G = 0 fastest (0.923 ms bwd; G = 4: 1.036 ms)
@@ -1957,6 +1981,7 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
   const float sl = scale * kLog2e;
   FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   fs.order_g = fa_order_g();
+  fs.prio = fa_prio();
   const bool v2 = D == 128 && fwd_v2_enabled() && scale > 0.f;   // v2 folds the scale into max / exp
   if (fsp && !v2) return (int)hipErrorInvalidValue;
   if (v2) {
@@ -1987,6 +2012,7 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
                hipStream_t st, const FaStrides* fsp = nullptr) {
   FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   fs.order_g = fa_order_g();
+  fs.prio = fa_prio();
   if (fsp && !(D == 128 && bwd_v2_enabled())) return (int)hipErrorInvalidValue;
   if (D == 128 && bwd_v2_enabled()) {
     const dim3 gk2(B * H, (Sk + NTKV / 2 - 1) / (NTKV / 2)), gq2(B * H, (S + BM2 - 1) / BM2), b2(NT2), bk(NTKV);

@@ -439,3 +439,74 @@ def spec(short, op):
         return f(op.kwargs)
     except (TypeError, ValueError):
         return None
+
+
+# ------------------------------------------------------------------------------- composites
+# calls whose reference static graph is SEVERAL ops (reference: the static branch of the Python
+# function appends them one by one): written as those ops with intermediate variables; in a
+# training program their grad op becomes the parts' grad ops in reverse order (static/ref_train.py)
+
+def _tmp_var(name, like, shape):
+    import torch
+    from .program import Variable
+    meta = torch.empty([1 if (s is None or s < 0) else int(s) for s in shape], dtype=like._t.dtype, device="meta")
+    return Variable(None, meta, name=name, declared_shape=[(-1 if s is None else int(s)) for s in shape])
+
+
+def _ce_composite(op):
+    """nn/functional/loss.py cross_entropy (static branch, hard labels, softmax, no weight or label
+    smoothing, ignore_index < 0): softmax_with_cross_entropy -> (Softmax, Loss), then the mean
+    (reduce_mean over all elements) or sum (reduce_sum)"""
+    kw = op.kwargs
+    if (op.args or kw.get("soft_label") or not kw.get("use_softmax", True) or kw.get("weight") is not None
+            or kw.get("label_smoothing", 0.0) or int(kw.get("ignore_index", -100)) >= 0
+            or kw.get("reduction", "mean") not in ("mean", "sum")):
+        return None
+    x, lab, out = kw.get("input"), kw.get("label"), op.outputs
+    if not (_is_t(x) and _is_t(lab)) or isinstance(out, (list, tuple)):
+        return None
+    axis = int(kw.get("axis", -1))
+    shape = list(getattr(x, "declared_shape", None) or x.shape)
+    lshape = list(shape)
+    lshape[axis] = 1
+    sm = _tmp_var(out.name + "@swce_softmax", x, shape)
+    loss = _tmp_var(out.name + "@swce_loss", x, lshape)
+    red = "reduce_mean" if kw.get("reduction", "mean") == "mean" else "reduce_sum"
+    return [("softmax_with_cross_entropy", {"Logits": [x], "Label": [lab]}, {"Softmax": [sm], "Loss": [loss]},
+             {"soft_label": False, "ignore_index": int(kw.get("ignore_index", -100)), "numeric_stable_mode": True,
+              "axis": axis, "use_softmax": True}),
+            (red, {"X": [loss]}, {"Out": [out]}, {"dim": [0], "keep_dim": False, "reduce_all": True})]
+
+
+COMPOSITE = {"nn.functional.loss.cross_entropy": _ce_composite}
+
+
+def composite(w, short, op):
+    """the op's parts [(type, {slot: [tensors]}, {slot: [Variables]}, attrs)] (cached per writer, so
+    the forward and its grad op see the same intermediates) or None"""
+    f = COMPOSITE.get(short)
+    if f is None:
+        return None
+    cache = w.__dict__.setdefault("_composite", {})
+    if id(op) not in cache:
+        cache[id(op)] = (op, f(op))
+    return cache[id(op)][1]
+
+
+def write_parts(w, parts, block_msg, role=None):
+    from .serialize import _set_attr
+    for typ, ins, outs, attrs in parts:
+        msg = block_msg.ops.add()
+        msg.type = typ
+        for k, v in attrs.items():
+            _set_attr(msg, k, v)
+        if role is not None:
+            _set_attr(msg, "op_role", role)
+        for slot, ts in ins.items():
+            s = msg.inputs.add()
+            s.parameter = slot
+            s.arguments.extend(w.tensor_name(t) for t in ts)
+        for slot, ts in outs.items():
+            s = msg.outputs.add()
+            s.parameter = slot
+            s.arguments.extend(w.tensor_name(t) for t in ts)

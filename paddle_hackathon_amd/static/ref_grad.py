@@ -62,6 +62,12 @@ def recompute_vjp(fwd_fn, fwd_kwargs, targets, douts):
             if l is not None:
                 g = next(it)
                 res[i] = _wrap(g if g is not None else torch.zeros_like(l))
+    seen = set()
+    for i, t in enumerate(targets):   # an input at several positions: its whole gradient once (the
+        if t is not None and id(t) in seen and res[i] is not None:   # writer sums the positions)
+            res[i] = _wrap(torch.zeros_like(_t(res[i])))
+        if t is not None:
+            seen.add(id(t))
     for i, t in enumerate(targets):   # integer inputs / unused: zeros of the input's shape
         if res[i] is None and t is not None:
             res[i] = _wrap(torch.zeros_like(_t(t), dtype=_t(t).dtype if _t(t).is_floating_point() else torch.float32))
@@ -197,6 +203,10 @@ def reshape_grad(dout, x_shape):
     return _wrap(_t(dout).reshape([int(v) for v in x_shape]))
 
 
+def reshape_like(dout, x):
+    return _wrap(_t(dout).reshape(_t(x).shape))
+
+
 def transpose_grad(dout, axis):
     inv = [0] * len(axis)
     for i, a in enumerate(axis):
@@ -230,9 +240,12 @@ def grad_converter(fwd_type, convert):
         return conv
     if fwd_type in ("reshape2", "squeeze2", "unsqueeze2", "flatten2"):
         def conv(r, ins, at):
-            xs = r.var(ins["XShape"][0])
-            shape = list(getattr(xs, "declared_shape", None) or xs.shape)[1:]
-            return reshape_grad, {"dout": _one(r, ins, "Out@GRAD"), "x_shape": shape}, "X@GRAD"
+            if "XShape" in ins:
+                xs = r.var(ins["XShape"][0])
+                shape = list(getattr(xs, "declared_shape", None) or xs.shape)[1:]
+                return reshape_grad, {"dout": _one(r, ins, "Out@GRAD"), "x_shape": shape}, "X@GRAD"
+            # no XShape (a program written here): the grad op carries the forward input X itself
+            return reshape_like, {"dout": _one(r, ins, "Out@GRAD"), "x": _one(r, ins, "X")}, "X@GRAD"
         return conv
     if fwd_type == "transpose2":
         def conv(r, ins, at):

@@ -45,7 +45,7 @@ def _tensors(v):
 def fwd_slots(w, fop):
     """(type, {slot: [tensors]} inputs, {slot: [Variables]} outputs, {attr: value}) of the forward op as
     the writer emits it, or None when it has no reference form"""
-    from .serialize import _REF, _fluid_ref, _qual_short, _EXTRA_ATTRS, _iter_vars
+    from .serialize import _REF, _fluid_ref, _qual_short, _EXTRA_ATTRS, _iter_vars, _derived_attrs
     from . import ref_emit
     short = _qual_short(fop.type)
     ref_op = fop.attrs.get("ref_op")
@@ -80,6 +80,7 @@ def fwd_slots(w, fop):
         elif v is not None:
             attrs[attr_map.get(k, k)] = v
     attrs.update(_EXTRA_ATTRS.get(short, {}))
+    attrs.update(_derived_attrs(short, fop.kwargs))
     return typ, ins, {out_slot: outs}, attrs
 
 
@@ -107,16 +108,39 @@ def emit_grad(w, program, op, msg, ins, outs):
         if g is None or id(o) not in out_slot_of:
             continue
         ins.setdefault(out_slot_of[id(o)] + "@GRAD", []).append(w.tensor_name(g))
-    for v, g in zip(op.kwargs["ins"], op.outputs):
-        slot = slot_of_in.get(id(v))
-        if slot is None:
+    # one gradient per input position ("@EMPTY@" where none is wanted); an input used at several
+    # positions (x * x) gets one partial per position, summed by a following `sum` op (the
+    # reference backward's @RENAME@ + sum)
+    want = {id(v): g for v, g in zip(op.kwargs["ins"], op.outputs)}
+    for v in op.kwargs["ins"]:
+        if id(v) not in slot_of_in:
             raise NotImplementedError(f"training program: {fop.type}_grad: input {getattr(v, 'name', v)} has no slot")
-        if len(f_ins[slot]) > 1:
-            raise NotImplementedError(f"training program: {typ}_grad of a list slot {slot}")
-        outs[slot + "@GRAD"] = [w.tensor_name(g)]
+    uses = {}
+    for ts in f_ins.values():
+        for t in ts:
+            uses[id(t)] = uses.get(id(t), 0) + 1
+    partials = {}
+    for slot, ts in f_ins.items():
+        names = []
+        for t in ts:
+            g = want.get(id(t))
+            if g is None:
+                names.append("@EMPTY@")
+            elif uses[id(t)] > 1:
+                from . import ref_emit
+                lst = partials.setdefault(id(t), (g, []))[1]
+                tmp = ref_emit._tmp_var(f"{w.tensor_name(g)}@RENAME@{len(lst)}", g, list(g.declared_shape or g.shape)
+                                        if hasattr(g, "declared_shape") else list(g.shape))
+                lst.append(tmp)
+                names.append(w.tensor_name(tmp))
+            else:
+                names.append(w.tensor_name(g))
+        if any(n != "@EMPTY@" for n in names):
+            outs[slot + "@GRAD"] = names
     for k, v in attrs.items():
         _set_attr(msg, k, v)
     _set_attr(msg, "op_role", 1)
+    w._pending_parts = [("sum", {"X": lst}, {"Out": [g]}, {}) for g, lst in partials.values()]
 
 
 def emit_sum(w, op, msg, ins, outs):
@@ -210,3 +234,40 @@ def emit_optimizer(w, op, block_msg):
             v = msg.outputs.add()
             v.parameter = slot
             v.arguments.extend(names)
+
+
+def emit_composite_grad(w, program, op, block_msg):
+    """the grad op of a call written as several reference ops (static/ref_emit.py COMPOSITE): the
+    parts' <type>_grad ops in reverse order, intermediate gradients as ``<name>@GRAD`` variables;
+    False when the forward call is not a composite"""
+    from . import ref_emit
+    from .serialize import _qual_short
+    fop = program.__dict__["_grad_of"][id(op)]
+    parts = ref_emit.composite(w, _qual_short(fop.type), fop)
+    if parts is None:
+        return False
+    grads = {id(o): g for o, g in zip(op.kwargs["outs"], op.kwargs["gouts"]) if g is not None}
+    want = {id(v): g for v, g in zip(op.kwargs["ins"], op.outputs)}
+    inter = {id(v) for _, _, outs, _ in parts for vs in outs.values() for v in vs} - \
+        {id(v) for v in _tensors(fop.outputs)}
+    gparts = []
+    for typ, ins, outs, attrs in reversed(parts):
+        g_ins = {slot: list(ts) for slot, ts in ins.items()}
+        for slot, vs in outs.items():
+            g_ins[slot] = list(vs)
+            gs = [grads[id(v)] for v in vs if id(v) in grads]
+            if gs:
+                g_ins[slot + "@GRAD"] = gs
+        g_outs = {}
+        for slot, ts in ins.items():
+            for t in ts:
+                if id(t) in want:
+                    g_outs.setdefault(slot + "@GRAD", []).append(want[id(t)])
+                elif id(t) in inter:
+                    gv = ref_emit._tmp_var(t.name + "@GRAD", t, list(t.declared_shape or t.shape))
+                    grads[id(t)] = gv
+                    g_outs.setdefault(slot + "@GRAD", []).append(gv)
+        if g_outs:
+            gparts.append((typ + "_grad", g_ins, g_outs, attrs))
+    ref_emit.write_parts(w, gparts, block_msg, role=1)
+    return True

@@ -106,6 +106,13 @@ def _fluid_ref(short):
     return (typ, _FLUID_SLOTS, "Out", {})
 
 
+def _derived_attrs(short, kw):
+    """reference attributes computed from our arguments (not a renaming)"""
+    if short in ("nn.functional.norm.batch_norm", "nn.functional.norm.batch_norm_act"):
+        return {"is_test": not kw.get("training", False)}
+    return {}
+
+
 _EXTRA_ATTRS = {
     "nn.functional.pooling.max_pool2d": {"pooling_type": "max"},
     "nn.functional.pooling.avg_pool2d": {"pooling_type": "avg"},
@@ -297,6 +304,8 @@ class _Writer:
                     _set_attr(msg, name, v)
             for k, v in _EXTRA_ATTRS.get(short, {}).items():
                 _set_attr(msg, k, v)
+            for k, v in _derived_attrs(short, op.kwargs).items():
+                _set_attr(msg, k, v)
             out_slot = ref[2] if ref else "Out"
             out_j = self.enc(op.outputs, out_slot, outs)
             _set_attr(msg, "__pha_fn__", op.type)
@@ -386,7 +395,7 @@ def program_to_desc(program, feed_vars, fetch_vars, train=False):
     """-> (ProgramDesc message, {persistable name: Tensor}); ``train``: the whole training program —
     backward ops as reference <type>_grad ops and one reference optimizer op per parameter
     (static/ref_train.py) — instead of the pruned forward"""
-    from . import ref_train as _rt
+    from . import ref_train as _rt, ref_emit
     w = _Writer(program)
     w.train = train
     desc = pb.ProgramDesc()
@@ -420,7 +429,19 @@ def program_to_desc(program, feed_vars, fetch_vars, train=False):
             if train and _rt.is_optimizer_op(op):
                 _rt.emit_optimizer(w, op, blocks[b.idx])
                 continue
+            if train and _rt.is_grad_op(program, op) and _rt.emit_composite_grad(w, program, op, blocks[b.idx]):
+                continue
+            parts = ref_emit.composite(w, _qual_short(op.type), op) if op.exec is None and \
+                op.attrs.get("ref_op") is None else None
+            if parts is not None:
+                ref_emit.write_parts(w, parts, blocks[b.idx])
+                for v in _iter_vars(op.outputs):
+                    w.var_block.setdefault(id(v), (b.idx, v))
+                continue
             w.op(op, blocks[b.idx].ops.add())
+            if getattr(w, "_pending_parts", None):   # e.g. the sum of a grad op's partial gradients
+                ref_emit.write_parts(w, w._pending_parts, blocks[b.idx], role=1)
+                w._pending_parts = None
             for v in _iter_vars(op.outputs):
                 w.var_block.setdefault(id(v), (b.idx, v))
     for i, v in enumerate(fetch_vars):
@@ -776,10 +797,15 @@ def _conv_pool2d(r, ins, at):
 
 
 def _conv_batch_norm(r, ins, at):
+    """batch_norm_op.cc: batch statistics (and running-stat updates with ``momentum``) unless
+    is_test / use_global_stats; a program written here carries our ``training`` flag as well"""
+    training = bool(at["training"]) if "training" in at else not at.get("is_test", False)
+    ugs = at.get("use_global_stats", None)
     return _fn("nn.functional.norm.batch_norm"), {
         "x": _one(r, ins, "X"), "running_mean": _one(r, ins, "Mean"), "running_var": _one(r, ins, "Variance"),
-        "weight": _one(r, ins, "Scale"), "bias": _one(r, ins, "Bias"), "training": False,
-        "epsilon": at.get("epsilon", 1e-5), "data_format": at.get("data_layout", "NCHW")}, "Y"
+        "weight": _one(r, ins, "Scale"), "bias": _one(r, ins, "Bias"), "training": training,
+        "momentum": at.get("momentum", 0.9), "epsilon": at.get("epsilon", 1e-5),
+        "data_format": at.get("data_layout", "NCHW"), "use_global_stats": ugs if ugs else None}, "Y"
 
 
 def _layer_norm_impl(x, scale=None, bias=None, epsilon=1e-5, begin_norm_axis=1):

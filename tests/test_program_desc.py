@@ -943,3 +943,57 @@ def test_training_program_round_trip(opt):
             np.testing.assert_allclose(loaded[n].numpy(), v, rtol=1e-5, atol=1e-6)
     finally:
         paddle.disable_static()
+
+
+def test_training_program_round_trip_conv_bn_ce():
+    """a conv -> batch_norm(relu) -> max-pool -> fc(tanh) -> layer_norm -> fc -> cross_entropy
+    classifier with Momentum, plus a squared-activation term (an input used twice by one op:
+    partial gradients + `sum`): written whole (cross_entropy as the reference's
+    softmax_with_cross_entropy + reduce_mean, batch_norm with is_test = False), loaded, and trained
+    on — losses and parameters follow the original program"""
+    paddle.enable_static()
+    try:
+        paddle.seed(3)
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [-1, 3, 8, 8], "float32")
+            y = paddle.static.data("y", [-1, 1], "int64")
+            h = paddle.static.nn.conv2d(x, 4, 3, padding=1)
+            h = paddle.static.nn.batch_norm(h, act="relu")
+            h = paddle.nn.functional.max_pool2d(h, 2)
+            h = paddle.reshape(h, [-1, 64])
+            h = paddle.static.nn.fc(h, 16, activation="tanh")
+            h = paddle.nn.functional.layer_norm(h, [16])
+            logits = paddle.static.nn.fc(h, 5)
+            loss = paddle.nn.functional.cross_entropy(logits, y) + 0.01 * paddle.mean(h * h)
+            paddle.optimizer.Momentum(0.05, 0.9).minimize(loss)
+        exe = paddle.static.Executor()
+        exe.run(start)
+        rs = np.random.RandomState(0)
+        batches = [(rs.randn(6, 3, 8, 8).astype("float32"), rs.randint(0, 5, (6, 1)).astype("int64"))
+                   for _ in range(5)]
+        exe.run(main, feed={"x": batches[0][0], "y": batches[0][1]}, fetch_list=[loss])
+        pbytes = paddle.static.serialize_program([x, y], [loss], program=main, training=True)
+        sbytes = paddle.static.serialize_persistables([x, y], [loss], program=main, training=True)
+        desc = pb.ProgramDesc()
+        desc.ParseFromString(pbytes)
+        types = [o.type for o in desc.blocks[0].ops]
+        for t in ("softmax_with_cross_entropy", "reduce_mean", "softmax_with_cross_entropy_grad", "batch_norm_grad",
+                  "conv2d_grad", "layer_norm_grad", "sum"):
+            assert t in types, (t, types)
+        assert types.count("momentum") == len(main.all_parameters())
+        bn = [o for o in desc.blocks[0].ops if o.type == "batch_norm"][0]
+        assert [a.b for a in bn.attrs if a.name == "is_test"] == [False]
+        ref = [float(np.asarray(exe.run(main, feed={"x": a, "y": b}, fetch_list=[loss])[0]).reshape(-1)[0])
+               for a, b in batches[1:]]
+        ref_params = {p.name: p.numpy().copy() for p in main.all_parameters()}
+        stub = paddle.static.deserialize_program(pbytes)
+        prog = paddle.static.deserialize_persistables(stub, sbytes)
+        got = [float(np.asarray(exe.run(prog, feed={"x": a, "y": b}, fetch_list=stub.fetches)[0]).reshape(-1)[0])
+               for a, b in batches[1:]]
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+        loaded = {t.name: t for t in prog.all_parameters()}
+        for n, v in ref_params.items():
+            np.testing.assert_allclose(loaded[n].numpy(), v, rtol=1e-4, atol=1e-6)
+    finally:
+        paddle.disable_static()
