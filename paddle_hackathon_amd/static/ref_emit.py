@@ -446,10 +446,11 @@ def spec(short, op):
 # function appends them one by one): written as those ops with intermediate variables; in a
 # training program their grad op becomes the parts' grad ops in reverse order (static/ref_train.py)
 
-def _tmp_var(name, like, shape):
+def _tmp_var(name, like, shape, dtype=None):
     import torch
     from .program import Variable
-    meta = torch.empty([1 if (s is None or s < 0) else int(s) for s in shape], dtype=like._t.dtype, device="meta")
+    meta = torch.empty([1 if (s is None or s < 0) else int(s) for s in shape], dtype=dtype or like._t.dtype,
+                       device="meta")
     return Variable(None, meta, name=name, declared_shape=[(-1 if s is None else int(s)) for s in shape])
 
 
@@ -478,7 +479,22 @@ def _ce_composite(op):
             (red, {"X": [loss]}, {"Out": [out]}, {"dim": [0], "keep_dim": False, "reduce_all": True})]
 
 
-COMPOSITE = {"nn.functional.loss.cross_entropy": _ce_composite}
+def _dropout_composite(op):
+    """dropout_op.cc: Out and the uint8 Mask (what dropout_grad multiplies by), is_test from our
+    ``training`` flag, implementation upscale_in_train / downgrade_in_infer"""
+    import torch
+    kw = op.kwargs
+    x, out, p = kw.get("x"), op.outputs, kw.get("p", 0.5)
+    if op.args or not _is_t(x) or kw.get("axis") is not None or _is_t(p) or isinstance(out, (list, tuple)):
+        return None
+    mode = kw.get("mode", "upscale_in_train")
+    mask = _tmp_var(out.name + "@dropout_mask", x, list(getattr(x, "declared_shape", None) or x.shape), torch.uint8)
+    return [("dropout", {"X": [x]}, {"Out": [out], "Mask": [mask]},
+             {"dropout_prob": float(p), "is_test": not kw.get("training", True), "fix_seed": False, "seed": 0,
+              "dropout_implementation": "upscale_in_train" if mode == "upscale_in_train" else "downgrade_in_infer"})]
+
+
+COMPOSITE = {"nn.functional.loss.cross_entropy": _ce_composite, "nn.functional.common.dropout": _dropout_composite}
 
 
 def composite(w, short, op):

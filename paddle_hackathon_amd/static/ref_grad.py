@@ -203,6 +203,16 @@ def reshape_grad(dout, x_shape):
     return _wrap(_t(dout).reshape([int(v) for v in x_shape]))
 
 
+def dropout_grad(dout, mask, p=0.5, implementation="downgrade_in_infer"):
+    """dropout_grad: dX = dOut * Mask (/ (1 - p) for upscale_in_train) — the forward's mask, not a
+    new draw"""
+    g = _t(dout)
+    d = g * _t(mask).to(g.dtype)
+    if implementation == "upscale_in_train":
+        d = d / (1.0 - p) if p < 1.0 else torch.zeros_like(g)
+    return _wrap(d)
+
+
 def reshape_like(dout, x):
     return _wrap(_t(dout).reshape(_t(x).shape))
 
@@ -246,6 +256,12 @@ def grad_converter(fwd_type, convert):
                 return reshape_grad, {"dout": _one(r, ins, "Out@GRAD"), "x_shape": shape}, "X@GRAD"
             # no XShape (a program written here): the grad op carries the forward input X itself
             return reshape_like, {"dout": _one(r, ins, "Out@GRAD"), "x": _one(r, ins, "X")}, "X@GRAD"
+        return conv
+    if fwd_type == "dropout":
+        def conv(r, ins, at):
+            return dropout_grad, {"dout": _one(r, ins, "Out@GRAD"), "mask": _one(r, ins, "Mask"),
+                                  "p": at.get("dropout_prob", 0.5),
+                                  "implementation": at.get("dropout_implementation", "downgrade_in_infer")}, "X@GRAD"
         return conv
     if fwd_type == "transpose2":
         def conv(r, ins, at):

@@ -825,10 +825,23 @@ def _dropout_infer(x, p=0.5, implementation="downgrade_in_infer"):
     return _wrap(x._t * (1.0 - p)) if implementation == "downgrade_in_infer" else x
 
 
+def _dropout_train(x, p=0.5, implementation="downgrade_in_infer"):
+    t = x._t
+    mask = torch.empty_like(t).bernoulli_(1.0 - p).to(torch.uint8)
+    out = t * mask.to(t.dtype)
+    if implementation == "upscale_in_train":
+        out = out / (1.0 - p) if p < 1.0 else torch.zeros_like(t)
+    return _wrap(out), _wrap(mask)
+
+
 def _conv_dropout(r, ins, at):
-    # saved inference programs run dropout in test mode (reference dropout_op.cc is_test path)
-    return _dropout_infer, {"x": _one(r, ins, "X"), "p": at.get("dropout_prob", 0.5),
-                            "implementation": at.get("dropout_implementation", "downgrade_in_infer")}, "Out"
+    """dropout_op.cc: the is_test path (inference programs, and every program without is_test =
+    False) scales or passes through; training programs draw the mask and keep it as Mask"""
+    kw = {"x": _one(r, ins, "X"), "p": at.get("dropout_prob", 0.5),
+          "implementation": at.get("dropout_implementation", "downgrade_in_infer")}
+    if at.get("is_test", True) is False:
+        return _dropout_train, kw, ("Out", "Mask")
+    return _dropout_infer, kw, "Out"
 
 
 def _reduce(path):

@@ -997,3 +997,39 @@ def test_training_program_round_trip_conv_bn_ce():
             np.testing.assert_allclose(loaded[n].numpy(), v, rtol=1e-4, atol=1e-6)
     finally:
         paddle.disable_static()
+
+
+def test_training_program_dropout_mask():
+    """dropout in a saved training program is the reference op with its uint8 Mask output and
+    dropout_grad multiplies by THAT mask (no second draw): dX = dOut * Mask / (1 - p)"""
+    paddle.enable_static()
+    try:
+        paddle.seed(3)
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [-1, 8], "float32")
+            h = paddle.static.nn.fc(x, 16, activation="relu")
+            hd = paddle.nn.functional.dropout(h, 0.3)
+            loss = paddle.mean(paddle.static.nn.fc(hd, 1) ** 2)
+            paddle.optimizer.SGD(0.1).minimize(loss)
+        exe = paddle.static.Executor()
+        exe.run(start)
+        pbytes = paddle.static.serialize_program([x], [loss], program=main, training=True)
+        sbytes = paddle.static.serialize_persistables([x], [loss], program=main, training=True)
+        desc = pb.ProgramDesc()
+        desc.ParseFromString(pbytes)
+        drop = [o for o in desc.blocks[0].ops if o.type == "dropout"][0]
+        mask_name = [a.arguments[0] for a in drop.outputs if a.parameter == "Mask"][0]
+        stub = paddle.static.deserialize_program(pbytes)
+        prog = paddle.static.deserialize_persistables(stub, sbytes)
+        X = np.random.RandomState(0).randn(32, 8).astype("float32")
+        out, mask, dout, dx = exe.run(prog, feed={"x": X}, fetch_list=[hd.name, mask_name, hd.name + "@GRAD",
+                                                                        h.name + "@GRAD"])
+        assert mask.dtype == np.uint8 and 0.4 < mask.mean() < 0.9
+        np.testing.assert_allclose(dx, dout * mask / 0.7, rtol=1e-5, atol=1e-7)
+        hv, = exe.run(prog, feed={"x": X}, fetch_list=[h.name])
+        losses = [float(np.asarray(exe.run(prog, feed={"x": X}, fetch_list=stub.fetches)[0]).reshape(-1)[0])
+                  for _ in range(25)]
+        assert losses[-1] < 0.5 * losses[0], losses
+    finally:
+        paddle.disable_static()
