@@ -495,13 +495,16 @@ def _dropout_composite(op):
 
 
 COMPOSITE = {"nn.functional.loss.cross_entropy": _ce_composite, "nn.functional.common.dropout": _dropout_composite}
+# written this way in training programs only (inference programs keep the call, which the
+# inference passes rewrite, e.g. delete_dropout_op_pass)
+TRAIN_ONLY = {"nn.functional.common.dropout"}
 
 
 def composite(w, short, op):
     """the op's parts [(type, {slot: [tensors]}, {slot: [Variables]}, attrs)] (cached per writer, so
     the forward and its grad op see the same intermediates) or None"""
     f = COMPOSITE.get(short)
-    if f is None:
+    if f is None or (short in TRAIN_ONLY and not getattr(w, "train", False)):
         return None
     cache = w.__dict__.setdefault("_composite", {})
     if id(op) not in cache:
