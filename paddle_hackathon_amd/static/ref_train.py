@@ -189,13 +189,14 @@ def emit_optimizer(w, op, block_msg):
         raise NotImplementedError(f"training program: optimizer {type(opt).__name__} has no reference op here")
     if op.kwargs.get("found_inf") is not None:
         raise NotImplementedError("training program: AMP loss scaling is not written as reference ops")
+    grads = _clip_and_decay(w, opt, kind, list(op.kwargs["params"]), list(op.kwargs["grads"]), block_msg)
     lr_val = float(opt.get_lr()) if hasattr(opt, "get_lr") else 0.01
     cache = w.__dict__.setdefault("_lr_tensor", {})
     lr = cache.get(lr_val)
     if lr is None:
         lr = cache[lr_val] = _named(_wrap(torch.tensor([lr_val], dtype=torch.float32)),
                                     f"learning_rate_{len(cache)}")
-    for p, g in zip(op.kwargs["params"], op.kwargs["grads"]):
+    for p, g in zip(op.kwargs["params"], grads):
         msg = block_msg.ops.add()
         ins = {"Param": [w.tensor_name(p)], "Grad": [w.tensor_name(g)], "LearningRate": [w.tensor_name(lr)]}
         outs = {"ParamOut": [w.tensor_name(p)]}
@@ -271,3 +272,67 @@ def emit_composite_grad(w, program, op, block_msg):
             gparts.append((typ + "_grad", g_ins, g_outs, attrs))
     ref_emit.write_parts(w, gparts, block_msg, role=1)
     return True
+
+
+def _clip_and_decay(w, opt, kind, params, grads, block_msg):
+    """the reference's gradient clip (clip.py append_gradient_clip_ops: ClipGradByGlobalNorm as
+    squared_l2_norm / sum / sqrt / elementwise_max / elementwise_div / elementwise_mul, ClipGradByValue
+    as clip) and L2 regularization (regularizer.py append_regularization_ops: scale + sum) ops in
+    front of the optimizer ops; -> the gradients the optimizer ops read"""
+    import torch
+    from . import ref_emit
+    from ..nn.clip import ClipGradByGlobalNorm, ClipGradByValue
+    from ..regularizer import L2Decay, L1Decay
+    parts = []
+    tmp = ref_emit._tmp_var
+    clip = getattr(opt, "_grad_clip", None)
+    out = list(grads)
+    clipped = [i for i, p in enumerate(params) if getattr(p, "need_clip", True)]
+    if isinstance(clip, ClipGradByGlobalNorm) and clipped:
+        sq = []
+        for i in clipped:
+            v = tmp(f"{w.tensor_name(grads[i])}@SQ", grads[i], [1], torch.float32)
+            parts.append(("squared_l2_norm", {"X": [grads[i]]}, {"Out": [v]}, {}))
+            sq.append(v)
+        like = sq[0]
+        gsq, gn, mx, den, sc = (tmp(f"@CLIP@{opt.__class__.__name__}@{n}", like, [1], torch.float32)
+                                for n in ("sum", "norm", "max", "denom", "scale"))
+        parts += [("sum", {"X": sq}, {"Out": [gsq]}, {}),
+                  ("sqrt", {"X": [gsq]}, {"Out": [gn]}, {}),
+                  ("fill_constant", {}, {"Out": [mx]}, {"shape": [1], "value": float(clip.clip_norm),
+                                                        "dtype": pb.vartype_of(torch.float32)}),
+                  ("elementwise_max", {"X": [gn], "Y": [mx]}, {"Out": [den]}, {"axis": -1}),
+                  ("elementwise_div", {"X": [mx], "Y": [den]}, {"Out": [sc]}, {"axis": -1})]
+        for i in clipped:
+            g = grads[i]
+            v = tmp(f"{w.tensor_name(g)}@CLIP", g, list(getattr(g, "declared_shape", None) or g.shape))
+            parts.append(("elementwise_mul", {"X": [g], "Y": [sc]}, {"Out": [v]}, {"axis": -1}))
+            out[i] = v
+    elif isinstance(clip, ClipGradByValue):
+        for i in clipped:
+            g = out[i]
+            v = tmp(f"{w.tensor_name(g)}@CLIP", g, list(getattr(g, "declared_shape", None) or g.shape))
+            parts.append(("clip", {"X": [g]}, {"Out": [v]}, {"min": float(clip.min), "max": float(clip.max)}))
+            out[i] = v
+    elif clip is not None:
+        raise NotImplementedError(f"training program: gradient clip {type(clip).__name__} is not written here")
+    if kind != "adamw":   # AdamW's decoupled decay is the op's coeff attribute
+        for i, p in enumerate(params):
+            reg = p.regularizer if getattr(p, "regularizer", None) is not None else getattr(opt, "regularization", None)
+            if reg is None:
+                continue
+            if isinstance(reg, L1Decay) or not isinstance(reg, (L2Decay, int, float)):
+                raise NotImplementedError(f"training program: regularizer {type(reg).__name__} is not written here")
+            coeff = float(reg.coeff if isinstance(reg, L2Decay) else reg)
+            if not coeff:
+                continue
+            g = out[i]
+            shape = list(getattr(g, "declared_shape", None) or g.shape)
+            d = tmp(f"{w.tensor_name(p)}@DECAY", g, shape)
+            v = tmp(f"{w.tensor_name(g)}@REG", g, shape)
+            parts += [("scale", {"X": [p]}, {"Out": [d]}, {"scale": coeff, "bias": 0.0, "bias_after_scale": True}),
+                      ("sum", {"X": [g, d]}, {"Out": [v]}, {})]
+            out[i] = v
+    if parts:
+        ref_emit.write_parts(w, parts, block_msg, role=2)
+    return out

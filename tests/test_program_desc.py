@@ -1033,3 +1033,55 @@ def test_training_program_dropout_mask():
         assert losses[-1] < 0.5 * losses[0], losses
     finally:
         paddle.disable_static()
+
+
+@pytest.mark.parametrize("case", ["sgd_gclip_l2", "mom_l2", "adam_vclip", "adamw_gclip"])
+def test_training_program_clip_and_decay(case):
+    """gradient clipping (global norm: squared_l2_norm / sum / sqrt / elementwise_max / div / mul;
+    by value: clip) and L2 regularization (scale + sum) are written as the reference's ops in front
+    of the optimizer ops; the loaded program trains like the original"""
+    paddle.enable_static()
+    try:
+        paddle.seed(3)
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [-1, 8], "float32")
+            y = paddle.static.data("y", [-1, 1], "float32")
+            h = paddle.static.nn.fc(x, 16, activation="relu")
+            loss = paddle.mean(paddle.square(paddle.static.nn.fc(h, 1) - y))
+            o = {"sgd_gclip_l2": lambda: paddle.optimizer.SGD(0.1, weight_decay=0.01,
+                                                             grad_clip=paddle.nn.ClipGradByGlobalNorm(0.05)),
+                 "mom_l2": lambda: paddle.optimizer.Momentum(0.05, 0.9, weight_decay=paddle.regularizer.L2Decay(0.02)),
+                 "adam_vclip": lambda: paddle.optimizer.Adam(0.01, grad_clip=paddle.nn.ClipGradByValue(0.02)),
+                 "adamw_gclip": lambda: paddle.optimizer.AdamW(0.01, weight_decay=0.1,
+                                                               grad_clip=paddle.nn.ClipGradByGlobalNorm(0.1))}[case]()
+            o.minimize(loss)
+        exe = paddle.static.Executor()
+        exe.run(start)
+        rs = np.random.RandomState(0)
+        batches = [(rs.randn(16, 8).astype("float32"), rs.randn(16, 1).astype("float32")) for _ in range(6)]
+        exe.run(main, feed={"x": batches[0][0], "y": batches[0][1]}, fetch_list=[loss])
+        pbytes = paddle.static.serialize_program([x, y], [loss], program=main, training=True)
+        sbytes = paddle.static.serialize_persistables([x, y], [loss], program=main, training=True)
+        desc = pb.ProgramDesc()
+        desc.ParseFromString(pbytes)
+        types = [op.type for op in desc.blocks[0].ops]
+        if "gclip" in case:
+            assert "squared_l2_norm" in types and "elementwise_max" in types
+        if "vclip" in case:
+            assert "clip" in types
+        if "l2" in case and not case.startswith("mom"):
+            assert "scale" in types
+        ref = [float(np.asarray(exe.run(main, feed={"x": a, "y": b}, fetch_list=[loss])[0]).reshape(-1)[0])
+               for a, b in batches[1:]]
+        rp = {p.name: p.numpy().copy() for p in main.all_parameters()}
+        stub = paddle.static.deserialize_program(pbytes)
+        prog = paddle.static.deserialize_persistables(stub, sbytes)
+        got = [float(np.asarray(exe.run(prog, feed={"x": a, "y": b}, fetch_list=stub.fetches)[0]).reshape(-1)[0])
+               for a, b in batches[1:]]
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+        lp = {p.name: p.numpy() for p in prog.all_parameters()}
+        for n in rp:
+            np.testing.assert_allclose(lp[n], rp[n], rtol=1e-5, atol=1e-6)
+    finally:
+        paddle.disable_static()
