@@ -468,10 +468,38 @@ int launch(const Args& a, hipStream_t st, int tile = -1, int bk = 0, int* stats_
   const int bm = cands[best][0], bn = cands[best][1];
   if (stats_rows) *stats_rows = (int)((a.M + bm - 1) / bm);   // row tiles with stats / bn_part rows
   const unsigned groups = (unsigned)std::max(1, groups_);
-  if (a.out_f32) {   // fp32 products (three-term bf16 split): one 128 x 128 x 32 instantiation
-    const long tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    hipLaunchKernelGGL((gemm256_kernel<T, 128, 128, 32, CONV, true>), dim3((unsigned)tiles, groups), dim3(NT), 0, st, a);
-    return (int)hipGetLastError();
+  if (a.out_f32) {
+    // fp32 products (three-term bf16 split, bf16 operands only): the split triples K, so the
+    // products are long-K — the large tiles with BK = 64 when the heuristic picks them, else
+    // 128 x 128 x 32
+    if constexpr (std::is_same<T, bf16_t>::value) {
+      auto gof = [&](auto bm_c, auto bn_c, auto bk_c) {
+        constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value, BKc = decltype(bk_c)::value;
+        const long tiles = ((a.M + BMc - 1) / BMc) * ((a.N + BNc - 1) / BNc);
+        hipLaunchKernelGGL((gemm256_kernel<T, BMc, BNc, BKc, CONV, true>), dim3((unsigned)tiles, groups), dim3(NT),
+                           0, st, a);
+      };
+      using I256 = std::integral_constant<int, 256>;
+      using I128 = std::integral_constant<int, 128>;
+      using I64 = std::integral_constant<int, 64>;
+      using I32 = std::integral_constant<int, 32>;
+      // (the 256 x 256 conv variant spills: its gather state and the fp32 epilogue exceed the budget)
+      bool done = false;
+      if constexpr (!CONV) {
+        if (a.K >= 512 && bm == 256 && bn == 256) {
+          gof(I256{}, I256{}, I64{});
+          done = true;
+        }
+      }
+      if (done) {
+      } else if (a.K >= 512 && bm == 256 && bn >= 128) gof(I256{}, I128{}, I64{});
+      else if (a.K >= 512 && bn == 256) gof(I128{}, I256{}, I64{});
+      else if (a.K >= 512 && bm >= 128 && bn >= 128) gof(I128{}, I128{}, I64{});
+      else gof(I128{}, I128{}, I32{});
+      return (int)hipGetLastError();
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BMc = decltype(bm_c)::value, BNc = decltype(bn_c)::value;

@@ -161,3 +161,8 @@ def globals():
 
 class EOFException(Exception):
     """raised by Executor.run when a started py_reader has no more batches"""
+
+
+def CostModel():   # noqa: N802 (the reference's core.CostModel class)
+    from ..cost_model import _CoreCostModel
+    return _CoreCostModel()

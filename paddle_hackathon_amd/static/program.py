@@ -23,6 +23,7 @@ import inspect
 import itertools
 import json
 import os
+import time
 
 import numpy as np
 import torch
@@ -807,7 +808,11 @@ def run_block(program, blk, env, free=None):
     """interpret the ops of ``blk`` in the value environment ``env`` (Variable id -> Tensor);
     ``free``: op index -> Variable ids to drop after that op (eager deletion)"""
     cut_ids = program.__dict__.get("_cut_ops") or ()
+    timer = program.__dict__.get("_op_timer")   # cost_model.profile_measure: per-op times
     for i, op in enumerate(blk.ops):
+        if timer is not None:
+            timer[1]()
+            t_op = time.perf_counter()
         saved = _cut_inputs(op, env) if id(op) in cut_ids else None
         if op.exec is not None:
             op.exec(program, env, op)
@@ -828,6 +833,9 @@ def run_block(program, blk, env, free=None):
                 _share_lod(op, out, e)
         if saved:   # later readers see the original values (and their graph)
             env.update(saved)
+        if timer is not None:
+            timer[1]()
+            timer[0].append((blk.idx, i, (time.perf_counter() - t_op) * 1e3))
         if free:
             for vid in free.get(i, ()):
                 env.pop(vid, None)
