@@ -148,15 +148,4 @@ class ModelAverage(Optimizer):
                 p._t.copy_(b)
 
 
-class DistributedFusedLamb(Lamb):
-    """LAMB whose state is sharded over the data-parallel group (reference
-    distributed_fused_lamb.py). Single-process it is plain LAMB; with sharding, use
-    ``fleet`` sharding stage 1 which shards any optimizer's state."""
-
-    def __init__(self, learning_rate=0.001, lamb_weight_decay=0.01, beta1=0.9, beta2=0.999, epsilon=1e-6,
-                 parameters=None, grad_clip=None, exclude_from_weight_decay_fn=None, clip_after_allreduce=True,
-                 is_grad_scaled_by_nranks=True, alignment=128, use_master_param_norm=True, gradient_accumulation_steps=1,
-                 use_master_acc_grad=True, nproc_per_node=None, name=None):
-        super().__init__(learning_rate=learning_rate, lamb_weight_decay=lamb_weight_decay, beta1=beta1, beta2=beta2,
-                         epsilon=epsilon, parameters=parameters, grad_clip=grad_clip,
-                         exclude_from_weight_decay_fn=exclude_from_weight_decay_fn, name=name)
+from .distributed_fused_lamb import DistributedFusedLamb  # noqa: E402,F401
