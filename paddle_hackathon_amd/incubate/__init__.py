@@ -15,6 +15,7 @@ from . import autotune  # noqa: F401
 from . import operators  # noqa: F401
 from . import passes  # noqa: F401
 from .passes import fuse_resnet_unit_pass  # noqa: F401
+from ..fluid.layer_helper import LayerHelper  # noqa: F401
 from .. import sparse  # noqa: F401
 
 __all__ = ["LookAhead", "ModelAverage", "softmax_mask_fuse_upper_triangle", "softmax_mask_fuse", "graph_send_recv",
