@@ -519,7 +519,7 @@ def write_parts(w, parts, block_msg, role=None):
         msg.type = typ
         for k, v in attrs.items():
             _set_attr(msg, k, v)
-        if role is not None:
+        if role is not None and "op_role" not in attrs:
             _set_attr(msg, "op_role", role)
         for slot, ts in ins.items():
             s = msg.inputs.add()

@@ -154,6 +154,7 @@ def _conv_swce(r, ins, at):
 
 
 FORWARD = {"softmax_with_cross_entropy": _conv_swce}
+# (AMP converters registered below, with the optimizers)
 
 
 def _align(y, xdim, axis):
@@ -369,12 +370,90 @@ def rmsprop_op(param, grad, moment, mean_square, learning_rate, mean_grad=None, 
     return param, moment, mean_square
 
 
+def _skipping(fn, returns):
+    """the optimizer op with its SkipUpdate input (AMP: the step found inf / nan): no update, the
+    state tensors pass through"""
+    def run(skip_update=None, **kw):
+        if skip_update is not None and bool(_t(skip_update).reshape(-1)[0]):
+            res = tuple(kw[k] for k in returns)
+            return res if len(res) > 1 else res[0]
+        return fn(**kw)
+    run.__name__ = fn.__name__
+    run.__module__ = fn.__module__
+    return run
+
+
 def _opt_conv(fn, slots, outs, attrs):
+    returns = [k for k in slots if k in ("param", "velocity", "moment", "moment1", "moment2", "beta1_pow",
+                                         "beta2_pow", "mean_square", "mean_grad")]
+    skipping = _skipping(fn, returns)
+
     def conv(r, ins, at):
         kw = {k: _one(r, ins, s) for k, s in slots.items()}
         kw.update({k: at.get(a, d) for k, (a, d) in attrs.items()})
+        if ins.get("SkipUpdate"):
+            kw["skip_update"] = _one(r, ins, "SkipUpdate")
+            return skipping, kw, tuple(outs)
         return fn, kw, tuple(outs)
     return conv
+
+
+# ------------------------------------------------------------------------------- AMP loss scaling
+def check_finite_unscale_op(xs, scale):
+    """check_finite_and_unscale_op.cc: Out = X / Scale, FoundInfinite = any non-finite"""
+    inv = 1.0 / _t(scale).float().reshape(-1)[0]
+    bad = None
+    outs = []
+    for x in xs:
+        u = _t(x).float() * inv
+        b = ~torch.isfinite(u).all()
+        bad = b if bad is None else (bad | b)
+        outs.append(_wrap(u.to(_t(x).dtype)))
+    if bad is None:
+        bad = torch.zeros((), dtype=torch.bool)
+    return outs, _wrap(bad.reshape(1))
+
+
+def update_loss_scaling_op(xs, found_inf, prev_scale, good, bad, incr_every_n_steps=1000, decr_every_n_nan_or_inf=2,
+                           incr_ratio=2.0, decr_ratio=0.5, stop_update=False):
+    """update_loss_scaling_op.cc: on overflow the gradients are zeroed and the bad-step counter
+    grows (scale * decr_ratio every decr_every_n_nan_or_inf of them, kept >= 1); otherwise the
+    good-step counter grows (scale * incr_ratio every incr_every_n_steps)"""
+    with torch.no_grad():
+        inf = bool(_t(found_inf).reshape(-1)[0])
+        if inf:
+            for x in xs:
+                _t(x).zero_()
+        if not stop_update:
+            s, gd, bd = _t(prev_scale), _t(good), _t(bad)
+            if inf:
+                gd.zero_()
+                bd.add_(1)
+                if int(bd.reshape(-1)[0]) >= decr_every_n_nan_or_inf:
+                    s.mul_(decr_ratio).clamp_(min=1.0)
+                    bd.zero_()
+            else:
+                bd.zero_()
+                gd.add_(1)
+                if int(gd.reshape(-1)[0]) >= incr_every_n_steps:
+                    s.mul_(incr_ratio)
+                    gd.zero_()
+    return list(xs), prev_scale, good, bad
+
+
+def _conv_cfu(r, ins, at):
+    return check_finite_unscale_op, {"xs": [r.var(n) for n in ins.get("X", [])], "scale": _one(r, ins, "Scale")}, \
+        ("Out*", "FoundInfinite")
+
+
+def _conv_uls(r, ins, at):
+    return update_loss_scaling_op, {
+        "xs": [r.var(n) for n in ins.get("X", [])], "found_inf": _one(r, ins, "FoundInfinite"),
+        "prev_scale": _one(r, ins, "PrevLossScaling"), "good": _one(r, ins, "InGoodSteps"),
+        "bad": _one(r, ins, "InBadSteps"), "incr_every_n_steps": at.get("incr_every_n_steps", 1000),
+        "decr_every_n_nan_or_inf": at.get("decr_every_n_nan_or_inf", 2), "incr_ratio": at.get("incr_ratio", 2.0),
+        "decr_ratio": at.get("decr_ratio", 0.5), "stop_update": at.get("stop_update", False)}, \
+        ("Out*", "LossScaling", "OutGoodSteps", "OutBadSteps")
 
 
 OPTIMIZERS = {
@@ -405,3 +484,5 @@ OPTIMIZERS = {
                          {"epsilon": ("epsilon", 1e-10), "decay": ("decay", 0.9), "momentum": ("momentum", 0.0),
                           "centered": ("centered", False)}),
 }
+
+FORWARD.update({"check_finite_and_unscale": _conv_cfu, "update_loss_scaling": _conv_uls})

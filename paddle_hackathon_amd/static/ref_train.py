@@ -187,8 +187,7 @@ def emit_optimizer(w, op, block_msg):
     kind = kind[:-len("optimizer")] if kind.endswith("optimizer") else kind
     if kind not in ("sgd", "momentum", "adam", "adamw"):
         raise NotImplementedError(f"training program: optimizer {type(opt).__name__} has no reference op here")
-    if op.kwargs.get("found_inf") is not None:
-        raise NotImplementedError("training program: AMP loss scaling is not written as reference ops")
+    found_inf = op.kwargs.get("found_inf")   # AMP: the optimizer ops read it as SkipUpdate
     grads = _clip_and_decay(w, opt, kind, list(op.kwargs["params"]), list(op.kwargs["grads"]), block_msg)
     lr_val = float(opt.get_lr()) if hasattr(opt, "get_lr") else 0.01
     cache = w.__dict__.setdefault("_lr_tensor", {})
@@ -227,6 +226,8 @@ def emit_optimizer(w, op, block_msg):
                 _set_attr(msg, "coeff", float(coeff if isinstance(coeff, (int, float)) else 0.01))
                 _set_attr(msg, "with_decay", True)
         _set_attr(msg, "op_role", 2)
+        if found_inf is not None:
+            ins["SkipUpdate"] = [w.tensor_name(found_inf)]
         for slot, names in ins.items():
             v = msg.inputs.add()
             v.parameter = slot
@@ -336,3 +337,67 @@ def _clip_and_decay(w, opt, kind, params, grads, block_msg):
     if parts:
         ref_emit.write_parts(w, parts, block_msg, role=2)
     return out
+
+
+# ------------------------------------------------------------------------------- AMP loss scaling
+def is_amp_op(op):
+    from . import passes
+    return op.fn in (passes._scaled_ones, passes._unscale_check, passes._update_scaling)
+
+
+def emit_amp(w, op, msg, ins, outs):
+    """static AMP (static/passes.py insert_loss_scaling) as the reference's ops: the loss gradient
+    = fill_constant(1) * loss_scaling (elementwise_mul), check_finite_and_unscale (X, Scale -> Out,
+    FoundInfinite) and update_loss_scaling (X, FoundInfinite, PrevLossScaling, In{Good,Bad}Steps ->
+    Out, LossScaling, Out{Good,Bad}Steps); the optimizer ops then take FoundInfinite as SkipUpdate"""
+    from .serialize import _set_attr
+    from . import passes, ref_emit
+    import torch
+    if op.fn is passes._scaled_ones:
+        x, scale = op.kwargs["x"], op.kwargs["scale"]
+        _named(scale, "loss_scaling_0")
+        one = ref_emit._tmp_var(w.tensor_name(op.outputs) + "@ONE", x, list(x._t.shape) or [1])
+        msg.type = "fill_constant"
+        outs["Out"] = [w.tensor_name(one)]
+        _set_attr(msg, "shape", [int(s) for s in (x._t.shape or [1])])
+        _set_attr(msg, "value", 1.0)
+        _set_attr(msg, "dtype", pb.vartype_of(x._t.dtype))
+        _set_attr(msg, "op_role", 257)
+        w._pending_parts = [("elementwise_mul", {"X": [one], "Y": [scale]}, {"Out": [op.outputs]},
+                             {"axis": -1, "op_role": 257})]
+        return
+    if op.fn is passes._unscale_check:
+        grads, scale = op.kwargs["grads"], op.kwargs["scale"]
+        _named(scale, "loss_scaling_0")
+        res = list(op.outputs)
+        msg.type = "check_finite_and_unscale"
+        ins["X"] = [w.tensor_name(g) for g in grads]
+        ins["Scale"] = [w.tensor_name(scale)]
+        outs["Out"] = [w.tensor_name(v) for v in res[:-1]]
+        outs["FoundInfinite"] = [w.tensor_name(res[-1])]
+        w._amp_unscaled = res[:-1]
+        _set_attr(msg, "op_role", 1)
+        return
+    kw = op.kwargs
+    for t, n in ((kw["scale"], "loss_scaling_0"), (kw["good"], "num_good_steps_0"), (kw["bad"], "num_bad_steps_0")):
+        _named(t, n)
+    xs = getattr(w, "_amp_unscaled", [])
+    msg.type = "update_loss_scaling"
+    ins["X"] = [w.tensor_name(v) for v in xs]
+    ins["FoundInfinite"] = [w.tensor_name(kw["found_inf"])]
+    ins["PrevLossScaling"] = [w.tensor_name(kw["scale"])]
+    ins["InGoodSteps"] = [w.tensor_name(kw["good"])]
+    ins["InBadSteps"] = [w.tensor_name(kw["bad"])]
+    outs["Out"] = list(ins["X"])
+    outs["LossScaling"] = list(ins["PrevLossScaling"])
+    outs["OutGoodSteps"] = list(ins["InGoodSteps"])
+    outs["OutBadSteps"] = list(ins["InBadSteps"])
+    for a in ("incr_every", "decr_every"):
+        pass
+    _set_attr(msg, "incr_every_n_steps", int(kw["incr_every"]))
+    _set_attr(msg, "decr_every_n_nan_or_inf", int(kw["decr_every"]))
+    _set_attr(msg, "incr_ratio", float(kw["incr_ratio"]))
+    _set_attr(msg, "decr_ratio", float(kw["decr_ratio"]))
+    _set_attr(msg, "stop_update", False)
+    _set_attr(msg, "op_role", 2)
+    _ = torch

@@ -275,6 +275,8 @@ class _Writer:
             _rt.emit_sum(self, op, msg, ins, outs)
         elif getattr(self, "train", False) and op.fn is _bw._fill_ones:
             _rt.emit_fill_ones(self, op, msg, ins, outs)
+        elif getattr(self, "train", False) and _rt.is_amp_op(op):
+            _rt.emit_amp(self, op, msg, ins, outs)
         elif getattr(self, "train", False) and op.type == "assign" and op.attrs.get("op_role") == "backward":
             _rt.emit_assign(self, op, msg, ins, outs)
         elif op.exec is not None:
@@ -589,8 +591,9 @@ class _Reader:
                         o = self.var(outs[out_spec][0], blk)
                     elif out_spec[0] == "list":
                         o = [self.var(n, blk) for n in outs[out_spec[1]]]
-                    else:     # one Variable per slot (absent optional slots get a fresh one)
-                        o = tuple(self.var(outs[sl][0], blk) if outs.get(sl) else
+                    else:     # one Variable per slot (absent optional slots get a fresh one; "Slot*": a list)
+                        o = tuple([self.var(n, blk) for n in outs.get(sl[:-1], [])] if sl.endswith("*") else
+                                  self.var(outs[sl][0], blk) if outs.get(sl) else
                                   self.var(f"{om.type}.{sl}.{len(self.vars)}", blk) for sl in out_spec)
                     fn = getattr(fn, "__wrapped_op__", fn)
                     qual = f"{fn.__module__}.{fn.__name__}"
