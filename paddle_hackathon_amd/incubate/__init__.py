@@ -10,6 +10,7 @@ from . import nn  # noqa: F401
 from . import autograd  # noqa: F401
 from . import asp  # noqa: F401
 from . import checkpoint  # noqa: F401
+from ..fluid.incubate.checkpoint import auto_checkpoint  # noqa: F401
 from . import distributed  # noqa: F401
 from . import autotune  # noqa: F401
 from . import operators  # noqa: F401
