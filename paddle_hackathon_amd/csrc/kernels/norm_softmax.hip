@@ -10,8 +10,6 @@
 // Reference behaviour: paddle/phi/kernels/gpu/layer_norm_kernel.cu,
 // layer_norm_grad_kernel.cu, softmax_kernel.cu / gpudnn/softmax_gpudnn.h.
 #include "common.h"
-#include <cstdlib>
-#include <type_traits>
 
 using namespace pha;
 
@@ -133,7 +131,7 @@ struct Raw8<float> {
 
 // BW waves per block (16 -> 1024 threads): a grid of one block per CU then still gives 4
 // waves per SIMD to hide HBM latency, while the dw/db partials stay one [H] row per block.
-template <typename T, typename W, int NCH, int BW, bool PF = false>
+template <typename T, typename W, int NCH, int BW>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 4 : NCH <= 4 ? 2 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const W* __restrict__ w, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, T* __restrict__ dx,
@@ -150,58 +148,21 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
   // H = 1537..2048 (NCH 4, the GPT-1.3B width): one HBM round trip per row with x / dy / dres held
   // raw in registers (2 waves per SIMD, no spills); other widths re-read x and dy in pass 2
   if constexpr (NCH == 4) {
-  // PF: the NEXT row's x / dy (and its mean / rstd) are loaded before this row is computed, so
-  // every wave keeps a row of loads in flight across its compute and stores (the residual
-  // gradient, read only at the end of pass 2, is issued with its own row)
-  Raw8<T> px[NCH], pg[NCH];
-  float pmu = 0.f, prs = 0.f;
-  auto load_row = [&](int rw, Raw8<T> (&ax)[NCH], Raw8<T> (&ag)[NCH]) {
+  for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
+    const float mu = mean[row], rs = rstd[row];
+    const T* xr = x + (long)row * H;
+    const T* gr = dy + (long)row * H;
+    // one HBM round trip per row: x, dy (and the residual gradient) are loaded once, kept as raw
+    // 16-B vectors and unpacked again for pass 2 (no second read, no dependent dres load)
+    Raw8<T> rx[NCH], rg[NCH], rr[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 512 + lane * 8;
       if (col < H) {
-        ax[c].ld(x + (long)rw * H + col);
-        ag[c].ld(dy + (long)rw * H + col);
+        rx[c].ld(xr + col);
+        rg[c].ld(gr + col);
+        if (dres) rr[c].ld(dres + (long)row * H + col);
       }
-    }
-  };
-  auto load_res = [&](int rw, Raw8<T> (&ar)[NCH]) {   // read last (pass 2): issued with the row
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int col = c * 512 + lane * 8;
-      if (col < H && dres) ar[c].ld(dres + (long)rw * H + col);
-    }
-  };
-  const int stride = gridDim.x * BW;
-  if constexpr (PF) {
-    const int r0 = blockIdx.x * BW + wid;
-    if (r0 < rows) {
-      load_row(r0, px, pg);
-      pmu = mean[r0];
-      prs = rstd[r0];
-    }
-  }
-  for (int row = blockIdx.x * BW + wid; row < rows; row += stride) {
-    float mu, rs;
-    // one HBM round trip per row: x, dy (and the residual gradient) are loaded once, kept as raw
-    // 16-B vectors and unpacked again for pass 2 (no second read, no dependent dres load)
-    Raw8<T> rx[NCH], rg[NCH], rr[NCH];
-    if constexpr (PF) {
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) { rx[c] = px[c]; rg[c] = pg[c]; }
-      mu = pmu;
-      rs = prs;
-      load_res(row, rr);
-      if (row + stride < rows) {
-        load_row(row + stride, px, pg);
-        pmu = mean[row + stride];
-        prs = rstd[row + stride];
-      }
-    } else {
-      mu = mean[row];
-      rs = rstd[row];
-      load_row(row, rx, rg);
-      load_res(row, rr);
     }
     // pass 1: row statistics of g = dy*w
     float s1 = 0.f, s2 = 0.f;
@@ -534,15 +495,6 @@ PHA_API int pha_layer_norm_fwd2(int dt, int wdt, const void* x, const void* r, v
   return rc;
 }
 
-// PHA_LN_BWD_PF=0: the H = 2048 backward without the next-row prefetch (A/B)
-inline bool ln_bwd_prefetch() {
-  static const int v = [] {
-    const char* e = getenv("PHA_LN_BWD_PF");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
-}
-
 // waves per block of the LN backward: 16 while the dw/db accumulators fit the 128-VGPR
 // budget of 4 waves/SIMD (H <= 1536), 8 above (two blocks per CU).
 constexpr int bwd_waves(int nch) { return nch <= 3 ? 16 : 8; }
@@ -611,15 +563,6 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
   PHA_DISPATCH_T(dt, T, {
     if (wdt == kF32) {
       rc = dispatch_nch_small(H, [&](auto nch) {
-        constexpr int NC = decltype(nch)::value;
-        if constexpr (NC == 4 && !std::is_same<T, float>::value) {   // (fp32 rows: no VGPRs left)
-          if (ln_bwd_prefetch()) {
-            hipLaunchKernelGGL((ln_bwd_kernel<T, float, 4, bwd_waves(4), true>), grid, dim3(bwd_waves(4) * 64), 0,
-                               stream, (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b,
-                               rows, H, (const T*)dres);
-            return;
-          }
-        }
         hipLaunchKernelGGL((ln_bwd_kernel<T, float, decltype(nch)::value, bwd_waves(decltype(nch)::value)>), grid, dim3(bwd_waves(decltype(nch)::value) * 64), 0, stream,
                            (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H,
                            (const T*)dres);
