@@ -156,6 +156,8 @@ class Optimizer:
         self._step_count += 1
         with torch.no_grad():
             self._update(pgs)
+        if getattr(self._learning_rate, "_auto_step", False):   # schedules that step with the optimizer
+            self._learning_rate.step()
 
     def _update(self, pgs):
         raise NotImplementedError

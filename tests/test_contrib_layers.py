@@ -1,0 +1,118 @@
+"""fluid.contrib.layers (reference: python/paddle/fluid/contrib/layers/nn.py) against numpy
+references of the op definitions (the reference's test_partial_concat_op / test_partial_sum_op /
+test_batch_fc_op / test_tdm_child_op / test_pow2_decay_with_linear_warmup_op formulas)."""
+import numpy as np
+import pytest
+import torch
+
+import paddle_hackathon_amd as paddle
+from paddle_hackathon_amd import fluid
+from paddle_hackathon_amd.fluid.contrib.layers import nn as C
+
+
+def test_fused_elemwise_activation():
+    rs = np.random.RandomState(0)
+    x, y = rs.randn(3, 4).astype("float32"), rs.randn(3, 4).astype("float32")
+    X, Y = paddle.to_tensor(x), paddle.to_tensor(y)
+    np.testing.assert_allclose(C.fused_elemwise_activation(X, Y, ["relu", "elementwise_add"]).numpy(),
+                               np.maximum(x + y, 0), rtol=1e-6)
+    np.testing.assert_allclose(C.fused_elemwise_activation(X, Y, ["elementwise_mul", "scale"], scale=0.5).numpy(),
+                               x * (y * 0.5), rtol=1e-6)
+    np.testing.assert_allclose(C.fused_elemwise_activation(X, Y, "elementwise_add,tanh").numpy(), x + np.tanh(y),
+                               rtol=1e-6)
+
+
+@pytest.mark.parametrize("start,length", [(0, -1), (2, 3), (-4, 2)])
+def test_partial_concat_and_sum(start, length):
+    rs = np.random.RandomState(1)
+    xs = [rs.randn(5, 7).astype("float32") for _ in range(3)]
+    s = start + 7 if start < 0 else start
+    n = 7 - s if length < 0 else length
+    ref_c = np.concatenate([v[:, s:s + n] for v in xs], 1)
+    ref_s = sum(v[:, s:s + n] for v in xs)
+    ts = [paddle.to_tensor(v) for v in xs]
+    np.testing.assert_allclose(C.partial_concat(ts, start, length).numpy(), ref_c)
+    np.testing.assert_allclose(C.partial_sum(ts, start, length).numpy(), ref_s, rtol=1e-6)
+
+
+def test_shuffle_batch_is_a_row_permutation():
+    x = np.arange(40, dtype="float32").reshape(10, 4)
+    a = C.shuffle_batch(paddle.to_tensor(x), seed=7).numpy()
+    b = C.shuffle_batch(paddle.to_tensor(x), seed=7).numpy()
+    np.testing.assert_array_equal(a, b)
+    assert sorted(map(tuple, a)) == sorted(map(tuple, x)) and not np.array_equal(a, x)
+
+
+def test_batch_fc_static():
+    rs = np.random.RandomState(2)
+    inp = rs.rand(4, 5, 6).astype("float32")
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [4, 5, 6], "float32")
+            out = C.batch_fc(x, [4, 6, 3], fluid.ParamAttr(name="w_0"), [4, 3], fluid.ParamAttr(name="b_0"), act="relu")
+        exe = paddle.static.Executor()
+        exe.run(start)
+        params = {p.name: p.numpy() for p in main.all_parameters()}
+        got, = exe.run(main, feed={"x": inp}, fetch_list=[out])
+    finally:
+        paddle.disable_static()
+    w, b = params["w_0"], params["b_0"]
+    ref = np.maximum(np.einsum("sbi,sio->sbo", inp, w) + b[:, None, :], 0)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_correlation_zero_displacement_and_shift():
+    rs = np.random.RandomState(3)
+    x = rs.randn(2, 3, 6, 7).astype("float32")
+    X = paddle.to_tensor(x)
+    out = C.correlation(X, X, pad_size=2, kernel_size=1, max_displacement=2, stride1=1, stride2=1).numpy()
+    assert out.shape == (2, 25, 6, 7)
+    # the centre displacement is the channel mean of x * x
+    np.testing.assert_allclose(out[:, 12], (x * x).mean(1), rtol=1e-5, atol=1e-6)
+    # displacement (dy, dx) = (0, 1): x[., i, j] * x[., i, j + 1] (zero past the border)
+    xs = np.zeros_like(x)
+    xs[..., :-1] = x[..., 1:]
+    np.testing.assert_allclose(out[:, 13], (x * xs).mean(1), rtol=1e-5, atol=1e-6)
+
+
+def test_tdm_child():
+    info = np.array([[0, 0, 0, 1, 2], [0, 1, 0, 3, 4], [0, 1, 0, 5, 6], [0, 2, 1, 0, 0], [1, 2, 1, 0, 0],
+                     [2, 2, 2, 0, 0], [3, 2, 2, 0, 0]], dtype="int32")
+    child, leaf = C._tdm_child_op(paddle.to_tensor(np.array([[2], [3]], "int32")), paddle.to_tensor(info), 2)
+    np.testing.assert_array_equal(child.numpy(), [[5, 6], [0, 0]])
+    np.testing.assert_array_equal(leaf.numpy(), [[1, 1], [0, 0]])
+
+
+def test_pow2_decay_with_linear_warmup_steps_with_the_optimizer():
+    sched = C.pow2_decay_with_linear_warmup(3, 8, 1.0, 0.1)
+    lin = paddle.nn.Linear(2, 2)
+    opt = paddle.optimizer.SGD(sched, parameters=lin.parameters())
+    lrs = []
+    for _ in range(10):
+        lrs.append(opt.get_lr())
+        lin(paddle.ones([1, 2])).sum().backward()
+        opt.step()
+        opt.clear_grad()
+    ref = []
+    for s in range(1, 11):
+        if s <= 3:
+            ref.append(s / 3)
+        elif s <= 8:
+            f = 1 - (s - 3) / 5
+            ref.append(0.9 * f * f + 0.1)
+        else:
+            ref.append(0.1)
+    np.testing.assert_allclose(lrs, ref, rtol=1e-6)
+
+
+def test_multiclass_nms2_index_and_absent_ops():
+    boxes = torch.tensor([[[0, 0, 1, 1], [0, 0, 1, 1.05], [2, 2, 3, 3]]], dtype=torch.float32)
+    scores = torch.tensor([[[0.9, 0.8, 0.7], [0.1, 0.2, 0.6]]], dtype=torch.float32)
+    out, idx = C.multiclass_nms2(paddle.to_tensor(boxes), paddle.to_tensor(scores), 0.05, 10, 10, 0.5,
+                                 background_label=-1, return_index=True)
+    o, i = out.numpy(), idx.numpy().reshape(-1)
+    assert len(o) == len(i) and set(i.tolist()) <= {0, 1, 2}
+    with pytest.raises(NotImplementedError):
+        C.tree_conv(None, None, 1)
