@@ -31,16 +31,16 @@ def _mlp_program(w1, w2, checkpoints=False):
 
 
 def _dygraph_grads(w1, w2, X, Y):
-    paddle.disable_static()
-    W1 = paddle.to_tensor(w1, stop_gradient=False)
-    W2 = paddle.to_tensor(w2, stop_gradient=False)
-    h1 = paddle.tanh(paddle.matmul(paddle.to_tensor(X), W1))
-    h2 = paddle.nn.functional.relu(h1 * 2.0 + h1)
-    loss = paddle.mean((paddle.matmul(h2, W2) - paddle.to_tensor(Y)) ** 2)
+    """the same computation in torch fp64 autograd (independent of any framework-global state a
+    previous test in the same worker may have left behind)"""
+    import torch
+    W1 = torch.tensor(w1, dtype=torch.float64, requires_grad=True)
+    W2 = torch.tensor(w2, dtype=torch.float64, requires_grad=True)
+    h1 = torch.tanh(torch.tensor(X, dtype=torch.float64) @ W1)
+    h2 = torch.relu(h1 * 2.0 + h1)
+    loss = ((h2 @ W2 - torch.tensor(Y, dtype=torch.float64)) ** 2).mean()
     loss.backward()
-    out = (loss.item(), W1.grad.numpy(), W2.grad.numpy())
-    paddle.enable_static()
-    return out
+    return loss.item(), W1.grad.numpy().astype("float32"), W2.grad.numpy().astype("float32")
 
 
 def _data():
