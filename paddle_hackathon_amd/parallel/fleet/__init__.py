@@ -389,10 +389,10 @@ class MultiSlotStringDataGenerator(MultiSlotDataGenerator):
     pass
 
 
-def __getattr__(name):   # fleet.elastic, imported lazily (it is also a `python -m` entry point)
-    if name == "elastic":
-        from .. import elastic
-        return elastic
+def __getattr__(name):   # submodules imported lazily (fleet.elastic is also a `python -m` entry point)
+    import importlib
+    if name in ("elastic", "metrics", "data_generator", "base", "runtime", "recompute"):
+        return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)
 
 
