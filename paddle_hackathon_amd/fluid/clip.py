@@ -31,3 +31,8 @@ class ErrorClipByValue:
         if t.requires_grad:
             t.register_hook(self)
         return var
+
+# 1.x names (reference: fluid/clip.py)
+GradientClipByGlobalNorm = ClipGradByGlobalNorm
+GradientClipByNorm = ClipGradByNorm
+GradientClipByValue = ClipGradByValue

@@ -166,3 +166,6 @@ class EOFException(Exception):
 def CostModel():   # noqa: N802 (the reference's core.CostModel class)
     from ..cost_model import _CoreCostModel
     return _CoreCostModel()
+
+
+VarBase = Tensor   # the 1.x dygraph tensor class (reference: core.VarBase)

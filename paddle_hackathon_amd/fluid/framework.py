@@ -62,3 +62,25 @@ def default_place():
 
 
 _current_expected_place = default_place
+
+def switch_main_program(program):
+    """make ``program`` the default main program; returns the previous one (reference:
+    fluid/framework.py switch_main_program)"""
+    from ..static import program as _P
+    prev = _P._state.main
+    _P._state.main = program
+    return prev
+
+
+def switch_startup_program(program):
+    from ..static import program as _P
+    prev = _P._state.startup
+    _P._state.startup = program
+    return prev
+
+
+def __getattr__(name):   # ParamBase / EagerParamBase: the framework's Parameter
+    if name in ("ParamBase", "EagerParamBase"):
+        from ..framework.core import Parameter
+        return Parameter
+    raise AttributeError(name)

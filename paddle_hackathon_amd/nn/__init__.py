@@ -18,3 +18,5 @@ from .layer import container as _c, common as _cm, conv_norm_pool as _cn, loss a
 __all__ = (["Layer", "ClipGradByGlobalNorm", "ClipGradByNorm", "ClipGradByValue", "BeamSearchDecoder",
             "dynamic_decode"] + _c.__all__ + _cm.__all__ + _cn.__all__ + _l.__all__ + _r.__all__ + _t.__all__)
 from . import quant  # noqa: F401,E402
+
+from . import loss  # noqa: E402,F401  (the paddle.nn.loss module path)

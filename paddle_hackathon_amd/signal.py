@@ -6,7 +6,7 @@ import torch
 from .framework.core import _wrap, _unwrap
 from .framework.dispatch import register_ops
 
-__all__ = ["stft", "istft"]
+__all__ = ["stft", "istft", "frame", "overlap_add"]
 
 
 def stft(x, n_fft, hop_length=None, win_length=None, window=None, center=True, pad_mode="reflect",
@@ -29,3 +29,40 @@ def istft(x, n_fft, hop_length=None, win_length=None, window=None, center=True, 
 
 
 register_ops(globals(), __all__)
+
+
+def frame(x, frame_length, hop_length, axis=-1, name=None):
+    """frames of ``frame_length`` every ``hop_length`` samples along the first or last axis
+    (reference: signal.py frame): axis=-1: [..., T] -> [..., frame_length, num_frames];
+    axis=0: [T, ...] -> [num_frames, frame_length, ...]"""
+    t = x._t
+    if axis not in (0, -1, t.dim() - 1):
+        raise ValueError("frame: axis must be 0 or -1")
+    if frame_length > t.shape[axis]:
+        raise ValueError("frame: frame_length exceeds the sequence length")
+    if axis == 0:
+        u = t.unfold(0, frame_length, hop_length)          # [num, ..., frame]
+        return _wrap(u.movedim(-1, 1).contiguous())
+    u = t.unfold(-1, frame_length, hop_length)             # [..., num, frame]
+    return _wrap(u.transpose(-1, -2).contiguous())
+
+
+def overlap_add(x, hop_length, axis=-1, name=None):
+    """the sum of overlapping frames (reference: signal.py overlap_add, the inverse layout of
+    ``frame``): axis=-1: [..., frame_length, num_frames] -> [..., (num - 1) * hop + frame_length];
+    axis=0: [num_frames, frame_length, ...] -> [(num - 1) * hop + frame_length, ...]"""
+    t = x._t
+    if axis == 0:
+        t = t.movedim(0, -1).movedim(0, -2)                # -> [..., frame_length, num_frames]
+    fl, nf = t.shape[-2], t.shape[-1]
+    n = (nf - 1) * hop_length + fl
+    lead = t.shape[:-2]
+    flat = t.reshape(-1, fl, nf)
+    out = torch.nn.functional.fold(flat, output_size=(1, n), kernel_size=(1, fl), stride=(1, hop_length))
+    out = out.reshape(*lead, n)
+    if axis == 0:
+        out = out.movedim(-1, 0)
+    return _wrap(out)
+
+
+register_ops(globals(), ["frame", "overlap_add"])

@@ -18,6 +18,7 @@ from .program import (Variable, Program, Block, OpDesc, default_main_program, de
                       InputSpec, Scope, run_program, plan_program_memory)
 from . import nn  # noqa: F401
 
+
 __all__ = ["BuildStrategy", "CompiledProgram", "ExecutionStrategy", "Executor", "ExponentialMovingAverage", "InputSpec",
            "IpuCompiledProgram", "IpuStrategy", "ParallelExecutor", "Print", "Program", "Variable",
            "WeightNormParamAttr", "accuracy", "append_backward", "auc", "cpu_places", "create_global_var",
@@ -313,3 +314,6 @@ def load_inference_model(path_prefix, executor=None, **kwargs):
     stub = deserialize_program(load_from_file(path_prefix + ".pdmodel"))
     prog = deserialize_persistables(stub, load_from_file(path_prefix + ".pdiparams"), executor)
     return [prog, [v.name for v in stub.feeds], stub.fetches]
+
+
+from . import amp  # noqa: E402,F401  (last: it imports fluid, which imports this package)

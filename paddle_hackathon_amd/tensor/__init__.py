@@ -204,3 +204,13 @@ def _patch():
 
 
 _patch()
+
+
+def __getattr__(name):   # tensor arrays (their module imports fluid, which imports this package)
+    if name in ("create_array", "array_write", "array_read", "array_length"):
+        from . import array as _a
+        return getattr(_a, name)
+    if name in ("stat", "array"):
+        import importlib
+        return importlib.import_module("." + name, __name__)
+    raise AttributeError(name)

@@ -706,3 +706,9 @@ def dot(x, y, name=None):
 
 
 register_ops(globals(), __all__)
+
+
+def inverse(x, name=None):
+    """(reference: tensor/math.py inverse) the matrix inverse over the last two axes"""
+    from .. import linalg
+    return linalg.inv(x)

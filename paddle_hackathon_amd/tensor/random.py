@@ -135,3 +135,10 @@ def randperm(n, dtype="int64", name=None):
 
 register_ops(globals(), ["bernoulli", "poisson", "multinomial", "normal", "normal_", "uniform_",
                          "exponential_", "randint_like"])
+
+
+def gaussian(shape, mean=0.0, std=1.0, dtype=None, name=None):
+    """(reference: tensor/random.py gaussian) samples of N(mean, std^2) with ``shape``"""
+    from .. import normal
+    out = normal(mean, std, shape)
+    return out.astype(dtype) if dtype is not None else out
