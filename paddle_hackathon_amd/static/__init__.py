@@ -316,4 +316,8 @@ def load_inference_model(path_prefix, executor=None, **kwargs):
     return [prog, [v.name for v in stub.feeds], stub.fetches]
 
 
-from . import amp  # noqa: E402,F401  (last: it imports fluid, which imports this package)
+def __getattr__(name):   # paddle.static.amp: imported on first use (it imports fluid, which imports static)
+    if name == "amp":
+        import importlib
+        return importlib.import_module(".amp", __name__)
+    raise AttributeError(name)

@@ -53,3 +53,12 @@ def test_tensor_array_and_switch_program():
         assert paddle.static.default_main_program() is prog
     finally:
         paddle.fluid.framework.switch_main_program(prev)
+
+
+def test_distributed_optional_subsystems_loaded():
+    """paddle.distributed's optional subsystems import together (a circular import there is
+    swallowed by the package's guarded import and would silently drop them)"""
+    d = paddle.distributed
+    for n in ("spawn", "launch", "fleet", "split", "group_sharded_parallel", "ps", "auto_parallel", "passes",
+              "shard_tensor", "shard_op", "ProcessMesh"):
+        assert hasattr(d, n), n
