@@ -262,6 +262,34 @@ def pow2_decay_with_linear_warmup(warmup_steps, total_steps, base_lr, end_lr, na
     return Pow2DecayWithLinearWarmup(learning_rate=base_lr, last_epoch=-1)
 
 
+# ------------------------------------------------------------------------------- rank attention
+def _rank_attention_op(input, rank_offset, rank_param, max_rank=3):
+    """rank_attention_op: instance i of rank r_i (rank_offset[i, 0], 1-based) attends to up to
+    max_rank items — item k has rank rank_offset[i, 2k+1] and row rank_offset[i, 2k+2] of
+    ``input`` — each through the [C, out] block of ``rank_param`` for (r_i - 1, its rank - 1):
+    out[i] = sum_k input[row_k] @ W[(r_i - 1) * max_rank + rank_k - 1] (invalid ranks: 0)"""
+    x, ro, w = _t(input), _t(rank_offset).long(), _t(rank_param)
+    N, C = x.shape
+    out_dim = w.shape[1]
+    lower = ro[:, 0] - 1                                           # [N]
+    faster = ro[:, 1::2][:, :max_rank] - 1                         # [N, K]
+    rows = ro[:, 2::2][:, :max_rank]                               # [N, K]
+    valid = (lower[:, None] >= 0) & (faster >= 0)
+    xk = x[rows.clamp(0, N - 1)] * valid[..., None].to(x.dtype)     # [N, K, C]
+    blk = (lower[:, None].clamp_min(0) * max_rank + faster.clamp_min(0))   # [N, K]
+    wk = w.reshape(max_rank * max_rank, C, out_dim)[blk]           # [N, K, C, out]
+    return _wrap(torch.einsum("nkc,nkco->no", xk, wk.to(x.dtype)))
+
+
+def rank_attention(input, rank_offset, rank_param_shape, rank_param_attr, max_rank=3, max_size=0):
+    """rank-aware attention of CTR models (reference: contrib/layers/nn.py rank_attention): the
+    parameter is [max_rank * max_rank * C, out]"""
+    from ...layer_helper import LayerHelper
+    helper = LayerHelper("rank_attention", input=input, param_attr=rank_param_attr)
+    w = helper.create_parameter(attr=rank_param_attr, shape=list(rank_param_shape), dtype=helper.input_dtype())
+    return _rank_attention_op(input, rank_offset, w, max_rank)
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -279,10 +307,9 @@ fused_embedding_seq_pool = _absent("fused_embedding_seq_pool",
 fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
 search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
 tdm_sampler = _absent("tdm_sampler", "TDM layer-wise sampling is not provided")
-rank_attention = _absent("rank_attention", "rank attention is not provided")
 bilateral_slice = _absent("bilateral_slice", "HDRNet bilateral slicing is not provided")
 _pull_box_extended_sparse = _absent("_pull_box_extended_sparse", "BoxPS pulls are not provided")
 
 
 register_ops(globals(), ["fused_elemwise_activation", "partial_concat", "partial_sum", "shuffle_batch", "_batch_fc_op",
-                         "correlation", "_tdm_child_op", "multiclass_nms2"])
+                         "correlation", "_tdm_child_op", "multiclass_nms2", "_rank_attention_op"])

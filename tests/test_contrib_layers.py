@@ -116,3 +116,25 @@ def test_multiclass_nms2_index_and_absent_ops():
     assert len(o) == len(i) and set(i.tolist()) <= {0, 1, 2}
     with pytest.raises(NotImplementedError):
         C.tree_conv(None, None, 1)
+
+
+def test_rank_attention_matches_reference_formula():
+    """the reference test's gen_input_help / gen_param_help construction, as a loop"""
+    rs = np.random.RandomState(4)
+    max_rank, CH, O = 3, 4, 5
+    rank_offset = np.array([[1, 2, 1, 3, 2, -1, -1], [2, 1, 0, 3, 2, -1, -1], [3, 1, 0, 2, 1, -1, -1],
+                            [1, -1, -1, -1, -1, -1, -1]], "int32")
+    x = rs.randn(4, CH).astype("float32")
+    w = rs.randn(max_rank * max_rank * CH, O).astype("float32")
+    ref = np.zeros((4, O), "float32")
+    for i in range(4):
+        lower = rank_offset[i, 0] - 1
+        for k in range(max_rank):
+            faster = rank_offset[i, 2 * k + 1] - 1
+            if lower < 0 or faster < 0:
+                continue
+            row = rank_offset[i, 2 * k + 2]
+            blk = w[(lower * max_rank + faster) * CH:(lower * max_rank + faster + 1) * CH]
+            ref[i] += x[row] @ blk
+    got = C._rank_attention_op(paddle.to_tensor(x), paddle.to_tensor(rank_offset), paddle.to_tensor(w), max_rank)
+    np.testing.assert_allclose(got.numpy(), ref, rtol=1e-5, atol=1e-5)
