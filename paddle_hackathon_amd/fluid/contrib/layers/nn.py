@@ -7,7 +7,7 @@ Composite tensor programs on the framework's ops (dygraph and static: every func
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text ops of
 this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling, tree_conv,
-fused_embedding_seq_pool, fused_seqpool_cvm, search_pyramid_hash, tdm_sampler, rank_attention,
+fused_embedding_seq_pool, fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
 bilateral_slice, _pull_box_extended_sparse) raise NotImplementedError naming themselves."""
 from __future__ import annotations
 
