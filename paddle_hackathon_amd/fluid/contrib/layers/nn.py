@@ -8,7 +8,7 @@ registered op; batch_fc is one batched GEMM, correlation one channel reduction p
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text ops of
 this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling, tree_conv,
 fused_embedding_seq_pool, fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
-bilateral_slice, _pull_box_extended_sparse) raise NotImplementedError naming themselves."""
+_pull_box_extended_sparse) raise NotImplementedError naming themselves."""
 from __future__ import annotations
 
 import torch
@@ -290,6 +290,45 @@ def rank_attention(input, rank_offset, rank_param_shape, rank_param_attr, max_ra
     return _rank_attention_op(input, rank_offset, w, max_rank)
 
 
+# ------------------------------------------------------------------------------- bilateral slice
+def bilateral_slice(x, guide, grid, has_offset, name=None):
+    """HDRNet bilateral-grid slicing (bilateral_slice_op): per pixel, the affine coefficients are
+    sampled trilinearly from grid [B, GC, GD, GH, GW] at (guide * GD, (y + .5) GH / H,
+    (x + .5) GW / W) (clamped cells, z weight max(1 - sqrt(dz^2 + 1e-8), 0)) and applied to the
+    input channels (+ the offset coefficient with ``has_offset``); differentiable in all three"""
+    xt, gt, gr = _t(x), _t(guide), _t(grid)
+    B, Cin, H, W = xt.shape
+    _, GC, GD, GH, GW = gr.shape
+    dev, dt = xt.device, xt.dtype
+    gx = (torch.arange(W, device=dev, dtype=dt) + 0.5) * GW / W           # [W]
+    gy = (torch.arange(H, device=dev, dtype=dt) + 0.5) * GH / H           # [H]
+    gz = gt * GD                                                           # [B, H, W]
+    fx, fy, fz = torch.floor(gx - 0.5), torch.floor(gy - 0.5), torch.floor(gz - 0.5).detach()
+    bidx = torch.arange(B, device=dev)[:, None, None].expand(B, H, W)
+    coeff = 0
+    for dx in (0, 1):
+        xx = fx + dx
+        wx = torch.clamp(1.0 - (xx + 0.5 - gx).abs(), min=0.0)[None, None, :]
+        xi = xx.clamp(0, GW - 1).long()[None, None, :].expand(B, H, W)
+        for dy in (0, 1):
+            yy = fy + dy
+            wy = torch.clamp(1.0 - (yy + 0.5 - gy).abs(), min=0.0)[None, :, None]
+            yi = yy.clamp(0, GH - 1).long()[None, :, None].expand(B, H, W)
+            for dz in (0, 1):
+                zz = fz + dz
+                wz = torch.clamp(1.0 - torch.sqrt((zz + 0.5 - gz) ** 2 + 1e-8), min=0.0)
+                zi = zz.clamp(0, GD - 1).long()
+                samp = gr.permute(0, 2, 3, 4, 1)[bidx, zi, yi, xi]             # [B, H, W, GC]
+                coeff = coeff + samp * (wx * wy * wz)[..., None]
+    stride = Cin + (1 if has_offset else 0)
+    cout = GC // stride
+    coeff = coeff.reshape(B, H, W, cout, stride)
+    out = (coeff[..., :Cin] * xt.permute(0, 2, 3, 1)[:, :, :, None, :]).sum(-1)
+    if has_offset:
+        out = out + coeff[..., Cin]
+    return _wrap(out.permute(0, 3, 1, 2).contiguous())
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -307,9 +346,9 @@ fused_embedding_seq_pool = _absent("fused_embedding_seq_pool",
 fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
 search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
 tdm_sampler = _absent("tdm_sampler", "TDM layer-wise sampling is not provided")
-bilateral_slice = _absent("bilateral_slice", "HDRNet bilateral slicing is not provided")
 _pull_box_extended_sparse = _absent("_pull_box_extended_sparse", "BoxPS pulls are not provided")
 
 
 register_ops(globals(), ["fused_elemwise_activation", "partial_concat", "partial_sum", "shuffle_batch", "_batch_fc_op",
-                         "correlation", "_tdm_child_op", "multiclass_nms2", "_rank_attention_op"])
+                         "correlation", "_tdm_child_op", "multiclass_nms2", "_rank_attention_op",
+                         "bilateral_slice"])

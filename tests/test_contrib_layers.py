@@ -138,3 +138,45 @@ def test_rank_attention_matches_reference_formula():
             ref[i] += x[row] @ blk
     got = C._rank_attention_op(paddle.to_tensor(x), paddle.to_tensor(rank_offset), paddle.to_tensor(w), max_rank)
     np.testing.assert_allclose(got.numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def _naive_bilateral(grid, guide, inp, has_offset):
+    """the reference test's naive_bilateral_slice_forward, as a loop"""
+    import math
+    B, GC, GD, GH, GW = grid.shape
+    _, Cin, H, W = inp.shape
+    stride = Cin + (1 if has_offset else 0)
+    cout = GC // stride
+    out = np.zeros((B, cout, H, W), "float64")
+    for b in range(B):
+        for oc in range(cout):
+            for y in range(H):
+                for x in range(W):
+                    gx, gy, gz = (x + 0.5) * GW / W, (y + 0.5) * GH / H, guide[b, y, x] * GD
+                    fx, fy, fz = int(np.floor(gx - 0.5)), int(np.floor(gy - 0.5)), int(np.floor(gz - 0.5))
+                    val = 0.0
+                    for ic in range(stride):
+                        cs = 0.0
+                        for xx in (fx, fx + 1):
+                            wx = max(1.0 - abs(xx + 0.5 - gx), 0.0)
+                            for yy in (fy, fy + 1):
+                                wy = max(1.0 - abs(yy + 0.5 - gy), 0.0)
+                                for zz in (fz, fz + 1):
+                                    wz = max(1.0 - math.sqrt((zz + 0.5 - gz) ** 2 + 1e-8), 0.0)
+                                    cs += grid[b, stride * oc + ic, min(max(zz, 0), GD - 1), min(max(yy, 0), GH - 1),
+                                               min(max(xx, 0), GW - 1)] * wx * wy * wz
+                        val += cs * (inp[b, ic, y, x] if ic < Cin else 1.0)
+                    out[b, oc, y, x] = val
+    return out
+
+
+@pytest.mark.parametrize("has_offset", [False, True])
+def test_bilateral_slice_matches_naive(has_offset):
+    rs = np.random.RandomState(5)
+    Cin, cout = 3, 2
+    GC = (Cin + int(has_offset)) * cout
+    grid = rs.randn(2, GC, 4, 3, 5).astype("float32")
+    guide = rs.rand(2, 6, 7).astype("float32")
+    inp = rs.randn(2, Cin, 6, 7).astype("float32")
+    got = C.bilateral_slice(paddle.to_tensor(inp), paddle.to_tensor(guide), paddle.to_tensor(grid), has_offset)
+    np.testing.assert_allclose(got.numpy(), _naive_bilateral(grid, guide, inp, has_offset), rtol=1e-4, atol=1e-4)
