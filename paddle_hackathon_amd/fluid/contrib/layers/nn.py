@@ -6,7 +6,7 @@ tdm_child_op, optimizers/pow2_decay_with_linear_warmup_op, detection/multiclass_
 Composite tensor programs on the framework's ops (dygraph and static: every function is a
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text ops of
-this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling, tree_conv,
+this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling,
 fused_embedding_seq_pool, fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
 _pull_box_extended_sparse) raise NotImplementedError naming themselves."""
 from __future__ import annotations
@@ -329,6 +329,63 @@ def bilateral_slice(x, guide, grid, has_offset, name=None):
     return _wrap(out.permute(0, 3, 1, 2).contiguous())
 
 
+# ------------------------------------------------------------------------------- tree conv
+def _tree_patch_coeffs(edges, n, max_depth):
+    """[n, n, 3] (eta_l, eta_r, eta_t) of node v in the patch of node u (tree_conv_op / TBCNN):
+    the patch of u is u itself (depth 0) and its descendants down to depth max_depth - 1; a child
+    at position idx of l siblings at depth d has eta_t = (max_depth - d) / max_depth,
+    eta_l = (1 - eta_t) * (0.5 if l == 1 else (idx - 1) / (l - 1)), eta_r = (1 - eta_t)(1 - eta_l)"""
+    import numpy as np
+    children = [[] for _ in range(n + 1)]
+    for a, b in edges:
+        if a > 0 and b > 0:
+            children[a].append(b)
+    E = np.zeros((n, n, 3), np.float64)
+
+    def add(u, v, idx, l, d):
+        et = (max_depth - d) / max_depth
+        el = (1.0 - et) * (0.5 if l == 1 else (idx - 1.0) / (l - 1.0))
+        E[u - 1, v - 1] += (el, (1.0 - et) * (1.0 - el), et)
+
+    def rec(u, node, d):
+        cs = children[node]
+        for idx, c in enumerate(cs, 1):
+            if d + 1 < max_depth:
+                add(u, c, idx, len(cs), d + 1)
+                rec(u, c, d + 1)
+    for u in range(1, n + 1):
+        add(u, u, 1, 1, 0)
+        rec(u, u, 0)
+    return E
+
+
+def _tree_conv_op(nodes_vector, edge_set, filter, max_depth=2):
+    """out[b, u] = sum_v x[b, v] (eta_l W_l + eta_r W_r + eta_t W_t) over the patch of u;
+    filter [F, 3, out, filters] -> out [B, n, out, filters]"""
+    x, w = _t(nodes_vector), _t(filter)
+    es = _t(edge_set).detach().cpu().long().numpy()
+    B, n, F = x.shape
+    coeffs = torch.stack([torch.from_numpy(_tree_patch_coeffs(es[b].tolist(), n, max_depth)) for b in range(B)])
+    coeffs = coeffs.to(device=x.device, dtype=x.dtype)                     # [B, n, n, 3]
+    return _wrap(torch.einsum("buvk,bvf,fkos->buos", coeffs, x, w.to(x.dtype)))
+
+
+def tree_conv(nodes_vector, edge_set, output_size, num_filters=1, max_depth=2, act="tanh", param_attr=None,
+              bias_attr=None, name=None):
+    """tree-based convolution (TBCNN): nodes_vector [B, n, F], edge_set [B, E, 2] (parent, child;
+    1-based, 0 = padding) -> act(conv + bias) [B, n, output_size, num_filters]"""
+    from ...layer_helper import LayerHelper
+    helper = LayerHelper("tree_conv", input=nodes_vector, nodes_vector=nodes_vector, act=act,
+                         param_attr=param_attr, bias_attr=bias_attr)
+    F = nodes_vector.shape[2]
+    w = helper.create_parameter(attr=param_attr, shape=[F, 3, output_size, num_filters],
+                                dtype=nodes_vector._t.dtype)
+    out = _tree_conv_op(nodes_vector, edge_set, w, max_depth)
+    if helper.bias_attr:
+        out = helper.append_bias_op(out)
+    return helper.append_activation(out)
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -340,7 +397,6 @@ def _absent(name, why):
 var_conv_2d = _absent("var_conv_2d", "LoD variable-size 2-D convolution is not provided")
 match_matrix_tensor = _absent("match_matrix_tensor", "LoD matching tensor is not provided")
 sequence_topk_avg_pooling = _absent("sequence_topk_avg_pooling", "LoD top-k average pooling is not provided")
-tree_conv = _absent("tree_conv", "tree-based convolution is not provided")
 fused_embedding_seq_pool = _absent("fused_embedding_seq_pool",
                                    "use embedding + fluid.layers.sequence_pool (same result, two ops)")
 fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
@@ -351,4 +407,4 @@ _pull_box_extended_sparse = _absent("_pull_box_extended_sparse", "BoxPS pulls ar
 
 register_ops(globals(), ["fused_elemwise_activation", "partial_concat", "partial_sum", "shuffle_batch", "_batch_fc_op",
                          "correlation", "_tdm_child_op", "multiclass_nms2", "_rank_attention_op",
-                         "bilateral_slice"])
+                         "bilateral_slice", "_tree_conv_op"])

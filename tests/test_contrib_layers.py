@@ -115,7 +115,7 @@ def test_multiclass_nms2_index_and_absent_ops():
     o, i = out.numpy(), idx.numpy().reshape(-1)
     assert len(o) == len(i) and set(i.tolist()) <= {0, 1, 2}
     with pytest.raises(NotImplementedError):
-        C.tree_conv(None, None, 1)
+        C.var_conv_2d(None, None, None, 1, 1)
 
 
 def test_rank_attention_matches_reference_formula():
@@ -180,3 +180,37 @@ def test_bilateral_slice_matches_naive(has_offset):
     inp = rs.randn(2, Cin, 6, 7).astype("float32")
     got = C.bilateral_slice(paddle.to_tensor(inp), paddle.to_tensor(guide), paddle.to_tensor(grid), has_offset)
     np.testing.assert_allclose(got.numpy(), _naive_bilateral(grid, guide, inp, has_offset), rtol=1e-4, atol=1e-4)
+
+
+def test_tree_conv_matches_reference_patches():
+    """the reference test's collect_node_patch / get_output_naive, as loops (its 17-node tree)"""
+    n, F, O, NF, depth = 17, 3, 2, 2, 2
+    adj = np.array([1, 2, 1, 3, 1, 4, 1, 5, 2, 6, 2, 7, 2, 8, 4, 9, 4, 10, 5, 11, 6, 12, 6, 13, 9, 14, 9, 15, 9, 16,
+                    9, 17], "int32").reshape(1, n - 1, 2).repeat(2, 0)
+    rs = np.random.RandomState(6)
+    vec = rs.rand(2, n, F).astype("float32")
+    W = rs.rand(F, 3, O, NF).astype("float32")
+    og = [[] for _ in range(n + 2)]
+    for a, b in adj[0]:
+        og[a].append(b)
+    Wt = np.transpose(W, (1, 0, 2, 3))
+    ref = np.zeros((2, n, O, NF), "float64")
+    for bi in range(2):
+        for u in range(1, n + 1):
+            patch = [(u, 1, 1, 0)]
+
+            def rec(node, d):
+                for idx, c in enumerate(og[node], 1):
+                    if d + 1 < depth:
+                        patch.append((c, idx, len(og[node]), d + 1))
+                        rec(c, d + 1)
+            rec(u, 0)
+            for v, idx, l, d in patch:
+                et = (depth - d) / depth
+                el = (1 - et) * (0.5 if l == 1 else (idx - 1) / (l - 1))
+                er = (1 - et) * (1 - el)
+                ref[bi, u - 1] += np.tensordot(vec[bi, v - 1], np.tensordot(np.array([el, er, et]), Wt, 1), 1)
+    got = C._tree_conv_op(paddle.to_tensor(vec), paddle.to_tensor(adj), paddle.to_tensor(W), depth)
+    np.testing.assert_allclose(got.numpy(), ref, rtol=1e-4, atol=1e-5)
+    out = C.tree_conv(paddle.to_tensor(vec), paddle.to_tensor(adj), O, NF, depth)
+    assert out.shape == [2, n, O, NF]
