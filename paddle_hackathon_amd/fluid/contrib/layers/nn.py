@@ -7,7 +7,7 @@ Composite tensor programs on the framework's ops (dygraph and static: every func
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text ops of
 this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling,
-fused_embedding_seq_pool, fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
+fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
 _pull_box_extended_sparse) raise NotImplementedError naming themselves."""
 from __future__ import annotations
 
@@ -386,6 +386,18 @@ def tree_conv(nodes_vector, edge_set, output_size, num_filters=1, max_depth=2, a
     return helper.append_activation(out)
 
 
+# ------------------------------------------------------------------------------- embedding + pool
+def fused_embedding_seq_pool(input, size, is_sparse=False, padding_idx=None, combiner="sum", param_attr=None,
+                             dtype="float32"):
+    """fused_embedding_seq_pool_op: the embedding rows of each sequence of the LoD ids summed
+    (combiner "sum") — the framework's embedding and LoD sequence_pool"""
+    from ... import layers as L
+    if combiner != "sum":
+        raise ValueError("fused_embedding_seq_pool: combiner must be 'sum'")
+    emb = L.embedding(input, size, is_sparse=is_sparse, padding_idx=padding_idx, param_attr=param_attr, dtype=dtype)
+    return L.sequence_pool(emb, "sum")
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -397,8 +409,6 @@ def _absent(name, why):
 var_conv_2d = _absent("var_conv_2d", "LoD variable-size 2-D convolution is not provided")
 match_matrix_tensor = _absent("match_matrix_tensor", "LoD matching tensor is not provided")
 sequence_topk_avg_pooling = _absent("sequence_topk_avg_pooling", "LoD top-k average pooling is not provided")
-fused_embedding_seq_pool = _absent("fused_embedding_seq_pool",
-                                   "use embedding + fluid.layers.sequence_pool (same result, two ops)")
 fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
 search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
 tdm_sampler = _absent("tdm_sampler", "TDM layer-wise sampling is not provided")
