@@ -5,10 +5,10 @@ tdm_child_op, optimizers/pow2_decay_with_linear_warmup_op, detection/multiclass_
 
 Composite tensor programs on the framework's ops (dygraph and static: every function is a
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
-fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text ops of
-this module (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling,
-fused_seqpool_cvm, search_pyramid_hash, tdm_sampler,
-_pull_box_extended_sparse) raise NotImplementedError naming themselves."""
+fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text
+matching ops (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling) work on LoDTensors in
+dygraph. fused_seqpool_cvm, search_pyramid_hash, tdm_sampler and _pull_box_extended_sparse raise
+NotImplementedError naming themselves."""
 from __future__ import annotations
 
 import torch
@@ -398,6 +398,150 @@ def fused_embedding_seq_pool(input, size, is_sparse=False, padding_idx=None, com
     return L.sequence_pool(emb, "sum")
 
 
+# ------------------------------------------------------------------------------- LoD text matching
+# The MatchPyramid-style ops: every sequence i of a 1-level LoD batch is its own small matrix/image
+# whose sizes come from the LoD of ``row``/``col`` (or of x/y). Each op is one batched torch call per
+# sequence (the batch is a python loop over sequences; each sequence's work is a GEMM / conv /
+# top-k on the device), autograd gives the grads. Outputs are [numel, 1] LoD tensors like the
+# reference's; dygraph / LoDTensor inputs (the LoD is host metadata).
+def _seq_lengths(t, what):
+    from ... import core as fcore
+    lod = fcore.lod_of(t)
+    if not lod:
+        raise ValueError(f"{what} must be a 1-level LoD tensor")
+    return fcore._lengths_from_offsets(lod[-1])
+
+
+def _lod_wrap(t, lens):
+    from ... import core as fcore
+    o = _wrap(t)
+    o._lod = [fcore._offsets_from_lengths(lens)]
+    return o
+
+
+def _match_matrix_tensor_op(x, y, w, dim_t):
+    """match_matrix_tensor_op (reference: operators/match_matrix_tensor_op.cc): for sequence pair
+    (a [n, h] of x, b [m, h] of y), Tmp = a . W as [n, dim_t, h] and Out[t] = (a W_t) b^T as
+    [dim_t, n, m]; both flattened per sequence. W is [h, dim_t, h]."""
+    xt, yt, wt = _t(x), _t(y), _t(w)
+    xl, yl = _seq_lengths(x, "match_matrix_tensor x"), _seq_lengths(y, "match_matrix_tensor y")
+    if len(xl) != len(yl):
+        raise ValueError(f"match_matrix_tensor: x has {len(xl)} sequences, y {len(yl)}")
+    tmp = torch.einsum("nh,htk->ntk", xt, wt.to(xt.dtype))          # one GEMM over every x row
+    outs, lens, xo, yo = [], [], 0, 0
+    for n, m in zip(xl, yl):
+        o = torch.einsum("ntk,mk->tnm", tmp[xo:xo + n], yt[yo:yo + m])
+        outs.append(o.reshape(-1))
+        lens.append(o.numel())
+        xo, yo = xo + n, yo + m
+    out = torch.cat(outs).reshape(-1, 1) if outs else xt.new_zeros(0, 1)
+    return _lod_wrap(out, lens), _lod_wrap(tmp.reshape(-1, 1).detach(), [n * dim_t * wt.shape[0] for n in xl])
+
+
+def match_matrix_tensor(x, y, channel_num, act=None, param_attr=None, dtype="float32", name=None):
+    """semantic matching matrix of two LoD word sequences through a learnable [h, channel_num, h]
+    W (reference: contrib/layers/nn.py match_matrix_tensor); returns (act(Out), Tmp)"""
+    from ...layer_helper import LayerHelper
+    h = x.shape[-1]
+    if len(x.shape) != 2 or len(y.shape) != 2 or y.shape[-1] != h:
+        raise ValueError(f"match_matrix_tensor: x {x.shape} and y {y.shape} must be [*, h] with one h")
+    helper = LayerHelper("match_matrix_tensor", param_attr=param_attr, act=act)
+    w = helper.create_parameter(attr=param_attr, shape=[h, channel_num, h], dtype=dtype)
+    out, tmp = _match_matrix_tensor_op(x, y, w, channel_num)
+    res = helper.append_activation(out)
+    res._lod = out._lod
+    return res, tmp
+
+
+def _var_conv_2d_op(input, row, col, w, input_channel, output_channel, stride=(1, 1), filter_size=(3, 3)):
+    """var_conv_2d_op (reference: operators/var_conv_2d_op.cc): sequence i of ``input`` is a
+    [C_in, rows_i, cols_i] image (rows/cols from the LoD of ``row``/``col``) convolved with the
+    [C_out, C_in*kh*kw] filter, "same"-style padding (kh//2 above, kw//2 left), stride s: output
+    [C_out, (rows-1)//s_h + 1, (cols-1)//s_w + 1] flattened. Also returns the im2col matrix (Col)."""
+    xt, wt = _t(input).reshape(-1), _t(w)
+    kh, kw = filter_size
+    sh, sw = stride
+    rows, cols = _seq_lengths(row, "var_conv_2d row"), _seq_lengths(col, "var_conv_2d col")
+    wk = wt.reshape(output_channel, input_channel, kh, kw).to(xt.dtype)
+    pad = (kw // 2, kw - 1 - kw // 2, kh // 2, kh - 1 - kh // 2)
+    outs, cols_out, olens, clens, off = [], [], [], [], 0
+    for H, W in zip(rows, cols):
+        n = input_channel * H * W
+        if H == 0 or W == 0:
+            olens.append(0)
+            clens.append(0)
+            off += n
+            continue
+        img = TF.pad(xt[off:off + n].reshape(1, input_channel, H, W), pad)
+        o = TF.conv2d(img, wk, stride=(sh, sw))
+        outs.append(o.reshape(-1))
+        olens.append(o.numel())
+        c = TF.unfold(img.detach(), (kh, kw), stride=(sh, sw))
+        cols_out.append(c.reshape(-1))
+        clens.append(c.numel())
+        off += n
+    if off != xt.numel():
+        raise ValueError(f"var_conv_2d: input has {xt.numel()} values, row/col/channels describe {off}")
+    out = torch.cat(outs).reshape(-1, 1) if outs else xt.new_zeros(0, 1)
+    colm = torch.cat(cols_out).reshape(-1, 1) if cols_out else xt.new_zeros(0, 1)
+    return _lod_wrap(out, olens), _lod_wrap(colm, clens)
+
+
+def var_conv_2d(input, row, col, input_channel, output_channel, filter_size, stride=1, param_attr=None, act=None,
+                dtype="float32", name=None):
+    """2-D convolution over variable-size LoD images (reference: contrib/layers/nn.py var_conv_2d)"""
+    from ...layer_helper import LayerHelper
+    fs = [filter_size] * 2 if isinstance(filter_size, int) else list(filter_size)
+    st = [stride] * 2 if isinstance(stride, int) else list(stride)
+    helper = LayerHelper("var_conv_2d", param_attr=param_attr, act=act)
+    w = helper.create_parameter(attr=param_attr, shape=[output_channel, input_channel * fs[0] * fs[1]], dtype=dtype)
+    out, _ = _var_conv_2d_op(input, row, col, w, input_channel, output_channel, st, fs)
+    res = helper.append_activation(out)
+    res._lod = out._lod
+    return res
+
+
+def _sequence_topk_avg_pooling_op(input, row, col, topks, channel_num):
+    """sequence_topk_avg_pooling_op (reference: operators/sequence_ops/
+    sequence_topk_avg_pooling_op.h): sequence i of ``input`` is [channel_num, rows_i, cols_i]; for
+    every (row, channel) the mean of the k largest of its cols_i values for each k in ``topks``
+    (missing values count as 0). Out is [sum rows, channel_num * len(topks)] with the LoD of
+    ``row``; pos holds the top-max_k column indices (-1 where cols_i < max_k)."""
+    xt = _t(input).reshape(-1)
+    rows, cols = _seq_lengths(row, "sequence_topk_avg_pooling row"), _seq_lengths(col, "sequence_topk_avg_pooling col")
+    topks = [int(k) for k in topks]
+    K = max(topks)
+    kidx = torch.tensor([k - 1 for k in topks], device=xt.device)
+    kdiv = torch.tensor(topks, dtype=xt.dtype, device=xt.device)
+    outs, poss, off = [], [], 0
+    for H, W in zip(rows, cols):
+        n = channel_num * H * W
+        seq = xt[off:off + n].reshape(channel_num, H, W).transpose(0, 1)     # [H, ch, W]
+        off += n
+        kk = min(K, W)
+        if kk > 0:
+            val, pos = torch.topk(seq, kk, dim=-1)
+        else:
+            val = seq.new_zeros(H, channel_num, 0)
+            pos = torch.zeros(H, channel_num, 0, dtype=torch.long, device=xt.device)
+        if kk < K:
+            val = torch.cat([val, val.new_zeros(H, channel_num, K - kk)], -1)
+            pos = torch.cat([pos, pos.new_full((H, channel_num, K - kk), -1)], -1)
+        outs.append((val.cumsum(-1)[..., kidx] / kdiv).reshape(H, -1))
+        poss.append(pos.reshape(-1))
+    if off != xt.numel():
+        raise ValueError(f"sequence_topk_avg_pooling: input has {xt.numel()} values, row/col/channels describe {off}")
+    out = torch.cat(outs) if outs else xt.new_zeros(0, channel_num * len(topks))
+    pos = torch.cat(poss).int() if poss else torch.zeros(0, dtype=torch.int32, device=xt.device)
+    return _lod_wrap(out, rows), _wrap(pos)
+
+
+def sequence_topk_avg_pooling(input, row, col, topks, channel_num):
+    """top-k average pooling of LoD matching matrices (reference: contrib/layers/nn.py
+    sequence_topk_avg_pooling); returns Out with the LoD of ``row``"""
+    return _sequence_topk_avg_pooling_op(input, row, col, topks, channel_num)[0]
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -406,9 +550,6 @@ def _absent(name, why):
     return f
 
 
-var_conv_2d = _absent("var_conv_2d", "LoD variable-size 2-D convolution is not provided")
-match_matrix_tensor = _absent("match_matrix_tensor", "LoD matching tensor is not provided")
-sequence_topk_avg_pooling = _absent("sequence_topk_avg_pooling", "LoD top-k average pooling is not provided")
 fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
 search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
 tdm_sampler = _absent("tdm_sampler", "TDM layer-wise sampling is not provided")

@@ -115,7 +115,7 @@ def test_multiclass_nms2_index_and_absent_ops():
     o, i = out.numpy(), idx.numpy().reshape(-1)
     assert len(o) == len(i) and set(i.tolist()) <= {0, 1, 2}
     with pytest.raises(NotImplementedError):
-        C.var_conv_2d(None, None, None, 1, 1)
+        C.search_pyramid_hash(None, 1, 1)
 
 
 def test_rank_attention_matches_reference_formula():
@@ -227,3 +227,120 @@ def test_fused_embedding_seq_pool_lod():
         initializer=paddle.nn.initializer.Assign(np.arange(15, dtype="float32").reshape(5, 3))))
     W = np.arange(15, dtype="float32").reshape(5, 3)
     np.testing.assert_allclose(out.numpy(), [W[1] + W[2], W[3], W[0] + 2 * W[4]])
+
+
+def _lod_tensor(arr, lens):
+    from paddle_hackathon_amd.fluid import core
+    t = core.LoDTensor()
+    t.set(arr, core.CPUPlace())
+    t.set_recursive_sequence_lengths([lens])
+    return t
+
+
+def test_match_matrix_tensor_lod():
+    """per sequence pair: out[t, i, j] = x_i . W[:, t, :] . y_j (reference test_match_matrix_tensor_op
+    shapes: h 20, dim_t 4, x lod [1, 2, 2], y lod [3, 1, 4]), grads through autograd"""
+    rng = np.random.default_rng(0)
+    h, T_, xl, yl = 20, 4, [1, 2, 2], [3, 1, 4]
+    x, y = rng.random((5, h), dtype=np.float32), rng.random((8, h), dtype=np.float32)
+    w = rng.random((h, T_, h), dtype=np.float32)
+    xt, yt = _lod_tensor(x, xl), _lod_tensor(y, yl)
+    xt.stop_gradient = False
+    out, tmp = C._match_matrix_tensor_op(xt, yt, paddle.to_tensor(w), T_)
+    ref, xo, yo = [], 0, 0
+    for n, m in zip(xl, yl):
+        a, b = x[xo:xo + n], y[yo:yo + m]
+        for t in range(T_):
+            ref.append((a @ w[:, t, :] @ b.T).reshape(-1))
+        xo, yo = xo + n, yo + m
+    np.testing.assert_allclose(out.numpy().reshape(-1), np.concatenate(ref), rtol=1e-5)
+    assert out._lod == [[0, 12, 20, 52]]          # dim_t * n * m per pair: 12, 8, 32
+    np.testing.assert_allclose(tmp.numpy().reshape(-1), np.einsum("nh,htk->ntk", x, w).reshape(-1), rtol=1e-5)
+    out.sum().backward()
+    gx = np.concatenate([np.einsum("htk,mk->h", w, y[yo:yo + m]).reshape(1, h).repeat(n, 0)
+                         for n, m, yo in zip(xl, yl, [0, 3, 4])])
+    np.testing.assert_allclose(xt.grad.numpy(), gx, rtol=1e-4)
+
+
+def _var_conv_ref(x, rows, cols, w, cin, cout, kh, kw, sh, sw):
+    out, off = [], 0
+    for H, W in zip(rows, cols):
+        img = x[off:off + cin * H * W].reshape(cin, H, W)
+        off += cin * H * W
+        th, tw = (H - 1) // sh + 1, (W - 1) // sw + 1
+        o = np.zeros((cout, th, tw), np.float64)
+        for oy in range(th):
+            for ox in range(tw):
+                for ky in range(kh):
+                    for kx in range(kw):
+                        iy, ix = oy * sh + ky - kh // 2, ox * sw + kx - kw // 2
+                        if 0 <= iy < H and 0 <= ix < W:
+                            o[:, oy, ox] += w[:, :, ky, kx] @ img[:, iy, ix]
+        out.append(o.reshape(-1))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("cin,cout,fs,st,rows,cols", [(8, 2, (2, 3), (1, 1), [2, 4], [3, 2]),
+                                                        (1, 2, (2, 3), (1, 1), [1, 10], [8, 4]),
+                                                        (3, 4, (3, 3), (2, 2), [5, 4], [6, 7])])
+def test_var_conv_2d_lod(cin, cout, fs, st, rows, cols):
+    """same shapes as the reference test_var_conv_2d cases; oracle is the direct padded sum"""
+    rng = np.random.default_rng(1)
+    feats = [r * c for r, c in zip(rows, cols)]
+    x = rng.random((sum(feats) * cin, 1), dtype=np.float32)
+    w = rng.random((cout, cin * fs[0] * fs[1]), dtype=np.float32)
+    xt = _lod_tensor(x, [f * cin for f in feats])
+    rt = _lod_tensor(np.zeros((sum(rows), 10), np.float32), rows)
+    ct = _lod_tensor(np.zeros((sum(cols), 10), np.float32), cols)
+    out, col = C._var_conv_2d_op(xt, rt, ct, paddle.to_tensor(w), cin, cout, st, fs)
+    ref = _var_conv_ref(x.reshape(-1), rows, cols, w.reshape(cout, cin, *fs), cin, cout, *fs, *st)
+    np.testing.assert_allclose(out.numpy().reshape(-1), ref, rtol=1e-5)
+    lens = [cout * ((r - 1) // st[0] + 1) * ((c - 1) // st[1] + 1) for r, c in zip(rows, cols)]
+    assert out._lod == [list(np.cumsum([0] + lens))]
+    # Out = W . Col per sequence
+    co = 0
+    K = cin * fs[0] * fs[1]
+    o_all, oo = out.numpy().reshape(-1), 0
+    for L in lens:
+        n = L // cout
+        np.testing.assert_allclose((w @ col.numpy().reshape(-1)[co:co + K * n].reshape(K, n)).reshape(-1),
+                                   o_all[oo:oo + L], rtol=1e-5)
+        co, oo = co + K * n, oo + L
+    # public layer: parameter shape and activation
+    y = C.var_conv_2d(xt, rt, ct, cin, cout, list(fs), list(st), act="relu")
+    assert y.shape == [sum(lens), 1] and y._lod == out._lod
+
+
+@pytest.mark.parametrize("topks,ch,rows,cols", [([1, 3, 5], 3, [30, 45], [25, 36]), ([2, 3], 5, [36], [48]),
+                                                 ([1, 4], 2, [3, 2], [2, 5])])
+def test_sequence_topk_avg_pooling_lod(topks, ch, rows, cols):
+    """reference test_sequence_topk_avg_pooling layout: out[r, c * len(topks) + j] = mean of the
+    topks[j] largest values of row r / channel c (zeros past the row's width); grad = 1/k per pick"""
+    feats = [r * c for r, c in zip(rows, cols)]
+    x = np.random.default_rng(2).permutation(sum(feats) * ch).astype(np.float32)
+    xt = _lod_tensor(x.reshape(-1, 1), [f * ch for f in feats])
+    xt.stop_gradient = False
+    rt = _lod_tensor(np.zeros((sum(rows), 4), np.float32), rows)
+    ct = _lod_tensor(np.zeros((sum(cols), 4), np.float32), cols)
+    out, pos = C._sequence_topk_avg_pooling_op(xt, rt, ct, topks, ch)
+    K = max(topks)
+    ref, g, off = [], np.zeros_like(x), 0
+    for H, W in zip(rows, cols):
+        blk = x[off:off + ch * H * W].reshape(ch, H, W)
+        for r in range(H):
+            row = []
+            for c in range(ch):
+                order = np.argsort(-blk[c, r])[:K]
+                vals = np.concatenate([blk[c, r][order], np.zeros(K - len(order))])
+                for k in topks:
+                    row.append(vals[:k].sum() / k)
+                    for p in order[:k]:
+                        g[off + c * H * W + r * W + p] += 1.0 / k
+            ref.append(row)
+        off += ch * H * W
+    np.testing.assert_allclose(out.numpy(), np.array(ref), rtol=1e-5)
+    assert out._lod == [list(np.cumsum([0] + rows))]
+    assert pos.shape == [sum(rows) * ch * K]
+    out.sum().backward()
+    np.testing.assert_allclose(xt.grad.numpy().reshape(-1), g, rtol=1e-5)
+    assert C.sequence_topk_avg_pooling(xt, rt, ct, topks, ch).shape == [sum(rows), ch * len(topks)]
