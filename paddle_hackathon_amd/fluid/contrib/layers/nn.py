@@ -7,8 +7,8 @@ Composite tensor programs on the framework's ops (dygraph and static: every func
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text
 matching ops (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling) work on LoDTensors in
-dygraph. fused_seqpool_cvm, search_pyramid_hash, tdm_sampler and _pull_box_extended_sparse raise
-NotImplementedError naming themselves."""
+dygraph, as do fused_seqpool_cvm and tdm_sampler. search_pyramid_hash and
+_pull_box_extended_sparse raise NotImplementedError naming themselves."""
 from __future__ import annotations
 
 import torch
@@ -542,6 +542,136 @@ def sequence_topk_avg_pooling(input, row, col, topks, channel_num):
     return _sequence_topk_avg_pooling_op(input, row, col, topks, channel_num)[0]
 
 
+# ------------------------------------------------------------------------------- CTR sequence pool + CVM
+class _SeqpoolCVM(torch.autograd.Function):
+    """fused_seqpool_cvm_op (reference: operators/fused/fused_seqpool_cvm_op.cu): per slot, the
+    rows of each LoD sequence summed (plus pad_value) by one index_add; with use_cvm the first two
+    columns become log(show+1) and log(click+1)-log(show+1), without it the cvm_offset columns are
+    dropped. The op's gradient is not the calculus one: every row of a sequence receives the
+    sequence's CVM values in its first cvm_offset columns and the output grad in the rest."""
+
+    @staticmethod
+    def forward(ctx, x, cvm, seg, B, pad_value, use_cvm, cvm_offset):
+        pooled = x.new_full((B, x.shape[1]), pad_value).index_add_(0, seg, x)
+        if use_cvm:
+            ls = torch.log(pooled[:, :1] + 1)
+            out = torch.cat([ls, torch.log(pooled[:, 1:2] + 1) - ls, pooled[:, 2:]], 1)
+        else:
+            out = pooled[:, cvm_offset:].clone()
+        ctx.save_for_backward(cvm, seg)
+        ctx.cfg = (use_cvm, cvm_offset)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        cvm, seg = ctx.saved_tensors
+        use_cvm, off = ctx.cfg
+        rest = g[:, off:] if use_cvm else g
+        rows = torch.cat([cvm[:, :off].to(g.dtype), rest], 1)        # [B, E]
+        return rows[seg], None, None, None, None, None, None
+
+
+def fused_seqpool_cvm(input, pool_type, cvm, pad_value=0.0, use_cvm=True, cvm_offset=2):
+    """sum sequence pool + continuous value model over a list of LoD slot embeddings
+    (reference: contrib/layers/nn.py fused_seqpool_cvm); returns one [batch, E] (use_cvm) or
+    [batch, E - cvm_offset] tensor per slot"""
+    from ... import core as fcore
+    if pool_type.upper() != "SUM":
+        raise ValueError(f"fused_seqpool_cvm only support SUM pooling now, and your type is: {pool_type}")
+    if not isinstance(input, (list, tuple)):
+        raise TypeError("fused_seqpool_cvm: input must be a list of LoD tensors")
+    c = _t(cvm)
+    outs = []
+    for x in input:
+        xt = _t(x)
+        lens = _seq_lengths(x, "fused_seqpool_cvm input")
+        seg = torch.repeat_interleave(torch.arange(len(lens), device=xt.device),
+                                      torch.tensor(lens, device=xt.device))
+        o = _wrap(_SeqpoolCVM.apply(xt, c, seg, len(lens), float(pad_value), bool(use_cvm), int(cvm_offset)))
+        o._lod = [fcore._offsets_from_lengths([1] * len(lens))]
+        outs.append(o)
+    return outs
+
+
+# ------------------------------------------------------------------------------- TDM sampling
+def _tdm_sampler_op(x, travel, layer, neg_samples_num_list, layer_offset_lod, output_positive=True, seed=0,
+                    dtype="int32"):
+    """tdm_sampler_op (reference: operators/tdm_sampler_op.h): for item x_i, layer l of the tree:
+    the positive node travel[x_i, l] (label 1) then neg_samples_num_list[l] distinct other nodes of
+    that layer drawn uniformly (label 0); a 0 (padding) positive gives all-zero samples with mask 0.
+    The draw is one random-key argsort per layer over the whole batch (without replacement,
+    positive excluded) instead of a per-item rejection loop."""
+    xt = _t(x).reshape(-1).long()
+    tr, ly = _t(travel).long(), _t(layer).reshape(-1).long()
+    od = {"int32": torch.int32, "int64": torch.int64}[str(dtype).replace("paddle.", "")]
+    gen = None
+    if seed:
+        gen = torch.Generator(device=xt.device)
+        gen.manual_seed(int(seed))
+    B = xt.numel()
+    outs, labels, masks = [], [], []
+    pos_all = tr[xt]                                                 # [B, L]
+    for l, k in enumerate(neg_samples_num_list):
+        lo, hi = layer_offset_lod[l], layer_offset_lod[l + 1]
+        nodes = ly[lo:hi]
+        if k > hi - lo - 1:
+            raise ValueError(f"tdm_sampler: {k} negatives at layer {l} but it has {hi - lo} nodes")
+        pos = pos_all[:, l]
+        bad = (pos != 0) & ((pos < nodes.min()) | (pos > nodes.max())) if len(nodes) else pos != 0
+        if bool(bad.any()):
+            raise ValueError(f"tdm_sampler: positive node id outside layer {l}")
+        cols, lab, msk = [], [], []
+        valid = (pos != 0).long()
+        if output_positive:
+            cols.append(pos[:, None])
+            lab.append(valid[:, None])
+            msk.append(valid[:, None])
+        if k:
+            keys = torch.rand(B, hi - lo, generator=gen, device=xt.device)
+            keys = keys.masked_fill(nodes[None, :] == pos[:, None], 2.0)
+            neg = nodes[keys.argsort(1)[:, :k]] * valid[:, None]
+            cols.append(neg)
+            lab.append(torch.zeros_like(neg))
+            msk.append(valid[:, None].expand(B, k))
+        outs.append(torch.cat(cols, 1))
+        labels.append(torch.cat(lab, 1))
+        masks.append(torch.cat(msk, 1))
+    return tuple(_wrap(torch.cat(v, 1).to(od)) for v in (outs, labels, masks))
+
+
+def tdm_sampler(x, neg_samples_num_list, layer_node_num_list, leaf_node_num, tree_travel_attr=None,
+                tree_layer_attr=None, output_positive=True, output_list=True, seed=0, tree_dtype="int32",
+                dtype="int32"):
+    """layer-wise negative sampling on a TDM tree (reference: contrib/layers/nn.py tdm_sampler);
+    travel [leaf_node_num, layers] and layer [node_nums, 1] are parameters like the reference's"""
+    from ...layer_helper import LayerHelper
+    from ....nn.initializer import Constant
+    if len(neg_samples_num_list) != len(layer_node_num_list):
+        raise ValueError("The shape of negative samples list must match the shape of layers.")
+    lod = [0]
+    for l, n in enumerate(layer_node_num_list):
+        if neg_samples_num_list[l] >= n:
+            raise ValueError(f"The number of negative samples must be less than the number of nodes in the layer {l}")
+        lod.append(lod[-1] + n)
+    if leaf_node_num >= lod[-1]:
+        raise ValueError("leaf_node_num must be less than total node nums.")
+    helper = LayerHelper("tdm_sampler")
+    travel = helper.create_parameter(attr=tree_travel_attr, shape=[leaf_node_num, len(layer_node_num_list)],
+                                     dtype=tree_dtype, default_initializer=Constant(0))
+    layer = helper.create_parameter(attr=tree_layer_attr, shape=[lod[-1], 1], dtype=tree_dtype,
+                                    default_initializer=Constant(0))
+    out, labels, mask = _tdm_sampler_op(x, travel, layer, neg_samples_num_list, lod, output_positive, seed, dtype)
+    if not output_list:
+        return out, labels, mask
+    res, s, pf = ([], [], []), 0, int(bool(output_positive))
+    for k in neg_samples_num_list:
+        e = s + k + pf
+        for lst, t in zip(res, (out, labels, mask)):
+            lst.append(_wrap(t._t[:, s:e].reshape(-1, k + pf, 1)))
+        s = e
+    return res
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -550,9 +680,7 @@ def _absent(name, why):
     return f
 
 
-fused_seqpool_cvm = _absent("fused_seqpool_cvm", "the CVM fused sequence pool is not provided")
 search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
-tdm_sampler = _absent("tdm_sampler", "TDM layer-wise sampling is not provided")
 _pull_box_extended_sparse = _absent("_pull_box_extended_sparse", "BoxPS pulls are not provided")
 
 

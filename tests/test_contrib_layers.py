@@ -344,3 +344,81 @@ def test_sequence_topk_avg_pooling_lod(topks, ch, rows, cols):
     out.sum().backward()
     np.testing.assert_allclose(xt.grad.numpy().reshape(-1), g, rtol=1e-5)
     assert C.sequence_topk_avg_pooling(xt, rt, ct, topks, ch).shape == [sum(rows), ch * len(topks)]
+
+
+@pytest.mark.parametrize("use_cvm", [True, False])
+def test_fused_seqpool_cvm(use_cvm):
+    """forward = sum pool + CVM log transform; backward = the op's CVM-broadcast rule
+    (reference: operators/fused/fused_seqpool_cvm_op.cu)"""
+    rng = np.random.default_rng(3)
+    lens_a, lens_b = [2, 0, 3], [1, 1, 1]
+    a, b = rng.random((5, 6), dtype=np.float32), rng.random((3, 6), dtype=np.float32)
+    ta, tb = _lod_tensor(a, lens_a), _lod_tensor(b, lens_b)
+    ta.stop_gradient = False
+    cvm = rng.random((3, 2), dtype=np.float32)
+    outs = C.fused_seqpool_cvm([ta, tb], "sum", paddle.to_tensor(cvm), pad_value=0.5, use_cvm=use_cvm)
+    for o, x, lens in zip(outs, (a, b), (lens_a, lens_b)):
+        offs = np.cumsum([0] + lens)
+        p = np.stack([x[s:e].sum(0) + 0.5 for s, e in zip(offs[:-1], offs[1:])])
+        if use_cvm:
+            ref = p.copy()
+            ref[:, 0] = np.log(p[:, 0] + 1)
+            ref[:, 1] = np.log(p[:, 1] + 1) - np.log(p[:, 0] + 1)
+        else:
+            ref = p[:, 2:]
+        np.testing.assert_allclose(o.numpy(), ref, rtol=1e-5)
+    g = np.arange(outs[0].numel(), dtype=np.float32).reshape(outs[0].shape)
+    outs[0].backward(paddle.to_tensor(g))
+    seg = np.repeat(np.arange(3), lens_a)
+    full = np.concatenate([cvm, g[:, 2:] if use_cvm else g], 1)
+    np.testing.assert_allclose(ta.grad.numpy(), full[seg], rtol=1e-6)
+    with pytest.raises(ValueError):
+        C.fused_seqpool_cvm([ta], "max", paddle.to_tensor(cvm))
+
+
+TRAVEL = [[1, 3, 7, 14], [1, 3, 7, 15], [1, 3, 8, 16], [1, 3, 8, 17], [1, 4, 9, 18], [1, 4, 9, 19], [1, 4, 10, 20],
+          [1, 4, 10, 21], [2, 5, 11, 22], [2, 5, 11, 23], [2, 5, 12, 24], [2, 5, 12, 25], [2, 6, 13, 0]]
+LAYERS = [[1, 2], [3, 4, 5, 6], [7, 8, 9, 10, 11, 12, 13], list(range(14, 26))]
+
+
+@pytest.mark.parametrize("negs,out_dtype", [([0, 0, 0, 0], "int32"), ([1, 1, 1, 1], "int64"), ([1, 2, 3, 4], "int32")])
+def test_tdm_sampler_reference_checks(negs, out_dtype):
+    """the reference test_tdm_sampler_op tree and its checks: positives follow the travel path,
+    samples of a layer are distinct members of it, labels 1/0, padding (node 0) masked out"""
+    import paddle_hackathon_amd as P
+    x = np.random.default_rng(4).integers(0, 13, (10, 1)).astype("int32")
+    lod = np.cumsum([0] + [len(l) for l in LAYERS]).tolist()
+    flat = np.array(sum(LAYERS, []), "int32").reshape(-1, 1)
+    out, lab, msk = C._tdm_sampler_op(P.to_tensor(x), P.to_tensor(np.array(TRAVEL, "int32")), P.to_tensor(flat),
+                                      negs, lod, True, 7, out_dtype)
+    assert out.numpy().dtype == np.dtype(out_dtype) and out.shape == [10, len(negs) + sum(negs)]
+    o, lb, m = out.numpy(), lab.numpy(), msk.numpy()
+    for i in range(10):
+        s, path = 0, []
+        for l, k in enumerate(negs):
+            e = s + k + 1
+            smp = o[i, s:e].tolist()
+            path.append(smp[0])
+            if smp[0] != 0:
+                assert len(set(smp)) == len(smp)
+                assert lb[i, s] == 1 and (lb[i, s + 1:e] == 0).all() and (m[i, s:e] == 1).all()
+            else:
+                assert (np.array(smp) == 0).all() and (m[i, s:e] == 0).all()
+            assert set(smp) <= set(LAYERS[l]) | {0}
+            s = e
+        assert path == TRAVEL[int(x[i, 0])]
+
+
+def test_tdm_sampler_layer_api():
+    from paddle_hackathon_amd import fluid as F
+    import paddle_hackathon_amd as P
+    travel = np.array([[1, 3], [1, 4], [2, 5], [2, 6]], "int32")
+    layer = np.arange(1, 7, dtype="int32").reshape(-1, 1)
+    smp, lab, msk = C.tdm_sampler(P.to_tensor(np.array([[0], [1], [2], [3]], "int32")), [0, 1], [2, 4], 4,
+                                  tree_travel_attr=F.ParamAttr(initializer=P.nn.initializer.Assign(travel)),
+                                  tree_layer_attr=F.ParamAttr(initializer=P.nn.initializer.Assign(layer)),
+                                  output_list=True, seed=1)
+    assert [t.shape for t in smp] == [[4, 1, 1], [4, 2, 1]]
+    np.testing.assert_array_equal(smp[0].numpy().reshape(-1), [1, 1, 2, 2])
+    np.testing.assert_array_equal(smp[1].numpy()[:, 0, 0], [3, 4, 5, 6])
+    assert (lab[1].numpy()[:, 1, 0] == 0).all()
