@@ -7,8 +7,8 @@ Composite tensor programs on the framework's ops (dygraph and static: every func
 registered op; batch_fc is one batched GEMM, correlation one channel reduction per displacement,
 fused_bn_add_act the fused BN + add + ReLU kernel path of ``batch_norm_act``). The LoD text
 matching ops (var_conv_2d, match_matrix_tensor, sequence_topk_avg_pooling) work on LoDTensors in
-dygraph, as do fused_seqpool_cvm and tdm_sampler. search_pyramid_hash and
-_pull_box_extended_sparse raise NotImplementedError naming themselves."""
+dygraph, as do fused_seqpool_cvm, tdm_sampler and search_pyramid_hash (without bloom filters).
+_pull_box_extended_sparse (a BoxPS pull) raises NotImplementedError naming itself."""
 from __future__ import annotations
 
 import torch
@@ -672,6 +672,86 @@ def tdm_sampler(x, neg_samples_num_list, layer_node_num_list, leaf_node_num, tre
     return res
 
 
+# ------------------------------------------------------------------------------- pyramid hash
+class _HashGather(torch.autograd.Function):
+    """gather of hashed weight slices; backward is the op's own update: W -= lr * dOut scattered
+    back (reference: pyramid_hash_op.cc hash_embedding_bp — the weight is trained inside the grad
+    kernel, not by an optimizer, so no W gradient is returned)"""
+
+    @staticmethod
+    def forward(ctx, w, idx, lr):
+        ctx.save_for_backward(idx)
+        ctx.w, ctx.lr = w, lr
+        return w.reshape(-1)[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, = ctx.saved_tensors
+        if ctx.lr:
+            with torch.no_grad():
+                ctx.w.view(-1).index_add_(0, idx.reshape(-1), g.reshape(-1).to(ctx.w.dtype), alpha=-ctx.lr)
+        return None, None, None
+
+
+def _pyramid_hash_op(x, w, num_emb, space_len, pyramid_layer, rand_len, drop_out_percent, is_training, seed=0,
+                     lr=0.0):
+    """pyramid_hash_op (reference: operators/pyramid_hash_op.cc): for each LoD sequence of ids,
+    every n-gram with 2 <= n <= pyramid_layer (kept with prob 1 - drop_out_percent when training) is
+    one output row whose num_emb values are rand_len-long slices of W at XXH32(ngram as float32
+    bytes, seed=j) % space_len for j = 0, rand_len, ...; a sequence with no kept n-gram gives one
+    zero row. Inference scales the rows by drop_out_percent like the reference. The hashing and the
+    index table are host work (as in the reference's CPU-only kernel); the gather runs on W's device."""
+    import numpy as np
+    import xxhash
+    lens = _seq_lengths(x, "search_pyramid_hash input")
+    xt = _t(x)
+    ids = xt.reshape(-1)[:xt.shape[0]].detach().cpu().numpy().astype(np.float32)
+    rng = np.random.default_rng(int(seed))
+    rows, top_lens, off = [], [], 0
+    chunks = np.arange(0, num_emb, rand_len)
+    for n in lens:
+        seq, kept = ids[off:off + n], 0
+        off += n
+        for layer in range(1, min(pyramid_layer, n)):
+            for l in range(n - layer):
+                if is_training and rng.random() < drop_out_percent:
+                    continue
+                b = seq[l:l + layer + 1].tobytes()
+                starts = [xxhash.xxh32_intdigest(b, int(j)) % space_len for j in chunks]
+                rows.append(np.concatenate([np.arange(s, s + rand_len)[:num_emb - j] for s, j in zip(starts, chunks)]))
+                kept += 1
+        if kept == 0:
+            rows.append(None)
+        top_lens.append(max(kept, 1))
+    wt = _t(w)
+    zero = [i for i, r in enumerate(rows) if r is None]
+    idx = torch.as_tensor(np.stack([r if r is not None else np.zeros(num_emb, np.int64) for r in rows]),
+                          dtype=torch.long, device=wt.device) if rows else torch.zeros(0, num_emb, dtype=torch.long)
+    out = _HashGather.apply(wt, idx, float(lr) if is_training else 0.0)
+    if zero:
+        keep = torch.ones(out.shape[0], 1, dtype=out.dtype, device=out.device)
+        keep[zero] = 0
+        out = out * keep
+    if not is_training:
+        out = out * drop_out_percent
+    return _lod_wrap(out, top_lens)
+
+
+def search_pyramid_hash(input, num_emb, space_len, pyramid_layer, rand_len, drop_out_percent, is_training, use_filter,
+                        white_list_len, black_list_len, seed, lr, param_attr=None, param_attr_wl=None,
+                        param_attr_bl=None, name=None, distribute_update_vars=None, dtype="float32"):
+    """pyramid hash n-gram embedding (reference: contrib/layers/nn.py search_pyramid_hash); the
+    weight is [space_len + rand_len, 1]. The bloom-filter white/black lists (use_filter with a
+    nonzero list length) are not supported."""
+    from ...layer_helper import LayerHelper
+    if use_filter and (white_list_len or black_list_len):
+        raise NotImplementedError("search_pyramid_hash: bloom-filter white/black lists are not supported")
+    helper = LayerHelper("search_pyramid_hash")
+    w = helper.create_parameter(attr=param_attr, shape=[space_len + rand_len, 1], dtype=dtype)
+    return _pyramid_hash_op(input, w, num_emb, space_len, pyramid_layer, rand_len, drop_out_percent, is_training,
+                            seed, lr)
+
+
 # ------------------------------------------------------------------------------- not provided
 def _absent(name, why):
     def f(*args, **kwargs):
@@ -680,7 +760,6 @@ def _absent(name, why):
     return f
 
 
-search_pyramid_hash = _absent("search_pyramid_hash", "pyramid hash embedding is not provided")
 _pull_box_extended_sparse = _absent("_pull_box_extended_sparse", "BoxPS pulls are not provided")
 
 

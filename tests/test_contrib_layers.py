@@ -115,7 +115,7 @@ def test_multiclass_nms2_index_and_absent_ops():
     o, i = out.numpy(), idx.numpy().reshape(-1)
     assert len(o) == len(i) and set(i.tolist()) <= {0, 1, 2}
     with pytest.raises(NotImplementedError):
-        C.search_pyramid_hash(None, 1, 1)
+        C._pull_box_extended_sparse(None, 1, 1)
 
 
 def test_rank_attention_matches_reference_formula():
@@ -422,3 +422,45 @@ def test_tdm_sampler_layer_api():
     np.testing.assert_array_equal(smp[0].numpy().reshape(-1), [1, 1, 2, 2])
     np.testing.assert_array_equal(smp[1].numpy()[:, 0, 0], [3, 4, 5, 6])
     assert (lab[1].numpy()[:, 1, 0] == 0).all()
+
+
+def test_search_pyramid_hash():
+    """reference test_pyramid_hash_op config (num_voc 128, num_emb 64, pyramid_layer 4, rand_len 16,
+    x lod [3, 5, 2, 6]); rows checked against an independent XXH32 slice table"""
+    import xxhash
+    rng = np.random.default_rng(5)
+    lens, num_emb, rand_len, space = [3, 5, 2, 1], 64, 16, 128 * 64
+    ids = rng.integers(0, 128, (sum(lens), 1)).astype("int32")
+    x = _lod_tensor(ids, lens)
+    w = rng.random((space + rand_len, 1), dtype=np.float32)
+    W = paddle.to_tensor(w)
+    out = C._pyramid_hash_op(x, W, num_emb, space, 4, rand_len, 0.5, False, seed=3)
+    ref, rl, off = [], [], 0
+    for n in lens:
+        seq = ids[off:off + n, 0].astype(np.float32)
+        off += n
+        k = 0
+        for layer in range(1, min(4, n)):
+            for l in range(n - layer):
+                b = seq[l:l + layer + 1].tobytes()
+                ref.append(np.concatenate([w[xxhash.xxh32_intdigest(b, j) % space:][:rand_len, 0]
+                                           for j in range(0, num_emb, rand_len)]) * 0.5)
+                k += 1
+        if k == 0:
+            ref.append(np.zeros(num_emb, np.float32))
+        rl.append(max(k, 1))
+    np.testing.assert_allclose(out.numpy(), np.stack(ref), rtol=1e-6)
+    assert out._lod == [list(np.cumsum([0] + rl))]
+    # training: dropped n-grams, and the grad kernel's in-place W update
+    W2 = paddle.to_tensor(w.copy())
+    tr = C._pyramid_hash_op(x, W2, num_emb, space, 4, rand_len, 0.5, True, seed=3, lr=0.1)
+    assert tr.shape[0] <= out.shape[0] and tr.shape[1] == num_emb
+    W2.stop_gradient = False
+    tr = C._pyramid_hash_op(x, W2, num_emb, space, 4, rand_len, 0.0, True, seed=3, lr=0.1)
+    tr.sum().backward()
+    delta = w[:, 0] - W2.numpy()[:, 0]
+    n_hashed = tr.shape[0] - sum(1 for n in lens if n < 2)         # the zero row of a 1-id sequence gets no update
+    np.testing.assert_allclose(delta.sum(), 0.1 * n_hashed * num_emb, rtol=1e-3)
+    assert (delta >= -1e-7).all() and delta.max() > 0
+    y = C.search_pyramid_hash(x, num_emb, space, 4, rand_len, 0.5, False, False, 0, 0, 3, 0.002)
+    assert y.shape == [sum(rl), num_emb]
