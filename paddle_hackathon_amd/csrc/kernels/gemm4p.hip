@@ -49,7 +49,21 @@ enum : int {
   EPI_TEMPORAL = 16384,  // stores with the default cache policy (else non-temporal)
   EPI_RSTAGE = 32768,    // NT: register-staged operands (global_load -> VGPR -> ds_write) instead of LDS-DMA
   EPI_EARLY = 65536,     // early-release schedule (see the EARLY main loop)
+  EPI_LATE_SHIFT = 17,   // NT + EARLY, bits 17-20: schedule variant LV (lv_lwg / lv_ldma / PIN)
 };
+
+// late-wait variants (LV): {LWG = phase-B group of the buffer wait (0: at the A/B boundary),
+// LDMA = DMAs of the next-next K-tile issued in phase A (groups RELG-15), the rest in phase B}
+// LV & 8 (PIN): an empty "memory" asm closes every MFMA group, so no IR pass sinks a group's LDS
+// fragment reads out of it (hipcc sank phase B's last reads past the loop latch: an uncovered
+// read burst + lgkmcnt stall at every K-tile boundary, profiles/README.md round 5).
+constexpr int lv_lwg(int lv) { return (lv & 7) == 1 ? 8 : (lv & 7) == 4 ? 12 : 0; }
+constexpr int lv_ldma(int lv) { return 8; }
+// LV & 7 in {2, 3, 5}: phase B reads in consumption order (LORD); phase A's 16 reads over the first
+// lv_rg groups (8: two per group up to the release at group 8; 6 / 4: two / four groups of MFMAs
+// between the last read and the release barrier's lgkmcnt(0))
+constexpr bool lv_lord(int lv) { return (lv & 7) == 2 || (lv & 7) == 3 || (lv & 7) == 5; }
+constexpr int lv_rg(int lv, int relg) { return (lv & 7) == 3 ? 6 : (lv & 7) == 5 ? 4 : relg; }
 
 struct Args {
   const void* a;
@@ -152,7 +166,7 @@ struct Sched {
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
 template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
-          bool GELU = false, bool RS = false, bool EARLY = false>
+          bool GELU = false, bool RS = false, bool EARLY = false, int LV = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -418,6 +432,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // EARLY: MFMA group at which phase A's fragment-read burst ends and the buffer is released
   constexpr int RELG = AKO ? PHA_G4P_RELG_TN : PHA_G4P_RELG_NT;
   static_assert(16 % RELG == 0 && RELG < 16, "the read burst covers the 16 fragment reads in whole groups");
+  constexpr int LWG = lv_lwg(LV), LDMA = lv_ldma(LV), LDMB = 16 - LDMA;
+  constexpr bool PIN = (LV & 8) != 0;
+  constexpr bool LORD = lv_lord(LV);
+  constexpr int LRG = lv_rg(LV, RELG);
+  static_assert(LWG == 0 || (LDMB <= LWG && RELG == 8), "late variants: every phase-B DMA before the wait");
 
   // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
   // into (na, nb). MODE 0: accumulate; 1: fresh tile (C = 0); 2: fresh tile with the previous
@@ -481,6 +500,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PIN) asm volatile("" ::: "memory");
     }
   };
   using yes = std::true_type;
@@ -497,17 +517,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // DMAs go out in A's groups 4-15 and B's groups 0-3 — one K-tile ahead of where the plain
   // schedule can issue them; the A/B boundary waits with a counted vmcnt for the previous set only.
   // Each DMA gets >= 112 MFMAs of latency cover instead of >= 64.
-  auto phaseE = [&](auto mode_c, auto rel_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8], uint4 (&nb)[8],
-                    int rbuf, int rkh, int stbuf) {
+  auto phaseE = [&](auto mode_c, auto rel_c, auto vbw_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8],
+                    uint4 (&nb)[8], int rbuf, int rkh, int stbuf) {
     constexpr int MODE = decltype(mode_c)::value;
     constexpr bool REL = decltype(rel_c)::value;   // phase A: read burst, release barrier, DMAs 0-11
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if constexpr (REL) {
-        if (s < RELG) {
+        if (s < LRG) {   // the 16 reads over groups 0..LRG-1 (LRG < RELG: LDS-latency cover before the release)
 #pragma unroll
-          for (int q = 0; q < 16 / RELG; ++q) {
-            const int r = (16 / RELG) * s + q;
+          for (int r = s * 16 / LRG; r < (s + 1) * 16 / LRG; ++r) {
             if (r & 1) nb[r >> 1] = readB(rbuf, rkh, r >> 1);
             else na[r >> 1] = readA(rbuf, rkh, r >> 1);
           }
@@ -518,11 +537,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           bar();
           stage_begin(stbuf);
         }
-        if (s >= RELG) stage_one(s - RELG);
+        if constexpr (LWG > 0) {
+          // LDMA DMAs over groups RELG-15 (one or two per group), the other LDMB in phase B
+          if (s >= RELG) {
+#pragma unroll
+            for (int d = (s - RELG) * LDMA / (16 - RELG); d < (s - RELG + 1) * LDMA / (16 - RELG); ++d) stage_one(d);
+          }
+        } else if (s >= RELG) {
+          stage_one(s - RELG);
+        }
+      } else if constexpr (LWG > 0) {
+        // LATE (LV != 0): the next K-tile's LDS buffer is waited for at group LWG of phase B instead
+        // of at the A/B boundary, and its 16 fragment reads (A0, B0-7, A1-7: the order the next
+        // phase A's groups consume them) follow in groups LWG-15. hipBLASLt's gfx950 NT kernel waits
+        // about two thirds into its iteration the same way (profiles/README.md round 5): each DMA
+        // gets 4 * LWG more MFMAs of latency cover.
+        if (s < LDMB) stage_one(LDMA + s);
+        if (s == LWG) {
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(decltype(vbw_c)::value) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          bar();
+        }
+        if (s >= LWG) {
+#pragma unroll
+          for (int r = (s - LWG) * 16 / (16 - LWG); r < (s - LWG + 1) * 16 / (16 - LWG); ++r) {
+            if (r == 0) na[0] = readA(rbuf, rkh, 0);
+            else if (r <= 8) nb[r - 1] = readB(rbuf, rkh, r - 1);
+            else na[r - 8] = readA(rbuf, rkh, r - 8);
+          }
+        }
       } else {
-        if constexpr (SCHED & 2) {
+        if constexpr ((SCHED & 2) && !LORD) {
           if (s & 1) nb[s >> 1] = readB(rbuf, rkh, s >> 1);
           else na[s >> 1] = readA(rbuf, rkh, s >> 1);
+        } else if constexpr (LORD) {
+          // one read per group in the order the next phase A consumes them (A0, B0-7, A1-7): its
+          // group 1 needs B4-7, read by group 8 here (the alternating order reads B7 last)
+          if (s == 0) na[0] = readA(rbuf, rkh, 0);
+          else if (s <= 8) nb[s - 1] = readB(rbuf, rkh, s - 1);
+          else na[s - 8] = readA(rbuf, rkh, s - 8);
         } else if (s < 8) {
 #pragma unroll
           for (int r = 2 * s; r < 2 * s + 2; ++r) {
@@ -558,6 +611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PIN) asm volatile("" ::: "memory");
     }
   };
 
@@ -600,25 +654,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // an epilogue phase's stores (capped at the counter's 63)
     constexpr int NSTE = (SPLIT || GELU) ? 64 : 32;
     constexpr int VB2 = 16 - RELG + NSTE > 63 ? 63 : 16 - RELG + NSTE;
+    // LATE: the wait sits in phase B after all 16 DMAs of the next-next K-tile (+ the stores)
+    constexpr int VL2 = 16 + NSTE > 63 ? 63 : 16 + NSTE;
+    using VW1 = std::integral_constant<int, LWG ? 16 : 0>;
+    using VW2 = std::integral_constant<int, LWG ? VL2 : 0>;
     for (int r = 0; sc.valid(r); ++r) {
       {
         const int buf = s & 1;
-        phaseE(M2{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(VB2) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        bar();
+        phaseE(M2{}, yes{}, VW2{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        if constexpr (LWG == 0) {
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(VB2) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          bar();
+        }
         set_epi(r);
-        phaseE(M0{}, no{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        phaseE(M0{}, no{}, VW2{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
         stage_end();
         ++s;
       }
       for (int k = 1; k < nk; ++k, ++s) {
         const int buf = s & 1;
-        phaseE(M0{}, yes{}, fa0, fb0, fa1, fb1, buf, 1, buf);
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(16 - RELG) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        bar();
-        phaseE(M0{}, no{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        phaseE(M0{}, yes{}, VW1{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        if constexpr (LWG == 0) {
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(16 - RELG) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          bar();
+        }
+        phaseE(M0{}, no{}, VW1{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
         stage_end();
       }
     }
@@ -729,8 +791,14 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
     hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, true, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (a.epi & EPI_GELU)
     return (int)hipErrorInvalidValue;
-  else if (!ako && !bko && !trans)
-    hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+  else if (!ako && !bko && !trans) {
+    const int lv = E && std::is_same<T, bf16_t>::value ? (a.epi >> EPI_LATE_SHIFT) & 15 : 0;
+    if (lv == 8) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 8>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 10) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 10>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 11) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 11>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 13) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 13>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+  }
   else if (ako && bko && !trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else if (ako && !bko && trans)

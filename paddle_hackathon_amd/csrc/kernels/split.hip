@@ -1,6 +1,7 @@
 // fp32 operands of the three-term split products (ops/conv_gemm.py split3, ops/gemm.py mm_f32):
 //
 //   x = hi + lo,  hi = bf16(x),  lo = bf16(x - hi)      (both round-to-nearest-even)
+//   (finite x past the largest bf16: hi = x truncated to bf16; non-finite x: lo = 0)
 //   out[o][p][i] = (bit p of lo_mask ? lo : hi)(x[o][i])      o < outer, p < 3, i < inner
 //
 // i.e. the concatenation of three parts along one dimension of a contiguous tensor (outer = the
@@ -23,10 +24,19 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
     uint32_t hw[4], lw[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint16_t h0 = f32_to_bf16(f[2 * k]), h1 = f32_to_bf16(f[2 * k + 1]);
-      const uint16_t l0 = f32_to_bf16(f[2 * k] - bf16_to_f32(h0)), l1 = f32_to_bf16(f[2 * k + 1] - bf16_to_f32(h1));
-      hw[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      lw[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+      uint16_t h[2], l[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float v = f[2 * k + e];
+        h[e] = f32_to_bf16(v);
+        // |v| above the largest bf16 rounds hi to inf: take the truncated hi instead (finite, and
+        // lo stays exact); a non-finite v keeps lo = 0 so hi + lo is v itself (inf - inf = NaN
+        // otherwise)
+        if (!__builtin_isfinite(bf16_to_f32(h[e])) && __builtin_isfinite(v)) h[e] = (uint16_t)(__float_as_uint(v) >> 16);
+        l[e] = __builtin_isfinite(v) ? f32_to_bf16(v - bf16_to_f32(h[e])) : (uint16_t)0;
+      }
+      hw[k] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      lw[k] = (uint32_t)l[0] | ((uint32_t)l[1] << 16);
     }
     const uint4 H = {hw[0], hw[1], hw[2], hw[3]}, L = {lw[0], lw[1], lw[2], lw[3]};
     uint4* dst = out + (size_t)o * 3 * inner8 + i8;

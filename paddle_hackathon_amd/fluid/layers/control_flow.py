@@ -668,17 +668,55 @@ def while_loop(cond, body, loop_vars, is_test=False, name=None):
     return SN.while_loop(cond, body, loop_vars, is_test, name)
 
 
-def _print(x, first_n, message, summarize):
-    t = T(x)
-    flat = t.reshape(-1)
-    vals = flat[:summarize].tolist() if summarize >= 0 else flat.tolist()
-    print(f"{message or ''} Tensor(shape={list(t.shape)}, dtype={t.dtype}) data: {vals}")
-    return x
+class _Printer:
+    """the reference print op (print_op.cc): at most ``first_n`` prints (-1: every run) of the
+    tensor's name, dtype, shape, LoD and its first ``summarize`` values (-1: all), prefixed by
+    ``message``; returns its input unchanged. Forward phase only (print_phase "backward" prints
+    nothing: gradients have no print op here)."""
+
+    def __init__(self, name, first_n, message, summarize, show_name, show_type, show_shape, show_lod, phase):
+        self.name, self.first_n, self.message, self.summarize = name, first_n, message, summarize
+        self.flags = (show_name, show_type, show_shape, show_lod)
+        self.phase, self.count = phase, 0
+
+    def __call__(self, x):
+        if self.phase == "backward" or (0 <= self.first_n <= self.count):
+            return x
+        self.count += 1
+        t = T(x)
+        flat = t.detach().reshape(-1)
+        vals = flat[:self.summarize] if self.summarize >= 0 else flat
+        lines = [self.message] if self.message else []
+        if self.flags[0] and self.name:
+            lines.append(f"Variable: {self.name}")
+        if self.flags[3]:
+            lines.append(f"  - lod: {fcore.lod_of(x) or '{}'}")
+        if self.flags[2]:
+            lines.append(f"  - shape: {list(t.shape)}")
+        if self.flags[1]:
+            lines.append(f"  - dtype: {str(t.dtype).replace('torch.', '')}")
+        lines.append(f"  - data: {vals.cpu().tolist()}")
+        print("\n".join(lines), flush=True)
+        return x
 
 
 def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True, print_tensor_type=True,
           print_tensor_shape=True, print_tensor_lod=True, print_phase="both"):
-    return _record_or_run(_print, "print", (input, first_n, message, summarize))
+    """control_flow.py:Print — records one ``print`` op (nothing is printed while the Program is
+    built; static/program.py registers its InferMeta as the identity)"""
+    pr = _Printer(getattr(input, "name", None), first_n, message, summarize, print_tensor_name, print_tensor_type,
+                  print_tensor_shape, print_tensor_lod, print_phase)
+
+    def print_(x):
+        return pr(x)
+    out = _record_or_run(print_, "print", (input,))
+    from ...static.program import set_ref_op
+    set_ref_op(out, "print", {"In": [input]}, {"Out": [out]}, {
+        "first_n": int(first_n), "message": message or "", "summarize": int(summarize),
+        "print_tensor_name": bool(print_tensor_name), "print_tensor_type": bool(print_tensor_type),
+        "print_tensor_shape": bool(print_tensor_shape), "print_tensor_lod": bool(print_tensor_lod),
+        "print_phase": str(print_phase).upper(), "is_forward": True})
+    return out
 
 
 def _assert(c, data, summarize):

@@ -12,7 +12,7 @@ import torch.nn.functional as TF
 
 from ...vision import ops as V
 from ...static import nn as SN
-from ._common import T, W, dev
+from ._common import T, W, dev, register
 from .. import core as fcore
 
 __all__ = ["prior_box", "density_prior_box", "multi_box_head", "bipartite_match", "target_assign",
@@ -800,3 +800,9 @@ def collect_fpn_proposals(multi_rois, multi_scores, min_level, max_level, post_n
     if rois_num_per_level is not None:
         return res, W(torch.tensor(lens, dtype=torch.int32, device=dev()))
     return res
+
+
+# every detection op records ONE op in a static Program (multi_box_head creates conv parameters:
+# a builder); their data-dependent output rows (NMS keeps, proposals) come from static/program.py's
+# example-run InferMeta as -1 dims
+register(globals(), __all__, skip={"multi_box_head"})

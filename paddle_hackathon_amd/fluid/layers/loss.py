@@ -16,7 +16,7 @@ __all__ = ["center_loss", "bpr_loss", "cross_entropy", "square_error_cost", "edi
            "margin_rank_loss", "sigmoid_cross_entropy_with_logits", "teacher_student_sigmoid_loss", "huber_loss",
            "kldiv_loss", "npair_loss", "mse_loss"]
 
-_BUILDERS = {"center_loss", "nce", "hsigmoid", "edit_distance", "sampled_softmax_with_cross_entropy"}
+_BUILDERS = {"center_loss", "nce", "hsigmoid", "sampled_softmax_with_cross_entropy"}
 
 
 def center_loss(input, label, num_classes, alpha, param_attr, update_center=True):

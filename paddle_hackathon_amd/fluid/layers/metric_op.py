@@ -1,15 +1,34 @@
-"""``fluid.layers.accuracy`` / ``auc`` (reference: python/paddle/fluid/layers/metric_op.py,
-paddle/fluid/operators/metrics/auc_op.h)."""
+"""``fluid.layers.accuracy`` / ``auc`` (reference: python/paddle/fluid/layers/metric_op.py:33,131,
+paddle/phi/kernels/cpu/auc_kernel.cc).
+
+``auc`` keeps its statistics where the reference keeps them: in persistable int64 buffers created
+with the layer (``batch_stat_pos / batch_stat_neg`` with the ``slide_steps`` ring and its step
+counter, ``stat_pos / stat_neg`` for the global curve). In a static Program they are the Program's
+persistable variables, updated in place by the two recorded ``auc`` ops at every run (two metrics in
+one program, or two programs, never share state); in dygraph every call creates fresh buffers, as
+the reference's ``create_global_variable`` does there."""
 from __future__ import annotations
 
 import torch
 
+from ...framework import core as _core
+from ...framework.dispatch import static_op
 from ._common import T, W, dev
 
 __all__ = ["accuracy", "auc"]
 
 
 def accuracy(input, label, k=1, correct=None, total=None):
+    """top-k accuracy [1] (fp32). In a static Program: the reference's two ops, top_k then
+    accuracy on its indices (metric_op.py:33)"""
+    from ...static.program import Variable, set_ref_op
+    if _core._mode.static and isinstance(input, Variable):
+        from ...tensor.search import topk
+        vals, idx = topk(input, k)
+        acc, c, t = _acc_rec(idx, label)
+        set_ref_op(acc, "accuracy", {"Out": [vals], "Indices": [idx], "Label": [label]},
+                   {"Accuracy": [acc], "Correct": [c], "Total": [t]}, {})
+        return acc
     x = T(input)
     y = T(label).reshape(-1, 1).long()
     topk = torch.topk(x, k, -1).indices
@@ -23,40 +42,90 @@ def accuracy(input, label, k=1, correct=None, total=None):
     return acc
 
 
-_STATE = {}
-
-
-def _auc_of(pos, neg, curve):
-    """trapezoid area under ROC (or PR) from per-threshold-bin positive / negative counts"""
-    tp = torch.flip(torch.cumsum(torch.flip(pos, [0]), 0), [0]).double()
-    fp = torch.flip(torch.cumsum(torch.flip(neg, [0]), 0), [0]).double()
+def _auc_area(pos, neg):
+    """calcAuc: trapezoids over the thresholds from the highest bin down, / (P * N)"""
+    tp = torch.flip(torch.cumsum(torch.flip(pos.double(), [0]), 0), [0])
+    fp = torch.flip(torch.cumsum(torch.flip(neg.double(), [0]), 0), [0])
+    tp_prev = torch.cat([tp[1:], tp.new_zeros(1)])
+    fp_prev = torch.cat([fp[1:], fp.new_zeros(1)])
+    area = ((fp - fp_prev).abs() * (tp + tp_prev) / 2).sum()
     P, N = tp[0], fp[0]
-    if P == 0 or N == 0:
-        return 0.0
-    if curve == "ROC":
-        tpr = torch.cat([tp / P, torch.zeros(1, dtype=tp.dtype)])
-        fpr = torch.cat([fp / N, torch.zeros(1, dtype=fp.dtype)])
-        return float(((fpr[:-1] - fpr[1:]) * (tpr[:-1] + tpr[1:]) / 2).sum())
-    prec = tp / (tp + fp).clamp_min(1)
-    rec = tp / P
-    rec2 = torch.cat([rec, torch.zeros(1, dtype=rec.dtype)])
-    return float(((rec2[:-1] - rec2[1:]) * prec).sum())
+    return torch.where((P > 0) & (N > 0), area / (P * N).clamp_min(1), area).reshape(1)
+
+
+def auc_op(predict, label, stat_pos, stat_neg, num_thresholds=2 ** 12 - 1, slide_steps=1, curve="ROC"):
+    """the reference ``auc`` op: bins the positive-class probability (the last column) into
+    ``num_thresholds + 1`` buckets, accumulates positives / negatives into the int64 stat buffers
+    IN PLACE (``slide_steps`` > 0: a ring of per-step buckets plus their running sum, the step
+    index in the last element) and returns the AUC of the accumulated counts (float64 [1]);
+    ``curve`` is accepted and, as in auc_kernel.cc, the area is the ROC one"""
+    p = T(predict)
+    p = p.reshape(p.shape[0], -1)[:, -1]
+    if bool(((p < 0) | (p > 1)).any()):
+        raise ValueError("auc: the predict data must be in [0, 1]")
+    y = T(label).reshape(-1)
+    nb = num_thresholds + 1
+    bins = (p.double() * num_thresholds).long().clamp(0, num_thresholds)
+    cpos = torch.bincount(bins[y > 0], minlength=nb)
+    cneg = torch.bincount(bins[y == 0], minlength=nb)
+    sp, sn = T(stat_pos).reshape(-1), T(stat_neg).reshape(-1)
+    with torch.no_grad():
+        if slide_steps == 0:
+            sp[:nb] += cpos.to(sp.device)
+            sn[:nb] += cneg.to(sn.device)
+            off = 0
+        else:
+            cur = int(sp[(slide_steps + 1) * nb]) % slide_steps
+            c0, s0 = cur * nb, slide_steps * nb
+            sp[s0:s0 + nb] -= sp[c0:c0 + nb]
+            sn[s0:s0 + nb] -= sn[c0:c0 + nb]
+            sp[c0:c0 + nb] = cpos.to(sp.device)
+            sn[c0:c0 + nb] = cneg.to(sn.device)
+            sp[s0:s0 + nb] += sp[c0:c0 + nb]
+            sn[s0:s0 + nb] += sn[c0:c0 + nb]
+            off = s0
+        a = _auc_area(sp[off:off + nb], sn[off:off + nb])
+        if slide_steps:
+            sp[(slide_steps + 1) * nb] += 1
+            sn[(slide_steps + 1) * nb] += 1
+    return W(a.to(dev()))
+
+
+_auc_rec = static_op(auc_op, "auc")
+
+
+def _acc_run(indices, label):
+    from ...static.ref_ops import accuracy_op
+    return accuracy_op(indices, label)
+
+
+_acc_rec = static_op(_acc_run, "accuracy")
+_auc_counter = [0]
+
+
+def _stat_buffer(shape, tag):
+    t = W(torch.zeros(shape, dtype=torch.int64, device=dev()))
+    t.persistable = True
+    _auc_counter[0] += 1
+    t.name = f"_generated_var_auc_{tag}_{_auc_counter[0]}"
+    return t
 
 
 def auc(input, label, curve="ROC", num_thresholds=2 ** 12 - 1, topk=1, slide_steps=1):
-    """(global AUC, batch AUC, [batch_stat_pos, batch_stat_neg, stat_pos, stat_neg]); the global
-    statistics accumulate over calls (the reference keeps them in persistable variables)"""
-    p = T(input).float()
-    p = p[:, -1] if p.dim() == 2 else p.reshape(-1)
-    y = T(label).reshape(-1).long()
-    bins = (p * num_thresholds).long().clamp(0, num_thresholds)
-    pos = torch.bincount(bins[y == 1], minlength=num_thresholds + 1).cpu()
-    neg = torch.bincount(bins[y != 1], minlength=num_thresholds + 1).cpu()
-    st = _STATE.setdefault((curve, num_thresholds), {"pos": torch.zeros_like(pos), "neg": torch.zeros_like(neg)})
-    st["pos"] += pos
-    st["neg"] += neg
-    g = _auc_of(st["pos"], st["neg"], curve)
-    b = _auc_of(pos, neg, curve)
-    f = lambda v: W(torch.tensor([v], dtype=torch.float64, device=dev()))  # noqa: E731
-    t = lambda v: W(v.reshape(1, -1).to(dev()))  # noqa: E731
-    return f(g), f(b), [t(pos), t(neg), t(st["pos"]), t(st["neg"])]
+    """(global AUC, batch AUC over the last ``slide_steps`` steps, [batch_stat_pos, batch_stat_neg,
+    stat_pos, stat_neg]) — metric_op.py:131"""
+    nb = num_thresholds + 1
+    batch_pos = _stat_buffer([(1 + slide_steps) * nb + 1], "batch_stat_pos")
+    batch_neg = _stat_buffer([(1 + slide_steps) * nb + 1], "batch_stat_neg")
+    stat_pos = _stat_buffer([1, nb], "stat_pos")
+    stat_neg = _stat_buffer([1, nb], "stat_neg")
+    from ...static.program import set_ref_op
+    outs = []
+    for sp, sn, ss in ((batch_pos, batch_neg, slide_steps), (stat_pos, stat_neg, 0)):
+        a = _auc_rec(input, label, sp, sn, num_thresholds=num_thresholds, slide_steps=ss, curve=curve)
+        set_ref_op(a, "auc", {"Predict": [input], "Label": [label], "StatPos": [sp], "StatNeg": [sn]},
+                   {"AUC": [a], "StatPosOut": [sp], "StatNegOut": [sn]},
+                   {"curve": curve, "num_thresholds": int(num_thresholds), "slide_steps": int(ss)})
+        outs.append(a)
+    batch_auc, global_auc = outs
+    return global_auc, batch_auc, [batch_pos, batch_neg, stat_pos, stat_neg]

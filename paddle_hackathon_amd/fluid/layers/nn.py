@@ -57,8 +57,10 @@ _BUILDERS = {"fc", "embedding", "linear_chain_crf", "crf_decoding", "conv2d", "c
              "instance_norm", "data_norm", "conv2d_transpose", "conv3d_transpose", "row_conv", "layer_norm",
              "group_norm", "spectral_norm", "prelu", "bilinear_tensor_product", "py_func", "deformable_conv",
              "autoincreased_step_counter", "affine_channel", "chunk_eval", "mean_iou", "similarity_focus", "hash",
-             "unique", "unique_with_counts", "where", "logical_and", "logical_or", "logical_xor", "logical_not", "filter_by_instag", "sampling_id", "random_crop",
-             "ctc_greedy_decoder", "lod_reset", "lod_append", "im2sequence"}
+             "logical_and", "logical_or", "logical_xor", "logical_not", "lod_reset", "lod_append"}
+# (unique / unique_with_counts / where / filter_by_instag / sampling_id / random_crop /
+# ctc_greedy_decoder / im2sequence record one op each: their data-dependent or host-read output
+# shapes come from static/program.py's example-run InferMeta)
 
 
 # ----------------------------------------------------------------------------- parameter builders

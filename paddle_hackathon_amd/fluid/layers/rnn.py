@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 
 from ...framework.core import Tensor
+from ...framework.dispatch import static_op
 from ...nn.layer.layers import Layer
 from ._common import fparam as _create_parameter
 from ...nn import decode as _decode
@@ -304,8 +305,14 @@ def dynamic_lstm(input, size, h_0=None, c_0=None, param_attr=None, bias_attr=Non
     H = size // 4
     w = _create_parameter([H, 4 * H], dtype, param_attr)
     b = _create_parameter([1, 7 * H if use_peepholes else 4 * H], dtype, bias_attr, is_bias=True)
-    return _lstm_run(input, H, w, b, None, use_peepholes, is_reverse, gate_activation, cell_activation,
-                     candidate_activation, h_0, c_0, None)
+    out = _lstm_rec(input, H, w, b, None, use_peepholes, is_reverse, gate_activation, cell_activation,
+                    candidate_activation, h_0, c_0, None)
+    from ...static.program import set_ref_op
+    set_ref_op(out, "lstm", {"Input": [input], "Weight": [w], "Bias": [b], "H0": [h_0], "C0": [c_0]},
+               {"Hidden": [out[0]], "Cell": [out[1]]},
+               {"use_peepholes": bool(use_peepholes), "is_reverse": bool(is_reverse), "gate_activation": gate_activation,
+                "cell_activation": cell_activation, "candidate_activation": candidate_activation})
+    return out
 
 
 def _lstm_run(input, H, w, b, proj, peep, reverse, ga, ca, cand, h0, c0, proj_act):
@@ -351,7 +358,7 @@ def dynamic_lstmp(input, size, proj_size, param_attr=None, bias_attr=None, use_p
     w = _create_parameter([proj_size, 4 * H], dtype, param_attr)
     pw = _create_parameter([H, proj_size], dtype, param_attr)
     b = _create_parameter([1, 7 * H if use_peepholes else 4 * H], dtype, bias_attr, is_bias=True)
-    return _lstm_run(input, H, w, b, pw, use_peepholes, is_reverse, gate_activation, cell_activation,
+    return _lstm_rec(input, H, w, b, pw, use_peepholes, is_reverse, gate_activation, cell_activation,
                      candidate_activation, h_0, c_0, proj_activation)
 
 
@@ -372,6 +379,15 @@ def dynamic_gru(input, size, param_attr=None, bias_attr=None, is_reverse=False, 
     H = size
     w = _create_parameter([H, 3 * H], "float32", param_attr)
     b = _create_parameter([1, 3 * H], "float32", bias_attr, is_bias=True)
+    out = _gru_rec(input, w, b, H, is_reverse, gate_activation, candidate_activation, h_0, origin_mode)
+    from ...static.program import set_ref_op
+    set_ref_op(out, "gru", {"Input": [input], "Weight": [w], "Bias": [b], "H0": [h_0]}, {"Hidden": [out]},
+               {"activation": candidate_activation, "gate_activation": gate_activation, "is_reverse": bool(is_reverse),
+                "origin_mode": bool(origin_mode)})
+    return out
+
+
+def _gru_run(input, w, b, H, is_reverse, gate_activation, candidate_activation, h_0, origin_mode):
     x, off = _seq_list(input)
     wt, bt = T(w), T(b).reshape(-1)
     hs = [None] * x.shape[0]
@@ -386,12 +402,22 @@ def dynamic_gru(input, size, param_attr=None, bias_attr=None, is_reverse=False, 
     return out
 
 
+# the recurrences record ONE op each in a static Program (the parameters are created by the
+# builders above; the op type is the reference's lstm / gru)
+_lstm_rec = static_op(_lstm_run, "lstm")
+_gru_rec = static_op(_gru_run, "gru")
+
+
 def gru_unit(input, hidden, size, param_attr=None, bias_attr=None, activation="tanh", gate_activation="sigmoid",
              origin_mode=False):
     """one GRU step on [N, 3H] projected input; -> (new hidden, reset_hidden_prev, gate)"""
     H = size // 3
     w = _create_parameter([H, 3 * H], "float32", param_attr)
     b = _create_parameter([1, 3 * H], "float32", bias_attr, is_bias=True)
+    return _gru_unit_rec(input, hidden, w, b, H, activation, gate_activation, origin_mode)
+
+
+def _gru_unit_run(input, hidden, w, b, H, activation, gate_activation, origin_mode):
     x, h = T(input), T(hidden)
     wt, bt = T(w), T(b).reshape(-1)
     xu, xr, xc = (x + bt).split(H, -1)
@@ -408,11 +434,19 @@ def lstm_unit(x_t, hidden_t_prev, cell_t_prev, forget_bias=0.0, param_attr=None,
     from .nn import fc
     D = T(hidden_t_prev).shape[-1]
     from ...tensor import concat
-    g = T(fc(concat([x_t, hidden_t_prev], 1), 4 * D, param_attr=param_attr, bias_attr=bias_attr))
-    i, f, o, gg = g.split(D, -1)
+    g = fc(concat([x_t, hidden_t_prev], 1), 4 * D, param_attr=param_attr, bias_attr=bias_attr)
+    return _lstm_unit_rec(g, cell_t_prev, D, forget_bias)
+
+
+def _lstm_unit_run(g, cell_t_prev, D, forget_bias):
+    i, f, o, gg = T(g).split(D, -1)
     c = torch.sigmoid(f + forget_bias) * T(cell_t_prev) + torch.sigmoid(i) * torch.tanh(gg)
     h = torch.sigmoid(o) * torch.tanh(c)
     return W(h), W(c)
+
+
+_gru_unit_rec = static_op(_gru_unit_run, "gru_unit")
+_lstm_unit_rec = static_op(_lstm_unit_run, "lstm_unit")
 
 
 def lstm(input, init_h, init_c, max_len, hidden_size, num_layers, dropout_prob=0.0, is_bidirec=False,

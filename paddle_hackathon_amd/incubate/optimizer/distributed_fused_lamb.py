@@ -88,6 +88,8 @@ class DistributedFusedLamb(Lamb):
                           acc=torch.zeros(total, dtype=torch.float32, device=dev)
                           if self._gradient_accumulation_steps > 1 else None,
                           b1p=1.0, b2p=1.0)
+        # a state_dict set before the first step (the usual resume order) was only parked
+        self._load_pending()
 
     # ---------------------------------------------------------------------------------- step
     def step(self):

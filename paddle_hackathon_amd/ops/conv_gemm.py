@@ -553,7 +553,11 @@ def split3(t, dim, order="hhl"):
         if rc == 0:
             return out
     hi = t.to(torch.bfloat16)
-    lo = (t - hi.float()).to(torch.bfloat16)
+    fin = torch.isfinite(t)
+    over = fin & ~torch.isfinite(hi)
+    if bool(over.any()):   # finite past the bf16 range: truncate instead of rounding to inf
+        hi = torch.where(over, (t.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16), hi)
+    lo = torch.where(fin, t - hi.float(), torch.zeros_like(t)).to(torch.bfloat16)
     return torch.cat([hi if c == "h" else lo for c in order], dim)
 
 

@@ -64,6 +64,7 @@ def bin_cnt(bits):
 
 
 def _axis_view(shape, axis):
+    axis = int(axis) % len(shape)   # negative quant_axis counts from the last dimension
     outer = 1
     for s in shape[:axis]:
         outer *= int(s)

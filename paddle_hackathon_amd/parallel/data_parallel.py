@@ -127,7 +127,15 @@ class _Reducer:
             if b.buf is None or b.buf.numel() != n or b.buf.device != grads[0].device or b.buf.dtype != cdt:
                 b.buf = torch.empty(n, dtype=cdt, device=grads[0].device)
             if cdt == b.dtype:
-                torch.cat([g.reshape(-1) for g in grads], out=b.buf)
+                # some grads may already be their slices of the buffer (only part of the bucket was
+                # cleared): copy the others into their slots; torch.cat(out=buf) would reject the
+                # inputs that alias its output
+                base, es, off = b.buf.data_ptr(), b.buf.element_size(), 0
+                for g in grads:
+                    k = g.numel()
+                    if g.data_ptr() != base + off * es:
+                        b.buf[off:off + k].copy_(g.reshape(-1))
+                    off += k
             else:
                 b.buf.copy_(torch.cat([g.reshape(-1) for g in grads]))
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
@@ -172,6 +180,39 @@ class _Reducer:
             views = [v.to(grads[0].dtype) for v in views]   # comm dtype (fp16_allreduce) back to fp32
             torch._foreach_copy_(grads, views)
 
+    def prepare_grads(self):
+        """Before a forward that will be followed by backward: gradients that an optimizer's
+        ``clear_grad(set_to_zero=False)`` dropped are re-pointed at their zeroed bucket slices, so
+        backward accumulates straight into the flat buffers RCCL reduces (no concatenation, no
+        re-adoption) — the bench's and the fleet trainers' clear mode. Gradients that still hold
+        values (accumulation over steps) are left alone."""
+        for b in self.buckets:
+            if b.buf is None or b.buf.dtype != b.dtype:
+                continue
+            dropped = [p for p in b.params if p._t.grad is None]
+            if not dropped:
+                continue
+            base, es, off, views = b.buf.data_ptr(), b.buf.element_size(), 0, []
+            for p in b.params:
+                n = p._t.numel()
+                g = p._t.grad
+                if g is None:
+                    views.append((p, off, n))
+                elif g.data_ptr() != base + off * es:
+                    views = None   # a foreign gradient tensor: keep the copying path for this bucket
+                    break
+                off += n
+            if views is None:
+                continue
+            with torch.no_grad():
+                if len(dropped) == len(b.params):
+                    b.buf.zero_()
+                for p, o, n in views:
+                    v = b.buf[o:o + n]
+                    if len(dropped) != len(b.params):
+                        v.zero_()
+                    p._t.grad = v.view_as(p._t)
+
     def remove(self):
         for h in self.handles:
             h.remove()
@@ -195,6 +236,8 @@ class DataParallel(Layer):
     def forward(self, *inputs, **kwargs):
         if self._reducer is not None:
             self._reducer.enabled = self._grad_need_sync
+            if torch.is_grad_enabled():
+                self._reducer.prepare_grads()
         return self._layers(*inputs, **kwargs)
 
     def no_sync(self):

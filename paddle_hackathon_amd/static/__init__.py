@@ -106,12 +106,10 @@ def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, n
 
 def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True, print_tensor_type=True,
           print_tensor_shape=True, print_tensor_lod=True, print_phase="both"):
-    from ..framework.dispatch import static_op
-
-    def _print(x):
-        print(f"{message or ''} {x}")
-        return x
-    return static_op(_print, "Print")(input)
+    """static.Print = fluid.layers.Print (one recorded print op)"""
+    from ..fluid.layers.control_flow import Print as _P
+    return _P(input, first_n, message, summarize, print_tensor_name, print_tensor_type, print_tensor_shape,
+              print_tensor_lod, print_phase)
 
 
 def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
@@ -130,11 +128,9 @@ def accuracy(input, label, k=1, correct=None, total=None):
 
 
 def auc(input, label, curve="ROC", num_thresholds=2 ** 12 - 1, topk=1, slide_steps=1, ins_tag_weight=None):
-    from ..metric import Auc
-    m = Auc(curve, num_thresholds)
-    m.update(input.numpy(), label.numpy())
-    v = _core.to_tensor(np.array(m.accumulate(), dtype="float32"))
-    return v, v, []
+    """static.auc = fluid.layers.auc (persistable stat buffers, two recorded auc ops)"""
+    from ..fluid.layers.metric_op import auc as _auc
+    return _auc(input, label, curve, num_thresholds, topk, slide_steps)
 
 
 def ctr_metric_bundle(input, label, ins_tag_weight=None):

@@ -2,8 +2,7 @@
 control_flow.py, sequence_lod.py). Parameter-creating builders (fc, conv2d, batch_norm …)
 create their parameters eagerly in the global scope and emit functional ops (recorded when
 called on static Variables). Control flow records one op whose replay evaluates the
-predicate and runs the chosen branch. LoD sequence ops take padded [B, T, ...] tensors
-plus a length tensor (MI355X build has no LoD tensors)."""
+predicate and runs the chosen branch. The sequence ops are fluid.layers.sequence_lod's (LoD inputs)."""
 from __future__ import annotations
 
 import numpy as np
@@ -383,127 +382,20 @@ class StaticRNN:
         return self._outputs[0] if len(self._outputs) == 1 else self._outputs
 
 
-# ----------------------------------------------------------------------------- sequence ops (padded)
-def _len_mask(x, length):
-    t = x._t
-    T = t.shape[1]
-    lens = length._t.reshape(-1) if length is not None else torch.full((t.shape[0],), T, device=t.device)
-    mask = torch.arange(T, device=t.device)[None, :] < lens[:, None]
-    return t, lens, mask
+# ----------------------------------------------------------------------------- sequence ops (LoD)
+# paddle.static.nn's sequence ops ARE fluid.layers.sequence_lod's (reference
+# python/paddle/static/nn/__init__.py:46-60): LoD inputs, one recorded op each.
+def _seq(name):
+    def f(*args, **kwargs):
+        from ..fluid.layers import sequence_lod
+        return getattr(sequence_lod, name)(*args, **kwargs)
+    f.__name__ = name
+    f.__qualname__ = name
+    f.__doc__ = f"fluid.layers.sequence_lod.{name} (LoD sequence op)"
+    return f
 
 
-def sequence_pool(input, pool_type, is_test=False, pad_value=0.0, length=None):
-    t, lens, m = _len_mask(input, length)
-    mf = m.unsqueeze(-1).to(t.dtype)
-    pt = pool_type.lower()
-    if pt == "sum":
-        r = (t * mf).sum(1)
-    elif pt == "average":
-        r = (t * mf).sum(1) / lens.clamp_min(1)[:, None].to(t.dtype)
-    elif pt == "sqrt":
-        r = (t * mf).sum(1) / lens.clamp_min(1)[:, None].to(t.dtype).sqrt()
-    elif pt == "max":
-        r = t.masked_fill(~m.unsqueeze(-1), float("-inf")).amax(1)
-    elif pt == "first":
-        r = t[:, 0]
-    else:
-        r = t[torch.arange(t.shape[0]), (lens - 1).clamp_min(0)]
-    return _wrap(r)
-
-
-def sequence_first_step(input, length=None):
-    return sequence_pool(input, "first", length=length)
-
-
-def sequence_last_step(input, length=None):
-    return sequence_pool(input, "last", length=length)
-
-
-def sequence_softmax(input, use_cudnn=False, name=None, length=None):
-    t, lens, m = _len_mask(input, length)
-    s = t.masked_fill(~m.reshape(m.shape + (1,) * (t.dim() - 2)), float("-inf"))
-    return _wrap(torch.nan_to_num(torch.softmax(s, 1)))
-
-
-def sequence_reverse(x, name=None, length=None):
-    t, lens, m = _len_mask(x, length)
-    T = t.shape[1]
-    idx = (lens[:, None] - 1 - torch.arange(T, device=t.device)[None, :]).clamp_min(0)
-    idx = torch.where(m, idx, torch.arange(T, device=t.device)[None, :].expand_as(idx))
-    return _wrap(torch.gather(t, 1, idx.reshape(idx.shape + (1,) * (t.dim() - 2)).expand_as(t)))
-
-
-def sequence_pad(x, pad_value, maxlen=None, name=None, length=None):
-    t, lens, m = _len_mask(x, length)
-    pv = pad_value._t if isinstance(pad_value, Tensor) else pad_value
-    out = torch.where(m.reshape(m.shape + (1,) * (t.dim() - 2)), t, torch.as_tensor(pv, dtype=t.dtype, device=t.device))
-    if maxlen is not None and maxlen > out.shape[1]:
-        out = torch.nn.functional.pad(out, [0, 0] * (t.dim() - 2) + [0, maxlen - out.shape[1]])
-    return _wrap(out), _wrap(lens)
-
-
-def sequence_unpad(x, length, name=None):
-    t = x._t
-    lens = length._t.reshape(-1).tolist()
-    return _wrap(torch.cat([t[i, :l] for i, l in enumerate(lens)]))
-
-
-def sequence_concat(input, name=None):
-    return _wrap(torch.cat([i._t for i in input], 1))
-
-
-def sequence_conv(input, num_filters, filter_size=3, filter_stride=1, padding=True, padding_start=None,
-                  bias_attr=None, param_attr=None, act=None, name=None):
-    d = input.shape[-1]
-    w = _create_parameter([filter_size * d, num_filters], "float32", param_attr)
-    b = None if bias_attr is False else _create_parameter([num_filters], "float32", bias_attr, is_bias=True)
-
-    def _sc(x, w, b):
-        t = x._t
-        start = -(filter_size // 2) if padding_start is None else padding_start
-        padded = torch.nn.functional.pad(t, [0, 0, -start, filter_size - 1 + start])
-        cols = padded.unfold(1, filter_size, 1).transpose(-1, -2).reshape(t.shape[0], t.shape[1], -1)
-        y = cols @ w._t
-        return _wrap(y + b._t if b is not None else y)
-    return _act(static_op(_sc, "sequence_conv")(input, w, b), act)
-
-
-def sequence_enumerate(input, win_size, pad_value=0, name=None):
-    t = input._t
-    padded = torch.nn.functional.pad(t, [0, win_size - 1], value=pad_value)
-    return _wrap(padded.unfold(-1, win_size, 1))
-
-
-def sequence_expand(x, y, ref_level=-1, name=None):
-    return _wrap(x._t.repeat_interleave(y._t.shape[1] if y._t.dim() > 1 else 1, 0))
-
-
-def sequence_expand_as(x, y, name=None):
-    return _wrap(x._t.unsqueeze(1).expand(-1, y._t.shape[1], *x._t.shape[1:]))
-
-
-def sequence_reshape(input, new_dim):
-    t = input._t
-    return _wrap(t.reshape(t.shape[0], -1, new_dim))
-
-
-def sequence_scatter(input, index, updates, name=None):
-    out = input._t.clone()
-    out.scatter_add_(1, index._t.long(), updates._t)
-    return _wrap(out)
-
-
-def sequence_slice(input, offset, length, name=None):
-    t = input._t
-    off, ln = offset._t.reshape(-1).tolist(), length._t.reshape(-1).tolist()
-    mx = int(max(ln)) if ln else 0
-    out = t.new_zeros((t.shape[0], mx) + tuple(t.shape[2:]))
-    for i, (o, l) in enumerate(zip(off, ln)):
-        out[i, :int(l)] = t[i, int(o):int(o) + int(l)]
-    return _wrap(out)
-
-
-register_ops(globals(), ["sequence_pool", "sequence_first_step", "sequence_last_step", "sequence_softmax",
-                         "sequence_reverse", "sequence_pad", "sequence_unpad", "sequence_concat", "sequence_enumerate",
-                         "sequence_expand", "sequence_expand_as", "sequence_reshape", "sequence_scatter",
-                         "sequence_slice"])
+for _n in ("sequence_pool", "sequence_first_step", "sequence_last_step", "sequence_softmax", "sequence_reverse",
+           "sequence_pad", "sequence_unpad", "sequence_concat", "sequence_enumerate", "sequence_expand",
+           "sequence_expand_as", "sequence_reshape", "sequence_scatter", "sequence_slice", "sequence_conv"):
+    globals()[_n] = _seq(_n)

@@ -31,7 +31,7 @@ import torch
 from ..framework import core as _core
 from ..framework.core import Tensor, Parameter, _wrap, convert_dtype, dtype_to_str
 
-__all__ = ["Variable", "Program", "Block", "OpDesc", "record_op", "default_main_program", "default_startup_program",
+__all__ = ["Variable", "Program", "Block", "OpDesc", "record_op", "set_ref_op", "default_main_program", "default_startup_program",
            "program_guard", "data", "Executor", "global_scope", "scope_guard", "append_backward", "gradients",
            "minimize_static", "enable_static", "disable_static", "name_scope", "OP_REGISTRY", "CompiledProgram",
            "BuildStrategy", "ExecutionStrategy", "InputSpec", "Scope"]
@@ -402,6 +402,164 @@ def _bind(fn, args, kwargs):
     return (), dict(b.arguments)
 
 
+# ----------------------------------------------------------------------------- InferMeta
+# Shapes / dtypes of a recorded op come from running it on meta tensors (phi's InferMeta role).
+# Two kinds of ops cannot run on meta tensors: ops whose output SIZE depends on input values
+# (the second example run; reference: NonZeroInferMeta / UniqueRawInferMeta / MaskedSelectInferMeta / MultiClassNMSInferMeta
+# give those dims -1, phi/infermeta/unary.cc:3377,3569, binary.cc:1489, multiary.cc) and ops that
+# read a host value on the way (one_hot's range check, accuracy's counts, LoD offsets). For both the
+# op runs once on small CPU EXAMPLE inputs of the recorded shapes (their output structure, dtypes
+# and static dims), and for the data-dependent ones a second run on other example values marks the
+# dims that moved as -1. The recorded op itself runs the real function at Executor.run time.
+_INFER_META = {}          # op name -> fn(*meta args, **meta kwargs) -> meta outputs
+_DATA_DEPENDENT = {"nonzero", "unique", "unique_consecutive", "masked_select", "where_index", "where",
+                   "multiclass_nms", "multiclass_nms2", "multiclass_nms3", "matrix_nms", "locality_aware_nms",
+                   "edit_distance", "ctc_align", "ctc_greedy_decoder", "generate_proposals", "distribute_fpn_proposals",
+                   "collect_fpn_proposals", "box_decoder_and_assign", "detection_output", "retinanet_detection_output",
+                   "sequence_erase", "sequence_enumerate", "filter_by_instag", "shuffle_batch", "tdm_sampler",
+                   "masked_scatter", "bincount", "histogram_dd", "segment_sum", "segment_mean", "segment_max",
+                   "segment_min", "unique_with_counts", "sample_neighbors", "graph_reindex", "graph_khop_sampler"}
+
+
+def register_infer_meta(*names):
+    """``@register_infer_meta("op")``: an explicit InferMeta for a recorded op (called with the
+    op's arguments, Variables as meta tensors; returns the outputs as meta tensors)"""
+    def deco(f):
+        for n in names:
+            _INFER_META[n] = f
+        return f
+    return deco
+
+
+@register_infer_meta("print", "Print")
+def _print_meta(x, *a, **k):   # the print op returns its input: nothing to run (or print) at build time
+    return x
+
+
+def _meta_unsupported(e):
+    if isinstance(e, NotImplementedError):
+        return True
+    msg = str(e)
+    return isinstance(e, (RuntimeError, ValueError, TypeError, IndexError)) and any(
+        k in msg for k in ("meta", "Meta", "has no value", "no data", "data-dependent", "DataDependent"))
+
+
+def _example(tree, dense, memo):
+    """CPU example values for an InferMeta run. ``dense`` True: floats (1..n)/(n+1) (distinct,
+    inside (0, 1)), integers zeros (valid indices / labels), bools True; False: all zeros / False;
+    "mixed": floats cycling -1, 0, 1, integers 0, 1, bools alternating (the probe run of a
+    data-dependent op, so comparisons and masks inside it see both outcomes)"""
+    if isinstance(tree, Variable):
+        k = id(tree)
+        if k not in memo:
+            m = tree._t
+            n = max(int(m.numel()), 1)
+            mixed = isinstance(dense, str)
+            if m.dtype.is_floating_point or m.dtype.is_complex:
+                if mixed:
+                    t = (torch.arange(n) % 3 - 1).to(m.dtype)
+                else:
+                    t = (torch.arange(1, n + 1, dtype=torch.float64) / (n + 1)).to(m.dtype) if dense else \
+                        torch.zeros(n, dtype=m.dtype)
+                t = t[:m.numel()].reshape(m.shape)
+            elif m.dtype == torch.bool:
+                t = (torch.arange(n) % 2 == 0)[:m.numel()].reshape(m.shape) if mixed else torch.full(m.shape, bool(dense))
+            else:
+                t = (torch.arange(n) % 2).to(m.dtype)[:m.numel()].reshape(m.shape) if mixed else \
+                    torch.zeros(m.shape, dtype=m.dtype)
+            v = _wrap(t)
+            lvl = getattr(tree, "lod_level", 0)
+            if lvl and t.dim():      # a LoD feed: one sequence per level over all rows
+                v._lod = [[0, int(t.shape[0])] for _ in range(lvl)]
+            memo[k] = v
+        return memo[k]
+    if isinstance(tree, Tensor):
+        if tree._t.device.type == "meta":
+            return _wrap(torch.zeros(tree._t.shape, dtype=tree._t.dtype))
+        # a captured parameter / persistable state: a CPU copy, so an op that updates its state in
+        # place (auc's stat buffers, batch_norm's running moments) leaves the real one untouched
+        if id(tree) not in memo:
+            c = _wrap(tree._t.detach().to("cpu", copy=True))
+            if getattr(tree, "_lod", None):
+                c._lod = tree._lod
+            memo[id(tree)] = c
+        return memo[id(tree)]
+    if isinstance(tree, list):
+        return [_example(t, dense, memo) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_example(t, dense, memo) for t in tree)
+    if isinstance(tree, dict):
+        return {k: _example(v, dense, memo) for k, v in tree.items()}
+    return tree
+
+
+def _meta_of(tree):
+    if isinstance(tree, Tensor):
+        return _wrap(tree._t.detach().to("meta"))
+    if isinstance(tree, torch.Tensor):
+        return _wrap(tree.detach().to("meta"))
+    if isinstance(tree, list):
+        return [_meta_of(t) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_meta_of(t) for t in tree)
+    return tree
+
+
+def _run_example(fn, bargs, bkw, dense):
+    """the op on example inputs, with the default device switched to the CPU for the call (the
+    ops' own allocations land beside the examples)"""
+    memo = {}
+    prev = _core._default_device
+    _core._default_device = torch.device("cpu")
+    try:
+        with torch.no_grad():
+            return fn(*_example(bargs, dense, memo), **_example(bkw, dense, memo))
+    finally:
+        _core._default_device = prev
+
+
+def _infer_meta(fn, name, bargs, bkw):
+    """-> (meta outputs, dynamic dims per output tensor or None)"""
+    _core._mode.record_depth += 1
+    try:
+        f = _INFER_META.get(name)
+        if f is not None:
+            return f(*_to_meta(bargs), **_to_meta(bkw)), None
+        try:
+            return fn(*_to_meta(bargs), **_to_meta(bkw)), None
+        except Exception as e:   # noqa: BLE001 - classified below
+            if not _meta_unsupported(e):
+                raise
+        out = _run_example(fn, bargs, bkw, True)
+        dyn = None
+        if name in _DATA_DEPENDENT:
+            a = list(_iter_tensors(out if isinstance(out, (list, tuple)) else [out]))
+            moved = [set() for _ in a]
+            for mode in (False, "mixed"):
+                try:
+                    other = _run_example(fn, bargs, bkw, mode)
+                except Exception:   # noqa: BLE001 - the other examples are only probes
+                    continue
+                b = list(_iter_tensors(other if isinstance(other, (list, tuple)) else [other]))
+                if len(a) != len(b):
+                    continue
+                for mv, ta, tb in zip(moved, a, b):
+                    if ta._t.dim() == tb._t.dim():
+                        mv.update(i for i, (x, y) in enumerate(zip(ta._t.shape, tb._t.shape)) if x != y)
+            dyn = [tuple(sorted(mv)) for mv in moved]
+        return _meta_of(out), dyn
+    finally:
+        _core._mode.record_depth -= 1
+
+
+def _mark_dynamic(outs, dyn):
+    if not dyn:
+        return
+    for v, dims in zip(_iter_vars(outs), dyn):
+        if dims:
+            v.declared_shape = [-1 if i in dims else int(s) for i, s in enumerate(v._t.shape)]
+
+
 def record_op(fn, name, args, kwargs):
     """Called by every wrapped op in static mode (see framework/dispatch.py)."""
     if not _has_var((args, kwargs)):
@@ -409,13 +567,10 @@ def record_op(fn, name, args, kwargs):
     qual = f"{fn.__module__}.{name}"
     OP_REGISTRY.setdefault(qual, fn)
     bargs, bkw = _bind(fn, args, kwargs)
-    _core._mode.record_depth += 1
-    try:
-        meta_out = fn(*_to_meta(bargs), **_to_meta(bkw))
-    finally:
-        _core._mode.record_depth -= 1
+    meta_out, dyn = _infer_meta(fn, name, bargs, bkw)
     blk = default_main_program().current_block()
     outs = _outputs_to_vars(meta_out, blk)
+    _mark_dynamic(outs, dyn)
     op = OpDesc(qual, fn, bargs, bkw, outs)
     if _OP_DEVICE[0] is not None:     # static.device_guard: pipeline stage / placement of the op
         op.attrs["op_device"] = _OP_DEVICE[0]
@@ -426,6 +581,17 @@ def record_op(fn, name, args, kwargs):
 
 
 _OP_DEVICE = [None]
+
+
+def set_ref_op(outs, typ, ins, routs, attrs):
+    """attach the reference op form (type, {slot: [tensors]} in / out, attributes) to the recorded op
+    that produced ``outs``: serialize_program / save_inference_model write it under that type and
+    the reader's converter (static/ref_ops.py) maps it back. No-op outside a static Program."""
+    v = next(_iter_vars(outs if isinstance(outs, (list, tuple)) else [outs]), None)
+    if v is None or getattr(v, "op", None) is None:
+        return
+    v.op.attrs["ref_op"] = (typ, {k: list(t) for k, t in ins.items() if t and t[0] is not None},
+                            {k: list(t) for k, t in routs.items() if t and t[0] is not None}, dict(attrs))
 
 
 # ----------------------------------------------------------------------------- backward / optimize ops

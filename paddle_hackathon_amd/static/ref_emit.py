@@ -390,8 +390,53 @@ def _resnet_unit(kw):
         "is_test": bool(kw["is_test"]), "act_type": kw.get("act") or "identity"}, {}
 
 
+def _nonzero(kw):
+    """paddle.nonzero -> where_index (Condition -> Out [-1, rank] int64)"""
+    if kw.get("as_tuple") or not _is_t(kw.get("x")):
+        return None
+    return "where_index", {"x": "Condition"}, "Out", {}, {}
+
+
+def _fluid_where(kw):
+    return "where_index", {"condition": "Condition"}, "Out", {}, {}
+
+
+def _masked_select(kw):
+    return "masked_select", {"x": "X", "mask": "Mask"}, "Y", {}, {}
+
+
+def _unique(kw):
+    """unique_op.cc: Out, then Indices / Index (inverse) / Counts as requested (is_sorted = True,
+    the 2.x paddle.unique form)"""
+    outs = ["Out"] + [s for f, s in (("return_index", "Indices"), ("return_inverse", "Index"),
+                                       ("return_counts", "Counts")) if kw.get(f)]
+    axis = kw.get("axis")
+    return "unique", {"x": "X"}, tuple(outs) if len(outs) > 1 else "Out", {
+        "dtype": pb.vartype_of(_dtype(kw.get("dtype", "int64"))), "return_index": bool(kw.get("return_index")),
+        "return_inverse": bool(kw.get("return_inverse")), "return_counts": bool(kw.get("return_counts")),
+        "axis": [] if axis is None else [int(axis)], "is_sorted": True}, {}
+
+
+def _dtype(d):
+    from ..framework.core import convert_dtype
+    return convert_dtype(d) or torch.int64
+
+
+def _edit_distance(kw):
+    if kw.get("ignored_tokens"):
+        return None   # the reference layer erases them with a sequence_erase op first
+    return "edit_distance", {"input": "Hyps", "label": "Refs", "input_length": "HypsLength",
+                             "label_length": "RefsLength"}, ("Out", "SequenceNum"), {
+        "normalized": bool(kw.get("normalized", True))}, {}
+
+
 _Q = "nn.quant.ops."
 EMIT = {
+    "fluid.layers.loss.edit_distance": _edit_distance,
+    "tensor.manipulation.nonzero": _nonzero,
+    "tensor.manipulation.masked_select": _masked_select,
+    "tensor.manipulation.unique": _unique,
+    "fluid.layers.nn.where": _fluid_where,
     "incubate.operators.resnet_unit.resnet_unit": _resnet_unit,
     **_SEQ,
     **_ACT,

@@ -557,6 +557,84 @@ def _interp(method):
     return conv
 
 
+# ---------------------------------------------------------- data-dependent / stateful ops (round 5)
+def unique_sorted_op(x, dtype=3, return_index=False, return_inverse=False, return_counts=False, axis=()):
+    """unique_op.cc with is_sorted (paddle.unique): Out [+ Indices, Index, Counts as requested]"""
+    from ..tensor.manipulation import unique
+    r = unique(_wrap(_t(x)), return_index, return_inverse, return_counts, axis[0] if axis else None,
+               pb.dtype_of(dtype) if dtype is not None and dtype >= 0 else "int64")
+    return r
+
+
+def unique_v1_op(x, dtype=2):
+    """unique_op.cc without is_sorted (fluid.layers.unique): first-occurrence order, (Out, Index)"""
+    from ..fluid.layers.nn import unique
+    return unique(_wrap(_t(x)), pb.dtype_of(dtype) if dtype is not None and dtype >= 0 else "int32")
+
+
+def _conv_unique(r, ins, at):
+    if not at.get("is_sorted", False):
+        return unique_v1_op, {"x": _one(r, ins, "X"), "dtype": at.get("dtype", 2)}, ("Out", "Index")
+    outs = ["Out"] + [sl for f, sl in (("return_index", "Indices"), ("return_inverse", "Index"),
+                                        ("return_counts", "Counts")) if at.get(f)]
+    kw = {"x": _one(r, ins, "X"), "dtype": at.get("dtype", 3), "return_index": at.get("return_index", False),
+          "return_inverse": at.get("return_inverse", False), "return_counts": at.get("return_counts", False),
+          "axis": at.get("axis", [])}
+    return unique_sorted_op, kw, tuple(outs) if len(outs) > 1 else "Out"
+
+
+def accuracy_op(indices, label):
+    """accuracy_op.cc on the top-k indices: (Accuracy [1] fp32, Correct [1] int32, Total [1] int32)"""
+    idx = _t(indices)
+    y = _t(label).reshape(-1, 1).long().to(idx.device)
+    hit = (idx.long() == y).any(-1)
+    n_ok = hit.sum().reshape(1)
+    n = hit.numel()
+    return (_wrap(n_ok.float() / max(n, 1)), _wrap(n_ok.int()),
+            _wrap(torch.tensor([n], dtype=torch.int32, device=idx.device)))
+
+
+def auc_ref_op(predict, label, stat_pos, stat_neg, num_thresholds=2 ** 12 - 1, slide_steps=1, curve="ROC"):
+    from ..fluid.layers.metric_op import auc_op
+    return auc_op(predict, label, stat_pos, stat_neg, num_thresholds, slide_steps, curve)
+
+
+def _conv_print(r, ins, at):
+    from ..fluid.layers.control_flow import _Printer
+    x = _one(r, ins, "In")
+    pr = _Printer(x.name if x is not None else None, at.get("first_n", -1), at.get("message", ""),
+                  at.get("summarize", 20), at.get("print_tensor_name", True), at.get("print_tensor_type", True),
+                  at.get("print_tensor_shape", True), at.get("print_tensor_lod", True),
+                  str(at.get("print_phase", "BOTH")).lower())
+
+    def print_op(x):
+        return pr(x)
+    return print_op, {"x": x}, "Out"
+
+
+def lstm_ref_op(input, weight, bias, h0=None, c0=None, use_peepholes=True, is_reverse=False,
+                gate_activation="sigmoid", cell_activation="tanh", candidate_activation="tanh"):
+    """lstm_op.cc (LoD input [T, 4D] already projected; gates {c, i, f, o}; peephole weights in
+    the bias tail) -> (Hidden, Cell)"""
+    from ..fluid.layers.rnn import _lstm_run
+    return _lstm_run(input, int(_t(weight).shape[0]), weight, bias, None, use_peepholes, is_reverse,
+                     gate_activation, cell_activation, candidate_activation, h0, c0, None)
+
+
+def gru_ref_op(input, weight, bias=None, h0=None, activation="tanh", gate_activation="sigmoid", is_reverse=False,
+               origin_mode=False):
+    """gru_op.cc (LoD input [T, 3D] already projected) -> Hidden"""
+    from ..fluid.layers.rnn import _gru_run
+    H = int(_t(weight).shape[0])
+    b = bias if bias is not None else _wrap(torch.zeros(1, 3 * H, device=_t(weight).device))
+    return _gru_run(input, weight, b, H, is_reverse, gate_activation, activation, h0, origin_mode)
+
+
+def edit_distance_ref_op(hyps, refs, hyps_length=None, refs_length=None, normalized=False):
+    from ..fluid.layers.loss import edit_distance
+    return edit_distance(hyps, refs, normalized, None, hyps_length, refs_length)
+
+
 def _kw(fn, slots, attrs, out, **fixed):
     """generic converter: slots {kwarg: input slot}, attrs {kwarg: (attr name, default)}"""
     def conv(r, ins, at):
@@ -826,6 +904,22 @@ CONVERT = {
     "clip": _kw(clip_op, {"x": "X"}, {"min": ("min", -3.4e38), "max": ("max", 3.4e38)}, "Out"),
     "where": _kw(where_op, {"condition": "Condition", "x": "X", "y": "Y"}, {}, "Out"),
     "where_index": _kw(where_index_op, {"condition": "Condition"}, {}, "Out"),
+    "unique": _conv_unique,
+    "accuracy": _kw(accuracy_op, {"indices": "Indices", "label": "Label"}, {}, ("Accuracy", "Correct", "Total")),
+    "auc": _kw(auc_ref_op, {"predict": "Predict", "label": "Label", "stat_pos": "StatPos", "stat_neg": "StatNeg"},
+               {"num_thresholds": ("num_thresholds", 2 ** 12 - 1), "slide_steps": ("slide_steps", 1),
+                "curve": ("curve", "ROC")}, "AUC"),
+    "print": _conv_print,
+    "lstm": _kw(lstm_ref_op, {"input": "Input", "weight": "Weight", "bias": "Bias", "h0": "H0", "c0": "C0"},
+                {"use_peepholes": ("use_peepholes", True), "is_reverse": ("is_reverse", False),
+                 "gate_activation": ("gate_activation", "sigmoid"), "cell_activation": ("cell_activation", "tanh"),
+                 "candidate_activation": ("candidate_activation", "tanh")}, ("Hidden", "Cell")),
+    "gru": _kw(gru_ref_op, {"input": "Input", "weight": "Weight", "bias": "Bias", "h0": "H0"},
+               {"activation": ("activation", "tanh"), "gate_activation": ("gate_activation", "sigmoid"),
+                "is_reverse": ("is_reverse", False), "origin_mode": ("origin_mode", False)}, "Hidden"),
+    "edit_distance": _kw(edit_distance_ref_op, {"hyps": "Hyps", "refs": "Refs", "hyps_length": "HypsLength",
+                                                "refs_length": "RefsLength"},
+                         {"normalized": ("normalized", False)}, ("Out", "SequenceNum")),
     "one_hot_v2": _kw(one_hot_op, {"x": "X"}, {"depth": ("depth", 1)}, "Out"),
     "one_hot": _kw(one_hot_op, {"x": "X"}, {"depth": ("depth", 1)}, "Out", v1=True),
     "range": _kw(range_op, {"start": "Start", "end": "End", "step": "Step"}, {}, "Out"),

@@ -224,7 +224,13 @@ def emit_optimizer(w, op, block_msg):
                 if coeff is None:
                     coeff = getattr(opt, "_weight_decay", 0.01)
                 _set_attr(msg, "coeff", float(coeff if isinstance(coeff, (int, float)) else 0.01))
-                _set_attr(msg, "with_decay", True)
+                # per parameter, as AdamW._decay_for / _lr_ratio apply them (reference adamw op:
+                # with_decay from apply_decay_param_fun, lr_ratio from the lr_ratio callable)
+                fn = getattr(opt, "_apply_decay_param_fun", None)
+                _set_attr(msg, "with_decay", bool(fn is None or fn(p.name)))
+                ratio_fn = getattr(opt, "_lr_ratio_fn", None)
+                if ratio_fn is not None:
+                    _set_attr(msg, "lr_ratio", float(ratio_fn(p)))
         _set_attr(msg, "op_role", 2)
         if found_inf is not None:
             ins["SkipUpdate"] = [w.tensor_name(found_inf)]

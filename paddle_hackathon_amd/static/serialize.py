@@ -89,7 +89,7 @@ _REF = {
                                                                        "padding": "paddings"}),
 }
 _FLUID_SLOTS = {"x": "X", "y": "Y", "input": "X", "label": "Label", "index": "Index", "updates": "Updates",
-                "condition": "Condition", "ids": "Ids"}
+                "condition": "Condition", "ids": "Ids", "bboxes": "BBoxes", "scores": "Scores"}
 _FLUID_TYPE = {"topk": "top_k", "reshape": "reshape2", "transpose": "transpose2", "squeeze": "squeeze2",
                "unsqueeze": "unsqueeze2", "flatten": "flatten2", "expand": "expand"}
 

@@ -147,6 +147,65 @@ def test_data_parallel_grads_are_bucket_views():
         assert r["n_cat_step2"] == 0
 
 
+def _dp_clear_modes(rank, world):
+    """the bench's clear mode (clear_grad(set_to_zero=False) drops the grads) keeps the bucket
+    views: the next forward re-points the dropped grads at their zeroed slices, so no copy into
+    the bucket runs; a partially cleared bucket (one grad dropped by hand) still reduces right"""
+    import torch
+    import paddle_hackathon_amd as paddle
+    rng = np.random.RandomState(123)
+    X = rng.randn(8, 8).astype("float32")
+    Y = rng.randn(8, 4).astype("float32")
+    out = {}
+    for mode in ("zero", "none", "partial", "partial_direct"):
+        paddle.seed(5)
+        model = _mlp(paddle)
+        dp = paddle.DataParallel(model, comm_buffer_size=1, last_comm_buffer_size=1)   # one shared bucket
+        opt = paddle.optimizer.SGD(0.1, parameters=model.parameters())
+        copies = []
+        real_copy = torch.Tensor.copy_
+
+        def counting_copy(self, *a, **k):
+            copies.append(1)
+            return real_copy(self, *a, **k)
+        for step in range(4):
+            if step == 3 and mode == "none":
+                torch.Tensor.copy_ = counting_copy
+            try:
+                # partial_direct: the inner layer is called (the reducer's hooks still fire, but no
+                # re-pointing runs): the copying path must cope with grads that alias the bucket
+                net = model if (mode == "partial_direct" and step > 0) else dp
+                loss = ((net(paddle.to_tensor(X[rank * 4:(rank + 1) * 4])) - paddle.to_tensor(Y[rank * 4:(rank + 1) * 4])) ** 2).mean()
+                loss.backward()
+            finally:
+                torch.Tensor.copy_ = real_copy
+            opt.step()
+            if mode == "zero":
+                opt.clear_grad()
+            elif mode == "none":
+                opt.clear_grad(set_to_zero=False)
+            else:   # zero every grad, then drop the first parameter's only
+                opt.clear_grad()
+                list(model.parameters())[0]._t.grad = None
+        red = dp._reducer
+        out[mode] = ([p.numpy().copy() for p in model.parameters()], len(copies),
+                     all(red._grads_in_buf(b) for b in red.buckets) if mode == "none" else None)
+    return out
+
+
+def test_data_parallel_bucket_views_survive_clear_modes():
+    res = run_dist(_dp_clear_modes, 2)
+    for r in res:
+        for a, b in zip(r["zero"][0], r["none"][0]):
+            np.testing.assert_allclose(a, b, rtol=1e-6)
+        for a, b in zip(r["zero"][0], r["partial"][0]):
+            np.testing.assert_allclose(a, b, rtol=1e-6)
+        for a, b in zip(r["zero"][0], r["partial_direct"][0]):
+            np.testing.assert_allclose(a, b, rtol=1e-6)
+        assert r["none"][1] == 0          # no gradient copied into a bucket on the 4th step
+    np.testing.assert_allclose(res[0]["none"][0][0], res[1]["none"][0][0], rtol=1e-6)
+
+
 def _tp_layers(rank, world):
     import torch
     import paddle_hackathon_amd as paddle

@@ -93,3 +93,39 @@ def test_incubate_surface():
     assert callable(inc.auto_checkpoint.train_epoch_range)
     importlib.import_module("paddle_hackathon_amd.fluid.incubate.fleet")
     importlib.import_module("paddle_hackathon_amd.fluid.incubate.checkpoint.auto_checkpoint")
+
+
+def test_state_dict_resume_before_first_step():
+    """build -> set_state_dict -> step (the usual resume order) continues exactly like the
+    uninterrupted run: moments, master shard, beta powers and the step count are restored."""
+    from paddle_hackathon_amd.incubate import DistributedFusedLamb
+    x, y = _data()
+
+    def make(ps):
+        return DistributedFusedLamb(0.01, 0.05, parameters=ps, alignment=16)
+
+    def run(m, opt, steps):
+        for _ in range(steps):
+            loss = paddle.mean((m(paddle.to_tensor(xs)) - paddle.to_tensor(ys)) ** 2)
+            loss.backward()
+            opt.step()
+            opt.clear_grad()
+
+    xs, ys = x, y
+    m_ref = _model()
+    o_ref = make(m_ref.parameters())
+    run(m_ref, o_ref, 4)
+    m_a = _model()
+    o_a = make(m_a.parameters())
+    run(m_a, o_a, 2)
+    msd = {k: v.numpy().copy() for k, v in m_a.state_dict().items()}
+    osd = o_a.state_dict()
+    assert osd["dfl_step"] == 2
+    m_b = _model()
+    m_b.set_state_dict({k: paddle.to_tensor(v) for k, v in msd.items()})
+    o_b = make(m_b.parameters())
+    o_b.set_state_dict(osd)
+    run(m_b, o_b, 2)
+    assert o_b._step_count == 4
+    for a, b in zip(m_b.parameters(), m_ref.parameters()):
+        np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-6, atol=1e-7)

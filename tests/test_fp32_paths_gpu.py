@@ -156,3 +156,33 @@ def test_split3_kernel_matches_torch(shape, dim, order):
     lo = (t - hi.float()).to(torch.bfloat16)
     ref = torch.cat([hi if c == "h" else lo for c in order], dim)
     assert got.shape == ref.shape and torch.equal(got.view(torch.int16), ref.view(torch.int16))
+
+
+def test_fp32_split_extremes():
+    """the split of values past the bf16 range and of non-finite values: finite inputs
+    near FLT_MAX stay finite (hi truncated, lo exact) and an inf / NaN input gives a non-finite
+    product wherever the fp64 product is non-finite (what AMP overflow checks read)"""
+    from paddle_hackathon_amd.ops import conv_gemm, gemm
+    torch.manual_seed(3)
+    t = torch.tensor([1.0, 3.39e38, -3.39e38, float("inf"), float("-inf"), float("nan"), 1e-3, 123.456] * 2,
+                     device="cuda")
+    s = conv_gemm.split3(t, 0, "hl").float()
+    hi, lo = s[:16], s[16:]
+    fin = torch.isfinite(t)
+    assert torch.isfinite(hi[fin]).all() and torch.isfinite(lo).all()
+    rel = ((hi[fin].double() + lo[fin].double() - t[fin].double()).abs() / t[fin].double().abs()).max().item()
+    assert rel < 2e-5
+    assert torch.isinf(hi[3]) and torch.isinf(hi[4]) and torch.isnan(hi[5])
+    # a GEMM with large finite entries: finite, ~2^-16 relative to fp64
+    a = torch.randn(64, 128, device="cuda")
+    b = torch.randn(128, 64, device="cuda")
+    a[0, :4] = 3e37
+    y = gemm.mm_f32(a, b)
+    ref = a.double() @ b.double()
+    assert torch.isfinite(y).all() and _rel(y, ref) < 2e-5
+    # an inf row: non-finite exactly where fp64 is non-finite, finite rows unchanged
+    a2 = a.clone()
+    a2[5, 7] = float("inf")
+    y2 = gemm.mm_f32(a2, b)
+    ref2 = a2.double() @ b.double()
+    assert torch.equal(torch.isfinite(y2), torch.isfinite(ref2))

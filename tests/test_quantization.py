@@ -359,3 +359,14 @@ def test_static_v2_passes_quantize_linear(tmp_path):
         assert "dequantize_linear" in types and not [t for t in types if t.startswith("paddle_hackathon_amd.")]
     finally:
         paddle.disable_static()
+
+
+def test_negative_quant_axis_is_the_last_dimension():
+    """quant_axis = -1 means the last dimension (it collapsed to scale[0] before)"""
+    import torch
+    from paddle_hackathon_amd.ops import quant
+    x = torch.randn(3, 4, 5)
+    s_neg, s_pos = quant.channel_abs_max(x, -1), quant.channel_abs_max(x, 2)
+    assert s_neg.shape == (5,) and torch.equal(s_neg, s_pos)
+    np.testing.assert_allclose(s_neg.numpy(), x.abs().amax(dim=(0, 1)).numpy())
+    assert torch.equal(quant.quant_dequant(x, s_neg, quant_axis=-1), quant.quant_dequant(x, s_pos, quant_axis=2))
