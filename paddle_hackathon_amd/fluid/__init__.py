@@ -8,7 +8,8 @@ from __future__ import annotations
 
 from . import core, framework, executor, layers, dygraph, io, initializer, param_attr, optimizer, regularizer, \
     clip, backward, unique_name, compiler, data_feeder, lod_tensor, metrics, nets, profiler, average, evaluator, \
-    input, reader, contrib, transpiler, incubate, parallel_executor  # noqa: F401
+    input, reader, contrib, transpiler, incubate, parallel_executor, device_worker, trainer_desc, \
+    trainer_factory  # noqa: F401
 from .framework import *  # noqa: F401,F403
 from .executor import *  # noqa: F401,F403
 from .data import data  # noqa: F401

@@ -269,9 +269,18 @@ def place_of(t: torch.Tensor) -> Place:
 # ----------------------------------------------------------------------------
 class _Mode:
     static = False
-    record_depth = 0
     trace = False  # op/layer host tracing on (paddle.profiler)
     check_nan_inf = False  # FLAGS_check_nan_inf: scan every op/layer output (and its grad)
+    _tl = threading.local()
+
+    # per thread: the dataset trainer's worker threads interpret Programs concurrently
+    @property
+    def record_depth(self):
+        return getattr(self._tl, "d", 0)
+
+    @record_depth.setter
+    def record_depth(self, v):
+        self._tl.d = v
 
 
 _mode = _Mode()

@@ -41,6 +41,9 @@ def _create_parameter(shape, dtype=None, attr=None, is_bias=False, default_initi
         else:
             init = I._global_weight_init or default_initializer or I.XavierUniform()
     init(p)
+    if _core._mode.static:   # the startup program re-initialises it for another Scope
+        from ...static.program import note_parameter
+        note_parameter(p, init)
     return p
 
 

@@ -319,11 +319,15 @@ def append_optimize_op(optimizer, params_grads, program=None, block=None, found_
     def _update(params, grads, found_inf=None):
         if found_inf is not None and bool(found_inf._t):
             return None
-        for p, g in zip(params, grads):
-            p._t.grad = g._t.detach().to(p._t.dtype)
-        with P._core_dynamic():
-            optimizer.step()
-        optimizer.clear_grad(set_to_zero=False)
+        # in a non-root Scope the params are that scope's copies: step them with its own state;
+        # Hogwild dataset-trainer threads apply their updates one at a time
+        from .trainer import hogwild_update
+        with hogwild_update(), P.optimizer_lock(optimizer), P.scoped_optimizer(optimizer, ps, params):
+            for p, g in zip(params, grads):
+                p._t.grad = g._t.detach().to(p._t.dtype)
+            with P._core_dynamic():
+                optimizer.step()
+            optimizer.clear_grad(set_to_zero=False)
         return None
 
     kw = {"params": ps, "grads": gs}

@@ -17,13 +17,16 @@ program round-trips through ``serialize_program`` / ``save_inference_model``.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import copy
 import inspect
 import itertools
 import json
 import os
+import threading
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -700,20 +703,65 @@ def _core_dynamic():
 
 
 # ----------------------------------------------------------------------------- scope / executor
-class Scope:
-    def __init__(self):
-        self.vars = {}
+class _TensorView:
+    """``scope.find_var(name).get_tensor()``: a LoDTensor handle onto the scope's value (reference
+    pybind tensor_py.h). ``set(array, place)`` writes INTO the held tensor when the shape and dtype
+    match — every program reading that parameter sees the new value at its next run — and
+    otherwise rebinds it."""
 
-    def var(self, name):
-        return self.vars.setdefault(name, _ScopeVar(name))
+    def __init__(self, holder):
+        self._h = holder
 
-    def find_var(self, name):
-        v = self.vars.get(name)
-        if v is None:
-            for p in default_main_program().all_parameters():
-                if p.name == name:
-                    return _ScopeVar(name, p)
-        return v
+    @property
+    def _v(self):
+        return self._h.value
+
+    def set(self, array, place=None):
+        arr = np.ascontiguousarray(array.numpy() if isinstance(array, Tensor) else np.asarray(array))
+        t = self._v
+        dev = _core._to_torch_device(place) if place is not None else (
+            t._t.device if t is not None and t._t.device.type != "meta" else _core.default_device())
+        new = torch.from_numpy(arr).to(dev)
+        if t is None:
+            self._h.value = _wrap(new)
+            return
+        with torch.no_grad():
+            if tuple(t._t.shape) == tuple(new.shape) and t._t.device == new.device:
+                t._t.copy_(new.to(t._t.dtype))
+            else:
+                t._t = new.to(t._t.dtype) if t._t.dtype.is_floating_point == new.dtype.is_floating_point else new
+
+    def __array__(self, dtype=None, copy=None):
+        # always a copy: the CPU tensor's numpy() would alias the live parameter memory
+        a = self._v._t.detach().cpu().numpy().copy() if self._v is not None else np.zeros([0], "float32")
+        return a.astype(dtype) if dtype is not None else a
+
+    def numpy(self):
+        return np.asarray(self)
+
+    def shape(self):
+        return list(self._v._t.shape) if self._v is not None else []
+
+    def _dtype(self):
+        return self._v._t.dtype if self._v is not None else None
+
+    def lod(self):
+        return [list(l) for l in (getattr(self._v, "_lod", None) or [])]
+
+    def set_lod(self, lod):
+        self._v._lod = [list(map(int, l)) for l in lod]
+
+    def recursive_sequence_lengths(self):
+        return [[b - a for a, b in zip(l[:-1], l[1:])] for l in self.lod()]
+
+    def set_recursive_sequence_lengths(self, lengths):
+        self.set_lod([list(np.concatenate([[0], np.cumsum(l)]).astype(int)) for l in lengths])
+
+    def _is_initialized(self):
+        return self._v is not None
+
+    def __repr__(self):
+        return f"LoDTensor(shape={self.shape()}, lod={self.lod()})"
 
 
 class _ScopeVar:
@@ -721,16 +769,116 @@ class _ScopeVar:
         self.name, self.value = name, value
 
     def get_tensor(self):
-        return self.value
+        return _TensorView(self)
+
+    def is_initialized(self):
+        return self.value is not None
 
     def set(self, value, place=None):
-        if self.value is not None and isinstance(self.value, Tensor):
-            self.value.set_value(value)
-        else:
-            self.value = _core.to_tensor(value)
+        self.get_tensor().set(value, place)
 
 
-_global_scope = Scope()
+# every persistable tensor a static Program created or ran (parameters, optimizer accumulators,
+# metric statistics) by name: what the root scope resolves names to
+_PERSISTABLES = weakref.WeakValueDictionary()
+
+
+def register_persistable(t):
+    n = getattr(t, "name", None)
+    if n:
+        _PERSISTABLES[n] = t
+
+
+class Scope:
+    """Holds the values of a Program's persistable variables (reference framework/scope.h,
+    fluid/executor.py:47). The root scope holds the tensors the Program was built with
+    (parameters are initialised when they are created); another scope holds its own copies:
+    ``Executor.run(startup, scope=s)`` initialises fresh parameters in ``s`` with their
+    initializers, and ``Executor.run(main, scope=s)`` reads and updates ``s``'s values (persistables
+    ``s`` lacks are copied in from the root at first use), so two scopes train independently.
+    Child scopes (``new_scope``) see their parents' variables."""
+
+    def __init__(self, parent=None, _root=False):
+        self.vars = {}
+        self._parent = parent
+        self._kids = []
+        self._root = _root
+
+    def var(self, name):
+        v = self.find_var(name)
+        if v is None:
+            v = self.vars[name] = _ScopeVar(name)
+            v.user = True   # created by the user: its value seeds a same-named persistable
+        return v
+
+    def find_var(self, name):
+        v = self.vars.get(name)
+        if v is None and self._root:
+            t = _PERSISTABLES.get(name)
+            if t is not None:
+                v = self.vars[name] = _ScopeVar(name, t)
+        if v is None and self._parent is not None:
+            return self._parent.find_var(name)
+        return v
+
+    def find_local_var(self, name):
+        return self.vars.get(name)
+
+    def new_scope(self):
+        c = Scope(self)
+        self._kids.append(c)
+        return c
+
+    def drop_kids(self):
+        self._kids = []
+
+    def kids(self):
+        return list(self._kids)
+
+    def local_var_names(self):
+        return list(self.vars)
+
+    def erase(self, names):
+        for n in names:
+            self.vars.pop(n, None)
+
+    def _bind(self, t):
+        """the value this scope holds for the persistable tensor ``t`` (created here from ``t`` when
+        missing: the root scope holds ``t`` itself, other scopes a copy)"""
+        name = getattr(t, "name", None)
+        if not name:
+            return t
+        if self._root:
+            # the root scope IS the build-time tensors: several programs (a loaded copy of a
+            # program, say) may each hold their own tensor under one name. A value the user put
+            # under the name before the first run (var(name).get_tensor().set) is taken over.
+            v = self.vars.get(name)
+            if v is not None and getattr(v, "user", False) and v.value is not None and v.value is not t and \
+                    tuple(v.value._t.shape) == tuple(t._t.shape):
+                with torch.no_grad():
+                    t._t.copy_(v.value._t.to(t._t.device, t._t.dtype))
+            self.vars[name] = _ScopeVar(name, t)
+            _PERSISTABLES[name] = t
+            return t
+        v = self.find_var(name)
+        if v is None or v.value is None:
+            val = t if self._root else (Parameter(data=t._t.detach().clone(), name=name, trainable=t.trainable)
+                                       if isinstance(t, Parameter) else _named_clone(t))
+            if v is None:
+                v = self.vars[name] = _ScopeVar(name, val)
+            else:
+                v.value = val
+        return v.value
+
+
+def _named_clone(t):
+    c = _wrap(t._t.detach().clone())
+    c.name = t.name
+    c.persistable = getattr(t, "persistable", True)
+    return c
+
+
+_global_scope = Scope(_root=True)
 
 
 def global_scope():
@@ -748,12 +896,106 @@ def scope_guard(scope):
         _global_scope = old
 
 
+def _scope_overrides(program, scope):
+    """{id(build-time tensor): the scope's value} for every persistable the program touches"""
+    over = {}
+    for t in _program_tensors(program):
+        if not (isinstance(t, Parameter) or getattr(t, "persistable", False)):
+            continue
+        v = scope._bind(t)
+        if v is not t:
+            over[id(t)] = v
+    return over
+
+
+class _RunScope(threading.local):   # the scope of the Executor.run in progress (per thread)
+    def __init__(self):
+        self.v = None
+
+    def __getitem__(self, i):
+        return self.v
+
+    def __setitem__(self, i, v):
+        self.v = v
+
+
+_RUN_SCOPE = _RunScope()
+
+
+_OPT_LOCKS = {}
+_OPT_LOCKS_GUARD = threading.Lock()
+
+
+def optimizer_lock(opt):
+    """the lock that serialises one optimizer's updates across dataset-trainer threads"""
+    with _OPT_LOCKS_GUARD:
+        return _OPT_LOCKS.setdefault(id(opt), threading.RLock())
+
+
+@contextlib.contextmanager
+def scoped_optimizer(opt, originals, values):
+    """an optimizer op running in a non-root scope: the step updates the scope's parameter copies
+    with the scope's own optimizer state (accumulators, master weights, step count)"""
+    sc = _RUN_SCOPE[0]
+    if sc is None or all(a is b for a, b in zip(originals, values)):
+        yield
+        return
+    st = sc.__dict__.setdefault("_opt_states", {}).setdefault(id(opt), {
+        "_accumulators": collections.defaultdict(dict), "_master_weights": {}, "_step_count": 0, "_pstep": {}})
+    saved = {k: getattr(opt, k, None) for k in st}
+    groups = [list(g["params"]) for g in opt._param_groups]
+    plist = opt._parameter_list
+    swap = {id(a): b for a, b in zip(originals, values)}
+    try:
+        for k, v in st.items():
+            setattr(opt, k, v)
+        for g in opt._param_groups:
+            g["params"] = [swap.get(id(q), q) for q in g["params"]]
+        opt._parameter_list = [swap.get(id(q), q) for q in (plist or [])]
+        yield
+    finally:
+        for k in st:
+            st[k] = getattr(opt, k)
+            setattr(opt, k, saved[k])
+        for g, ps in zip(opt._param_groups, groups):
+            g["params"] = ps
+        opt._parameter_list = plist
+
+
+def _init_in_scope(startup, scope):
+    """the startup program run in ``scope``: fresh parameters from their initializers"""
+    if scope._root:
+        return
+    for p, init in startup.__dict__.get("_param_inits", ()):
+        q = Parameter(list(p._t.shape), p._t.dtype, name=p.name, trainable=p.trainable)
+        if init is not None:
+            init(q)
+        else:
+            q._t.data.copy_(p._t)
+        v = scope.vars.get(p.name)
+        if v is None:
+            scope.vars[p.name] = _ScopeVar(p.name, q)
+        else:
+            v.value = q
+
+
+def note_parameter(p, init):
+    """a parameter created in a static Program: the startup program re-runs ``init`` for another
+    scope, and the root scope resolves its name"""
+    if not _core._mode.static:
+        return
+    register_persistable(p)
+    default_startup_program().__dict__.setdefault("_param_inits", []).append((p, init))
+
+
 def _subst(tree, env):
     if isinstance(tree, Variable):
         try:
             return env[id(tree)]
         except KeyError:
             raise RuntimeError(f"variable {tree.name} has no value (missing feed?)")
+    if isinstance(tree, Tensor):   # a persistable: the running scope's value (Scope._bind)
+        return env.get(id(tree), tree)
     if isinstance(tree, list):
         return [_subst(t, env) for t in tree]
     if isinstance(tree, tuple):
@@ -861,11 +1103,21 @@ def _program_tensors(program):
     return out
 
 
-def run_program(program, feed, fetch_list):
+def run_program(program, feed, fetch_list, scope=None):
     """Interpret ``program`` with ``feed``; returns fetched Tensors (real). Intermediate values are
-    dropped right after their last reader (eager deletion)."""
+    dropped right after their last reader (eager deletion). Persistables read and write ``scope``'s
+    values (default: the root scope, i.e. the tensors the program was built with)."""
     blk = program.global_block()
-    env = {}
+    sc = scope if scope is not None else _global_scope
+    env = _scope_overrides(program, sc)
+    prev_scope, _RUN_SCOPE[0] = _RUN_SCOPE[0], (sc if env else None)
+    try:
+        return _run_program(program, blk, env, feed, fetch_list)
+    finally:
+        _RUN_SCOPE[0] = prev_scope
+
+
+def _run_program(program, blk, env, feed, fetch_list):
     for name, val in (feed or {}).items():
         v = blk.vars.get(name)
         if v is None:
@@ -900,7 +1152,7 @@ def run_program(program, feed, fetch_list):
     for f in fetch_list or []:
         if isinstance(f, str):
             if f not in blk.vars:   # a persistable (parameter / optimizer state) by name
-                hit = [t for t in _program_tensors(program) if getattr(t, "name", None) == f]
+                hit = [env.get(id(t), t) for t in _program_tensors(program) if getattr(t, "name", None) == f]
                 if not hit:
                     raise KeyError(f)
                 res.append(_wrap(hit[0]._t.detach().clone()))   # a snapshot: later steps update it in place
@@ -909,7 +1161,7 @@ def run_program(program, feed, fetch_list):
         if isinstance(f, Variable):
             res.append(env[id(f)])
         elif isinstance(f, Tensor):
-            res.append(f)
+            res.append(env.get(id(f), f))
         else:
             raise TypeError(f"cannot fetch {f!r}")
     return res
@@ -1043,9 +1295,12 @@ class Executor:
         if isinstance(program, CompiledProgram):
             outs = program._run(feed, fetch_list)
         else:
+            sc = scope if scope is not None else _global_scope
+            if program.__dict__.get("_param_inits"):
+                _init_in_scope(program, sc)
             if not program.global_block().ops:
                 return []
-            outs = run_program(program, feed, fetch_list)
+            outs = run_program(program, feed, fetch_list, sc)
         if return_numpy:
             return [o.numpy() if isinstance(o, Tensor) else o for o in outs]
         return outs
@@ -1058,10 +1313,18 @@ class Executor:
 
     def train_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
                            fetch_info=None, print_period=100, fetch_handler=None):
-        for batch in dataset:
-            self.run(program, feed=batch, fetch_list=fetch_list)
+        """``thread`` Hogwild (or, for a parameter-server program, DownpourSGD) worker threads over
+        the dataset's batches (static/trainer.py)"""
+        from .trainer import run_from_dataset
+        return run_from_dataset(self, program, dataset, scope, thread, False, debug, fetch_list, fetch_info,
+                                print_period, fetch_handler)
 
-    infer_from_dataset = train_from_dataset
+    def infer_from_dataset(self, program=None, dataset=None, scope=None, thread=0, debug=False, fetch_list=None,
+                           fetch_info=None, print_period=100, fetch_handler=None):
+        """the program's inference part (backward / optimizer ops dropped) over the dataset"""
+        from .trainer import run_from_dataset
+        return run_from_dataset(self, program, dataset, scope, thread, True, debug, fetch_list, fetch_info,
+                                print_period, fetch_handler)
 
 
 class BuildStrategy:
