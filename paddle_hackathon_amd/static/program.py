@@ -1293,7 +1293,7 @@ class Executor:
             for r in readers:
                 feed.update(r._next_feed())
         if isinstance(program, CompiledProgram):
-            outs = program._run(feed, fetch_list)
+            outs = program._run(feed, fetch_list, scope)
         else:
             sc = scope if scope is not None else _global_scope
             if program.__dict__.get("_param_inits"):
@@ -1351,6 +1351,33 @@ class ExecutionStrategy:
         self.use_thread_barrier = False
 
 
+def data_parallel_program(program, world, bucket_bytes=64 << 20):
+    """insert the bucketed, backward-overlapped gradient all-reduce (mean over ``world`` ranks) in
+    front of ``program``'s optimizer ops, in place; a program already rewritten is left alone"""
+    if program.__dict__.get("_dp_world"):
+        return program
+    from ..parallel.fleet.static_optimizers import StaticFleetOptimizer
+    blk = program.global_block()
+    opt_ops = [op for op in blk.ops if op.attrs.get("op_role") in ("optimize", 2) and "grads" in op.kwargs]
+    if not opt_ops:
+        program.__dict__["_dp_world"] = world
+        return program
+    for op in opt_ops:
+        blk.ops.remove(op)
+    helper = StaticFleetOptimizer.__new__(StaticFleetOptimizer)
+    helper.world = world
+    grads = [g for op in opt_ops for g in op.kwargs["grads"]]
+    reduced = helper._insert_overlapped_allreduce(blk, grads, bucket_bytes, world=world)
+    k = 0
+    for op in opt_ops:
+        n = len(op.kwargs["grads"])
+        op.kwargs = dict(op.kwargs, grads=tuple(reduced[k:k + n]))
+        k += n
+        blk.append_op(op)
+    program.__dict__["_dp_world"] = world
+    return program
+
+
 class CompiledProgram:
     """Program + build strategy. With ``build_strategy.use_hip_graph`` a forward-only program is
     captured once per feed signature into a HIP graph and replayed (static input/output
@@ -1363,15 +1390,36 @@ class CompiledProgram:
 
     def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, share_vars_from=None,
                            places=None):
+        """data parallelism over the job's ranks (reference compiler.py:178). One process drives
+        one MI355X: with more than one rank (``torch.distributed`` initialised — RCCL / gloo) every
+        gradient of the program's optimizer ops is all-reduced (mean) in buckets whose collectives
+        start right after their last gradient op and are waited for before the update (the static
+        fleet DP pass). Several places in one process are refused: start one process per GPU."""
         if build_strategy is not None:
             self._build_strategy = build_strategy
+        if places is not None and len(list(places)) > 1:
+            raise ValueError("with_data_parallel: one process per GPU on MI355X — start one process per device "
+                             "(paddle.distributed.launch / spawn) instead of passing several places")
+        import torch.distributed as tdist
+        env_world = int(os.environ.get("PADDLE_TRAINERS_NUM", "1"))
+        if tdist.is_available() and tdist.is_initialized():
+            world = tdist.get_world_size()
+        elif env_world > 1:
+            raise RuntimeError(f"with_data_parallel: PADDLE_TRAINERS_NUM={env_world} but no process group is "
+                               "initialised; call paddle.distributed.init_parallel_env() (or fleet.init) first")
+        else:
+            world = 1
+        if world > 1:
+            mb = getattr(self._build_strategy, "fuse_grad_size_in_MB", None) or 64
+            data_parallel_program(self._program, world, int(mb * 1024 * 1024))
+        self._dp_world = world
         return self
 
-    def _run(self, feed, fetch_list):
+    def _run(self, feed, fetch_list, scope=None):
         has_opt = any(is_train_op(op) for op in self._program.global_block().ops)
         if not self._build_strategy.use_hip_graph or has_opt or not torch.cuda.is_available() \
-                or has_control_flow(self._program):   # data-dependent branches cannot be captured
-            return run_program(self._program, feed, fetch_list)
+                or has_control_flow(self._program) or (scope is not None and scope is not _global_scope):
+            return run_program(self._program, feed, fetch_list, scope)   # (branches cannot be captured)
         key = tuple((k, tuple(np.shape(v if not isinstance(v, Tensor) else v._t)), str(getattr(v, "dtype", "")))
                     for k, v in sorted(feed.items()))
         ent = self._graphs.get(key)
