@@ -294,6 +294,7 @@ class QuantizationFreezePass:
                 s = Q.channel_abs_max(w._t, axis) if axis is not None else Q.abs_max(w._t)
                 with torch.no_grad():
                     w._t.copy_(_qdq_value(w._t, s, op.kwargs.get("bit_length", self._wbits), axis).to(w._t.dtype))
+                w._frozen_quant = (s.detach().clone(), axis)   # ConvertToInt8Pass stores on this grid
                 outs = op.outputs if isinstance(op.outputs, (tuple, list)) else (op.outputs,)
                 rewire[id(outs[0])] = w
                 continue
@@ -328,15 +329,22 @@ class ConvertToInt8Pass:
             if not isinstance(wt, Parameter):
                 continue
             if id(wt) not in done:
-                s = Q.channel_abs_max(wt._t, axis)
-                lv = Q.quant_dequant(wt._t, s, self._bits, 0, dequant=False, quant_axis=axis, out_dtype=torch.float32)
+                frozen = getattr(wt, "_frozen_quant", None)
+                if frozen is not None:   # the freeze pass's own scale (per tensor or per channel)
+                    s, qaxis = frozen
+                else:
+                    s, qaxis = Q.channel_abs_max(wt._t, axis), axis
+                if qaxis is None:
+                    s = s.reshape(-1)[:1].float()
+                lv = Q.quant_dequant(wt._t, s, self._bits, 0, dequant=False, quant_axis=qaxis,
+                                     out_dtype=torch.float32)
                 q = Parameter(data=lv.to(torch.int8), name=(wt.name or "w") + ".int8", trainable=False)
                 q.stop_gradient = True
                 sp = Parameter(data=s.float(), name=(wt.name or "w") + ".scale", trainable=False)
                 sp.stop_gradient = True
                 out = _new_var(blk, _wrap(wt._t.to("meta")), (wt.name or "w") + ".dequantized")
                 dq = _make_op("dequantize_linear", {"x": q, "scale": sp, "bit_length": self._bits,
-                                                    "quant_axis": axis}, out)
+                                                    "quant_axis": qaxis if qaxis is not None else -1}, out)
                 _insert_before(blk, op, dq)
                 done[id(wt)] = out
             _replace_input(op, w, done[id(wt)])

@@ -555,6 +555,53 @@ def _infer_meta(fn, name, bargs, bkw):
         _core._mode.record_depth -= 1
 
 
+_PROBE = 7   # the size a -1 dim takes in the second meta run (the first uses 1)
+
+
+def _dynamic_dims(v):
+    ds = v.declared_shape
+    if ds is None or len(ds) != v._t.dim():
+        return ()
+    return tuple(i for i, d in enumerate(ds) if d is not None and d < 0)
+
+
+def _to_probe(tree):
+    if isinstance(tree, Variable):
+        dims = _dynamic_dims(tree)
+        if not dims:
+            return _wrap(tree._t)
+        shp = [_PROBE if i in dims else int(s) for i, s in enumerate(tree._t.shape)]
+        return _wrap(torch.empty(shp, dtype=tree._t.dtype, device="meta"))
+    if isinstance(tree, list):
+        return [_to_probe(t) for t in tree]
+    if isinstance(tree, tuple):
+        return tuple(_to_probe(t) for t in tree)
+    if isinstance(tree, dict):
+        return {k: _to_probe(v) for k, v in tree.items()}
+    return _to_meta(tree)
+
+
+def _propagate_dynamic(fn, bargs, bkw, meta_out):
+    """-1 dims through an op: a second meta run with the inputs' -1 dims at another size; the
+    output dims that move with it are -1 (a -1 batch stays -1 through the layers, as the
+    reference's InferMeta keeps it). None when no input has a -1 dim or the probe fails."""
+    if not any(_dynamic_dims(v) for v in _iter_vars((bargs, bkw))):
+        return None
+    _core._mode.record_depth += 1
+    try:
+        probe = fn(*_to_probe(bargs), **_to_probe(bkw))
+    except Exception:   # noqa: BLE001 - e.g. a reshape to fixed dims: the output stays static
+        return None
+    finally:
+        _core._mode.record_depth -= 1
+    a = list(_iter_tensors(meta_out if isinstance(meta_out, (list, tuple)) else [meta_out]))
+    b = list(_iter_tensors(probe if isinstance(probe, (list, tuple)) else [probe]))
+    if len(a) != len(b):
+        return None
+    return [tuple(i for i, (x, y) in enumerate(zip(ta._t.shape, tb._t.shape)) if x != y)
+            if ta._t.dim() == tb._t.dim() else () for ta, tb in zip(a, b)]
+
+
 def _mark_dynamic(outs, dyn):
     if not dyn:
         return
@@ -571,6 +618,8 @@ def record_op(fn, name, args, kwargs):
     OP_REGISTRY.setdefault(qual, fn)
     bargs, bkw = _bind(fn, args, kwargs)
     meta_out, dyn = _infer_meta(fn, name, bargs, bkw)
+    if dyn is None and os.environ.get("PHA_STATIC_DYN_DIMS", "1") != "0":
+        dyn = _propagate_dynamic(fn, bargs, bkw, meta_out)
     blk = default_main_program().current_block()
     outs = _outputs_to_vars(meta_out, blk)
     _mark_dynamic(outs, dyn)
