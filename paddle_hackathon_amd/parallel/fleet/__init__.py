@@ -24,9 +24,10 @@ from ..topology import CommunicateTopology, HybridCommunicateGroup, ParallelMode
 from .. import mp_layers, pipeline
 from ..data_parallel import DataParallel, sync_params_buffers
 from . import meta_parallel, utils  # noqa: F401
+from .utils import HybridParallelInferenceHelper  # noqa: F401
 from .role_maker import PaddleCloudRoleMaker, UserDefinedRoleMaker, Role  # noqa: F401
 
-__all__ = ["CommunicateTopology", "DistributedStrategy", "Fleet", "HybridCommunicateGroup", "MultiSlotDataGenerator",
+__all__ = ["CommunicateTopology", "DistributedStrategy", "Fleet", "HybridCommunicateGroup", "HybridParallelInferenceHelper", "MultiSlotDataGenerator",
            "MultiSlotStringDataGenerator", "PaddleCloudRoleMaker", "Role", "UserDefinedRoleMaker", "UtilBase",
            "init", "distributed_model", "distributed_optimizer", "get_hybrid_communicate_group", "worker_index",
            "worker_num", "is_first_worker", "worker_endpoints", "barrier_worker", "meta_parallel", "utils"]

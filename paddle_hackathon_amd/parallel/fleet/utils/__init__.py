@@ -1,6 +1,7 @@
 """fleet.utils (reference: python/paddle/distributed/fleet/utils/__init__.py)."""
 from ...recompute import recompute, recompute_sequential  # noqa: F401
-from . import hybrid_parallel_util  # noqa: F401
+from . import hybrid_parallel_util, hybrid_parallel_inference  # noqa: F401
+from .hybrid_parallel_inference import HybridParallelInferenceHelper  # noqa: F401
 
 
 class LocalFS:

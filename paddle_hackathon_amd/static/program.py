@@ -176,6 +176,8 @@ class Block:
         return [v for v in self.vars.values() if isinstance(v, Parameter)]
 
     def append_op(self, op):
+        if _OP_DEVICE[0] is not None and "op_device" not in op.attrs:   # static.device_guard
+            op.attrs["op_device"] = _OP_DEVICE[0]
         self.ops.append(op)
         return op
 

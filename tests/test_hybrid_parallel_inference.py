@@ -1,0 +1,83 @@
+"""fleet.utils.HybridParallelInferenceHelper (reference distributed/fleet/utils/
+hybrid_parallel_inference.py:23; round-4 verdict item 10): the reference's documented generation
+While loop, cut into two pipeline stages with device_guard, runs split over two gloo ranks (send /
+recv at the stage boundary, the token array and the loop condition synced from the last stage in
+the While body) and gives every rank the single-process result."""
+import numpy as np
+
+from dist_helper import run_dist
+
+
+def _program(paddle):
+    import paddle_hackathon_amd.fluid.layers as layers
+    main, start = paddle.static.Program(), paddle.static.Program()
+    device = "gpu"
+    with paddle.static.program_guard(main, start):
+        with paddle.fluid.device_guard(f"{device}:0"):
+            X = paddle.static.data(name="X", shape=[None, 2], dtype="float32")
+        with paddle.fluid.device_guard(f"{device}:all"):
+            max_len = layers.fill_constant(shape=[1], dtype="int64", value=5, force_cpu=False, name="n")
+            step_idx = layers.fill_constant(shape=[1], dtype="int64", value=0, force_cpu=False, name="i")
+            data = layers.array_write(X, step_idx)
+            cond_int = layers.fill_constant(shape=[1], dtype="int64", value=0, force_cpu=False, name="cond_int")
+            cond = layers.less_than(x=step_idx, y=max_len)
+            while_op = layers.While(cond, is_test=True)
+        with while_op.block():
+            with paddle.fluid.device_guard(f"{device}:all"):
+                input = layers.array_read(array=data, i=step_idx)
+                layers.increment(x=step_idx, value=1.0, in_place=True)
+                layers.array_write(input, i=step_idx, array=data)
+            with paddle.fluid.device_guard(f"{device}:0"):
+                w1 = paddle.static.create_parameter(shape=[2, 5], dtype="float32", attr=paddle.ParamAttr(
+                    initializer=paddle.nn.initializer.Constant(0.5)), is_bias=False)
+                hidden1 = paddle.matmul(input, w1)
+            with paddle.fluid.device_guard(f"{device}:1"):
+                w2 = paddle.static.create_parameter(shape=[5, 2], dtype="float32", attr=paddle.ParamAttr(
+                    initializer=paddle.nn.initializer.Constant(0.3)), is_bias=False)
+                hidden2 = paddle.tanh(paddle.matmul(hidden1, w2))
+                layers.array_write(hidden2, i=step_idx, array=data)
+                layers.less_than(x=step_idx, y=max_len, cond=cond)
+                layers.assign(layers.cast(cond, dtype="int32"), cond_int)
+            with paddle.fluid.device_guard(f"{device}:all"):
+                layers.assign(layers.cast(cond_int, dtype="bool"), cond)
+        with paddle.fluid.device_guard(f"{device}:all"):
+            out = layers.create_array(data.dtype)
+            layers.assign(data, out)
+    return main, start, data, cond_int, out
+
+
+_X = np.random.RandomState(0).uniform(size=[2, 2]).astype("float32")
+
+
+def _worker(rank, world):
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.distributed import fleet
+    paddle.enable_static()
+    main, start, data, cond_int, out = _program(paddle)
+    helper = fleet.HybridParallelInferenceHelper(start, main, micro_batch_size=2, num_pp=2, init_comm=True)
+    helper.gen_infer_program([data], [cond_int])
+    types = [op.type for b in main.blocks for op in b.ops]
+    exe = paddle.static.Executor()
+    exe.run(start)
+    res = exe.run(main, feed={"X": _X}, fetch_list=[out])
+    return np.asarray(res[0]), types
+
+
+def test_two_stage_generation_loop_matches_single_process():
+    import paddle_hackathon_amd as paddle
+    res = run_dist(_worker, 2)
+    paddle.enable_static()
+    try:
+        main, start, data, cond_int, out = _program(paddle)
+        exe = paddle.static.Executor()
+        exe.run(start)
+        ref = np.asarray(exe.run(main, feed={"X": _X}, fetch_list=[out])[0])
+    finally:
+        paddle.disable_static()
+    assert ref.shape == (6, 2, 2)
+    for arr, types in res:
+        np.testing.assert_allclose(arr, ref, rtol=1e-6)
+        assert "send_v2" in types or "recv_v2" in types
+    # stage 0 sends hidden1 and receives the synced array + condition; stage 1 the reverse
+    assert "send_v2" in res[0][1] and "recv_v2" in res[0][1] and "recv_v2" in res[1][1]
+    assert "matmul" not in " ".join(t for t in res[0][1] if "tanh" in t)
