@@ -77,6 +77,8 @@ struct Args {
   float* ws;    // split-K: fp32 partial slabs [splits][M][N] (C unused)
   int splits;
   void* aux;    // EPI_GELU: pre-activation output, same shape and row stride as C
+  int batch;    // batched products: item b reads A + b * sa, B + b * sb and writes C + b * sc
+  long long sa, sb, sc;   // (element strides; the tiles of all batches share one persistent grid)
 };
 
 constexpr int OPB = 256 * 64 * 2;   // one operand image (32 KB)
@@ -143,14 +145,16 @@ __device__ __forceinline__ void mma0(f32x4& d, const uint4& a, const uint4& b) {
 // HBM / MALL reads spread over the channels) while the 32 CUs of an XCD share panels in its L2.
 // Otherwise lin = r * G + pos. lin -> (tm, tn) in GROUP_M-row panels.
 struct Sched {
-  int tiles_m, tiles_n, total, G, pos, gm, splits;
+  int tiles_m, tiles_n, total, G, pos, gm, splits, per_batch;
   int c0, c1, step;   // this workgroup's chunk [c0, c1) and stride
   __device__ __forceinline__ bool valid(int r) const { return c0 + r * step < c1; }
   // work item of round r: tile (tm, tn) and K slice (the slices of a tile are adjacent items)
-  __device__ __forceinline__ void tile(int r, int& tm, int& tn, int& slice) const {
+  __device__ __forceinline__ void tile(int r, int& tm, int& tn, int& slice, int& bi) const {
     const int item = c0 + r * step;
-    const int lin = item / splits;
+    int lin = item / splits;
     slice = __builtin_amdgcn_readfirstlane(item - lin * splits);
+    bi = __builtin_amdgcn_readfirstlane(lin / per_batch);   // batch index (tiles of one batch adjacent)
+    lin -= bi * per_batch;
     const int group = lin / (gm * tiles_n);
     const int first_m = group * gm;
     const int gsize = min(tiles_m - first_m, gm);
@@ -180,7 +184,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   sc.tiles_m = (M + 255) >> 8;
   sc.tiles_n = (N + 255) >> 8;
   sc.splits = nsplit;
-  sc.total = sc.tiles_m * sc.tiles_n * nsplit;
+  sc.per_batch = sc.tiles_m * sc.tiles_n;
+  sc.total = sc.per_batch * nsplit * p.batch;
   sc.G = gridDim.x;
   sc.gm = p.group_m;
   {
@@ -213,8 +218,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const unsigned lds0 = lds_u32(smem);
 
   auto set_tile = [&](int r) {   // DMA offsets + bases of round r's tile
-    int tm, tn, slice;
-    sc.tile(r, tm, tn, slice);
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
     const size_t k0 = (size_t)slice * nk * 64;   // first K of the item
     const int m0 = tm << 8, n0 = tn << 8;
 #pragma unroll
@@ -238,8 +243,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (op == 0) aoff[u] = off; else boff[u] = off;
       }
     }
-    abase = static_cast<const char*>(p.a) + (AKO ? (size_t)m0 * 2 + k0 * p.lda * 2 : (size_t)m0 * p.lda * 2 + k0 * 2);
-    bbase = static_cast<const char*>(p.b) + (BKO ? (size_t)n0 * 2 + k0 * p.ldb * 2 : (size_t)n0 * p.ldb * 2 + k0 * 2);
+    abase = static_cast<const char*>(p.a) + (size_t)bi * p.sa * 2 +
+            (AKO ? (size_t)m0 * 2 + k0 * p.lda * 2 : (size_t)m0 * p.lda * 2 + k0 * 2);
+    bbase = static_cast<const char*>(p.b) + (size_t)bi * p.sb * 2 +
+            (BKO ? (size_t)n0 * 2 + k0 * p.ldb * 2 : (size_t)n0 * p.ldb * 2 + k0 * 2);
     if constexpr (BIAS && !SPLIT) {   // the tile's 256 output-column biases -> slot r & 3 (wave w: 64 of them)
       const int c0 = OT ? m0 : n0, No = OT ? M : N;
       const int col = min(c0 + wid * 64 + lane, No - 1);
@@ -330,15 +337,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const char* e_aux = static_cast<const char*>(p.aux);
   int e_rows = 0, e_cols = 0, e_slot = 0;
   auto set_epi = [&](int r) {
-    int tm, tn, slice;
-    sc.tile(r, tm, tn, slice);
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
     const int r0 = OT ? tn << 8 : tm << 8, c0 = OT ? tm << 8 : tn << 8;
     e_slot = r & 3;
     if constexpr (SPLIT)
       e_base = reinterpret_cast<const char*>(p.ws) + (size_t)slice * Mo * No * 4 +
                ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 4);
     else
-      e_base = static_cast<const char*>(p.c) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+      e_base = static_cast<const char*>(p.c) + (size_t)bi * p.sc * 2 + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
     if constexpr (GELU) e_aux = static_cast<const char*>(p.aux) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
     // (EPI_NOSTORE, measurement only: zero rows, every store is issued and dropped)
     e_rows = (p.epi & EPI_NOSTORE) ? 0 : Mo - r0 - wrow;
@@ -824,9 +831,12 @@ using namespace pha;
 // transposed store (C is then [N][ldc]). Requires K % 64 == 0; M, N, lda, ldb, ldc % 8 == 0; 16-B
 // aligned base pointers; K-outer operand dims >= 8; per-panel byte offsets < 2^32; 256 output rows
 // x ldc x 2 bytes < 2^31. grid: workgroups (<= tiles; the caller passes the CU count).
-PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
-                       long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
-                       int group_m, float* ws, int splits, hipStream_t stream, void* aux) {
+// batch > 1: C_i = A_i . B_i for i < batch, A_i = a + i * sa (elements; likewise b, c), all tiles of
+// all items in one persistent launch (torch.bmm / paddle.bmm with per-batch right operands).
+PHA_API int pha_gemm4p_batched(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda,
+                               long ldb, long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias,
+                               int grid, int group_m, float* ws, int splits, hipStream_t stream, void* aux, int batch,
+                               long sa, long sb, long sc) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || M % 8 || N % 8 || lda % 8 || ldb % 8 || ldc % 8)
     return (int)hipErrorInvalidValue;
   if ((a_kouter && M < 8) || (b_kouter && N < 8)) return (int)hipErrorInvalidValue;
@@ -839,16 +849,27 @@ PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, lo
   if ((epi & g4p::EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if ((epi & g4p::EPI_GELU) && (!aux || ((size_t)aux & 15) || splits > 1)) return (int)hipErrorInvalidValue;
   if (splits < 1) splits = 1;
+  if (batch < 1 || (batch > 1 && (splits > 1 || (epi & g4p::EPI_GELU) || (sa | sb | sc) % 8 || sa < 0 || sb < 0 || sc < 0)))
+    return (int)hipErrorInvalidValue;
+  if ((double)batch * ((M + 255) / 256) * ((N + 255) / 256) >= 2147483647.0) return (int)hipErrorInvalidValue;
   if (splits > 1 && (!ws || (K / 64) % splits || !a_kouter || !b_kouter || trans || (size_t)ws & 15))
     return (int)hipErrorInvalidValue;
-  const long tiles = ((M + 255) / 256) * ((N + 255) / 256) * splits;
+  const long tiles = ((M + 255) / 256) * ((N + 255) / 256) * splits * batch;
   if (grid <= 0 || grid > tiles) grid = (int)tiles;
   if (group_m <= 0) group_m = 4;
-  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits, aux};
+  g4p::Args p{a, b, c, bias, (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc, epi, group_m, ws, splits, aux,
+              batch, sa, sb, sc};
   const bool bs = epi & g4p::EPI_BIAS;
   if (dt == kBF16) return bs ? g4p::launch<bf16_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                              : g4p::launch<bf16_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
   if (dt == kF16) return bs ? g4p::launch<half_t, true>(p, a_kouter, b_kouter, trans, grid, stream)
                             : g4p::launch<half_t, false>(p, a_kouter, b_kouter, trans, grid, stream);
   return (int)hipErrorInvalidValue;
+}
+
+PHA_API int pha_gemm4p(int dt, const void* a, const void* b, void* c, long M, long N, long K, long lda, long ldb,
+                       long ldc, int a_kouter, int b_kouter, int trans, int epi, const float* bias, int grid,
+                       int group_m, float* ws, int splits, hipStream_t stream, void* aux) {
+  return pha_gemm4p_batched(dt, a, b, c, M, N, K, lda, ldb, ldc, a_kouter, b_kouter, trans, epi, bias, grid, group_m,
+                            ws, splits, stream, aux, 1, 0, 0, 0);
 }

@@ -260,10 +260,12 @@ class ConvElementwiseAddActPass(Pass):
             if nxt is None or ACTS.get(nxt.type) != "relu":
                 continue
             new = _fused(FO.conv2d_fusion, dict(conv.kwargs, residual=residual, act="relu"), nxt.outputs)
-            blk.ops[blk.ops.index(conv)] = new
+            # at the activation's position: the residual may come from an op after the conv (the
+            # other branch of a block: conv -> add(other_conv_bn, conv) -> relu)
+            blk.ops[blk.ops.index(nxt)] = new
             if last is not conv:
                 blk.ops.remove(last)
-            blk.ops.remove(nxt)
+            blk.ops.remove(conv)
             g = _Graph(blk.ops, fetches)
             n += 1
         return n

@@ -76,9 +76,46 @@ class MultiHeadAttention(Layer):
             return self.Cache(_wrap(z), _wrap(z.clone()))
         return self.Cache(key, value)
 
+    def _forward_ops(self, query, key, value, attn_mask, cache):
+        """the reference's op-level graph (nn/layer/transformer.py MultiHeadAttention.forward:
+        projections, reshape2 / transpose2 to [B, H, S, D], scaled matmul_v2, mask add, softmax,
+        dropout, matmul_v2, transpose2 / reshape2, out projection): what static Programs
+        (jit.save, to_static) record, so a saved model holds reference op types"""
+        from ... import tensor as T
+
+        def heads(t):
+            return T.transpose(T.reshape(t, [0, 0, self.num_heads, self.head_dim]), [0, 2, 1, 3])
+        q = heads(self.q_proj(query))
+        if isinstance(cache, self.StaticCache):
+            k, v = cache.k, cache.v
+        else:
+            k, v = heads(self.k_proj(key)), heads(self.v_proj(value))
+        if isinstance(cache, self.Cache):
+            k, v = T.concat([cache.k, k], axis=2), T.concat([cache.v, v], axis=2)
+            cache = self.Cache(k, v)
+        product = T.matmul(T.scale(q, self.head_dim ** -0.5), k, transpose_y=True)
+        if attn_mask is not None:
+            m = attn_mask
+            if str(m.dtype).endswith(("bool", "int32", "int64", "uint8")):
+                m = T.scale(T.cast(m, product.dtype), 1e9, bias=-1e9)   # keep 0, masked -1e9
+            product = product + m
+        weights = F.softmax(product)
+        if self.dropout:
+            weights = F.dropout(weights, self.dropout, training=self.training, mode="upscale_in_train")
+        out = T.reshape(T.transpose(T.matmul(weights, v), [0, 2, 1, 3]), [0, 0, self.embed_dim])
+        outs = [self.out_proj(out)]
+        if self.need_weights:
+            outs.append(weights)
+        if cache is not None:
+            outs.append(cache)
+        return outs[0] if len(outs) == 1 else tuple(outs)
+
     def forward(self, query, key=None, value=None, attn_mask=None, cache=None):
         key = query if key is None else key
         value = query if value is None else value
+        from ...framework.core import _mode
+        if _mode.static:
+            return self._forward_ops(query, key, value, attn_mask, cache)
         q = self._split(self.q_proj(query)._t)
         if isinstance(cache, self.StaticCache):
             k, v = cache.k._t, cache.v._t
@@ -139,7 +176,8 @@ class TransformerEncoderLayer(Layer):
         self.activation = activation
 
     def _ffn_act(self, x):
-        if self.activation == "gelu":
+        from ...framework.core import _mode
+        if self.activation == "gelu" and not _mode.static:
             from ... import ops
             h = torch.matmul(x._t, self.linear1.weight._t)
             return _wrap(ops.bias_gelu(h, self.linear1.bias._t)) if self.linear1.bias is not None else F.gelu(_wrap(h))

@@ -3,6 +3,8 @@
   * ``_C/libpha_kernels.so`` — gfx950 HIP kernels (csrc/kernels/*.hip)
   * ``_C/libpha_runtime.so`` — host C++ runtime (csrc/runtime/*.cpp): data-loader
     ring buffer, gradient bucket planner, host tracer, best-fit arena allocator.
+  * ``_C/libpha_infer.so`` — native inference engine with the reference's C API subset
+    (csrc/infer, header csrc/infer/pha_infer.h).
 
 Usage: ``python -m paddle_hackathon_amd.ops.build [--force]``.
 """
@@ -126,8 +128,28 @@ def build_runtime(force=False, verbose=True):
     return target
 
 
+def build_infer(force=False, verbose=True):
+    """``_C/libpha_infer.so`` — the native inference engine + its C API (csrc/infer: host C++ and
+    the gfx950 kernels of its device path, linked against the HIP runtime only)"""
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "infer", "*.cpp")) + glob.glob(os.path.join(CSRC, "infer", "*.hip")))
+    hdrs = glob.glob(os.path.join(CSRC, "infer", "*.h"))
+    if not srcs:
+        return None
+    target = os.path.join(OUT, "libpha_infer.so")
+    flags = ["-O3", "-std=c++20", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-pthread"]
+    if not force and not _stale(srcs + hdrs, target, flags):
+        return target
+    _run([_hipcc()] + flags + ["-o", target + ".tmp"] + srcs)
+    os.replace(target + ".tmp", target)
+    _write_stamp(srcs + hdrs, target, flags)
+    if verbose:
+        print(f"[pha] built {target} (native inference engine)")
+    return target
+
+
 def build_all(force=False, verbose=True):
-    return build_kernels(force, verbose), build_runtime(force, verbose)
+    return build_kernels(force, verbose), build_runtime(force, verbose), build_infer(force, verbose)
 
 
 if __name__ == "__main__":

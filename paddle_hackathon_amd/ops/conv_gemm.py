@@ -540,6 +540,7 @@ _wlayouts = {}
 def split3(t, dim, order="hhl"):
     """fp32 t -> bf16 parts concatenated along ``dim`` in ``order`` (h = hi, l = lo); one pass of
     csrc/kernels/split.hip on the GPU"""
+    assert len(order) == 3 and set(order) <= {"h", "l"}, f"split3 takes three parts, got {order!r}"
     dim = dim % t.dim()
     inner = t[(0,) * dim].numel() if t.numel() else 0
     if (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and inner and inner % 8 == 0
@@ -554,9 +555,9 @@ def split3(t, dim, order="hhl"):
             return out
     hi = t.to(torch.bfloat16)
     fin = torch.isfinite(t)
+    # finite past the bf16 range: truncate instead of rounding to inf (no host sync: graph-capturable)
     over = fin & ~torch.isfinite(hi)
-    if bool(over.any()):   # finite past the bf16 range: truncate instead of rounding to inf
-        hi = torch.where(over, (t.view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16), hi)
+    hi = torch.where(over, (t.contiguous().view(torch.int32) >> 16).to(torch.int16).view(torch.bfloat16), hi)
     lo = torch.where(fin, t - hi.float(), torch.zeros_like(t)).to(torch.bfloat16)
     return torch.cat([hi if c == "h" else lo for c in order], dim)
 

@@ -40,6 +40,9 @@ def _L():
         L.pha_gemm4w.restype = c_int
         L.pha_gemm4p.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P, P]
         L.pha_gemm4p.restype = c_int
+        L.pha_gemm4p_batched.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, I, I, I, P, I, I, P, I, P, P, I,
+                                         LG, LG, LG]
+        L.pha_gemm4p_batched.restype = c_int
         L.pha_gemm8w.argtypes = [I, P, P, P, LG, LG, LG, LG, LG, LG, I, P, I, P]
         L.pha_gemm8w.restype = c_int
         L.pha_colsum_finish.argtypes = [I, P, P, I, I, P]
@@ -209,7 +212,14 @@ def _epi_default(a_kouter, b_kouter, trans_out, K):
     long-K NT, ~1 % on the TN weight gradients and K = 2048 NT, +0.3-0.4 % on the whole GPT step
     (profiles/gemm4p_early_ab_r3.log, gemm4p_relg_ab_r3.log). PHA_G4P_EARLY=0 selects the plain
     schedule (1 forces the early one)."""
-    return 0 if os.environ.get("PHA_G4P_EARLY", "1") == "0" else EPI_EARLY
+    if os.environ.get("PHA_G4P_EARLY", "1") == "0":
+        return 0
+    if not (a_kouter or b_kouter or trans_out):
+        # NT: PIN variant (LV 8 — an empty memory asm closes every MFMA group so no IR pass sinks
+        # a group's LDS reads past the loop latch): 1-3 % over LV 0 on every GPT NT shape,
+        # bitwise identical (profiles/g4p_late_ab_r5.log); PHA_G4P_LV overrides
+        return EPI_EARLY | (int(os.environ.get("PHA_G4P_LV", "8")) << 17)
+    return EPI_EARLY
 
 
 def nn_p(a, b, bias=None, **kw):
@@ -243,6 +253,87 @@ def _impl():
 
 
 _AUTO_OWN = ("tn", "nn")
+
+
+def bmm_p(a, b, a_kouter=False, b_kouter=False, trans_out=False):
+    """batched C_i = op(A_i) @ op(B_i) on ONE persistent gemm4p launch (the tiles of every item share
+    the grid): a / b are [batch, ., .] with unit inner stride, layouts as ``gemm_p``. Batch strides
+    may be 0 (a broadcast operand)."""
+    assert a.dim() == 3 and b.dim() == 3 and a.shape[0] == b.shape[0]
+    assert a.stride(2) == 1 and b.stride(2) == 1
+    Bn = a.shape[0]
+    M, Ka = (a.shape[2], a.shape[1]) if a_kouter else (a.shape[1], a.shape[2])
+    N, Kb = (b.shape[2], b.shape[1]) if b_kouter else (b.shape[1], b.shape[2])
+    assert Ka == Kb
+    assert (a_kouter, b_kouter, trans_out) in ((False, False, False), (True, True, False), (True, False, True))
+    OM, ON = (N, M) if trans_out else (M, N)
+    c = torch.empty(Bn, OM, ON, dtype=a.dtype, device=a.device)
+    epi = _epi_default(a_kouter, b_kouter, trans_out, Ka)
+    rc = _L().pha_gemm4p_batched(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(1), b.stride(1),
+                                 c.stride(1), int(a_kouter), int(b_kouter), int(trans_out), epi, None,
+                                 _num_cus(a.device), 0, None, 1, _stream(a), None, Bn, a.stride(0), b.stride(0),
+                                 c.stride(0))
+    if rc != 0:
+        raise RuntimeError(f"pha_gemm4p_batched failed ({rc}) batch={Bn} M={M} N={N} K={Ka}")
+    return c
+
+
+def _bmm_ok(t):
+    """a [batch, R, C] view the batched kernel reads directly: unit stride on one of the two inner
+    dims, 16-B aligned rows and batch offsets, 32-bit tile offsets"""
+    if not (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 3 and t.data_ptr() % 16 == 0):
+        return False
+    s0, s1, s2 = t.stride()
+    ld = s1 if s2 == 1 else (s2 if s1 == 1 else -1)
+    return ld > 0 and ld % 8 == 0 and s0 % 8 == 0 and s0 >= 0 and ld * 256 * 2 < 2 ** 32
+
+
+def bmm_own(a, b):
+    """C [batch, M, N] = a [batch, M, K] @ b [batch, K, N] on the batched own kernel, each operand
+    row-major or transposed (column-major) in its last two dims; None when the operands do not fit
+    (K % 64, M / N % 8, strides)"""
+    Bn, M, K = a.shape
+    N = b.shape[2]
+    if K % 64 or M % 8 or N % 8 or not (_bmm_ok(a) and _bmm_ok(b)) or not _lib.native_available():
+        return None
+    a_row, b_row = a.stride(2) == 1, b.stride(2) == 1
+    if a_row and b_row:        # NN: C^T = B^T A^T through the transposed store
+        return bmm_p(b, a, True, False, trans_out=True)
+    if a_row:                  # b^T [N, K] row-major: NT
+        return bmm_p(a, b.transpose(1, 2), False, False)
+    if b_row:                  # a^T [K, M] row-major: TN
+        return bmm_p(a.transpose(1, 2), b, True, True)
+    # both transposed: C^T = B^T A^T as NN on the row-major views
+    return bmm_p(a.transpose(1, 2), b.transpose(1, 2), True, False, trans_out=True).transpose(1, 2)
+
+
+class _BMM(torch.autograd.Function):
+    """C = A @ B per batch item; dA = dC B^T, dB = A^T dC (transposed views, no copies)"""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return bmm_own(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g if g.stride(2) == 1 or g.stride(1) == 1 else g.contiguous()
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = bmm_own(g, b.transpose(1, 2))
+            if da is None:
+                da = torch.bmm(g, b.transpose(1, 2))
+        if ctx.needs_input_grad[1]:
+            db = bmm_own(a.transpose(1, 2), g)
+            if db is None:
+                db = torch.bmm(a.transpose(1, 2), g)
+        return da, db
+
+
+def _bmm_fits(x3, y3):
+    return (x3.dim() == 3 and y3.dim() == 3 and x3.shape[2] % 64 == 0 and x3.shape[1] % 8 == 0
+            and y3.shape[2] % 8 == 0 and _bmm_ok(x3) and _bmm_ok(y3))
 
 
 def _auto_own_nt(N, K):
@@ -505,6 +596,18 @@ def matmul(a, b, transpose_a=False, transpose_b=False):
         a2 = _c(a.reshape(-1, a.shape[-1]))
         out = _NT.apply(a2, _c(b)) if transpose_b else _NN.apply(a2, _c(b))
         return out.reshape(*lead, out.shape[-1])
+    if _gemm_dtype_ok(a, b) and a.dim() >= 3 and b.dim() >= 3 and _impl() != "library":
+        # batched right operands: one persistent launch over every item's tiles (broadcast batch
+        # dims as stride-0 views, no copies)
+        x = a.transpose(-1, -2) if transpose_a else a
+        y = b.transpose(-1, -2) if transpose_b else b
+        lead = torch.broadcast_shapes(x.shape[:-2], y.shape[:-2])
+        xe, ye = x.expand(*lead, *x.shape[-2:]), y.expand(*lead, *y.shape[-2:])
+        x3 = xe.reshape(-1, *x.shape[-2:]) if xe.dim() != 3 else xe
+        y3 = ye.reshape(-1, *y.shape[-2:]) if ye.dim() != 3 else ye
+        if _bmm_fits(x3, y3):
+            out = _BMM.apply(x3, y3)
+            return out.reshape(*lead, *out.shape[-2:])
     if _f32_ok(a, b) and a.dim() >= 2 and b.dim() == 2 and (a.dim() == 2 or not transpose_a):
         x = a.transpose(-1, -2) if transpose_a else a
         y = b.transpose(-1, -2) if transpose_b else b

@@ -430,8 +430,80 @@ def _edit_distance(kw):
         "normalized": bool(kw.get("normalized", True))}, {}
 
 
+def _pair(v, n=2):
+    if isinstance(v, int) and not isinstance(v, bool):
+        return [v] * n
+    if _ints(v) and len(v) == n:
+        return list(v)
+    raise ValueError(v)
+
+
+def _paddings(p):
+    """(paddings, padding_algorithm) of conv_op.cc / pool_op.cc from a 2.x ``padding`` argument"""
+    if isinstance(p, str):
+        return [0, 0], p.upper()
+    if isinstance(p, int) and not isinstance(p, bool):
+        return [p, p], "EXPLICIT"
+    if _ints(p) and len(p) in (2, 4):
+        return list(p), "EXPLICIT"
+    if isinstance(p, (list, tuple)) and len(p) == 4 and all(_ints(q) and len(q) == 2 for q in p):
+        return [x for q in p[2:] for x in q], "EXPLICIT"   # NCHW pairs: the spatial two
+    raise ValueError(p)
+
+
+def _conv2d(kw):
+    """conv_op.cc: strides / paddings / dilations as INTS (2.x F.conv2d's static branch)"""
+    if not (_is_t(kw.get("x")) and _is_t(kw.get("weight"))):
+        return None
+    pads, algo = _paddings(kw.get("padding", 0))
+    slots = {"x": "Input", "weight": "Filter"}
+    if _is_t(kw.get("bias")):
+        slots["bias"] = "Bias"
+    groups = int(kw.get("groups", 1))
+    w = kw["weight"]
+    depthwise = groups > 1 and groups == int(w._t.shape[0]) and int(w._t.shape[1]) == 1
+    return "depthwise_conv2d" if depthwise else "conv2d", slots, "Output", {
+        "strides": _pair(kw.get("stride", 1)), "paddings": pads, "padding_algorithm": algo,
+        "dilations": _pair(kw.get("dilation", 1)), "groups": groups,
+        "data_format": kw.get("data_format", "NCHW"), "use_cudnn": True}, {}
+
+
+def _pool2d(kind):
+    def emit(kw):
+        if not _is_t(kw.get("x")) or kw.get("return_mask") or kw.get("divisor_override"):
+            return None
+        k = _pair(kw["kernel_size"])
+        st = kw.get("stride")
+        pads, algo = _paddings(kw.get("padding", 0))
+        return "pool2d", {"x": "X"}, "Out", {
+            "pooling_type": kind, "ksize": k, "strides": k if st is None else _pair(st), "paddings": pads,
+            "padding_algorithm": algo, "global_pooling": False, "adaptive": False,
+            "ceil_mode": bool(kw.get("ceil_mode", False)), "exclusive": bool(kw.get("exclusive", True)),
+            "data_format": kw.get("data_format", "NCHW"), "use_cudnn": True}, {}
+    return emit
+
+
+def _adaptive_pool2d(kind):
+    def emit(kw):
+        if not _is_t(kw.get("x")) or kw.get("return_mask"):
+            return None
+        os_ = kw["output_size"]
+        if isinstance(os_, (list, tuple)) and any(o is None for o in os_):
+            return None
+        return "pool2d", {"x": "X"}, "Out", {
+            "pooling_type": kind, "ksize": _pair(os_), "strides": [1, 1], "paddings": [0, 0],
+            "padding_algorithm": "EXPLICIT", "global_pooling": False, "adaptive": True, "ceil_mode": False,
+            "exclusive": True, "data_format": kw.get("data_format", "NCHW"), "use_cudnn": True}, {}
+    return emit
+
+
 _Q = "nn.quant.ops."
 EMIT = {
+    "nn.functional.conv.conv2d": _conv2d,
+    "nn.functional.pooling.max_pool2d": _pool2d("max"),
+    "nn.functional.pooling.avg_pool2d": _pool2d("avg"),
+    "nn.functional.pooling.adaptive_avg_pool2d": _adaptive_pool2d("avg"),
+    "nn.functional.pooling.adaptive_max_pool2d": _adaptive_pool2d("max"),
     "fluid.layers.loss.edit_distance": _edit_distance,
     "tensor.manipulation.nonzero": _nonzero,
     "tensor.manipulation.masked_select": _masked_select,

@@ -110,6 +110,19 @@ def _derived_attrs(short, kw):
     """reference attributes computed from our arguments (not a renaming)"""
     if short in ("nn.functional.norm.batch_norm", "nn.functional.norm.batch_norm_act"):
         return {"is_test": not kw.get("training", False)}
+    x = kw.get("x")
+    rank = x._t.dim() if isinstance(x, Tensor) else None
+    if short == "nn.functional.common.linear" and rank:
+        # fc_op.cc: the leading in_num_col_dims dims are rows (a [B, S, H] input: 2)
+        return {"in_num_col_dims": rank - 1, "activation_type": ""}
+    if short == "nn.functional.norm.layer_norm" and rank:
+        ns = kw.get("normalized_shape")
+        n = 1 if isinstance(ns, int) else len(ns or [1])
+        return {"begin_norm_axis": rank - n}
+    if short == "nn.functional.common.dropout":
+        mode = kw.get("mode", "upscale_in_train")
+        return {"is_test": not kw.get("training", True),
+                "dropout_implementation": "upscale_in_train" if mode == "upscale_in_train" else "downgrade_in_infer"}
     return {}
 
 

@@ -17,7 +17,10 @@ from ...ops import conv_gemm as _conv_gemm
 def _bn_act(bn, x, residual=None, relu=True):
     """bn(x) (+ residual) (+ relu) as ONE fused pass when ``bn`` is a plain BatchNorm layer
     (the reference's fuse_bn_add_act_ops pass, done eagerly); otherwise the unfused ops."""
-    if type(bn) in (nn.BatchNorm2D, nn.BatchNorm) and getattr(bn, "_act", None) is None:
+    from ...framework.core import _mode
+    # static Programs (jit.save / to_static) record the reference's separate batch_norm /
+    # elementwise_add / relu ops — what a saved inference model holds
+    if type(bn) in (nn.BatchNorm2D, nn.BatchNorm) and getattr(bn, "_act", None) is None and not _mode.static:
         return F.batch_norm_act(x, bn._mean, bn._variance, bn.weight, bn.bias, bn.training, bn._momentum,
                                 bn._epsilon, bn._data_format, bn._use_global_stats, residual=residual,
                                 act="relu" if relu else None)

@@ -166,8 +166,9 @@ def test_fp32_split_extremes():
     torch.manual_seed(3)
     t = torch.tensor([1.0, 3.39e38, -3.39e38, float("inf"), float("-inf"), float("nan"), 1e-3, 123.456] * 2,
                      device="cuda")
-    s = conv_gemm.split3(t, 0, "hl").float()
-    hi, lo = s[:16], s[16:]
+    s = conv_gemm.split3(t, 0, "hlh").float()   # three parts along dim 0: hi, lo, hi
+    hi, lo = s[:16], s[16:32]
+    torch.testing.assert_close(s[32:], hi, rtol=0, atol=0, equal_nan=True)
     fin = torch.isfinite(t)
     assert torch.isfinite(hi[fin]).all() and torch.isfinite(lo).all()
     rel = ((hi[fin].double() + lo[fin].double() - t[fin].double()).abs() / t[fin].double().abs()).max().item()

@@ -42,8 +42,8 @@ def test_paddle_matmul_own_layouts(ta, tb, M, N, K, monkeypatch):
 
 
 def test_paddle_matmul_batched_left_and_bmm(monkeypatch):
-    """[B, S, K] @ [K, N] flattens into the own kernels; a true bmm (per-batch right operands) is a
-    counted fallback, with the right values"""
+    """[B, S, K] @ [K, N] flattens into the own kernels; a true bmm (per-batch right operands) runs
+    on the batched own kernel (gemm4p batched mode, no fallback), with the right values"""
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.ops import fallback
     monkeypatch.setenv("PHA_GEMM_IMPL", "own")
@@ -55,7 +55,7 @@ def test_paddle_matmul_batched_left_and_bmm(monkeypatch):
     torch.testing.assert_close(out._t.float(), a.float() @ w.float(), atol=0.05, rtol=0.02)
     b3 = _r(3, 64, 16)
     out = paddle.bmm(paddle.to_tensor(a), paddle.to_tensor(b3))
-    assert fallback.counts().get("matmul", 0) == 1
+    assert fallback.total() == 0
     torch.testing.assert_close(out._t.float(), a.float() @ b3.float(), atol=0.05, rtol=0.02)
     lin = paddle.nn.functional.linear(paddle.to_tensor(a), paddle.to_tensor(w))
     torch.testing.assert_close(lin._t.float(), a.float() @ w.float(), atol=0.05, rtol=0.02)
