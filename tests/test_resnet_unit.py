@@ -19,20 +19,38 @@ def _ref(u, x, z, fmt, mode, gy=None):
         if fmt == "NHWC":
             t, w = t.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2)
         return torch.nn.functional.conv2d(t, w, stride=s, padding=u._padding)
-    xt = x._t.detach().double().requires_grad_()
-    fx = u.filter_x._t.detach().double().requires_grad_()
+    def leaf(p):
+        return p._t.detach().double().requires_grad_()
+
+    def affine(t, sc, bi):
+        return t * sc.reshape(1, -1, 1, 1) + bi.reshape(1, -1, 1, 1)
+    xt, fx, sx, bx = leaf(x), leaf(u.filter_x), leaf(u.scale_x), leaf(u.bias_x)
     c = conv(xt, fx, u._stride)
-    out = _bn(c)
+    out = affine(_bn(c), sx, bx)
+    grads = {"filter_x": fx, "scale_x": sx, "bias_x": bx}
     if mode == "add":
         zt = z._t.detach().double()
         out = out + (zt.permute(0, 3, 1, 2) if fmt == "NHWC" else zt)
     if mode == "short":
-        out = out + _bn(conv(z._t.detach().double(), u.filter_z._t.detach().double(), u._stride_z))
+        fz, sz, bz = leaf(u.filter_z), leaf(u.scale_z), leaf(u.bias_z)
+        grads.update(filter_z=fz, scale_z=sz, bias_z=bz)
+        out = out + affine(_bn(conv(z._t.detach().double(), fz, u._stride_z)), sz, bz)
     out = torch.relu(out)
     if fmt == "NHWC":
         out = out.permute(0, 2, 3, 1)
     out.backward(torch.ones_like(out) if gy is None else gy.double().to(out.device))
+    _ref.param_grads = {k: v.grad for k, v in grads.items()}
     return out, xt.grad, fx.grad, c.detach().mean((0, 2, 3))
+
+
+def _check_param_grads(u, tol):
+    """filter and BN scale / bias gradients against the fp64 oracle (relative, in norm)"""
+    for name, ref in _ref.param_grads.items():
+        g = getattr(u, name).grad
+        assert g is not None, name
+        r = ref.to(g._t.device)
+        err = ((g._t.double() - r).norm() / r.norm().clamp_min(1e-30)).item()
+        assert err < tol, (name, err)
 
 
 @pytest.mark.parametrize("fmt", ["NHWC", "NCHW"])
@@ -56,6 +74,7 @@ def test_resnet_unit_matches_conv_bn_add_relu(fmt, mode):
     np.testing.assert_allclose(y.numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(x.grad.numpy(), gx.numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(u.filter_x.grad.numpy(), gw.numpy(), rtol=1e-4, atol=1e-4)
+    _check_param_grads(u, 1e-5)
     # running mean moved by (1 - momentum) of the batch mean
     np.testing.assert_allclose(u.mean_x.numpy().reshape(-1), 0.1 * mean.numpy(), rtol=1e-4, atol=1e-6)
     u.eval()
@@ -122,6 +141,8 @@ def test_resnet_unit_gpu_bf16_nhwc(mode):
         # same unit lands at 2.1 % from the fp64 oracle too (plain: 0.2 %)
         gxd = gx.to(y._t.device)
         assert ((x.grad._t.double() - gxd).norm() / gxd.norm()).item() < (4e-2 if short else 1e-2)
+        # filter gradients (bf16 wgrad GEMM over bf16 dY) and BN scale / bias gradients (fp32)
+        _check_param_grads(u, 4e-2 if short else 1.5e-2)
     finally:
         paddle.set_device("cpu")
 
