@@ -17,7 +17,9 @@ LAMB over ONE flat fp32 buffer of all parameters (each parameter's slot aligned 
   4. the updated shards are ALL-GATHERED and copied back into the parameters.
 
 One reduce-scatter, two small all-reduces and one all-gather per step — on xGMI the two large
-collectives are bandwidth-optimal rings over the flat buffer. Single-process it is exactly
+collectives are bandwidth-optimal rings over the flat buffer. On the GPU steps 2-3 are three HIP
+kernels (csrc/kernels/lamb.hip: gradient square sum; clip + moments + direction + per-parameter
+norm sums; trust-ratio update), the clip scale and trust ratios staying on the device. Single-process it is exactly
 ``optimizer.Lamb`` (tests/test_distributed_fused_lamb.py checks 2 gloo ranks against it). Works in
 dygraph and in static programs (the static optimizer op steps the optimizer)."""
 from __future__ import annotations
@@ -81,7 +83,10 @@ class DistributedFusedLamb(Lamb):
             master[o:o + n] = (m._t if m is not None else p._t).detach().reshape(-1).float()
         wd = torch.tensor([0.0 if (self._exclude is not None and self._exclude(p)) else float(self._wd)
                            for p in params] + [0.0], dtype=torch.float32, device=dev)
+        lr_ratio = torch.tensor([self._lr_ratio(p, self._param_groups[0]) for p in params] + [1.0],
+                                dtype=torch.float32, device=dev)
         self._flat = dict(params=list(params), ids=[id(p) for p in params], offs=offs, total=total, shard=shard,
+                          pid32=pid[lo:lo + shard].to(torch.int32).contiguous(), lr_ratio=lr_ratio,
                           lo=lo, world=world, rank=rank, pid=pid[lo:lo + shard].contiguous(),
                           master=master[lo:lo + shard].clone(), m1=torch.zeros(shard, device=dev),
                           m2=torch.zeros(shard, device=dev), wd=wd,
@@ -123,6 +128,74 @@ class DistributedFusedLamb(Lamb):
                 g.div_(world)
         else:
             g = flat_g
+        if self._fused_ok(dev):
+            self._fused_update(F, g, world, clip)
+        else:
+            self._torch_update(F, g, world, clip)
+        if world > 1:
+            full = torch.empty(F["total"], dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(full, F["master"])
+        else:
+            full = F["master"]
+        with torch.no_grad():
+            for p, o in zip(F["params"], F["offs"]):
+                n = p._t.numel()
+                v = full[o:o + n].view(p._t.shape)
+                m = self._master(p)
+                if m is not None:
+                    m._t.copy_(v)
+                p._t.copy_(v.to(p._t.dtype))
+        self._step_count += 1
+
+    @staticmethod
+    def _fused_ok(dev):
+        from ...ops import _lib
+        return dev.type == "cuda" and _lib.native_available()
+
+    def _fused_update(self, F, g, world, clip):
+        """steps 2-3 as the lamb.hip kernels (clip scale, trust ratios and lr stay on the device)"""
+        from ctypes import c_float, c_int, c_long, c_void_p
+        from ...ops import _lib
+        L = _lib._load()
+        if not getattr(L, "_lamb_sig", False):
+            P = c_void_p
+            L.pha_lamb_sq.argtypes = [P, c_long, P, P, P]
+            L.pha_lamb_moment.argtypes = [P, P, P, P, P, P, P, c_int, c_long] + [c_float] * 7 + [P, P]
+            L.pha_lamb_apply.argtypes = [P, P, P, P, P, c_int, c_long, c_float, P, P]
+            L._lamb_sig = True
+        dev = g.device
+        st = c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        ptr = lambda t: c_void_p(0 if t is None else t.data_ptr())   # noqa: E731
+        n = F["shard"]
+        g = g.contiguous()
+        gsq = None
+        if clip > 0 and self._clip_after_allreduce:
+            part = torch.empty(8192, dtype=torch.float32, device=dev)
+            gsq = torch.empty(1, dtype=torch.float32, device=dev)
+            rc = L.pha_lamb_sq(ptr(g), n, ptr(part), ptr(gsq), st)
+            if rc:
+                raise RuntimeError(f"pha_lamb_sq failed ({rc})")
+            if world > 1:
+                dist.all_reduce(gsq)
+        b1, b2 = self._beta1, self._beta2
+        F["b1p"] *= b1
+        F["b2p"] *= b2
+        npar = len(F["params"]) + 1
+        norms = torch.zeros(2, npar, dtype=torch.float32, device=dev)
+        rc = L.pha_lamb_moment(ptr(g), ptr(F["m1"]), ptr(F["m2"]), ptr(F["master"]), ptr(F["pid32"]), ptr(F["wd"]),
+                               ptr(norms), npar, n, b1, b2, 1 - F["b1p"], 1 - F["b2p"], self._epsilon, 1.0,
+                               clip if gsq is not None else 0.0, ptr(gsq), st)
+        if rc:
+            raise RuntimeError(f"pha_lamb_moment failed ({rc})")
+        if world > 1:
+            dist.all_reduce(norms)
+        rc = L.pha_lamb_apply(ptr(F["master"]), ptr(g), ptr(F["pid32"]), ptr(norms), ptr(F["lr_ratio"]), npar, n,
+                              float(self.get_lr()), None, st)
+        if rc:
+            raise RuntimeError(f"pha_lamb_apply failed ({rc})")
+
+    def _torch_update(self, F, g, world, clip):
+        dev = g.device
         if clip > 0 and self._clip_after_allreduce:
             sq = g.square().sum().reshape(1)
             if world > 1:
@@ -145,23 +218,7 @@ class DistributedFusedLamb(Lamb):
         wn, rn = norms[0].sqrt(), norms[1].sqrt()
         trust = torch.where((wn > 0) & (rn > 0), wn / rn.clamp_min(1e-30), torch.ones_like(wn))
         lr = float(self.get_lr())
-        ratio = torch.tensor([self._lr_ratio(p, self._param_groups[0]) for p in F["params"]] + [1.0],
-                             dtype=torch.float32, device=dev)
-        w.sub_(lr * (ratio * trust)[pid] * r)
-        if world > 1:
-            full = torch.empty(F["total"], dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(full, w)
-        else:
-            full = w
-        with torch.no_grad():
-            for p, o in zip(F["params"], F["offs"]):
-                n = p._t.numel()
-                v = full[o:o + n].view(p._t.shape)
-                m = self._master(p)
-                if m is not None:
-                    m._t.copy_(v)
-                p._t.copy_(v.to(p._t.dtype))
-        self._step_count += 1
+        w.sub_(lr * (F["lr_ratio"] * trust)[pid] * r)
 
     # ---------------------------------------------------------------------------------- state
     def state_dict(self):

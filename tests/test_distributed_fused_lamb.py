@@ -3,6 +3,7 @@ ranks (reduce-scatter of gradients, all-reduced per-parameter LAMB norms, all-ga
 updated shards). One process: identical to optimizer.Lamb. Two gloo ranks, each with half of a
 batch: identical to one process on the whole batch (gradients averaged)."""
 import numpy as np
+import pytest
 import torch
 
 import paddle_hackathon_amd as paddle
@@ -129,3 +130,26 @@ def test_state_dict_resume_before_first_step():
     assert o_b._step_count == 4
     for a, b in zip(m_b.parameters(), m_ref.parameters()):
         np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("clip", [None, 0.05])
+def test_fused_kernels_match_torch_path(clip, monkeypatch):
+    """the lamb.hip kernels (device clip scale, per-parameter norm atomics) against the torch
+    sequence on the same GPU, several steps, with and without global-norm clipping"""
+    from paddle_hackathon_amd.incubate import DistributedFusedLamb
+    from paddle_hackathon_amd.nn.clip import ClipGradByGlobalNorm
+    paddle.set_device("gpu")
+    try:
+        x, y = _data()
+        res = {}
+        for fused in (True, False):
+            monkeypatch.setattr(DistributedFusedLamb, "_fused_ok", staticmethod(lambda dev, f=fused: f))
+            res[fused] = _train(lambda ps: DistributedFusedLamb(
+                0.01, 0.05, parameters=ps, exclude_from_weight_decay_fn=lambda p: p.ndim == 1,
+                grad_clip=ClipGradByGlobalNorm(clip) if clip else None), x, y, steps=4)
+        for a, b in zip(res[True], res[False]):
+            np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+        assert torch.cuda.is_available()
+    finally:
+        paddle.set_device("cpu")

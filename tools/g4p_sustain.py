@@ -2,6 +2,7 @@
 variant runs back to back for ~1.5 s on model-like data (weights N(0, 0.02), unit-variance
 activations); the reported time is the mean of the last second. Own gemm4p (LV 0 / 8) vs hipBLASLt.
 python tools/g4p_sustain.py"""
+import os
 import sys
 import time
 
@@ -13,7 +14,12 @@ from paddle_hackathon_amd.ops import gemm as G  # noqa: E402
 T = 32768
 
 
-def sustain(fn, secs=1.5, tail=1.0):
+SECS = float(os.environ.get("SUSTAIN_SECS", "1.5"))
+SHAPES = os.environ.get("SHAPES")
+
+
+def sustain(fn, secs=SECS, tail=None):
+    tail = secs * 2 / 3 if tail is None else tail
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     n = 0
@@ -37,6 +43,8 @@ def main():
     tot = {}
     for name, N, K in (("fc2 fwd", 2048, 8192), ("qkv dX", 2048, 6144), ("qkv fwd", 6144, 2048),
                        ("out fwd", 2048, 2048), ("fc2 dX", 8192, 2048)):
+        if SHAPES and name not in SHAPES.split(","):
+            continue
         x = torch.randn(T, K, device="cuda").bfloat16()
         wt = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
         b = torch.randn(N, device="cuda") * 0.02
