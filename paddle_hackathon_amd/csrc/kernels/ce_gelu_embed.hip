@@ -379,8 +379,12 @@ template <> __device__ __forceinline__ void ld4<float>(const float* p, float (&o
 }
 
 template <typename T>
+// Token chunks (grid.z, `chunk` tokens each, ws != null): a small vocabulary (token types, positions)
+// leaves too few (row, column) blocks to fill the chip — each chunk then writes fp32 partial rows to
+// ws[z] and chunk_sum_kernel adds the chunks in order (still deterministic).
 __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __restrict__ ids, const T* __restrict__ gy,
-                                                            T* __restrict__ gw, long n, int D, long V, long pad) {
+                                                            T* __restrict__ gw, long n, int D, long V, long pad,
+                                                            long chunk, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) unsigned char eb_smem[];
   float* acc = reinterpret_cast<float*>(eb_smem);                       // [EB_ROWS][EB_DCH]
   int* list = reinterpret_cast<int*>(eb_smem + EB_ROWS * EB_DCH * 4);   // [EB_CAP]
@@ -408,9 +412,10 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
     __syncthreads();
     cnt = 0;
   };
-  for (long base = 0; base < n; base += 256) {
+  const long t0 = (long)blockIdx.z * chunk, t1 = min(n, t0 + chunk);
+  for (long base = t0; base < t1; base += 256) {
     const long r = base + tid;
-    const long id = r < n ? ids[r] : -1;
+    const long id = r < t1 ? ids[r] : -1;
     const bool m = id >= v0 && id < v0 + EB_ROWS && id < V && id != pad;
     const unsigned long long bal = __ballot(m);
     const int pre = __popcll(bal & ((1ULL << lane) - 1ULL));
@@ -435,6 +440,10 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
       const long v = v0 + row;
       if (v >= V) break;
       const float* a = acc + row * EB_DCH + c;
+      if (ws) {
+        *reinterpret_cast<float4*>(ws + ((long)blockIdx.z * V + v) * D + d0 + c) = make_float4(a[0], a[1], a[2], a[3]);
+        continue;
+      }
       T* o = gw + v * D + d0 + c;
 #pragma unroll
       for (int q = 0; q < 4; ++q) Cvt<T>::st(o, q, a[q]);
@@ -544,12 +553,32 @@ PHA_API int pha_maxpool2d_nhwc_bwd(int dt, const void* gy, const uint8_t* idx, v
   return (int)hipGetLastError();
 }
 
-// gw [V][D] (T) = embedding gradient of gy [n][D] (T) for ids [n] (int64); padding row pad (or -1)
+// out[i] = sum_z ws[z][i] in chunk order (4 per thread)
+template <typename T>
+__global__ __launch_bounds__(256) void chunk_sum_kernel(const float* __restrict__ ws, T* __restrict__ out, int Z, long len) {
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < len; i += (long)gridDim.x * 1024) {
+    float4 s = *reinterpret_cast<const float4*>(ws + i);
+    for (int z = 1; z < Z; ++z) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + (long)z * len + i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    Cvt<T>::st(out + i, 0, s.x);
+    Cvt<T>::st(out + i, 1, s.y);
+    Cvt<T>::st(out + i, 2, s.z);
+    Cvt<T>::st(out + i, 3, s.w);
+  }
+}
+
+// gw [V][D] (T) = embedding gradient of gy [n][D] (T) for ids [n] (int64); padding row pad (or -1).
+// chunks > 1: token ranges of ceil(n / chunks) per grid.z slice with fp32 partials in ws
+// ([chunks][V][D] floats), summed in order into gw.
 PHA_API int pha_embedding_bwd(int dt, const int64_t* ids, const void* gy, void* gw, long n, int D, long V, long pad,
-                              hipStream_t stream) {
+                              hipStream_t stream, int chunks, float* ws) {
   if (n <= 0 || D <= 0 || V <= 0) return (int)hipErrorInvalidValue;
   if (D % 4 || n >= (1L << 26)) return (int)hipErrorInvalidValue;
-  const dim3 grid((unsigned)((V + EB_ROWS - 1) / EB_ROWS), (unsigned)((D + EB_DCH - 1) / EB_DCH));
+  if (chunks < 1 || (chunks > 1 && !ws) || chunks > 65535) return (int)hipErrorInvalidValue;
+  const long chunk = (n + chunks - 1) / chunks;
+  const dim3 grid((unsigned)((V + EB_ROWS - 1) / EB_ROWS), (unsigned)((D + EB_DCH - 1) / EB_DCH), (unsigned)chunks);
   const size_t lds = (size_t)EB_ROWS * EB_DCH * 4 + EB_CAP * 4 + 16;
   PHA_DISPATCH_T(dt, T, {
     static bool attr = false;
@@ -557,7 +586,13 @@ PHA_API int pha_embedding_bwd(int dt, const int64_t* ids, const void* gy, void* 
       hipFuncSetAttribute((const void*)embedding_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr = true;
     }
-    hipLaunchKernelGGL(embedding_bwd_kernel<T>, grid, dim3(256), lds, stream, ids, (const T*)gy, (T*)gw, n, D, V, pad);
+    hipLaunchKernelGGL(embedding_bwd_kernel<T>, grid, dim3(256), lds, stream, ids, (const T*)gy, (T*)gw, n, D, V, pad,
+                       chunk, chunks > 1 ? ws : nullptr);
+    if (chunks > 1) {
+      const long len = V * (long)D;
+      const unsigned g = (unsigned)std::min((len / 4 + 255) / 256, 8192L);
+      hipLaunchKernelGGL(chunk_sum_kernel<T>, dim3(g), dim3(256), 0, stream, ws, (T*)gw, chunks, len);
+    }
   });
   return (int)hipGetLastError();
 }

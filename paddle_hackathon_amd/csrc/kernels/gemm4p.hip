@@ -64,6 +64,10 @@ constexpr int lv_ldma(int lv) { return 8; }
 // between the last read and the release barrier's lgkmcnt(0))
 constexpr bool lv_lord(int lv) { return (lv & 7) == 2 || (lv & 7) == 3 || (lv & 7) == 5; }
 constexpr int lv_rg(int lv, int relg) { return (lv & 7) == 3 ? 6 : (lv & 7) == 5 ? 4 : relg; }
+// LV & 7 == 6 (BURST): phase B's 16 reads two per group over groups 0-7 in consumption order, so the
+// next phase A's first groups never wait on reads issued in phase B's last groups (the counted
+// lgkmcnt waits at the top of every phase in the LV 0 / 8 ISA, profiles/README.md round 5)
+constexpr bool lv_burst(int lv) { return (lv & 7) == 6; }
 
 struct Args {
   const void* a;
@@ -442,6 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int LWG = lv_lwg(LV), LDMA = lv_ldma(LV), LDMB = 16 - LDMA;
   constexpr bool PIN = (LV & 8) != 0;
   constexpr bool LORD = lv_lord(LV);
+  constexpr bool BURST = lv_burst(LV);
   constexpr int LRG = lv_rg(LV, RELG);
   static_assert(LWG == 0 || (LDMB <= LWG && RELG == 8), "late variants: every phase-B DMA before the wait");
 
@@ -574,7 +579,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         }
       } else {
-        if constexpr ((SCHED & 2) && !LORD) {
+        if constexpr (BURST) {
+          if (s < 8) {
+#pragma unroll
+            for (int r = 2 * s; r < 2 * s + 2; ++r) {
+              if (r == 0) na[0] = readA(rbuf, rkh, 0);
+              else if (r <= 8) nb[r - 1] = readB(rbuf, rkh, r - 1);
+              else na[r - 8] = readA(rbuf, rkh, r - 8);
+            }
+          }
+        } else if constexpr ((SCHED & 2) && !LORD) {
           if (s & 1) nb[s >> 1] = readB(rbuf, rkh, s >> 1);
           else na[s >> 1] = readA(rbuf, rkh, s >> 1);
         } else if constexpr (LORD) {
@@ -804,6 +818,8 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
     else if (lv == 10) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 10>), dim3(grid), dim3(256), 0, st, a);
     else if (lv == 11) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 11>), dim3(grid), dim3(256), 0, st, a);
     else if (lv == 13) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 13>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 14) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 14>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 6) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 6>), dim3(grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   }
   else if (ako && bko && !trans)

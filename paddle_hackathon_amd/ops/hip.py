@@ -41,7 +41,7 @@ def _L():
             "pha_bias_gelu_fwd": [I, P, P, P, LG, I, I, P],
             "pha_bias_gelu_bwd": [I, P, P, P, P, LG, I, I, P],
             "pha_embedding_fwd": [P, P, P, LG, I, LG, P],
-            "pha_embedding_bwd": [I, P, P, P, LG, I, LG, LG, P],
+            "pha_embedding_bwd": [I, P, P, P, LG, I, LG, LG, P, I, P],
             "pha_multi_tensor_adam": [I, I, P, P, I, F, F, F, F, F, F, F, I, P, P, P, P, P],
             "pha_multi_tensor_momentum": [I, I, P, P, I, F, F, F, I, P],
             "pha_multi_tensor_l2sq": [P, P, I, P, P, P],
@@ -361,8 +361,16 @@ def embedding_bwd(ids, gy, vocab, padding_idx=None):
     gy2 = gy.reshape(-1, D).contiguous()
     gw = torch.empty(vocab, D, dtype=gy.dtype, device=gy.device)
     pad = -1 if padding_idx is None else int(padding_idx) % vocab
-    _check(_L().pha_embedding_bwd(_DT[gy.dtype], _ptr(ids), _ptr(gy2), _ptr(gw), ids.numel(), D, vocab, pad,
-                                  _stream(gy)), "embedding_bwd")
+    n = ids.numel()
+    # a small vocabulary (token types, positions) gives few (row, column) blocks: split the tokens
+    # into chunks (>= 1024 tokens each) so ~512 blocks stream them, fp32 partials summed in order
+    blocks = -(-vocab // 32) * -(-D // 1024)
+    chunks = 1
+    if blocks < 512 and n >= 2048:
+        chunks = max(1, min(-(-512 // blocks), n // 1024, 65535))
+    ws = torch.empty(chunks, vocab, D, dtype=torch.float32, device=gy.device) if chunks > 1 else None
+    _check(_L().pha_embedding_bwd(_DT[gy.dtype], _ptr(ids), _ptr(gy2), _ptr(gw), n, D, vocab, pad,
+                                  _stream(gy), chunks, _ptr(ws)), "embedding_bwd")
     return gw
 
 

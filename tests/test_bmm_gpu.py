@@ -9,7 +9,15 @@ import paddle_hackathon_amd as paddle
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _on_gpu():
+    paddle.set_device("gpu")
+    yield
+    paddle.set_device("cpu")
+
+
 def _rel(a, b):
+    a = a.to(b.device)
     return ((a.float() - b.float()).norm() / b.float().norm()).item()
 
 

@@ -49,10 +49,9 @@ def main():
         wt = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
         b = torch.randn(N, device="cuda") * 0.02
         fl = 2.0 * T * N * K
-        var = {"lv0": lambda: G.gemm_p(x, wt, bias=b, epi_extra=G.EPI_EARLY),
-               "lv8": lambda: G.gemm_p(x, wt, bias=b, epi_extra=G.EPI_EARLY | (8 << 17)),
-               "lv8nb": lambda: G.gemm_p(x, wt, epi_extra=G.EPI_EARLY | (8 << 17)),
-               "lib": lambda: torch.addmm(b.bfloat16(), x, wt.t())}
+        lvs = [int(v) for v in os.environ.get("LVS", "0,8").split(",")]
+        var = {f"lv{lv}": (lambda lv=lv: G.gemm_p(x, wt, bias=b, epi_extra=G.EPI_EARLY | (lv << 17))) for lv in lvs}
+        var["lib"] = lambda: torch.addmm(b.bfloat16(), x, wt.t())
         res = {}
         for rep in range(2):
             for k, fn in var.items():
