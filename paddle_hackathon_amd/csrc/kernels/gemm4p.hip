@@ -50,6 +50,10 @@ enum : int {
   EPI_RSTAGE = 32768,    // NT: register-staged operands (global_load -> VGPR -> ds_write) instead of LDS-DMA
   EPI_EARLY = 65536,     // early-release schedule (see the EARLY main loop)
   EPI_LATE_SHIFT = 17,   // NT + EARLY, bits 17-20: schedule variant LV (lv_lwg / lv_ldma / PIN)
+  EPI_L2ONLY = 1 << 21,  // measurement only: every DMA re-reads the item's first K-tile (L2-resident
+                         // operands: isolates the main loop from HBM / MALL latency; wrong results)
+  EPI_RING = 1 << 22,    // NT: the 4-slot ring of 32-deep stages (gemm4r_kernel), K % 64 == 0, K >= 128
+  EPI_ADEEP = 1 << 23,   // NT without bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel), K >= 256
 };
 
 // late-wait variants (LV): {LWG = phase-B group of the buffer wait (0: at the A/B boundary),
@@ -265,10 +269,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int st_buf = 0;
   // Past the last tile the cursor stays on the last K-tile: those DMAs land in a buffer nothing
   // reads any more (no branch in the MFMA stream); the kernel drains them before it exits.
+  const bool l2only = (p.epi & EPI_L2ONLY) != 0;
   auto stage_begin = [&](int buf) {
     st_on = sc.valid(rs);
-    st_a = abase + (size_t)(st_on ? ks : nk - 1) * astep;
-    st_b = bbase + (size_t)(st_on ? ks : nk - 1) * bstep;
+    const int kk = l2only ? 0 : (st_on ? ks : nk - 1);
+    st_a = abase + (size_t)kk * astep;
+    st_b = bbase + (size_t)kk * bstep;
     st_buf = buf;
   };
   auto stage_one = [&](int gi) {   // DMA gi (0..15): u = gi >> 1, operand gi & 1
@@ -787,6 +793,534 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   Vec8<T>::st(c + (long)m * ldc + n, acc);
 }
 
+// ================================================================================================
+// RING: the NT main loop on a 4-slot ring of 32-deep K stages (EPI_RING). gemm4p's two 64-deep LDS
+// buffers leave each LDS-DMA 1.5-2.5 MFMA phases of latency cover, and the long-K NT products are
+// latency-bound on the HBM / MALL fetches: the same schedule with L2-resident operands
+// (EPI_L2ONLY) runs at hipBLASLt's speed (profiles/README.md round 5). Here stage q + 4 is DMA'd
+// into slot q % 4 during phase q (one phase = one 32-deep stage = 64 MFMAs per wave) and read
+// during phase q + 3: 2.1-3 phases of cover, one barrier per phase. A stage's operand images are
+// plain [256][32] bf16 rows (64 B): a fragment read (16 rows x 4 chunks) and a DMA piece (16 rows)
+// are both one contiguous KiB, conflict-free without a swizzle.
+//
+// Per phase, at its start: s_waitcnt vmcnt(N) (the stage read in this phase has landed: N = the
+// VMEM ops issued after its DMAs — two phases of DMAs plus the stores of an epilogue phase among
+// them) + lgkmcnt(0) (this wave's reads of the slot about to be overwritten are done) + barrier.
+// Then 16 MFMA groups: DMA d of the cursor stage before even groups, the next stage's 16 fragment
+// reads two per group over groups 0-7, and in a tile's first phase the previous tile's
+// accumulators stored right before the MFMAs that overwrite them (gemm4p's overlapped epilogue).
+// ================================================================================================
+constexpr int R_OPB = 256 * 32 * 2;            // one operand image of a 32-deep stage (16 KiB)
+constexpr int R_STAGE = 2 * R_OPB;             // A image, B image
+constexpr int R_NS = 4;                        // ring slots
+constexpr int R_BIAS_OFF = R_NS * R_STAGE;     // 4 bias slots of 256 fp32 after the ring
+constexpr int R_SMEM = R_BIAS_OFF + 4 * 1024;
+
+template <typename T, bool BIAS, bool GELU>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4r_kernel(Args p) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[R_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nst = K >> 5;   // stages per tile (even, >= 4: the launcher checks)
+
+  Sched sc;
+  sc.tiles_m = (M + 255) >> 8;
+  sc.tiles_n = (N + 255) >> 8;
+  sc.splits = 1;
+  sc.per_batch = sc.tiles_m * sc.tiles_n;
+  sc.total = sc.per_batch * p.batch;
+  sc.G = gridDim.x;
+  sc.gm = p.group_m;
+  {
+    const int bid = blockIdx.x, G = gridDim.x;
+    const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7;
+    sc.pos = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (r8 == 0 && !(p.epi & EPI_ROUNDS)) {
+      const int qt = sc.total >> 3, rt = sc.total & 7;
+      sc.c0 = (xcd < rt ? xcd * (qt + 1) : rt * (qt + 1) + (xcd - rt) * qt) + (bid >> 3);
+      sc.c1 = sc.c0 - (bid >> 3) + qt + (xcd < rt ? 1 : 0);
+      sc.step = q8;
+    } else {
+      sc.c0 = sc.pos;
+      sc.c1 = sc.total;
+      sc.step = G;
+    }
+  }
+  if (!sc.valid(0)) return;
+
+  // ---- DMA cursor: round rs, stage ks; 4 A + 4 B pieces (16 rows x 64 B) per wave and stage ----
+  unsigned aoff[4], boff[4];
+  const char* abase;
+  const char* bbase;
+  int rs = 0, ks = 0;
+  const unsigned lds0 = lds_u32(smem);
+  const bool l2only = (p.epi & EPI_L2ONLY) != 0;
+  auto set_tile = [&](int r) {
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
+    const int m0 = tm << 8, n0 = tn << 8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = (wid * 4 + u) * 16 + (lane >> 2);
+      const int ga = min(m0 + row, M - 1) - m0, gb = min(n0 + row, N - 1) - n0;
+      aoff[u] = ((unsigned)ga * (unsigned)p.lda + (unsigned)((lane & 3) * 8)) * 2u;
+      boff[u] = ((unsigned)gb * (unsigned)p.ldb + (unsigned)((lane & 3) * 8)) * 2u;
+    }
+    abase = static_cast<const char*>(p.a) + (size_t)bi * p.sa * 2 + (size_t)m0 * p.lda * 2;
+    bbase = static_cast<const char*>(p.b) + (size_t)bi * p.sb * 2 + (size_t)n0 * p.ldb * 2;
+    if constexpr (BIAS) {
+      const int col = min(n0 + wid * 64 + lane, N - 1);
+      glds4(p.bias + col, lds0 + R_BIAS_OFF + (r & 3) * 1024 + wid * 256);
+    }
+  };
+  const char* st_a = nullptr;
+  const char* st_b = nullptr;
+  bool st_on = false;
+  int st_slot = 0;
+  auto stage_begin = [&](int slot) {   // past the last tile the cursor repeats its last stage (unread slots)
+    st_on = sc.valid(rs);
+    const int kk = l2only ? 0 : (st_on ? ks : nst - 1);
+    st_a = abase + (size_t)kk * 64;
+    st_b = bbase + (size_t)kk * 64;
+    st_slot = slot;
+  };
+  auto stage_one = [&](int d) {   // d = 0..7: piece d >> 1 of operand d & 1
+    const int u = d >> 1;
+    const unsigned dst = lds0 + st_slot * R_STAGE + (d & 1) * R_OPB + (wid * 4 + u) * 1024;
+    if (d & 1) glds_sv(boff[u], st_b, dst);
+    else glds_sv(aoff[u], st_a, dst);
+  };
+  auto stage_end = [&]() {
+    if (!st_on) return;
+    if (++ks == nst) {
+      ks = 0;
+      ++rs;
+      if (sc.valid(rs)) set_tile(rs);
+    }
+  };
+
+  const int fr = lane & 15, fk = lane >> 4;
+  auto readA = [&](int slot, int i) -> uint4 {
+    return *reinterpret_cast<const uint4*>(smem + slot * R_STAGE + (wr * 128 + i * 16 + fr) * 64 + fk * 16);
+  };
+  auto readB = [&](int slot, int j) -> uint4 {
+    return *reinterpret_cast<const uint4*>(smem + slot * R_STAGE + R_OPB + (wc * 128 + j * 16 + fr) * 64 + fk * 16);
+  };
+
+  // ---- epilogue geometry (gemm4p's non-OT layout) ------------------------------------------------
+  const int ldc2 = p.ldc * 2;
+  const int wrow = wr * 128;
+  const int lcol = wc * 128 + (fk & 1) * 16 + (fk >> 1) * 8;
+  const unsigned lane_voff = (unsigned)(fr * ldc2 + lcol * 2);
+  const char* e_base = static_cast<const char*>(p.c);
+  const char* e_aux = static_cast<const char*>(p.aux);
+  int e_rows = 0, e_cols = 0, e_slot = 0;
+  auto set_epi = [&](int r) {
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
+    const int r0 = tm << 8, c0 = tn << 8;
+    e_slot = r & 3;
+    e_base = static_cast<const char*>(p.c) + (size_t)bi * p.sc * 2 + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    if constexpr (GELU) e_aux = static_cast<const char*>(p.aux) + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    e_rows = (p.epi & EPI_NOSTORE) ? 0 : M - r0 - wrow;
+    e_cols = N - c0;
+  };
+  auto store_pair = [&](const f32x4& x0, const f32x4& x1, int rb, int cb) {
+    float v0[4], v1[4];
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v0[0]), "=v"(v0[1]), "=v"(v0[2]), "=v"(v0[3]) : "a"(x0[0]), "a"(x0[1]), "a"(x0[2]), "a"(x0[3]));
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v1[0]), "=v"(v1[1]), "=v"(v1[2]), "=v"(v1[3]) : "a"(x1[0]), "a"(x1[1]), "a"(x1[2]), "a"(x1[3]));
+    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
+    const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    auto pack_swap = [&](const float (&a)[4], const float (&b)[4]) {
+      unsigned q00 = pk<T>(a[0], a[1]), q01 = pk<T>(a[2], a[3]);
+      unsigned q10 = pk<T>(b[0], b[1]), q11 = pk<T>(b[2], b[3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(q00, q10, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(q01, q11, false, false);
+      return u32x4{s0[0], s1[0], s0[1], s1[1]};
+    };
+    auto rsrc = [&](const char* base) {
+      const size_t bp = (size_t)(base + (size_t)rb * 16 * ldc2);
+      const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+      const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+      return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0, nbytes,
+                                               0x00020000);
+    };
+    if constexpr (GELU) __builtin_amdgcn_raw_buffer_store_b128(pack_swap(v0, v1), rsrc(e_aux), voff + cb * 32, 0, 2);
+    if constexpr (BIAS) {
+      const unsigned char* bs = smem + R_BIAS_OFF + e_slot * 1024 + wc * 512 + 16 * fk;
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bs + cb * 64);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bs + cb * 64 + 64);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] += b0[e];
+        v1[e] += b1[e];
+      }
+    }
+    if constexpr (GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] = gelu_t(v0[e]);
+        v1[e] = gelu_t(v1[e]);
+      }
+    }
+    const auto rs_ = rsrc(e_base);
+    const u32x4 q = pack_swap(v0, v1);
+    if (p.epi & EPI_TEMPORAL) __builtin_amdgcn_raw_buffer_store_b128(q, rs_, voff + cb * 32, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(q, rs_, voff + cb * 32, 0, 2);
+  };
+
+  f32x4 acc[8][8];
+  uint4 fa0[8], fb0[8], fa1[8], fb1[8];
+  // VMEM ops allowed outstanding at the start of phase kq of a tile: the two phases of DMAs issued
+  // after the needed stage's, plus the stores of an epilogue phase among them (capped at 63:
+  // waiting for more than needed is only slower)
+  constexpr int NSTO = GELU ? 64 : 32;
+  auto phase = [&](auto epi_c, auto nv_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8], uint4 (&nb)[8], int q) {
+    constexpr bool EP = decltype(epi_c)::value;
+    constexpr int NV = decltype(nv_c)::value;
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(NV) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bar();
+    stage_begin(q & 3);
+    const int rslot = (q + 1) & 3;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if ((s & 1) == 0) stage_one(s >> 1);
+      if (s < 8) {
+#pragma unroll
+        for (int r = 2 * s; r < 2 * s + 2; ++r) {   // consumption order: A0, B0-7, A1-7
+          if (r == 0) na[0] = readA(rslot, 0);
+          else if (r <= 8) nb[r - 1] = readB(rslot, r - 1);
+          else na[r - 8] = readA(rslot, r - 8);
+        }
+      }
+      const int i = s >> 1, jb = (s & 1) * 4;
+      if constexpr (EP) {
+        store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+        store_pair(acc[i][jb + 2], acc[i][jb + 3], i, jb + 2);
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int j = jb + qq;
+        if constexpr (EP) mma0<T>(acc[i][j], cb[j], ca[i]);
+        else acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+    }
+    stage_end();
+  };
+  using yes = std::true_type;
+  using no = std::false_type;
+  constexpr int NV_E = 16 + 0;                                  // phase 0: the previous tile's last 3
+  constexpr int NV_1 = 16 + NSTO > 63 ? 63 : 16 + NSTO;         // phase 1: the epilogue phase is in the window
+  constexpr int NV_3 = 16 + 4 * (NSTO / 32);                    // phase 3: its stores after the last DMA
+  using V0 = std::integral_constant<int, NV_E>;
+  using V1 = std::integral_constant<int, NV_1>;
+  using V3 = std::integral_constant<int, NV_3>;
+
+  // ---- prologue: stages 0-3 into slots 0-3, stage 0's fragments -----------------------------------
+  set_tile(0);
+#pragma unroll
+  for (int b = 0; b < R_NS; ++b) {
+    stage_begin(b);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) stage_one(d);
+    stage_end();
+  }
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  bar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa0[i] = readA(0, i);
+    fb0[i] = readB(0, i);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int q = 0;   // global phase = stage index; slot q & 3
+  for (int r = 0; sc.valid(r); ++r) {
+    phase(yes{}, V0{}, fa0, fb0, fa1, fb1, q);   // kq 0: the previous tile written out
+    set_epi(r);
+    phase(no{}, V1{}, fa1, fb1, fa0, fb0, q + 1);
+    phase(no{}, V1{}, fa0, fb0, fa1, fb1, q + 2);
+    phase(no{}, V3{}, fa1, fb1, fa0, fb0, q + 3);
+    q += 4;
+    for (int k = 4; k < nst; k += 2, q += 2) {
+      phase(no{}, V0{}, fa0, fb0, fa1, fb1, q);
+      phase(no{}, V0{}, fa1, fb1, fa0, fb0, q + 1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jb = 0; jb < 8; jb += 2) store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+}
+
+// ================================================================================================
+// A-DEEP (EPI_ADEEP, NT, no bias / GELU yet): gemm4p's early-release schedule with the LDS split
+// 3 : 2 between the operands — three 32 KiB slots for the activation panel A (streamed from HBM)
+// and two for the weight panel B^T (re-read across the chip, mostly L2 / MALL hits): 160 KiB.
+// K-tile t reads A slot t % 3 and B slot t % 2; B of tile t + 2 is DMA'd in phase A(t) after the
+// release barrier, A of tile t + 3 in phase B(t): the A fetches get ~2 K-tiles of latency cover
+// (one in gemm4p), B's 1.25. One counted vmcnt + two barriers per K-tile, as gemm4p.
+// ================================================================================================
+constexpr int AD_SLOT = 256 * 64 * 2;           // 32 KiB operand image of one 64-deep K-tile
+constexpr int AD_B0 = 3 * AD_SLOT;              // B slots after the three A slots
+constexpr int AD_SMEM = 5 * AD_SLOT;            // 160 KiB
+
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4a_kernel(Args p) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[AD_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int M = p.M, N = p.N, K = p.K;
+  const int nk = K >> 6;   // >= 4 (launcher)
+
+  Sched sc;
+  sc.tiles_m = (M + 255) >> 8;
+  sc.tiles_n = (N + 255) >> 8;
+  sc.splits = 1;
+  sc.per_batch = sc.tiles_m * sc.tiles_n;
+  sc.total = sc.per_batch * p.batch;
+  sc.G = gridDim.x;
+  sc.gm = p.group_m;
+  {
+    const int bid = blockIdx.x, G = gridDim.x;
+    const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7;
+    sc.pos = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (r8 == 0 && !(p.epi & EPI_ROUNDS)) {
+      const int qt = sc.total >> 3, rt = sc.total & 7;
+      sc.c0 = (xcd < rt ? xcd * (qt + 1) : rt * (qt + 1) + (xcd - rt) * qt) + (bid >> 3);
+      sc.c1 = sc.c0 - (bid >> 3) + qt + (xcd < rt ? 1 : 0);
+      sc.step = q8;
+    } else {
+      sc.c0 = sc.pos;
+      sc.c1 = sc.total;
+      sc.step = G;
+    }
+  }
+  if (!sc.valid(0)) return;
+
+  const unsigned lds0 = lds_u32(smem);
+  const bool l2only = (p.epi & EPI_L2ONLY) != 0;
+  // two DMA cursors (A three K-tiles ahead, B two): per operand a round, a K-tile, the tile's base
+  // and the lanes' 8 piece offsets (gemm4p's NT geometry: piece g = 8 rows x 128 B, chunk ^ row & 7)
+  struct Cur {
+    int rs, ks;
+    const char* base;
+    unsigned off[8];
+    const char* st;
+    bool on;
+    int slot;
+  };
+  Cur ca_{0, 0, nullptr, {}, nullptr, false, 0}, cb_{0, 0, nullptr, {}, nullptr, false, 0};
+  auto set_tile = [&](Cur& c, bool isA, int r) {
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
+    const int base = isA ? tm << 8 : tn << 8, dim = isA ? M : N, ld = isA ? p.lda : p.ldb;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = (wid * 8 + u) * 8 + (lane >> 3);
+      const int grow = min(base + row, dim - 1) - base;
+      c.off[u] = ((unsigned)grow * (unsigned)ld + (unsigned)(((lane & 7) ^ (row & 7)) * 8)) * 2u;
+    }
+    c.base = static_cast<const char*>(isA ? p.a : p.b) + (size_t)bi * (isA ? p.sa : p.sb) * 2 + (size_t)base * ld * 2;
+  };
+  auto begin = [&](Cur& c, int slot) {
+    c.on = sc.valid(c.rs);
+    const int kk = l2only ? 0 : (c.on ? c.ks : nk - 1);
+    c.st = c.base + (size_t)kk * 128;
+    c.slot = slot;
+  };
+  auto dma = [&](Cur& c, unsigned img0, int u) {
+    glds_sv(c.off[u], c.st, img0 + c.slot * AD_SLOT + (wid * 8 + u) * 1024);
+  };
+  auto end = [&](Cur& c, bool isA) {
+    if (!c.on) return;
+    if (++c.ks == nk) {
+      c.ks = 0;
+      ++c.rs;
+      if (sc.valid(c.rs)) set_tile(c, isA, c.rs);
+    }
+  };
+
+  const int fr = lane & 15, fk = lane >> 4;
+  auto readA = [&](int slot, int kh, int i) -> uint4 {
+    const int row = wr * 128 + i * 16 + fr;
+    return *reinterpret_cast<const uint4*>(smem + slot * AD_SLOT + row * 128 + (((kh * 4 + fk) ^ (fr & 7)) << 4));
+  };
+  auto readB = [&](int slot, int kh, int j) -> uint4 {
+    const int row = wc * 128 + j * 16 + fr;
+    return *reinterpret_cast<const uint4*>(smem + AD_B0 + slot * AD_SLOT + row * 128 + (((kh * 4 + fk) ^ (fr & 7)) << 4));
+  };
+
+  const int ldc2 = p.ldc * 2;
+  const int wrow = wr * 128;
+  const int lcol = wc * 128 + (fk & 1) * 16 + (fk >> 1) * 8;
+  const unsigned lane_voff = (unsigned)(fr * ldc2 + lcol * 2);
+  const char* e_base = static_cast<const char*>(p.c);
+  int e_rows = 0, e_cols = 0;
+  auto set_epi = [&](int r) {
+    int tm, tn, slice, bi;
+    sc.tile(r, tm, tn, slice, bi);
+    const int r0 = tm << 8, c0 = tn << 8;
+    e_base = static_cast<const char*>(p.c) + (size_t)bi * p.sc * 2 + ((size_t)(r0 + wrow) * ldc2 + (size_t)c0 * 2);
+    e_rows = (p.epi & EPI_NOSTORE) ? 0 : M - r0 - wrow;
+    e_cols = N - c0;
+  };
+  auto store_pair = [&](const f32x4& x0, const f32x4& x1, int rb, int cb) {
+    float v0[4], v1[4];
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v0[0]), "=v"(v0[1]), "=v"(v0[2]), "=v"(v0[3]) : "a"(x0[0]), "a"(x0[1]), "a"(x0[2]), "a"(x0[3]));
+    asm volatile("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+                 "v_accvgpr_read_b32 %3, %7"
+                 : "=v"(v1[0]), "=v"(v1[1]), "=v"(v1[2]), "=v"(v1[3]) : "a"(x1[0]), "a"(x1[1]), "a"(x1[2]), "a"(x1[3]));
+    const int nbytes = __builtin_amdgcn_readfirstlane(max(min(e_rows - rb * 16, 16), 0) * ldc2);
+    const unsigned voff = (lcol + cb * 16 < e_cols) ? lane_voff : 0x80000000u;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    unsigned q00 = pk<T>(v0[0], v0[1]), q01 = pk<T>(v0[2], v0[3]);
+    unsigned q10 = pk<T>(v1[0], v1[1]), q11 = pk<T>(v1[2], v1[3]);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(q00, q10, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(q01, q11, false, false);
+    const size_t bp = (size_t)(e_base + (size_t)rb * 16 * ldc2);
+    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)bp);
+    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(bp >> 32));
+    const auto rsc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((size_t)bhi << 32) | blo), (short)0,
+                                                       nbytes, 0x00020000);
+    const u32x4 qv{s0[0], s1[0], s0[1], s1[1]};
+    if (p.epi & EPI_TEMPORAL) __builtin_amdgcn_raw_buffer_store_b128(qv, rsc, voff + cb * 32, 0, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(qv, rsc, voff + cb * 32, 0, 2);
+  };
+
+  f32x4 acc[8][8];
+  uint4 fa0[8], fb0[8], fa1[8], fb1[8];
+  // phase A of K-tile t: MFMAs on k-half 0; k-half 1's 16 reads in a burst over groups 0-7; release
+  // barrier at group 8 (A slot t % 3 and B slot t % 2 are fully read); B of tile t + 2 DMA'd over
+  // groups 8-15
+  auto phaseA = [&](auto ep_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8], uint4 (&nb)[8], int t) {
+    constexpr bool EP = decltype(ep_c)::value;
+    const int as = t % 3, bs = t & 1;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < 8) {
+#pragma unroll
+        for (int r = 2 * s; r < 2 * s + 2; ++r) {
+          if (r & 1) nb[r >> 1] = readB(bs, 1, r >> 1);
+          else na[r >> 1] = readA(as, 1, r >> 1);
+        }
+      }
+      if (s == 8) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        bar();
+        begin(cb_, bs);
+      }
+      if (s >= 8) dma(cb_, lds0 + AD_B0, s - 8);
+      const int i = s >> 1, jb = (s & 1) * 4;
+      if constexpr (EP) {
+        store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+        store_pair(acc[i][jb + 2], acc[i][jb + 3], i, jb + 2);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = jb + q;
+        if constexpr (EP) mma0<T>(acc[i][j], cb[j], ca[i]);
+        else acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+    }
+    end(cb_, false);
+  };
+  // phase B of K-tile t: MFMAs on k-half 1; k-half 0 of tile t + 1 read one per group (consumption
+  // order); A of tile t + 3 DMA'd over groups 0-7 into A slot t % 3
+  auto phaseB = [&](uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8], uint4 (&nb)[8], int t) {
+    const int as = t % 3, as1 = (t + 1) % 3, bs1 = (t + 1) & 1;
+    begin(ca_, as);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s == 0) na[0] = readA(as1, 0, 0);
+      else if (s <= 8) nb[s - 1] = readB(bs1, 0, s - 1);
+      else na[s - 8] = readA(as1, 0, s - 8);
+      if (s < 8) dma(ca_, lds0, s);
+      const int i = s >> 1, jb = (s & 1) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = jb + q;
+        acc[i][j] = Mf<T>::mma(cb[j], ca[i], acc[i][j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+    }
+    end(ca_, true);
+  };
+
+  // ---- prologue: A tiles 0-2 into A slots 0-2, B tiles 0-1 into B slots 0-1 ----------------------
+  set_tile(ca_, true, 0);
+  set_tile(cb_, false, 0);
+  for (int b = 0; b < 2; ++b) {
+    begin(cb_, b);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dma(cb_, lds0 + AD_B0, u);
+    end(cb_, false);
+  }
+  for (int a = 0; a < 3; ++a) {
+    begin(ca_, a);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dma(ca_, lds0, u);
+    end(ca_, true);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa0[i] = readA(0, 0, i);
+    fb0[i] = readB(0, 0, i);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // boundary A(t) -> B(t): tile t + 1's B (DMA'd in A(t-1)) and A (in B(t-2)) have landed; younger:
+  // A(t+2)'s 8 DMAs (B(t-1)), B(t+2)'s 8 (A(t)) and an epilogue phase's 32 stores
+  int t = 0;
+  for (int r = 0; sc.valid(r); ++r) {
+    phaseA(std::true_type{}, fa0, fb0, fa1, fb1, t);
+    asm volatile("s_waitcnt vmcnt(48)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bar();
+    set_epi(r);
+    phaseB(fa1, fb1, fa0, fb0, t);
+    ++t;
+    for (int k = 1; k < nk; ++k, ++t) {
+      phaseA(std::false_type{}, fa0, fb0, fa1, fb1, t);
+      asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bar();
+      phaseB(fa1, fb1, fa0, fb0, t);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jb = 0; jb < 8; jb += 2) store_pair(acc[i][jb], acc[i][jb + 1], i, jb);
+}
+
 template <typename T, bool BIAS, bool E>
 int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
   if (a.splits > 1) {   // TN only (weight gradients)
@@ -802,6 +1336,19 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
       hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, false, true>), dim3(grid), dim3(256), 0, st, a);
       return (int)hipGetLastError();
     }
+  }
+  if constexpr (!BIAS) {
+    if ((a.epi & EPI_ADEEP) && !(a.epi & EPI_GELU) && !ako && !bko && !trans && a.K >= 256) {
+      hipLaunchKernelGGL((gemm4a_kernel<T>), dim3(grid), dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if ((a.epi & EPI_RING) && !ako && !bko && !trans && a.K >= 128 && a.K % 64 == 0) {
+    if (a.epi & EPI_GELU)
+      hipLaunchKernelGGL((gemm4r_kernel<T, BIAS, true>), dim3(grid), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm4r_kernel<T, BIAS, false>), dim3(grid), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
   }
   if (!E && (a.epi & EPI_RSTAGE) && !ako && !bko && !trans) {
     if (a.epi & EPI_GELU)

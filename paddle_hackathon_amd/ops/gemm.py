@@ -27,6 +27,8 @@ from . import _lib
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_DGELU, EPI_COLSUM, EPI_AUXOUT, EPI_TRANS = 1, 2, 4, 8, 16, 32, 64
 EPI_RSTAGE = 32768   # gemm4p NT: register-staged operands
 EPI_EARLY = 65536    # gemm4p: early-release schedule (read burst + buffer release early in phase A)
+EPI_RING = 1 << 22   # gemm4p NT: 4-slot ring of 32-deep stages (gemm4r_kernel; K % 64 == 0, K >= 128)
+EPI_ADEEP = 1 << 23  # gemm4p NT, no bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel; K >= 256)
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
@@ -216,9 +218,15 @@ def _epi_default(a_kouter, b_kouter, trans_out, K):
         return 0
     if not (a_kouter or b_kouter or trans_out):
         # NT: PIN variant (LV 8 — an empty memory asm closes every MFMA group so no IR pass sinks
-        # a group's LDS reads past the loop latch): 1-3 % over LV 0 on every GPT NT shape,
-        # bitwise identical (profiles/g4p_late_ab_r5.log); PHA_G4P_LV overrides
-        return EPI_EARLY | (int(os.environ.get("PHA_G4P_LV", "8")) << 17)
+        # a group's LDS reads past the loop latch): 1-3 % over LV 0 on every GPT NT shape in bursts,
+        # bitwise identical (profiles/g4p_late_ab_r5.log); PHA_G4P_LV overrides. Long-K products
+        # without an epilogue take the A-deep build (3 A + 2 B LDS slots, ~2 K-tiles of cover for the
+        # streamed activation panel): 2.5-3 % faster at K >= 6144 under sustained load, bitwise
+        # equal (profiles/g4p_adeep_sustain_r5.log); the kernel picks it only without bias / GELU
+        lv = int(os.environ.get("PHA_G4P_LV", "8")) << 17
+        if K >= 4096 and os.environ.get("PHA_G4P_ADEEP", "1") != "0":
+            return EPI_EARLY | lv | EPI_ADEEP
+        return EPI_EARLY | lv
     return EPI_EARLY
 
 

@@ -49,8 +49,16 @@ def main():
         wt = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
         b = torch.randn(N, device="cuda") * 0.02
         fl = 2.0 * T * N * K
-        lvs = [int(v) for v in os.environ.get("LVS", "0,8").split(",")]
-        var = {f"lv{lv}": (lambda lv=lv: G.gemm_p(x, wt, bias=b, epi_extra=G.EPI_EARLY | (lv << 17))) for lv in lvs}
+        lvs = os.environ.get("LVS", "0,8").split(",")
+        var = {}
+        for lv in lvs:
+            if lv == "adeep":   # no-bias kernel: compared with the no-bias two-buffer build and x @ w^T
+                var["lv8nb"] = lambda: G.gemm_p(x, wt, epi_extra=G.EPI_EARLY | (8 << 17))
+                var["adeep"] = lambda: G.gemm_p(x, wt, epi_extra=G.EPI_EARLY | G.EPI_ADEEP)
+                var["libnb"] = lambda: x @ wt.t()
+                continue
+            epi = G.EPI_EARLY | (G.EPI_RING if lv == "ring" else int(lv) << 17)
+            var["ring" if lv == "ring" else f"lv{lv}"] = (lambda epi=epi: G.gemm_p(x, wt, bias=b, epi_extra=epi))
         var["lib"] = lambda: torch.addmm(b.bfloat16(), x, wt.t())
         res = {}
         for rep in range(2):
