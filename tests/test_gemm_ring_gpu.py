@@ -51,9 +51,10 @@ def test_ring_gelu_aux_and_batched():
 
 @pytest.mark.parametrize("M,N,K", [(4096, 2048, 1024), (1000, 2056, 640), (2048, 6144, 256), (520, 776, 320),
                                    (8192, 2048, 8192)])
-def test_adeep_bitwise_equals_two_buffer_kernel(M, N, K):
+def test_adeep_bitwise_equals_two_buffer_kernel(M, N, K, monkeypatch):
     """EPI_ADEEP (3 A + 2 B LDS slots): same MFMA order, bitwise equal to the two-buffer kernel"""
     from paddle_hackathon_amd.ops import gemm as G
+    monkeypatch.setenv("PHA_G4P_ADEEP", "0")   # the reference: the default would pick A-deep at K >= 4096
     g = torch.Generator(device="cuda").manual_seed(M + N + K + 1)
     a, bt = _r(M, K, g=g), _r(N, K, g=g)
     ref = G.gemm_p(a, bt, epi_extra=G.EPI_EARLY)
