@@ -133,6 +133,10 @@ struct FaExt {
   unsigned seed;         // dropout stream
   unsigned thresh;       // drop when the element's 16-bit random < thresh  (thresh = rate * 65536)
   float keep_scale;      // 1 / (1 - rate)
+  // gradient outputs' element strides (0: dense [B, S, H, D]): token and head strides of dQ and of
+  // dK / dV, so a packed [B, S, H, 3D] QKV gradient is written in place (no concatenation pass)
+  long gq_tok = 0, gkv_tok = 0;
+  int gq_head = 0, gkv_head = 0;
 };
 
 __device__ __forceinline__ unsigned fa_mix(unsigned x) {   // lowbias32 finaliser

@@ -925,8 +925,11 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
     }
   }
   if (key < Sk) {
-    T* dkr = dK + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;   // dK/dV are [B, Sk, H, D]
-    T* dvr = dV + ((long)b * Sk + key) * ((long)H * D) + (long)head * D;
+    // dK/dV are [B, Sk, H, D] (or strided into a packed QKV gradient: ex.gkv_tok / gkv_head)
+    const long gt = ex.gkv_tok ? ex.gkv_tok : (long)H * D;
+    const long gh = ex.gkv_head ? ex.gkv_head : D;
+    T* dkr = dK + ((long)b * Sk + key) * gt + (long)head * gh;
+    T* dvr = dV + ((long)b * Sk + key) * gt + (long)head * gh;
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
@@ -1099,7 +1102,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
     }
   }
   if (q < S) {
-    T* qrow = dQ + ((long)b * S + q) * qstride + (long)head * D;
+    T* qrow = dQ + ((long)b * S + q) * (ex.gq_tok ? ex.gq_tok : qstride) + (long)head * (ex.gq_head ? ex.gq_head : D);
 #pragma unroll
     for (int db = 0; db < ND; ++db)
 #pragma unroll
@@ -2108,13 +2111,21 @@ PHA_API int pha_flash_attn_fwd_ext(int dt, const void* q, const void* k, const v
   return (int)hipErrorInvalidValue;
 }
 
+// g*_tok / g*_head: element strides of the dQ and dK / dV outputs (0 = dense [B, S, H, D]); with
+// Hk == H the three may point into one packed [B, S, H, 3D] gradient
 PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const void* v, const void* dout,
                                    const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int S,
                                    int Sk, int H, int Hk, int D, float scale, int causal, const float* bias, long sb,
-                                   long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
+                                   long sh, long sq, float dropout, unsigned seed, hipStream_t stream, long gq_tok,
+                                   int gq_head, long gkv_tok, int gkv_head) {
   if (H % Hk || (D != 32 && D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
     return (int)hipErrorInvalidValue;
+  if ((gkv_tok || gkv_head) && Hk != H) return (int)hipErrorInvalidValue;
   FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  ex.gq_tok = gq_tok;
+  ex.gq_head = gq_head;
+  ex.gkv_tok = gkv_tok;
+  ex.gkv_head = gkv_head;
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
   if (dt == kBF16) return dispatch_ext<bf16_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
   if (dt == kF16) return dispatch_ext<half_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);

@@ -97,10 +97,11 @@ class BertSelfAttention(nn.Layer):
         B, S, _ = x.shape
         Hn, Dh = self.cfg.num_heads, self.cfg.head_dim
         qkv = self.qkv(x)._t.reshape(B, S, Hn, 3 * Dh)
-        q, k, v = qkv.split(Dh, dim=-1)
         drop = self.cfg.attention_dropout if self.training else 0.0
-        # padded batch: additive key mask [B, 1, 1, S]; attention dropout in-kernel
-        o = _ops.flash_attention(q, k, v, causal=False, dropout_p=drop, training=self.training, mask=attn_bias)
+        # padded batch: additive key mask [B, 1, 1, S]; attention dropout in-kernel; the packed
+        # entry writes dq | dk | dv into one gradient (no split-backward concatenation)
+        o = _ops.flash_attention_qkvpacked(qkv, Hn, causal=False, dropout_p=drop, training=self.training,
+                                           mask=attn_bias)
         return self.out(_wrap(o.reshape(B, S, Hn * Dh)))
 
 

@@ -15,6 +15,6 @@ from __future__ import annotations
 from ._lib import native_available, lib, require_native  # noqa: F401
 from .fused import (  # noqa: F401
     gelu, bias_gelu, softmax, layer_norm, rms_norm, softmax_cross_entropy, embedding,
-    fused_adam_, fused_momentum_, flash_attention, bias_dropout_residual_layer_norm,
+    fused_adam_, fused_momentum_, flash_attention, flash_attention_qkvpacked, bias_dropout_residual_layer_norm,
     global_norm_sq, scale_grads_, check_finite_and_unscale_, batch_norm_train, add_relu,
 )

@@ -295,17 +295,24 @@ def flash_attention(q, k, v, causal=False, dropout_p=0.0, scale=None, training=T
     return o.transpose(1, 2)
 
 
-def flash_attention_qkvpacked(qkv, num_heads, causal=False, dropout_p=0.0, scale=None, training=True):
-    """qkv: [B, S, 3*H*D] or [B, S, H, 3D] fused projection (per head q|k|v) -> [B, S, H, D]."""
+def flash_attention_qkvpacked(qkv, num_heads, causal=False, dropout_p=0.0, scale=None, training=True, mask=None):
+    """qkv: [B, S, 3*H*D] or [B, S, H, 3D] fused projection (per head q|k|v) -> [B, S, H, D].
+    With a mask or dropout the extension kernels write the packed gradient in place (no
+    split-backward concatenation)."""
     B, S = qkv.shape[0], qkv.shape[1]
     q4 = qkv.reshape(B, S, num_heads, -1)
+    drop = dropout_p if training else 0.0
+    if (mask is not None or drop) and _use_hip(q4):
+        o = _hip.flash_attention_packed_ext(q4, causal, scale, mask, drop)
+        if o is not None:
+            return o
     if (_use_hip(q4) and not (training and dropout_p > 0) and q4.is_contiguous()
             and (scale is None or scale > 0)   # the packed forward folds a positive scale into its max
             and _hip.flash_attn_packed_supported(q4, num_heads)):
         return _hip.FlashAttentionPacked.apply(q4, bool(causal), scale)
     D = q4.shape[-1] // 3
     q, k, v = q4.split(D, dim=-1)
-    return flash_attention(q, k, v, causal=causal, dropout_p=dropout_p, scale=scale, training=training)
+    return flash_attention(q, k, v, causal=causal, dropout_p=dropout_p, scale=scale, training=training, mask=mask)
 
 
 # ----------------------------------------------------------------------------

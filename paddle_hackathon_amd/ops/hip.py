@@ -649,7 +649,7 @@ class FlashAttentionExt(torch.autograd.Function):
             L.pha_flash_attn_fwd_ext.argtypes = [I, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG, F, U, P]
             L.pha_flash_attn_fwd_ext.restype = c_int
             L.pha_flash_attn_bwd_ext.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG,
-                                                 F, U, P]
+                                                 F, U, P, LG, I, LG, I]
             L.pha_flash_attn_bwd_ext.restype = c_int
             L._fa_ext_sig = True
         _check(L.pha_flash_attn_fwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, S, Sk, H, Hk, D,
@@ -676,13 +676,62 @@ class FlashAttentionExt(torch.autograd.Function):
         sb, sh, sq = ctx.strides
         _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
                                         _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk, H, Hk, D, ctx.scale, int(ctx.causal),
-                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q)),
+                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q), 0, 0, 0, 0),
                "flash_attn_bwd_ext")
         if Hk != H:
             g = H // Hk
             dk = dk.view(B, Sk, Hk, g, D).sum(3)
             dv = dv.view(B, Sk, Hk, g, D).sum(3)
         return dq, dk, dv, None, None, None, None
+
+
+class FlashAttentionExtPacked(torch.autograd.Function):
+    """FlashAttentionExt on a packed [B, S, H, 3D] projection (q | k | v per head, the BERT / fused
+    QKV layout): the forward takes dense copies of the three slices, the backward writes dq / dk /
+    dv straight into ONE packed [B, S, H, 3D] gradient through the kernels' output strides — no
+    concatenation pass (0.67 ms per BERT-base step, profiles/README.md round 5)"""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale, mask, dropout_p):
+        B, S, H, D3 = qkv.shape
+        D = D3 // 3
+        q, k, v = (qkv[..., i * D:(i + 1) * D].contiguous() for i in range(3))
+        o = FlashAttentionExt.forward(ctx, q, k, v, causal, scale, mask, dropout_p)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        B, S, H, D = q.shape
+        L = _L()
+        delta = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        g = torch.empty((B, S, H, 3 * D), dtype=q.dtype, device=q.device)
+        _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S),
+                                               c_int(H), c_int(D), _stream(q)), "flash_attn_bwd_preprocess")
+        sb, sh, sq = ctx.strides
+        es = g.element_size()
+        base = g.data_ptr()
+        _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
+                                        c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), B, S, S,
+                                        H, H, D, ctx.scale, int(ctx.causal), _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p,
+                                        ctx.seed, _stream(q), 3 * H * D, 3 * D, 3 * H * D, 3 * D),
+               "flash_attn_bwd_ext(packed)")
+        return g, None, None, None, None
+
+
+def flash_attention_packed_ext(qkv, causal, scale, mask=None, dropout_p=0.0):
+    """attention over a packed [B, S, H, 3D] projection with a mask and / or dropout (head dims 32 /
+    64 / 128 / 256); None when the ext kernels cannot take it (the caller splits instead)"""
+    B, S, H, D3 = qkv.shape
+    D = D3 // 3
+    if D3 % 3 or D not in (32, 64, 128, 256) or not qkv.is_cuda or qkv.dtype not in (torch.bfloat16, torch.float16):
+        return None
+    q = qkv[..., :D]
+    if not flash_attn_supported(q, q, q, dropout_p, mask):
+        return None
+    sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+    return FlashAttentionExtPacked.apply(qkv, bool(causal), sc, mask, float(dropout_p))
 
 
 def flash_attention_any(q, k, v, causal, scale, mask=None, dropout_p=0.0):

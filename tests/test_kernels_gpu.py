@@ -1027,6 +1027,34 @@ def test_flash_attention_dropout_regenerated_in_backward(rate, with_mask):
         assert (a.float() - b).abs().max() / b.abs().max() < 3e-2
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("rate,with_mask", [(0.1, True), (0.0, True), (0.2, False)])
+def test_flash_attention_packed_ext_writes_strided_grads(D, rate, with_mask):
+    """packed [B, S, H, 3D] entry with mask / dropout: dq | dk | dv written through the kernels'
+    output strides equal (bitwise) the split path's dense gradients concatenated"""
+    from paddle_hackathon_amd import ops
+    from paddle_hackathon_amd.ops import hip
+    B, S, H = 2, 136, 3
+    torch.manual_seed(5)
+    qkv = torch.randn(B, S, H, 3 * D, device="cuda").bfloat16()
+    mask = None
+    if with_mask:
+        mask = torch.where(torch.arange(S, device="cuda") < S - 9, 0.0, -1e4).reshape(1, 1, 1, S).expand(B, 1, 1, S)
+    a = qkv.clone().requires_grad_()
+    torch.manual_seed(99)
+    o1 = ops.flash_attention_qkvpacked(a, H, dropout_p=rate, training=True, mask=mask)
+    assert o1.grad_fn is not None and "FlashAttentionExtPacked" in type(o1.grad_fn).__name__
+    do = torch.randn_like(o1)
+    (g1,) = torch.autograd.grad(o1, a, do)
+    b = qkv.clone().requires_grad_()
+    q, k, v = b.split(D, dim=-1)
+    torch.manual_seed(99)
+    o2 = hip.FlashAttentionExt.apply(q, k, v, False, 1.0 / math.sqrt(D), mask, float(rate))
+    (g2,) = torch.autograd.grad(o2, b, do)
+    assert torch.equal(o1, o2)
+    assert torch.equal(g1, g2)
+
+
 def test_bert_attention_runs_on_own_kernels():
     """BERT-base attention (dropout 0.1, key-padding mask) goes to FlashAttentionExt, not SDPA"""
     from paddle_hackathon_amd.ops import hip
