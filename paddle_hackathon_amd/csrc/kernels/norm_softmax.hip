@@ -34,9 +34,10 @@ __device__ __forceinline__ bool bd_keep(unsigned seed, long idx, unsigned thresh
 }
 
 struct BdArgs {            // x -> dropout(x + xb) before the residual add (thresh 0: no dropout)
-  const void* xb;          // [H] bias of x (type W), may be null
+  const void* xb;          // [H] bias of x (fp32 when xb_f32, else type T), may be null
   unsigned seed, thresh;
   float kscale;
+  int xb_f32;
 };
 
 template <typename T, typename W, int NCH>
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int H, float eps, const T* __restrict__ r = nullptr,
-                                                     T* __restrict__ hs = nullptr, BdArgs bd = BdArgs{nullptr, 0u, 0u, 1.f}) {
+                                                     T* __restrict__ hs = nullptr, BdArgs bd = BdArgs{nullptr, 0u, 0u, 1.f, 0}) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -63,7 +64,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
         Vec8<T>::ld(r + (long)row * H + col, rv);
         if (bd.xb || bd.thresh) {   // fused bias + dropout of x (rounded to T as a separate op would store)
           float bv[8];
-          if (bd.xb) Vec8<W>::ld((const W*)bd.xb + col, bv);
+          if (bd.xb) {
+            if (bd.xb_f32) Vec8<float>::ld((const float*)bd.xb + col, bv);
+            else Vec8<T>::ld((const T*)bd.xb + col, bv);
+          }
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             float z = round_to<T>(v[c][i] + (bd.xb ? bv[i] : 0.f));
@@ -131,19 +135,27 @@ struct Raw8<float> {
 
 // BW waves per block (16 -> 1024 threads): a grid of one block per CU then still gives 4
 // waves per SIMD to hide HBM latency, while the dw/db partials stay one [H] row per block.
-template <typename T, typename W, int NCH, int BW>
+// XS: also per-block partial column sums of the final dx (part_x) — the bias gradient of a linear
+// layer whose output entered the residual sum (its bias folded into the add-LN forward), so that
+// layer's backward needs no separate column-sum pass over the same gradient
+template <typename T, typename W, int NCH, int BW, bool XS = false>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 4 : NCH <= 4 ? 2 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const W* __restrict__ w, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, T* __restrict__ dx,
                                                          float* __restrict__ part_w, float* __restrict__ part_b,
-                                                         int rows, int H, const T* __restrict__ dres) {
+                                                         int rows, int H, const T* __restrict__ dres,
+                                                         float* __restrict__ part_x = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float aw[NCH][8], ab[NCH][8];
+  float aw[NCH][8], ab[NCH][8], ax[XS ? NCH : 1][8];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { aw[c][i] = 0.f; ab[c][i] = 0.f; }
+    for (int i = 0; i < 8; ++i) {
+      aw[c][i] = 0.f;
+      ab[c][i] = 0.f;
+      if constexpr (XS) ax[c][i] = 0.f;
+    }
 
   // H = 1537..2048 (NCH 4, the GPT-1.3B width): one HBM round trip per row with x / dy / dres held
   // raw in registers (2 waves per SIMD, no spills); other widths re-read x and dy in pass 2
@@ -161,7 +173,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
       if (col < H) {
         rx[c].ld(xr + col);
         rg[c].ld(gr + col);
-        if (dres) rr[c].ld(dres + (long)row * H + col);
+        if (!XS && dres) rr[c].ld(dres + (long)row * H + col);   // XS: re-read in pass 2 (registers)
       }
     }
     // pass 1: row statistics of g = dy*w
@@ -201,9 +213,14 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
         }
         if (dres) {  // fused residual branch: dx += d(sum output)
           float rv[8];
-          rr[c].unpack(rv);
+          if constexpr (XS) Vec8<T>::ld(dres + (long)row * H + col, rv);
+          else rr[c].unpack(rv);
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] += rv[i];
+        }
+        if constexpr (XS) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ax[c][i] += round_to<T>(o[i]);   // the stored gradient's sum
         }
         Vec8<T>::st(dr + col, o);
       }
@@ -256,6 +273,10 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] += rv[i];
         }
+        if constexpr (XS) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ax[c][i] += round_to<T>(o[i]);   // the stored gradient's sum
+        }
         Vec8<T>::st(dr + col, o);
       }
     }
@@ -265,9 +286,13 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
   __shared__ float red[BW][512];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < (XS ? 3 : 2); ++pass) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = pass == 0 ? aw[c][i] : ab[c][i];
+      for (int i = 0; i < 8; ++i) {
+        float v = pass == 0 ? aw[c][i] : ab[c][i];
+        if constexpr (XS) v = pass == 2 ? ax[c][i] : v;
+        red[wid][lane * 8 + i] = v;
+      }
       __syncthreads();
       for (int k = threadIdx.x; k < 512; k += BW * 64) {
         const int cc = c * 512 + k;
@@ -275,7 +300,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
           float t = 0.f;
 #pragma unroll
           for (int q = 0; q < BW; ++q) t += red[q][k];
-          float* dst = pass == 0 ? part_w : part_b;
+          float* dst = pass == 0 ? part_w : pass == 1 ? part_b : part_x;
           dst[(long)blockIdx.x * H + cc] = t;
         }
       }
@@ -508,12 +533,14 @@ PHA_API int pha_layer_norm_bwd_nblocks(int rows, int H) {
 
 // fused_bias_dropout_residual_layer_norm forward: hs = r + dropout(x + xb) (stored), y = LN(hs).
 // thresh = round(p * 65536) (0: no dropout), kscale = 1 / (1 - p).
-PHA_API int pha_bdrln_fwd(int dt, int wdt, const void* x, const void* xb, const void* r, void* hs, const void* w,
-                          const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps, unsigned seed,
-                          unsigned thresh, float kscale, hipStream_t stream) {
+// xbdt: dtype of xb (fp32 or the activation type)
+PHA_API int pha_bdrln_fwd2(int dt, int wdt, int xbdt, const void* x, const void* xb, const void* r, void* hs,
+                           const void* w, const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps,
+                           unsigned seed, unsigned thresh, float kscale, hipStream_t stream) {
   if (H % 8 || rows <= 0 || !r || !hs) return (int)hipErrorInvalidValue;
+  if (xb && xbdt != kF32 && xbdt != dt) return (int)hipErrorInvalidValue;
   const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
-  const BdArgs bd{xb, seed, thresh, kscale};
+  const BdArgs bd{xb, seed, thresh, kscale, xbdt == kF32 ? 1 : 0};
   int rc = 0;
   PHA_DISPATCH_T(dt, T, {
     if (wdt == kF32) {
@@ -531,6 +558,12 @@ PHA_API int pha_bdrln_fwd(int dt, int wdt, const void* x, const void* xb, const 
     }
   });
   return rc;
+}
+
+PHA_API int pha_bdrln_fwd(int dt, int wdt, const void* x, const void* xb, const void* r, void* hs, const void* w,
+                          const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps, unsigned seed,
+                          unsigned thresh, float kscale, hipStream_t stream) {
+  return pha_bdrln_fwd2(dt, wdt, wdt, x, xb, r, hs, w, b, y, mean, rstd, rows, H, eps, seed, thresh, kscale, stream);
 }
 
 PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
@@ -579,6 +612,47 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
       if (rc) return rc;
       col_sum<T>(part_w, (T*)dw, nblocks, H, stream);
       if (db) col_sum<T>(part_b, (T*)db, nblocks, H, stream);
+    }
+  });
+  return rc ? rc : (int)hipGetLastError();
+}
+
+// pha_layer_norm_bwd2 plus dxs = column sums of the final dx (type wdt; part_x: [nblocks + 8, H])
+PHA_API int pha_layer_norm_bwd3(int dt, int wdt, int xsdt, const void* dy, const void* x, const void* w, const float* mean,
+                                const float* rstd, const void* dres, void* dx, void* dw, void* db, void* dxs,
+                                float* part_w, float* part_b, float* part_x, int nblocks, int rows, int H,
+                                hipStream_t stream) {
+  if (!dxs || !part_x)
+    return pha_layer_norm_bwd2(dt, wdt, dy, x, w, mean, rstd, dres, dx, dw, db, part_w, part_b, nblocks, rows, H,
+                               stream);
+  if (H % 8 || rows <= 0 || nblocks <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid(nblocks);
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    if (wdt == kF32) {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        constexpr int N = decltype(nch)::value;
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, N, bwd_waves(N), true>), grid, dim3(bwd_waves(N) * 64), 0, stream,
+                           (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H,
+                           (const T*)dres, part_x);
+      });
+      if (rc) return rc;
+      col_sum<float>(part_w, (float*)dw, nblocks, H, stream);
+      if (db) col_sum<float>(part_b, (float*)db, nblocks, H, stream);
+      if (xsdt == kF32) col_sum<float>(part_x, (float*)dxs, nblocks, H, stream);
+      else col_sum<T>(part_x, (T*)dxs, nblocks, H, stream);
+    } else {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        constexpr int N = decltype(nch)::value;
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, N, bwd_waves(N), true>), grid, dim3(bwd_waves(N) * 64), 0, stream,
+                           (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows, H,
+                           (const T*)dres, part_x);
+      });
+      if (rc) return rc;
+      col_sum<T>(part_w, (T*)dw, nblocks, H, stream);
+      if (db) col_sum<T>(part_b, (T*)db, nblocks, H, stream);
+      if (xsdt == kF32) col_sum<float>(part_x, (float*)dxs, nblocks, H, stream);
+      else col_sum<T>(part_x, (T*)dxs, nblocks, H, stream);
     }
   });
   return rc ? rc : (int)hipGetLastError();

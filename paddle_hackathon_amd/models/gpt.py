@@ -16,6 +16,7 @@ MI355X-first choices:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -89,14 +90,18 @@ class GPTAttention(nn.Layer):
             self.qkv_proj = nn.Linear(h, 3 * h, weight_attr=_w_attr(cfg))
             self.out_proj = nn.Linear(h, h, weight_attr=_w_attr(cfg, out_scale))
 
-    def forward(self, x):
+    def forward(self, x, defer_bias=False):
+        """defer_bias: return (projection without its bias, the bias) for the next add-LN kernel
+        to add (its backward then yields the bias gradient as a by-product)"""
         B, S = x._t.shape[0], x._t.shape[1]
         qkv = self.qkv_proj(x)._t.reshape(B, S, self.num_heads, 3 * self.head_dim)
         drop = self.cfg.attention_dropout if self.training else 0.0
         o = _ops.fused.flash_attention_qkvpacked(qkv, self.num_heads, causal=True, dropout_p=drop,
                                                  training=self.training)
-        o = o.reshape(B, S, self.num_heads * self.head_dim)
-        return self.out_proj(_wrap(o))
+        o = _wrap(o.reshape(B, S, self.num_heads * self.head_dim))
+        if defer_bias and self.cfg.tensor_parallel_degree <= 1:
+            return F.linear(o, self.out_proj.weight, None), self.out_proj.bias
+        return self.out_proj(o)
 
 
 class GPTMLP(nn.Layer):
@@ -113,13 +118,20 @@ class GPTMLP(nn.Layer):
             self.linear1 = nn.Linear(h, f, weight_attr=_w_attr(cfg))
             self.linear2 = nn.Linear(f, h, weight_attr=_w_attr(cfg, out_scale))
 
-    def forward(self, x):
+    def forward(self, x, defer_bias=False):
+        """defer_bias: return (fc2 output without its bias, the bias), as GPTAttention.forward"""
         if self.cfg.tensor_parallel_degree <= 1:
             from ..ops import mlp as _mlp
             l1, l2 = self.linear1, self.linear2
             if _mlp.available(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t):
                 # one node: bias+GELU folded into the GEMM epilogues when that measures faster
+                if defer_bias:
+                    return _wrap(_mlp.fused_mlp(x._t, l1.weight._t, l1.bias._t, l2.weight._t, None)), l2.bias
                 return _wrap(_mlp.fused_mlp(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t))
+            if defer_bias:
+                h = _cg.matmul_kn(x._t, l1.weight._t)
+                h = _ops.bias_gelu(h, l1.bias._t, approximate=True)
+                return F.linear(_wrap(h), l2.weight, None), l2.bias
         if self.cfg.tensor_parallel_degree > 1:
             # column-parallel fc1 computed here (bias fused into the GELU): its input must pass
             # c_identity so the backward all-reduces the partial input gradients over the TP group
@@ -147,12 +159,21 @@ class GPTDecoderLayer(nn.Layer):
         h, m = self.forward_fused(x, None)
         return h + m
 
-    def _add_ln(self, norm, x, delta):
+    def _add_ln(self, norm, x, delta, dbias=None):
         if delta is None:
             return x, norm(x)
         h, y = _ops.fused.add_layer_norm(x._t, delta._t, norm.weight._t, None if norm.bias is None else norm.bias._t,
-                                         norm._epsilon)
+                                         norm._epsilon, xb=None if dbias is None else dbias._t)
         return _wrap(h), _wrap(y)
+
+    def forward_deferred(self, x, delta, dbias):
+        """forward_fused with the output projections' biases deferred too: the layer input is
+        ``x + (delta + dbias)``; returns (h, m, mbias). No dropout on the residual branches."""
+        h, a_in = self._add_ln(self.norm1, x, delta, dbias)
+        a, abias = self.self_attn(a_in, defer_bias=True)
+        h2, m_in = self._add_ln(self.norm2, h, a, abias)
+        m, mbias = self.mlp(m_in, defer_bias=True)
+        return h2, m, mbias
 
     def forward_fused(self, x, delta):
         """Residual stream with the adds deferred into the next LayerNorm kernel: the layer
@@ -193,9 +214,19 @@ class GPTModel(nn.Layer):
         self.layers = nn.LayerList([GPTDecoderLayer(cfg) for _ in range(cfg.num_layers)])
         self.final_norm = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
 
+    def _defer_ok(self):
+        c = self.cfg
+        return (c.tensor_parallel_degree <= 1 and not (c.recompute and self.training)
+                and not (c.hidden_dropout and self.training) and os.environ.get("PHA_GPT_DEFER_BIAS", "0") == "1")
+
     def forward(self, input_ids, position_ids=None):
         x = self.embeddings(input_ids, position_ids)
         delta = None
+        if self._defer_ok():
+            dbias = None
+            for layer in self.layers:
+                x, delta, dbias = layer.forward_deferred(x, delta, dbias)
+            return self.layers[-1]._add_ln(self.final_norm, x, delta, dbias)[1]
         for layer in self.layers:
             if self.cfg.recompute and self.training:
                 from ..parallel.recompute import recompute

@@ -126,34 +126,46 @@ def layer_norm(x, normalized_shape, weight=None, bias=None, eps=1e-5):
 
 
 class _AddLayerNorm(torch.autograd.Function):
-    """(x, r) -> (h = x + r, y = LN(h)) in one kernel; backward folds dh into dx."""
+    """(x, r) -> (h = x + r, y = LN(h)) in one kernel; backward folds dh into dx.
+    With ``xb`` (the bias of the branch output r, e.g. an attention / MLP output projection run
+    without its bias): h = x + (r + xb); the backward's LN kernel also sums dh over the rows,
+    which is xb's gradient — no separate column-sum pass over dh in the projection's backward."""
 
     @staticmethod
-    def forward(ctx, x, r, w, b, eps):
-        y, mean, rstd, h = _hip.layer_norm_fwd(x, w, b, eps, residual=r)
+    def forward(ctx, x, r, w, b, eps, xb=None):
+        if xb is None:
+            y, mean, rstd, h = _hip.layer_norm_fwd(x, w, b, eps, residual=r)
+        else:
+            y, mean, rstd, h = _hip.bdrln_fwd(r, xb, x, w, b, eps, 0, 0, 1.0)
         ctx.save_for_backward(h, w, b, mean, rstd)
+        ctx.xb_dtype = None if xb is None else xb.dtype
         return h, y
 
     @staticmethod
     def backward(ctx, gh, gy):
         h, w, b, mean, rstd = ctx.saved_tensors
+        xbd = ctx.xb_dtype
         if gy is None:
-            return gh, gh, None, None, None
-        gx, gw, gb = _hip.layer_norm_bwd(gy.contiguous(), h, w, mean, rstd, b is not None,
-                                         dres=None if gh is None else gh.contiguous())
-        return gx, gx, gw, gb, None
+            gxb = None if xbd is None else gh.reshape(-1, gh.shape[-1]).sum(0, dtype=torch.float32).to(xbd)
+            return gh, gh, None, None, None, gxb
+        res = _hip.layer_norm_bwd(gy.contiguous(), h, w, mean, rstd, b is not None,
+                                  dres=None if gh is None else gh.contiguous(), dx_colsum=xbd)
+        gx, gw, gb = res[:3]
+        gxb = None if xbd is None else (res[3] if res[3].dtype == xbd else res[3].to(xbd))
+        return gx, gx, gw, gb, None, gxb
 
 
-def add_layer_norm(x, residual, weight, bias=None, eps=1e-5):
-    """Pre-LN residual step: returns (h, LN(h)) with h = x + residual (one HIP kernel each way)."""
+def add_layer_norm(x, residual, weight, bias=None, eps=1e-5, xb=None):
+    """Pre-LN residual step: returns (h, LN(h)) with h = x + residual (one HIP kernel each way);
+    ``xb`` (optional): a bias of ``residual`` added in the same pass (h = x + (residual + xb))."""
     H = weight.numel()
     if (_use_hip(x) and x.is_contiguous() and residual.is_contiguous() and residual.dtype == x.dtype
             and residual.shape == x.shape and x.dtype in (torch.bfloat16, torch.float32, torch.float16)
             and weight.dtype in (x.dtype, torch.float32) and H % 8 == 0 and H <= 4096
-            and (bias is None or bias.dtype == weight.dtype)):
+            and (bias is None or bias.dtype == weight.dtype) and (xb is None or xb.numel() == H)):
         return _AddLayerNorm.apply(x, residual, weight.reshape(-1), None if bias is None else bias.reshape(-1),
-                                   float(eps))
-    h = x + residual
+                                   float(eps), None if xb is None else xb.reshape(-1))
+    h = x + (residual if xb is None else residual + xb)
     return h, layer_norm(h, [H], weight, bias, eps)
 
 

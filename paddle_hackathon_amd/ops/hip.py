@@ -32,6 +32,8 @@ def _L():
             "pha_layer_norm_bwd_nblocks": [I, I],
             "pha_layer_norm_fwd2": [I, I, P, P, P, P, P, P, P, P, I, I, F, P],
             "pha_layer_norm_bwd2": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+            "pha_layer_norm_bwd3": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+            "pha_bdrln_fwd2": [I, I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
             "pha_bdrln_fwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
             "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
@@ -100,8 +102,10 @@ def layer_norm_fwd(x, w, b, eps, residual=None):
     return (y, mean, rstd) if residual is None else (y, mean, rstd, hs)
 
 
-def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None):
-    """dx = LN'(dy) (+ dres: gradient of a fused residual sum). ``x`` is the normalised input."""
+def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None, dx_colsum=None):
+    """dx = LN'(dy) (+ dres: gradient of a fused residual sum). ``x`` is the normalised input.
+    dx_colsum (a dtype: fp32 or x's): also return the column sums of dx in it — the gradient of a
+    bias that was folded into the forward's residual sum (add_layer_norm's ``xb``)."""
     H = w.numel()
     rows = x.numel() // H
     nblocks = int(_L().pha_layer_norm_bwd_nblocks(rows, H))  # partials [nblocks, H]
@@ -110,7 +114,14 @@ def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None):
     db = torch.empty_like(w) if has_bias else None
     if dres is not None:
         assert dres.shape == x.shape and dres.dtype == x.dtype and dres.is_contiguous()
-    part = torch.empty((2, nblocks + 8, H), dtype=torch.float32, device=x.device)  # + column-sum stage rows
+    part = torch.empty((3 if dx_colsum else 2, nblocks + 8, H), dtype=torch.float32, device=x.device)  # + stage rows
+    if dx_colsum is not None:
+        xs_dt = dx_colsum if dx_colsum in (torch.float32, x.dtype) else torch.float32
+        dxs = torch.empty(H, dtype=xs_dt, device=x.device)
+        _check(_L().pha_layer_norm_bwd3(_DT[x.dtype], _DT[w.dtype], _DT[xs_dt], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd),
+                                        _ptr(dres), _ptr(dx), _ptr(dw), _ptr(db), _ptr(dxs), _ptr(part[0]),
+                                        _ptr(part[1]), _ptr(part[2]), nblocks, rows, H, _stream(x)), "layer_norm_bwd3")
+        return dx, dw, db, dxs
     _check(_L().pha_layer_norm_bwd2(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean), _ptr(rstd),
                                     _ptr(dres), _ptr(dx), _ptr(dw), _ptr(db), _ptr(part[0]), _ptr(part[1]), nblocks, rows, H,
                                     _stream(x)), "layer_norm_bwd")
@@ -127,8 +138,11 @@ def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale):
     y, hs = torch.empty_like(x), torch.empty_like(x)
     mean = torch.empty(rows, dtype=torch.float32, device=x.device)
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-    xb = None if xbias is None else xbias.contiguous().to(w.dtype)
-    _check(_L().pha_bdrln_fwd(_DT[x.dtype], _DT[w.dtype], _ptr(x), _ptr(xb), _ptr(residual), _ptr(hs),
+    xb = None if xbias is None else xbias.contiguous()
+    if xb is not None and xb.dtype not in (torch.float32, x.dtype):
+        xb = xb.float()
+    xbdt = _DT[w.dtype] if xb is None else _DT[xb.dtype]
+    _check(_L().pha_bdrln_fwd2(_DT[x.dtype], _DT[w.dtype], xbdt, _ptr(x), _ptr(xb), _ptr(residual), _ptr(hs),
                               _ptr(w.contiguous()), _ptr(None if b is None else b.contiguous()), _ptr(y), _ptr(mean),
                               _ptr(rstd), rows, H, float(eps), int(seed), int(thresh), float(kscale), _stream(x)),
            "bdrln_fwd")

@@ -86,7 +86,7 @@ class FusedMLP(torch.autograd.Function):
     def forward(ctx, x2d, w1, b1, w2, b2, mode):
         from .conv_gemm import weight_t
         a, pre = _fwd(mode, x2d, w1, b1)
-        y = G.mm_nt_bias(a, weight_t(w2), b2)
+        y = G.mm_nt(a, weight_t(w2)) if b2 is None else G.mm_nt_bias(a, weight_t(w2), b2)
         ctx.save_for_backward(x2d, w1, b1, w2, pre, a)
         ctx.mode = mode
         return y
@@ -97,7 +97,7 @@ class FusedMLP(torch.autograd.Function):
         x2d, w1, b1, w2, pre, a = ctx.saved_tensors
         gy = gy.contiguous()
         dw2 = weight_grad(a, gy)
-        db2 = _hip.col_sum(gy)
+        db2 = _hip.col_sum(gy) if ctx.needs_input_grad[4] else None
         g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1)
         dx = G.mm_nt(g, w1) if ctx.needs_input_grad[0] else None
         dw1 = weight_grad(x2d, g)
@@ -105,7 +105,8 @@ class FusedMLP(torch.autograd.Function):
 
 
 def fused_mlp(x, w1, b1, w2, b2):
-    """gelu_tanh(x @ w1 + b1) @ w2 + b2 for x [..., H], w1 [H, F], w2 [F, H] (Paddle [in, out])"""
+    """gelu_tanh(x @ w1 + b1) @ w2 + b2 for x [..., H], w1 [H, F], w2 [F, H] (Paddle [in, out]);
+    b2 None: no output bias (the caller adds it, e.g. in the next add-LN kernel)"""
     x2d = x.reshape(-1, x.shape[-1])
     if not x2d.is_contiguous():
         x2d = x2d.contiguous()

@@ -82,6 +82,71 @@ def test_add_layer_norm_fused(H, rows):
     assert torch.allclose(b.grad, br.grad, atol=0.5, rtol=2e-2)
 
 
+@pytest.mark.parametrize("H", [768, 2048, 4096])
+@pytest.mark.parametrize("xb_dtype", [torch.float32, torch.bfloat16])
+def test_add_layer_norm_folded_bias(H, xb_dtype):
+    """h = x + (r + xb), y = LN(h): the branch bias xb is added in the LN kernel and its gradient is
+    the column sum of the stored dx, produced by the LN backward kernel (dx_colsum)"""
+    from paddle_hackathon_amd.ops import fused
+    torch.manual_seed(3)
+    rows = 3000
+    x = torch.randn(rows, H, device="cuda").bfloat16().requires_grad_(True)
+    r = torch.randn(rows, H, device="cuda").bfloat16().requires_grad_(True)
+    xb = torch.randn(H, device="cuda").to(xb_dtype).requires_grad_(True)
+    w = (torch.rand(H, device="cuda") + 0.5).requires_grad_(True)
+    b = torch.randn(H, device="cuda").requires_grad_(True)
+    h, y = fused.add_layer_norm(x, r, w, b, 1e-5, xb=xb)
+    hs = (x.detach() + (r.detach() + xb.detach().to(w.dtype)).bfloat16())   # the rounding the kernel does
+    assert torch.equal(h, hs.detach())
+    dy, dh = torch.randn(rows, H, device="cuda").bfloat16(), torch.randn(rows, H, device="cuda").bfloat16()
+    torch.autograd.backward([h, y], [dh, dy])
+    assert torch.equal(x.grad, r.grad)
+    ref = x.grad.float().sum(0)
+    assert xb.grad.dtype == xb_dtype
+    assert (xb.grad.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    # the plain path (no xb) gives the same dx
+    x2, r2 = x.detach().clone().requires_grad_(True), (r.detach() + xb.detach().to(torch.bfloat16)).requires_grad_(True)
+    h2, y2 = fused.add_layer_norm(x2, r2, w.detach(), b.detach(), 1e-5)
+    torch.autograd.backward([h2, y2], [dh, dy])
+    if xb_dtype == torch.bfloat16:
+        assert torch.equal(h2, h)
+        assert torch.equal(x2.grad, x.grad)
+
+
+def test_gpt_deferred_bias_matches_plain():
+    """GPT layers with the output-projection biases folded into the add-LN kernels (the default)
+    give the plain per-layer path's loss and bias gradients"""
+    import os
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.models.gpt import GPTForPretraining, gpt_config
+    paddle.set_device("gpu")
+    try:
+        paddle.seed(7)
+        cfg = gpt_config("gpt-tiny", hidden_size=256, num_heads=4, ffn_hidden_size=1024)
+        m = GPTForPretraining(cfg)
+        m.bfloat16()   # the bf16 fused-MLP / flash-attention / add-LN kernels
+        ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (2, 128)))
+        lab = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (2, 128)))
+        out = {}
+        for mode in ("1", "0"):
+            os.environ["PHA_GPT_DEFER_BIAS"] = mode
+            for p in m.parameters():
+                p.clear_grad()
+            loss = m(ids, labels=lab)
+            loss.backward()
+            out[mode] = (float(loss), {n: p.grad._t.float().clone() for n, p in m.named_parameters()
+                                       if n.endswith("bias") and p.grad is not None})
+        os.environ.pop("PHA_GPT_DEFER_BIAS", None)
+        assert abs(out["1"][0] - out["0"][0]) < 2e-2 * max(1.0, abs(out["0"][0]))
+        assert out["1"][1].keys() == out["0"][1].keys()
+        for n, g in out["0"][1].items():
+            d = (out["1"][1][n] - g).abs().max().item()
+            assert d <= 3e-2 * max(1e-3, g.abs().max().item()) + 1e-3, (n, d)
+    finally:
+        os.environ.pop("PHA_GPT_DEFER_BIAS", None)
+        paddle.set_device("cpu")
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H", [128, 1024, 2048, 4096])
 def test_softmax(dt, H):
