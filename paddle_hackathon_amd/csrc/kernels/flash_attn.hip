@@ -691,6 +691,445 @@ __global__ __launch_bounds__(NT2) void fa_fwd_v3_kernel(const T* __restrict__ Q,
   }
 }
 
+// ============================================================================================
+// Forward v4 (D = 128): 4 waves x 64 query rows — two 32-row blocks A, B per wave, one wave per
+// SIMD with the whole 512-register file — and the softmax software-pipelined against the MFMAs
+// INSIDE each wave (the 8-wave kernels rely on the two waves of a SIMD drifting apart, which the
+// per-tile barrier prevents). The pipeline runs over 32-key sub-tiles u (half a 64-key DMA tile),
+// which keeps the in-flight scores at 2 x 16 registers per block:
+//   phase 1:  S(u) = K_u Q^T for A and B (16 MFMAs; each K fragment read once for both blocks)
+//             || finish of u-1: second half of its exps, row sums, P(u-1) packed to bf16
+//   phase 2:  O^T += V_{u-1}^T P(u-1)^T for A and B (16 MFMAs; each V fragment read once)
+//             || start of u: row max, running-max update, first half of its exps
+// The O rescale a raised running max needs (deferred by kThr as in v3) lands after phase 2's
+// MFMAs, i.e. between P(u-1) V and P(u) V. K / V tiles arrive by LDS-DMA a whole tile ahead
+// (K ring of 2, V ring of 3: V(t-1) is still read in tile t's first sub-tile), one barrier per
+// 64-key tile.
+// ============================================================================================
+#ifndef PHA_FA4_GROUPS
+#define PHA_FA4_GROUPS 1
+#endif
+#ifndef PHA_FA4_SLOTS
+#define PHA_FA4_SLOTS 1   // hand-slotted steady sub-tiles (step_steady)
+#endif
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, T* __restrict__ O,
+                      float* __restrict__ LSE, int S, int Sk, int H, int Hk, float scale_log2, FaStrides fs) {
+  typedef typename MF<T>::frag frag;
+  constexpr int ND = 4, NK = 8;
+  constexpr int TILE = BN * 128 * 2;   // 16 KiB per K or V tile
+  __shared__ __attribute__((aligned(16))) unsigned char smem[5 * TILE];   // K ring [2] | V ring [3]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+            lr = lane & 31;
+  const int nqb = (S + BM2 - 1) / BM2;
+  int bh, rank;
+  fa_block(gridDim.x * gridDim.y / nqb, nqb, fs.order_g, bh, rank);
+  const int qb = CAUSAL ? (nqb - 1 - rank) : rank;
+  const int head = bh % H, b = bh / H;
+  const int hk = head / (H / Hk);
+  const int q0 = qb * BM2;
+  const int wq0 = q0 + wid * 64;               // block A rows wq0 + [0, 32), block B rows wq0 + 32 + [0, 32)
+  const int qa = wq0 + lr, qbq = wq0 + 32 + lr;
+  const long qstride = fs.q_tok, kstride = fs.kv_tok;
+  const T* Qb = Q + ((long)b * S) * qstride + (long)head * fs.q_head;
+  const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
+  const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
+
+  frag qA[NK], qB[NK];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    u32x4 va = {0, 0, 0, 0}, vb = {0, 0, 0, 0};
+    if (qa < S) va = *reinterpret_cast<const u32x4*>(Qb + (long)qa * qstride + 16 * kk + 8 * h);
+    if (qbq < S) vb = *reinterpret_cast<const u32x4*>(Qb + (long)qbq * qstride + 16 * kk + 8 * h);
+    qA[kk] = as_frag<frag>(va);
+    qB[kk] = as_frag<frag>(vb);
+  }
+  f32x16 oA[ND], oB[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { oA[i] = zero16(); oB[i] = zero16(); }
+  float mA = -INFINITY, mB = -INFINITY, lA = 0.f, lB = 0.f, uA = 0.f, uB = 0.f, alA = 1.f, alB = 1.f;
+  bool rsA = false, rsB = false;
+
+  int kend = Sk;
+  if (CAUSAL) kend = min(Sk, q0 + BM2);
+  const int ntile = (kend + BN - 1) / BN;
+  const int nsub = (kend + 31) / 32;
+  // last 32-key sub-tile with a visible key for this wave (causal: keys <= wq0 + 63)
+  const int ulast = CAUSAL ? min(nsub - 1, wq0 / 32 + 1) : nsub - 1;
+
+  const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
+  // 16 1-KiB LDS-DMA pieces per tile (4 rows each), 4 per wave; K rows swizzled as k_lds_off, V
+  // rows as v_lds_off (the tr-read image)
+  auto load_k = [&](int k0, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gidx = wid * 4 + u, row = gidx * 4 + (lane >> 4);
+      const int ch = (lane & 15) ^ (row & 15);
+      const unsigned voff = (unsigned)(((long)(min(k0 + row, Sk - 1) - k0) * kstride + ch * 8) * 2);
+      fa_glds16(voff, Kb + (long)k0 * kstride, __builtin_amdgcn_readfirstlane(lds0 + slot * TILE + gidx * 1024));
+    }
+  };
+  auto load_v = [&](int k0, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gidx = wid * 4 + u, row = gidx * 4 + (lane >> 4);
+      const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const unsigned voff = (unsigned)(((long)(min(k0 + row, Sk - 1) - k0) * kstride + ch * 8) * 2);
+      fa_glds16(voff, Vb + (long)k0 * kstride,
+                __builtin_amdgcn_readfirstlane(lds0 + (2 + slot) * TILE + gidx * 1024));
+    }
+  };
+
+  const int g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  int koff[NK], troff[ND][2];
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) koff[kk] = lr * 256 + 16 * ((2 * kk + h) ^ (lr & 15));
+#pragma unroll
+  for (int db = 0; db < ND; ++db)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi)
+      troff[db][hi] = (4 * h + tq) * 256 + hi * 2048 +
+                      16 * (4 * (db ^ tq) + ((2 * (g & 1) + (tp >> 1)) ^ ((h + 2 * hi) & 3))) + 8 * (tp & 1);
+
+  // the previous sub-tile's scores per block: [0, 8) already exponentiated, [8, 16) raw
+  float pvA[16], pvB[16];
+  u32x4 pA[2], pB[2];
+  constexpr float kThr = 8.f;
+  // masked scores -> -inf (sub-tiles that straddle the causal diagonal or the key end)
+  auto mask_s = [&](float (&sv)[16], int k0, int qrow) __attribute__((always_inline)) {
+    const int base = k0 + 4 * h;
+    const int lim1 = CAUSAL ? qrow - base : 1 << 20, lim2 = Sk - base;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rb = (r & 3) + 8 * (r >> 2);
+      sv[r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : sv[r];
+    }
+  };
+
+  // top of tile t: K(t), V(t) landed, every wave done with K(t-1) and V(t-2); then issue K(t+1),
+  // V(t+1) into the freed ring slots (every wave issues its share, active or not)
+  int tsync = -1;
+  auto sync_to = [&](int t) __attribute__((always_inline)) {
+    while (tsync < t) {
+      ++tsync;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // asm DMA: untracked by the compiler
+      __syncthreads();
+      if (tsync + 1 < ntile) {
+        load_k((tsync + 1) * BN, (tsync + 1) & 1);
+        load_v((tsync + 1) * BN, (tsync + 1) % 3);
+      }
+    }
+  };
+  u32x4 kf[NK], vf[2 * ND];   // fragments read one phase ahead (one wave per SIMD: no other wave
+                              // hides an LDS read's latency)
+  auto load_kf = [&](int u) __attribute__((always_inline)) {
+    const unsigned char* kl = smem + ((u >> 1) & 1) * TILE + (u & 1) * 8192;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) kf[kk] = *reinterpret_cast<const u32x4*>(kl + koff[kk]);
+  };
+  auto load_vf = [&](int u) __attribute__((always_inline)) {
+    const unsigned char* vl = smem + (2 + ((u >> 1) % 3)) * TILE + (u & 1) * 8192;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int db = 0; db < ND; ++db) {
+        const u32x2 lo = ds_read_tr16(vl + ks * 4096 + troff[db][0]);
+        const u32x2 hi = ds_read_tr16(vl + ks * 4096 + troff[db][1]);
+        vf[ks * ND + db] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
+  };
+  // one sub-tile step: CUR = sub-tile u has visible keys for this wave, PREV = u - 1 had. The
+  // score accumulators start from an inline zero and are read out once; everything the softmax
+  // touches lives in VGPRs (no accumulator-register round trips)
+  auto step = [&](auto cur_c, auto prev_c, int u) __attribute__((always_inline)) {
+    constexpr bool CUR = decltype(cur_c)::value, PREV = decltype(prev_c)::value;
+    const int k0 = u * 32;
+    f32x16 cA, cB;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 1: QK^T of sub-tile u || finish of u - 1
+    if constexpr (CUR) {
+      cA = zero16();
+      cB = zero16();
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        cA = MF<T>::mma(as_frag<frag>(kf[kk]), qA[kk], cA);
+        cB = MF<T>::mma(as_frag<frag>(kf[kk]), qB[kk], cB);
+      }
+    }
+    if constexpr (PREV) load_vf(u - 1);   // V fragments of P(u-1) V, read under the QK^T MFMAs
+    if constexpr (PREV) {
+#pragma unroll
+      for (int r = 8; r < 16; ++r) {
+        pvA[r] = fexp2(fmaf(pvA[r], scale_log2, -uA));
+        pvB[r] = fexp2(fmaf(pvB[r], scale_log2, -uB));
+      }
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sa += pvA[r]; sb += pvB[r]; }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pA[ks][j] = MF<T>::pack(pvA[8 * ks + 2 * j], pvA[8 * ks + 2 * j + 1]);
+          pB[ks][j] = MF<T>::pack(pvB[8 * ks + 2 * j], pvB[8 * ks + 2 * j + 1]);
+        }
+      sa += __shfl_xor(sa, 32, 64);
+      sb += __shfl_xor(sb, 32, 64);
+      lA += sa;
+      lB += sb;
+    }
+    if constexpr (PHA_FA4_GROUPS && CUR && PREV) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // tile top of the next 64-key tile in the middle of an odd sub-tile, so the next sub-tile's K
+    // fragments can be read under this one's P V MFMAs
+    if ((u & 1) && ((u + 1) >> 1) < ntile) sync_to((u + 1) >> 1);
+    float sA[16], sB[16];
+    if constexpr (CUR) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sA[r] = cA[r]; sB[r] = cB[r]; }
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0)) mask_s(sA, k0, qa);
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0 + 32)) mask_s(sB, k0, qbq);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 2: P(u-1) V of sub-tile u - 1 || start of u
+    if constexpr (PREV) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int db = 0; db < ND; ++db) {
+          oA[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pA[ks]), oA[db]);
+          oB[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pB[ks]), oB[db]);
+        }
+    }
+    if constexpr (CUR) load_kf(u + 1);   // next sub-tile's K fragments, read under the P V MFMAs
+    if constexpr (CUR) {
+      float ta = -INFINITY, tb = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { ta = fmaxf(ta, sA[r]); tb = fmaxf(tb, sB[r]); }
+      ta = fmaxf(ta, __shfl_xor(ta, 32, 64)) * scale_log2;
+      tb = fmaxf(tb, __shfl_xor(tb, 32, 64)) * scale_log2;
+      rsA = !__all(ta <= mA + kThr);
+      rsB = !__all(tb <= mB + kThr);
+      const float nA = rsA ? fmaxf(mA, ta) : mA, nB = rsB ? fmaxf(mB, tb) : mB;
+      const float unA = nA == -INFINITY ? 0.f : nA, unB = nB == -INFINITY ? 0.f : nB;
+      alA = rsA ? fexp2(mA - unA) : 1.f;
+      alB = rsB ? fexp2(mB - unB) : 1.f;
+      mA = nA;
+      mB = nB;
+      uA = unA;
+      uB = unB;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        pvA[r] = fexp2(fmaf(sA[r], scale_log2, -uA));
+        pvB[r] = fexp2(fmaf(sB[r], scale_log2, -uB));
+        pvA[8 + r] = sA[8 + r];
+        pvB[8 + r] = sB[8 + r];
+      }
+    }
+    if constexpr (PHA_FA4_GROUPS && CUR && PREV) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (CUR) {   // a raised running max rescales O after P(u-1) V, before P(u) V
+      lA *= alA;
+      lB *= alB;
+      if (rsA) {
+        asm volatile("" ::: "memory");   // keep the (rare) rescale a branch, not a multiply per step
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oA[i][r] *= alA;
+      }
+      if (rsB) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oB[i][r] *= alB;
+      }
+    }
+  };
+
+  // steady sub-tile (CUR and PREV): MFMAs, LDS reads and softmax VALU placed slot by slot
+  // behind sched_barrier fences (the compiler's own schedule issues the MFMAs as one burst and
+  // the VALU after it — no overlap at one wave per SIMD): per slot the A and B MFMAs, one or two
+  // operand reads for the next phase and ~10 VALU
+  auto step_steady = [&](int u) __attribute__((always_inline)) {
+    f32x16 cA = zero16(), cB = zero16();
+    float sa = 0.f, sb = 0.f;
+    const unsigned char* vl = smem + (2 + (((u - 1) >> 1) % 3)) * TILE + ((u - 1) & 1) * 8192;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 1: QK^T of u || finish of u - 1 || V fragments of u - 1
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      cA = MF<T>::mma(as_frag<frag>(kf[j]), qA[j], cA);
+      {
+        const int ks = j >> 2, db = j & 3;
+        const u32x2 lo = ds_read_tr16(vl + ks * 4096 + troff[db][0]);
+        const u32x2 hi = ds_read_tr16(vl + ks * 4096 + troff[db][1]);
+        vf[j] = u32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
+      pvA[8 + j] = fexp2(fmaf(pvA[8 + j], scale_log2, -uA));
+      sa += pvA[j];
+      sa += pvA[8 + j];
+      if (j & 1) {
+        const int e = 2 * (j >> 1);   // pack units of elements e, e+1 (ready) and 8+e, 9+e (just done)
+        pA[0][j >> 1] = MF<T>::pack(pvA[e], pvA[e + 1]);
+        pA[1][j >> 1] = MF<T>::pack(pvA[8 + e], pvA[9 + e]);
+      }
+      cB = MF<T>::mma(as_frag<frag>(kf[j]), qB[j], cB);
+      pvB[8 + j] = fexp2(fmaf(pvB[8 + j], scale_log2, -uB));
+      sb += pvB[j];
+      sb += pvB[8 + j];
+      if (j & 1) {
+        const int e = 2 * (j >> 1);
+        pB[0][j >> 1] = MF<T>::pack(pvB[e], pvB[e + 1]);
+        pB[1][j >> 1] = MF<T>::pack(pvB[8 + e], pvB[9 + e]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    sa += __shfl_xor(sa, 32, 64);
+    sb += __shfl_xor(sb, 32, 64);
+    lA += sa;
+    lB += sb;
+    if ((u & 1) && ((u + 1) >> 1) < ntile) sync_to((u + 1) >> 1);
+    {   // sub-tiles straddling the causal diagonal or the key end (the last one or two per wave)
+      const int k0 = u * 32;
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0)) {
+        const int base = k0 + 4 * h;
+        const int la = CAUSAL ? qa - base : 1 << 20, lb = CAUSAL ? qbq - base : 1 << 20, l2 = Sk - base;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rb = (r & 3) + 8 * (r >> 2);
+          cA[r] = ((rb > la) | (rb >= l2)) ? -INFINITY : cA[r];
+          cB[r] = ((rb > lb) | (rb >= l2)) ? -INFINITY : cB[r];
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 2: P(u-1) V || start of u || K fragments of u + 1
+    const unsigned char* kl = smem + (((u + 1) >> 1) & 1) * TILE + ((u + 1) & 1) * 8192;
+    float ta = -INFINITY, tb = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ks = j >> 2, db = j & 3;
+      oA[db] = MF<T>::mma(as_frag<frag>(vf[j]), as_frag<frag>(pA[ks]), oA[db]);
+      kf[j] = *reinterpret_cast<const u32x4*>(kl + koff[j]);
+      if (j < 4) {
+        ta = fmaxf(ta, fmaxf(fmaxf(cA[4 * j], cA[4 * j + 1]), fmaxf(cA[4 * j + 2], cA[4 * j + 3])));
+        tb = fmaxf(tb, fmaxf(fmaxf(cB[4 * j], cB[4 * j + 1]), fmaxf(cB[4 * j + 2], cB[4 * j + 3])));
+      }
+      if (j == 4) {
+        ta = fmaxf(ta, __shfl_xor(ta, 32, 64)) * scale_log2;
+        tb = fmaxf(tb, __shfl_xor(tb, 32, 64)) * scale_log2;
+        rsA = !__all(ta <= mA + kThr);
+        rsB = !__all(tb <= mB + kThr);
+        const float nA = rsA ? fmaxf(mA, ta) : mA, nB = rsB ? fmaxf(mB, tb) : mB;
+        const float unA = nA == -INFINITY ? 0.f : nA, unB = nB == -INFINITY ? 0.f : nB;
+        alA = rsA ? fexp2(mA - unA) : 1.f;
+        alB = rsB ? fexp2(mB - unB) : 1.f;
+        mA = nA;
+        mB = nB;
+        uA = unA;
+        uB = unB;
+      }
+      if (j >= 4) {
+        const int r = 2 * (j - 4);
+        pvA[r] = fexp2(fmaf(cA[r], scale_log2, -uA));
+        pvA[r + 1] = fexp2(fmaf(cA[r + 1], scale_log2, -uA));
+        pvA[8 + r] = cA[8 + r];
+        pvA[9 + r] = cA[9 + r];
+      }
+      oB[db] = MF<T>::mma(as_frag<frag>(vf[j]), as_frag<frag>(pB[ks]), oB[db]);
+      if (j >= 4) {
+        const int r = 2 * (j - 4);
+        pvB[r] = fexp2(fmaf(cB[r], scale_log2, -uB));
+        pvB[r + 1] = fexp2(fmaf(cB[r + 1], scale_log2, -uB));
+        pvB[8 + r] = cB[8 + r];
+        pvB[9 + r] = cB[9 + r];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lA *= alA;
+    lB *= alB;
+    if (rsA) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oA[i][r] *= alA;
+    }
+    if (rsB) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oB[i][r] *= alB;
+    }
+  };
+
+  using TT = std::true_type;
+  using FF = std::false_type;
+
+  if (ntile > 0) {
+    load_k(0, 0);
+    load_v(0, 0);
+    // first sub-tile, the steady loop (a tile-top sync before every even sub-tile), the drain, then
+    // the causal tail (barriers / DMAs only). Per-iteration variants inside the loop body make the
+    // register allocator spill, hence the peeled first and last steps.
+    sync_to(0);
+    load_kf(0);
+    step(TT{}, FF{}, 0);
+    int u = 1;
+    if (PHA_FA4_SLOTS)
+      for (; u <= ulast; ++u) step_steady(u);
+    else
+      for (; u <= ulast; ++u) step(TT{}, TT{}, u);
+    step(FF{}, TT{}, u);
+    sync_to(ntile - 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA left in flight at exit
+
+  auto store = [&](const f32x16 (&o)[ND], float l, float m, int q) __attribute__((always_inline)) {
+    if (q >= S) return;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    T* orow = O + ((long)b * S + q) * fs.o_tok + (long)head * fs.o_head;
+#pragma unroll
+    for (int db = 0; db < ND; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(o[db][4 * gg + 0] * inv, o[db][4 * gg + 1] * inv);
+        w[1] = MF<T>::pack(o[db][4 * gg + 2] * inv, o[db][4 * gg + 3] * inv);
+        *reinterpret_cast<u32x2*>(orow + d) = w;
+      }
+    if (h == 0) LSE[((long)b * H + head) * S + q] = (l > 0.f) ? (m + log2f(l)) * kLn2 : INFINITY;
+  };
+  store(oA, lA, mA, qa);
+  store(oB, lB, mB, qbq);
+}
+
 // delta[b,h,q] = sum_d dO * O  (fp32)
 template <typename T, int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(const T* __restrict__ O, const T* __restrict__ dO,
@@ -1952,6 +2391,11 @@ bool fwd_v3() {  // PHA_FA_FWD=v2 selects the register-staged forward kernel (A/
   return !(e && e[0] == 'v' && e[1] == '2');
 }
 
+bool fwd_v4() {  // PHA_FA_FWD=v4: the 4-wave software-pipelined forward
+  const char* e = getenv("PHA_FA_FWD");
+  return e && e[0] == 'v' && e[1] == '4';
+}
+
 bool dq_v3() {  // PHA_FA_DQ=v2 selects the register-staged dQ kernel (A/B comparisons)
   const char* e = getenv("PHA_FA_DQ");
   return !(e && e[0] == 'v' && e[1] == '2');
@@ -1989,7 +2433,12 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
   if (fsp && !v2) return (int)hipErrorInvalidValue;
   if (v2) {
     const dim3 g2(B * H, (S + BM2 - 1) / BM2), b2(NT2);
-    if (fwd_v3() && causal)
+    if (fwd_v4()) {
+      if (causal)
+        hipLaunchKernelGGL((fa_fwd_v4_kernel<T, true>), g2, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
+      else
+        hipLaunchKernelGGL((fa_fwd_v4_kernel<T, false>), g2, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
+    } else if (fwd_v3() && causal)
       hipLaunchKernelGGL((fa_fwd_v3_kernel<T, true>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);
     else if (fwd_v3())
       hipLaunchKernelGGL((fa_fwd_v3_kernel<T, false>), g2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk, H, Hk, sl, fs);

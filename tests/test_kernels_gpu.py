@@ -377,10 +377,33 @@ def test_flash_attention_fwd_v2_v3(causal, S, Sk, monkeypatch):
     k = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16()
     v = torch.randn(B, Sk, Hk, D, device="cuda").bfloat16()
     ref = _ref_attn(q, k, v, causal)
-    for mode in ("v2", "v3"):
+    for mode in ("v2", "v3", "v4"):
         monkeypatch.setenv("PHA_FA_FWD", mode)
         o = hip.FlashAttention.apply(q, k, v, causal, None)
         assert (o.float() - ref).abs().max().item() < 2e-2, mode
+
+
+@pytest.mark.parametrize("causal,S,Sk", [(True, 1100, 1100), (False, 700, 1300), (True, 2048, 2048)])
+def test_flash_attention_fwd_v4_lse_and_grads(causal, S, Sk, monkeypatch):
+    """the software-pipelined forward (v4): output vs fp32, and the backward that consumes its LSE
+    gives v3's gradients"""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(4)
+    B, H, D = 1, 4, 128
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    k = torch.randn(B, Sk, H, D, device="cuda").bfloat16()
+    v = torch.randn(B, Sk, H, D, device="cuda").bfloat16()
+    do = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    res = {}
+    for mode in ("v3", "v4"):
+        monkeypatch.setenv("PHA_FA_FWD", mode)
+        qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+        o = hip.FlashAttention.apply(qq, kk, vv, causal, None)
+        res[mode] = (o.detach(), *torch.autograd.grad(o, (qq, kk, vv), do))
+    ref = _ref_attn(q, k, v, causal)
+    assert (res["v4"][0].float() - ref).abs().max().item() < 2e-2
+    for a, b in zip(res["v4"], res["v3"]):
+        assert (a.float() - b.float()).abs().max().item() < 2e-2 * max(1.0, b.float().abs().max().item())
 
 
 def test_flash_attention_gqa():
