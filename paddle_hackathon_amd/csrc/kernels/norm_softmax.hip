@@ -584,6 +584,17 @@ void col_sum(float* part, W* out, int P, int H, hipStream_t stream) {
   }
 }
 
+// [P, H] fp32 row partials -> [H] column sums in dt (a bias gradient's last step); part needs
+// P + 8 rows (the chip-wide first stage writes rows [P, P + 8))
+PHA_API int pha_col_sum_rows(int dt, float* part, void* out, int P, int H, hipStream_t stream) {
+  if (P <= 0 || H <= 0) return (int)hipErrorInvalidValue;
+  if (dt == kF32) col_sum<float>(part, (float*)out, P, H, stream);
+  else if (dt == kBF16) col_sum<bf16_t>(part, (bf16_t*)out, P, H, stream);
+  else if (dt == kF16) col_sum<half_t>(part, (half_t*)out, P, H, stream);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
 // part_w / part_b: workspace [nblocks + 8, H] fp32 each (nblocks = pha_layer_norm_bwd_nblocks;
 // the last 8 rows are the column-sum stage);
 // dw/db outputs (may be null db); dres (optional): gradient of the fused residual sum, added to dx.

@@ -34,6 +34,7 @@ def _L():
             "pha_layer_norm_bwd2": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
             "pha_layer_norm_bwd3": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
             "pha_bdrln_fwd2": [I, I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
+            "pha_col_sum_rows": [I, P, P, I, I, P],
             "pha_bdrln_fwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
             "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
@@ -291,12 +292,13 @@ def bias_gelu_bwd(gy, x, b, approximate):
         gx = torch.empty_like(x)
         rows = n // H
         rpb = max(16, -(-rows // 512))   # >= 2048 blocks at 16384 x 8192: 8 per CU for streaming
-        part = torch.empty((-(-rows // rpb), H), dtype=torch.float32, device=x.device)
+        P = -(-rows // rpb)
+        part = torch.empty((P + 8, H), dtype=torch.float32, device=x.device)   # + column-sum stage rows
         L = _L()
         L.pha_bias_gelu_bwd_db.restype = c_int
         _check(L.pha_bias_gelu_bwd_db(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), _ptr(part), c_int(rows),
                                       c_int(H), c_int(rpb), c_int(int(approximate)), _stream(x)), "bias_gelu_bwd_db")
-        return gx, part.sum(0).to(b.dtype)
+        return gx, _col_sum_rows(part, P, b.dtype)
     else:
         gx = torch.empty_like(x)
         _check(_L().pha_bias_gelu_bwd(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), n, H, int(approximate), _stream(x)), "bias_gelu_bwd")
@@ -311,12 +313,24 @@ def col_sum(gy2d, out_dtype=None):
     if gy2d.dtype == torch.float32 or H % 8 or not gy2d.is_contiguous():
         return gy2d.sum(0, dtype=torch.float32).to(out_dtype or gy2d.dtype)
     rpb = max(16, -(-rows // 512))
-    part = torch.empty((-(-rows // rpb), H), dtype=torch.float32, device=gy2d.device)
+    P = -(-rows // rpb)
+    part = torch.empty((P + 8, H), dtype=torch.float32, device=gy2d.device)   # + column-sum stage rows
     L = _L()
     L.pha_col_sum_partial.restype = c_int
     _check(L.pha_col_sum_partial(_DT[gy2d.dtype], _ptr(gy2d), _ptr(part), c_int(rows), c_int(H), c_int(rpb),
                                  _stream(gy2d)), "col_sum_partial")
-    return part.sum(0).to(out_dtype or gy2d.dtype)
+    return _col_sum_rows(part, P, out_dtype or gy2d.dtype)
+
+
+def _col_sum_rows(part, P, dtype):
+    """column sums of the first P rows of the fp32 partials ``part`` ([P + 8, H]: the last rows are
+    the kernel's first-stage workspace) into a new [H] tensor of ``dtype``"""
+    H = part.shape[1]
+    if dtype not in _DT or not hasattr(_L(), "pha_col_sum_rows"):
+        return part[:P].sum(0).to(dtype)
+    out = torch.empty(H, dtype=dtype, device=part.device)
+    _check(_L().pha_col_sum_rows(_DT[dtype], _ptr(part), _ptr(out), P, H, _stream(part)), "col_sum_rows")
+    return out
 
 
 class MaxPool2dNHWC(torch.autograd.Function):
