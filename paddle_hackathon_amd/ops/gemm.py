@@ -382,7 +382,10 @@ def _splits(M, N, K, dev):
     """split-K factor for a weight gradient: the smallest power of two (<= 16, dividing the K-tiles)
     whose work items fill the chip's rounds to >= 95 % (tiles x splits over whole multiples of the
     CU count: GPT-1.3B's qkv dW has 192 tiles — split 2 would run 384 items in two rounds, 75 %
-    busy; split 4 runs 768 in three full rounds); grids of >= 2 rounds already stay unsplit"""
+    busy; split 4 runs 768 in three full rounds); grids of >= 2 rounds already stay unsplit, and so
+    do grids of >= 3/4 of a round: the qkv dW's 192 tiles unsplit beat split 4 (714 vs 739 us
+    sustained, profiles/tn_wgrad_r5/tn_sustain.log — the slabs' fp32 traffic and the reduce cost
+    more than the idle quarter)"""
     tiles = -(-M // 256) * -(-N // 256)
     cus = _num_cus(dev)
     ktiles = K // 64
@@ -390,7 +393,7 @@ def _splits(M, N, K, dev):
     def eff(sp):
         items = tiles * sp
         return items / (-(-items // cus) * cus)
-    if tiles >= 2 * cus:
+    if tiles >= 2 * cus or 4 * tiles >= 3 * cus:
         return 1
     sp = 1
     while (tiles * sp < cus or eff(sp) < 0.95) and sp < 16 and ktiles % (sp * 2) == 0 and ktiles // (sp * 2) >= 4:
