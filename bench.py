@@ -55,9 +55,11 @@ def _args():
                     help="GPT: group-sharded data parallelism over the gpus / (tp * pp) data ranks (1: optimizer "
                          "state, 2: + gradients, 3: + parameters); composes with --pp (BASELINE config 5: "
                          "--model gpt3-13b --pp 2 --sharding-stage 3 --recompute on 8 GPUs)")
-    ap.add_argument("--gemm-tuning", default="db", choices=["db", "tune", "off"],
-                    help="db: load the in-tree hipBLASLt solution database (TunableOp, no tuning); "
-                         "tune: benchmark solutions for new shapes and write the database; off: library heuristics")
+    ap.add_argument("--gemm-tuning", default="off", choices=["db", "tune", "off"],
+                    help="off (default): the library heuristics for the products the static policy leaves on "
+                         "hipBLASLt; db: load the in-tree TunableOp solution database (within noise of off: "
+                         "124.4 / 123.4k vs 124.2 / 122.9k tokens/s alternating on one box, "
+                         "profiles/gemm_tuning_db_ab_r5.txt); tune: benchmark solutions and write the database")
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
