@@ -975,18 +975,21 @@ def _bn_bwd_on():
     return _bn_stats_on() and os.environ.get("PHA_CONV_BN_BWD", "0") == "1"
 
 
-def res_route_begin(x):
+def res_route_begin(x, kind="bn"):
     """Residual-gradient route for a residual block whose input ``x`` (torch tensor) feeds exactly
-    two ops: the block's first convolution and, as ``residual``, the fused BN-add-ReLU that ends the
-    block. Autograd would add the two gradients of x in a separate pass; with the route, the BN's
-    backward hands its residual gradient over and the convolution's dgrad epilogue adds it (one
-    fewer read + write of the activation gradient per block). Returns the route token (or None
-    when not applicable); call ``res_route_end`` after the block's forward."""
+    two ops: the block's first convolution and (kind "bn") as ``residual`` the fused BN-add-ReLU that
+    ends the block, or (kind "conv") the downsample shortcut's convolution. Autograd would add the
+    two gradients of x in a separate pass; with the route, the other consumer's backward hands its
+    gradient of x over and the first convolution's dgrad epilogue adds it (one fewer read + write of
+    the activation gradient per block). Returns the route token (or None when not applicable); call
+    ``res_route_end`` after the block's forward."""
     import os
     if os.environ.get("PHA_RES_ROUTE", "1") == "0" or not torch.is_grad_enabled() or not x.requires_grad \
             or not x.is_cuda or x.dtype not in _DT or x.dim() != 4:
         return None
-    route = {"armed": False}
+    if kind == "conv" and os.environ.get("PHA_RES_ROUTE_CONV", "1") == "0":
+        return None
+    route = {"armed": False, "kind": kind}
     x._pha_res_route = route
     return route
 
@@ -1008,10 +1011,14 @@ class Conv2dNHWC256(torch.autograd.Function):
     def forward(ctx, x, weight, bias, stride, padding, dilation):
         ctx.save_for_backward(x)
         route = getattr(x, "_pha_res_route", None)   # first conv of a routed residual block
-        ctx.route = None
+        ctx.route = ctx.route_src = None
         if route is not None and not route.get("armed"):
             route["armed"] = True
             ctx.route = route
+        elif route is not None and route.get("kind") == "conv" and not route.get("sink"):
+            # the downsample shortcut's conv: hands its dx to the armed first conv's dgrad epilogue
+            route["sink"] = True
+            ctx.route_src = route
         ctx.weight = weight   # the parameter object itself (a leaf input): its layout cache entries match
         ctx.conf = (stride, padding, dilation, bias is not None)
         src = getattr(x, "_pha_bn_src", None)   # x is a batch norm's output: fuse its backward sums
@@ -1030,9 +1037,15 @@ class Conv2dNHWC256(torch.autograd.Function):
         gy = gy.contiguous()
         route = ctx.route
         addend = route.pop("g", None) if route is not None and route.get("sink") else None
+        if route is not None:
+            route["done"] = True
         dx = conv256_dgrad(gy, weight, x.shape, stride, padding, dilation,
                            bn_src=ctx.bn_src if _bn_bwd_on() else None,
                            addend=addend) if ctx.needs_input_grad[0] else None
+        src = ctx.route_src
+        if src is not None and dx is not None and not src.get("done"):
+            src["g"] = dx   # the first conv's dgrad (still to run) adds it in its epilogue
+            dx = None
         dw = conv256_wgrad(gy, x, weight.shape, stride, padding, dilation) if ctx.needs_input_grad[1] else None
         db = gy.float().sum((0, 1, 2)).to(gy.dtype) if has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None

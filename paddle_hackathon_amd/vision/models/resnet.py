@@ -80,8 +80,10 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        # identity block: conv1 adds the residual gradient in its dgrad epilogue (conv_gemm.res_route_begin)
-        route = _conv_gemm.res_route_begin(x._t) if self.downsample is None and self.training else None
+        # conv1 adds x's other gradient in its dgrad epilogue (conv_gemm.res_route_begin): the residual
+        # gradient of an identity block, the shortcut conv's dx of a downsample block
+        route = _conv_gemm.res_route_begin(x._t, "bn" if self.downsample is None else "conv") if self.training \
+            else None
         try:
             out = _bn_act(self.bn1, self.conv1(x))
             out = _bn_act(self.bn2, self.conv2(out))

@@ -1246,6 +1246,48 @@ def test_resnet_residual_grad_route(monkeypatch):
         assert (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-6
 
 
+@pytest.mark.parametrize("stride", [1, 2])
+def test_resnet_shortcut_grad_route(monkeypatch, stride):
+    """downsample bottleneck: the shortcut conv's dx is handed to conv1, whose dgrad epilogue adds
+    it (no autograd add of the two gradients of the block input); gradients equal the unrouted sum"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd import nn
+    from paddle_hackathon_amd.ops import conv_gemm
+    from paddle_hackathon_amd.vision.models.resnet import BottleneckBlock
+    paddle.set_device("gpu:0")
+    seen = []
+    orig = conv_gemm.conv256_dgrad
+
+    def spy(*a, **k):
+        seen.append(k.get("addend") is not None)
+        return orig(*a, **k)
+    monkeypatch.setattr(conv_gemm, "conv256_dgrad", spy)
+    results = []
+    for route in ("1", "0"):
+        monkeypatch.setenv("PHA_RES_ROUTE", route)
+        seen.clear()
+        paddle.seed(6)
+        ds = nn.Sequential(nn.Conv2D(64, 128, 1, stride=stride, bias_attr=False, data_format="NHWC"),
+                           nn.BatchNorm2D(128, data_format="NHWC"))
+        blk = BottleneckBlock(64, 32, stride=stride, downsample=ds, data_format="NHWC")
+        blk = paddle.amp.decorate(blk, level="O2", dtype="bfloat16")
+        blk.train()
+        g = torch.Generator("cuda").manual_seed(10)
+        xt = torch.randn(4, 14, 14, 64, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        x = paddle.Tensor(xt)
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            y = blk(x)
+        (y.astype("float32") ** 2).mean().backward()
+        results.append([xt.grad.float().clone()] + [p._t.grad.float().clone() for p in blk.parameters()
+                                                     if p._t.grad is not None])
+        if route == "1":
+            assert any(seen), "conv1's dgrad did not receive the shortcut conv's gradient"
+        else:
+            assert not any(seen)
+    for a, b in zip(*results):
+        assert (a - b).abs().max() <= 2e-2 * b.abs().max() + 1e-6
+
+
 def test_conv_dgrad_addend():
     """the conv epilogue addend: dgrad(dy) + r in one launch equals dgrad(dy) + r"""
     from paddle_hackathon_amd.ops import conv_gemm
