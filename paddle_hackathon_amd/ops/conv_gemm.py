@@ -491,7 +491,7 @@ def conv256_dgrad(dy, w, x_shape, stride, padding, dilation, bn_src=None, addend
             dx._pha_bn_bwd = (bn[1], bn[2], bn[0][3], dx._version)
         return dx
     if (sh, sw) == (1, 1):
-        wt = _wlayout(w, "dgrad", lambda t: t.flip(2, 3).permute(1, 2, 3, 0).contiguous())   # [Ci][KH][KW][Co]
+        wt = _wlayout(w, "dgrad", lambda t: _flip_hw(t).permute(1, 2, 3, 0).contiguous())   # [Ci][KH][KW][Co]
         dx = torch.empty(N, H, W, Ci, dtype=dy.dtype, device=dy.device)
         return _done(_run(dy, wt, (1, 1), (dh * (KH - 1) - ph, dw * (KW - 1) - pw), (dh, dw), out=dx,
                           remap=(0, 0, 1, 1, H, W), addend=addend))
@@ -830,6 +830,11 @@ def conv2d_nhwc256_grouped(x, weight, bias, stride, padding, dilation, groups):
 
 def conv2d_nhwc256_f32(x, weight, bias, stride, padding, dilation):
     return Conv2dNHWC256F32.apply(x, weight, bias, tuple(stride), tuple(padding), tuple(dilation))
+
+
+def _flip_hw(t):
+    """the filter's spatial flip (a no-op, and no kernel, for 1x1 filters)"""
+    return t if t.shape[2] == 1 and t.shape[3] == 1 else t.flip(2, 3)
 
 
 def _wlayout(w, kind, make):
