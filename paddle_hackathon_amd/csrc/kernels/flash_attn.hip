@@ -2066,10 +2066,14 @@ __global__ __launch_bounds__(NTKV) __attribute__((amdgpu_waves_per_eu(1, 1))) vo
 // probability loop is one code path with no selects), and each 32-key block's 16 row reads issued
 // ahead of its MFMAs (one LDS latency per block).
 template <typename T, bool CAUSAL>
+// Od (optional): the forward output — delta = rowsum(dO * O) is then formed here from the dO
+// fragments already in registers and stored to DELTA for the dK/dV kernel launched after this one
+// (no separate preprocess pass re-reading dO).
 __global__ __launch_bounds__(NT2) void fa_bwd_dq_v3(const T* __restrict__ Q, const T* __restrict__ K,
                                                     const T* __restrict__ V, const T* __restrict__ dO,
-                                                    const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale, FaStrides fs) {
+                                                    const float* __restrict__ LSE, float* __restrict__ DELTA,
+                                                    T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale, FaStrides fs,
+                                                    const T* __restrict__ Od = nullptr) {
   typedef typename MF<T>::frag frag;
   constexpr int NK = 8, ND = 4;
   constexpr int IMG = BN * 256;
@@ -2094,7 +2098,6 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v3(const T* __restrict__ Q, con
   const T* Vb = V + (long)b * Sk * kstride + (long)hk * fs.kv_head;
   const float scale_log2 = scale * kLog2e;
   const float lse2 = (q < S) ? LSE[((long)b * H + head) * S + q] * kLog2e : 0.f;
-  const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
 
   frag qf[NK], gf[NK];
 #pragma unroll
@@ -2106,6 +2109,23 @@ __global__ __launch_bounds__(NT2) void fa_bwd_dq_v3(const T* __restrict__ Q, con
     }
     qf[kk] = as_frag<frag>(a);
     gf[kk] = as_frag<frag>(c);
+  }
+  float dlt;
+  if (Od) {   // O shares dO's strides (both dense [B, S, H, D] outputs)
+    const T* Ob = Od + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+    float sdl = 0.f;
+    if (q < S) {
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const frag of = as_frag<frag>(*reinterpret_cast<const u32x4*>(Ob + (long)q * fs.o_tok + 16 * kk + 8 * h));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sdl += (float)gf[kk][i] * (float)of[i];
+      }
+    }
+    dlt = sdl + __shfl_xor(sdl, 32, 64);
+    if (h == 0 && q < S) DELTA[((long)b * H + head) * S + q] = dlt;
+  } else {
+    dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
   }
   f32x16 dq[ND];
 #pragma unroll
@@ -2461,7 +2481,7 @@ int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
 template <typename T>
 int launch_bwd(const void* q, const void* k, const void* v, const void* dout, const float* lse, const float* delta,
                void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, int D, float scale, int causal,
-               hipStream_t st, const FaStrides* fsp = nullptr) {
+               hipStream_t st, const FaStrides* fsp = nullptr, const void* o = nullptr) {
   FaStrides fs = fsp ? *fsp : dense_strides(H, Hk, D);
   fs.order_g = fa_order_g();
   fs.prio = fa_prio();
@@ -2480,10 +2500,25 @@ int launch_bwd(const void* q, const void* k, const void* v, const void* dout, co
                        (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                       \
     if (dq_v3())                                                                                                   \
       hipLaunchKernelGGL((fa_bwd_dq_v3<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
-                         (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs);                             \
+                         (const T*)dout, lse, const_cast<float*>(delta), (T*)dq, S, Sk, H, Hk, scale, fs);        \
     else                                                                                                           \
       hipLaunchKernelGGL((fa_bwd_dq_v2<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
                          (const T*)dout, lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs)
+    if (o && dq_v3()) {   // delta formed inside dQ (launched first), then read by dK/dV
+#define FB3(CC)                                                                                                    \
+      hipLaunchKernelGGL((fa_bwd_dq_v3<T, CC>), gq2, b2, 0, st, (const T*)q, (const T*)k, (const T*)v,            \
+                         (const T*)dout, lse, const_cast<float*>(delta), (T*)dq, S, Sk, H, Hk, scale, fs,         \
+                         (const T*)o);                                                                             \
+      if (dkdv_v3())                                                                                               \
+        hipLaunchKernelGGL((fa_bwd_dkdv_v3<T, CC>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,        \
+                           (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs);                   \
+      else                                                                                                         \
+        hipLaunchKernelGGL((fa_bwd_dkdv_v2<T, CC, true>), gk2, bk, 0, st, (const T*)q, (const T*)k, (const T*)v,  \
+                           (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs)
+      if (causal) { FB3(true); } else { FB3(false); }
+#undef FB3
+      return (int)hipGetLastError();
+    }
     if (causal) { FB2(true); } else { FB2(false); }
 #undef FB2
     return (int)hipGetLastError();
@@ -2619,6 +2654,36 @@ PHA_API int pha_flash_attn_bwd(int dt, const void* q, const void* k, const void*
   if (H % Hk || (D != 64 && D != 128 && D != 256) || B <= 0 || S <= 0 || Sk <= 0) return (int)hipErrorInvalidValue;
   if (dt == kBF16) return launch_bwd<bf16_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
   if (dt == kF16) return launch_bwd<half_t>(q, k, v, dout, lse, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+// pha_flash_attn_bwd_packed with o: the row constants delta = rowsum(dO * O) are formed inside the
+// dQ kernel (launched before dK/dV) into `delta` (scratch [B, H, S] fp32) instead of by the
+// separate preprocess pass; falls back to preprocess + the two kernels when the v3 kernels are off
+PHA_API int pha_flash_attn_bwd_packed_od(int dt, const void* qkv, const void* o, const void* dout, const float* lse,
+                                         float* delta, void* dqkv, int B, int S, int H, int D, float scale, int causal,
+                                         hipStream_t stream) {
+  if (D != 128 || S <= 0) return (int)hipErrorInvalidValue;
+  FaStrides f;
+  f.order_g = 0;
+  f.q_tok = f.kv_tok = f.dq_tok = f.dkv_tok = 3L * H * D;
+  f.q_head = f.kv_head = f.dq_head = f.dkv_head = 3 * D;
+  f.o_tok = (long)H * D;
+  f.o_head = D;
+  const bool inq = bwd_v2_enabled() && dq_v3() && !getenv("PHA_FA_DELTA_PASS");
+  if (!inq) {
+    const int rc = pha_flash_attn_bwd_preprocess(dt, o, dout, delta, B, S, H, D, stream);
+    if (rc) return rc;
+  }
+  const size_t es = 2;
+  const char* in = static_cast<const char*>(qkv);
+  char* out = static_cast<char*>(dqkv);
+  if (dt == kBF16)
+    return launch_bwd<bf16_t>(in, in + D * es, in + 2 * D * es, dout, lse, delta, out, out + D * es, out + 2 * D * es, B,
+                              S, S, H, H, D, scale, causal, stream, &f, inq ? o : nullptr);
+  if (dt == kF16)
+    return launch_bwd<half_t>(in, in + D * es, in + 2 * D * es, dout, lse, delta, out, out + D * es, out + 2 * D * es, B,
+                              S, S, H, H, D, scale, causal, stream, &f, inq ? o : nullptr);
   return (int)hipErrorInvalidValue;
 }
 

@@ -882,6 +882,14 @@ class FlashAttentionPacked(torch.autograd.Function):
         L.pha_flash_attn_bwd_packed.restype = c_int
         delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
         dqkv = torch.empty_like(qkv)
+        if not _bwd_fused(D) and hasattr(L, "pha_flash_attn_bwd_packed_od"):
+            # delta = rowsum(dO * O) formed inside the dQ kernel (no separate preprocess pass)
+            L.pha_flash_attn_bwd_packed_od.restype = c_int
+            _check(L.pha_flash_attn_bwd_packed_od(c_int(_DT[qkv.dtype]), _ptr(qkv), _ptr(o), _ptr(do), _ptr(lse),
+                                                  _ptr(delta), _ptr(dqkv), c_int(B), c_int(S), c_int(H), c_int(D),
+                                                  c_float(ctx.scale), c_int(int(ctx.causal)), _stream(qkv)),
+                   "flash_attn_bwd_packed_od")
+            return dqkv, None, None
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[qkv.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B),
                                                c_int(S), c_int(H), c_int(D), _stream(qkv)), "flash_attn_bwd_preprocess")
         if _bwd_fused(D):

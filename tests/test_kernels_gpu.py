@@ -383,6 +383,30 @@ def test_flash_attention_fwd_v2_v3(causal, S, Sk, monkeypatch):
         assert (o.float() - ref).abs().max().item() < 2e-2, mode
 
 
+@pytest.mark.parametrize("causal,S", [(True, 1100), (False, 520)])
+def test_flash_attention_packed_delta_in_dq(causal, S, monkeypatch):
+    """packed backward with delta = rowsum(dO * O) formed inside the dQ kernel (launched before dK/dV)
+    against the separate preprocess pass (PHA_FA_DELTA_PASS=1) and fp32 SDPA"""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(12)
+    B, H, D = 2, 4, 128
+    qkv = torch.randn(B, S, H, 3 * D, device="cuda").bfloat16()
+    do = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    res = {}
+    for mode in ("inq", "pass"):
+        if mode == "pass":
+            monkeypatch.setenv("PHA_FA_DELTA_PASS", "1")
+        a = qkv.clone().requires_grad_()
+        o = hip.FlashAttentionPacked.apply(a, causal, None)
+        (res[mode],) = torch.autograd.grad(o, a, do)
+    assert (res["inq"].float() - res["pass"].float()).abs().max().item() < 1e-2 * res["pass"].float().abs().max().item()
+    qf = qkv.float().requires_grad_()
+    q, k, v = (t.transpose(1, 2) for t in qf.split(D, dim=-1))
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal).transpose(1, 2)
+    (gref,) = torch.autograd.grad(ref, qf, do.float())
+    assert (res["inq"].float() - gref).abs().max().item() < 3e-2 * gref.abs().max().item()
+
+
 @pytest.mark.parametrize("causal,S,Sk", [(True, 1100, 1100), (False, 700, 1300), (True, 2048, 2048)])
 def test_flash_attention_fwd_v4_lse_and_grads(causal, S, Sk, monkeypatch):
     """the software-pipelined forward (v4): output vs fp32, and the backward that consumes its LSE
