@@ -731,8 +731,12 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
   const int head = bh % H, b = bh / H;
   const int hk = head / (H / Hk);
   const int q0 = qb * BM2;
-  const int wq0 = q0 + wid * 64;               // block A rows wq0 + [0, 32), block B rows wq0 + 32 + [0, 32)
-  const int qa = wq0 + lr, qbq = wq0 + 32 + lr;
+  // block A rows rA0 + [0, 32) in the workgroup's lower half, block B rows rB0 + [0, 32) mirrored in
+  // the upper half (wave 0: rows 0-31 and 224-255, wave 3: 96-127 and 128-159): under the causal
+  // mask every wave then has the same work — A's keys end where B's are still running, and the
+  // steps after A's last run B alone at half the cost
+  const int rA0 = q0 + 32 * wid, rB0 = q0 + BM2 - 32 - 32 * wid;
+  const int qa = rA0 + lr, qbq = rB0 + lr;
   const long qstride = fs.q_tok, kstride = fs.kv_tok;
   const T* Qb = Q + ((long)b * S) * qstride + (long)head * fs.q_head;
   const T* Kb = K + ((long)b * Sk) * kstride + (long)hk * fs.kv_head;
@@ -757,8 +761,9 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
   if (CAUSAL) kend = min(Sk, q0 + BM2);
   const int ntile = (kend + BN - 1) / BN;
   const int nsub = (kend + 31) / 32;
-  // last 32-key sub-tile with a visible key for this wave (causal: keys <= wq0 + 63)
-  const int ulast = CAUSAL ? min(nsub - 1, wq0 / 32 + 1) : nsub - 1;
+  // last 32-key sub-tile with a visible key for block A / B (causal: keys <= the block's last row)
+  const int uA_last = CAUSAL ? min(nsub - 1, (rA0 + 31) / 32) : nsub - 1;
+  const int uB_last = CAUSAL ? min(nsub - 1, (rB0 + 31) / 32) : nsub - 1;
 
   const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)smem;
   // 16 1-KiB LDS-DMA pieces per tile (4 rows each), 4 per wave; K rows swizzled as k_lds_off, V
@@ -841,118 +846,91 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
         vf[ks * ND + db] = u32x4{lo[0], lo[1], hi[0], hi[1]};
       }
   };
-  // one sub-tile step: CUR = sub-tile u has visible keys for this wave, PREV = u - 1 had. The
-  // score accumulators start from an inline zero and are read out once; everything the softmax
-  // touches lives in VGPRs (no accumulator-register round trips)
-  auto step = [&](auto cur_c, auto prev_c, int u) __attribute__((always_inline)) {
-    constexpr bool CUR = decltype(cur_c)::value, PREV = decltype(prev_c)::value;
+  // one sub-tile step with per-block flags: CA / CB = sub-tile u has visible keys for block A / B,
+  // PA / PB = sub-tile u - 1 had. The score accumulators start from an inline zero and are read out
+  // once; everything the softmax touches lives in VGPRs (no accumulator-register round trips)
+  auto step = [&](auto ca_c, auto pa_c, auto cb_c, auto pb_c, int u) __attribute__((always_inline)) {
+    constexpr bool CA = decltype(ca_c)::value, PA = decltype(pa_c)::value;
+    constexpr bool CB = decltype(cb_c)::value, PB = decltype(pb_c)::value;
     const int k0 = u * 32;
     f32x16 cA, cB;
     __builtin_amdgcn_sched_barrier(0);
     // ---- phase 1: QK^T of sub-tile u || finish of u - 1
-    if constexpr (CUR) {
-      cA = zero16();
-      cB = zero16();
+    if constexpr (CA) cA = zero16();
+    if constexpr (CB) cB = zero16();
+    if constexpr (CA || CB) {
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {
-        cA = MF<T>::mma(as_frag<frag>(kf[kk]), qA[kk], cA);
-        cB = MF<T>::mma(as_frag<frag>(kf[kk]), qB[kk], cB);
+        if constexpr (CA) cA = MF<T>::mma(as_frag<frag>(kf[kk]), qA[kk], cA);
+        if constexpr (CB) cB = MF<T>::mma(as_frag<frag>(kf[kk]), qB[kk], cB);
       }
     }
-    if constexpr (PREV) load_vf(u - 1);   // V fragments of P(u-1) V, read under the QK^T MFMAs
-    if constexpr (PREV) {
+    if constexpr (PA || PB) load_vf(u - 1);   // V fragments of P(u-1) V, read under the QK^T MFMAs
+    auto finish = [&](float (&pv)[16], u32x4 (&pp)[2], float um, float& l) __attribute__((always_inline)) {
 #pragma unroll
-      for (int r = 8; r < 16; ++r) {
-        pvA[r] = fexp2(fmaf(pvA[r], scale_log2, -uA));
-        pvB[r] = fexp2(fmaf(pvB[r], scale_log2, -uB));
-      }
-      float sa = 0.f, sb = 0.f;
+      for (int r = 8; r < 16; ++r) pv[r] = fexp2(fmaf(pv[r], scale_log2, -um));
+      float sm = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sa += pvA[r]; sb += pvB[r]; }
+      for (int r = 0; r < 16; ++r) sm += pv[r];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pA[ks][j] = MF<T>::pack(pvA[8 * ks + 2 * j], pvA[8 * ks + 2 * j + 1]);
-          pB[ks][j] = MF<T>::pack(pvB[8 * ks + 2 * j], pvB[8 * ks + 2 * j + 1]);
-        }
-      sa += __shfl_xor(sa, 32, 64);
-      sb += __shfl_xor(sb, 32, 64);
-      lA += sa;
-      lB += sb;
-    }
-    if constexpr (PHA_FA4_GROUPS && CUR && PREV) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-      }
-    }
+        for (int jj = 0; jj < 4; ++jj) pp[ks][jj] = MF<T>::pack(pv[8 * ks + 2 * jj], pv[8 * ks + 2 * jj + 1]);
+      l += sm + __shfl_xor(sm, 32, 64);
+    };
+    if constexpr (PA) finish(pvA, pA, uA, lA);
+    if constexpr (PB) finish(pvB, pB, uB, lB);
     __builtin_amdgcn_sched_barrier(0);
     // tile top of the next 64-key tile in the middle of an odd sub-tile, so the next sub-tile's K
     // fragments can be read under this one's P V MFMAs
     if ((u & 1) && ((u + 1) >> 1) < ntile) sync_to((u + 1) >> 1);
     float sA[16], sB[16];
-    if constexpr (CUR) {
+    if constexpr (CA) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sA[r] = cA[r]; sB[r] = cB[r]; }
-      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0)) mask_s(sA, k0, qa);
-      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0 + 32)) mask_s(sB, k0, qbq);
+      for (int r = 0; r < 16; ++r) sA[r] = cA[r];
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > rA0)) mask_s(sA, k0, qa);
+    }
+    if constexpr (CB) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sB[r] = cB[r];
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > rB0)) mask_s(sB, k0, qbq);
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- phase 2: P(u-1) V of sub-tile u - 1 || start of u
-    if constexpr (PREV) {
+    if constexpr (PA || PB) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int db = 0; db < ND; ++db) {
-          oA[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pA[ks]), oA[db]);
-          oB[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pB[ks]), oB[db]);
+          if constexpr (PA) oA[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pA[ks]), oA[db]);
+          if constexpr (PB) oB[db] = MF<T>::mma(as_frag<frag>(vf[ks * ND + db]), as_frag<frag>(pB[ks]), oB[db]);
         }
     }
-    if constexpr (CUR) load_kf(u + 1);   // next sub-tile's K fragments, read under the P V MFMAs
-    if constexpr (CUR) {
-      float ta = -INFINITY, tb = -INFINITY;
+    if constexpr (CA || CB) load_kf(u + 1);   // next sub-tile's K fragments, read under the P V MFMAs
+    auto start = [&](const float (&sv)[16], float (&pv)[16], float& m, float& um, float& al, bool& rs)
+                     __attribute__((always_inline)) {
+      float t = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { ta = fmaxf(ta, sA[r]); tb = fmaxf(tb, sB[r]); }
-      ta = fmaxf(ta, __shfl_xor(ta, 32, 64)) * scale_log2;
-      tb = fmaxf(tb, __shfl_xor(tb, 32, 64)) * scale_log2;
-      rsA = !__all(ta <= mA + kThr);
-      rsB = !__all(tb <= mB + kThr);
-      const float nA = rsA ? fmaxf(mA, ta) : mA, nB = rsB ? fmaxf(mB, tb) : mB;
-      const float unA = nA == -INFINITY ? 0.f : nA, unB = nB == -INFINITY ? 0.f : nB;
-      alA = rsA ? fexp2(mA - unA) : 1.f;
-      alB = rsB ? fexp2(mB - unB) : 1.f;
-      mA = nA;
-      mB = nB;
-      uA = unA;
-      uB = unB;
+      for (int r = 0; r < 16; ++r) t = fmaxf(t, sv[r]);
+      t = fmaxf(t, __shfl_xor(t, 32, 64)) * scale_log2;
+      rs = !__all(t <= m + kThr);
+      const float nm = rs ? fmaxf(m, t) : m;
+      const float un = nm == -INFINITY ? 0.f : nm;
+      al = rs ? fexp2(m - un) : 1.f;
+      m = nm;
+      um = un;
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        pvA[r] = fexp2(fmaf(sA[r], scale_log2, -uA));
-        pvB[r] = fexp2(fmaf(sB[r], scale_log2, -uB));
-        pvA[8 + r] = sA[8 + r];
-        pvB[8 + r] = sB[8 + r];
+        pv[r] = fexp2(fmaf(sv[r], scale_log2, -um));
+        pv[8 + r] = sv[8 + r];
       }
-    }
-    if constexpr (PHA_FA4_GROUPS && CUR && PREV) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      }
-    }
+    };
+    if constexpr (CA) start(sA, pvA, mA, uA, alA, rsA);
+    if constexpr (CB) start(sB, pvB, mB, uB, alB, rsB);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (CUR) {   // a raised running max rescales O after P(u-1) V, before P(u) V
+    // a raised running max rescales O after P(u-1) V, before P(u) V
+    if constexpr (CA) {
       lA *= alA;
-      lB *= alB;
       if (rsA) {
         asm volatile("" ::: "memory");   // keep the (rare) rescale a branch, not a multiply per step
 #pragma unroll
@@ -960,6 +938,9 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
 #pragma unroll
           for (int r = 0; r < 16; ++r) oA[i][r] *= alA;
       }
+    }
+    if constexpr (CB) {
+      lB *= alB;
       if (rsB) {
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -1015,7 +996,7 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
     if ((u & 1) && ((u + 1) >> 1) < ntile) sync_to((u + 1) >> 1);
     {   // sub-tiles straddling the causal diagonal or the key end (the last one or two per wave)
       const int k0 = u * 32;
-      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > wq0)) {
+      if ((k0 + 32 > Sk) || (CAUSAL && k0 + 31 > rA0)) {
         const int base = k0 + 4 * h;
         const int la = CAUSAL ? qa - base : 1 << 20, lb = CAUSAL ? qbq - base : 1 << 20, l2 = Sk - base;
 #pragma unroll
@@ -1099,13 +1080,19 @@ void fa_fwd_v4_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T*
     // register allocator spill, hence the peeled first and last steps.
     sync_to(0);
     load_kf(0);
-    step(TT{}, FF{}, 0);
+    step(TT{}, FF{}, TT{}, FF{}, 0);
     int u = 1;
     if (PHA_FA4_SLOTS)
-      for (; u <= ulast; ++u) step_steady(u);
+      for (; u <= uA_last; ++u) step_steady(u);
     else
-      for (; u <= ulast; ++u) step(TT{}, TT{}, u);
-    step(FF{}, TT{}, u);
+      for (; u <= uA_last; ++u) step(TT{}, TT{}, TT{}, TT{}, u);
+    if (uA_last == uB_last) {
+      step(FF{}, TT{}, FF{}, TT{}, u);   // both drain
+    } else {
+      step(FF{}, TT{}, TT{}, TT{}, u);   // A drains, B goes on
+      for (++u; u <= uB_last; ++u) step(FF{}, FF{}, TT{}, TT{}, u);
+      step(FF{}, FF{}, FF{}, TT{}, u);   // B drains
+    }
     sync_to(ntile - 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA left in flight at exit
