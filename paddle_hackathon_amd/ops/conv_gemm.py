@@ -883,33 +883,45 @@ def _tn_ws(sp, M, N, dev):
     return torch.empty((sp + (-(-sp // 16) if sp > 32 else 0)) * M * N, dtype=torch.float32, device=dev)
 
 
+_TN_SPLIT_CANDS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512)
+_retune_tn = [False]   # tools/tune_conv256.py --retune-tn: time TN launches even where the table has a pick
+
+
 def _run_tn(key, M, N, K, dev, call):
-    """the tile of a TN launch (table, else timed when enabled, else the fewest padded tiles);
-    call(tile, splits, ws) launches it"""
-    ch = _lookup(key)
+    """the (tile, split-K factor) of a TN launch: the table's pick — [tile, splits], or a bare tile
+    with the formula's splits — else, with timing enabled, the fastest of every candidate tile x
+    split factor (the formula's two rounds of work items is 1.1-1.6x off the best on ResNet-50's
+    small-output wgrads, profiles/wgrad_split_r5/), else the fewest padded tiles with the formula's
+    splits; call(tile, splits, ws) launches it"""
+    ch = _tuned.get(key) if _retune_tn[0] else _lookup(key)
     if ch is None:
         tiles = _tn_tiles(M, N)
-        if not _timing() or torch.cuda.is_current_stream_capturing() or len(tiles) == 1:
+        if not _timing() or torch.cuda.is_current_stream_capturing():
             # fewest tiles (least MFMA padding), larger tiles first on ties
             ch = min(tiles, key=lambda t: -(-M // _TN_CANDS[t][0]) * -(-N // _TN_CANDS[t][1]))
         else:
             best_t = float("inf")
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            kb = -(-K // 32)
             for t in tiles:
-                sp = _tn_splits(M, N, K, t, dev)
-                ws = _tn_ws(sp, M, N, dev)
-                call(t, sp, ws)
-                ev0.record()
-                for _ in range(3):
+                cands = sorted({s for s in _TN_SPLIT_CANDS if s <= max(1, kb // 4)} | {_tn_splits(M, N, K, t, dev)})
+                for sp in cands:
+                    ws = _tn_ws(sp, M, N, dev)
                     call(t, sp, ws)
-                ev1.record()
-                ev1.synchronize()
-                el = ev0.elapsed_time(ev1)
-                if el < best_t:
-                    best_t, ch = el, t
+                    ev0.record()
+                    for _ in range(5):
+                        call(t, sp, ws)
+                    ev1.record()
+                    ev1.synchronize()
+                    el = ev0.elapsed_time(ev1)
+                    if el < best_t:
+                        best_t, ch = el, (t, sp)
             _tuned[key] = ch
-    sp = _tn_splits(M, N, K, ch, dev)
-    call(ch, sp, _tn_ws(sp, M, N, dev))
+    if isinstance(ch, tuple):
+        t, sp = ch
+    else:
+        t, sp = ch, _tn_splits(M, N, K, ch, dev)
+    call(t, sp, _tn_ws(sp, M, N, dev))
 
 
 def gemm256_tn(a, b, out=None, out_dtype=None, accumulate=False):

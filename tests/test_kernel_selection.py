@@ -38,6 +38,21 @@ def test_conv_timing_autotune_is_opt_in(monkeypatch):
     assert not cg._timing()
 
 
+def test_tn_pick_carries_split_factor(monkeypatch):
+    """a weight-gradient table entry [tile, splits] fixes the split-K factor too; a bare tile keeps
+    the formula's splits"""
+    from paddle_hackathon_amd.ops import conv_gemm as cg
+    key = ("wgrad", "synthetic-shape")
+    monkeypatch.setattr(cg, "_tn_ws", lambda sp, M, N, dev: None)
+    monkeypatch.setattr(cg, "_num_cus", lambda dev: 256)
+    calls = []
+    monkeypatch.setitem(cg._tuned, key, (3, 48))
+    cg._run_tn(key, 128, 1152, 200704, "cpu", lambda t, sp, ws: calls.append((t, sp)))
+    monkeypatch.setitem(cg._tuned, key, 3)
+    cg._run_tn(key, 128, 1152, 200704, "cpu", lambda t, sp, ws: calls.append((t, sp)))
+    assert calls == [(3, 48), (3, cg._tn_splits(128, 1152, 200704, 3, "cpu"))]
+
+
 def test_gemm_policy_is_static(monkeypatch):
     from paddle_hackathon_amd.ops import gemm as G
     monkeypatch.setenv("PHA_GEMM_IMPL", "auto")

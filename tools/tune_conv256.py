@@ -40,9 +40,12 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[256])
     ap.add_argument("--formats", nargs="+", default=["NHWC", "NCHW"])
     ap.add_argument("--out", default=conv_gemm.TUNING_TABLE)
+    ap.add_argument("--retune-tn", action="store_true",
+                    help="re-time only the weight-gradient / TN launches (tile x split-K), keep the other picks")
     a = ap.parse_args()
     paddle.set_device("gpu")
     conv_gemm.set_timing_autotune(True)
+    conv_gemm._retune_tn[0] = a.retune_tn
     for b in a.batch:
         for f in a.formats:
             run(b, f)
