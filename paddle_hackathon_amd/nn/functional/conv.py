@@ -68,13 +68,61 @@ def _to_ncx(t, data_format):
     return t, False
 
 
+def _s2d_ok(x, w, stride, dilation):
+    import os
+    s = stride[0]
+    C = x.shape[-1]
+    return (os.environ.get("PHA_CONV_S2D", "1") != "0" and C % 8 != 0 and s > 1 and stride[1] == s
+            and tuple(dilation) == (1, 1) and w.shape[2] > s and w.shape[3] > s and s * s * C <= 32
+            and x.dtype in (torch.bfloat16, torch.float16))
+
+
+def _space_to_depth(x, w, stride, pad):
+    """a stride-s convolution of a narrow input (the RGB stem: C = 3, 7x7, stride 2) rewritten as a
+    stride-1 convolution of the input's s x s space-to-depth image — channel (a, b, c) of pixel
+    (hq, wq) holds padded-input pixel (s*hq + a, s*wq + b), channel c — with the filter's taps
+    regrouped the same way (ceil(k/s)^2 taps of s*s*c' channels, zero taps past k). The stem's
+    implicit GEMM then reduces over K = 4*4*16 = 256 instead of 7*7*8 = 392 (the input padded to 8
+    channels) and reads 32-B tap rows instead of 16-B ones. Returns (image, filter) for a stride-1,
+    unpadded convolution with the same output."""
+    N, H, W, C = x.shape
+    Co, _, KH, KW = w.shape
+    s = stride[0]
+    ph, pw = pad
+    kh, kw = -(-KH // s), -(-KW // s)
+    OH, OW = (H + 2 * ph - KH) // s + 1, (W + 2 * pw - KW) // s + 1
+    Hq, Wq = OH + kh - 1, OW + kw - 1
+    c4 = C
+    while (s * s * c4) % 8:
+        c4 += 1
+    z = x.new_zeros(N, Hq, Wq, s, s, c4)
+    for a in range(s):
+        hq0 = max(0, -(-(ph - a) // s))
+        r0 = s * hq0 + a - ph
+        nh = min(Hq - hq0, len(range(r0, H, s)))
+        for b in range(s):
+            wq0 = max(0, -(-(pw - b) // s))
+            q0 = s * wq0 + b - pw
+            nw = min(Wq - wq0, len(range(q0, W, s)))
+            if nh > 0 and nw > 0:
+                z[:, hq0:hq0 + nh, wq0:wq0 + nw, a, b, :C] = \
+                    x[:, r0:r0 + s * (nh - 1) + 1:s, q0:q0 + s * (nw - 1) + 1:s, :]
+    wp = TF.pad(w, [0, s * kw - KW, 0, s * kh - KH, 0, c4 - C])          # [Co, c4, s*kh, s*kw]
+    wz = wp.view(Co, c4, kh, s, kw, s).permute(0, 3, 5, 1, 2, 4).reshape(Co, s * s * c4, kh, kw)
+    return z.view(N, Hq, Wq, s * s * c4), wz
+
+
 def _hip_conv2d(x, w, bias, stride, pad, dilation, groups):
     """NHWC conv on the gfx950 implicit-GEMM MFMA kernels (ops/conv_gemm.py: forward, dgrad and
     wgrad on the 256-tile glds kernels of gemm256.hip; PHA_CONV_KERNEL=v1 selects the older
-    gemm_conv.hip path). Inputs whose channel count is not a multiple of 8 (the RGB stem) are
-    zero-padded to 8 channels."""
+    gemm_conv.hip path). Narrow strided inputs (the RGB stem) run as the stride-1 convolution of
+    their space-to-depth image (``_space_to_depth``, PHA_CONV_S2D=0: off); other inputs whose
+    channel count is not a multiple of 8 are zero-padded to 8 channels."""
     import os
     from ...ops import conv_gemm
+    if _s2d_ok(x, w, stride, dilation) and os.environ.get("PHA_CONV_KERNEL", "256") != "v1":
+        z, wz = _space_to_depth(x, w, list(stride), list(pad))
+        return conv_gemm.conv2d_nhwc256(z, wz, bias, (1, 1), (0, 0), (1, 1))
     if x.shape[-1] % 8 != 0:
         c = x.shape[-1]
         cp = (c + 7) // 8 * 8

@@ -105,6 +105,36 @@ def test_conv2d_dispatch_own_kernels(fmt, groups, k, stride, dil, padding):
         _close(z._t, zr, torch.bfloat16, "maxpool")
 
 
+@pytest.mark.parametrize("s2d", ["1", "0"])
+@pytest.mark.parametrize("H,W,k,s,p", [(32, 32, 7, 2, 3), (33, 30, 7, 2, 3), (20, 20, 3, 2, 1)])
+def test_rgb_stem_conv_space_to_depth(monkeypatch, s2d, H, W, k, s, p):
+    """the RGB stem (3 channels, stride 2) through paddle conv2d on the own kernels, as the stride-1
+    convolution of its space-to-depth image (PHA_CONV_S2D=1, default) or padded to 8 channels:
+    output, dx and dw match fp32"""
+    import paddle_hackathon_amd as paddle
+    from paddle_hackathon_amd.ops import fallback
+    monkeypatch.setenv("PHA_CONV_S2D", s2d)
+    paddle.set_device("gpu")
+    torch.manual_seed(0)
+    x = torch.randn(4, H, W, 3, device="cuda").bfloat16()
+    w = (torch.randn(64, 3, k, k, device="cuda") / (3 * k * k) ** 0.5).bfloat16()
+    xr, wr = (t.float().detach().requires_grad_(True) for t in (x, w))
+    ref = TF.conv2d(xr.permute(0, 3, 1, 2), wr, None, s, p).permute(0, 2, 3, 1)
+    xa, wa = paddle.to_tensor(x), paddle.to_tensor(w)
+    xa.stop_gradient = False
+    wa.stop_gradient = False
+    fallback.reset()
+    y = paddle.nn.functional.conv2d(xa, wa, stride=s, padding=p, data_format="NHWC")
+    assert fallback.counts().get("conv2d", 0) == 0, fallback.counts()
+    assert tuple(y.shape) == tuple(ref.shape)
+    _close(y._t, ref, torch.bfloat16, "fwd")
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    (y * paddle.to_tensor(gy.bfloat16())).sum().backward()
+    _close(xa.grad._t, xr.grad, torch.bfloat16, "dx")
+    _close(wa.grad._t, wr.grad, torch.bfloat16, "dw")
+
+
 def _no_conv_fallback_step(model, x, y):
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.ops import fallback
