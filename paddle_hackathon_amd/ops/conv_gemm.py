@@ -341,7 +341,7 @@ def _autotune(key, run):
     """(tile shape, BK) of the 256-row-tile kernels for this problem: the table's pick, else (with
     timing enabled, outside graph capture) the fastest candidate on the real operands, else the
     kernel heuristic (-1, 0)"""
-    ch = _lookup(key)
+    ch = _tuned.get(key) if _retune_conv[0] else _lookup(key)
     if ch is not None:
         return ch
     if not _timing() or torch.cuda.is_current_stream_capturing():
@@ -885,6 +885,7 @@ def _tn_ws(sp, M, N, dev):
 
 _TN_SPLIT_CANDS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512)
 _retune_tn = [False]   # tools/tune_conv256.py --retune-tn: time TN launches even where the table has a pick
+_retune_conv = [False]   # tools/tune_conv256.py --retune-all: the same for the forward / dgrad launches
 
 
 def _run_tn(key, M, N, K, dev, call):

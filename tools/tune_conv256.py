@@ -42,10 +42,12 @@ def main():
     ap.add_argument("--out", default=conv_gemm.TUNING_TABLE)
     ap.add_argument("--retune-tn", action="store_true",
                     help="re-time only the weight-gradient / TN launches (tile x split-K), keep the other picks")
+    ap.add_argument("--retune-all", action="store_true", help="re-time every launch of the run (conv and TN)")
     a = ap.parse_args()
     paddle.set_device("gpu")
     conv_gemm.set_timing_autotune(True)
-    conv_gemm._retune_tn[0] = a.retune_tn
+    conv_gemm._retune_tn[0] = a.retune_tn or a.retune_all
+    conv_gemm._retune_conv[0] = a.retune_all
     for b in a.batch:
         for f in a.formats:
             run(b, f)
