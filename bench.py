@@ -41,10 +41,12 @@ def _args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt3-1.3b")
     ap.add_argument("--micro-batch", type=int, default=None,
-                    help="per-GPU batch (default: GPT 32 x 2048 tokens, BERT 32, ResNet 256); GPT micro-batch 16 "
-                         "measured +7.6 %% tokens/s over 8 and 32 +1.3 %% over 16 on one MI355X (bigger GEMMs, the "
-                         "optimizer and the gradient all-reduce amortised over more tokens; 128.5 GB of the 288 GB "
-                         "HBM at 32, profiles/gpt3_micro_batch_r5.txt); ResNet 512 measured slower than 256")
+                    help="per-GPU batch (default: GPT 48 x 2048 tokens, BERT 32, ResNet 256); GPT micro-batch 16 "
+                         "measured +7.6 %% tokens/s over 8, 32 +1.3 %% over 16, 48 +0.5 %% over 32 on one MI355X "
+                         "(bigger GEMMs, the optimizer and the gradient all-reduce amortised over more tokens; "
+                         "183 GB of the 288 GB HBM at 48 — 64 adds another +0.5 %% at 237 GB, too little headroom "
+                         "for the multi-rank buffers; profiles/gpt3_micro_batch_r5.txt); ResNet 512 measured "
+                         "slower than 256")
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -132,7 +134,7 @@ def main():
     tp, pp = max(1, a.tp), max(1, a.pp)
     if world % (tp * pp):
         raise SystemExit(f"--tp {tp} x --pp {pp} must divide the world size {world}")
-    B, S = a.micro_batch or (32 if a.model == "gpt3-1.3b" else 2), a.seq_len
+    B, S = a.micro_batch or (48 if a.model == "gpt3-1.3b" else 2), a.seq_len
     lo = Layout(world=world, tp=tp, pp=pp, sharding_stage=a.sharding_stage,
                 micro_batches=(a.micro_batches or 2 * pp) if pp > 1 else 1)
     if pp > 1 and B % lo.micro_batches:
