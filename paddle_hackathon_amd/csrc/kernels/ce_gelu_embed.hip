@@ -258,15 +258,18 @@ struct PoolGeo {
   int N, H, W, C, OH, OW, KH, KW, sh, sw, ph, pw;
 };
 
-template <typename T>
+// I: index type of the element walk — unsigned 32-bit whenever the tensor allows (a 64-bit
+// division / modulo is a long software sequence on CDNA; four per element made both kernels
+// VALU-bound at ~40-60 % of the HBM rate on ResNet-50's 112x112x64 pooling)
+template <typename T, typename I>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeo g) {
-  const int cv = g.C / 8;
-  const long total = (long)g.N * g.OH * g.OW * cv;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+  const I cv = (I)(g.C / 8);
+  const I total = (I)g.N * (I)g.OH * (I)g.OW * cv;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
     const int c8 = (int)(i % cv);
-    const long pix = i / cv;
-    const int ow = (int)(pix % g.OW), oh = (int)((pix / g.OW) % g.OH), n = (int)(pix / ((long)g.OW * g.OH));
+    const I pix = i / cv, prow = pix / (I)g.OW;
+    const int ow = (int)(pix - prow * (I)g.OW), n = (int)(prow / (I)g.OH), oh = (int)(prow - (I)n * (I)g.OH);
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -287,25 +290,25 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
           }
       }
     }
-    Vec8<T>::st(y + i * 8, best);
+    Vec8<T>::st(y + (long)i * 8, best);
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
     packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-    *reinterpret_cast<uint2*>(idx + i * 8) = packed;
+    *reinterpret_cast<uint2*>(idx + (long)i * 8) = packed;
   }
 }
 
 // gather form (no atomics): an input pixel sums the gradients of the <= ceil(K/s)^2 windows that
 // cover it and chose it
-template <typename T>
+template <typename T, typename I>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ gy, const uint8_t* __restrict__ idx,
                                                           T* __restrict__ gx, PoolGeo g) {
-  const int cv = g.C / 8;
-  const long total = (long)g.N * g.H * g.W * cv;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+  const I cv = (I)(g.C / 8);
+  const I total = (I)g.N * (I)g.H * (I)g.W * cv;
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < total; i += (I)gridDim.x * 256) {
     const int c8 = (int)(i % cv);
-    const long pix = i / cv;
-    const int iw = (int)(pix % g.W), ih = (int)((pix / g.W) % g.H), n = (int)(pix / ((long)g.W * g.H));
+    const I pix = i / cv, prow = pix / (I)g.W;
+    const int iw = (int)(pix - prow * (I)g.W), n = (int)(prow / (I)g.H), ih = (int)(prow - (I)n * (I)g.H);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
         }
       }
     }
-    Vec8<T>::st(gx + i * 8, acc);
+    Vec8<T>::st(gx + (long)i * 8, acc);
   }
 }
 
@@ -536,7 +539,10 @@ PHA_API int pha_maxpool2d_nhwc_fwd(int dt, const void* x, void* y, uint8_t* idx,
   const long total = (long)N * OH * OW * (C / 8);
   const unsigned grid = (unsigned)std::min((total + 255) / 256, 8192L);
   PHA_DISPATCH_T(dt, T, {
-    hipLaunchKernelGGL((maxpool_fwd_kernel<T>), dim3(grid), dim3(256), 0, stream, (const T*)x, (T*)y, idx, g);
+    if (total * 8 < (1L << 31))   // 32-bit walk (element offsets i * 8 included)
+      hipLaunchKernelGGL((maxpool_fwd_kernel<T, unsigned>), dim3(grid), dim3(256), 0, stream, (const T*)x, (T*)y, idx, g);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_kernel<T, long>), dim3(grid), dim3(256), 0, stream, (const T*)x, (T*)y, idx, g);
   });
   return (int)hipGetLastError();
 }
@@ -548,7 +554,10 @@ PHA_API int pha_maxpool2d_nhwc_bwd(int dt, const void* gy, const uint8_t* idx, v
   const long total = (long)N * H * W * (C / 8);
   const unsigned grid = (unsigned)std::min((total + 255) / 256, 8192L);
   PHA_DISPATCH_T(dt, T, {
-    hipLaunchKernelGGL((maxpool_bwd_kernel<T>), dim3(grid), dim3(256), 0, stream, (const T*)gy, idx, (T*)gx, g);
+    if (total * 8 < (1L << 31))
+      hipLaunchKernelGGL((maxpool_bwd_kernel<T, unsigned>), dim3(grid), dim3(256), 0, stream, (const T*)gy, idx, (T*)gx, g);
+    else
+      hipLaunchKernelGGL((maxpool_bwd_kernel<T, long>), dim3(grid), dim3(256), 0, stream, (const T*)gy, idx, (T*)gx, g);
   });
   return (int)hipGetLastError();
 }
