@@ -134,7 +134,7 @@ def main():
     tp, pp = max(1, a.tp), max(1, a.pp)
     if world % (tp * pp):
         raise SystemExit(f"--tp {tp} x --pp {pp} must divide the world size {world}")
-    B, S = a.micro_batch or (48 if a.model == "gpt3-1.3b" else 2), a.seq_len
+    B, S = _gpt_micro_batch(a, torch, world, rank), a.seq_len
     lo = Layout(world=world, tp=tp, pp=pp, sharding_stage=a.sharding_stage,
                 micro_batches=(a.micro_batches or 2 * pp) if pp > 1 else 1)
     if pp > 1 and B % lo.micro_batches:
@@ -312,6 +312,30 @@ def _resnet_graphed(a, world):
     if world > 1 and collective.get_backend() != "nccl":
         return False   # host (gloo) collectives cannot be captured
     return a.graph == "on" or world == 1
+
+
+def _gpt_micro_batch(a, torch, world, rank):
+    """per-GPU micro-batch: --micro-batch, else 2 for the larger GPTs, else 48 for GPT-3 1.3B
+    (182.9 GB peak) when every rank has the free HBM for it — stepping down to 32 (128.5 GB) or 16
+    (74 GB) otherwise, so a card with less free memory than an MI355X's 288 GB runs instead of
+    failing; ranks agree on the smallest free memory, so they all pick the same size"""
+    if a.micro_batch:
+        return a.micro_batch
+    if a.model != "gpt3-1.3b":
+        return 2
+    free_gb = torch.cuda.mem_get_info()[0] / 2 ** 30
+    if world > 1:
+        import torch.distributed as td
+        t = torch.tensor([free_gb], dtype=torch.float64,
+                         device="cuda" if td.get_backend() == "nccl" else "cpu")
+        td.all_reduce(t, op=td.ReduceOp.MIN)
+        free_gb = float(t.item())
+    for mb, need_gb in ((48, 200), (32, 145), (16, 90)):
+        if free_gb >= need_gb:
+            break
+    if mb != 48 and rank == 0:
+        print(f"[bench] {free_gb:.0f} GB free HBM: GPT micro-batch {mb} instead of 48", file=sys.stderr, flush=True)
+    return mb
 
 
 def bench_resnet(a, paddle, dist, world, rank, emit=True):
