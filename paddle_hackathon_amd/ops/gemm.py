@@ -149,6 +149,18 @@ def _num_cus(dev):
     return torch.cuda.get_device_properties(dev).multi_processor_count
 
 
+def _group_m(a_kouter, b_kouter, K, N):
+    """tile-walk panel height (M-tile rows per panel) of a gemm4p launch: 8 for NT products with
+    K < 4096, measured at the bench's M = 98,304 (2048 x 2048: 667 vs 701 us at the kernel's
+    default 4; 6144 x 2048: 1848 vs 1879 us; profiles/nt_mb48_r5/r5_groupm.log), else 4 (long-K NT
+    is best at 4: 2289 vs 2378 us at 8; so is the 50304-wide head: 15.0 vs 16.2 ms).
+    PHA_G4P_GROUP_M overrides."""
+    env = os.environ.get("PHA_G4P_GROUP_M")
+    if env:
+        return int(env)
+    return 8 if (not a_kouter and not b_kouter and K < 4096 and N <= 8192) else 4
+
+
 def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=False, epi_extra=0, grid=0,
            group_m=0, splits=1, gelu_aux=None):
     """C = op(A) @ op(B) (+ bias[output column]) on the persistent epilogue-overlapped kernel
@@ -178,6 +190,8 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
         assert (a_kouter, b_kouter, trans_out, splits) == (False, False, False, 1)
         assert gelu_aux.shape == c.shape and gelu_aux.stride() == c.stride() and gelu_aux.dtype == c.dtype
         epi |= EPI_GELU
+    if group_m <= 0:
+        group_m = _group_m(a_kouter, b_kouter, Ka, N)
     rc = _L().pha_gemm4p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
                          int(a_kouter), int(b_kouter), int(trans_out), epi, _ptr(bias), grid or _num_cus(a.device),
                          group_m, _ptr(ws), splits, _stream(a), _ptr(gelu_aux))
@@ -344,10 +358,20 @@ def _bmm_fits(x3, y3):
             and y3.shape[2] % 8 == 0 and _bmm_ok(x3) and _bmm_ok(y3))
 
 
+# NT shapes (N, K) where gemm4p matches hipBLASLt in isolation at the bench's M = 98,304: the GPT-3
+# 1.3B qkv forward, 1830 vs 1842 us (profiles/nt_mb48_r5/r5_nt_mb48_gm8.log). Opt-in
+# (PHA_GEMM_AUTO_NT_OWN=1): inside the training step it measured -0.55 % (125.5k vs 126.2k
+# tokens/s, three alternating pairs, profiles/nt_mb48_r5/)
+_AUTO_OWN_NT_SHAPES = {(6144, 2048)}
+
+
 def _auto_own_nt(N, K):
-    """NT products the auto policy keeps on gemm4p: N <= 2048 and K <= 2048 (the attention output
-    projection's forward and dX), where it ties hipBLASLt (204 vs 206 us at 32768x2048x2048,
-    profiles/gemm4p_early_ab_r3.log); longer-K / wider NT products stay on the library, 4-12 % faster"""
+    """NT products the auto policy puts on gemm4p, both opt-in: the isolated ties above
+    (PHA_GEMM_AUTO_NT_OWN=1), and (PHA_GEMM_AUTO_NT=1) N <= 2048 and K <= 2048 (the attention output projection's forward and
+    dX, 204 vs 206 us at 32768x2048x2048, profiles/gemm4p_early_ab_r3.log, but 10 % behind at
+    M = 98,304); the other NT products stay on the library, 3-10 % faster"""
+    if (N, K) in _AUTO_OWN_NT_SHAPES and os.environ.get("PHA_GEMM_AUTO_NT_OWN", "0") == "1":
+        return True
     return N <= 2048 and K <= 2048 and os.environ.get("PHA_GEMM_AUTO_NT", "0") == "1"
 
 
