@@ -185,7 +185,7 @@ __global__ __launch_bounds__(NT) void gemm256_kernel(Args p) {
     brow[j] = reinterpret_cast<const char*>(Bt + (bok[j] ? n : 0) * p.ldb);
   }
   // source chunk: row % RPI == lrow for every instruction, so the swizzle is per lane constant
-  const int sch = BK == 64 ? (lch ^ (lrow & 7)) : (lch ^ ((lrow >> 2) & 3));
+  const int sch = BK == 64 ? (lch ^ (lrow & 7)) : (lch ^ ((0x78 >> (((lrow >> 2) & 3) << 1)) & 3));   // img_off<BK>
 
   auto issue = [&](int stage, long k0) {
     unsigned char* sa = smem + stage * STAGE;

@@ -39,7 +39,12 @@ template <> struct Mf<half_t> {
 template <int BK>
 __device__ __forceinline__ int img_off(int row, int chunk) {
   if constexpr (BK == 64) return row * 128 + ((chunk ^ (row & 7)) << 4);
-  else return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+  // BK 32 (64-B rows): XOR of the 4-row block's entry in f = {0, 2, 3, 1}. ds_read_b128 serves
+  // lanes {0-3, 12-15, 20-27} (and three more such groups) in one LDS cycle, i.e. fragment rows
+  // 0-3 and 12-15 of chunk k with rows 4-11 of chunk k + 1; the plain (row >> 2) & 3 put rows
+  // 0-3 / k and 4-7 / k + 1 on the same 16-B slots — a 2-way conflict in every group (37-47 %
+  // SQ_LDS_BANK_CONFLICT, profiles/resnet_pmc_r5/). f makes all four groups conflict-free.
+  else return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) << 1)) & 3)) << 4);
 }
 
 // 16-B global -> LDS DMA (global_load_lds_dwordx4; M0 = the wave's LDS destination, lane-linear).
