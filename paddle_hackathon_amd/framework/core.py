@@ -681,7 +681,10 @@ class Parameter(Tensor):
             data = data._t
         data = data.detach()
         self._t = data
-        self._name = name if name is not None else _unique_name("param")
+        if name is None:   # reference ParamBase: unique_name.generate("_param_base")
+            from ..utils import unique_name
+            name = unique_name.generate("_param_base")
+        self._name = name
         self._persistable = True
         self.optimize_attr = kwargs.get("optimize_attr", {"learning_rate": 1.0})
         self.regularizer = kwargs.get("regularizer", None)

@@ -144,8 +144,17 @@ class _BatchNormBase(Layer):
         else:
             self.bias = self.create_parameter([num_features], attr=bias_attr, is_bias=True)
         dev = _core.default_device()
-        self.register_buffer("_mean", _wrap(torch.zeros(num_features, dtype=torch.float32, device=dev)))
-        self.register_buffer("_variance", _wrap(torch.ones(num_features, dtype=torch.float32, device=dev)))
+        mean = _wrap(torch.zeros(num_features, dtype=torch.float32, device=dev))
+        var = _wrap(torch.ones(num_features, dtype=torch.float32, device=dev))
+        # the reference creates the running statistics as non-trainable parameters named
+        # {name}_mean / {name}_variance, else the layer's next two .w names (batch_norm2d_0.w_1 /
+        # .w_2, python/paddle/nn/layer/norm.py:627-646): same names here, kept as buffers
+        from ...utils import unique_name
+        mean.name = name + "_mean" if name else unique_name.generate(self._full_name + ".w")
+        var.name = name + "_variance" if name else unique_name.generate(self._full_name + ".w")
+        mean.persistable = var.persistable = True
+        self.register_buffer("_mean", mean)
+        self.register_buffer("_variance", var)
 
     def forward(self, input):
         return F.batch_norm(input, self._mean, self._variance, self.weight, self.bias, self.training,

@@ -10,6 +10,7 @@ from __future__ import annotations
 import collections
 import copy
 import itertools
+import re
 import weakref
 
 import numpy as np
@@ -18,20 +19,30 @@ import torch
 from ...framework import core as _core
 from ...framework.core import Tensor, Parameter, convert_dtype, default_device, _wrap
 from ...framework.param_attr import ParamAttr
+from ...utils import unique_name
 
 __all__ = ["Layer", "HookRemoveHelper"]
 
-_layer_name_counter = collections.defaultdict(itertools.count)
 
-
-def _create_parameter(shape, dtype=None, attr=None, is_bias=False, default_initializer=None, name=None):
+def _create_parameter(shape, dtype=None, attr=None, is_bias=False, default_initializer=None, name=None,
+                      helper="create_parameter"):
+    """A parameter named as the reference's LayerHelperBase.create_parameter names it
+    (python/paddle/fluid/layer_helper_base.py:329): ``{helper}.w_N`` / ``{helper}.b_N`` from the
+    global ``unique_name`` generator, where ``helper`` is the owning Layer's full name
+    (``linear_0``) or a per-call ``unique_name.generate(op_type)`` (``fc_0``); an explicit
+    ``ParamAttr(name=...)`` / ``name`` wins."""
     from .. import initializer as I
     attr = ParamAttr._to_attr(attr)
     if attr is False:
         return None
     dt = convert_dtype(dtype) or _core._default_dtype
     shape = [int(s) for s in shape]
-    p = Parameter(shape, dt, name=attr.name or name, trainable=attr.trainable,
+    pname = attr.name or name
+    if pname is None:
+        if helper == "create_parameter":   # paddle.create_parameter: LayerHelper("create_parameter")
+            helper = unique_name.generate(helper)
+        pname = unique_name.generate(helper + (".b" if is_bias else ".w"))
+    p = Parameter(shape, dt, name=pname, trainable=attr.trainable,
                   optimize_attr={"learning_rate": attr.learning_rate}, regularizer=attr.regularizer,
                   need_clip=attr.need_clip, do_model_average=attr.do_model_average)
     init = attr.initializer
@@ -67,7 +78,9 @@ class Layer:
         self.training = True
         if name_scope is None:
             name_scope = _camel_to_snake(type(self).__name__)
-        self._full_name = f"{name_scope}_{next(_layer_name_counter[name_scope])}"
+        # reference fluid/dygraph/layers.py:107 — the GLOBAL unique_name generator, so the names of
+        # layers and their parameters (linear_0.w_0) match a reference run of the same script
+        self._full_name = unique_name.generate(name_scope)
         self._dtype = dtype
         self._parameters = collections.OrderedDict()
         self._buffers = collections.OrderedDict()
@@ -94,11 +107,13 @@ class Layer:
 
     # -- creation -------------------------------------------------------------------
     def create_parameter(self, shape, attr=None, dtype=None, is_bias=False, default_initializer=None):
-        return _create_parameter(shape, dtype or self._dtype, attr, is_bias, default_initializer)
+        return _create_parameter(shape, dtype or self._dtype, attr, is_bias, default_initializer,
+                                 helper=self._full_name)
 
     def create_variable(self, name=None, persistable=None, dtype=None):
         t = _wrap(torch.empty(0, dtype=convert_dtype(dtype) or _core._default_dtype, device=default_device()))
-        t.name = name or _core._unique_name(self._full_name + ".var")
+        t.name = ".".join([self._full_name, name]) if name else \
+            unique_name.generate(self._full_name + "._generated_var")
         t.persistable = bool(persistable)
         return t
 
@@ -407,10 +422,10 @@ class Layer:
         pass
 
 
+_FIRST_CAP = re.compile("(.)([A-Z][a-z]+)")
+_ALL_CAP = re.compile("([a-z])([A-Z])")
+
+
 def _camel_to_snake(name):
-    out = []
-    for i, c in enumerate(name):
-        if c.isupper() and i > 0 and not name[i - 1].isupper():
-            out.append("_")
-        out.append(c.lower())
-    return "".join(out)
+    """BatchNorm2D -> batch_norm2d, Conv2DTranspose -> conv2d_transpose (the reference's rule)"""
+    return _ALL_CAP.sub(r"\1_\2", _FIRST_CAP.sub(r"\1_\2", name)).lower()

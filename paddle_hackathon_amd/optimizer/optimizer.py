@@ -4,13 +4,15 @@ adagrad,adadelta,rmsprop,lamb}.py; kernels phi/kernels/gpu/{adam,adamw,momentum,
 Adam/AdamW/Momentum/SGD update *every* parameter with one multi-tensor HIP
 launch per (param dtype, grad dtype) group (ops.fused_adam_ / fused_momentum_),
 with fp32 master weights for bf16/fp16 parameters (``multi_precision``).
-Accumulator names follow the reference (``{param}_moment1_0`` …) so optimizer
-checkpoints (.pdopt) keep the same keys.
+Accumulator names follow the reference (``linear_0.w_0_moment1_0`` …) so optimizer
+checkpoints (.pdopt) keep the same keys; a restore is strict (see ``set_state_dict``).
 """
 from __future__ import annotations
 
 import collections
 import math
+import re
+import warnings
 
 import numpy as np
 import torch
@@ -20,6 +22,7 @@ from ..framework import core as _core
 from ..regularizer import L1Decay, L2Decay, WeightDecayRegularizer
 from .. import ops as _ops
 from .lr import LRScheduler
+from ..utils import unique_name
 
 __all__ = ["Optimizer", "SGD", "Momentum", "Adam", "AdamW", "Adamax", "Adagrad", "Adadelta", "RMSProp", "Lamb"]
 
@@ -80,19 +83,52 @@ class Optimizer:
         self._learning_rate = scheduler
 
     # -- accumulators ---------------------------------------------------------------
+    _STATE_META = ("master_weights", "LR_Scheduler", "@step_count@")
+
+    def _loaded_accs(self):
+        return [k for k in self._state_loaded if k not in self._STATE_META]
+
+    def _take_loaded(self, base, key):
+        """the loaded value of accumulator ``key`` (= ``unique_name.generate(base)``); a saved
+        name with another generator suffix (``base_N``: the saving process had created more
+        optimizers over the same parameters) is taken when it is the only one"""
+        if key in self._state_loaded:
+            return self._state_loaded.pop(key)
+        pat = re.compile(re.escape(base) + r"_\d+$")
+        hits = [k for k in self._state_loaded if pat.match(k)]
+        if len(hits) == 1:
+            return self._state_loaded.pop(hits[0])
+        return None
+
+    def _acc_base(self, pname, name):
+        # an optimizer created with name="opt" prefixes its accumulators (optimizer.py:623-624)
+        return f"{pname}_{self._name}_{name}" if self._name else f"{pname}_{name}"
+
     def _acc(self, name, p, dtype=torch.float32, fill=0.0, shape=None):
+        """accumulator ``name`` of parameter ``p``, named as the reference's _add_accumulator names
+        it — ``unique_name.generate(f"{param.name}_{name}")``, e.g. ``linear_0.w_0_moment1_0``
+        (python/paddle/optimizer/optimizer.py:636). Once a state dict is loaded, every accumulator
+        created must come from it: a missing one raises as the reference's assertion does
+        (optimizer.py:656-659) instead of silently restarting from ``fill``."""
         d = self._accumulators[name]
         t = d.get(p.name)
         if t is None:
-            key = f"{p.name}_{name}_0"
-            if key in self._state_loaded:
-                src = self._state_loaded.pop(key)
+            base = self._acc_base(p.name, name)
+            key = unique_name.generate(base)
+            src = self._take_loaded(base, key) if self._state_loaded else None
+            if src is None and self.__dict__.get("_strict_acc"):
+                raise AssertionError(f"Optimizer set error, {key} should in state dict")
+            if src is not None:
                 src_t = src._t if isinstance(src, Tensor) else torch.as_tensor(np.asarray(src))
                 t = _wrap(src_t.to(device=p._t.device, dtype=dtype).clone())
+                if shape is None and tuple(t._t.shape) != tuple(p._t.shape):
+                    raise ValueError(f"accumulator {key}: loaded shape {tuple(t._t.shape)} != parameter "
+                                     f"{p.name} shape {tuple(p._t.shape)}")
             else:
                 shp = p._t.shape if shape is None else shape
                 t = _wrap(torch.full(shp, fill, dtype=dtype, device=p._t.device))
             t.name = key
+            t.persistable = True
             d[p.name] = t
         return t
 
@@ -108,7 +144,7 @@ class Optimizer:
                 m = _wrap(src_t.to(device=p._t.device, dtype=torch.float32).clone())
             else:
                 m = _wrap(p._t.detach().float().clone())
-            m.name = p.name + "_fp32_master_0"
+            m.name = unique_name.generate(p.name + "_fp32_master")
             self._master_weights[p.name] = m
         return m
 
@@ -210,19 +246,29 @@ class Optimizer:
         return sd
 
     def set_state_dict(self, state_dict):
+        """Restore accumulators / master weights / LR state (reference optimizer.py:310). Keys are
+        the reference's accumulator names; accumulators that exist are overwritten now, the rest
+        are taken when first created — and from then on every accumulator must be in the dict
+        (AssertionError otherwise, as the reference). Keys that belong to no parameter of this
+        optimizer are reported (a renamed model restored nothing for them)."""
         state_dict = dict(state_dict)
         if isinstance(self._learning_rate, LRScheduler) and "LR_Scheduler" in state_dict:
             self._learning_rate.set_state_dict(state_dict.pop("LR_Scheduler"))
         self._step_count = int(state_dict.pop("@step_count@", self._step_count))
         self.__dict__.pop("_pstep", None)   # per-parameter counts are re-read from the loaded beta-pow accumulators
-        # existing accumulators are overwritten now; the rest are loaded lazily on first use
         for name, d in self._accumulators.items():
             for pname, t in d.items():
-                if t.name in state_dict:
-                    v = state_dict.pop(t.name)
-                    src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
-                    with torch.no_grad():
-                        t._t.copy_(src.to(t._t.device, t._t.dtype).reshape(t._t.shape))
+                base = self._acc_base(pname, name)
+                v = state_dict.pop(t.name, None)
+                if v is None:
+                    pat = re.compile(re.escape(base) + r"_\d+$")
+                    hits = [k for k in state_dict if pat.match(k)]
+                    v = state_dict.pop(hits[0]) if len(hits) == 1 else None
+                if v is None:
+                    raise AssertionError(f"Optimizer set error, {t.name} should in state dict")
+                src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+                with torch.no_grad():
+                    t._t.copy_(src.to(t._t.device, t._t.dtype).reshape(t._t.shape))
         mw = state_dict.get("master_weights")
         if mw:
             for pname, m in list(self._master_weights.items()):
@@ -231,6 +277,13 @@ class Optimizer:
                     src = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
                     with torch.no_grad():
                         m._t.copy_(src.to(m._t.device, torch.float32))
+        names = sorted({p.name for g in self._param_groups for p in g["params"]}, key=len, reverse=True)
+        stray = [k for k in state_dict if k not in self._STATE_META and not any(k.startswith(n + "_") for n in names)]
+        if stray and names:
+            warnings.warn(f"optimizer state: {len(stray)} key(s) match no parameter of this optimizer and are "
+                          f"ignored (e.g. {stray[:3]}); parameter names look like {names[-1]!r}", stacklevel=2)
+            for k in stray:
+                state_dict.pop(k)
         # snapshot the rest (loaded lazily on first use): the caller's dict may hold live tensors
         # of another optimizer that keep changing after this call
         snap = {}
@@ -242,6 +295,7 @@ class Optimizer:
             else:
                 snap[k] = v
         self._state_loaded.update(snap)
+        self._strict_acc = bool(self._loaded_accs())
 
     set_dict = set_state_dict
 

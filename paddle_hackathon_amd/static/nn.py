@@ -14,6 +14,7 @@ from ..framework.param_attr import ParamAttr
 from ..nn import functional as F
 from ..nn import initializer as I
 from ..nn.layer.layers import _create_parameter
+from ..utils import unique_name as _unique_name
 
 __all__ = ["fc", "batch_norm", "embedding", "sparse_embedding", "conv2d", "conv2d_transpose", "conv3d",
            "conv3d_transpose", "layer_norm", "group_norm", "instance_norm", "data_norm", "prelu",
@@ -29,18 +30,19 @@ def _act(x, act):
 
 
 def fc(x, size, num_flatten_dims=1, weight_attr=None, bias_attr=None, activation=None, name=None):
+    _h = name or _unique_name.generate("fc")
     xs = x if isinstance(x, (list, tuple)) else [x]
     out = None
     for xi in xs:
         in_dim = int(np.prod(xi.shape[num_flatten_dims:]))
-        w = _create_parameter([in_dim, size], xi.dtype, weight_attr)
+        w = _create_parameter([in_dim, size], xi.dtype, weight_attr, helper=_h)
         from ..tensor import reshape
         flat = reshape(xi, [-1 if num_flatten_dims == 1 else 0] * 0 + list(xi.shape[:num_flatten_dims]) + [in_dim]) \
             if len(xi.shape) != num_flatten_dims + 1 else xi
         y = F.linear(flat, w)
         out = y if out is None else out + y
     if bias_attr is not False:
-        b = _create_parameter([size], out.dtype, bias_attr, is_bias=True)
+        b = _create_parameter([size], out.dtype, bias_attr, is_bias=True, helper=_h)
         out = out + b
     return _act(out, activation)
 
@@ -48,9 +50,10 @@ def fc(x, size, num_flatten_dims=1, weight_attr=None, bias_attr=None, activation
 def batch_norm(input, act=None, is_test=False, momentum=0.9, epsilon=1e-05, param_attr=None, bias_attr=None,
                data_layout="NCHW", in_place=False, name=None, moving_mean_name=None, moving_variance_name=None,
                do_model_average_for_mean_and_var=True, use_global_stats=False):
+    _h = name or _unique_name.generate("batch_norm")
     c = input.shape[1] if data_layout == "NCHW" else input.shape[-1]
-    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0))
-    b = _create_parameter([c], "float32", bias_attr, is_bias=True)
+    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0), helper=_h)
+    b = _create_parameter([c], "float32", bias_attr, is_bias=True, helper=_h)
     from ..framework import core
     mean = _wrap(torch.zeros(c, device=core.default_device()))
     var = _wrap(torch.ones(c, device=core.default_device()))
@@ -62,7 +65,8 @@ def batch_norm(input, act=None, is_test=False, momentum=0.9, epsilon=1e-05, para
 
 
 def embedding(input, size, is_sparse=False, is_distributed=False, padding_idx=None, param_attr=None, dtype="float32"):
-    w = _create_parameter(list(size), dtype, param_attr, default_initializer=I.XavierUniform())
+    _h = _unique_name.generate("embedding")
+    w = _create_parameter(list(size), dtype, param_attr, default_initializer=I.XavierUniform(), helper=_h)
     return F.embedding(input, w, padding_idx)
 
 
@@ -79,12 +83,14 @@ def sparse_embedding(input, size, padding_idx=None, is_test=False, entry=None, t
 
 def _conv(fn, transpose, input, num_filters, filter_size, stride, padding, dilation, groups, param_attr, bias_attr,
           act, data_format, nd, output_size=None):
+    _h = _unique_name.generate(fn.__name__)   # conv2d / conv3d / conv2d_transpose / conv3d_transpose
     cin = input.shape[1] if data_format[1] == "C" else input.shape[-1]
     k = filter_size if isinstance(filter_size, (list, tuple)) else [filter_size] * nd
     shape = ([cin, num_filters // (groups or 1)] if transpose else [num_filters, cin // (groups or 1)]) + list(k)
     fan_in = cin // (groups or 1) * int(np.prod(k))
-    w = _create_parameter(shape, input.dtype, param_attr, default_initializer=I.Normal(0.0, (2.0 / fan_in) ** 0.5))
-    b = None if bias_attr is False else _create_parameter([num_filters], input.dtype, bias_attr, is_bias=True)
+    w = _create_parameter(shape, input.dtype, param_attr, default_initializer=I.Normal(0.0, (2.0 / fan_in) ** 0.5),
+                          helper=_h)
+    b = None if bias_attr is False else _create_parameter([num_filters], input.dtype, bias_attr, is_bias=True, helper=_h)
     if transpose:
         y = fn(input, w, b, stride, padding, 0, dilation, groups or 1, output_size, data_format) if nd == 2 else \
             fn(input, w, b, stride, padding, 0, groups or 1, dilation, output_size, data_format)
@@ -121,24 +127,27 @@ def conv3d_transpose(input, num_filters, output_size=None, filter_size=None, pad
 
 def layer_norm(input, scale=True, shift=True, begin_norm_axis=1, epsilon=1e-05, param_attr=None, bias_attr=None,
                act=None, name=None):
+    _h = name or _unique_name.generate("layer_norm")
     shape = input.shape[begin_norm_axis:]
     n = int(np.prod(shape))
-    w = _create_parameter([n], "float32", param_attr, default_initializer=I.Constant(1.0)) if scale else None
-    b = _create_parameter([n], "float32", bias_attr, is_bias=True) if shift else None
+    w = _create_parameter([n], "float32", param_attr, default_initializer=I.Constant(1.0), helper=_h) if scale else None
+    b = _create_parameter([n], "float32", bias_attr, is_bias=True, helper=_h) if shift else None
     return _act(F.layer_norm(input, shape, w, b, epsilon), act)
 
 
 def group_norm(input, groups, epsilon=1e-05, param_attr=None, bias_attr=None, act=None, data_layout="NCHW", name=None):
+    _h = name or _unique_name.generate("group_norm")
     c = input.shape[1] if data_layout == "NCHW" else input.shape[-1]
-    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0))
-    b = _create_parameter([c], "float32", bias_attr, is_bias=True)
+    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0), helper=_h)
+    b = _create_parameter([c], "float32", bias_attr, is_bias=True, helper=_h)
     return _act(F.group_norm(input, groups, epsilon, w, b, data_layout), act)
 
 
 def instance_norm(input, epsilon=1e-05, param_attr=None, bias_attr=None, name=None):
+    _h = name or _unique_name.generate("instance_norm")
     c = input.shape[1]
-    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0))
-    b = _create_parameter([c], "float32", bias_attr, is_bias=True)
+    w = _create_parameter([c], "float32", param_attr, default_initializer=I.Constant(1.0), helper=_h)
+    b = _create_parameter([c], "float32", bias_attr, is_bias=True, helper=_h)
     return F.instance_norm(input, weight=w, bias=b, eps=epsilon)
 
 
@@ -159,13 +168,14 @@ def data_norm(input, act=None, epsilon=1e-05, param_attr=None, data_layout="NCHW
 
 
 def prelu(x, mode, param_attr=None, data_format="NCHW", name=None):
+    _h = name or _unique_name.generate("prelu")
     if mode == "all":
         shape = [1]
     elif mode == "channel":
         shape = [x.shape[1] if data_format == "NCHW" else x.shape[-1]]
     else:
         shape = list(x.shape[1:])
-    w = _create_parameter(shape, "float32", param_attr, default_initializer=I.Constant(0.25))
+    w = _create_parameter(shape, "float32", param_attr, default_initializer=I.Constant(0.25), helper=_h)
 
     def _prelu(x, w):
         t, wt = x._t, w._t
@@ -176,17 +186,19 @@ def prelu(x, mode, param_attr=None, data_format="NCHW", name=None):
 
 
 def bilinear_tensor_product(x, y, size, act=None, name=None, param_attr=None, bias_attr=None):
-    w = _create_parameter([size, x.shape[-1], y.shape[-1]], "float32", param_attr)
-    b = None if bias_attr is False else _create_parameter([1, size], "float32", bias_attr, is_bias=True)
+    _h = name or _unique_name.generate("bilinear_tensor_product")
+    w = _create_parameter([size, x.shape[-1], y.shape[-1]], "float32", param_attr, helper=_h)
+    b = None if bias_attr is False else _create_parameter([1, size], "float32", bias_attr, is_bias=True, helper=_h)
     return _act(F.bilinear(x, y, w, b), act)
 
 
 def deform_conv2d(x, offset, mask, num_filters, filter_size, stride=1, padding=0, dilation=1, groups=1,
                   deformable_groups=1, im2col_step=1, weight_attr=None, bias_attr=None, name=None):
+    _h = name or _unique_name.generate("deformable_conv")
     from ..vision.ops import deform_conv2d as _dc
     k = filter_size if isinstance(filter_size, (list, tuple)) else [filter_size] * 2
-    w = _create_parameter([num_filters, x.shape[1] // groups] + list(k), "float32", weight_attr)
-    b = None if bias_attr is False else _create_parameter([num_filters], "float32", bias_attr, is_bias=True)
+    w = _create_parameter([num_filters, x.shape[1] // groups] + list(k), "float32", weight_attr, helper=_h)
+    b = None if bias_attr is False else _create_parameter([num_filters], "float32", bias_attr, is_bias=True, helper=_h)
     return static_op(_dc, "deform_conv2d")(x, offset, w, b, stride, padding, dilation, deformable_groups, groups, mask)
 
 
@@ -198,9 +210,10 @@ def spectral_norm(weight, dim=0, power_iters=1, eps=1e-12, name=None):
 
 def nce(input, label, num_total_classes, sample_weight=None, param_attr=None, bias_attr=None, num_neg_samples=None,
         name=None, sampler="uniform", custom_dist=None, seed=0, is_sparse=False):
+    _h = name or _unique_name.generate("nce")
     dim = input.shape[-1]
-    w = _create_parameter([num_total_classes, dim], "float32", param_attr)
-    b = _create_parameter([num_total_classes, 1], "float32", bias_attr, is_bias=True)
+    w = _create_parameter([num_total_classes, dim], "float32", param_attr, helper=_h)
+    b = _create_parameter([num_total_classes, 1], "float32", bias_attr, is_bias=True, helper=_h)
     k = num_neg_samples or 10
 
     def _nce(x, lab, w, b):
@@ -216,8 +229,9 @@ def nce(input, label, num_total_classes, sample_weight=None, param_attr=None, bi
 
 
 def row_conv(input, future_context_size, param_attr=None, act=None):
+    _h = _unique_name.generate("row_conv")
     d = input.shape[-1]
-    w = _create_parameter([future_context_size + 1, d], "float32", param_attr)
+    w = _create_parameter([future_context_size + 1, d], "float32", param_attr, helper=_h)
 
     def _rc(x, w):
         t = x._t
@@ -230,9 +244,10 @@ def row_conv(input, future_context_size, param_attr=None, act=None):
 
 
 def crf_decoding(input, param_attr, label=None, length=None):
+    _h = _unique_name.generate("crf_decoding")
     from ..text import viterbi_decode
     n = input.shape[-1]
-    trans = _create_parameter([n + 2, n], "float32", param_attr)
+    trans = _create_parameter([n + 2, n], "float32", param_attr, helper=_h)
 
     def _crf(x, tr, ln):
         lens = ln._t if ln is not None else torch.full((x._t.shape[0],), x._t.shape[1], dtype=torch.int64, device=x._t.device)
