@@ -29,6 +29,7 @@ EPI_RSTAGE = 32768   # gemm4p NT: register-staged operands
 EPI_EARLY = 65536    # gemm4p: early-release schedule (read burst + buffer release early in phase A)
 EPI_RING = 1 << 22   # gemm4p NT: 4-slot ring of 32-deep stages (gemm4r_kernel; K % 64 == 0, K >= 128)
 EPI_ADEEP = 1 << 23  # gemm4p NT, no bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel; K >= 256)
+EPI_WSTAG = 1 << 24  # gemm4p NT + EARLY: wave w issues its LDS-DMA after MFMA w of a group
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
