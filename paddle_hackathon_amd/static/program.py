@@ -567,20 +567,52 @@ def _dynamic_dims(v):
     return tuple(i for i, d in enumerate(ds) if d is not None and d < 0)
 
 
-def _to_probe(tree):
+def _to_probe(tree, size=_PROBE):
     if isinstance(tree, Variable):
         dims = _dynamic_dims(tree)
         if not dims:
             return _wrap(tree._t)
-        shp = [_PROBE if i in dims else int(s) for i, s in enumerate(tree._t.shape)]
+        shp = [size if i in dims else int(s) for i, s in enumerate(tree._t.shape)]
         return _wrap(torch.empty(shp, dtype=tree._t.dtype, device="meta"))
     if isinstance(tree, list):
-        return [_to_probe(t) for t in tree]
+        return [_to_probe(t, size) for t in tree]
     if isinstance(tree, tuple):
-        return tuple(_to_probe(t) for t in tree)
+        return tuple(_to_probe(t, size) for t in tree)
     if isinstance(tree, dict):
-        return {k: _to_probe(v) for k, v in tree.items()}
+        return {k: _to_probe(v, size) for k, v in tree.items()}
     return _to_meta(tree)
+
+
+def _infer_meta_dynamic(fn, bargs, bkw):
+    """InferMeta for an op that rejects the size-1 stand-in of a -1 dim (BatchNorm training at a
+    1 x 1 map: "more than 1 value per channel", instance / group statistics ...). The reference's
+    InferMeta is shape-only (phi/infermeta/multiary.cc:437) and never sees a value; here the op
+    runs on meta inputs whose -1 dims take two probe sizes, the output dims that follow them
+    become -1 (stored as 1, as every -1 dim of a recorded Variable) and the rest are static.
+    None when no input has a -1 dim or a probe fails too."""
+    if not any(_dynamic_dims(v) for v in _iter_vars((bargs, bkw))):
+        return None
+    _core._mode.record_depth += 1
+    try:
+        a = fn(*_to_probe(bargs, _PROBE), **_to_probe(bkw, _PROBE))
+        b = fn(*_to_probe(bargs, _PROBE + 6), **_to_probe(bkw, _PROBE + 6))
+    except Exception:   # noqa: BLE001 - the original error is raised by the caller
+        return None
+    finally:
+        _core._mode.record_depth -= 1
+    ta = list(_iter_tensors(a if isinstance(a, (list, tuple)) else [a]))
+    tb = list(_iter_tensors(b if isinstance(b, (list, tuple)) else [b]))
+    if len(ta) != len(tb):
+        return None
+    dyn = []
+    for x, y in zip(ta, tb):
+        d = tuple(i for i, (p, q) in enumerate(zip(x._t.shape, y._t.shape)) if p != q) \
+            if x._t.dim() == y._t.dim() else ()
+        dyn.append(d)
+        if d:   # the -1 dims' stand-in size 1, in place
+            x._t = torch.empty([1 if i in d else int(n) for i, n in enumerate(x._t.shape)], dtype=x._t.dtype,
+                               device="meta")
+    return _meta_of(a), dyn
 
 
 def _propagate_dynamic(fn, bargs, bkw, meta_out):
@@ -619,7 +651,13 @@ def record_op(fn, name, args, kwargs):
     qual = f"{fn.__module__}.{name}"
     OP_REGISTRY.setdefault(qual, fn)
     bargs, bkw = _bind(fn, args, kwargs)
-    meta_out, dyn = _infer_meta(fn, name, bargs, bkw)
+    try:
+        meta_out, dyn = _infer_meta(fn, name, bargs, bkw)
+    except Exception:
+        r = _infer_meta_dynamic(fn, bargs, bkw)
+        if r is None:
+            raise
+        meta_out, dyn = r
     if dyn is None and os.environ.get("PHA_STATIC_DYN_DIMS", "1") != "0":
         dyn = _propagate_dynamic(fn, bargs, bkw, meta_out)
     blk = default_main_program().current_block()
