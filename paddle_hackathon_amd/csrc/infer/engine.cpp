@@ -303,10 +303,15 @@ size_t dtype_size(int dt) {
 }
 
 Buffer::Buffer(size_t bytes, int d) : n(bytes), dev(d) {
-  p = dev >= 0 ? gpu::alloc(bytes) : ::operator new(bytes ? bytes : 16);
+  if (dev >= 0) {
+    ctx = gpu::current();
+    p = gpu::alloc(bytes);
+  } else {
+    p = ::operator new(bytes ? bytes : 16);
+  }
 }
 Buffer::~Buffer() {
-  if (dev >= 0) gpu::free(p);
+  if (dev >= 0) gpu::release(ctx, p, n);
   else ::operator delete(p);
 }
 
@@ -331,8 +336,10 @@ Tensor to_device(const Tensor& t, int dev) {
 namespace {
 // ---- the params stream ---------------------------------------------------------------------------
 Tensor read_lod_tensor(const std::string& buf, size_t& off) {
-  auto need = [&](size_t n) {
-    if (off + n > buf.size()) throw Error("params stream truncated");
+  // every length read from the file is checked against the bytes left before it is used
+  // (n > size - off cannot wrap, unlike off + n > size)
+  auto need = [&](uint64_t n) {
+    if (off > buf.size() || n > buf.size() - off) throw Error("params stream truncated");
   };
   uint32_t ver;
   need(4);
@@ -343,11 +350,14 @@ Tensor read_lod_tensor(const std::string& buf, size_t& off) {
   need(8);
   std::memcpy(&nlod, buf.data() + off, 8);
   off += 8;
+  if (nlod > 8) throw Error("params stream: " + std::to_string(nlod) + " LoD levels");
   for (uint64_t i = 0; i < nlod; ++i) {
     uint64_t nb;
     need(8);
     std::memcpy(&nb, buf.data() + off, 8);
-    off += 8 + nb;
+    off += 8;
+    need(nb);
+    off += nb;
   }
   need(8);
   std::memcpy(&ver, buf.data() + off, 4);
@@ -356,11 +366,20 @@ Tensor read_lod_tensor(const std::string& buf, size_t& off) {
   int32_t dsz;
   std::memcpy(&dsz, buf.data() + off, 4);
   off += 4;
-  need((size_t)dsz);
+  if (dsz < 0) throw Error("params stream: negative tensor desc size");
+  need((uint64_t)dsz);
   int dtype = F32;
   std::vector<int64_t> dims;
   parse_tensor_desc(Wire(buf.data() + off, (size_t)dsz), dtype, dims);
   off += (size_t)dsz;
+  uint64_t elems = 1;
+  for (auto d : dims) {
+    if (d < 0) throw Error("params stream: negative dim in a persistable's shape");
+    if (d && elems > (uint64_t)INT64_MAX / (uint64_t)d) throw Error("params stream: tensor size overflows");
+    elems *= (uint64_t)d;
+  }
+  if (elems > (uint64_t)INT64_MAX / 8) throw Error("params stream: tensor size overflows");
+  need(elems * dtype_size(dtype));   // before allocating it
   Tensor t = make_tensor(dims, dtype, -1);
   need(t.bytes());
   std::memcpy(t.raw(), buf.data() + off, t.bytes());
@@ -1344,31 +1363,35 @@ const std::map<std::string, OpFn>& registry() {
 struct Predictor {
   Program prog;
   int dev = -1;
+  gpu::Context* gctx = nullptr;   // this predictor's device, stream and block pool
   std::map<std::string, Tensor> params;   // persistables, on the device
   std::vector<std::string> in_names, out_names;
   std::map<std::string, Tensor> inputs;   // set_input values (device)
   std::vector<Tensor> outputs;            // last run's fetch values (host)
   std::vector<std::vector<std::string>> release;   // per op: intermediates dead after it
   std::string unsupported;
+  std::vector<std::string> applied_passes;
 
-  Predictor(const std::string& model_file, const std::string& params_file, int device) : dev(device) {
+  Predictor(const std::string& model_file, const std::string& params_file, int device, bool ir_optim = true)
+      : dev(device) {
     prog = parse_program(read_file(model_file));
-    if (dev >= 0) gpu::set_device(dev);
-    const Block& b = prog.blocks[0];
-    // persistables in name order (save_combine writes them sorted by name)
+    if (dev >= 0) gctx = gpu::create_context(dev);
+    gpu::Bind bind(gctx);
+    Block& b = prog.blocks[0];
+    // persistables in name order (save_combine writes them sorted by name), read on the host
     std::vector<std::string> pnames;
     for (auto& v : b.vars)
       if (v.persistable && v.type == 7 && v.name != "feed" && v.name != "fetch") pnames.push_back(v.name);
     std::sort(pnames.begin(), pnames.end());
+    std::map<std::string, Tensor> host;
     if (!pnames.empty()) {
       const std::string pb = read_file(params_file);
       size_t off = 0;
-      for (auto& n : pnames) {
-        Tensor t = read_lod_tensor(pb, off);
-        params[n] = dev >= 0 ? to_device(t, dev) : t;
-      }
+      for (auto& n : pnames) host[n] = read_lod_tensor(pb, off);
       if (off != pb.size()) throw Error("params file has trailing bytes (program / params mismatch)");
     }
+    if (ir_optim) run_passes(b, host);
+    for (auto& kv : host) params[kv.first] = dev >= 0 ? to_device(kv.second, dev) : kv.second;
     std::map<int, std::string> ins, outs;
     std::set<std::string> missing;
     for (auto& op : b.ops) {
@@ -1390,8 +1413,100 @@ struct Predictor {
       if (!params.count(kv.first) && !keep.count(kv.first)) release[kv.second].push_back(kv.first);
   }
 
+  ~Predictor() {
+    {
+      gpu::Bind bind(gctx);
+      params.clear();
+      inputs.clear();
+      outputs.clear();
+    }
+    gpu::destroy_context(gctx);
+  }
+
+  // ---- IR passes on the host copies of the persistables (reference paddle_pass_builder.cc:108:
+  // conv_bn_fuse_pass, conv_eltwiseadd_bn_fuse_pass, conv_elementwise_add_fuse_pass) -------------
+  static std::map<std::string, int> consumers(const Block& b) {
+    std::map<std::string, int> n;
+    for (auto& op : b.ops)
+      for (auto& kv : op.inputs)
+        for (auto& v : kv.second) ++n[v];
+    return n;
+  }
+  static const OpDesc* sole_consumer(const Block& b, const std::string& v, size_t after) {
+    const OpDesc* hit = nullptr;
+    for (size_t i = after; i < b.ops.size(); ++i)
+      for (auto& kv : b.ops[i].inputs)
+        for (auto& n : kv.second)
+          if (n == v) {
+            if (hit) return nullptr;
+            hit = &b.ops[i];
+          }
+    return hit;
+  }
+  void run_passes(Block& b, std::map<std::string, Tensor>& host) {
+    int add_fused = 0, bn_fused = 0;
+    auto is_conv = [](const OpDesc& o) { return o.type == "conv2d" || o.type == "depthwise_conv2d"; };
+    auto f32_param = [&](const std::string& n) { return host.count(n) && host[n].dtype == F32; };
+    for (size_t i = 0; i < b.ops.size(); ++i) {
+      OpDesc& conv = b.ops[i];
+      if (!is_conv(conv) || conv.gets("data_format", "NCHW") == "NHWC" || !f32_param(conv.in("Filter"))) continue;
+      // conv + elementwise_add(per-channel persistable, axis 1) -> conv with Bias
+      if (conv.in("Bias").empty()) {
+        const OpDesc* add = sole_consumer(b, conv.out("Output"), i + 1);
+        if (add && add->type == "elementwise_add" && add->in("X") == conv.out("Output") && add->geti("axis", -1) == 1 &&
+            f32_param(add->in("Y")) && host[add->in("Y")].numel() == host[conv.in("Filter")].shape[0]) {
+          conv.inputs["Bias"] = {add->in("Y")};
+          const std::string out = add->out("Out");
+          b.ops.erase(b.ops.begin() + (add - &b.ops[0]));
+          conv.outputs["Output"] = {out};
+          ++add_fused;
+        }
+      }
+      // conv (+ Bias) + batch_norm (inference statistics) -> conv with folded filter and bias
+      const OpDesc* bn = sole_consumer(b, conv.out("Output"), i + 1);
+      if (!bn || bn->type != "batch_norm" || bn->in("X") != conv.out("Output")) continue;
+      if (!(bn->getb("is_test", false) || bn->getb("use_global_stats", false))) continue;
+      if (bn->gets("data_layout", "NCHW") != "NCHW") continue;
+      const std::string sn = bn->in("Scale"), bnb = bn->in("Bias"), mn = bn->in("Mean"), vn = bn->in("Variance");
+      if (!f32_param(sn) || !f32_param(bnb) || !f32_param(mn) || !f32_param(vn)) continue;
+      const Tensor& w = host[conv.in("Filter")];
+      const int64_t Co = w.shape[0], per = w.numel() / Co;
+      const float eps = (float)bn->getf("epsilon", 1e-5);
+      Tensor nw = make_tensor(w.shape, F32, -1), nb = make_tensor({Co}, F32, -1);
+      const float* cb = conv.in("Bias").empty() ? nullptr : host[conv.in("Bias")].data<float>();
+      for (int64_t c = 0; c < Co; ++c) {
+        const float k = host[sn].data<float>()[c] / std::sqrt(host[vn].data<float>()[c] + eps);
+        for (int64_t e = 0; e < per; ++e) nw.data<float>()[c * per + e] = w.data<float>()[c * per + e] * k;
+        nb.data<float>()[c] = ((cb ? cb[c] : 0.f) - host[mn].data<float>()[c]) * k + host[bnb].data<float>()[c];
+      }
+      const std::string base = conv.out("Output");
+      host[base + "@bn_folded_filter"] = nw;
+      host[base + "@bn_folded_bias"] = nb;
+      conv.inputs["Filter"] = {base + "@bn_folded_filter"};
+      conv.inputs["Bias"] = {base + "@bn_folded_bias"};
+      const std::string out = bn->out("Y");
+      b.ops.erase(b.ops.begin() + (bn - &b.ops[0]));
+      conv.outputs["Output"] = {out};
+      ++bn_fused;
+    }
+    // persistables no op reads any more (the original filters / BN statistics) are dropped
+    const auto uses = consumers(b);
+    for (auto it = host.begin(); it != host.end();) {
+      if (!uses.count(it->first)) it = host.erase(it);
+      else ++it;
+    }
+    if (add_fused) applied_passes.push_back("conv_elementwise_add_fuse_pass x" + std::to_string(add_fused));
+    if (bn_fused) applied_passes.push_back("conv_bn_fuse_pass x" + std::to_string(bn_fused));
+  }
+
+  void set_input(const std::string& name, const Tensor& host_t) {
+    gpu::Bind bind(gctx);
+    inputs[name] = dev >= 0 ? to_device(host_t, dev) : host_t;
+  }
+
   void run() {
     if (!unsupported.empty()) throw Error("the program has ops the native engine does not run: " + unsupported);
+    gpu::Bind bind(gctx);
     const Block& b = prog.blocks[0];
     std::map<std::string, Tensor> env = params;
     for (auto& n : in_names) {
@@ -1425,6 +1540,7 @@ using pha_infer::Tensor;
 
 struct PhaPredictor {
   Predictor* p;
+  std::string passes;
 };
 
 namespace {
@@ -1444,10 +1560,22 @@ int guard(F&& f) {
 
 extern "C" {
 
-PhaPredictor* pha_infer_create(const char* model_file, const char* params_file, int device) {
+PhaPredictor* pha_infer_create2(const char* model_file, const char* params_file, int device, int ir_optim) {
   PhaPredictor* out = nullptr;
-  guard([&] { out = new PhaPredictor{new Predictor(model_file, params_file ? params_file : "", device)}; });
+  guard([&] {
+    auto* pr = new Predictor(model_file, params_file ? params_file : "", device, ir_optim != 0);
+    std::string s;
+    for (auto& x : pr->applied_passes) s += (s.empty() ? "" : ";") + x;
+    out = new PhaPredictor{pr, s};
+  });
   return out;
+}
+PhaPredictor* pha_infer_create(const char* model_file, const char* params_file, int device) {
+  return pha_infer_create2(model_file, params_file, device, 1);
+}
+const char* pha_infer_applied_passes(const PhaPredictor* p) { return p->passes.c_str(); }
+size_t pha_infer_pooled_bytes(const PhaPredictor* p) {
+  return p->p->gctx ? pha_infer::gpu::pooled_bytes(p->p->gctx) : 0;
 }
 const char* pha_infer_last_error(void) { return g_err.c_str(); }
 int pha_infer_num_inputs(const PhaPredictor* p) { return (int)p->p->in_names.size(); }
@@ -1461,7 +1589,7 @@ int pha_infer_set_input(PhaPredictor* p, const char* name, int dtype, const int6
   return guard([&] {
     Tensor host = pha_infer::make_tensor(std::vector<int64_t>(shape, shape + ndim), dtype, -1);
     std::memcpy(host.raw(), data, host.bytes());
-    p->p->inputs[name] = p->p->dev >= 0 ? pha_infer::to_device(host, p->p->dev) : host;
+    p->p->set_input(name, host);
   });
 }
 int pha_infer_run(PhaPredictor* p) { return guard([&] { p->p->run(); }); }
@@ -1492,6 +1620,7 @@ struct PD_Config {
   std::string prog, params;
   bool gpu = false;
   int dev = 0;
+  bool ir_optim = true;
 };
 struct PD_Predictor {
   PhaPredictor* p;
@@ -1504,6 +1633,8 @@ struct PD_Tensor {
 };
 
 PD_Config* PD_ConfigCreate(void) { return new PD_Config(); }
+void PD_ConfigSwitchIrOptim(PD_Config* c, PD_Bool x) { c->ir_optim = x != 0; }
+PD_Bool PD_ConfigIrOptim(PD_Config* c) { return c->ir_optim; }
 void PD_ConfigDestroy(PD_Config* c) { delete c; }
 void PD_ConfigSetModel(PD_Config* c, const char* prog, const char* params) {
   c->prog = prog;
@@ -1520,7 +1651,7 @@ PD_Bool PD_ConfigUseGpu(PD_Config* c) { return c->gpu; }
 int32_t PD_ConfigGpuDeviceId(PD_Config* c) { return c->dev; }
 
 PD_Predictor* PD_PredictorCreate(PD_Config* c) {
-  PhaPredictor* p = pha_infer_create(c->prog.c_str(), c->params.c_str(), c->gpu ? c->dev : -1);
+  PhaPredictor* p = pha_infer_create2(c->prog.c_str(), c->params.c_str(), c->gpu ? c->dev : -1, c->ir_optim);
   delete c;
   if (!p) {
     std::fprintf(stderr, "PD_PredictorCreate: %s\n", g_err.c_str());

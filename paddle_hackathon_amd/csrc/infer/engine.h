@@ -61,10 +61,15 @@ Program parse_program(const std::string& bytes);
 enum DType { BOOL = 0, I16 = 1, I32 = 2, I64 = 3, F16 = 4, F32 = 5, F64 = 6, U8 = 20, I8 = 21 };
 size_t dtype_size(int dt);
 
+namespace gpu {
+struct Context;
+}
+
 struct Buffer {
   void* p = nullptr;
   size_t n = 0;
   int dev = -1;   // -1 host
+  gpu::Context* ctx = nullptr;   // device blocks: the pool they return to
   Buffer(size_t bytes, int dev);
   ~Buffer();
   Buffer(const Buffer&) = delete;
@@ -98,11 +103,24 @@ struct Error : std::runtime_error {
 
 // ---- GPU entry points (gpu.hip). All fp32 unless noted; stream = the engine's stream. ------------
 namespace gpu {
-void set_device(int dev);
+// a predictor's device, stream and block pool; GPU calls run on the context bound to the thread
+Context* create_context(int dev);
+void destroy_context(Context* c);
+struct Bind {   // RAII: hipSetDevice(c->dev) + bind c to this thread; restores both on exit
+  explicit Bind(Context* c);
+  ~Bind();
+  Bind(const Bind&) = delete;
+  Bind& operator=(const Bind&) = delete;
+  void* prev_ctx;
+  Context* ctx;
+  int prev_dev = 0;
+};
+Context* current();
+size_t pooled_bytes(Context* c);
 void* stream();
 void sync();
-void* alloc(size_t n);
-void free(void* p);
+void* alloc(size_t n);                       // from the bound context's pool
+void release(Context* c, void* p, size_t n); // back to c's pool
 void h2d(void* dst, const void* src, size_t n);
 void d2h(void* dst, const void* src, size_t n);
 void d2d(void* dst, const void* src, size_t n);

@@ -8,15 +8,33 @@
 
 #include <cmath>
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "engine.h"
 
 namespace pha_infer {
 namespace gpu {
 
+// Per-predictor device context: device id, its own non-blocking stream and a caching pool of
+// device blocks (exact-size free lists, rounded to 256 B). Every entry point below runs on the
+// context bound to the calling thread (``Bind``), so two predictors on different devices, or a
+// predictor driven from a thread whose current HIP device was changed by someone else, each use
+// their own device and stream (reference: Config.EnableUseGpu(mem, dev_id) per predictor, the
+// pooled allocator of analysis_predictor.cc:398-406).
+struct Context {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::map<size_t, std::vector<void*>> free_blocks;
+  std::vector<void*> all_blocks;
+  size_t pooled_bytes = 0;
+};
+
 namespace {
-hipStream_t g_stream = nullptr;
+thread_local Context* tl_ctx = nullptr;
 
 void ck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
@@ -349,30 +367,83 @@ Dims8 dims(int nd, const int64_t* shape, const int64_t* sx, const int64_t* sy) {
 }
 }  // namespace
 
-void set_device(int dev) {
+Context* create_context(int dev) {
   ck(hipSetDevice(dev), "hipSetDevice");
-  if (!g_stream) ck(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking), "hipStreamCreate");
+  auto* c = new Context();
+  c->dev = dev;
+  ck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  return c;
 }
-void* stream() { return g_stream; }
-void sync() { ck(hipStreamSynchronize(g_stream), "hipStreamSynchronize"); }
+void destroy_context(Context* c) {
+  if (!c) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(c->dev);
+  (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->all_blocks) (void)hipFree(p);
+  (void)hipStreamDestroy(c->stream);
+  (void)hipSetDevice(prev);
+  delete c;
+}
+Bind::Bind(Context* c) : prev_ctx(tl_ctx), ctx(c) {
+  if (!c) return;
+  (void)hipGetDevice(&prev_dev);
+  ck(hipSetDevice(c->dev), "hipSetDevice");
+  tl_ctx = c;
+}
+Bind::~Bind() {
+  if (!ctx) return;
+  tl_ctx = static_cast<Context*>(prev_ctx);
+  (void)hipSetDevice(prev_dev);
+}
+Context* current() {
+  if (!tl_ctx) throw Error("native engine: GPU call outside a predictor's device context");
+  return tl_ctx;
+}
+static hipStream_t cur_stream() { return current()->stream; }
+void* stream() { return cur_stream(); }
+void sync() { ck(hipStreamSynchronize(cur_stream()), "hipStreamSynchronize"); }
 void* alloc(size_t n) {
+  Context* c = current();
+  const size_t sz = ((n ? n : 16) + 255) & ~(size_t)255;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->free_blocks.find(sz);
+    if (it != c->free_blocks.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      return p;
+    }
+  }
   void* p = nullptr;
-  ck(hipMalloc(&p, n ? n : 16), "hipMalloc");
+  ck(hipMalloc(&p, sz), "hipMalloc");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->all_blocks.push_back(p);
+  c->pooled_bytes += sz;
   return p;
 }
-void free(void* p) {
-  if (p) (void)hipFree(p);
+// a block back into its context's pool: reused by later allocations of the same size, which are
+// ordered after every use of the block on the context's single stream; freed with the context
+void release(Context* c, void* p, size_t n) {
+  if (!p || !c) return;
+  const size_t sz = ((n ? n : 16) + 255) & ~(size_t)255;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->free_blocks[sz].push_back(p);
+}
+size_t pooled_bytes(Context* c) {
+  std::lock_guard<std::mutex> g(c->mu);
+  return c->pooled_bytes;
 }
 void h2d(void* dst, const void* src, size_t n) {
-  ck(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, g_stream), "h2d");
+  ck(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, cur_stream()), "h2d");
   sync();
 }
 void d2h(void* dst, const void* src, size_t n) {
-  ck(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, g_stream), "d2h");
+  ck(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, cur_stream()), "d2h");
   sync();
 }
 void d2d(void* dst, const void* src, size_t n) {
-  ck(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, g_stream), "d2d");
+  ck(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, cur_stream()), "d2d");
 }
 
 void gemm(const float* A, const float* B, float* C, const float* bias, int batch, int M, int N, int K, int64_t sAb,
@@ -381,27 +452,27 @@ void gemm(const float* A, const float* B, float* C, const float* bias, int batch
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (batch > 65535) throw Error("gemm: batch > 65535");
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
-  hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, g_stream, A, B, C, bias, M, N, K, sAb, sAm, sAk, sBb, sBk, sBn,
+  hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, cur_stream(), A, B, C, bias, M, N, K, sAb, sAm, sAk, sBb, sBk, sBn,
                      sCb, sCm, alpha, relu ? 1 : 0);
   ck_launch("gemm");
 }
 
 void im2col(const float* x, float* col, int C, int H, int W, int KH, int KW, int OH, int OW, int sh, int sw, int pt,
             int pl, int dh, int dw) {
-  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for((int64_t)C * KH * KW * OH * OW)), dim3(256), 0, g_stream, x, col, C,
+  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for((int64_t)C * KH * KW * OH * OW)), dim3(256), 0, cur_stream(), x, col, C,
                      H, W, KH, KW, OH, OW, sh, sw, pt, pl, dh, dw);
   ck_launch("im2col");
 }
 
 void depthwise_conv(const float* x, const float* w, float* y, int N, int C, int H, int W, int KH, int KW, int OH,
                     int OW, int sh, int sw, int pt, int pl, int dh, int dw, int mult) {
-  hipLaunchKernelGGL(dwconv_kernel, dim3(blocks_for((int64_t)N * C * mult * OH * OW)), dim3(256), 0, g_stream, x, w, y,
+  hipLaunchKernelGGL(dwconv_kernel, dim3(blocks_for((int64_t)N * C * mult * OH * OW)), dim3(256), 0, cur_stream(), x, w, y,
                      N, C, H, W, KH, KW, OH, OW, sh, sw, pt, pl, dh, dw, mult);
   ck_launch("depthwise_conv");
 }
 
 void unary(const float* x, float* y, int64_t n, int op, float a, float b) {
-  hipLaunchKernelGGL(unary_kernel, dim3(blocks_for(n)), dim3(256), 0, g_stream, x, y, n, op, a, b);
+  hipLaunchKernelGGL(unary_kernel, dim3(blocks_for(n)), dim3(256), 0, cur_stream(), x, y, n, op, a, b);
   ck_launch("unary");
 }
 
@@ -410,7 +481,7 @@ void binary(const float* x, const float* y, float* out, int op, int nd, const in
   int64_t total = 1;
   for (int k = 0; k < nd; ++k) total *= shape[k];
   if (!total) return;
-  hipLaunchKernelGGL(binary_kernel, dim3(blocks_for(total)), dim3(256), 0, g_stream, x, y, out, op, nd,
+  hipLaunchKernelGGL(binary_kernel, dim3(blocks_for(total)), dim3(256), 0, cur_stream(), x, y, out, op, nd,
                      dims(nd, shape, sx, sy), total);
   ck_launch("binary");
 }
@@ -418,14 +489,14 @@ void binary(const float* x, const float* y, float* out, int op, int nd, const in
 void batch_norm(const float* x, float* y, const float* scale, const float* bias, const float* mean,
                 const float* var, float eps, int64_t N, int64_t C, int64_t inner) {
   const int64_t total = N * C * inner;
-  hipLaunchKernelGGL(bn_kernel, dim3(blocks_for(total)), dim3(256), 0, g_stream, x, y, scale, bias, mean, var, eps, C,
+  hipLaunchKernelGGL(bn_kernel, dim3(blocks_for(total)), dim3(256), 0, cur_stream(), x, y, scale, bias, mean, var, eps, C,
                      inner, total);
   ck_launch("batch_norm");
 }
 
 void pool2d(const float* x, float* y, int N, int C, int H, int W, int OH, int OW, int KH, int KW, int sh, int sw,
             int pt, int pl, bool maxp, bool exclusive, bool adaptive) {
-  hipLaunchKernelGGL(pool_kernel, dim3(blocks_for((int64_t)N * C * OH * OW)), dim3(256), 0, g_stream, x, y, N, C, H, W,
+  hipLaunchKernelGGL(pool_kernel, dim3(blocks_for((int64_t)N * C * OH * OW)), dim3(256), 0, cur_stream(), x, y, N, C, H, W,
                      OH, OW, KH, KW, sh, sw, pt, pl, maxp ? 1 : 0, exclusive ? 1 : 0, adaptive ? 1 : 0);
   ck_launch("pool2d");
 }
@@ -437,31 +508,31 @@ void strided_copy(const void* in, void* out, int esize, int nd, const int64_t* s
   const Dims8 d = dims(nd, shape, strides, nullptr);
   const dim3 g(blocks_for(total));
   if (esize == 4)
-    hipLaunchKernelGGL(strided_kernel<uint32_t>, g, dim3(256), 0, g_stream, (const uint32_t*)in, (uint32_t*)out, nd, d, total);
+    hipLaunchKernelGGL(strided_kernel<uint32_t>, g, dim3(256), 0, cur_stream(), (const uint32_t*)in, (uint32_t*)out, nd, d, total);
   else if (esize == 8)
-    hipLaunchKernelGGL(strided_kernel<uint64_t>, g, dim3(256), 0, g_stream, (const uint64_t*)in, (uint64_t*)out, nd, d, total);
+    hipLaunchKernelGGL(strided_kernel<uint64_t>, g, dim3(256), 0, cur_stream(), (const uint64_t*)in, (uint64_t*)out, nd, d, total);
   else if (esize == 2)
-    hipLaunchKernelGGL(strided_kernel<uint16_t>, g, dim3(256), 0, g_stream, (const uint16_t*)in, (uint16_t*)out, nd, d, total);
+    hipLaunchKernelGGL(strided_kernel<uint16_t>, g, dim3(256), 0, cur_stream(), (const uint16_t*)in, (uint16_t*)out, nd, d, total);
   else
-    hipLaunchKernelGGL(strided_kernel<uint8_t>, g, dim3(256), 0, g_stream, (const uint8_t*)in, (uint8_t*)out, nd, d, total);
+    hipLaunchKernelGGL(strided_kernel<uint8_t>, g, dim3(256), 0, cur_stream(), (const uint8_t*)in, (uint8_t*)out, nd, d, total);
   ck_launch("strided_copy");
 }
 
 void softmax(const float* x, float* y, int64_t outer, int64_t n, int64_t inner) {
   const int64_t rows = outer * inner;
   if (rows > 2147483647) throw Error("softmax: too many rows");
-  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)rows), dim3(256), 0, g_stream, x, y, n, inner);
+  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)rows), dim3(256), 0, cur_stream(), x, y, n, inner);
   ck_launch("softmax");
 }
 
 void layer_norm(const float* x, float* y, const float* scale, const float* bias, int64_t rows, int64_t cols,
                 float eps) {
-  hipLaunchKernelGGL(layer_norm_kernel, dim3((unsigned)rows), dim3(256), 0, g_stream, x, y, scale, bias, cols, eps);
+  hipLaunchKernelGGL(layer_norm_kernel, dim3((unsigned)rows), dim3(256), 0, cur_stream(), x, y, scale, bias, cols, eps);
   ck_launch("layer_norm");
 }
 
 void embedding(const int64_t* ids, const float* w, float* out, int64_t n, int64_t H, int64_t V, int64_t pad) {
-  hipLaunchKernelGGL(embedding_kernel, dim3(blocks_for(n * H)), dim3(256), 0, g_stream, ids, w, out, n, H, V, pad);
+  hipLaunchKernelGGL(embedding_kernel, dim3(blocks_for(n * H)), dim3(256), 0, cur_stream(), ids, w, out, n, H, V, pad);
   ck_launch("embedding");
 }
 
@@ -469,7 +540,7 @@ void cast(const void* x, int xdt, void* y, int ydt, int64_t n) {
   const dim3 g(blocks_for(n));
 #define PHA_CAST(XT, XC, YT, YC)                                                                              \
   if (xdt == XC && ydt == YC) {                                                                               \
-    hipLaunchKernelGGL((cast_kernel<XT, YT>), g, dim3(256), 0, g_stream, (const XT*)x, (YT*)y, n);            \
+    hipLaunchKernelGGL((cast_kernel<XT, YT>), g, dim3(256), 0, cur_stream(), (const XT*)x, (YT*)y, n);            \
     ck_launch("cast");                                                                                        \
     return;                                                                                                   \
   }
@@ -486,7 +557,7 @@ void cast(const void* x, int xdt, void* y, int ydt, int64_t n) {
 }
 
 void fill(float* y, int64_t n, float v) {
-  hipLaunchKernelGGL(fill_kernel, dim3(blocks_for(n)), dim3(256), 0, g_stream, y, n, v);
+  hipLaunchKernelGGL(fill_kernel, dim3(blocks_for(n)), dim3(256), 0, cur_stream(), y, n, v);
   ck_launch("fill");
 }
 

@@ -41,6 +41,12 @@ int pha_infer_output_shape(const PhaPredictor* p, int i, int64_t* shape, int* nd
 int pha_infer_copy_output(const PhaPredictor* p, int i, void* dst, size_t bytes);
 // op types of the loaded program the engine cannot run ("" when none)
 const char* pha_infer_unsupported_ops(const PhaPredictor* p);
+// ir_optim = 0: run the program as written (no conv + elementwise_add / conv + batch_norm folding)
+PhaPredictor* pha_infer_create2(const char* model_file, const char* params_file, int device, int ir_optim);
+// the IR passes that rewrote the program at load ("conv_bn_fuse_pass x53;..."; "" when none)
+const char* pha_infer_applied_passes(const PhaPredictor* p);
+// device bytes held by the predictor's block pool (0 on the host)
+size_t pha_infer_pooled_bytes(const PhaPredictor* p);
 void pha_infer_destroy(PhaPredictor* p);
 
 // ---- reference C API subset -------------------------------------------------------------------
@@ -58,6 +64,8 @@ typedef struct PD_OneDimArrayInt32 {
 } PD_OneDimArrayInt32;
 
 PD_Config* PD_ConfigCreate(void);
+void PD_ConfigSwitchIrOptim(PD_Config* c, PD_Bool x);
+PD_Bool PD_ConfigIrOptim(PD_Config* c);
 void PD_ConfigDestroy(PD_Config* c);
 void PD_ConfigSetModel(PD_Config* c, const char* prog_file_path, const char* params_file_path);
 const char* PD_ConfigGetProgFile(PD_Config* c);

@@ -55,6 +55,7 @@ enum : int {
   EPI_RING = 1 << 22,    // NT: the 4-slot ring of 32-deep stages (gemm4r_kernel), K % 64 == 0, K >= 128
   EPI_ADEEP = 1 << 23,   // NT without bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel), K >= 256
   EPI_WSTAG = 1 << 24,   // NT + EARLY: wave w issues its LDS-DMA after MFMA w of the group (LV + 16)
+  EPI_KSTAG_SHIFT = 25,  // bits 25-26: K-start stagger (1: per XCD, 2: per tile, 3: per slot in the XCD)
 };
 
 // late-wait variants (LV): {LWG = phase-B group of the buffer wait (0: at the A/B boundary),
@@ -238,9 +239,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const size_t astep = AKO ? (size_t)64 * p.lda * 2 : 128, bstep = BKO ? (size_t)64 * p.ldb * 2 : 128;
   const unsigned lds0 = lds_u32(smem);
 
+  // K-start stagger: the cursor walks a tile's K-tiles from kofs, wrapping (every work item still
+  // sums all of its K-tiles; only the order rotates). With power-of-two row pitches every workgroup
+  // reading the same K columns at once lands on a fraction of the memory channels
+  const int ksm = (p.epi >> EPI_KSTAG_SHIFT) & 3;
+  int kofs = 0;
   auto set_tile = [&](int r) {   // DMA offsets + bases of round r's tile
     int tm, tn, slice, bi;
     sc.tile(r, tm, tn, slice, bi);
+    if (ksm == 1) kofs = ((blockIdx.x & 7) * nk) >> 3;
+    else if (ksm == 2) kofs = __builtin_amdgcn_readfirstlane(((tm * 5 + tn * 3) & 15) * nk >> 4);
+    else if (ksm == 3) kofs = (((blockIdx.x >> 3) & 7) * nk) >> 3;
     const size_t k0 = (size_t)slice * nk * 64;   // first K of the item
     const int m0 = tm << 8, n0 = tn << 8;
 #pragma unroll
@@ -285,7 +294,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const bool l2only = (p.epi & EPI_L2ONLY) != 0;
   auto stage_begin = [&](int buf) {
     st_on = sc.valid(rs);
-    const int kk = l2only ? 0 : (st_on ? ks : nk - 1);
+    int kk = l2only ? 0 : (st_on ? ks : nk - 1) + kofs;
+    if (kk >= nk) kk -= nk;
     st_a = abase + (size_t)kk * astep;
     st_b = bbase + (size_t)kk * bstep;
     st_buf = buf;

@@ -31,6 +31,12 @@ def _lib():
         P, I, C = ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p
         L.pha_infer_create.argtypes = [C, C, I]
         L.pha_infer_create.restype = P
+        L.pha_infer_create2.argtypes = [C, C, I, I]
+        L.pha_infer_create2.restype = P
+        L.pha_infer_applied_passes.argtypes = [P]
+        L.pha_infer_applied_passes.restype = C
+        L.pha_infer_pooled_bytes.argtypes = [P]
+        L.pha_infer_pooled_bytes.restype = ctypes.c_size_t
         L.pha_infer_last_error.restype = C
         for f in ("pha_infer_num_inputs", "pha_infer_num_outputs"):
             getattr(L, f).argtypes = [P]
@@ -55,18 +61,26 @@ def _lib():
 
 
 class NativePredictor:
-    """``NativePredictor(model_file, params_file, device=-1)``: device -1 runs on the host, k >= 0 on
-    GPU k. ``run({name: ndarray})`` -> list of output ndarrays (fetch order)."""
+    """``NativePredictor(model_file, params_file, device=-1, ir_optim=True)``: device -1 runs on the
+    host, k >= 0 on GPU k (its own HIP stream and pooled device memory). ``run({name: ndarray})`` ->
+    list of output ndarrays (fetch order). ``ir_optim`` folds conv + elementwise_add(bias) and conv +
+    batch_norm at load (``applied_passes`` lists what fired). One predictor per thread (the
+    reference PredictorPool model); the ctypes calls release the GIL."""
 
-    def __init__(self, model_file, params_file, device=-1):
+    def __init__(self, model_file, params_file, device=-1, ir_optim=True):
         L = _lib()
-        self._h = L.pha_infer_create(model_file.encode(), (params_file or "").encode(), int(device))
+        self._h = L.pha_infer_create2(model_file.encode(), (params_file or "").encode(), int(device), int(bool(ir_optim)))
         if not self._h:
             raise RuntimeError(f"native predictor: {L.pha_infer_last_error().decode()}")
         self.input_names = [L.pha_infer_input_name(self._h, i).decode() for i in range(L.pha_infer_num_inputs(self._h))]
         self.output_names = [L.pha_infer_output_name(self._h, i).decode()
                              for i in range(L.pha_infer_num_outputs(self._h))]
         self.unsupported = [s for s in L.pha_infer_unsupported_ops(self._h).decode().split(",") if s]
+        self.applied_passes = [s for s in L.pha_infer_applied_passes(self._h).decode().split(";") if s]
+
+    def pooled_bytes(self):
+        """device bytes in this predictor's block pool"""
+        return int(_lib().pha_infer_pooled_bytes(self._h))
 
     def run(self, feeds):
         L = _lib()

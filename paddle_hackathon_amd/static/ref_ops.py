@@ -660,6 +660,18 @@ def _conv_resnet_unit(r, ins, at):
     return resnet_unit, kw, "Y"
 
 
+def _conv_rnn(r, ins, at):
+    """rnn_op.cc: Input, PreState, WeightList, SequenceLength -> Out, State (Reserve / DropoutState
+    are the cuDNN workspace and dropout state: not produced here)"""
+    from ..nn.functional.rnn_op import rnn_op
+    kw = {"input": _one(r, ins, "Input"), "pre_state": _many(r, ins, "PreState"),
+          "weight_list": _many(r, ins, "WeightList"), "sequence_length": _one(r, ins, "SequenceLength"),
+          "dropout_prob": at.get("dropout_prob", 0.0), "is_bidirec": at.get("is_bidirec", False),
+          "input_size": at.get("input_size", 10), "hidden_size": at.get("hidden_size", 100),
+          "num_layers": at.get("num_layers", 1), "mode": at.get("mode", "LSTM"), "is_test": at.get("is_test", False)}
+    return rnn_op, kw, ("Out", "State*")
+
+
 def _conv_stack(r, ins, at):
     return stack_op, {"xs": _many(r, ins, "X"), "axis": at.get("axis", 0)}, "Y"
 
@@ -874,6 +886,7 @@ CONVERT = {
     # shape / indexing
     "stack": _conv_stack,
     "resnet_unit": _conv_resnet_unit,
+    "rnn": _conv_rnn,
     "unstack": _conv_unstack,
     "split": _conv_split,
     "gather": _conv_gather,

@@ -119,21 +119,29 @@ def test_native_errors_are_reported(tmp_path):
         pred.run({})
 
 
-def _client():
-    """the C++ client (tests/native_infer/infer_main.cpp) linked against libpha_infer.so"""
-    exe = os.path.join(HERE, "native_infer", "_build", "infer_main")
+_CLIENTS = {}
+
+
+def _client(tmp_path):
+    """the C++ client (tests/native_infer/infer_main.cpp) linked against libpha_infer.so, built from
+    source into the test's tmp dir (once per source text and library path in a session)"""
+    import hashlib
     src = os.path.join(HERE, "native_infer", "infer_main.cpp")
-    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
-        os.makedirs(os.path.dirname(exe), exist_ok=True)
+    libdir = os.path.dirname(lib_path())
+    with open(src, "rb") as f:
+        key = (hashlib.sha256(f.read()).hexdigest(), libdir)
+    exe = _CLIENTS.get(key)
+    if exe is None or not os.path.exists(exe):
+        exe = str(tmp_path / "infer_main")
         inc = os.path.join(os.path.dirname(HERE), "paddle_hackathon_amd", "csrc", "infer")
-        libdir = os.path.dirname(lib_path())
         subprocess.run(["g++", "-O2", "-std=c++17", "-I", inc, src, "-o", exe, "-L", libdir, "-lpha_infer",
                         f"-Wl,-rpath,{libdir}"], check=True)
+        _CLIENTS[key] = exe
     return exe
 
 
 def _run_client(tmp_path, m, p, feeds, device):
-    args = [_client(), m, p, str(device), str(tmp_path / "out")]
+    args = [_client(tmp_path), m, p, str(device), str(tmp_path / "out")]
     for n, v in feeds.items():
         f = tmp_path / f"in_{n}.bin"
         v.tofile(f)
@@ -178,3 +186,122 @@ def test_native_gpu_matches_host(tmp_path):
     ref = _python_predictor(m, p, feeds)
     for g, r in zip(got, ref):
         np.testing.assert_allclose(g, r, rtol=2e-4, atol=2e-5)
+
+
+def test_ir_passes_fold_conv_bn_and_match_unfused(tmp_path):
+    """conv_bn_fuse_pass / conv_elementwise_add_fuse_pass at load (reference paddle_pass_builder.cc:108):
+    ResNet-18's 20 conv + batch_norm pairs fold into filters + biases; results match the unfused
+    program and the Python predictor"""
+    name, m, p, feeds = _cases(tmp_path)[0]
+    fused = NativePredictor(m, p, device=-1)
+    plain = NativePredictor(m, p, device=-1, ir_optim=False)
+    assert any(s.startswith("conv_bn_fuse_pass x20") for s in fused.applied_passes), fused.applied_passes
+    assert plain.applied_passes == []
+    a, b = fused.run(feeds), plain.run(feeds)
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5)
+    for x, y in zip(a, _python_predictor(m, p, feeds)):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5)
+
+
+def _corrupt_params(tmp_path, p, edit):
+    data = bytearray(open(p, "rb").read())
+    edit(data)
+    bad = str(tmp_path / "bad.pdiparams")
+    with open(bad, "wb") as f:
+        f.write(bytes(data))
+    return bad
+
+
+def test_malformed_params_stream_is_a_clean_error(tmp_path):
+    import struct
+    name, m, p, feeds = _cases(tmp_path)[2]
+
+    def huge_lod(d):   # LoD level count of the first tensor
+        d[4:12] = struct.pack("<Q", 1 << 40)
+
+    def neg_desc(d):   # tensor desc size of the first tensor (no LoD levels in it)
+        d[16:20] = struct.pack("<i", -5)
+    for edit in (huge_lod, neg_desc, lambda d: d.__delitem__(slice(len(d) - 7, len(d)))):
+        bad = _corrupt_params(tmp_path, p, edit)
+        with pytest.raises(RuntimeError, match="params stream|trailing|truncated"):
+            NativePredictor(m, bad, device=-1)
+
+
+def _pool_threads(m, p, feeds, device, n=4, reps=3):
+    import threading
+    preds = [NativePredictor(m, p, device=device) for _ in range(n)]
+    res, errs = [None] * n, []
+
+    def work(i):
+        try:
+            for _ in range(reps):
+                res[i] = preds[i].run(feeds)
+        except Exception as e:   # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=work, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    return res, preds
+
+
+def test_predictor_pool_threads_host(tmp_path):
+    name, m, p, feeds = _cases(tmp_path)[0]
+    res, _ = _pool_threads(m, p, feeds, -1)
+    for r in res[1:]:
+        for a, b in zip(r, res[0]):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_predictor_pool_threads_gpu_own_streams_and_pool(tmp_path):
+    """four predictors (each its own stream and block pool) driven from four threads at once; a
+    second run of a predictor allocates nothing new (pooled memory)"""
+    import torch
+    name, m, p, feeds = _cases(tmp_path)[0]
+    res, preds = _pool_threads(m, p, feeds, 0)
+    host = NativePredictor(m, p, device=-1).run(feeds)
+    for r in res:
+        for a, h in zip(r, host):
+            np.testing.assert_allclose(a, h, rtol=2e-4, atol=2e-5)
+    before = preds[0].pooled_bytes()
+    assert before > 0
+    preds[0].run(feeds)
+    assert preds[0].pooled_bytes() == before
+    torch.cuda.set_device(0)   # torch's current device changes nothing for the predictor
+    preds[1].run(feeds)
+
+
+@pytest.mark.gpu
+def test_native_resnet50_latency_log(tmp_path):
+    """not a gate: ResNet-50 batch-8 latency of the native GPU predictor (conv + BN folded) next to
+    the Python predictor on the same files, for the log"""
+    import time
+    from paddle_hackathon_amd.vision.models import resnet50
+    paddle.seed(0)
+    m, p = _save(tmp_path, resnet50(), [InputSpec([None, 3, 224, 224], "float32", "x")], "r50")
+    feeds = {"x": np.random.RandomState(0).randn(8, 3, 224, 224).astype("float32")}
+    nat = NativePredictor(m, p, device=0)
+    nat.run(feeds)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        out = nat.run(feeds)
+    t_nat = (time.perf_counter() - t0) / 5
+    cfg = inference.Config(m, p)
+    cfg.enable_use_gpu(100, 0)
+    pred = inference.create_predictor(cfg)
+    h = pred.get_input_handle("x")
+    h.copy_from_cpu(feeds["x"])
+    pred.run()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        h.copy_from_cpu(feeds["x"])
+        pred.run()
+        ref = [pred.get_output_handle(n).copy_to_cpu() for n in pred.get_output_names()]
+    t_py = (time.perf_counter() - t0) / 5
+    np.testing.assert_allclose(out[0], ref[0], rtol=5e-2, atol=5e-2)
+    print(f"\n[native-infer] ResNet-50 b8 fp32: native {t_nat * 1e3:.1f} ms ({nat.applied_passes}), "
+          f"python predictor {t_py * 1e3:.1f} ms")

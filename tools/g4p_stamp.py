@@ -27,9 +27,13 @@ def main():
         grid = G._num_cus(x.device)
         ws = torch.zeros(grid * 4 * 4, dtype=torch.int64, device="cuda")
         epi_base = G.EPI_EARLY | G.EPI_BIAS
+        bb = b.bfloat16()
 
         def run(lv, w=None):
-            epi = epi_base | ((lv & 15) << 17) | (G.EPI_WSTAG if lv & 16 else 0)
+            if lv < 0:   # hipBLASLt on the same operands
+                torch.addmm(bb, x, wt.t(), out=c)
+                return
+            epi = epi_base | ((lv % 100 & 15) << 17) | (G.EPI_WSTAG if lv % 100 & 16 else 0) | ((lv // 100) << 25)
             rc = L.pha_gemm4p(G._DT[x.dtype], G._ptr(x), G._ptr(wt), G._ptr(c), T, N, K, K, K, N, 0, 0, 0,
                               epi, G._ptr(b), grid, G._group_m(False, False, K, N), G._ptr(w),
                               1, G._stream(x), None)
@@ -41,8 +45,8 @@ def main():
                 run(8)
             torch.cuda.synchronize()
         res = {}
-        plain = [int(v) for v in os.environ.get("LVS", "8,24").split(",")]
-        stamped = [int(v) for v in os.environ.get("STAMPED", "15,31").split(",")]
+        plain = [int(v) for v in os.environ.get("LVS", "8,108,208,308,-1").split(",")]
+        stamped = [int(v) for v in os.environ.get("STAMPED", "15,115").split(",") if v]
         for _ in range(3):
             for lv in plain + stamped:
                 torch.cuda.synchronize()
