@@ -323,7 +323,12 @@ def _gpt_micro_batch(a, torch, world, rank):
         return a.micro_batch
     if a.model != "gpt3-1.3b":
         return 2
+    if max(1, a.tp) > 1 or max(1, a.pp) > 1 or a.sharding_stage or a.recompute:
+        return 16   # the free-memory thresholds below were measured for the plain DP layout only
     free_gb = torch.cuda.mem_get_info()[0] / 2 ** 30
+    # ranks that share one device (a gloo rehearsal on one GPU) each get their share of it
+    per_dev = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // max(1, torch.cuda.device_count()))
+    free_gb /= per_dev
     if world > 1:
         import torch.distributed as td
         t = torch.tensor([free_gb], dtype=torch.float64,

@@ -5,7 +5,8 @@ hybrid_parallel_inference.py:23): splits a static inference Program — typicall
 
 ``gen_infer_program`` rewrites the main program in place for this rank:
 
-* every op keeps its ``op_device`` ("gpu:k" = stage k, "gpu:all" or none = every stage);
+* every op keeps its ``op_device`` ("gpu:k" = stage k, "gpu:all" = every stage: readers and the
+  while op are marked so; any other op without one is an error, as in the reference);
 * a variable produced on stage p and read on stage q gets a ``send_v2`` right after its producer
   on p and a ``recv_v2`` at the same program position on q (both walk the program in one order,
   so the point-to-point messages pair up in order — what RCCL needs, it has no tags);
@@ -56,6 +57,7 @@ class _P2P:
     def send_tensor(self, t, dst):
         t = t.detach().contiguous()
         t = t.cpu() if self.cpu else t.to(self.device)
+        assert t.dim() <= _HDR - 2, f"send_tensor: {t.dim()} dims (the header holds at most {_HDR - 2})"
         hdr = torch.zeros(_HDR, dtype=torch.int64)
         hdr[0] = t.dim()
         hdr[1:1 + t.dim()] = torch.tensor(list(t.shape), dtype=torch.int64)
@@ -214,12 +216,34 @@ class HybridParallelInferenceHelper:
                 keep.append(op)
         blk.ops = keep
 
+    _DEVICE_ALL = ("create_py_reader", "read", "create_double_buffer_reader", "while")
+
+    def _add_op_device_attr(self, blk):
+        """reader and while ops run on every stage ("gpu:all"), as the reference marks them
+        (hybrid_parallel_inference.py:446)"""
+        for op in blk.ops:
+            if op.type.rsplit(".", 1)[-1] in self._DEVICE_ALL:
+                op.attrs["op_device"] = "gpu:all"
+            if op.type == "while":
+                self._add_op_device_attr(self._main_program.blocks[op.attrs["sub_block"]])
+
+    def _check_validation(self, blk):
+        """every other op must carry its stage (reference _check_validation, :475): an op without
+        op_device would be kept on every stage and fail later reading a value another stage made"""
+        for op in blk.ops:
+            if op.type == "while":
+                self._check_validation(self._main_program.blocks[op.attrs["sub_block"]])
+            dev = op.attrs.get("op_device")
+            assert dev, f"{op.type} has no op_device set (use static.device_guard('gpu:k') for every op)"
+
     def gen_infer_program(self, sync_in_while_lastpp2firstpp_var_names=None, sync_in_while_var_names=None,
                           debug=False):
         """rewrite the main (and startup) program for this rank's pipeline stage"""
-        xfer = _P2P(self._device)
         main = self._main_program
         gblk = main.global_block()
+        self._add_op_device_attr(gblk)
+        self._check_validation(gblk)
+        xfer = _P2P(self._device)
         self._insert_boundaries(gblk, xfer)
         whiles = [op for op in gblk.ops if op.type == "while"]
         assert len(whiles) < 2, "More than one while op found."
