@@ -602,15 +602,42 @@ void op_conv2d(Ctx& c, const OpDesc& op) {
         }
       });
     }
+  } else if (c.gpu()) {
+    // the whole batch per launch: out[n][co][p] = sum_k W[co][k] col[n][k][p] as one batched GEMM
+    // per group (A shared across images); a 1x1 / stride-1 / unpadded conv multiplies x in place
+    const int Kg = Cg * KH * KW, P = OH * OW, Cog = Co / groups;
+    const bool direct = KH == 1 && KW == 1 && sh == 1 && sw == 1 && p.t == 0 && p.l == 0 && p.b == 0 && p.r == 0 &&
+                        OH == H && OW == W;
+    Tensor col;
+    const float* src = x.data<float>();
+    int64_t sbb = (int64_t)C * H * W;
+    if (!direct) {
+      col = c.alloc({(int64_t)N * C * KH * KW, P});
+      gpu::im2col(x.data<float>(), col.data<float>(), C, H, W, KH, KW, OH, OW, sh, sw, p.t, p.l, dh, dw, N);
+      src = col.data<float>();
+      sbb = (int64_t)C * KH * KW * P;
+    }
+    for (int g = 0; g < groups; ++g) {
+      GemmArgs ga;
+      ga.A = w.data<float>() + (int64_t)g * Cog * Kg;
+      ga.B = src + (int64_t)g * Kg * P;
+      ga.C = y.data<float>() + (int64_t)g * Cog * P;
+      ga.batch = N;
+      ga.M = Cog; ga.N = P; ga.K = Kg;
+      ga.sAb = 0; ga.sAm = Kg; ga.sAk = 1;
+      ga.sBb = sbb; ga.sBk = P; ga.sBn = 1;
+      ga.sCb = (int64_t)Co * P; ga.sCm = P;
+      gemm(c, ga);
+    }
+    if (bias) gpu::row_bias_act(y.data<float>(), bias, Co, P, N, false);
+    bias = nullptr;
   } else {
     // im2col per image + GEMM per group: out[co, p] = sum_k W[co, k] col[k, p]
     const int Kg = Cg * KH * KW, P = OH * OW, Cog = Co / groups;
     Tensor col = c.alloc({(int64_t)C * KH * KW, P});
     for (int n = 0; n < N; ++n) {
       const float* xn = x.data<float>() + (int64_t)n * C * H * W;
-      if (c.gpu()) {
-        gpu::im2col(xn, col.data<float>(), C, H, W, KH, KW, OH, OW, sh, sw, p.t, p.l, dh, dw);
-      } else {
+      {
         float* cp = col.data<float>();
         parallel_for((int64_t)C * KH * KW, [&](int64_t a, int64_t b) {
           for (int64_t r = a; r < b; ++r) {

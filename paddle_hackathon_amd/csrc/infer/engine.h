@@ -130,9 +130,11 @@ void d2d(void* dst, const void* src, size_t n);
 void gemm(const float* A, const float* B, float* C, const float* bias, int batch, int M, int N, int K,
           int64_t sAb, int64_t sAm, int64_t sAk, int64_t sBb, int64_t sBk, int64_t sBn, int64_t sCb, int64_t sCm,
           float alpha, bool relu);
-// col [C*KH*KW][OH*OW] of one NCHW image
+// col [N][C*KH*KW][OH*OW] of N NCHW images
 void im2col(const float* x, float* col, int C, int H, int W, int KH, int KW, int OH, int OW, int sh, int sw, int pt,
-            int pl, int dh, int dw);
+            int pl, int dh, int dw, int N);
+// y[b][r][i] += bias[r] (then ReLU) over batch x rows x inner
+void row_bias_act(float* y, const float* bias, int64_t rows, int64_t inner, int64_t batch, bool relu);
 void depthwise_conv(const float* x, const float* w, float* y, int N, int C, int H, int W, int KH, int KW, int OH,
                     int OW, int sh, int sw, int pt, int pl, int dh, int dw, int mult);
 enum Unary { RELU, RELU6, SIGMOID, TANH, GELU, GELU_TANH, SILU, HARD_SWISH, HARD_SIGMOID, LEAKY_RELU, EXP, SQRT,

@@ -110,9 +110,164 @@ __global__ __launch_bounds__(256) void gemm_kernel(const float* __restrict__ A, 
       }
 }
 
+// 128 x 128 x 16 fp32 MFMA GEMM: 4 waves (2 x 2) of 64 x 64, 16 accumulators per wave; the next
+// K-tile is loaded into registers (16-B loads along the contiguous dimension when the layout
+// allows) while the current one multiplies, then written to the other LDS buffer: one barrier per
+// K-tile. LDS rows are padded to 144 floats so the four 16-lane rows of a fragment read hit four
+// disjoint bank groups.
+constexpr int TB = 128, TK = 16, TPAD = 16;
+
+template <bool AV, bool BV>
+__global__ __launch_bounds__(256) void gemm128_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                      float* __restrict__ C, const float* __restrict__ bias, int M,
+                                                      int N, int K, int64_t sAb, int64_t sAm, int64_t sAk,
+                                                      int64_t sBb, int64_t sBk, int64_t sBn, int64_t sCb,
+                                                      int64_t sCm, float alpha, int relu) {
+  __shared__ float As[2][TK][TB + TPAD];
+  __shared__ float Bs[2][TK][TB + TPAD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+  const int64_t bz = blockIdx.z;
+  A += bz * sAb;
+  B += bz * sBb;
+  C += bz * sCb;
+  // per-thread staging registers: 8 A values and 8 B values per K-tile
+  float ra[8], rb[8];
+  auto load = [&](int k0) {
+    if constexpr (AV) {   // A[m][k] with k contiguous: thread -> (row m, 4-wide k chunk), 2 passes
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r, m = e >> 2, kq = (e & 3) * 4;
+        const int gm = m0 + m, gk = k0 + kq;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gm < M && gk < K) v = *reinterpret_cast<const f4*>(A + gm * sAm + gk);
+        ra[4 * r] = v[0]; ra[4 * r + 1] = v[1]; ra[4 * r + 2] = v[2]; ra[4 * r + 3] = v[3];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = tid + 256 * r;
+        int m, k;
+        if (sAk == 1) { m = e >> 4; k = e & 15; } else { m = e & 127; k = e >> 7; }
+        const int gm = m0 + m, gk = k0 + k;
+        ra[r] = (gm < M && gk < K) ? A[gm * sAm + gk * sAk] : 0.f;
+      }
+    }
+    if constexpr (BV) {   // B[k][n] with n contiguous: thread -> (k row, 4-wide n chunk), 2 passes
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r, k = e >> 5, nq = (e & 31) * 4;
+        const int gk = k0 + k, gn = n0 + nq;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (gk < K && gn < N) v = *reinterpret_cast<const f4*>(B + gk * sBk + gn);
+        rb[4 * r] = v[0]; rb[4 * r + 1] = v[1]; rb[4 * r + 2] = v[2]; rb[4 * r + 3] = v[3];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = tid + 256 * r;
+        int n, k;
+        if (sBn == 1) { n = e & 127; k = e >> 7; } else { n = e >> 4; k = e & 15; }
+        const int gn = n0 + n, gk = k0 + k;
+        rb[r] = (gn < N && gk < K) ? B[gk * sBk + gn * sBn] : 0.f;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    if constexpr (AV) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r, m = e >> 2, kq = (e & 3) * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) As[buf][kq + q][m] = ra[4 * r + q];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = tid + 256 * r;
+        int m, k;
+        if (sAk == 1) { m = e >> 4; k = e & 15; } else { m = e & 127; k = e >> 7; }
+        As[buf][k][m] = ra[r];
+      }
+    }
+    if constexpr (BV) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r, k = e >> 5, nq = (e & 31) * 4;
+        *reinterpret_cast<f4*>(&Bs[buf][k][nq]) = f4{rb[4 * r], rb[4 * r + 1], rb[4 * r + 2], rb[4 * r + 3]};
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int e = tid + 256 * r;
+        int n, k;
+        if (sBn == 1) { n = e & 127; k = e >> 7; } else { n = e >> 4; k = e & 15; }
+        Bs[buf][k][n] = rb[r];
+      }
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < K; k0 += TK) {
+    const bool more = k0 + TK < K;
+    if (more) load(k0 + TK);
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 4) {
+      const int kr = kk + (lane >> 4), c = lane & 15;
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[cur][kr][wm * 64 + i * 16 + c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[cur][kr][wn * 64 + j * 16 + c];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // D[i][j]: column = lane % 16, rows 4 * (lane / 16) + r
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (m < M && n < N) {
+          float v = alpha * acc[i][j][r];
+          if (bias) v += bias[n];
+          if (relu) v = v > 0.f ? v : 0.f;
+          C[m * sCm + n] = v;
+        }
+      }
+}
+
+// bias along the GEMM's rows (conv: one value per output channel = row)
+__global__ void row_bias_act_kernel(float* __restrict__ y, const float* __restrict__ bias, int64_t rows,
+                                    int64_t inner, int64_t batch, int relu) {
+  const int64_t total = batch * rows * inner;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = y[i] + (bias ? bias[(i / inner) % rows] : 0.f);
+    y[i] = relu && v < 0.f ? 0.f : v;
+  }
+}
+
 __global__ void im2col_kernel(const float* __restrict__ x, float* __restrict__ col, int C, int H, int W, int KH,
-                              int KW, int OH, int OW, int sh, int sw, int pt, int pl, int dh, int dw) {
-  const int64_t total = (int64_t)C * KH * KW * OH * OW;
+                              int KW, int OH, int OW, int sh, int sw, int pt, int pl, int dh, int dw, int N) {
+  // col[n][c * KH * KW + kh * KW + kw][oh * OW + ow] for every image n of the batch
+  const int64_t per = (int64_t)C * KH * KW * OH * OW, total = per * N;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int ow = i % OW;
     int64_t t = i / OW;
@@ -121,9 +276,11 @@ __global__ void im2col_kernel(const float* __restrict__ x, float* __restrict__ c
     const int kw = t % KW;
     t /= KW;
     const int kh = t % KH;
-    const int c = (int)(t / KH);
+    t /= KH;
+    const int c = (int)(t % C);
+    const int64_t n = t / C;
     const int ih = oh * sh - pt + kh * dh, iw = ow * sw - pl + kw * dw;
-    col[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? x[((int64_t)c * H + ih) * W + iw] : 0.f;
+    col[i] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? x[((n * C + c) * H + ih) * W + iw] : 0.f;
   }
 }
 
@@ -451,6 +608,21 @@ void gemm(const float* A, const float* B, float* C, const float* bias, int batch
           bool relu) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (batch > 65535) throw Error("gemm: batch > 65535");
+  if ((int64_t)M * N >= 64 * 64 * 8) {   // the 128-tile kernel, 16-B loads where the layout allows
+    const bool av = sAk == 1 && K % 4 == 0 && sAm % 4 == 0 && sAb % 4 == 0 && ((size_t)A & 15) == 0;
+    const bool bv = sBn == 1 && N % 4 == 0 && sBk % 4 == 0 && sBb % 4 == 0 && ((size_t)B & 15) == 0;
+    dim3 grid((N + TB - 1) / TB, (M + TB - 1) / TB, batch);
+#define PHA_G128(X, Y)                                                                                        \
+  hipLaunchKernelGGL((gemm128_kernel<X, Y>), grid, dim3(256), 0, cur_stream(), A, B, C, bias, M, N, K, sAb, sAm, sAk, \
+                     sBb, sBk, sBn, sCb, sCm, alpha, relu ? 1 : 0)
+    if (av && bv) PHA_G128(true, true);
+    else if (av) PHA_G128(true, false);
+    else if (bv) PHA_G128(false, true);
+    else PHA_G128(false, false);
+#undef PHA_G128
+    ck_launch("gemm128");
+    return;
+  }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, batch);
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, cur_stream(), A, B, C, bias, M, N, K, sAb, sAm, sAk, sBb, sBk, sBn,
                      sCb, sCm, alpha, relu ? 1 : 0);
@@ -458,10 +630,15 @@ void gemm(const float* A, const float* B, float* C, const float* bias, int batch
 }
 
 void im2col(const float* x, float* col, int C, int H, int W, int KH, int KW, int OH, int OW, int sh, int sw, int pt,
-            int pl, int dh, int dw) {
-  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for((int64_t)C * KH * KW * OH * OW)), dim3(256), 0, cur_stream(), x, col, C,
-                     H, W, KH, KW, OH, OW, sh, sw, pt, pl, dh, dw);
+            int pl, int dh, int dw, int N) {
+  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for((int64_t)N * C * KH * KW * OH * OW)), dim3(256), 0, cur_stream(), x,
+                     col, C, H, W, KH, KW, OH, OW, sh, sw, pt, pl, dh, dw, N);
   ck_launch("im2col");
+}
+void row_bias_act(float* y, const float* bias, int64_t rows, int64_t inner, int64_t batch, bool relu) {
+  hipLaunchKernelGGL(row_bias_act_kernel, dim3(blocks_for(batch * rows * inner)), dim3(256), 0, cur_stream(), y, bias,
+                     rows, inner, batch, relu ? 1 : 0);
+  ck_launch("row_bias_act");
 }
 
 void depthwise_conv(const float* x, const float* w, float* y, int N, int C, int H, int W, int KH, int KW, int OH,
