@@ -56,6 +56,8 @@ enum : int {
   EPI_ADEEP = 1 << 23,   // NT without bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel), K >= 256
   EPI_WSTAG = 1 << 24,   // NT + EARLY: wave w issues its LDS-DMA after MFMA w of the group (LV + 16)
   EPI_KSTAG_SHIFT = 25,  // bits 25-26: K-start stagger (1: per XCD, 2: per tile, 3: per slot in the XCD)
+  EPI_COLSUM = 1 << 27,  // TN + EARLY: column sums of B (a linear layer's bias gradient: the sum of dY over
+                         // the tokens) from the B fragments the MFMAs already hold, into aux (see CS)
 };
 
 // late-wait variants (LV): {LWG = phase-B group of the buffer wait (0: at the A/B boundary),
@@ -161,6 +163,20 @@ __device__ __forceinline__ void mma0(f32x4& d, const uint4& a, const uint4& b) {
     asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "+a"(d) : "v"(va), "v"(vb));
 }
 
+// c + x . sel for two 16-bit values (v_dot2, fp32 accumulate): sel = ONES2 sums x's pair, 0 adds 0
+template <typename T>
+constexpr unsigned ONES2 = std::is_same<T, bf16_t>::value ? 0x3f803f80u : 0x3c003c00u;
+template <typename T>
+__device__ __forceinline__ float dot2sel(unsigned x, unsigned sel, float c) {
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, x), __builtin_bit_cast(bf2, sel), c, false);
+  } else {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, x), __builtin_bit_cast(h2, sel), c, false);
+  }
+}
+
 // tile schedule of one workgroup. With G % 8 == 0 (G / 8 workgroups per XCD under round-robin
 // placement) every XCD owns a contiguous chunk of the linear tile order and its workgroups walk it
 // together: lin = chunk_start + r * (G / 8) + slot, so the 8 XCDs work on far-apart panels (their
@@ -192,7 +208,7 @@ struct Sched {
 // with fewer tiles than CUs); each item writes its fp32 partial tile to its slab of p.ws and
 // pha_gemm4p's reduce kernel sums the slabs in slice order (deterministic) into C (+ bias).
 template <typename T, bool AKO, bool BKO, bool OT, bool BIAS, bool SKIPEPI = false, bool SPLIT = false,
-          bool GELU = false, bool RS = false, bool EARLY = false, int LV = 0>
+          bool GELU = false, bool RS = false, bool EARLY = false, int LV = 0, bool CS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4p_kernel(Args p) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -468,6 +484,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   f32x4 acc[8][8];
   uint4 fa0[8], fb0[8], fa1[8], fb1[8];
+  // CS: per-lane column sums of the B fragments (fragment j: column wc*128 + 16j + fr, k-quarter fk)
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   constexpr int SCHED = AKO ? 0 : 2;   // read placement, as gemm4w's per-layout winners
   // EARLY: MFMA group at which phase A's fragment-read burst ends and the buffer is released
   constexpr int RELG = AKO ? PHA_G4P_RELG_TN : PHA_G4P_RELG_NT;
@@ -562,7 +580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // schedule can issue them; the A/B boundary waits with a counted vmcnt for the previous set only.
   // Each DMA gets >= 112 MFMAs of latency cover instead of >= 64.
   auto phaseE = [&](auto mode_c, auto rel_c, auto vbw_c, uint4 (&ca)[8], uint4 (&cb)[8], uint4 (&na)[8],
-                    uint4 (&nb)[8], int rbuf, int rkh, int stbuf) {
+                    uint4 (&nb)[8], int rbuf, int rkh, int stbuf, auto cs_c, unsigned onesel) {
     constexpr int MODE = decltype(mode_c)::value;
     constexpr bool REL = decltype(rel_c)::value;   // phase A: read burst, release barrier, DMAs 0-11
 #pragma unroll
@@ -677,6 +695,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           else mma0<T>(acc[i][j], cb[j], ca[i]);
         }
       }
+      // CS phases (branch-free: a taken branch per group cost 12 % of the TN kernel): group s < 8
+      // adds the 8 k-values of B fragment s (column wc*128 + 16s + fr) dotted with onesel — 1.0 x 2
+      // on the wave row that sums this k-half of this K-tile, 0 on the other
+      if constexpr (decltype(cs_c)::value) {
+        if (s < 8) {   // (s is a constant after unrolling: no branch)
+          csum[s & 7] = dot2sel<T>(cb[s & 7].x, onesel, csum[s & 7]);
+          csum[s & 7] = dot2sel<T>(cb[s & 7].y, onesel, csum[s & 7]);
+          csum[s & 7] = dot2sel<T>(cb[s & 7].z, onesel, csum[s & 7]);
+          csum[s & 7] = dot2sel<T>(cb[s & 7].w, onesel, csum[s & 7]);
+        }
+      } else {
+        (void)onesel;
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (PIN) asm volatile("" ::: "memory");
     }
@@ -727,9 +758,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     using VW2 = std::integral_constant<int, LWG ? VL2 : 0>;
     const unsigned long long sp_0 = STAMP ? __builtin_amdgcn_s_memtime() : 0;
     for (int r = 0; sc.valid(r); ++r) {
+      // CS: the item's K-tiles [klo, khi) are summed by this tile row (each of the tiles_m tile rows
+      // takes its own 1/tiles_m of the K range, so the extra VALU work is spread over the grid);
+      // wave row wr takes k-half wr of each of them
+      int klo = 0, khi = 0;
+      if constexpr (CS) {
+        int tm, tn, slice, bi;
+        sc.tile(r, tm, tn, slice, bi);
+        klo = __builtin_amdgcn_readfirstlane(tm * nk / sc.tiles_m);
+        khi = __builtin_amdgcn_readfirstlane((tm + 1) * nk / sc.tiles_m);
+      }
+      // CS: K-tile k's k-half h is summed by wave row h when klo <= k < khi (sel below)
+      using CSY = std::integral_constant<bool, CS>;
+      auto sel = [&](int k, int h) -> unsigned {
+        return (CS && k >= klo && k < khi && wr == h) ? ONES2<T> : 0u;
+      };
       {
         const int buf = s & 1;
-        phaseE(M2{}, yes{}, VW2{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        phaseE(M2{}, yes{}, VW2{}, fa0, fb0, fa1, fb1, buf, 1, buf, CSY{}, sel(0, 0));
         if constexpr (LWG == 0) {
           if constexpr (STAMP) sp_t = __builtin_amdgcn_s_memtime();
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(VB2) : "memory");
@@ -742,13 +788,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
         }
         set_epi(r);
-        phaseE(M0{}, no{}, VW2{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        phaseE(M0{}, no{}, VW2{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf, CSY{}, sel(0, 1));
         stage_end();
         ++s;
       }
-      for (int k = 1; k < nk; ++k, ++s) {
+      auto ktile = [&](auto cs_c, int k) {
         const int buf = s & 1;
-        phaseE(M0{}, yes{}, VW1{}, fa0, fb0, fa1, fb1, buf, 1, buf);
+        phaseE(M0{}, yes{}, VW1{}, fa0, fb0, fa1, fb1, buf, 1, buf, cs_c, sel(k, 0));
         if constexpr (LWG == 0) {
           if constexpr (STAMP) sp_t = __builtin_amdgcn_s_memtime();
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(16 - RELG) : "memory");
@@ -760,8 +806,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        phaseE(M0{}, no{}, VW1{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf);
+        phaseE(M0{}, no{}, VW1{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf, cs_c, sel(k, 1));
         stage_end();
+      };
+      // (one loop: cutting it at klo / khi into dot2-free and dot2 copies raised the VGPR count
+      // 207 -> 256 with 61 SGPR spills; the 4 dot2s per group ride in the MFMA issue gaps)
+      for (int k = 1; k < nk; ++k, ++s) ktile(CSY{}, k);
+      if constexpr (CS) {
+        // the item is done: sum the 4 k-quarters (lanes l, l+16, l+32, l+48) of every fragment. The
+        // swaps pair DIFFERENT fragments (a swap of a register with itself is a no-op): after
+        // permlane32_swap(f_j, f_j+4) + add, lanes 0-31 hold f_j's half sums and lanes 32-63 f_j+4's;
+        // after permlane16_swap(u_j, u_j+1) + add, 16-lane row 0..3 holds the totals of fragments
+        // (j, j+1, j+4, j+5). Lane row fk then stores two fragments to row
+        // (slice * tiles_m + tm) * 2 + wr of the fp32 partials [2 * splits * tiles_m][N]
+        int tm, tn, slice, bi;
+        sc.tile(r, tm, tn, slice, bi);
+        // (asm swaps: hipcc's permlane*_swap builtins fed into an add came out as vdst + vdst, the
+        // second result dropped — the ISA showed v_add_f32 vX, vA, vA after v_permlane32_swap vA, vB)
+        float u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x0 = csum[j], x1 = csum[j + 4];
+          asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x0), "+v"(x1));
+          u[j] = x0 + x1;
+        }
+        float w[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float x0 = u[2 * j], x1 = u[2 * j + 1];
+          asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x0), "+v"(x1));
+          w[j] = x0 + x1;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) csum[j] = 0.f;
+        const int f0 = (fk & 1) + (fk >> 1) * 4;   // w[0]: fragment f0, w[1]: fragment f0 + 2
+        float* row = static_cast<float*>(p.aux) + (size_t)((slice * sc.tiles_m + tm) * 2 + wr) * N;
+        const int c0 = (tn << 8) + wc * 128 + 16 * f0 + fr;
+        if (c0 < N) row[c0] = w[0];
+        if (c0 + 32 < N) row[c0 + 32] = w[1];
       }
     }
     if constexpr (STAMP) {   // diagnostic output (vector stores from lane 0 into the workspace)
@@ -1388,7 +1470,14 @@ template <typename T, bool BIAS, bool E>
 int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t st) {
   if (a.splits > 1) {   // TN only (weight gradients)
     if (!(ako && bko && !trans)) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+    bool cs = false;
+    if constexpr (E) {
+      if (a.epi & EPI_COLSUM) {
+        cs = true;
+        hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E, 0, true>), dim3(grid), dim3(256), 0, st, a);
+      }
+    }
+    if (!cs) hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, false, false, true, false, false, E>), dim3(grid), dim3(256), 0, st, a);
     const long elems = (long)a.M * a.N;
     hipLaunchKernelGGL((splitk_reduce_kernel<T, BIAS>), dim3((unsigned)((elems / 8 + 255) / 256)), dim3(256), 0, st,
                        a.ws, static_cast<T*>(a.c), a.bias, a.M, a.N, a.ldc, a.splits);
@@ -1435,8 +1524,15 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
     else if (lv == 6) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 6>), dim3(grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   }
-  else if (ako && bko && !trans)
+  else if (ako && bko && !trans) {
+    if constexpr (E) {
+      if (a.epi & EPI_COLSUM) {
+        hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 0, true>), dim3(grid), dim3(256), 0, st, a);
+        return (int)hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+  }
   else if (ako && !bko && trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, true, false, true, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   else
@@ -1477,6 +1573,11 @@ PHA_API int pha_gemm4p_batched(int dt, const void* a, const void* b, void* c, lo
   if (((size_t)a | (size_t)b | (size_t)c) & 15) return (int)hipErrorInvalidValue;
   if ((epi & g4p::EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if ((epi & g4p::EPI_GELU) && (!aux || ((size_t)aux & 15) || splits > 1)) return (int)hipErrorInvalidValue;
+  // COLSUM: TN, early schedule, no K-start stagger (the K sub-ranges of the tile rows must tile the
+  // item's K-tiles in cursor order), fp32 partials [2 * splits * ceil(M / 256)][N] in aux
+  if ((epi & g4p::EPI_COLSUM) && (!aux || ((size_t)aux & 3) || !a_kouter || !b_kouter || trans || batch != 1 ||
+                                  !(epi & g4p::EPI_EARLY) || ((epi >> g4p::EPI_KSTAG_SHIFT) & 3) || (epi & g4p::EPI_GELU)))
+    return (int)hipErrorInvalidValue;
   if (splits < 1) splits = 1;
   if (batch < 1 || (batch > 1 && (splits > 1 || (epi & g4p::EPI_GELU) || (sa | sb | sc) % 8 || sa < 0 || sb < 0 || sc < 0)))
     return (int)hipErrorInvalidValue;

@@ -43,8 +43,11 @@ class _LinearBias(torch.autograd.Function):
         x2d, w = ctx.saved_tensors
         gy = gy.contiguous()
         dx = _gemm.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
-        dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
-        db = _ops.hip.col_sum(gy) if ctx.needs_input_grad[2] else None
+        if ctx.needs_input_grad[1] and ctx.needs_input_grad[2]:
+            dw, db = _gemm.mm_tn_db(x2d.contiguous(), gy)   # bias gradient from the dW GEMM's B fragments
+        else:
+            dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
+            db = _ops.hip.col_sum(gy) if ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

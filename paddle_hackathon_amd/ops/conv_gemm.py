@@ -1275,8 +1275,12 @@ class LinearNT(torch.autograd.Function):
         gy = gy.contiguous()
         from . import gemm as _g4
         dx = _g4.mm_nt(gy, w) if ctx.needs_input_grad[0] else None
-        dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
-        db = hip.col_sum(gy) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dw = db = None
+        if ctx.needs_input_grad[1] and ctx.has_b and ctx.needs_input_grad[2]:
+            dw, db = _g4.mm_tn_db(x2d.contiguous(), gy)   # bias gradient from the dW GEMM's B fragments
+        else:
+            dw = weight_grad(x2d.contiguous(), gy) if ctx.needs_input_grad[1] else None
+            db = hip.col_sum(gy) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
 

@@ -30,6 +30,7 @@ EPI_EARLY = 65536    # gemm4p: early-release schedule (read burst + buffer relea
 EPI_RING = 1 << 22   # gemm4p NT: 4-slot ring of 32-deep stages (gemm4r_kernel; K % 64 == 0, K >= 128)
 EPI_ADEEP = 1 << 23  # gemm4p NT, no bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel; K >= 256)
 EPI_WSTAG = 1 << 24  # gemm4p NT + EARLY: wave w issues its LDS-DMA after MFMA w of a group
+G4P_COLSUM = 1 << 27  # gemm4p TN + EARLY: column sums of B (bias gradient) from the MFMA B fragments
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
@@ -163,13 +164,16 @@ def _group_m(a_kouter, b_kouter, K, N):
 
 
 def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=False, epi_extra=0, grid=0,
-           group_m=0, splits=1, gelu_aux=None):
+           group_m=0, splits=1, gelu_aux=None, colsum=False):
     """C = op(A) @ op(B) (+ bias[output column]) on the persistent epilogue-overlapped kernel
     (csrc/kernels/gemm4p.hip). Layouts: NT (False, False), TN (True, True), and with trans_out
     (True, False) the transposed product C^T [N, M] (``nn_p`` runs x @ W through it).
     splits > 1 (TN only): split-K into fp32 slabs + an in-order reduce (few-tile weight gradients).
     gelu_aux (NT only): C = gelu_tanh(A B^T + bias) and gelu_aux <- A B^T (the pre-activation
-    without the bias, shaped and strided like C) from the same epilogue."""
+    without the bias, shaped and strided like C) from the same epilogue.
+    colsum (TN only): also the column sums of B over K (a linear layer's bias gradient sum_t dY[t]),
+    summed by the main loop from the B fragments it already holds; returns (C, fp32 partials
+    [2 * splits * ceil(M / 256), N]) — finish with colsum_finish."""
     assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
     assert a.stride(1) == 1 and b.stride(1) == 1
     M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
@@ -191,6 +195,12 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
         assert (a_kouter, b_kouter, trans_out, splits) == (False, False, False, 1)
         assert gelu_aux.shape == c.shape and gelu_aux.stride() == c.stride() and gelu_aux.dtype == c.dtype
         epi |= EPI_GELU
+    part = None
+    if colsum:
+        assert (a_kouter, b_kouter, trans_out) == (True, True, False) and gelu_aux is None
+        part = torch.empty(2 * splits * -(-M // 256), N, dtype=torch.float32, device=a.device)
+        epi |= G4P_COLSUM | EPI_EARLY
+        gelu_aux = part
     if group_m <= 0:
         group_m = _group_m(a_kouter, b_kouter, Ka, N)
     rc = _L().pha_gemm4p(_DT[a.dtype], _ptr(a), _ptr(b), _ptr(c), M, N, Ka, a.stride(0), b.stride(0), c.stride(0),
@@ -198,7 +208,7 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
                          group_m, _ptr(ws), splits, _stream(a), _ptr(gelu_aux))
     if rc != 0:
         raise RuntimeError(f"pha_gemm4p failed ({rc}) M={M} N={N} K={Ka} a_kouter={a_kouter} b_kouter={b_kouter}")
-    return c
+    return (c, part) if colsum else c
 
 
 def gemm_8w(a, bt, bias=None, out=None, epi_extra=0, group_m=0):
@@ -514,6 +524,23 @@ def mm_tn(a, b):
             ap, bp = _pad2(a, 64, 8), _pad2(b, 64, 8)
             return gemm_p(ap, bp, True, True, splits=_splits(ap.shape[1], bp.shape[1], ap.shape[0], a.device))[:M, :N]
     return _lib_call("tn", "tn", (M, N, K), lambda: a.t() @ b)
+
+
+def mm_tn_db(a, b, db_dtype=None):
+    """(a [K, M]^T @ b [K, N], column sums of b over K) — a linear layer's weight and bias gradients
+    (x^T dY, sum_t dY[t]) from ONE pass over dY: the persistent TN kernel sums the B fragments it
+    feeds to the MFMAs (v_dot2 against 1.0, each tile row of the grid taking 1/tiles_m of the K
+    range) instead of a separate column-sum kernel re-reading dY from HBM.
+    Reference: fused_gemm_epilogue_op.cu:298 (the bias gradient of the fused linear backward)."""
+    K, M = a.shape
+    N = b.shape[1]
+    if _own_ok("tn", a, b) and b.dtype == a.dtype and os.environ.get("PHA_TN_COLSUM", "1") != "0":
+        a, b = _c(a), _c(b)
+        if supported(M, N, K, a, b):
+            c, part = gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device), colsum=True)
+            return c, colsum_finish(part, db_dtype or b.dtype)
+    from . import hip as _hip
+    return mm_tn(a, b), _hip.col_sum(b, db_dtype)
 
 
 # ----------------------------------------------------------------------------------------------

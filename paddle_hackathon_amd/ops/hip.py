@@ -277,7 +277,9 @@ def bias_gelu_fwd(x, b, approximate):
     return y
 
 
-def bias_gelu_bwd(gy, x, b, approximate):
+def bias_gelu_bwd(gy, x, b, approximate, want_db=True):
+    """(d(gelu(x + b)) / dx . gy, its column sums — the bias gradient; None with want_db=False, for
+    callers that take it from the next weight-gradient GEMM, ops/gemm.mm_tn_db)"""
     n = x.numel()
     H = x.shape[-1]
     if n % 8 or (b is not None and H % 8):
@@ -287,7 +289,16 @@ def bias_gelu_bwd(gy, x, b, approximate):
             y = TF.gelu(xx, approximate="tanh" if approximate else "none")
             (gx,) = torch.autograd.grad(y, xx, gy.float())
         gx = gx.to(x.dtype)
-    elif b is not None and x.dtype != torch.float32 and hasattr(_L(), "pha_bias_gelu_bwd_db"):
+    elif b is not None and not want_db and x.dtype != torch.float32:
+        gx = torch.empty_like(x)
+        rows = n // H
+        rpb = max(16, -(-rows // 512))
+        L = _L()
+        L.pha_bias_gelu_bwd_rows.restype = c_int
+        _check(L.pha_bias_gelu_bwd_rows(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), c_int(rows), c_int(H),
+                                        c_int(rpb), c_int(int(approximate)), _stream(x)), "bias_gelu_bwd_rows")
+        return gx, None
+    elif b is not None and want_db and x.dtype != torch.float32 and hasattr(_L(), "pha_bias_gelu_bwd_db"):
         # gx and the per-row-block column sums of gx in one pass; db = sum of the partials
         gx = torch.empty_like(x)
         rows = n // H
@@ -302,7 +313,7 @@ def bias_gelu_bwd(gy, x, b, approximate):
     else:
         gx = torch.empty_like(x)
         _check(_L().pha_bias_gelu_bwd(_DT[x.dtype], _ptr(gy), _ptr(x), _ptr(b), _ptr(gx), n, H, int(approximate), _stream(x)), "bias_gelu_bwd")
-    gb = gx.reshape(-1, H).sum(0, dtype=torch.float32).to(b.dtype) if b is not None else None
+    gb = gx.reshape(-1, H).sum(0, dtype=torch.float32).to(b.dtype) if b is not None and want_db else None
     return gx, gb
 
 

@@ -52,13 +52,13 @@ def _fwd(mode, x2d, w1, b1):
     return _hip.bias_gelu_fwd(h, b1, True), h
 
 
-def _bwd_gelu(mode, gy, w2, pre, b1):
-    """-> (d pre-activation, d b1) from the MLP output gradient"""
+def _bwd_gelu(mode, gy, w2, pre, b1, want_db=True):
+    """-> (d pre-activation, d b1 or None with want_db=False) from the MLP output gradient"""
     if mode == 1:
         g, part = G.gemm(gy, w2, False, False, act="dgelu", aux=pre, colsum=True)
         return g, G.colsum_finish(part, b1.dtype)
     ga = G.mm_nt(gy, w2)
-    return _hip.bias_gelu_bwd(ga, pre, b1, True)
+    return _hip.bias_gelu_bwd(ga, pre, b1, True, want_db=want_db)
 
 
 _MODES = {"pass": 0, "force": 1, "epi": 2}
@@ -96,11 +96,19 @@ class FusedMLP(torch.autograd.Function):
         from .conv_gemm import weight_grad
         x2d, w1, b1, w2, pre, a = ctx.saved_tensors
         gy = gy.contiguous()
-        dw2 = weight_grad(a, gy)
-        db2 = _hip.col_sum(gy) if ctx.needs_input_grad[4] else None
-        g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1)
+        # both bias gradients come out of the weight-gradient GEMMs that already read dY / dpre
+        # (G.mm_tn_db: column sums of the TN kernel's B fragments), no separate pass over either
+        if ctx.needs_input_grad[4]:
+            dw2, db2 = G.mm_tn_db(a, gy)
+        else:
+            dw2, db2 = weight_grad(a, gy), None
+        fused_db = ctx.mode != 1
+        g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1, want_db=not fused_db)
         dx = G.mm_nt(g, w1) if ctx.needs_input_grad[0] else None
-        dw1 = weight_grad(x2d, g)
+        if fused_db:
+            dw1, db1 = G.mm_tn_db(x2d, g, b1.dtype)
+        else:
+            dw1 = weight_grad(x2d, g)
         return dx, dw1, db1, dw2, db2, None
 
 

@@ -39,13 +39,18 @@ def test_gpt_micro_batch_steps_down_with_free_memory():
     spec.loader.exec_module(bench)
 
     def fake_torch(free_gb):
-        cuda = types.SimpleNamespace(mem_get_info=lambda: (free_gb * 2 ** 30, 288 * 2 ** 30))
+        cuda = types.SimpleNamespace(mem_get_info=lambda: (free_gb * 2 ** 30, 288 * 2 ** 30),
+                                     device_count=lambda: 1)
         return types.SimpleNamespace(cuda=cuda)
 
-    def args(mb=None, model="gpt3-1.3b"):
-        return types.SimpleNamespace(micro_batch=mb, model=model)
+    def args(mb=None, model="gpt3-1.3b", tp=1, pp=1, sharding_stage=0, recompute=False):
+        return types.SimpleNamespace(micro_batch=mb, model=model, tp=tp, pp=pp, sharding_stage=sharding_stage,
+                                     recompute=recompute)
     assert bench._gpt_micro_batch(args(), fake_torch(287), 1, 0) == 48
     assert bench._gpt_micro_batch(args(), fake_torch(180), 1, 0) == 32
     assert bench._gpt_micro_batch(args(), fake_torch(100), 1, 0) == 16
     assert bench._gpt_micro_batch(args(mb=12), fake_torch(20), 1, 0) == 12
     assert bench._gpt_micro_batch(args(model="gpt3-13b"), fake_torch(287), 1, 0) == 2
+    # the free-memory thresholds were measured for the plain DP layout: other layouts take 16
+    assert bench._gpt_micro_batch(args(tp=4), fake_torch(287), 1, 0) == 16
+    assert bench._gpt_micro_batch(args(pp=2, sharding_stage=3, recompute=True), fake_torch(287), 1, 0) == 16
