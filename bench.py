@@ -254,7 +254,18 @@ def _timed(a, step, world, rank, dist):
 
 
 def bench_bert(a, paddle, dist, world, rank):
-    """BERT-base pre-training (MLM 15 % masked positions + NSP), seq 512, bf16 O2, AdamW."""
+    """BERT-base pre-training (MLM 15 % masked positions + NSP), seq 512, bf16 O2, AdamW. Replayed as
+    one hipGraph under the same policy as ResNet (--graph): the eager step is host-bound (Python
+    issue time ~ GPU time, profiles/bert_host_prof_r6.log); dropout masks stay fresh per replay
+    through the kernels' device seed word (ops/hip.dropout_seed), Adam reads lr / beta powers from
+    device scalars."""
+    import torch
+    cap_stream = torch.cuda.Stream() if _resnet_graphed(a, world) else torch.cuda.current_stream()
+    with torch.cuda.stream(cap_stream):
+        return _bench_bert(a, paddle, dist, world, rank, cap_stream)
+
+
+def _bench_bert(a, paddle, dist, world, rank, cap_stream):
     import torch
     from paddle_hackathon_amd.models import bert_config, BertForPretraining, BertPretrainingCriterion
     S = a.seq_len if a.seq_len != 2048 else 512
@@ -291,6 +302,11 @@ def bench_bert(a, paddle, dist, world, rank):
         opt.clear_grad(set_to_zero=False)
         return loss
 
+    graphed = _resnet_graphed(a, world)
+    if graphed:
+        from paddle_hackathon_amd.device.cuda.graphs import wrap_cuda_graph
+        step = wrap_cuda_graph(step)
+        step._stream = cap_stream
     elapsed, loss = _timed(a, step, world, rank, dist)
     value = B * world * a.steps / elapsed
     if rank == 0:
@@ -301,7 +317,7 @@ def bench_bert(a, paddle, dist, world, rank):
             "vs_baseline": None, "dtype": "bf16", "data": "synthetic token ids / masks, random-init weights",
             "config": {"model": "BERT-base" if cfg.hidden_size == 768 else a.model, "global_batch": B * world,
                        "seq_len": S, "parallelism": f"dp{world}", "tokens_per_sec": round(value * S, 1),
-                       "final_loss": round(float(loss.item()), 4)}}), flush=True)
+                       "final_loss": round(float(loss.item()), 4), "hip_graph": bool(graphed)}}), flush=True)
 
 
 def _resnet_graphed(a, world):

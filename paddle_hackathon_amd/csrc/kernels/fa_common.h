@@ -137,7 +137,12 @@ struct FaExt {
   // dK / dV, so a packed [B, S, H, 3D] QKV gradient is written in place (no concatenation pass)
   long gq_tok = 0, gkv_tok = 0;
   int gq_head = 0, gkv_head = 0;
+  // hipGraph replays: a device word xor-ed into seed (bumped by a captured kernel every replay, so
+  // each replay draws a new mask; the backward reads the forward's copy). null: seed alone
+  const unsigned* seedp = nullptr;
 };
+
+__device__ __forceinline__ unsigned fa_seed(const FaExt& ex) { return ex.seedp ? ex.seed ^ *ex.seedp : ex.seed; }
 
 __device__ __forceinline__ unsigned fa_mix(unsigned x) {   // lowbias32 finaliser
   x ^= x >> 16;

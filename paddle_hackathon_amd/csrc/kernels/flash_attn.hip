@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void fa_fwd_kernel(const T* __restrict__ Q, co
   const T* Vb = V + ((long)b * Sk) * kstride + (long)hk * D;
   // extensions: this lane's bias row and dropout stream (query on the lane)
   const float* brow = ((EXT & 1) && q < S) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)q * ex.sq : nullptr;
-  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(ex.seed, b * H + head), q) : 0u;
+  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(fa_seed(ex), b * H + head), q) : 0u;
 
   // Q fragments (B operand of S^T = K Q^T): Q[q][16kk + 8h + j]
   frag qf[NK];
@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dkdv_kernel(const T* __restrict__ 
   const float scale_log2 = scale * kLog2e;
   // extensions (key on the lane): bias column of this key, dropout stream of the (b, h)
   const float* bcol = (EXT & 1) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + min(key, Sk - 1) : nullptr;
-  const unsigned dstream = (EXT & 2) ? fa_stream(ex.seed, b * H + head) : 0u;
+  const unsigned dstream = (EXT & 2) ? fa_stream(fa_seed(ex), b * H + head) : 0u;
 
   // keys past Sk read row Sk - 1 (finite; their P and dS are masked to 0 and their dK / dV rows
   // are not stored): unconditional loads, no exec branch per load
@@ -1400,7 +1400,7 @@ __global__ __launch_bounds__(256) void fa_bwd_dq_kernel(const T* __restrict__ Q,
   const float dlt = (q < S) ? DELTA[((long)b * H + head) * S + q] : 0.f;
   // clamped row (q past S reads row S - 1; its probabilities are masked): read unconditionally
   const float* brow = (EXT & 1) ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)min(q, S - 1) * ex.sq : nullptr;
-  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(ex.seed, b * H + head), q) : 0u;
+  const unsigned drow = (EXT & 2) ? fa_row(fa_stream(fa_seed(ex), b * H + head), q) : 0u;
 
   frag qf[NK], gf[NK];
 #pragma unroll
@@ -2572,10 +2572,12 @@ int dispatch_ext(bool bwd, const void* q, const void* k, const void* v, void* o,
 // backward regenerates the same mask from it). Head dims 32 / 64 / 128 / 256.
 PHA_API int pha_flash_attn_fwd_ext(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B,
                                    int S, int Sk, int H, int Hk, int D, float scale, int causal, const float* bias,
-                                   long sb, long sh, long sq, float dropout, unsigned seed, hipStream_t stream) {
+                                   long sb, long sh, long sq, float dropout, unsigned seed, hipStream_t stream,
+                                   const unsigned* seedp) {
   if (H % Hk || (D != 32 && D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
     return (int)hipErrorInvalidValue;
   FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  ex.seedp = seedp;
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
   if (dt == kBF16) return dispatch_ext<bf16_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
   if (dt == kF16) return dispatch_ext<half_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
@@ -2588,7 +2590,7 @@ PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const v
                                    const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int S,
                                    int Sk, int H, int Hk, int D, float scale, int causal, const float* bias, long sb,
                                    long sh, long sq, float dropout, unsigned seed, hipStream_t stream, long gq_tok,
-                                   int gq_head, long gkv_tok, int gkv_head) {
+                                   int gq_head, long gkv_tok, int gkv_head, const unsigned* seedp) {
   if (H % Hk || (D != 32 && D != 64 && D != 128 && D != 256) || S <= 0 || Sk <= 0 || dropout < 0.f || dropout >= 1.f)
     return (int)hipErrorInvalidValue;
   if ((gkv_tok || gkv_head) && Hk != H) return (int)hipErrorInvalidValue;
@@ -2597,6 +2599,7 @@ PHA_API int pha_flash_attn_bwd_ext(int dt, const void* q, const void* k, const v
   ex.gq_head = gq_head;
   ex.gkv_tok = gkv_tok;
   ex.gkv_head = gkv_head;
+  ex.seedp = seedp;
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
   if (dt == kBF16) return dispatch_ext<bf16_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);
   if (dt == kF16) return dispatch_ext<half_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H, Hk, D, scale, causal, ex, stream);

@@ -34,6 +34,9 @@ using namespace g256;
 #ifndef PHA_G4P_RELG_NT
 #define PHA_G4P_RELG_NT 8
 #endif
+#ifndef PHA_G4P_CS_SPLITLOOP
+#define PHA_G4P_CS_SPLITLOOP 1
+#endif
 #ifndef PHA_G4P_RELG_TN
 #define PHA_G4P_RELG_TN 8
 #endif
@@ -809,9 +812,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         phaseE(M0{}, no{}, VW1{}, fa1, fb1, fa0, fb0, buf ^ 1, 0, buf, cs_c, sel(k, 1));
         stage_end();
       };
-      // (one loop: cutting it at klo / khi into dot2-free and dot2 copies raised the VGPR count
-      // 207 -> 256 with 61 SGPR spills; the 4 dot2s per group ride in the MFMA issue gaps)
-      for (int k = 1; k < nk; ++k, ++s) ktile(CSY{}, k);
+      // the K-tile loop cut at klo / khi: only the phases of [klo, khi) carry the dot2s (all-on
+      // dot2 phases cost the TN kernel 9-13 %, profiles/tn_colsum_r6/)
+      if constexpr (CS && PHA_G4P_CS_SPLITLOOP) {
+        using CSN = std::false_type;
+        int k = 1;
+        for (; k < klo; ++k, ++s) ktile(CSN{}, k);
+        for (; k < khi; ++k, ++s) ktile(CSY{}, k);
+        for (; k < nk; ++k, ++s) ktile(CSN{}, k);
+      } else {
+        for (int k = 1; k < nk; ++k, ++s) ktile(CSY{}, k);
+      }
       if constexpr (CS) {
         // the item is done: sum the 4 k-quarters (lanes l, l+16, l+32, l+48) of every fragment. The
         // swaps pair DIFFERENT fragments (a swap of a register with itself is a no-op): after

@@ -38,7 +38,10 @@ struct BdArgs {            // x -> dropout(x + xb) before the residual add (thre
   unsigned seed, thresh;
   float kscale;
   int xb_f32;
+  const unsigned* seedp;   // hipGraph replays: device word xor-ed into seed (null: seed alone)
 };
+
+__device__ __forceinline__ unsigned bd_seed(const BdArgs& bd) { return bd.seedp ? bd.seed ^ *bd.seedp : bd.seed; }
 
 template <typename T, typename W, int NCH>
 // With `r` set: the pre-LN residual add is fused in — hs = x + r (rounded to T, exactly what
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             float z = round_to<T>(v[c][i] + (bd.xb ? bv[i] : 0.f));
-            if (bd.thresh) z = bd_keep(bd.seed, (long)row * H + col + i, bd.thresh) ? round_to<T>(z * bd.kscale) : 0.f;
+            if (bd.thresh) z = bd_keep(bd_seed(bd), (long)row * H + col + i, bd.thresh) ? round_to<T>(z * bd.kscale) : 0.f;
             v[c][i] = z;
           }
         }
@@ -348,7 +351,9 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
 template <typename T, int NCH, int BW>
 __global__ __launch_bounds__(BW * 64) void dropout_bias_bwd_kernel(const T* __restrict__ dh, T* __restrict__ dx,
                                                                    float* __restrict__ part, int rows, int H,
-                                                                   unsigned seed, unsigned thresh, float kscale) {
+                                                                   unsigned seed, unsigned thresh, float kscale,
+                                                                   const unsigned* __restrict__ seedp) {
+  if (seedp) seed ^= *seedp;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   float acc[NCH][8];
@@ -536,11 +541,11 @@ PHA_API int pha_layer_norm_bwd_nblocks(int rows, int H) {
 // xbdt: dtype of xb (fp32 or the activation type)
 PHA_API int pha_bdrln_fwd2(int dt, int wdt, int xbdt, const void* x, const void* xb, const void* r, void* hs,
                            const void* w, const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps,
-                           unsigned seed, unsigned thresh, float kscale, hipStream_t stream) {
+                           unsigned seed, unsigned thresh, float kscale, hipStream_t stream, const unsigned* seedp) {
   if (H % 8 || rows <= 0 || !r || !hs) return (int)hipErrorInvalidValue;
   if (xb && xbdt != kF32 && xbdt != dt) return (int)hipErrorInvalidValue;
   const dim3 grid((rows + kWaves - 1) / kWaves), block(256);
-  const BdArgs bd{xb, seed, thresh, kscale, xbdt == kF32 ? 1 : 0};
+  const BdArgs bd{xb, seed, thresh, kscale, xbdt == kF32 ? 1 : 0, seedp};
   int rc = 0;
   PHA_DISPATCH_T(dt, T, {
     if (wdt == kF32) {
@@ -563,7 +568,8 @@ PHA_API int pha_bdrln_fwd2(int dt, int wdt, int xbdt, const void* x, const void*
 PHA_API int pha_bdrln_fwd(int dt, int wdt, const void* x, const void* xb, const void* r, void* hs, const void* w,
                           const void* b, void* y, float* mean, float* rstd, int rows, int H, float eps, unsigned seed,
                           unsigned thresh, float kscale, hipStream_t stream) {
-  return pha_bdrln_fwd2(dt, wdt, wdt, x, xb, r, hs, w, b, y, mean, rstd, rows, H, eps, seed, thresh, kscale, stream);
+  return pha_bdrln_fwd2(dt, wdt, wdt, x, xb, r, hs, w, b, y, mean, rstd, rows, H, eps, seed, thresh, kscale, stream,
+                        nullptr);
 }
 
 PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, const void* b, void* y,
@@ -679,14 +685,15 @@ PHA_API int pha_layer_norm_bwd(int dt, int wdt, const void* dy, const void* x, c
 // backward of the dropout(x + xb) branch: dx = dh * mask * kscale; dbias (type of wdt, may be null)
 // = column sums of dx; part: workspace [nblocks + 8, H] fp32 (nblocks = pha_layer_norm_bwd_nblocks)
 PHA_API int pha_dropout_bias_bwd(int dt, int wdt, const void* dh, void* dx, void* dbias, float* part, int nblocks,
-                                 int rows, int H, unsigned seed, unsigned thresh, float kscale, hipStream_t stream) {
+                                 int rows, int H, unsigned seed, unsigned thresh, float kscale, hipStream_t stream,
+                                 const unsigned* seedp) {
   if (H % 8 || rows <= 0 || nblocks <= 0) return (int)hipErrorInvalidValue;
   int rc = 0;
   PHA_DISPATCH_T(dt, T, {
     rc = dispatch_nch_small(H, [&](auto nch) {
       constexpr int bw = bwd_waves(decltype(nch)::value);
       hipLaunchKernelGGL((dropout_bias_bwd_kernel<T, decltype(nch)::value, bw>), dim3(nblocks), dim3(bw * 64), 0,
-                         stream, (const T*)dh, (T*)dx, part, rows, H, seed, thresh, kscale);
+                         stream, (const T*)dh, (T*)dx, part, rows, H, seed, thresh, kscale, seedp);
     });
     if (rc) return rc;
     if (dbias) {

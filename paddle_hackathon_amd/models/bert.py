@@ -190,6 +190,8 @@ class BertPretrainingCriterion(nn.Layer):
 
     def forward(self, mlm_logits, nsp_logits, mlm_labels, nsp_labels):
         mlm = _ops.softmax_cross_entropy(mlm_logits._t.contiguous(), mlm_labels._t.reshape(-1).long())
-        mlm = mlm[mlm_labels._t.reshape(-1) != -100].float().mean() if mlm.dim() else mlm
+        if mlm.dim():   # mean over the labelled positions, as a masked sum (boolean indexing syncs the host)
+            valid = (mlm_labels._t.reshape(-1) != -100).to(torch.float32)
+            mlm = (mlm.float() * valid).sum() / valid.sum().clamp_min(1.0)
         nsp = TF.cross_entropy(nsp_logits._t.float(), nsp_labels._t.reshape(-1).long())
         return _wrap(mlm + nsp)

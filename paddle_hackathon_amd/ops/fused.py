@@ -185,10 +185,11 @@ class _BiasDropoutResidualLN(torch.autograd.Function):
     def forward(ctx, x, residual, bias, w, b, p, eps):
         thresh = min(65535, int(round(p * 65536))) if p > 0 else 0
         kscale = 1.0 / (1.0 - p) if p > 0 else 1.0
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if thresh else 0
-        y, mean, rstd, hs = _hip.bdrln_fwd(x, bias, residual, w, b, eps, seed, thresh, kscale)
+        seed, seed_dev = _hip.dropout_seed(x.device) if thresh else (0, None)
+        y, mean, rstd, hs = _hip.bdrln_fwd(x, bias, residual, w, b, eps, seed, thresh, kscale, seed_dev)
         ctx.save_for_backward(hs, w, mean, rstd)
         ctx.cfg = (seed, thresh, kscale, b is not None, None if bias is None else bias.dtype)
+        ctx.seed_dev = seed_dev
         return y
 
     @staticmethod
@@ -199,7 +200,7 @@ class _BiasDropoutResidualLN(torch.autograd.Function):
         if thresh == 0 and xb_dt is None:
             dx, dxb = dh, None
         else:
-            dx, dxb = _hip.dropout_bias_bwd(dh, seed, thresh, kscale, xb_dt)
+            dx, dxb = _hip.dropout_bias_bwd(dh, seed, thresh, kscale, xb_dt, ctx.seed_dev)
         return dx, dh, dxb, dw, db, None, None
 
 

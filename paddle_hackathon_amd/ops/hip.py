@@ -33,10 +33,10 @@ def _L():
             "pha_layer_norm_fwd2": [I, I, P, P, P, P, P, P, P, P, I, I, F, P],
             "pha_layer_norm_bwd2": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
             "pha_layer_norm_bwd3": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
-            "pha_bdrln_fwd2": [I, I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
+            "pha_bdrln_fwd2": [I, I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P, P],
             "pha_col_sum_rows": [I, P, P, I, I, P],
             "pha_bdrln_fwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
-            "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P],
+            "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
             "pha_softmax_bwd": [I, P, P, P, I, I, P],
             "pha_softmax_ce_fwd": [I, P, P, P, P, LG, I, I, P],
@@ -129,7 +129,28 @@ def layer_norm_bwd(dy, x, w, mean, rstd, has_bias, dres=None, dx_colsum=None):
     return dx, dw, db
 
 
-def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale):
+def dropout_seed(device):
+    """(host seed, device seed word or None) for a dropout site whose mask the backward regenerates.
+    Eager: a fresh host seed. Inside a hipGraph capture the host value would be baked into every
+    replay, so the kernels also xor in a device word: a per-device counter bumped by a captured
+    kernel (each replay advances it) and copied for this site — the copy is what the site's
+    backward reads, whatever later sites did to the counter."""
+    seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    buf = _SEED_BUFS.get(device)
+    if buf is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dropout inside a hipGraph capture needs one eager step first")
+        buf = _SEED_BUFS[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    if not torch.cuda.is_current_stream_capturing():
+        return seed, None
+    buf.add_(1)
+    return seed, buf.clone()
+
+
+_SEED_BUFS = {}
+
+
+def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale, seed_dev=None):
     """fused_bias_dropout_residual_layer_norm forward: hs = residual + dropout(x + xbias), y = LN(hs).
     Returns (y, mean, rstd, hs)."""
     H = w.numel()
@@ -145,12 +166,13 @@ def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale):
     xbdt = _DT[w.dtype] if xb is None else _DT[xb.dtype]
     _check(_L().pha_bdrln_fwd2(_DT[x.dtype], _DT[w.dtype], xbdt, _ptr(x), _ptr(xb), _ptr(residual), _ptr(hs),
                               _ptr(w.contiguous()), _ptr(None if b is None else b.contiguous()), _ptr(y), _ptr(mean),
-                              _ptr(rstd), rows, H, float(eps), int(seed), int(thresh), float(kscale), _stream(x)),
+                              _ptr(rstd), rows, H, float(eps), int(seed), int(thresh), float(kscale), _stream(x),
+                              _ptr(seed_dev)),
            "bdrln_fwd")
     return y, mean, rstd, hs
 
 
-def dropout_bias_bwd(dh, seed, thresh, kscale, bias_dtype=None):
+def dropout_bias_bwd(dh, seed, thresh, kscale, bias_dtype=None, seed_dev=None):
     """dx = dh * mask * kscale (the forward's regenerated mask) and dbias = column sums of dx."""
     H = dh.shape[-1]
     rows = dh.numel() // H
@@ -160,7 +182,8 @@ def dropout_bias_bwd(dh, seed, thresh, kscale, bias_dtype=None):
     wdt = _DT[bias_dtype] if bias_dtype is not None else _DT[dh.dtype]
     part = torch.empty((nblocks + 8, H), dtype=torch.float32, device=dh.device)
     _check(_L().pha_dropout_bias_bwd(_DT[dh.dtype], wdt, _ptr(dh), _ptr(dx), _ptr(db), _ptr(part), nblocks, rows, H,
-                                     int(seed), int(thresh), float(kscale), _stream(dh)), "dropout_bias_bwd")
+                                     int(seed), int(thresh), float(kscale), _stream(dh), _ptr(seed_dev)),
+           "dropout_bias_bwd")
     return dx, db
 
 
@@ -679,23 +702,24 @@ class FlashAttentionExt(torch.autograd.Function):
         Sk, Hk = k.shape[1], k.shape[2]
         sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
         bias, (sb, sh, sq) = (None, (0, 0, 0)) if mask is None else _fa_bias(mask, B, H, S, Sk, q.device)
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if dropout_p else 0
+        seed, seed_dev = dropout_seed(q.device) if dropout_p else (0, None)
         o = torch.empty_like(q)
         lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
         L = _L()
         if not getattr(L, "_fa_ext_sig", False):
             P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
-            L.pha_flash_attn_fwd_ext.argtypes = [I, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG, F, U, P]
+            L.pha_flash_attn_fwd_ext.argtypes = [I, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG, F, U, P, P]
             L.pha_flash_attn_fwd_ext.restype = c_int
             L.pha_flash_attn_bwd_ext.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, LG, LG, LG,
-                                                 F, U, P, LG, I, LG, I]
+                                                 F, U, P, LG, I, LG, I, P]
             L.pha_flash_attn_bwd_ext.restype = c_int
             L._fa_ext_sig = True
         _check(L.pha_flash_attn_fwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), B, S, Sk, H, Hk, D,
-                                        sc, int(causal), _ptr(bias), sb, sh, sq, float(dropout_p), seed, _stream(q)),
+                                        sc, int(causal), _ptr(bias), sb, sh, sq, float(dropout_p), seed, _stream(q),
+                                        _ptr(seed_dev)),
                "flash_attn_fwd_ext")
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.bias, ctx.strides, ctx.seed = bias, (sb, sh, sq), seed
+        ctx.bias, ctx.strides, ctx.seed, ctx.seed_dev = bias, (sb, sh, sq), seed, seed_dev
         ctx.causal, ctx.scale, ctx.dropout_p = causal, sc, float(dropout_p)
         return o
 
@@ -715,7 +739,8 @@ class FlashAttentionExt(torch.autograd.Function):
         sb, sh, sq = ctx.strides
         _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
                                         _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk, H, Hk, D, ctx.scale, int(ctx.causal),
-                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q), 0, 0, 0, 0),
+                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q), 0, 0, 0, 0,
+                                        _ptr(ctx.seed_dev)),
                "flash_attn_bwd_ext")
         if Hk != H:
             g = H // Hk
@@ -754,7 +779,7 @@ class FlashAttentionExtPacked(torch.autograd.Function):
         _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
                                         c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), B, S, S,
                                         H, H, D, ctx.scale, int(ctx.causal), _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p,
-                                        ctx.seed, _stream(q), 3 * H * D, 3 * D, 3 * H * D, 3 * D),
+                                        ctx.seed, _stream(q), 3 * H * D, 3 * D, 3 * H * D, 3 * D, _ptr(ctx.seed_dev)),
                "flash_attn_bwd_ext(packed)")
         return g, None, None, None, None
 
