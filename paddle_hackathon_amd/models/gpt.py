@@ -143,6 +143,10 @@ class GPTMLP(nn.Layer):
 
 
 class GPTDecoderLayer(nn.Layer):
+    # stage-3 sharding gathers the whole block as one unit: its forward reads the sublayers'
+    # weights directly (fused kernels), so per-sublayer hooks would never fire
+    _sharding_unit = True
+
     def __init__(self, cfg: GPTConfig):
         super().__init__()
         self.cfg = cfg
@@ -155,13 +159,20 @@ class GPTDecoderLayer(nn.Layer):
     def _drop(self, t):
         return F.dropout(t, self.dropout, training=self.training) if self.dropout and self.training else t
 
-    def forward(self, x):
-        h, m = self.forward_fused(x, None)
-        return h + m
+    def forward(self, x, delta=None, fused=False):
+        """fused: (h, m) of forward_fused (the model's residual-deferred chain, called through the
+        Layer so forward hooks — stage-3 gathers — fire); else the layer output h + m"""
+        h, m = self.forward_fused(x, delta)
+        return (h, m) if fused else h + m
 
     def _add_ln(self, norm, x, delta, dbias=None):
         if delta is None:
             return x, norm(x)
+        if norm.weight._t.numel() == 0 and dbias is None:
+            # the norm's weights are released by stage-3 sharding (its own unit, outside this
+            # block): call it through the Layer so the gather hook fires
+            h = x + delta
+            return h, norm(h)
         h, y = _ops.fused.add_layer_norm(x._t, delta._t, norm.weight._t, None if norm.bias is None else norm.bias._t,
                                          norm._epsilon, xb=None if dbias is None else dbias._t)
         return _wrap(h), _wrap(y)
@@ -230,9 +241,9 @@ class GPTModel(nn.Layer):
         for layer in self.layers:
             if self.cfg.recompute and self.training:
                 from ..parallel.recompute import recompute
-                x, delta = recompute(layer.forward_fused, x, delta)
+                x, delta = recompute(layer, x, delta, fused=True)
             else:
-                x, delta = layer.forward_fused(x, delta)
+                x, delta = layer(x, delta, fused=True)
         if delta is None:
             return self.final_norm(x)
         return self.layers[-1]._add_ln(self.final_norm, x, delta)[1]
@@ -245,6 +256,11 @@ class GPTForPretraining(nn.Layer):
         super().__init__()
         self.cfg = cfg
         self.gpt = GPTModel(cfg)
+
+    def shared_parameters(self):
+        """the tied input / output embedding (read directly by the logits GEMM): stage-3 sharding
+        keeps it replicated, as the pipeline form does for its shared layers"""
+        return [self.gpt.embeddings.word_embeddings.weight]
 
     def logits(self, h):
         w = self.gpt.embeddings.word_embeddings.weight

@@ -13,6 +13,7 @@ ranks see different ones (both split the batch), so ``data_ranks = dp * sharding
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 _LEVEL = {1: "os", 2: "os_g", 3: "p_g_os"}
@@ -114,7 +115,10 @@ class GPTTrainer:
         if lo.sharding_stage and lo.sharding > 1:
             from paddle_hackathon_amd.parallel.sharding import group_sharded_parallel
             keep = getattr(model, "shared_parameters", lambda: [])()
-            m2, opt, _ = group_sharded_parallel(model, opt, _LEVEL[lo.sharding_stage],
+            # stage 3 shards parameters of >= segment elements (PHA_STAGE3_SEGMENT; the tests force
+            # the tiny models' blocks to shard too)
+            seg = int(os.environ.get("PHA_STAGE3_SEGMENT", str(2 ** 20)))
+            m2, opt, _ = group_sharded_parallel(model, opt, _LEVEL[lo.sharding_stage], segment_size=seg,
                                                 group=hcg.get_sharding_parallel_group(), replicate=keep)
             if lo.pp == 1:
                 model = m2

@@ -20,6 +20,8 @@ collective after backward is short).
 from __future__ import annotations
 
 import torch
+
+from .recompute import queue_outer_callback as _queue_outer
 import torch.distributed as dist
 
 from ..framework.core import Tensor, _wrap
@@ -95,7 +97,7 @@ class _Reducer:
                 return
             if not self._callback_queued:
                 self._callback_queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+                _queue_outer(self._finalize)
             b = self.buckets[self.param_bucket[key]]
             b.ready_count += 1
             if b.ready_count == len(b.params):

@@ -6,11 +6,35 @@ so dropout masks match, then back-propagates through the recomputed graph.
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 
 from ..framework.core import Tensor, _wrap
 
 __all__ = ["recompute", "recompute_sequential"]
+
+
+class _Nesting(threading.local):
+    def __init__(self):
+        self.depth = 0
+        self.deferred = []
+
+
+_NEST = _Nesting()
+
+
+def queue_outer_callback(cb):
+    """queue ``cb`` to run when the OUTERMOST backward in progress finishes. Gradient hooks firing
+    inside a recomputed segment run in the nested backward of _Recompute.backward, and
+    ``queue_callback`` would attach to that nested graph task — a reducer / sharding finaliser
+    would then run after the first recomputed segment and miss every later gradient. Inside a
+    recompute backward the callback is held and queued on the outer task when the segment ends."""
+    if _NEST.depth > 0:
+        if cb not in _NEST.deferred:
+            _NEST.deferred.append(cb)
+    else:
+        torch.autograd.Variable._execution_engine.queue_callback(cb)
 
 
 def _tracker_states():
@@ -71,7 +95,15 @@ class _Recompute(torch.autograd.Function):
         outs_t = [o._t if isinstance(o, Tensor) else o for o in outs]
         pairs = [(o, g) for o, g in zip(outs_t, grads) if isinstance(o, torch.Tensor) and o.requires_grad and g is not None]
         if pairs:
-            torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+            _NEST.depth += 1
+            try:
+                torch.autograd.backward([p[0] for p in pairs], [p[1] for p in pairs])
+            finally:
+                _NEST.depth -= 1
+            if _NEST.depth == 0 and _NEST.deferred:
+                cbs, _NEST.deferred = _NEST.deferred, []
+                for cb in cbs:   # this node runs in the outer backward: its graph task takes them
+                    torch.autograd.Variable._execution_engine.queue_callback(cb)
         gin = [t.grad if isinstance(t, torch.Tensor) else None for t in inputs]
         return (None, None, None, None, *gin)
 

@@ -44,6 +44,8 @@ import contextlib
 import math
 
 import torch
+
+from .recompute import queue_outer_callback as _queue_outer
 import torch.distributed as dist
 
 from ..framework.core import Tensor, Parameter, _wrap
@@ -233,7 +235,7 @@ class GroupShardedOptimizer:
                 return
             if not self._queued:
                 self._queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                _queue_outer(self._finish)
             b.ready += 1
             if b.ready == len(b.params):
                 self._launch(b)
@@ -418,7 +420,11 @@ class GroupShardedStage3(Layer):
         self._replicated = []
         seen = set()
         for sub in layer.sublayers(include_self=True):
-            own = [p for p in sub._parameters.values() if p is not None and id(p) not in seen]
+            # a layer class with _sharding_unit = True (a transformer block whose forward reads its
+            # sublayers' weights directly, fused kernels, never calling them) is ONE unit with all
+            # of its parameters, gathered by its own hooks; otherwise each sublayer's own ones
+            src = sub.parameters() if getattr(type(sub), "_sharding_unit", False) else sub._parameters.values()
+            own = [p for p in src if p is not None and id(p) not in seen]
             for p in own:
                 seen.add(id(p))
             rep_ids = {id(p) for p in replicate}
@@ -490,7 +496,12 @@ class GroupShardedStage3(Layer):
         A request the pool cannot place falls back to a plain allocation (counted)."""
         self._arena = self._pool = None
         self._pool_fallbacks = 0
-        if not self._units or os.environ.get("PHA_STAGE3_ARENA", "1") == "0":
+        # opt-in only: autograd keeps shallow copies / views of gathered weights in saved
+        # activations, and an explicitly freed arena region is re-gathered into while they still
+        # point at it (GPT blocks sharded at segment 64 trained differently from one process from
+        # the second update on; plain allocations stay alive while referenced and match exactly —
+        # tests/test_bench_layouts.py::test_stage3_sharded_blocks_with_recompute)
+        if not self._units or os.environ.get("PHA_STAGE3_ARENA", "0") != "1":
             return
         try:
             from ..utils import native
@@ -552,6 +563,13 @@ class GroupShardedStage3(Layer):
 
     def _release(self, u):
         if not u.gathered:
+            if u.full_work is not None:   # a prefetch nobody consumed: drop it (its data may go stale)
+                if hasattr(u.full_work, "wait"):
+                    u.full_work.wait()
+                u.full_work = None
+                u.full_src = None
+                u.bucket.flat_param = None
+                self._free_full(u)
             return
         for p in u.bucket.params:
             p._t.data = torch.empty(0, dtype=p._t.dtype, device=p._t.device)
@@ -575,20 +593,24 @@ class GroupShardedStage3(Layer):
                     self._seen.add(id(u))
                     self._order.append(u)
                 self._gather(u)
-            if not self._recording:
+            # layer-ahead prefetch — not when recompute re-runs the forward inside the backward:
+            # the next layer's backward is already done, its gather would sit unconsumed
+            if not self._recording and torch._C._current_graph_task_id() == -1:
                 nxt = self._neighbor(units[-1], +1)
                 if nxt is not None:
-                    self._issue_gather(nxt)   # layer-ahead prefetch
+                    self._issue_gather(nxt)
         return hook
 
     def _make_post_fwd(self, units):
         def hook(layer, inputs, out):
             if torch.is_grad_enabled():
+                # on EVERY output that needs a gradient: the backward may reach any of them first
+                # (a block returning (h, m) runs m's nodes before h's hook fires); gathering is
+                # idempotent
                 outs = out if isinstance(out, (tuple, list)) else [out]
                 for o in outs:
                     if isinstance(o, Tensor) and o._t.requires_grad:
                         o._t.register_hook(self._make_pre_bwd(units))
-                        break
             for u in units:
                 self._release(u)
             return None
@@ -598,7 +620,7 @@ class GroupShardedStage3(Layer):
         def hook(g):
             if not self._queued:
                 self._queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                _queue_outer(self._finish)
             for u in units:
                 self._gather(u)
             prv = self._neighbor(units[0], -1)
@@ -640,7 +662,7 @@ class GroupShardedStage3(Layer):
         def hook(t):
             if not self._queued:
                 self._queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                _queue_outer(self._finish)
             self._rep_ready += 1
         return hook
 

@@ -26,12 +26,15 @@ def _ids(n_rows):
     return np.random.RandomState(8).randint(0, 512, (n_rows, S + 1)).astype("int64")
 
 
-def _run(rank, world, layout_kw, state, amp=False):
+def _run(rank, world, layout_kw, state, amp=False, cfg=None, segment=None):
+    import os
     import paddle_hackathon_amd as paddle
+    if segment is not None:
+        os.environ["PHA_STAGE3_SEGMENT"] = str(segment)
     from paddle_hackathon_amd.models.gpt_train import GPTTrainer, Layout
     lo = Layout(world=world, **layout_kw)
     # TP ranks load their slices of the full state (GPTTrainer slices it)
-    tr = GPTTrainer("gpt-tiny", lo, rank, lr=1e-2, amp=amp, cfg_overrides=CFG, state=state)
+    tr = GPTTrainer("gpt-tiny", lo, rank, lr=1e-2, amp=amp, cfg_overrides=cfg or CFG, state=state)
     ids = _ids(B * lo.data_ranks)
     d = tr.data_rank()
     mine = ids[d * B:(d + 1) * B]
@@ -41,11 +44,11 @@ def _run(rank, world, layout_kw, state, amp=False):
     return {"losses": losses, "data_rank": d, "name": lo.name(), "dtypes": dtypes}
 
 
-def _reference(state, data_ranks, amp=False):
+def _reference(state, data_ranks, amp=False, cfg=None):
     import paddle_hackathon_amd as paddle
     from paddle_hackathon_amd.models.gpt_train import GPTTrainer, Layout
     paddle.set_device("cpu")
-    tr = GPTTrainer("gpt-tiny", Layout(world=1), 0, lr=1e-2, amp=amp, cfg_overrides=CFG, state=state)
+    tr = GPTTrainer("gpt-tiny", Layout(world=1), 0, lr=1e-2, amp=amp, cfg_overrides=cfg or CFG, state=state)
     ids = _ids(B * data_ranks)
     inp, lab = paddle.to_tensor(ids[:, :-1]), paddle.to_tensor(ids[:, 1:])
     return [float(tr.step(inp, lab).astype("float32").numpy().reshape(-1)[0]) for _ in range(STEPS)]
@@ -96,3 +99,25 @@ def test_layout_bf16_amp_matches_single_process(world, layout):
     mean = np.mean([by_d[d][0] for d in sorted(by_d)], axis=0)
     np.testing.assert_allclose(mean, ref, rtol=3e-2, atol=3e-2)
     assert ref[-1] < ref[0]
+
+
+@pytest.mark.parametrize("recompute", [False, True], ids=["plain", "recompute"])
+@pytest.mark.parametrize("world,layout", [
+    (2, {"sharding_stage": 3}),                                       # sharding2 (p_g_os)
+    (4, {"pp": 2, "sharding_stage": 3, "micro_batches": 2}),          # pp2 x sharding2 (p_g_os)
+], ids=["sharding2_s3", "pp2_sharding2_s3"])
+def test_stage3_sharded_blocks_with_recompute(world, layout, recompute):
+    """BASELINE config 5's structure (stage-3 + PP + recompute) with every decoder block actually
+    sharded (segment 64 elements): a block is ONE stage-3 unit (its fused forward reads the
+    sublayers' weights directly, so per-sublayer hooks would never gather them), it is called
+    through the Layer (hooks fire) also when recompute re-runs it in the backward"""
+    cfg = dict(CFG, recompute=recompute)
+    state = _state()
+    res = run_dist(_run, world, args=(layout, state, False, cfg, 64))
+    data_ranks = max(r["data_rank"] for r in res) + 1
+    ref = _reference(state, data_ranks, cfg=cfg)
+    by_d = {}
+    for r in res:
+        by_d.setdefault(r["data_rank"], []).append(r["losses"])
+    mean = np.mean([by_d[d][0] for d in sorted(by_d)], axis=0)
+    np.testing.assert_allclose(mean, ref, rtol=2e-4, atol=2e-5)
