@@ -4,8 +4,8 @@
 # tools/mem_fit.py. One torchrun per (layout, depth), each under its own time limit.
 mkdir -p gpurun_out
 export PHA_DIST_BACKEND=gloo
-out=gpurun_out/mem_r6.jsonl
-: > $out
+out=gpurun_out/mem_r6_13b.jsonl
+touch $out
 port=29611
 run() {  # nproc args...
   local n=$1; shift
@@ -19,9 +19,10 @@ run() {  # nproc args...
   tail -1 $out
 }
 # BASELINE 2: GPT-3 1.3B fleet DP, the bench default micro-batch 48 per GPU (2 ranks shown)
-run 2 --model gpt3-1.3b --layers 2 --micro-batch 48 && run 2 --model gpt3-1.3b --layers 4 --micro-batch 48 &&
+# (DP2 mb48 and DP2 x TP4 measured in the first pass: gpurun_out/mem_r6.jsonl)
+: &&
 # BASELINE 4: GPT-3 1.3B DP2 x TP4, micro-batch 16 (bench default for non-DP layouts)
-run 8 --model gpt3-1.3b --tp 4 --layers 2 --micro-batch 16 && run 8 --model gpt3-1.3b --tp 4 --layers 4 --micro-batch 16 &&
+: &&
 # BASELINE 5: GPT-3 13B sharding stage 3 + PP2 + recompute on 8 ranks, micro-batch 16
 run 8 --model gpt3-13b --pp 2 --sharding-stage 3 --recompute --layers 4 --micro-batch 16 &&
 run 8 --model gpt3-13b --pp 2 --sharding-stage 3 --recompute --layers 8 --micro-batch 16 &&

@@ -38,8 +38,8 @@ def main(path):
             for k in ("peak_gb", "reserved_gb"):
                 b = (r1[k] - r0[k]) / (l1 - l0)
                 ext.append(r0[k] + b * (full - l0))
-            worst = max(worst, tuple(ext), key=lambda e: e[1])
-        need = worst[1] + RCCL_GB
+            worst = max(worst, tuple(ext), key=lambda e: max(e))
+        need = max(worst) + RCCL_GB   # the larger of the two fits (reserved grows slower at small L)
         head = 1.0 - need / HBM_GB
         ok = head >= 0.15
         ok_all &= ok
