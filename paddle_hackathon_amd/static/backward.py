@@ -322,6 +322,8 @@ def append_optimize_op(optimizer, params_grads, program=None, block=None, found_
         # in a non-root Scope the params are that scope's copies: step them with its own state;
         # Hogwild dataset-trainer threads apply their updates one at a time
         from .trainer import hogwild_update
+        # lock-free Hogwild batches ran on parameter aliases: the update goes to the real ones
+        params = [getattr(p, "_hogwild_of", p) for p in params]
         with hogwild_update(), P.optimizer_lock(optimizer), P.scoped_optimizer(optimizer, ps, params):
             for p, g in zip(params, grads):
                 p._t.grad = g._t.detach().to(p._t.dtype)

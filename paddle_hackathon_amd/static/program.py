@@ -1200,6 +1200,14 @@ def run_program(program, feed, fetch_list, scope=None):
     sc = scope if scope is not None else _global_scope
     env = _scope_overrides(program, sc)
     prev_scope, _RUN_SCOPE[0] = _RUN_SCOPE[0], (sc if env else None)
+    from .trainer import hogwild_alias
+    if hogwild_alias():
+        for t in _program_tensors(program):
+            if isinstance(t, Parameter) and id(t) not in env and t._t.is_floating_point():
+                a = _wrap(t._t.data)   # same storage, own version counter
+                a._t.requires_grad_(t._t.requires_grad)
+                a.name, a.persistable, a._hogwild_of = t.name, True, t
+                env[id(t)] = a
     try:
         return _run_program(program, blk, env, feed, fetch_list)
     finally:

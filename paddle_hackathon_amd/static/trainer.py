@@ -71,6 +71,15 @@ class _Worker(threading.local):
     def __init__(self):
         self.rw = None          # the trainer's lock while this thread is a worker
         self.reading = False    # holds the read side (inside a batch, before its update)
+        self.alias = False      # lock-free Hogwild: the batch reads parameter aliases (see below)
+
+
+def hogwild_alias():
+    """inside a lock-free Hogwild worker: run_program binds every trainable parameter to an alias
+    sharing its storage with its own autograd version counter (``tensor.data``), so other threads'
+    in-place updates land in this batch's reads (Hogwild's racy reads) without invalidating the
+    tensors its backward saved; the update is applied to the real parameter"""
+    return _WORKER.alias
 
 
 _WORKER = _Worker()
@@ -123,16 +132,24 @@ class DeviceWorker:
 
 
 class Hogwild(DeviceWorker):
-    """lock-free asynchronous SGD over shared parameters (hogwild_worker.cc)"""
+    """lock-free asynchronous SGD over shared parameters (hogwild_worker.cc: every thread runs the
+    whole program on its batches against the shared parameters; no thread waits for another's
+    forward / backward). Each batch reads parameter aliases (``hogwild_alias``): other threads'
+    updates show up in its reads while it runs, as in the reference, and its own update is one
+    optimizer step on the real parameters, serialised only against other updates (the
+    optimizer's state is one object)"""
+    lock_free = True
 
 
-class DownpourSGD(DeviceWorker):
-    """parameter-server worker (downpour_worker.cc): sparse pulls before and pushes after the
-    batch — here the fleet PS program's own pull / push ops (parallel/ps)"""
+class DownpourSGD(Hogwild):
+    """parameter-server worker (downpour_worker.cc): Hogwild threads whose program pulls its
+    sparse rows / dense tables before the batch and pushes their gradients after it (the fleet PS
+    program's own pull / push ops, parallel/ps); the server applies pushes asynchronously"""
 
 
 class DownpourSGDOPT(DownpourSGD):
-    pass
+    """downpour_worker_opt.cc: the same loop (the reference variant differs in its C++ scheduling
+    of pulls only)"""
 
 
 class Section(DeviceWorker):
@@ -336,22 +353,32 @@ def _run_trainer(trainer, executor, program, dataset, scope, fetch_handler):
 
     rw = _RWLock()
 
+    # Hogwild / Downpour workers on the root scope run lock-free on parameter aliases; other
+    # workers (and non-root scopes, whose parameters are the scope's copies) keep the read / write
+    # lock between batches and updates
+    lock_free = bool(getattr(trainer.device_worker, "lock_free", False)) and not trainer.infer and \
+        getattr(scope, "_root", True)
+
     def worker(tid):
         dw = trainer.device_worker
-        _WORKER.rw = rw
+        _WORKER.rw = None if lock_free else rw
+        _WORKER.alias = lock_free
         try:
             while True:
                 batch = chan.get()
                 if batch is _END:
                     return
-                rw.acquire_read()
-                _WORKER.reading = True
-                try:
+                if lock_free:
                     out = dw.run_batch(executor, prog, batch, fetch_vars, scope)
-                finally:
-                    if _WORKER.reading:
-                        _WORKER.reading = False
-                        rw.release_read()
+                else:
+                    rw.acquire_read()
+                    _WORKER.reading = True
+                    try:
+                        out = dw.run_batch(executor, prog, batch, fetch_vars, scope)
+                    finally:
+                        if _WORKER.reading:
+                            _WORKER.reading = False
+                            rw.release_read()
                 stats["batches"][tid] += 1
                 if fetch_vars and out:
                     vals = [o.numpy() if hasattr(o, "numpy") else np.asarray(o) for o in out]
@@ -366,6 +393,7 @@ def _run_trainer(trainer, executor, program, dataset, scope, fetch_handler):
                 pass
         finally:
             _WORKER.rw = None
+            _WORKER.alias = False
 
     mon = FetchHandlerMonitor(scope, fetch_handler, latest) if fetch_handler is not None else None
     if mon is not None:

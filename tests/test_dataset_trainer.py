@@ -85,8 +85,10 @@ def test_hogwild_threads_converge(tmp_path, threads, capsys):
         assert f"over {threads} threads" in out
         assert l1 < 0.5 * l0, (l0, l1)
         _RESULTS[threads] = l1
-        if len(_RESULTS) == 2:   # 4 Hogwild threads (stale gradients) end near the single-thread loss
-            assert _RESULTS[4] < 1.4 * _RESULTS[1], _RESULTS
+        if len(_RESULTS) == 2:
+            # 4 lock-free Hogwild threads read parameters mid-update (stale gradients, as the
+            # reference's hogwild_worker): they end near, not at, the single-thread loss
+            assert _RESULTS[4] < 2.0 * _RESULTS[1], _RESULTS
     finally:
         paddle.disable_static()
 
@@ -129,3 +131,40 @@ def test_trainer_factory_picks_workers():
     assert isinstance(t, MultiTrainer) and isinstance(t.device_worker, Hogwild)
     t = TrainerFactory()._create_trainer({"trainer": "DistMultiTrainer", "device_worker": "DownpourSGD"})
     assert isinstance(t, DistMultiTrainer) and isinstance(t.device_worker, DownpourSGD)
+
+
+def test_hogwild_is_lock_free_on_parameter_aliases(tmp_path, monkeypatch):
+    """Hogwild / Downpour workers never take the batch / update read-write lock; each batch runs
+    on aliases of the parameters (same storage, separate autograd versions) and its update lands
+    in the real parameters"""
+    from paddle_hackathon_amd.static import trainer as T
+    from paddle_hackathon_amd.static import program as P
+    files = _write_files(str(tmp_path), nfiles=2, per=200)
+    seen = {"alias": 0, "same_storage": 0}
+    orig_run = P._run_program
+
+    def spy(program, blk, env, feed, fetch_list):
+        for v in env.values():
+            o = getattr(v, "_hogwild_of", None)
+            if o is not None:
+                seen["alias"] += 1
+                seen["same_storage"] += int(v._t.data_ptr() == o._t.data_ptr() and v._t is not o._t)
+        return orig_run(program, blk, env, feed, fetch_list)
+
+    def no_lock(self):
+        raise AssertionError("Hogwild worker took the read-write lock")
+    monkeypatch.setattr(P, "_run_program", spy)
+    monkeypatch.setattr(T._RWLock, "acquire_read", no_lock)
+    paddle.enable_static()
+    try:
+        main, start, slots, loss = _build()
+        exe = paddle.static.Executor()
+        exe.run(start)
+        params = [p for p in main.all_parameters()]
+        before = [p.numpy().copy() for p in params]
+        ds = _dataset(files, slots, 3)
+        exe.train_from_dataset(main, ds, thread=3)
+        assert seen["alias"] > 0 and seen["same_storage"] == seen["alias"], seen
+        assert any(not np.allclose(b, p.numpy()) for b, p in zip(before, params))   # real params updated
+    finally:
+        paddle.disable_static()
