@@ -66,12 +66,13 @@ def _args():
     ap.add_argument("--gemm-tuning-file", default=None, help="database path (default: the in-tree one)")
     ap.add_argument("--gemm-tuning-ms", type=int, default=15, help="tune: time budget per GEMM shape")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="ResNet-50: replay the whole training step (fwd + bwd + Momentum) as one hipGraph "
-                         "(paddle.device.cuda.graphs.wrap_cuda_graph). auto = on for a single rank (also with "
-                         "--force-dp) and off for multi-rank jobs: capturing the DataParallel RCCL all-reduce "
-                         "across ranks is unverified (only one GPU per test box; the gloo rehearsal cannot "
-                         "capture collectives), so multi-rank ResNet timing is eager unless --graph on, which "
-                         "builds the model and reducer on the capture stream and captures the all-reduce")
+                    help="replay the whole training step (fwd + bwd + optimizer) as one hipGraph "
+                         "(paddle.device.cuda.graphs.wrap_cuda_graph). auto: BERT on a single rank (its eager "
+                         "step is host-bound: graphed 1,242-1,275 vs eager 1,236 samples/s), ResNet-50 eager "
+                         "(eager measured ahead of the graph in every alternating pair: 9,086 / 9,077, 9,077 / "
+                         "9,012, 9,123 / 9,082 img/s); on: graph (multi-rank: builds the model and reducer on "
+                         "the capture stream and captures the RCCL all-reduce — unverified across ranks, one "
+                         "GPU per test box); off: eager")
     ap.add_argument("--force-dp", action="store_true",
                     help="ResNet-50: wrap the model in DataParallel (RCCL reducer) even on one rank — checks the "
                          "graph-captured all-reduce path on a single GPU")
@@ -260,7 +261,7 @@ def bench_bert(a, paddle, dist, world, rank):
     through the kernels' device seed word (ops/hip.dropout_seed), Adam reads lr / beta powers from
     device scalars."""
     import torch
-    cap_stream = torch.cuda.Stream() if _resnet_graphed(a, world) else torch.cuda.current_stream()
+    cap_stream = torch.cuda.Stream() if _bert_graphed(a, world) else torch.cuda.current_stream()
     with torch.cuda.stream(cap_stream):
         return _bench_bert(a, paddle, dist, world, rank, cap_stream)
 
@@ -302,7 +303,7 @@ def _bench_bert(a, paddle, dist, world, rank, cap_stream):
         opt.clear_grad(set_to_zero=False)
         return loss
 
-    graphed = _resnet_graphed(a, world)
+    graphed = _bert_graphed(a, world)
     if graphed:
         from paddle_hackathon_amd.device.cuda.graphs import wrap_cuda_graph
         step = wrap_cuda_graph(step)
@@ -320,14 +321,23 @@ def _bench_bert(a, paddle, dist, world, rank, cap_stream):
                        "final_loss": round(float(loss.item()), 4), "hip_graph": bool(graphed)}}), flush=True)
 
 
-def _resnet_graphed(a, world):
-    """whether the ResNet step is replayed as one hipGraph (see --graph)"""
+def _graphed(a, world, auto):
+    """whether a step is replayed as one hipGraph (see --graph); ``auto``: the model's default on
+    a single rank"""
     if a.warmup < 2 or a.graph == "off":
         return False
     from paddle_hackathon_amd.parallel import collective
     if world > 1 and collective.get_backend() != "nccl":
         return False   # host (gloo) collectives cannot be captured
-    return a.graph == "on" or world == 1
+    return a.graph == "on" or (auto and world == 1)
+
+
+def _resnet_graphed(a, world):
+    return _graphed(a, world, auto=False)
+
+
+def _bert_graphed(a, world):
+    return _graphed(a, world, auto=True)
 
 
 def _gpt_micro_batch(a, torch, world, rank):
