@@ -131,6 +131,13 @@ class BertLayer(nn.Layer):
 
     def forward(self, x, attn_bias=None):
         x = self._add_norm(self.attention(x, attn_bias), x, self.norm1)
+        from ..ops import mlp as _mlp
+        l1, l2 = self.linear1, self.linear2
+        if _mlp.available(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t):
+            # one autograd node: both weight gradients on the own TN kernel with the bias gradients
+            # from its B fragments, the exact-GELU backward pass without a column-sum side job
+            y = _wrap(_mlp.fused_mlp(x._t, l1.weight._t, l1.bias._t, l2.weight._t, l2.bias._t, approximate=False))
+            return self._add_norm(y, x, self.norm2)
         h = torch.matmul(x._t, self.linear1.weight._t)
         h = _ops.bias_gelu(h, self.linear1.bias._t, approximate=False)
         return self._add_norm(self.linear2(_wrap(h)), x, self.norm2)

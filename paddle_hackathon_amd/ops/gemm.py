@@ -173,7 +173,7 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
     without the bias, shaped and strided like C) from the same epilogue.
     colsum (TN only): also the column sums of B over K (a linear layer's bias gradient sum_t dY[t]),
     summed by the main loop from the B fragments it already holds; returns (C, fp32 partials
-    [2 * splits * ceil(M / 256), N]) — finish with colsum_finish."""
+    [2 * splits * ceil(M / 256) (+ 8 workspace rows), N]) — finish with colsum_rows_finish."""
     assert a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2 and b.dim() == 2
     assert a.stride(1) == 1 and b.stride(1) == 1
     M, Ka = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
@@ -198,7 +198,8 @@ def gemm_p(a, b, a_kouter=False, b_kouter=False, bias=None, out=None, trans_out=
     part = None
     if colsum:
         assert (a_kouter, b_kouter, trans_out) == (True, True, False) and gelu_aux is None
-        part = torch.empty(2 * splits * -(-M // 256), N, dtype=torch.float32, device=a.device)
+        # + 8 rows: the first-stage workspace of the two-stage column reduction (hip._col_sum_rows)
+        part = torch.empty(2 * splits * -(-M // 256) + 8, N, dtype=torch.float32, device=a.device)
         epi |= G4P_COLSUM | EPI_EARLY
         gelu_aux = part
     if group_m <= 0:
@@ -258,6 +259,15 @@ def _epi_default(a_kouter, b_kouter, trans_out, K):
 def nn_p(a, b, bias=None, **kw):
     """a [M, K] @ b [K, N] (+ bias) on the persistent kernel as (b^T a^T)^T"""
     return gemm_p(b, a, True, False, bias=bias, trans_out=True, **kw)
+
+
+def colsum_rows_finish(part, dtype):
+    """column sums of gemm_p(colsum=True)'s partials (all rows but the last 8, the workspace) on the
+    two-stage HIP column reduction: row blocks in parallel, then one pass over their sums (the
+    one-thread-per-column colsum_finish walked up to 2 x 16 x tiles rows serially on 3-12
+    workgroups: 2.2 ms per BERT step)"""
+    from . import hip as _hip
+    return _hip._col_sum_rows(part, part.shape[0] - 8, dtype)
 
 
 def colsum_finish(part, dtype):
@@ -538,7 +548,7 @@ def mm_tn_db(a, b, db_dtype=None):
         a, b = _c(a), _c(b)
         if supported(M, N, K, a, b):
             c, part = gemm_p(a, b, True, True, splits=_splits(M, N, K, a.device), colsum=True)
-            return c, colsum_finish(part, db_dtype or b.dtype)
+            return c, colsum_rows_finish(part, db_dtype or b.dtype)
     from . import hip as _hip
     return mm_tn(a, b), _hip.col_sum(b, db_dtype)
 

@@ -39,8 +39,9 @@ def _own_ok(x2d, w1, w2):
     return (G._own_ok("nn", x2d, w1, w2) and G.supported(F, M, H, w1, x2d) and G.supported(M, F, H, x2d, w2))
 
 
-def _fwd(mode, x2d, w1, b1):
-    """-> (activation, saved pre-activation); modes 0 / 2 save x W1 (bias not added), mode 1 x W1 + b1"""
+def _fwd(mode, x2d, w1, b1, approximate=True):
+    """-> (activation, saved pre-activation); modes 0 / 2 save x W1 (bias not added), mode 1 x W1 + b1.
+    approximate=False (exact erf GELU, BERT): mode 0 only (the GEMM epilogues compute tanh-GELU)"""
     if mode == 1:
         return G.nn(x2d, w1, bias=b1, act="gelu", aux_out=True)
     from .conv_gemm import weight_t
@@ -49,16 +50,16 @@ def _fwd(mode, x2d, w1, b1):
         if r is not None:
             return r
     h = G.mm_nt(x2d, weight_t(w1))
-    return _hip.bias_gelu_fwd(h, b1, True), h
+    return _hip.bias_gelu_fwd(h, b1, approximate), h
 
 
-def _bwd_gelu(mode, gy, w2, pre, b1, want_db=True):
+def _bwd_gelu(mode, gy, w2, pre, b1, want_db=True, approximate=True):
     """-> (d pre-activation, d b1 or None with want_db=False) from the MLP output gradient"""
     if mode == 1:
         g, part = G.gemm(gy, w2, False, False, act="dgelu", aux=pre, colsum=True)
         return g, G.colsum_finish(part, b1.dtype)
     ga = G.mm_nt(gy, w2)
-    return _hip.bias_gelu_bwd(ga, pre, b1, True, want_db=want_db)
+    return _hip.bias_gelu_bwd(ga, pre, b1, approximate, want_db=want_db)
 
 
 _MODES = {"pass": 0, "force": 1, "epi": 2}
@@ -83,12 +84,12 @@ _DEFAULT = "epi"
 
 class FusedMLP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2d, w1, b1, w2, b2, mode):
+    def forward(ctx, x2d, w1, b1, w2, b2, mode, approximate=True):
         from .conv_gemm import weight_t
-        a, pre = _fwd(mode, x2d, w1, b1)
+        a, pre = _fwd(mode, x2d, w1, b1, approximate)
         y = G.mm_nt(a, weight_t(w2)) if b2 is None else G.mm_nt_bias(a, weight_t(w2), b2)
         ctx.save_for_backward(x2d, w1, b1, w2, pre, a)
-        ctx.mode = mode
+        ctx.mode, ctx.approximate = mode, approximate
         return y
 
     @staticmethod
@@ -103,23 +104,24 @@ class FusedMLP(torch.autograd.Function):
         else:
             dw2, db2 = weight_grad(a, gy), None
         fused_db = ctx.mode != 1
-        g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1, want_db=not fused_db)
+        g, db1 = _bwd_gelu(ctx.mode, gy, w2, pre, b1, want_db=not fused_db, approximate=ctx.approximate)
         dx = G.mm_nt(g, w1) if ctx.needs_input_grad[0] else None
         if fused_db:
             dw1, db1 = G.mm_tn_db(x2d, g, b1.dtype)
         else:
             dw1 = weight_grad(x2d, g)
-        return dx, dw1, db1, dw2, db2, None
+        return dx, dw1, db1, dw2, db2, None, None
 
 
-def fused_mlp(x, w1, b1, w2, b2):
-    """gelu_tanh(x @ w1 + b1) @ w2 + b2 for x [..., H], w1 [H, F], w2 [F, H] (Paddle [in, out]);
+def fused_mlp(x, w1, b1, w2, b2, approximate=True):
+    """gelu(x @ w1 + b1) @ w2 + b2 for x [..., H], w1 [H, F], w2 [F, H] (Paddle [in, out]); tanh
+    GELU by default, exact (erf) with approximate=False (chain 0: GEMM + bias-GELU pass);
     b2 None: no output bias (the caller adds it, e.g. in the next add-LN kernel)"""
     x2d = x.reshape(-1, x.shape[-1])
     if not x2d.is_contiguous():
         x2d = x2d.contiguous()
-    mode = pick_mode(x2d, w1, b1, w2)
-    y = FusedMLP.apply(x2d, w1, b1, w2, b2, mode)
+    mode = pick_mode(x2d, w1, b1, w2) if approximate else 0
+    y = FusedMLP.apply(x2d, w1, b1, w2, b2, mode, bool(approximate))
     return y.reshape(list(x.shape[:-1]) + [w2.shape[1]])
 
 

@@ -25,8 +25,8 @@ def test_mm_tn_db_matches_plain_tn_and_fp32_colsum(K, M, N, dt):
     ref = G.gemm_p(x, dy, True, True, splits=sp, epi_extra=G.EPI_EARLY)
     dw, part = G.gemm_p(x, dy, True, True, splits=sp, colsum=True)
     assert torch.equal(dw, ref), "the column sums changed the product"
-    assert part.shape == (2 * sp * -(-M // 256), N)
-    db = G.colsum_finish(part, torch.float32)
+    assert part.shape == (2 * sp * -(-M // 256) + 8, N)
+    db = G.colsum_rows_finish(part, torch.float32)
     f32 = dy.float().sum(0)
     assert ((db - f32).abs().max() / f32.abs().max().clamp_min(1)).item() < 1e-5
     dw2, db2 = G.mm_tn_db(x, dy)
@@ -41,7 +41,7 @@ def test_forced_splits_and_refused_layouts():
     for sp in (1, 2, 4, 8):
         dw, part = G.gemm_p(x, dy, True, True, splits=sp, colsum=True)
         assert torch.equal(dw, G.gemm_p(x, dy, True, True, splits=sp, epi_extra=G.EPI_EARLY))
-        db = G.colsum_finish(part, torch.float32)
+        db = G.colsum_rows_finish(part, torch.float32)
         assert torch.allclose(db, dy.float().sum(0), rtol=1e-5, atol=1e-3)
     with pytest.raises(AssertionError):
         G.gemm_p(x.t().contiguous(), dy.t().contiguous(), colsum=True)   # NT: no column sums
@@ -68,14 +68,19 @@ def test_linear_and_mlp_backward_bias_grads():
         x2 = _r(2048, H, g=g).requires_grad_(True)
         w1, w2 = (_r(H, F, g=g) * 0.03).requires_grad_(True), (_r(F, H, g=g) * 0.03).requires_grad_(True)
         b1, b2 = (_r(F, g=g) * 0.1).requires_grad_(True), (_r(H, g=g) * 0.1).requires_grad_(True)
-        y2 = mlp.fused_mlp(x2, w1, b1, w2, b2)
-        gy2 = _r(2048, H, g=g)
-        y2.backward(gy2)
-        xs = [t.detach().float().requires_grad_(True) for t in (x2, w1, b1, w2, b2)]
-        h = torch.nn.functional.gelu(xs[0] @ xs[1] + xs[2], approximate="tanh")
-        (h @ xs[3] + xs[4]).backward(gy2.float())
-        for got, ref in zip((x2.grad, w1.grad, b1.grad, w2.grad, b2.grad), xs):
-            ref = ref.grad
-            assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2
+        for approx in (True, False):   # tanh GELU (GPT) and exact erf GELU (BERT, chain 0)
+            for t in (x2, w1, b1, w2, b2):
+                t.grad = None
+            y2 = mlp.fused_mlp(x2, w1, b1, w2, b2, approximate=approx)
+            gy2 = _r(2048, H, g=g)
+            y2.backward(gy2)
+            xs = [t.detach().float().requires_grad_(True) for t in (x2, w1, b1, w2, b2)]
+            h = torch.nn.functional.gelu(xs[0] @ xs[1] + xs[2], approximate="tanh" if approx else "none")
+            yr = h @ xs[3] + xs[4]
+            yr.backward(gy2.float())
+            assert ((y2.float() - yr).norm() / yr.norm()).item() < 1e-2
+            for got, ref in zip((x2.grad, w1.grad, b1.grad, w2.grad, b2.grad), xs):
+                ref = ref.grad
+                assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2, approx
     finally:
         paddle.set_device("cpu")
