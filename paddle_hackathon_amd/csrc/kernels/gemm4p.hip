@@ -61,7 +61,18 @@ enum : int {
   EPI_KSTAG_SHIFT = 25,  // bits 25-26: K-start stagger (1: per XCD, 2: per tile, 3: per slot in the XCD)
   EPI_COLSUM = 1 << 27,  // TN + EARLY: column sums of B (a linear layer's bias gradient: the sum of dY over
                          // the tokens) from the B fragments the MFMAs already hold, into aux (see CS)
+  EPI_SPREAD_SHIFT = 28, // NT + EARLY + PIN, bits 28-29: DMA placement (see sp_na / sp_gb)
 };
+
+// SPREAD (LV bits 5-6): where the 16 DMAs of the next-next K-tile go. The plain EARLY schedule
+// issues one per MFMA group over A groups 8-15 + B groups 0-7: 16 consecutive groups in which the
+// CU's four waves push 4 KiB per 64 MFMA cycles into the texture path (its 64 B / clk), and none in
+// the other 16. SPREAD puts sp_na of them over A groups RELG-15 and the rest over B groups
+// 0..sp_gb-1, so the same bytes go out at up to half the rate (less issue back-pressure on the
+// MFMA stream), at the price of less latency cover for the last ones (>= 16 groups instead of 24).
+constexpr int sp_mode(int lv) { return (lv >> 5) & 3; }
+constexpr int sp_na(int lv, int relg) { return sp_mode(lv) == 3 ? 6 : sp_mode(lv) ? 8 : 16 - relg; }
+constexpr int sp_gb(int lv, int relg) { return sp_mode(lv) == 2 ? 12 : sp_mode(lv) ? 16 : relg; }
 
 // late-wait variants (LV): {LWG = phase-B group of the buffer wait (0: at the A/B boundary),
 // LDMA = DMAs of the next-next K-tile issued in phase A (groups RELG-15), the rest in phase B}
@@ -501,6 +512,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr bool WSTAG = lv_wstag(LV);
   unsigned long long sp_t = 0, sp_ab = 0, sp_rel = 0, sp_n = 0;
   constexpr int LRG = lv_rg(LV, RELG);
+  constexpr int SPM = sp_mode(LV), SNA = sp_na(LV, RELG), SGB = sp_gb(LV, RELG);
+  static_assert(SPM == 0 || (LWG == 0 && !WSTAG && !AKO && !BKO), "SPREAD: NT early schedule only");
   static_assert(LWG == 0 || (LDMB <= LWG && RELG == 8), "late variants: every phase-B DMA before the wait");
 
   // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
@@ -615,6 +628,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int d = (s - RELG) * LDMA / (16 - RELG); d < (s - RELG + 1) * LDMA / (16 - RELG); ++d) stage_one(d);
           }
+        } else if constexpr (SPM != 0) {
+          if (s >= RELG) {
+#pragma unroll
+            for (int d = (s - RELG) * SNA / (16 - RELG); d < (s - RELG + 1) * SNA / (16 - RELG); ++d) stage_one(d);
+          }
         } else if (s >= RELG) {
           if constexpr (WSTAG) dq = s - RELG;
           else stage_one(s - RELG);
@@ -666,7 +684,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             else na[r - 8] = readA(rbuf, rkh, r - 8);
           }
         }
-        if (s < RELG) {
+        if constexpr (SPM != 0) {
+          if (s < SGB) {
+#pragma unroll
+            for (int d = SNA + s * (16 - SNA) / SGB; d < SNA + (s + 1) * (16 - SNA) / SGB; ++d) stage_one(d);
+          }
+        } else if (s < RELG) {
           if constexpr (WSTAG) dq = 16 - RELG + s;
           else stage_one(16 - RELG + s);
         }
@@ -754,7 +777,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // VMEM ops younger than the previous K-tile's DMAs at the A/B boundary: phase A's 12 DMAs, plus
     // an epilogue phase's stores (capped at the counter's 63)
     constexpr int NSTE = (SPLIT || GELU) ? 64 : 32;
-    constexpr int VB2 = 16 - RELG + NSTE > 63 ? 63 : 16 - RELG + NSTE;
+    constexpr int VB2 = SNA + NSTE > 63 ? 63 : SNA + NSTE;
     // LATE: the wait sits in phase B after all 16 DMAs of the next-next K-tile (+ the stores)
     constexpr int VL2 = 16 + NSTE > 63 ? 63 : 16 + NSTE;
     using VW1 = std::integral_constant<int, LWG ? 16 : 0>;
@@ -800,7 +823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         phaseE(M0{}, yes{}, VW1{}, fa0, fb0, fa1, fb1, buf, 1, buf, cs_c, sel(k, 0));
         if constexpr (LWG == 0) {
           if constexpr (STAMP) sp_t = __builtin_amdgcn_s_memtime();
-          asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(16 - RELG) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" :: "n"(SNA) : "memory");
           __builtin_amdgcn_sched_barrier(0);
           bar();
           if constexpr (STAMP) {
@@ -1523,8 +1546,14 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
   else if (a.epi & EPI_GELU)
     return (int)hipErrorInvalidValue;
   else if (!ako && !bko && !trans) {
-    const int lv = E && std::is_same<T, bf16_t>::value ? ((a.epi >> EPI_LATE_SHIFT) & 15) | ((a.epi & EPI_WSTAG) ? 16 : 0) : 0;
-    if (lv == 8) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 8>), dim3(grid), dim3(256), 0, st, a);
+    const int lv = E && std::is_same<T, bf16_t>::value
+                       ? ((a.epi >> EPI_LATE_SHIFT) & 15) | ((a.epi & EPI_WSTAG) ? 16 : 0) | (((a.epi >> EPI_SPREAD_SHIFT) & 3) << 5)
+                       : 0;
+    if (lv == 40) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 40>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 72) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 72>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 104) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 104>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 47 && a.ws) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 47>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 8)hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 8>), dim3(grid), dim3(256), 0, st, a);
     else if (lv == 10) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 10>), dim3(grid), dim3(256), 0, st, a);
     else if (lv == 11) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 11>), dim3(grid), dim3(256), 0, st, a);
     else if (lv == 13) hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E, 13>), dim3(grid), dim3(256), 0, st, a);

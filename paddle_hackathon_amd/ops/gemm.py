@@ -31,6 +31,7 @@ EPI_RING = 1 << 22   # gemm4p NT: 4-slot ring of 32-deep stages (gemm4r_kernel; 
 EPI_ADEEP = 1 << 23  # gemm4p NT, no bias / GELU: 3 A + 2 B LDS slots (gemm4a_kernel; K >= 256)
 EPI_WSTAG = 1 << 24  # gemm4p NT + EARLY: wave w issues its LDS-DMA after MFMA w of a group
 G4P_COLSUM = 1 << 27  # gemm4p TN + EARLY: column sums of B (bias gradient) from the MFMA B fragments
+G4P_SPREAD_SHIFT = 28  # gemm4p NT + EARLY, bits 28-29: LDS-DMA placement over 24-28 MFMA groups
 _DT = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}
 
 
@@ -233,6 +234,12 @@ def gemm_8w(a, bt, bias=None, out=None, epi_extra=0, group_m=0):
     return c
 
 
+def _lv_bits(lv):
+    """gemm4p NT schedule variant LV -> epilogue flag bits: LV & 15 at bit 17 (late-wait / PIN /
+    stamp), LV & 16 = EPI_WSTAG, (LV >> 5) & 3 at bit 28 (SPREAD DMA placement, gemm4p.hip sp_na)"""
+    return ((lv & 15) << 17) | (EPI_WSTAG if lv & 16 else 0) | (((lv >> 5) & 3) << G4P_SPREAD_SHIFT)
+
+
 def _epi_default(a_kouter, b_kouter, trans_out, K):
     """gemm4p main-loop schedule (bitwise-identical results either way): the early-release schedule
     on every layout — phase A's fragment reads in a burst over 8 MFMA groups, the LDS buffer
@@ -245,11 +252,13 @@ def _epi_default(a_kouter, b_kouter, trans_out, K):
     if not (a_kouter or b_kouter or trans_out):
         # NT: PIN variant (LV 8 — an empty memory asm closes every MFMA group so no IR pass sinks
         # a group's LDS reads past the loop latch): 1-3 % over LV 0 on every GPT NT shape in bursts,
-        # bitwise identical (profiles/g4p_late_ab_r5.log); PHA_G4P_LV overrides. Long-K products
+        # bitwise identical (profiles/g4p_late_ab_r5.log), plus SPREAD (LV 40: the next-next K-tile's
+        # DMAs over 24 MFMA groups instead of 16): 1-3 % on long K, level at K = 2048, +0.2 % on the
+        # library-free GPT step (profiles/g4p_spread_r6/); PHA_G4P_LV overrides. Long-K products
         # without an epilogue take the A-deep build (3 A + 2 B LDS slots, ~2 K-tiles of cover for the
         # streamed activation panel): 2.5-3 % faster at K >= 6144 under sustained load, bitwise
         # equal (profiles/g4p_adeep_sustain_r5.log); the kernel picks it only without bias / GELU
-        lv = int(os.environ.get("PHA_G4P_LV", "8")) << 17
+        lv = _lv_bits(int(os.environ.get("PHA_G4P_LV", "40")))
         if K >= 4096 and os.environ.get("PHA_G4P_ADEEP", "1") != "0":
             return EPI_EARLY | lv | EPI_ADEEP
         return EPI_EARLY | lv

@@ -60,3 +60,22 @@ def test_adeep_bitwise_equals_two_buffer_kernel(M, N, K, monkeypatch):
     ref = G.gemm_p(a, bt, epi_extra=G.EPI_EARLY)
     got = G.gemm_p(a, bt, epi_extra=G.EPI_EARLY | G.EPI_ADEEP)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("lv", [40, 72, 104])
+@pytest.mark.parametrize("M,N,K,bias", [(4096, 2048, 1024, True), (1000, 2056, 640, False), (520, 776, 4096, True),
+                                        (2048, 6144, 128, True)])
+def test_spread_dma_placement_bitwise(lv, M, N, K, bias, monkeypatch):
+    """SPREAD (gemm4p.hip sp_na / sp_gb: the next-next K-tile's DMAs over 24-28 MFMA groups) only
+    moves LDS-DMA issue points: bitwise equal to the shipped LV 8 schedule, incl. the first K-tile's
+    counted wait with the previous tile's stores in flight"""
+    from paddle_hackathon_amd.ops import gemm as G
+    monkeypatch.setenv("PHA_G4P_ADEEP", "0")
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + lv)
+    a, bt = _r(M, K, g=g), _r(N, K, g=g)
+    b = torch.randn(N, device="cuda", generator=g) if bias else None
+    monkeypatch.setenv("PHA_G4P_LV", "8")
+    ref = G.gemm_p(a, bt, bias=b)
+    monkeypatch.setenv("PHA_G4P_LV", str(lv))
+    got = G.gemm_p(a, bt, bias=b)
+    assert torch.equal(got, ref)
