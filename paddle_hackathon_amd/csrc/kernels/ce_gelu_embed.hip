@@ -15,25 +15,48 @@ using namespace pha;
 
 namespace {
 
-template <typename T>
+// VEC: V % 8 == 0 (16-B row loads); else one element per lane-iteration (vocabularies like
+// BERT's 30522: the rows are not 16-B aligned, and the fp32 torch fallback cost ~0.6 ms per step)
+template <typename T, bool VEC = true>
 __global__ __launch_bounds__(256) void softmax_ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                              float* __restrict__ loss, float* __restrict__ lse_out,
                                                              int V, int ignore_index) {
   const long row = blockIdx.x;
   const T* xr = logits + row * (long)V;
   float m = -INFINITY, s = 0.f;
-  for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
-    float v[8];
-    Vec8<T>::ld(xr + c, v);
-    float vm = v[0];
+  if constexpr (VEC) {
+    for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
+      float v[8];
+      Vec8<T>::ld(xr + c, v);
+      float vm = v[0];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) vm = fmaxf(vm, v[i]);
-    const float nm = fmaxf(m, vm);
-    float acc = s * __expf(m - nm);
+      for (int i = 1; i < 8; ++i) vm = fmaxf(vm, v[i]);
+      const float nm = fmaxf(m, vm);
+      float acc = s * __expf(m - nm);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc += __expf(v[i] - nm);
-    m = nm;
-    s = acc;
+      for (int i = 0; i < 8; ++i) acc += __expf(v[i] - nm);
+      m = nm;
+      s = acc;
+    }
+  } else {
+    for (int c0 = 0; c0 < V; c0 += 256 * 8) {   // 8 strided elements per thread, then one update
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = c0 + i * 256 + (int)threadIdx.x;
+        v[i] = c < V ? Cvt<T>::ld(xr, c) : -INFINITY;
+      }
+      float vm = v[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) vm = fmaxf(vm, v[i]);
+      const float nm = fmaxf(m, vm);
+      if (nm == -INFINITY) continue;
+      float acc = s * __expf(m - nm);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += __expf(v[i] - nm);
+      m = nm;
+      s = acc;
+    }
   }
   // merge (m, s) pairs across the wave, then across waves
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -65,7 +88,7 @@ __global__ __launch_bounds__(256) void softmax_ce_fwd_kernel(const T* __restrict
   }
 }
 
-template <typename T>
+template <typename T, bool VEC = true>
 __global__ __launch_bounds__(256) void softmax_ce_bwd_kernel(const float* __restrict__ gloss, const T* __restrict__ logits,
                                                              const int64_t* __restrict__ labels, const float* __restrict__ lse,
                                                              T* __restrict__ dx, int V, int ignore_index) {
@@ -76,6 +99,13 @@ __global__ __launch_bounds__(256) void softmax_ce_bwd_kernel(const float* __rest
   const float l = lse[row];
   const T* xr = logits + row * (long)V;
   T* dr = dx + row * (long)V;
+  if constexpr (!VEC) {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      const float p = __expf(Cvt<T>::ld(xr, c) - l);
+      Cvt<T>::st(dr, c, g * (p - (c == lab ? 1.f : 0.f)));
+    }
+    return;
+  }
   for (int c = threadIdx.x * 8; c < V; c += 256 * 8) {
     float v[8], o[8];
     Vec8<T>::ld(xr + c, v);
@@ -494,18 +524,24 @@ inline int grid_for(long n, int per_block) {
 
 PHA_API int pha_softmax_ce_fwd(int dt, const void* logits, const int64_t* labels, float* loss, float* lse,
                                long rows, int V, int ignore_index, hipStream_t stream) {
-  if (V % 8) return (int)hipErrorInvalidValue;
+  if (V <= 0) return (int)hipErrorInvalidValue;
   PHA_DISPATCH_T(dt, T, {
-    hipLaunchKernelGGL((softmax_ce_fwd_kernel<T>), dim3(rows), dim3(256), 0, stream, (const T*)logits, labels, loss, lse, V, ignore_index);
+    if (V % 8 == 0)
+      hipLaunchKernelGGL((softmax_ce_fwd_kernel<T, true>), dim3(rows), dim3(256), 0, stream, (const T*)logits, labels, loss, lse, V, ignore_index);
+    else
+      hipLaunchKernelGGL((softmax_ce_fwd_kernel<T, false>), dim3(rows), dim3(256), 0, stream, (const T*)logits, labels, loss, lse, V, ignore_index);
   });
   return (int)hipGetLastError();
 }
 
 PHA_API int pha_softmax_ce_bwd(int dt, const float* gloss, const void* logits, const int64_t* labels, const float* lse,
                                void* dx, long rows, int V, int ignore_index, hipStream_t stream) {
-  if (V % 8) return (int)hipErrorInvalidValue;
+  if (V <= 0) return (int)hipErrorInvalidValue;
   PHA_DISPATCH_T(dt, T, {
-    hipLaunchKernelGGL((softmax_ce_bwd_kernel<T>), dim3(rows), dim3(256), 0, stream, gloss, (const T*)logits, labels, lse, (T*)dx, V, ignore_index);
+    if (V % 8 == 0)
+      hipLaunchKernelGGL((softmax_ce_bwd_kernel<T, true>), dim3(rows), dim3(256), 0, stream, gloss, (const T*)logits, labels, lse, (T*)dx, V, ignore_index);
+    else
+      hipLaunchKernelGGL((softmax_ce_bwd_kernel<T, false>), dim3(rows), dim3(256), 0, stream, gloss, (const T*)logits, labels, lse, (T*)dx, V, ignore_index);
   });
   return (int)hipGetLastError();
 }

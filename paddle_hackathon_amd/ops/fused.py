@@ -246,7 +246,7 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
     V = logits.shape[-1]
     l2 = logits.reshape(-1, V)
     lab = labels.reshape(-1)
-    if _use_hip(logits) and logits.dtype in (torch.bfloat16, torch.float32, torch.float16) and V % 8 == 0:
+    if _use_hip(logits) and logits.dtype in (torch.bfloat16, torch.float32, torch.float16) and V > 0:
         if not l2.is_contiguous():
             l2 = l2.contiguous()
         loss = _SoftmaxCE.apply(l2, lab.to(torch.int64).contiguous(), int(ignore_index))

@@ -433,26 +433,27 @@ def _lib_call(layout, name, shape, fn):
 
 
 def _splits(M, N, K, dev):
-    """split-K factor for a weight gradient: the smallest power of two (<= 16, dividing the K-tiles)
-    whose work items fill the chip's rounds to >= 95 % (tiles x splits over whole multiples of the
-    CU count: GPT-1.3B's qkv dW has 192 tiles — split 2 would run 384 items in two rounds, 75 %
-    busy; split 4 runs 768 in three full rounds); grids of >= 2 rounds already stay unsplit, and so
-    do grids of >= 3/4 of a round: the qkv dW's 192 tiles unsplit beat split 4 (714 vs 739 us
-    sustained, profiles/tn_wgrad_r5/tn_sustain.log — the slabs' fp32 traffic and the reduce cost
-    more than the idle quarter)"""
+    """split-K factor for a weight gradient: grids of >= 2 rounds stay unsplit, and so do grids of
+    >= 3/4 of a round (the qkv dW's 192 tiles unsplit beat split 4: 714 vs 739 us sustained,
+    profiles/tn_wgrad_r5/tn_sustain.log). Below that, the power of two (<= 16, dividing the K-tiles,
+    >= 4 K-tiles per item) with the least modelled time: rounds of work items x K-tiles per item x
+    0.76 us (one K-tile of a 256 x 256 tile) + splits x tiles x 0.12 us (each item's fp32 slab written
+    and read back by the in-order reduce). Filling every CU is not the goal: BERT-base's fc1 / fc2
+    dW (36 tiles, 256 K-tiles) run 116 us at split 4 (144 items on 256 CUs) vs 164 us at the old
+    fill-the-rounds pick of 16, qkv dW 89.5 (split 8) vs 122 us (profiles/bert_tn_ab_r6.log)."""
     tiles = -(-M // 256) * -(-N // 256)
     cus = _num_cus(dev)
     ktiles = K // 64
-
-    def eff(sp):
-        items = tiles * sp
-        return items / (-(-items // cus) * cus)
     if tiles >= 2 * cus or 4 * tiles >= 3 * cus:
         return 1
+    best, best_t = 1, None
     sp = 1
-    while (tiles * sp < cus or eff(sp) < 0.95) and sp < 16 and ktiles % (sp * 2) == 0 and ktiles // (sp * 2) >= 4:
+    while sp <= 16 and ktiles % sp == 0 and ktiles // sp >= 4:
+        t = -(-tiles * sp // cus) * (ktiles // sp) * 0.76 + (sp > 1) * sp * tiles * 0.12
+        if best_t is None or t < best_t:
+            best, best_t = sp, t
         sp *= 2
-    return sp
+    return best
 
 
 def _pad2(t, rm, cm):

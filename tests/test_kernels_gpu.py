@@ -163,7 +163,7 @@ def test_softmax(dt, H):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("V", [512, 50304, 32000])
+@pytest.mark.parametrize("V", [512, 50304, 32000, 30522, 7])   # 30522 / 7: the element-wise (V % 8 != 0) path
 def test_softmax_cross_entropy(dt, V):
     from paddle_hackathon_amd import ops
     rows = 67
