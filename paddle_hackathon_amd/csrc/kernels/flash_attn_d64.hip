@@ -1,0 +1,649 @@
+// Flash attention for head dim 64 (BERT-base / -large, ViT, GPT-2-sized models) on gfx950, with the
+// in-kernel dropout of the probabilities and packed-QKV strides. Reference behaviour:
+// paddle/fluid/operators/fused/fmha_ref.h:87-172 (softmax(Q K^T / sqrt(d)) with dropout, then P V)
+// and its backward in fused_attention_op.cu; the dropout mask is the counter hash of fa_common.h
+// (seed, b*H + h, query, key), so these kernels and the generic 4-wave ones regenerate the same mask.
+//
+// Why separate kernels. The generic 4-wave kernels (flash_attn.hip fa_*_kernel<T, 64, ..>) stage
+// K / V through registers with a software transpose of V (u16 shuffles per element), take two
+// barriers per tile and work on 32-query tiles in the dK/dV kernel: 262 TF/s forward, ~200 TF/s
+// backward at the BERT shape (profiles/fa_bert_time.log). Here, as in the D = 128 v3 kernels:
+//  * 8 waves x 32 rows per workgroup, tiles by LDS-DMA (global_load_lds_dwordx4, 1-KiB pieces of 8
+//    rows), one barrier per tile, the next tile in flight during the current one;
+//  * ONE 128-B-row image layout for every operand, read both by rows (ds_read_b128, the MFMA A
+//    operand of Q K^T / K Q^T / dO V^T) and transposed (ds_read_b64_tr_b16: V^T for P V, dO^T / Q^T
+//    for dV / dK, K^T for dQ). 16-B chunk c of row r sits at chunk c ^ f(r),
+//    f(r) = ((r >> 1) & 1) << 2 | ((r >> 2) & 3): the 32 rows of a b128 fragment read (lane groups
+//    {0-3,12-15,20-27} / {4-11,16-19,28-31}) land on 16 distinct 16-B slots per bank row, and the
+//    4 rows x 64 B of a transposed read fill all 64 banks;
+//  * swapped products with the accumulators as the next MFMA's B operand (P^T / dS^T / P / dS never
+//    touch LDS); masks as -inf initial accumulators; row constants (-lse / scale, -delta) as the
+//    initial accumulators of the dK/dV kernel's S / dP chains (CDNA guide App. B).
+#include "fa_common.h"
+
+namespace {
+
+constexpr int IMG64 = 64 * 128;   // one 64-row x 64-element operand image (8 KiB)
+
+__device__ __forceinline__ int f64(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+
+__device__ __forceinline__ void glds64(unsigned voff, const void* sbase, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+               :: "v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+
+// 1-KiB piece p (rows 8p .. 8p+7) of the 64-row tile starting at row r0 of an operand with row
+// stride rs (elements): lane L writes physical chunk L & 7 of row 8p + (L >> 3), so it fetches the
+// logical chunk (L & 7) ^ f(row). Rows past rmax read row rmax (finite; masked by the caller).
+template <typename T>
+__device__ __forceinline__ void dma64(const T* base, long rs, int r0, int rmax, int p, int lane, unsigned lds) {
+  const int row = 8 * p + (lane >> 3);
+  const int lch = (lane & 7) ^ f64(row);
+  const unsigned voff = (unsigned)(((long)(min(r0 + row, rmax) - r0) * rs + lch * 8) * 2);
+  glds64(voff, base + (long)r0 * rs, __builtin_amdgcn_readfirstlane(lds + p * 1024));
+}
+
+__device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
+  return (unsigned)(size_t)(__attribute__((address_space(3))) const unsigned char*)p;
+}
+
+// per-lane offsets of the transposed reads (rows 16 ks + 4h + tq (+8), 32-column block db): the
+// A operand of an O^T / dV^T / dK^T / dQ^T product; + ks * 2048 (+ 4096 per 32-row half)
+__device__ __forceinline__ void tr_offsets(int lane, int (&troff)[2][2]) {
+  const int h = lane >> 5, g = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int f = (((tq >> 1) & 1) << 2) | ((h + 2 * hi) & 3);
+      troff[db][hi] = (4 * h + tq + 8 * hi) * 128 + 16 * ((4 * db + 2 * (g & 1) + (tp >> 1)) ^ f) + 8 * (tp & 1);
+    }
+}
+
+__device__ __forceinline__ u32x4 trA(const unsigned char* img, const int (&troff)[2][2], int db) {
+  const u32x2 lo = ds_read_tr16(img + troff[db][0]);
+  const u32x2 hi = ds_read_tr16(img + troff[db][1]);
+  return u32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// ============================================================================================
+// forward: workgroup = 8 waves = 256 queries of one (batch, head), query on the MFMA lane;
+// per 64-key tile S^T = K Q^T (2 x 4 MFMAs), online softmax (deferred rescale), dropout on P for
+// the P V product only (the row sum is undropped), O^T += V^T P^T (4 x 2 MFMAs)
+// ============================================================================================
+template <typename T, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T* __restrict__ K,
+                                                const T* __restrict__ V, T* __restrict__ O, float* __restrict__ LSE,
+                                                int S, int Sk, int H, int Hk, float scale_log2, FaStrides fs, FaExt ex) {
+  typedef typename MF<T>::frag frag;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * IMG64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, lr = lane & 31;
+  const int nqb = (S + 255) >> 8;
+  const int bh = blockIdx.y, rank = blockIdx.x;
+  const int qb = CAUSAL ? nqb - 1 - rank : rank;
+  const int head = bh % H, b = bh / H, hk = head / (H / Hk);
+  const int q0 = qb * 256, wq0 = q0 + wid * 32, q = wq0 + lr;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* Kb = K + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+
+  frag qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    u32x4 v = {0, 0, 0, 0};
+    if (q < S) v = *reinterpret_cast<const u32x4*>(Qb + (long)q * fs.q_tok + 16 * kk + 8 * h);
+    qf[kk] = as_frag<frag>(v);
+  }
+  unsigned drow = 0;
+  if constexpr (DROP) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
+  f32x16 o[2];
+  o[0] = zero16();
+  o[1] = zero16();
+  float m_run = -INFINITY, l_run = 0.f;
+  const int kend = CAUSAL ? min(Sk, q0 + 256) : Sk;
+  const int ntile = (kend + 63) >> 6;
+
+  const unsigned lds0 = lds_addr(smem);
+  auto load_tile = [&](int k0, int buf) {   // 16 pieces (K 0-7, V 8-15), two per wave
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gidx = wid * 2 + u, which = gidx >> 3;
+      dma64(which ? Vb : Kb, fs.kv_tok, k0, Sk - 1, gidx & 7, lane, lds0 + buf * 2 * IMG64 + which * IMG64);
+    }
+  };
+  int koff[4], troff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) koff[kk] = lr * 128 + 16 * ((2 * kk + h) ^ f64(lr));
+  tr_offsets(lane, troff);
+
+  if (ntile > 0) {
+    load_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * 64, cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + 64, cur ^ 1);
+    const unsigned char* kl = smem + cur * 2 * IMG64;
+    const unsigned char* vl = kl + IMG64;
+    if (!(CAUSAL && k0 > wq0 + 31)) {
+      f32x16 s[2];
+      s[0] = zero16();
+      s[1] = zero16();
+      if ((k0 + 64 > Sk) || (CAUSAL && k0 + 63 > wq0)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int base = k0 + kb * 32 + 4 * h;
+          const int lim1 = CAUSAL ? q - base : 1 << 20, lim2 = Sk - base;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rb = (r & 3) + 8 * (r >> 2);
+            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const u32x4 a = *reinterpret_cast<const u32x4*>(kl + kb * 4096 + koff[kk]);
+          s[kb] = MF<T>::mma(as_frag<frag>(a), qf[kk], s[kb]);
+        }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, s[kb][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;
+      constexpr float kThr = 8.f;
+      if (!__all(tmax <= m_run + kThr)) {
+        const float m_new = fmaxf(m_run, tmax);
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const float alpha = fexp2(m_run - m_use);
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        m_run = m_new;
+      }
+      const float m_use = (m_run == -INFINITY) ? 0.f : m_run;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(s[kb][r], scale_log2, -m_use));
+          s[kb][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 32, 64);
+      l_run += psum;
+      if constexpr (DROP) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + acc_row(r, h);
+            s[kb][r] = fa_keep(drow, key, ex.thresh) ? s[kb][r] * ex.keep_scale : 0.f;
+          }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f32x16& sv = s[ks >> 1];
+        const int s8 = (ks & 1) * 8;
+        u32x4 pw;
+        pw[0] = MF<T>::pack(sv[s8 + 0], sv[s8 + 1]);
+        pw[1] = MF<T>::pack(sv[s8 + 2], sv[s8 + 3]);
+        pw[2] = MF<T>::pack(sv[s8 + 4], sv[s8 + 5]);
+        pw[3] = MF<T>::pack(sv[s8 + 6], sv[s8 + 7]);
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+          o[db] = MF<T>::mma(as_frag<frag>(trA(vl + ks * 2048, troff, db)), as_frag<frag>(pw), o[db]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMA'd tile has landed (asm: untracked)
+    __syncthreads();
+  }
+  if (q < S) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    T* orow = O + ((long)b * S + q) * fs.o_tok + (long)head * fs.o_head;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(o[db][4 * gg + 0] * inv, o[db][4 * gg + 1] * inv);
+        w[1] = MF<T>::pack(o[db][4 * gg + 2] * inv, o[db][4 * gg + 3] * inv);
+        *reinterpret_cast<u32x2*>(orow + d) = w;
+      }
+    if (h == 0) LSE[(long)bh * S + q] = (l_run > 0.f) ? (m_run + log2f(l_run)) * kLn2 : INFINITY;
+  }
+}
+
+// ============================================================================================
+// dQ: the forward's geometry (query on the lane, 256 queries per workgroup); per 64-key tile
+//   S^T = K Q^T, dP^T = V dO^T (row reads of the K / V images; Q / dO fragments in registers),
+//   P^T = exp2(c S^T - lse), dS^T = P^T (Z dP^T / (1 - rate) - delta), dQ^T += K^T dS^T (transposed
+//   reads of the K image, dS^T packed as the B operand)
+// ============================================================================================
+template <typename T, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T* __restrict__ K,
+                                               const T* __restrict__ V, const T* __restrict__ dO,
+                                               const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                               T* __restrict__ dQ, int S, int Sk, int H, int Hk, float scale,
+                                               FaStrides fs, FaExt ex) {
+  typedef typename MF<T>::frag frag;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * IMG64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, lr = lane & 31;
+  const int nqb = (S + 255) >> 8;
+  const int bh = blockIdx.y, rank = blockIdx.x;
+  const int qb = CAUSAL ? nqb - 1 - rank : rank;
+  const int head = bh % H, b = bh / H, hk = head / (H / Hk);
+  const int q0 = qb * 256, wq0 = q0 + wid * 32, q = wq0 + lr;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+  const int qc = min(q, S - 1);
+  frag qf[4], gf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    qf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Qb + (long)qc * fs.q_tok + 16 * kk + 8 * h));
+    gf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(dOb + (long)qc * fs.o_tok + 16 * kk + 8 * h));
+  }
+  const float c2 = scale * kLog2e;
+  const float nl = -LSE[(long)bh * S + qc] * kLog2e, del = DELTA[(long)bh * S + qc];
+  unsigned drow = 0;
+  if constexpr (DROP) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
+  f32x16 dqt[2];
+  dqt[0] = zero16();
+  dqt[1] = zero16();
+  const int kend = CAUSAL ? min(Sk, q0 + 256) : Sk;
+  const int ntile = (kend + 63) >> 6;
+  const unsigned lds0 = lds_addr(smem);
+  auto load_tile = [&](int k0, int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gidx = wid * 2 + u, which = gidx >> 3;
+      dma64(which ? Vb : Kb, fs.kv_tok, k0, Sk - 1, gidx & 7, lane, lds0 + buf * 2 * IMG64 + which * IMG64);
+    }
+  };
+  int koff[4], troff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) koff[kk] = lr * 128 + 16 * ((2 * kk + h) ^ f64(lr));
+  tr_offsets(lane, troff);
+
+  if (ntile > 0) {
+    load_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = t * 64, cur = t & 1;
+    if (t + 1 < ntile) load_tile(k0 + 64, cur ^ 1);
+    const unsigned char* kl = smem + cur * 2 * IMG64;
+    const unsigned char* vl = kl + IMG64;
+    if (!(CAUSAL && k0 > wq0 + 31)) {
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        dp[kb] = zero16();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+      }
+      if ((k0 + 64 > Sk) || (CAUSAL && k0 + 63 > wq0)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const int base = k0 + kb * 32 + 4 * h;
+          const int lim1 = CAUSAL ? q - base : 1 << 20, lim2 = Sk - base;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rb = (r & 3) + 8 * (r >> 2);
+            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const u32x4 ka = *reinterpret_cast<const u32x4*>(kl + kb * 4096 + koff[kk]);
+          const u32x4 va = *reinterpret_cast<const u32x4*>(vl + kb * 4096 + koff[kk]);
+          s[kb] = MF<T>::mma(as_frag<frag>(ka), qf[kk], s[kb]);
+          dp[kb] = MF<T>::mma(as_frag<frag>(va), gf[kk], dp[kb]);
+        }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(s[kb][r], c2, nl));
+          float g = dp[kb][r];
+          if constexpr (DROP) {
+            const int key = k0 + kb * 32 + acc_row(r, h);
+            g = fa_keep(drow, key, ex.thresh) ? g * ex.keep_scale : 0.f;
+          }
+          s[kb][r] = p * (g - del);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f32x16& sv = s[ks >> 1];
+        const int s8 = (ks & 1) * 8;
+        u32x4 w;
+        w[0] = MF<T>::pack(sv[s8 + 0], sv[s8 + 1]);
+        w[1] = MF<T>::pack(sv[s8 + 2], sv[s8 + 3]);
+        w[2] = MF<T>::pack(sv[s8 + 4], sv[s8 + 5]);
+        w[3] = MF<T>::pack(sv[s8 + 6], sv[s8 + 7]);
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+          dqt[db] = MF<T>::mma(as_frag<frag>(trA(kl + ks * 2048, troff, db)), as_frag<frag>(w), dqt[db]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (q < S) {
+    const long gt = ex.gq_tok ? ex.gq_tok : (long)H * 64;
+    const long gh = ex.gq_head ? ex.gq_head : 64;
+    T* row = dQ + ((long)b * S + q) * gt + (long)head * gh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 w;
+        w[0] = MF<T>::pack(dqt[db][4 * gg + 0] * scale, dqt[db][4 * gg + 1] * scale);
+        w[1] = MF<T>::pack(dqt[db][4 * gg + 2] * scale, dqt[db][4 * gg + 3] * scale);
+        *reinterpret_cast<u32x2*>(row + d) = w;
+      }
+  }
+}
+
+// ============================================================================================
+// dK / dV: workgroup = 8 waves = 256 keys, key on the MFMA lane, K / V fragments and dK^T / dV^T
+// in registers; per 64-query tile (Q, dO images by LDS-DMA; -lse/scale, -delta and the dropout
+// row seeds staged in LDS with it), two 32-query halves:
+//   S = Q K^T (from -lse/scale), dP = dO V^T (from -delta, or 0 with dropout), p = exp2(c S),
+//   dV^T += dO^T (Z p / (1 - rate)), dK^T += Q^T (p (Z dP / (1 - rate) - delta))
+// ============================================================================================
+constexpr int RC64 = 3 * 64 * 4;   // -lse/scale, -delta, row seeds of one tile
+
+template <typename T, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const T* __restrict__ K,
+                                                 const T* __restrict__ V, const T* __restrict__ dO,
+                                                 const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                 T* __restrict__ dK, T* __restrict__ dV, int S, int Sk, int H, int Hk,
+                                                 float scale, FaStrides fs, FaExt ex) {
+  typedef typename MF<T>::frag frag;
+  constexpr int BUF = 2 * IMG64 + RC64;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, lr = lane & 31;
+  const int bh = blockIdx.y;
+  const int head = bh % H, b = bh / H, hk = head / (H / Hk);
+  const int k0 = blockIdx.x * 256, wk0 = k0 + wid * 32, key = wk0 + lr;
+  const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
+  const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
+  const T* Kb = K + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+  const T* Vb = V + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
+  const float* lse_b = LSE + (long)bh * S;
+  const float* del_b = DELTA + (long)bh * S;
+  const float c2 = scale * kLog2e, nis = -1.f / scale;
+  unsigned dstream = 0;
+  if constexpr (DROP) dstream = fa_stream(fa_seed(ex), b * H + head);
+
+  const int keyc = min(key, Sk - 1);
+  frag kf[4], vf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    kf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Kb + (long)keyc * fs.kv_tok + 16 * kk + 8 * h));
+    vf[kk] = as_frag<frag>(*reinterpret_cast<const u32x4*>(Vb + (long)keyc * fs.kv_tok + 16 * kk + 8 * h));
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) through the builtin (see flash_attn.hip dK/dV v2)
+  f32x16 dvt[2], dkt[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dvt[i] = zero16(); dkt[i] = zero16(); }
+
+  const unsigned lds0 = lds_addr(smem);
+  float rcv = 0.f;
+  unsigned rseed = 0;
+  auto load_tile = [&](int qt, int buf) {   // 16 pieces (Q 0-7, dO 8-15) + the row constants
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int gidx = wid * 2 + u, which = gidx >> 3;
+      if (which) dma64(dOb, fs.o_tok, qt, S - 1, gidx & 7, lane, lds0 + buf * BUF + IMG64);
+      else dma64(Qb, fs.q_tok, qt, S - 1, gidx & 7, lane, lds0 + buf * BUF);
+    }
+    if (tid < 128) rcv = (tid < 64 ? lse_b : del_b)[min(qt + (tid & 63), S - 1)];
+    if constexpr (DROP) {
+      if (tid >= 128 && tid < 192) rseed = fa_row(dstream, qt + (tid & 63));
+    }
+  };
+  auto store_rc = [&](int buf) {
+    float* rc = reinterpret_cast<float*>(smem + buf * BUF + 2 * IMG64);
+    if (tid < 128) rc[tid] = tid < 64 ? rcv * nis : -rcv;
+    if constexpr (DROP) {
+      if (tid >= 128 && tid < 192) reinterpret_cast<unsigned*>(rc)[tid] = rseed;
+    }
+  };
+  int aoff[4], troff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) aoff[kk] = lr * 128 + 16 * ((2 * kk + h) ^ f64(lr));
+  tr_offsets(lane, troff);
+
+  const int qstart = CAUSAL ? (k0 / 64) * 64 : 0;
+  const int ntile = qstart < S ? (S - qstart + 63) / 64 : 0;
+  if (ntile > 0) {
+    load_tile(qstart, 0);
+    store_rc(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  int buf = 0;
+  for (int t = 0; t < ntile; ++t) {
+    const int qt = qstart + t * 64;
+    if (t + 1 < ntile) load_tile(qt + 64, buf ^ 1);
+    const unsigned char* img = smem + buf * BUF;
+    const unsigned char* doimg = img + IMG64;
+    const float* rc = reinterpret_cast<const float*>(img + 2 * IMG64);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int qh = qt + 32 * j;
+      if (CAUSAL && wk0 > qh + 31) continue;   // every key of the wave after every query of the half
+      f32x16 sa, da;
+      float dl[16];
+      unsigned sd[16];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {   // rows 32j + 8m + 4h + {0..3}: registers 4m .. 4m+3
+        const float4 l4 = *reinterpret_cast<const float4*>(rc + 32 * j + 8 * m + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(rc + 64 + 32 * j + 8 * m + 4 * h);
+        sa[4 * m + 0] = l4.x; sa[4 * m + 1] = l4.y; sa[4 * m + 2] = l4.z; sa[4 * m + 3] = l4.w;
+        if constexpr (DROP) {
+          dl[4 * m + 0] = d4.x; dl[4 * m + 1] = d4.y; dl[4 * m + 2] = d4.z; dl[4 * m + 3] = d4.w;   // -delta
+          const uint4 s4 = *reinterpret_cast<const uint4*>(rc + 128 + 32 * j + 8 * m + 4 * h);
+          sd[4 * m + 0] = s4.x; sd[4 * m + 1] = s4.y; sd[4 * m + 2] = s4.z; sd[4 * m + 3] = s4.w;
+          da[4 * m + 0] = da[4 * m + 1] = da[4 * m + 2] = da[4 * m + 3] = 0.f;
+        } else {
+          da[4 * m + 0] = d4.x; da[4 * m + 1] = d4.y; da[4 * m + 2] = d4.z; da[4 * m + 3] = d4.w;
+        }
+      }
+      if ((qh + 32 > S) || (wk0 + 32 > Sk) || (CAUSAL && wk0 + 31 > qh)) {
+        const int lim = key >= Sk ? 32 : (CAUSAL ? key - qh - 4 * h : -1);
+        const int lim2 = S - qh - 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rb = (r & 3) + 8 * (r >> 2);
+          sa[r] = ((rb < lim) | (rb >= lim2)) ? -INFINITY : sa[r];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const u32x4 qa = *reinterpret_cast<const u32x4*>(img + j * 4096 + aoff[kk]);
+        const u32x4 ga = *reinterpret_cast<const u32x4*>(doimg + j * 4096 + aoff[kk]);
+        sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
+        da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(sa[r] * c2);
+        if constexpr (DROP) {
+          const bool kp = fa_keep(sd[r], key, ex.thresh);
+          sa[r] = kp ? p * ex.keep_scale : 0.f;
+          da[r] = p * ((kp ? da[r] * ex.keep_scale : 0.f) + dl[r]);
+        } else {
+          sa[r] = p;
+          da[r] = p * da[r];
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 pw, dw;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          pw[jj] = MF<T>::pack(sa[8 * s2 + 2 * jj], sa[8 * s2 + 2 * jj + 1]);
+          dw[jj] = MF<T>::pack(da[8 * s2 + 2 * jj], da[8 * s2 + 2 * jj + 1]);
+        }
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          dvt[db] = MF<T>::mma(as_frag<frag>(trA(doimg + j * 4096 + s2 * 2048, troff, db)), as_frag<frag>(pw), dvt[db]);
+          dkt[db] = MF<T>::mma(as_frag<frag>(trA(img + j * 4096 + s2 * 2048, troff, db)), as_frag<frag>(dw), dkt[db]);
+        }
+      }
+    }
+    buf ^= 1;
+    if (t + 1 < ntile) store_rc(buf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (key < Sk) {
+    const long gt = ex.gkv_tok ? ex.gkv_tok : (long)H * 64;
+    const long gh = ex.gkv_head ? ex.gkv_head : 64;
+    T* dkr = dK + ((long)b * Sk + key) * gt + (long)head * gh;
+    T* dvr = dV + ((long)b * Sk + key) * gt + (long)head * gh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = db * 32 + 8 * gg + 4 * h;
+        u32x2 wk, wv;
+        wk[0] = MF<T>::pack(dkt[db][4 * gg + 0] * scale, dkt[db][4 * gg + 1] * scale);
+        wk[1] = MF<T>::pack(dkt[db][4 * gg + 2] * scale, dkt[db][4 * gg + 3] * scale);
+        wv[0] = MF<T>::pack(dvt[db][4 * gg + 0], dvt[db][4 * gg + 1]);
+        wv[1] = MF<T>::pack(dvt[db][4 * gg + 2], dvt[db][4 * gg + 3]);
+        *reinterpret_cast<u32x2*>(dkr + d) = wk;
+        *reinterpret_cast<u32x2*>(dvr + d) = wv;
+      }
+  }
+}
+
+template <typename T, bool C, bool DR>
+void launch64(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
+              const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
+              const FaStrides& fs, const FaExt& ex, hipStream_t st) {
+  const dim3 gq((S + 255) / 256, B * H), gk((Sk + 255) / 256, B * H), blk(512);
+  if (!bwd) {
+    hipLaunchKernelGGL((fa64_fwd<T, C, DR>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk,
+                       H, Hk, scale * kLog2e, fs, ex);
+    return;
+  }
+  hipLaunchKernelGGL((fa64_dkdv<T, C, DR>), gk, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
+                     lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
+  hipLaunchKernelGGL((fa64_dq<T, C, DR>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
+                     lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs, ex);
+}
+
+template <typename T>
+int dispatch64(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
+               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
+               int causal, const FaStrides& fs, const FaExt& ex, hipStream_t st) {
+  const bool dr = ex.thresh != 0;
+  if (causal) {
+    if (dr) launch64<T, true, true>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+    else launch64<T, true, false>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+  } else {
+    if (dr) launch64<T, false, true>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+    else launch64<T, false, false>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+  }
+  return (int)hipGetLastError();
+}
+
+bool check64(const void* q, const void* k, const void* v, int S, int Sk, int H, int Hk, long q_tok, int q_head,
+             long kv_tok, int kv_head, long o_tok, int o_head, float dropout) {
+  if (S <= 0 || Sk <= 0 || H <= 0 || Hk <= 0 || H % Hk || dropout < 0.f || dropout >= 1.f) return false;
+  if (((size_t)q | (size_t)k | (size_t)v) & 15) return false;
+  if ((q_tok | kv_tok | o_tok) % 8 || (q_head | kv_head | o_head) % 8) return false;
+  // the DMA's 32-bit offsets: 64 rows of the widest row stride
+  return 64.0 * (double)(q_tok > kv_tok ? (q_tok > o_tok ? q_tok : o_tok) : (kv_tok > o_tok ? kv_tok : o_tok)) * 2 <
+         4294967295.0;
+}
+
+FaStrides strides64(long q_tok, int q_head, long kv_tok, int kv_head, long o_tok, int o_head) {
+  FaStrides f;
+  f.order_g = 0;
+  f.q_tok = q_tok;
+  f.kv_tok = kv_tok;
+  f.o_tok = o_tok;
+  f.dq_tok = f.dkv_tok = 0;
+  f.q_head = q_head;
+  f.kv_head = kv_head;
+  f.o_head = o_head;
+  f.dq_head = f.dkv_head = 0;
+  return f;
+}
+
+}  // namespace
+
+// Head dim 64 forward: q [B, S, H, 64] / k, v [B, Sk, Hk, 64] with element strides (token, head)
+// q_tok / q_head, kv_tok / kv_head (a packed [B, S, H, 3 * 64] projection is read in place), o with
+// o_tok / o_head, lse [B, H, S] fp32; dropout in [0, 1) with the generic kernels' mask stream.
+PHA_API int pha_fa64_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk,
+                         int H, int Hk, float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head,
+                         long o_tok, int o_head, float dropout, unsigned seed, const unsigned* seedp,
+                         hipStream_t stream) {
+  if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
+      ((size_t)o & 7))
+    return (int)hipErrorInvalidValue;
+  FaExt ex{nullptr, 0, 0, 0, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  ex.seedp = seedp;
+  if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
+  const FaStrides fs = strides64(q_tok, q_head, kv_tok, kv_head, o_tok, o_head);
+  if (dt == kBF16)
+    return dispatch64<bf16_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk,
+                              scale, causal, fs, ex, stream);
+  if (dt == kF16)
+    return dispatch64<half_t>(false, q, k, v, o, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, S, Sk, H, Hk,
+                              scale, causal, fs, ex, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+// Head dim 64 backward (delta = rowsum(dO * O) from pha_flash_attn_bwd_preprocess): dout with the
+// o strides, dq with gq_tok / gq_head, dk / dv with gkv_tok / gkv_head (0: dense [B, S, H, 64];
+// dk / dv per query head — the caller sums GQA groups)
+PHA_API int pha_fa64_bwd(int dt, const void* q, const void* k, const void* v, const void* dout, const float* lse,
+                         const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
+                         float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head, long o_tok,
+                         int o_head, long gq_tok, int gq_head, long gkv_tok, int gkv_head, float dropout,
+                         unsigned seed, const unsigned* seedp, hipStream_t stream) {
+  if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
+      ((size_t)dout & 15) || ((size_t)dq & 7) || ((size_t)dk & 7) || ((size_t)dv & 7) || (gq_tok | gkv_tok) % 4 ||
+      (gq_head | gkv_head) % 4)
+    return (int)hipErrorInvalidValue;
+  FaExt ex{nullptr, 0, 0, 0, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  ex.seedp = seedp;
+  ex.gq_tok = gq_tok;
+  ex.gq_head = gq_head;
+  ex.gkv_tok = gkv_tok;
+  ex.gkv_head = gkv_head;
+  if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
+  const FaStrides fs = strides64(q_tok, q_head, kv_tok, kv_head, o_tok, o_head);
+  if (dt == kBF16)
+    return dispatch64<bf16_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H,
+                              Hk, scale, causal, fs, ex, stream);
+  if (dt == kF16)
+    return dispatch64<half_t>(true, q, k, v, nullptr, const_cast<float*>(lse), dout, delta, dq, dk, dv, B, S, Sk, H,
+                              Hk, scale, causal, fs, ex, stream);
+  return (int)hipErrorInvalidValue;
+}

@@ -690,6 +690,43 @@ def _fa_bias(mask, B, H, S, Sk, device):
     return mask, (mask.stride(0), mask.stride(1), mask.stride(2))
 
 
+def _fa64_on(D, mask):
+    """head dim 64 without an additive mask: the 8-wave LDS-DMA kernels of flash_attn_d64.hip
+    (packed strides, in-kernel dropout with the generic kernels' mask stream); PHA_FA64=0 keeps the
+    generic 4-wave kernels"""
+    import os
+    L = _lib.lib
+    return (D == 64 and mask is None and L is not None and hasattr(L, "pha_fa64_fwd")
+            and os.environ.get("PHA_FA64", "1") != "0")
+
+
+def _fa64_sig(L):
+    if not getattr(L, "_fa64_sig", False):
+        P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
+        L.pha_fa64_fwd.argtypes = [I, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, F, U, P, P]
+        L.pha_fa64_fwd.restype = c_int
+        L.pha_fa64_bwd.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, LG, I,
+                                   LG, I, F, U, P, P]
+        L.pha_fa64_bwd.restype = c_int
+        L._fa64_sig = True
+    return L
+
+
+def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_, dropout_p, seed, seed_dev, st):
+    """qs / kvs / os_: (token, head) element strides of q, k / v and o"""
+    L = _fa64_sig(_L())
+    _check(L.pha_fa64_fwd(dt, qp, kp, vp, _ptr(o), _ptr(lse), B, S, Sk, H, Hk, sc, int(causal), qs[0], qs[1], kvs[0],
+                          kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st), "fa64_fwd")
+
+
+def _fa64_bwd(dt, qp, kp, vp, do, lse, delta, dqp, dkp, dvp, B, S, Sk, H, Hk, sc, causal, qs, kvs, gqs, gkvs,
+              dropout_p, seed, seed_dev, st):
+    L = _fa64_sig(_L())
+    _check(L.pha_fa64_bwd(dt, qp, kp, vp, _ptr(do), _ptr(lse), _ptr(delta), dqp, dkp, dvp, B, S, Sk, H, Hk, sc,
+                          int(causal), qs[0], qs[1], kvs[0], kvs[1], H * 64, 64, gqs[0], gqs[1], gkvs[0], gkvs[1],
+                          float(dropout_p), seed, _ptr(seed_dev), st), "fa64_bwd")
+
+
 class FlashAttentionExt(torch.autograd.Function):
     """Flash attention with an additive mask and / or dropout (4-wave kernels, head dims
     32 / 64 / 128): the dropout mask is a counter-based hash of (seed, b*H+h, query, key),
@@ -705,6 +742,14 @@ class FlashAttentionExt(torch.autograd.Function):
         seed, seed_dev = dropout_seed(q.device) if dropout_p else (0, None)
         o = torch.empty_like(q)
         lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
+        ctx.fa64 = _fa64_on(D, mask)
+        if ctx.fa64:
+            _fa64_fwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), o, lse, B, S, Sk, H, Hk, sc, causal, (H * D, D),
+                      (Hk * D, D), (H * D, D), dropout_p, seed, seed_dev, _stream(q))
+            ctx.save_for_backward(q, k, v, o, lse)
+            ctx.bias, ctx.strides, ctx.seed, ctx.seed_dev = None, (0, 0, 0), seed, seed_dev
+            ctx.causal, ctx.scale, ctx.dropout_p = causal, sc, float(dropout_p)
+            return o
         L = _L()
         if not getattr(L, "_fa_ext_sig", False):
             P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
@@ -736,12 +781,17 @@ class FlashAttentionExt(torch.autograd.Function):
         dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S),
                                                c_int(H), c_int(D), _stream(q)), "flash_attn_bwd_preprocess")
-        sb, sh, sq = ctx.strides
-        _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
-                                        _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk, H, Hk, D, ctx.scale, int(ctx.causal),
-                                        _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed, _stream(q), 0, 0, 0, 0,
-                                        _ptr(ctx.seed_dev)),
-               "flash_attn_bwd_ext")
+        if getattr(ctx, "fa64", False):
+            _fa64_bwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), do, lse, delta, _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk,
+                      H, Hk, ctx.scale, ctx.causal, (H * D, D), (Hk * D, D), (0, 0), (0, 0), ctx.dropout_p, ctx.seed,
+                      ctx.seed_dev, _stream(q))
+        else:
+            sb, sh, sq = ctx.strides
+            _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
+                                            _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk, H, Hk, D, ctx.scale,
+                                            int(ctx.causal), _ptr(ctx.bias), sb, sh, sq, ctx.dropout_p, ctx.seed,
+                                            _stream(q), 0, 0, 0, 0, _ptr(ctx.seed_dev)),
+                   "flash_attn_bwd_ext")
         if Hk != H:
             g = H // Hk
             dk = dk.view(B, Sk, Hk, g, D).sum(3)
@@ -759,12 +809,42 @@ class FlashAttentionExtPacked(torch.autograd.Function):
     def forward(ctx, qkv, causal, scale, mask, dropout_p):
         B, S, H, D3 = qkv.shape
         D = D3 // 3
+        ctx.fa64p = _fa64_on(D, mask) and qkv.is_contiguous()
+        if ctx.fa64p:   # head dim 64: the kernels read q | k | v in place (no slice copies)
+            sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
+            seed, seed_dev = dropout_seed(qkv.device) if dropout_p else (0, None)
+            o = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
+            lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+            es, base = qkv.element_size(), qkv.data_ptr()
+            _fa64_fwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), o, lse,
+                      B, S, S, H, H, sc, causal, (3 * H * D, 3 * D), (3 * H * D, 3 * D), (H * D, D), dropout_p,
+                      seed, seed_dev, _stream(qkv))
+            ctx.save_for_backward(qkv, o, lse)
+            ctx.seed, ctx.seed_dev, ctx.causal, ctx.scale, ctx.dropout_p = seed, seed_dev, causal, sc, float(dropout_p)
+            return o
         q, k, v = (qkv[..., i * D:(i + 1) * D].contiguous() for i in range(3))
         o = FlashAttentionExt.forward(ctx, q, k, v, causal, scale, mask, dropout_p)
         return o
 
     @staticmethod
     def backward(ctx, do):
+        if ctx.fa64p:
+            qkv, o, lse = ctx.saved_tensors
+            do = do.contiguous()
+            B, S, H, D3 = qkv.shape
+            D = D3 // 3
+            L = _L()
+            delta = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+            g = torch.empty_like(qkv)
+            _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[qkv.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B),
+                                                   c_int(S), c_int(H), c_int(D), _stream(qkv)),
+                   "flash_attn_bwd_preprocess")
+            es, base, gb = qkv.element_size(), qkv.data_ptr(), g.data_ptr()
+            st = (3 * H * D, 3 * D)
+            _fa64_bwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), do, lse,
+                      delta, c_void_p(gb), c_void_p(gb + D * es), c_void_p(gb + 2 * D * es), B, S, S, H, H, ctx.scale,
+                      ctx.causal, st, st, st, st, ctx.dropout_p, ctx.seed, ctx.seed_dev, _stream(qkv))
+            return g, None, None, None, None
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
         B, S, H, D = q.shape
