@@ -181,13 +181,21 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
       psum += __shfl_xor(psum, 32, 64);
       l_run += psum;
       if constexpr (DROP) {
+        unsigned wb[2] = {0u, 0u};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kb * 32 + acc_row(r, h);
-            s[kb][r] = fa_keep(drow, key, ex.thresh) ? s[kb][r] * ex.keep_scale : 0.f;
+            const bool kp = fa_keep(drow, key, ex.thresh);
+            wb[kb] |= (unsigned)kp << acc_row(r, h);
+            s[kb][r] = kp ? s[kb][r] * ex.keep_scale : 0.f;
           }
+        if (ex.dmask) {   // the two 32-key words of this tile: lane half h stores word h
+          const unsigned w0 = wb[0] | (unsigned)__shfl_xor((int)wb[0], 32, 64);
+          const unsigned w1 = wb[1] | (unsigned)__shfl_xor((int)wb[1], 32, 64);
+          if (q < S) ex.dmask[((long)bh * S + q) * ex.dmask_w + 2 * t + h] = h ? w1 : w0;
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
 //   P^T = exp2(c S^T - lse), dS^T = P^T (Z dP^T / (1 - rate) - delta), dQ^T += K^T dS^T (transposed
 //   reads of the K image, dS^T packed as the B operand)
 // ============================================================================================
-template <typename T, bool CAUSAL, bool DROP>
+template <typename T, bool CAUSAL, int DR>
 __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T* __restrict__ K,
                                                const T* __restrict__ V, const T* __restrict__ dO,
                                                const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -258,7 +266,8 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
   const float c2 = scale * kLog2e;
   const float nl = -LSE[(long)bh * S + qc] * kLog2e, del = DELTA[(long)bh * S + qc];
   unsigned drow = 0;
-  if constexpr (DROP) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
+  if constexpr (DR == 1) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
+  const unsigned* mrow = DR == 2 ? ex.dmask + ((long)bh * S + qc) * ex.dmask_w : nullptr;
   f32x16 dqt[2];
   dqt[0] = zero16();
   dqt[1] = zero16();
@@ -288,6 +297,8 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
     const unsigned char* kl = smem + cur * 2 * IMG64;
     const unsigned char* vl = kl + IMG64;
     if (!(CAUSAL && k0 > wq0 + 31)) {
+      u32x2 mw = {0u, 0u};
+      if constexpr (DR == 2) mw = *reinterpret_cast<const u32x2*>(mrow + 2 * t);
       f32x16 s[2], dp[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -322,9 +333,11 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(fmaf(s[kb][r], c2, nl));
           float g = dp[kb][r];
-          if constexpr (DROP) {
+          if constexpr (DR == 1) {
             const int key = k0 + kb * 32 + acc_row(r, h);
             g = fa_keep(drow, key, ex.thresh) ? g * ex.keep_scale : 0.f;
+          } else if constexpr (DR == 2) {
+            g = ((mw[kb] >> acc_row(r, h)) & 1u) ? g * ex.keep_scale : 0.f;
           }
           s[kb][r] = p * (g - del);
         }
@@ -369,9 +382,9 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 //   S = Q K^T (from -lse/scale), dP = dO V^T (from -delta, or 0 with dropout), p = exp2(c S),
 //   dV^T += dO^T (Z p / (1 - rate)), dK^T += Q^T (p (Z dP / (1 - rate) - delta))
 // ============================================================================================
-constexpr int RC64 = 3 * 64 * 4;   // -lse/scale, -delta, row seeds of one tile
+constexpr int RC64 = 3 * 64 * 4 + 8 * 64 * 4;   // -lse/scale, -delta, row seeds, keep bits [8 words][64 rows]
 
-template <typename T, bool CAUSAL, bool DROP>
+template <typename T, bool CAUSAL, int DR>
 __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const T* __restrict__ K,
                                                  const T* __restrict__ V, const T* __restrict__ dO,
                                                  const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -392,8 +405,9 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   const float* lse_b = LSE + (long)bh * S;
   const float* del_b = DELTA + (long)bh * S;
   const float c2 = scale * kLog2e, nis = -1.f / scale;
+  constexpr bool DROP = DR != 0;
   unsigned dstream = 0;
-  if constexpr (DROP) dstream = fa_stream(fa_seed(ex), b * H + head);
+  if constexpr (DR == 1) dstream = fa_stream(fa_seed(ex), b * H + head);
 
   const int keyc = min(key, Sk - 1);
   frag kf[4], vf[4];
@@ -410,6 +424,7 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   const unsigned lds0 = lds_addr(smem);
   float rcv = 0.f;
   unsigned rseed = 0;
+  uint4 mreg = {0u, 0u, 0u, 0u};
   auto load_tile = [&](int qt, int buf) {   // 16 pieces (Q 0-7, dO 8-15) + the row constants
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -418,15 +433,30 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
       else dma64(Qb, fs.q_tok, qt, S - 1, gidx & 7, lane, lds0 + buf * BUF);
     }
     if (tid < 128) rcv = (tid < 64 ? lse_b : del_b)[min(qt + (tid & 63), S - 1)];
-    if constexpr (DROP) {
+    if constexpr (DR == 1) {
       if (tid >= 128 && tid < 192) rseed = fa_row(dstream, qt + (tid & 63));
+    } else if constexpr (DR == 2) {   // the 8 keep words of the workgroup's 256 keys, 4 per thread
+      if (tid >= 256 && tid < 384) {
+        const int i = tid - 256;
+        mreg = *reinterpret_cast<const uint4*>(ex.dmask + ((long)bh * S + min(qt + (i >> 1), S - 1)) * ex.dmask_w +
+                                               (k0 >> 5) + 4 * (i & 1));
+      }
     }
   };
   auto store_rc = [&](int buf) {
     float* rc = reinterpret_cast<float*>(smem + buf * BUF + 2 * IMG64);
     if (tid < 128) rc[tid] = tid < 64 ? rcv * nis : -rcv;
-    if constexpr (DROP) {
+    if constexpr (DR == 1) {
       if (tid >= 128 && tid < 192) reinterpret_cast<unsigned*>(rc)[tid] = rseed;
+    } else if constexpr (DR == 2) {   // transposed to [word][row]: a lane's 4 consecutive rows are one b128
+      if (tid >= 256 && tid < 384) {
+        const int i = tid - 256;
+        unsigned* mk = reinterpret_cast<unsigned*>(rc) + 192 + 4 * (i & 1) * 64 + (i >> 1);
+        mk[0] = mreg.x;
+        mk[64] = mreg.y;
+        mk[128] = mreg.z;
+        mk[192] = mreg.w;
+      }
     }
   };
   int aoff[4], troff[2][2];
@@ -463,7 +493,8 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
         sa[4 * m + 0] = l4.x; sa[4 * m + 1] = l4.y; sa[4 * m + 2] = l4.z; sa[4 * m + 3] = l4.w;
         if constexpr (DROP) {
           dl[4 * m + 0] = d4.x; dl[4 * m + 1] = d4.y; dl[4 * m + 2] = d4.z; dl[4 * m + 3] = d4.w;   // -delta
-          const uint4 s4 = *reinterpret_cast<const uint4*>(rc + 128 + 32 * j + 8 * m + 4 * h);
+          // DR 1: the rows' hash seeds; DR 2: the rows' keep words of this wave's 32 keys
+          const uint4 s4 = *reinterpret_cast<const uint4*>(rc + (DR == 1 ? 128 : 192 + wid * 64) + 32 * j + 8 * m + 4 * h);
           sd[4 * m + 0] = s4.x; sd[4 * m + 1] = s4.y; sd[4 * m + 2] = s4.z; sd[4 * m + 3] = s4.w;
           da[4 * m + 0] = da[4 * m + 1] = da[4 * m + 2] = da[4 * m + 3] = 0.f;
         } else {
@@ -486,11 +517,27 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
         sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
         da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
       }
+      // dropout draws: lanes 2i, 2i+1 hold keys 2m, 2m+1, and fa_keep takes both keys' 16-bit
+      // halves from ONE 32-bit hash of (row seed ^ key / 2): each lane of the pair hashes 8 of the
+      // 16 rows and the pair swaps results (DPP quad_perm 1,0,3,2) — half the multiply-heavy hashes
+      unsigned rnd[16];
+      if constexpr (DR == 1) {
+        const bool odd = lane & 1;
+        const unsigned kx = (unsigned)(key >> 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned mine = fa_mix((odd ? sd[i + 8] : sd[i]) ^ kx);
+          const unsigned other = (unsigned)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false);
+          rnd[i] = odd ? other : mine;
+          rnd[i + 8] = odd ? mine : other;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = fexp2(sa[r] * c2);
         if constexpr (DROP) {
-          const bool kp = fa_keep(sd[r], key, ex.thresh);
+          const bool kp = DR == 2 ? ((sd[r] >> lr) & 1u) != 0
+                                  : ((lane & 1) ? (rnd[r] >> 16) : (rnd[r] & 0xffffu)) >= ex.thresh;   // = fa_keep(sd[r], key, ..)
           sa[r] = kp ? p * ex.keep_scale : 0.f;
           da[r] = p * ((kp ? da[r] * ex.keep_scale : 0.f) + dl[r]);
         } else {
@@ -539,13 +586,13 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   }
 }
 
-template <typename T, bool C, bool DR>
+template <typename T, bool C, int DR>
 void launch64(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
               const FaStrides& fs, const FaExt& ex, hipStream_t st) {
   const dim3 gq((S + 255) / 256, B * H), gk((Sk + 255) / 256, B * H), blk(512);
   if (!bwd) {
-    hipLaunchKernelGGL((fa64_fwd<T, C, DR>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk,
+    hipLaunchKernelGGL((fa64_fwd<T, C, DR != 0>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk,
                        H, Hk, scale * kLog2e, fs, ex);
     return;
   }
@@ -559,14 +606,14 @@ template <typename T>
 int dispatch64(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
                const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
                int causal, const FaStrides& fs, const FaExt& ex, hipStream_t st) {
-  const bool dr = ex.thresh != 0;
+  const int dr = ex.thresh == 0 ? 0 : (bwd && ex.dmask ? 2 : 1);
+#define L64(C, D) launch64<T, C, D>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st)
   if (causal) {
-    if (dr) launch64<T, true, true>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
-    else launch64<T, true, false>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+    if (dr == 2) L64(true, 2); else if (dr == 1) L64(true, 1); else L64(true, 0);
   } else {
-    if (dr) launch64<T, false, true>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
-    else launch64<T, false, false>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+    if (dr == 2) L64(false, 2); else if (dr == 1) L64(false, 1); else L64(false, 0);
   }
+#undef L64
   return (int)hipGetLastError();
 }
 
@@ -596,18 +643,24 @@ FaStrides strides64(long q_tok, int q_head, long kv_tok, int kv_head, long o_tok
 
 }  // namespace
 
+// keep-mask words per query row (keys rounded up to the dK/dV workgroup's 256): the forward's
+// dmask is [B * H * S * words] uint32
+PHA_API int pha_fa64_mask_words(int Sk) { return 8 * ((Sk + 255) / 256); }
+
 // Head dim 64 forward: q [B, S, H, 64] / k, v [B, Sk, Hk, 64] with element strides (token, head)
 // q_tok / q_head, kv_tok / kv_head (a packed [B, S, H, 3 * 64] projection is read in place), o with
 // o_tok / o_head, lse [B, H, S] fp32; dropout in [0, 1) with the generic kernels' mask stream.
 PHA_API int pha_fa64_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk,
                          int H, int Hk, float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head,
                          long o_tok, int o_head, float dropout, unsigned seed, const unsigned* seedp,
-                         hipStream_t stream) {
+                         hipStream_t stream, unsigned* dmask) {
   if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
-      ((size_t)o & 7))
+      ((size_t)o & 7) || ((size_t)dmask & 15))
     return (int)hipErrorInvalidValue;
   FaExt ex{nullptr, 0, 0, 0, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
   ex.seedp = seedp;
+  ex.dmask = dropout > 0.f ? dmask : nullptr;
+  ex.dmask_w = pha_fa64_mask_words(Sk);
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
   const FaStrides fs = strides64(q_tok, q_head, kv_tok, kv_head, o_tok, o_head);
   if (dt == kBF16)
@@ -626,7 +679,7 @@ PHA_API int pha_fa64_bwd(int dt, const void* q, const void* k, const void* v, co
                          const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
                          float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head, long o_tok,
                          int o_head, long gq_tok, int gq_head, long gkv_tok, int gkv_head, float dropout,
-                         unsigned seed, const unsigned* seedp, hipStream_t stream) {
+                         unsigned seed, const unsigned* seedp, hipStream_t stream, const unsigned* dmask) {
   if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
       ((size_t)dout & 15) || ((size_t)dq & 7) || ((size_t)dk & 7) || ((size_t)dv & 7) || (gq_tok | gkv_tok) % 4 ||
       (gq_head | gkv_head) % 4)
@@ -637,6 +690,9 @@ PHA_API int pha_fa64_bwd(int dt, const void* q, const void* k, const void* v, co
   ex.gq_head = gq_head;
   ex.gkv_tok = gkv_tok;
   ex.gkv_head = gkv_head;
+  ex.dmask = dropout > 0.f ? const_cast<unsigned*>(dmask) : nullptr;
+  ex.dmask_w = pha_fa64_mask_words(Sk);
+  if ((size_t)dmask & 15) return (int)hipErrorInvalidValue;
   if (dropout > 0.f && ex.thresh == 0) ex.thresh = 1;
   const FaStrides fs = strides64(q_tok, q_head, kv_tok, kv_head, o_tok, o_head);
   if (dt == kBF16)

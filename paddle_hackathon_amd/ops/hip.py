@@ -703,28 +703,38 @@ def _fa64_on(D, mask):
 def _fa64_sig(L):
     if not getattr(L, "_fa64_sig", False):
         P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
-        L.pha_fa64_fwd.argtypes = [I, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, F, U, P, P]
+        L.pha_fa64_fwd.argtypes = [I, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, F, U, P, P, P]
         L.pha_fa64_fwd.restype = c_int
         L.pha_fa64_bwd.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, LG, I,
-                                   LG, I, F, U, P, P]
+                                   LG, I, F, U, P, P, P]
+        L.pha_fa64_mask_words.argtypes = [I]
+        L.pha_fa64_mask_words.restype = c_int
         L.pha_fa64_bwd.restype = c_int
         L._fa64_sig = True
     return L
 
 
 def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_, dropout_p, seed, seed_dev, st):
-    """qs / kvs / os_: (token, head) element strides of q, k / v and o"""
+    """qs / kvs / os_: (token, head) element strides of q, k / v and o. With dropout, returns the keep
+    mask as bits (int32 [B * H * S * words]) for the backward — the reference fused attention keeps
+    its dropout mask too (fmha_ref.h dropout_mask_out); PHA_FA64_MASKBITS=0 re-hashes instead"""
+    import os
     L = _fa64_sig(_L())
+    dmask = None
+    if dropout_p and os.environ.get("PHA_FA64_MASKBITS", "1") != "0":
+        dmask = torch.empty(B * H * S * L.pha_fa64_mask_words(Sk), dtype=torch.int32, device=o.device)
     _check(L.pha_fa64_fwd(dt, qp, kp, vp, _ptr(o), _ptr(lse), B, S, Sk, H, Hk, sc, int(causal), qs[0], qs[1], kvs[0],
-                          kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st), "fa64_fwd")
+                          kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask)),
+           "fa64_fwd")
+    return dmask
 
 
 def _fa64_bwd(dt, qp, kp, vp, do, lse, delta, dqp, dkp, dvp, B, S, Sk, H, Hk, sc, causal, qs, kvs, gqs, gkvs,
-              dropout_p, seed, seed_dev, st):
+              dropout_p, seed, seed_dev, st, dmask=None):
     L = _fa64_sig(_L())
     _check(L.pha_fa64_bwd(dt, qp, kp, vp, _ptr(do), _ptr(lse), _ptr(delta), dqp, dkp, dvp, B, S, Sk, H, Hk, sc,
                           int(causal), qs[0], qs[1], kvs[0], kvs[1], H * 64, 64, gqs[0], gqs[1], gkvs[0], gkvs[1],
-                          float(dropout_p), seed, _ptr(seed_dev), st), "fa64_bwd")
+                          float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask)), "fa64_bwd")
 
 
 class FlashAttentionExt(torch.autograd.Function):
@@ -744,8 +754,8 @@ class FlashAttentionExt(torch.autograd.Function):
         lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
         ctx.fa64 = _fa64_on(D, mask)
         if ctx.fa64:
-            _fa64_fwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), o, lse, B, S, Sk, H, Hk, sc, causal, (H * D, D),
-                      (Hk * D, D), (H * D, D), dropout_p, seed, seed_dev, _stream(q))
+            ctx.dmask = _fa64_fwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), o, lse, B, S, Sk, H, Hk, sc, causal,
+                                  (H * D, D), (Hk * D, D), (H * D, D), dropout_p, seed, seed_dev, _stream(q))
             ctx.save_for_backward(q, k, v, o, lse)
             ctx.bias, ctx.strides, ctx.seed, ctx.seed_dev = None, (0, 0, 0), seed, seed_dev
             ctx.causal, ctx.scale, ctx.dropout_p = causal, sc, float(dropout_p)
@@ -784,7 +794,7 @@ class FlashAttentionExt(torch.autograd.Function):
         if getattr(ctx, "fa64", False):
             _fa64_bwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), do, lse, delta, _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk,
                       H, Hk, ctx.scale, ctx.causal, (H * D, D), (Hk * D, D), (0, 0), (0, 0), ctx.dropout_p, ctx.seed,
-                      ctx.seed_dev, _stream(q))
+                      ctx.seed_dev, _stream(q), ctx.dmask)
         else:
             sb, sh, sq = ctx.strides
             _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
@@ -816,9 +826,9 @@ class FlashAttentionExtPacked(torch.autograd.Function):
             o = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
             lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
             es, base = qkv.element_size(), qkv.data_ptr()
-            _fa64_fwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), o, lse,
-                      B, S, S, H, H, sc, causal, (3 * H * D, 3 * D), (3 * H * D, 3 * D), (H * D, D), dropout_p,
-                      seed, seed_dev, _stream(qkv))
+            ctx.dmask = _fa64_fwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es),
+                                  c_void_p(base + 2 * D * es), o, lse, B, S, S, H, H, sc, causal, (3 * H * D, 3 * D),
+                                  (3 * H * D, 3 * D), (H * D, D), dropout_p, seed, seed_dev, _stream(qkv))
             ctx.save_for_backward(qkv, o, lse)
             ctx.seed, ctx.seed_dev, ctx.causal, ctx.scale, ctx.dropout_p = seed, seed_dev, causal, sc, float(dropout_p)
             return o
@@ -843,7 +853,7 @@ class FlashAttentionExtPacked(torch.autograd.Function):
             st = (3 * H * D, 3 * D)
             _fa64_bwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), do, lse,
                       delta, c_void_p(gb), c_void_p(gb + D * es), c_void_p(gb + 2 * D * es), B, S, S, H, H, ctx.scale,
-                      ctx.causal, st, st, st, st, ctx.dropout_p, ctx.seed, ctx.seed_dev, _stream(qkv))
+                      ctx.causal, st, st, st, st, ctx.dropout_p, ctx.seed, ctx.seed_dev, _stream(qkv), ctx.dmask)
             return g, None, None, None, None
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
@@ -915,9 +925,15 @@ class FlashAttention(torch.autograd.Function):
         sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
         o = torch.empty_like(q)
         lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
-        L = _L()
-        _check(L.pha_flash_attn_fwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), c_int(B), c_int(S), c_int(Sk),
-                                    c_int(H), c_int(Hk), c_int(D), c_float(sc), c_int(int(causal)), _stream(q)), "flash_attn_fwd")
+        ctx.fa64 = _fa64_on(D, None)
+        if ctx.fa64:
+            _fa64_fwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), o, lse, B, S, Sk, H, Hk, sc, causal, (H * D, D),
+                      (Hk * D, D), (H * D, D), 0.0, 0, None, _stream(q))
+        else:
+            L = _L()
+            _check(L.pha_flash_attn_fwd(c_int(_DT[q.dtype]), _ptr(q), _ptr(k), _ptr(v), _ptr(o), _ptr(lse), c_int(B),
+                                        c_int(S), c_int(Sk), c_int(H), c_int(Hk), c_int(D), c_float(sc),
+                                        c_int(int(causal)), _stream(q)), "flash_attn_fwd")
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal = causal
         ctx.scale = sc
@@ -936,7 +952,10 @@ class FlashAttention(torch.autograd.Function):
         dv = torch.empty_like(v) if Hk == H else torch.empty((B, Sk, H, D), dtype=v.dtype, device=v.device)
         _check(L.pha_flash_attn_bwd_preprocess(c_int(_DT[q.dtype]), _ptr(o), _ptr(do), _ptr(delta), c_int(B), c_int(S), c_int(H), c_int(D),
                                                _stream(q)), "flash_attn_bwd_preprocess")
-        if _bwd_fused(D):
+        if getattr(ctx, "fa64", False):
+            _fa64_bwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), do, lse, delta, _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk,
+                      H, Hk, ctx.scale, ctx.causal, (H * D, D), (Hk * D, D), (0, 0), (0, 0), 0.0, 0, None, _stream(q))
+        elif _bwd_fused(D):
             # single-kernel backward; dQ is summed over key blocks in an fp32 workspace
             acc = torch.empty((B, S, H, D), dtype=torch.float32, device=q.device)
             L.pha_flash_attn_bwd_fused.restype = c_int

@@ -125,3 +125,41 @@ def test_fa64_kernels_are_the_ones_running(monkeypatch):
     q = torch.randn(1, 128, 2, 64, device="cuda").bfloat16()
     hip.FlashAttentionExt.apply(q, q, q, False, 0.125, None, 0.1)
     assert called["ext"] == 0 and hasattr(L, "pha_fa64_fwd")
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_fa64_plain_entry_matches_generic(causal, monkeypatch):
+    """ops.flash_attention without mask / dropout at D = 64 (FlashAttention: GPT-2-sized models)
+    runs the new kernels; same result as the generic 4-wave kernels"""
+    from paddle_hackathon_amd import ops
+    torch.manual_seed(1)
+    q, k, v = (torch.randn(2, 384, 6, 64, device="cuda").bfloat16() for _ in range(3))
+    do = torch.randn_like(q)
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("PHA_FA64", on)
+        qg, kg, vg = (t.clone().requires_grad_() for t in (q, k, v))
+        o = ops.flash_attention(qg, kg, vg, causal=causal)
+        res.append((o.float(),) + tuple(x.float() for x in torch.autograd.grad(o, (qg, kg, vg), do)))
+    for a, b in zip(*res):
+        assert _rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_fa64_stored_keep_bits_equal_rehashed_mask(causal, monkeypatch):
+    """the backward reading the forward's keep bits (default) is bitwise equal to the backward that
+    re-hashes the mask (PHA_FA64_MASKBITS=0), incl. a ragged key count"""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(4)
+    B, S, H = 2, 328, 3
+    qkv = torch.randn(B, S, H, 192, device="cuda").bfloat16()
+    do = torch.randn(B, S, H, 64, device="cuda").bfloat16()
+    res = []
+    for mb in ("1", "0"):
+        monkeypatch.setenv("PHA_FA64_MASKBITS", mb)
+        a = qkv.clone().requires_grad_()
+        torch.manual_seed(21)
+        o = hip.flash_attention_packed_ext(a, causal, None, None, 0.1)
+        (g,) = torch.autograd.grad(o, a, do)
+        res.append((o, g))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

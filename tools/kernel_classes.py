@@ -7,7 +7,7 @@ import re
 _RULES = [
     ("own GEMM (gemm4p/gemm4w/gemm8p)", lambda n: re.search(r"pha::g4[pw]::|pha::g8p::|gemm4[pw]_kernel|gemm8p_kernel", n)),
     ("own conv GEMM (gemm256/gemm_conv)", lambda n: re.search(r"gemm256|conv256|gemm_conv|conv_gemm|pha::g256::", n)),
-    ("own flash attention", lambda n: re.search(r"\bfa_|flash|attn", n) and "at::native" not in n),
+    ("own flash attention", lambda n: re.search(r"\bfa_|\bfa64_|flash|attn", n) and "at::native" not in n),
     ("own layer_norm / softmax / CE", lambda n: re.search(r"ln_fwd|ln_bwd|col_reduce|col_partial|softmax|_ce_|bdrln", n)
      and "at::native" not in n),
     ("own batch_norm", lambda n: re.search(r"\bbn_|batch_norm", n) and "MIOpen" not in n and "at::native" not in n),
