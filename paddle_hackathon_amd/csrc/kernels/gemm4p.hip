@@ -513,7 +513,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   unsigned long long sp_t = 0, sp_ab = 0, sp_rel = 0, sp_n = 0;
   constexpr int LRG = lv_rg(LV, RELG);
   constexpr int SPM = sp_mode(LV), SNA = sp_na(LV, RELG), SGB = sp_gb(LV, RELG);
-  static_assert(SPM == 0 || (LWG == 0 && !WSTAG && !AKO && !BKO), "SPREAD: NT early schedule only");
+  static_assert(SPM == 0 || (LWG == 0 && !WSTAG), "SPREAD: the early schedule without late waits / wave stagger");
   static_assert(LWG == 0 || (LDMB <= LWG && RELG == 8), "late variants: every phase-B DMA before the wait");
 
   // One k-half phase: MFMA groups of 4 on (ca, cb); with RD the 16 fragment reads of (rbuf, rkh)
@@ -1565,13 +1565,21 @@ int launch_e(const Args& a, int ako, int bko, int trans, int grid, hipStream_t s
     else hipLaunchKernelGGL((gemm4p_kernel<T, false, false, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   }
   else if (ako && bko && !trans) {
+    // TN schedule variants (weight gradients): LV 8 (PIN) / 40 (PIN + SPREAD, the ops/gemm.py default:
+    // 1.2-4.3 % on the GPT dW products, tools/tn_lv_ab.py)
+    const int lv = E && std::is_same<T, bf16_t>::value && !BIAS
+                       ? ((a.epi >> EPI_LATE_SHIFT) & 15) | (((a.epi >> EPI_SPREAD_SHIFT) & 3) << 5) : 0;
     if constexpr (E) {
       if (a.epi & EPI_COLSUM) {
-        hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 0, true>), dim3(grid), dim3(256), 0, st, a);
+        if (lv == 40) hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 40, true>), dim3(grid), dim3(256), 0, st, a);
+        else if (lv == 8) hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 8, true>), dim3(grid), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 0, true>), dim3(grid), dim3(256), 0, st, a);
         return (int)hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
+    if (lv == 40) hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 40>), dim3(grid), dim3(256), 0, st, a);
+    else if (lv == 8) hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E, 8>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm4p_kernel<T, true, true, false, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
   }
   else if (ako && !bko && trans)
     hipLaunchKernelGGL((gemm4p_kernel<T, true, false, true, BIAS, false, false, false, false, E>), dim3(grid), dim3(256), 0, st, a);
