@@ -430,6 +430,7 @@ namespace {
 struct Ctx {
   int dev;
   std::map<std::string, Tensor>& env;
+  bool bf16 = false;   // GEMM-class ops (mul / matmul / fc / conv via im2col) on bf16 MFMA
   Tensor& get(const std::string& n) {
     auto it = env.find(n);
     if (it == env.end()) throw Error("variable " + n + " has no value");
@@ -484,6 +485,10 @@ struct GemmArgs {
 };
 
 void gemm(Ctx& c, const GemmArgs& g) {
+  if (c.gpu() && c.bf16 &&
+      gpu::gemm_bf16(g.A, g.B, g.C, g.bias, g.batch, g.M, g.N, g.K, g.sAb, g.sAm, g.sAk, g.sBb, g.sBk, g.sBn, g.sCb,
+                     g.sCm, g.alpha, g.relu))
+    return;
   if (c.gpu()) {
     gpu::gemm(g.A, g.B, g.C, g.bias, g.batch, g.M, g.N, g.K, g.sAb, g.sAm, g.sAk, g.sBb, g.sBk, g.sBn, g.sCb, g.sCm,
               g.alpha, g.relu);
@@ -1399,8 +1404,11 @@ struct Predictor {
   std::string unsupported;
   std::vector<std::string> applied_passes;
 
-  Predictor(const std::string& model_file, const std::string& params_file, int device, bool ir_optim = true)
-      : dev(device) {
+  bool bf16 = false;   // Config.EnableMkldnnBfloat16 (reference AnalysisConfig): bf16 matrix products
+
+  Predictor(const std::string& model_file, const std::string& params_file, int device, bool ir_optim = true,
+            bool bf16_ = false)
+      : dev(device), bf16(bf16_) {
     prog = parse_program(read_file(model_file));
     if (dev >= 0) gctx = gpu::create_context(dev);
     gpu::Bind bind(gctx);
@@ -1541,7 +1549,7 @@ struct Predictor {
       if (it == inputs.end()) throw Error("input " + n + " was not set");
       env[n] = it->second;
     }
-    Ctx c{dev, env};
+    Ctx c{dev, env, bf16};
     for (size_t i = 0; i < b.ops.size(); ++i) {
       const OpDesc& op = b.ops[i];
       if (op.type == "feed" || op.type == "fetch") continue;
@@ -1587,15 +1595,19 @@ int guard(F&& f) {
 
 extern "C" {
 
-PhaPredictor* pha_infer_create2(const char* model_file, const char* params_file, int device, int ir_optim) {
+PhaPredictor* pha_infer_create3(const char* model_file, const char* params_file, int device, int ir_optim,
+                                int bf16) {
   PhaPredictor* out = nullptr;
   guard([&] {
-    auto* pr = new Predictor(model_file, params_file ? params_file : "", device, ir_optim != 0);
+    auto* pr = new Predictor(model_file, params_file ? params_file : "", device, ir_optim != 0, bf16 != 0);
     std::string s;
     for (auto& x : pr->applied_passes) s += (s.empty() ? "" : ";") + x;
     out = new PhaPredictor{pr, s};
   });
   return out;
+}
+PhaPredictor* pha_infer_create2(const char* model_file, const char* params_file, int device, int ir_optim) {
+  return pha_infer_create3(model_file, params_file, device, ir_optim, 0);
 }
 PhaPredictor* pha_infer_create(const char* model_file, const char* params_file, int device) {
   return pha_infer_create2(model_file, params_file, device, 1);
@@ -1648,6 +1660,7 @@ struct PD_Config {
   bool gpu = false;
   int dev = 0;
   bool ir_optim = true;
+  bool bf16 = false;
 };
 struct PD_Predictor {
   PhaPredictor* p;
@@ -1662,6 +1675,10 @@ struct PD_Tensor {
 PD_Config* PD_ConfigCreate(void) { return new PD_Config(); }
 void PD_ConfigSwitchIrOptim(PD_Config* c, PD_Bool x) { c->ir_optim = x != 0; }
 PD_Bool PD_ConfigIrOptim(PD_Config* c) { return c->ir_optim; }
+// reference: AnalysisConfig::EnableMkldnnBfloat16 — here the GPU device path's matrix products
+// (mul / matmul / fc / convolutions) run with bf16 operands on the MFMA GEMM of libpha_kernels.so
+void PD_ConfigEnableMkldnnBfloat16(PD_Config* c) { c->bf16 = true; }
+PD_Bool PD_ConfigMkldnnBfloat16Enabled(PD_Config* c) { return c->bf16; }
 void PD_ConfigDestroy(PD_Config* c) { delete c; }
 void PD_ConfigSetModel(PD_Config* c, const char* prog, const char* params) {
   c->prog = prog;
@@ -1678,7 +1695,7 @@ PD_Bool PD_ConfigUseGpu(PD_Config* c) { return c->gpu; }
 int32_t PD_ConfigGpuDeviceId(PD_Config* c) { return c->dev; }
 
 PD_Predictor* PD_PredictorCreate(PD_Config* c) {
-  PhaPredictor* p = pha_infer_create2(c->prog.c_str(), c->params.c_str(), c->gpu ? c->dev : -1, c->ir_optim);
+  PhaPredictor* p = pha_infer_create3(c->prog.c_str(), c->params.c_str(), c->gpu ? c->dev : -1, c->ir_optim, c->bf16);
   delete c;
   if (!p) {
     std::fprintf(stderr, "PD_PredictorCreate: %s\n", g_err.c_str());

@@ -130,6 +130,13 @@ void d2d(void* dst, const void* src, size_t n);
 void gemm(const float* A, const float* B, float* C, const float* bias, int batch, int M, int N, int K,
           int64_t sAb, int64_t sAm, int64_t sAk, int64_t sBb, int64_t sBk, int64_t sBn, int64_t sCb, int64_t sCm,
           float alpha, bool relu);
+// the same product with bf16 operands on the kernel library's persistent MFMA GEMM (libpha_kernels.so
+// pha_gemm4p_batched, resolved next to this library): A / B converted to zero-padded bf16 images
+// (B as B^T [N][K], the NT layout), fp32 accumulation, bf16 result widened into C with alpha / bias
+// / ReLU. Returns false (nothing done) when the kernel library cannot be loaded.
+bool gemm_bf16(const float* A, const float* B, float* C, const float* bias, int batch, int M, int N, int K,
+               int64_t sAb, int64_t sAm, int64_t sAk, int64_t sBb, int64_t sBk, int64_t sBn, int64_t sCb,
+               int64_t sCm, float alpha, bool relu);
 // col [N][C*KH*KW][OH*OW] of N NCHW images
 void im2col(const float* x, float* col, int C, int H, int W, int KH, int KW, int OH, int OW, int sh, int sw, int pt,
             int pl, int dh, int dw, int N);

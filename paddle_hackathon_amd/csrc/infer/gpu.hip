@@ -6,6 +6,8 @@
 // softmax / layer_norm / elementwise in phi/kernels/gpu).
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -627,6 +629,127 @@ void gemm(const float* A, const float* B, float* C, const float* bias, int batch
   hipLaunchKernelGGL(gemm_kernel, grid, dim3(256), 0, cur_stream(), A, B, C, bias, M, N, K, sAb, sAm, sAk, sBb, sBk, sBn,
                      sCb, sCm, alpha, relu ? 1 : 0);
   ck_launch("gemm");
+}
+
+// ---- bf16 GEMM on the kernel library ---------------------------------------------------------------
+namespace {
+typedef int (*Gemm4pBatched)(int, const void*, const void*, void*, long, long, long, long, long, long, int, int, int,
+                             int, const float*, int, int, float*, int, hipStream_t, void*, int, long, long, long);
+
+Gemm4pBatched g4p_entry() {
+  static Gemm4pBatched fn = []() -> Gemm4pBatched {
+    Dl_info info{};
+    if (!dladdr(reinterpret_cast<void*>(&g4p_entry), &info) || !info.dli_fname) return nullptr;
+    std::string dir(info.dli_fname);
+    dir = dir.substr(0, dir.find_last_of('/') + 1);
+    void* h = dlopen((dir + "libpha_kernels.so").c_str(), RTLD_NOW | RTLD_GLOBAL);
+    return h ? reinterpret_cast<Gemm4pBatched>(dlsym(h, "pha_gemm4p_batched")) : nullptr;
+  }();
+  return fn;
+}
+
+// dst[b][r][c] (rows_p x cols_p, zero outside rows x cols) = bf16(src[b * sb + r * sr + c * sc])
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                      int rows, int cols, int rows_p, int cols_p, int64_t sb,
+                                                      int64_t sr, int64_t sc, int64_t total) {
+  for (int64_t i = blockIdx.x * 256L + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t per = (int64_t)rows_p * cols_p;
+    const int64_t b = i / per, rc = i - b * per;
+    const int r = (int)(rc / cols_p), c = (int)(rc - (int64_t)r * cols_p);
+    float v = 0.f;
+    if (r < rows && c < cols) v = src[b * sb + r * sr + c * sc];
+    uint32_t u = __float_as_uint(v);
+    u += 0x7fffu + ((u >> 16) & 1u);   // round to nearest even (finite inputs)
+    dst[i] = (uint16_t)(u >> 16);
+  }
+}
+
+// the same conversion when the source's unit stride runs along r (a B [K][N] operand turned into the
+// NT layout's B^T, or a transposed A): 64 x 64 tiles through LDS, so both the fp32 reads (along r)
+// and the bf16 writes (along c) are coalesced
+__global__ __launch_bounds__(256) void to_bf16_t_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                        int rows, int cols, int rows_p, int cols_p, int64_t sb,
+                                                        int64_t sc) {
+  __shared__ float tile[64][65];
+  const int64_t b = blockIdx.z;
+  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int j = ty; j < 64; j += 4) {
+    const int r = r0 + tx, c = c0 + j;
+    tile[j][tx] = (r < rows && c < cols) ? src[b * sb + (int64_t)c * sc + r] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 64; j += 4) {
+    const int r = r0 + j, c = c0 + tx;
+    if (r < rows_p && c < cols_p) {
+      uint32_t u = __float_as_uint(tile[tx][j]);
+      u += 0x7fffu + ((u >> 16) & 1u);
+      dst[(b * rows_p + r) * cols_p + c] = (uint16_t)(u >> 16);
+    }
+  }
+}
+
+void convert_bf16(const float* src, uint16_t* dst, int nbatch, int rows, int cols, int rows_p, int cols_p, int64_t sb,
+                  int64_t sr, int64_t sc) {
+  if (sr == 1 && sc != 1) {
+    hipLaunchKernelGGL(to_bf16_t_kernel, dim3((rows_p + 63) / 64, (cols_p + 63) / 64, nbatch), dim3(256), 0,
+                       cur_stream(), src, dst, rows, cols, rows_p, cols_p, sb, sc);
+  } else {
+    const int64_t n = (int64_t)nbatch * rows_p * cols_p;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks_for(n)), dim3(256), 0, cur_stream(), src, dst, rows, cols, rows_p,
+                       cols_p, sb, sr, sc, n);
+  }
+}
+
+// C[b][m][n] = relu(alpha * c16[b][m][n] + bias[n]) over the unpadded M x N
+__global__ __launch_bounds__(256) void from_bf16_kernel(const uint16_t* __restrict__ c16, float* __restrict__ C,
+                                                        const float* __restrict__ bias, int M, int N, int ldc,
+                                                        int64_t sb16, int64_t sCb, int64_t sCm, float alpha, int relu,
+                                                        int64_t total) {
+  for (int64_t i = blockIdx.x * 256L + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t per = (int64_t)M * N;
+    const int64_t b = i / per, mn = i - b * per;
+    const int m = (int)(mn / N), n = (int)(mn - (int64_t)m * N);
+    float v = alpha * __uint_as_float((uint32_t)c16[b * sb16 + (int64_t)m * ldc + n] << 16);
+    if (bias) v += bias[n];
+    if (relu && v < 0.f) v = 0.f;
+    C[b * sCb + (int64_t)m * sCm + n] = v;
+  }
+}
+}  // namespace
+
+bool gemm_bf16(const float* A, const float* B, float* C, const float* bias, int batch, int M, int N, int K,
+               int64_t sAb, int64_t sAm, int64_t sAk, int64_t sBb, int64_t sBk, int64_t sBn, int64_t sCb,
+               int64_t sCm, float alpha, bool relu) {
+  Gemm4pBatched fn = g4p_entry();
+  if (!fn || M <= 0 || N <= 0 || K <= 0 || batch <= 0) return false;
+  const int Mp = (M + 7) / 8 * 8, Np = (N + 7) / 8 * 8, Kp = (K + 63) / 64 * 64;
+  const int ba = sAb ? batch : 1, bb = sBb ? batch : 1;
+  const size_t na = (size_t)ba * Mp * Kp, nb = (size_t)bb * Np * Kp, nc = (size_t)batch * Mp * Np;
+  Context* cx = current();
+  if (ba > 65535 || bb > 65535) return false;
+  auto* a16 = static_cast<uint16_t*>(alloc(na * 2));
+  auto* b16 = static_cast<uint16_t*>(alloc(nb * 2));
+  auto* c16 = static_cast<uint16_t*>(alloc(nc * 2));
+  convert_bf16(A, a16, ba, M, K, Mp, Kp, sAb, sAm, sAk);
+  convert_bf16(B, b16, bb, N, K, Np, Kp, sBb, sBn, sBk);
+  ck_launch("to_bf16");
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cx->dev);
+  // NT (A [M][K], B^T [N][K]) with the early-release schedule, PIN + SPREAD DMA placement (LV 40, the
+  // training path's default: ops/gemm.py _epi_default)
+  const int epi = 65536 | (8 << 17) | (1 << 28);
+  const int rc = fn(1, a16, b16, c16, Mp, Np, Kp, Kp, Kp, Np, 0, 0, 0, epi, nullptr, cus, 0, nullptr, 1, cx->stream,
+                    nullptr, batch, ba > 1 ? (long)Mp * Kp : 0, bb > 1 ? (long)Np * Kp : 0, (long)Mp * Np);
+  if (rc != 0) throw Error("pha_gemm4p_batched failed (" + std::to_string(rc) + ")");
+  const int64_t tot = (int64_t)batch * M * N;
+  hipLaunchKernelGGL(from_bf16_kernel, dim3(blocks_for(tot)), dim3(256), 0, cur_stream(), c16, C, bias, M, N, Np,
+                     (int64_t)Mp * Np, sCb, sCm, alpha, relu ? 1 : 0, tot);
+  ck_launch("from_bf16");
+  release(cx, a16, na * 2);
+  release(cx, b16, nb * 2);
+  release(cx, c16, nc * 2);
+  return true;
 }
 
 void im2col(const float* x, float* col, int C, int H, int W, int KH, int KW, int OH, int OW, int sh, int sw, int pt,

@@ -43,6 +43,8 @@ int pha_infer_copy_output(const PhaPredictor* p, int i, void* dst, size_t bytes)
 const char* pha_infer_unsupported_ops(const PhaPredictor* p);
 // ir_optim = 0: run the program as written (no conv + elementwise_add / conv + batch_norm folding)
 PhaPredictor* pha_infer_create2(const char* model_file, const char* params_file, int device, int ir_optim);
+// bf16 != 0: the GPU path's matrix products run with bf16 operands on libpha_kernels.so's MFMA GEMM
+PhaPredictor* pha_infer_create3(const char* model_file, const char* params_file, int device, int ir_optim, int bf16);
 // the IR passes that rewrote the program at load ("conv_bn_fuse_pass x53;..."; "" when none)
 const char* pha_infer_applied_passes(const PhaPredictor* p);
 // device bytes held by the predictor's block pool (0 on the host)
@@ -66,6 +68,8 @@ typedef struct PD_OneDimArrayInt32 {
 PD_Config* PD_ConfigCreate(void);
 void PD_ConfigSwitchIrOptim(PD_Config* c, PD_Bool x);
 PD_Bool PD_ConfigIrOptim(PD_Config* c);
+void PD_ConfigEnableMkldnnBfloat16(PD_Config* c);
+PD_Bool PD_ConfigMkldnnBfloat16Enabled(PD_Config* c);
 void PD_ConfigDestroy(PD_Config* c);
 void PD_ConfigSetModel(PD_Config* c, const char* prog_file_path, const char* params_file_path);
 const char* PD_ConfigGetProgFile(PD_Config* c);

@@ -33,6 +33,8 @@ def _lib():
         L.pha_infer_create.restype = P
         L.pha_infer_create2.argtypes = [C, C, I, I]
         L.pha_infer_create2.restype = P
+        L.pha_infer_create3.argtypes = [C, C, I, I, I]
+        L.pha_infer_create3.restype = P
         L.pha_infer_applied_passes.argtypes = [P]
         L.pha_infer_applied_passes.restype = C
         L.pha_infer_pooled_bytes.argtypes = [P]
@@ -65,11 +67,14 @@ class NativePredictor:
     host, k >= 0 on GPU k (its own HIP stream and pooled device memory). ``run({name: ndarray})`` ->
     list of output ndarrays (fetch order). ``ir_optim`` folds conv + elementwise_add(bias) and conv +
     batch_norm at load (``applied_passes`` lists what fired). One predictor per thread (the
-    reference PredictorPool model); the ctypes calls release the GIL."""
+    reference PredictorPool model); the ctypes calls release the GIL. ``bf16`` (the reference's
+    ``Config.enable_mkldnn_bfloat16``): on the GPU the matrix products (mul / matmul / fc and the
+    im2col convolutions) run with bf16 operands on the kernel library's MFMA GEMM, fp32 elsewhere."""
 
-    def __init__(self, model_file, params_file, device=-1, ir_optim=True):
+    def __init__(self, model_file, params_file, device=-1, ir_optim=True, bf16=False):
         L = _lib()
-        self._h = L.pha_infer_create2(model_file.encode(), (params_file or "").encode(), int(device), int(bool(ir_optim)))
+        self._h = L.pha_infer_create3(model_file.encode(), (params_file or "").encode(), int(device),
+                                      int(bool(ir_optim)), int(bool(bf16)))
         if not self._h:
             raise RuntimeError(f"native predictor: {L.pha_infer_last_error().decode()}")
         self.input_names = [L.pha_infer_input_name(self._h, i).decode() for i in range(L.pha_infer_num_inputs(self._h))]

@@ -305,3 +305,61 @@ def test_native_resnet50_latency_log(tmp_path):
     np.testing.assert_allclose(out[0], ref[0], rtol=5e-2, atol=5e-2)
     print(f"\n[native-infer] ResNet-50 b8 fp32: native {t_nat * 1e3:.1f} ms ({nat.applied_passes}), "
           f"python predictor {t_py * 1e3:.1f} ms")
+
+
+def _relmax(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-6))
+
+
+@pytest.mark.gpu
+def test_native_gpu_bf16_matches_fp32(tmp_path):
+    """bf16 matrix products (NativePredictor(bf16=True) / PD_ConfigEnableMkldnnBfloat16: mul / matmul
+    / fc and the im2col convolutions on libpha_kernels.so's MFMA GEMM) against the fp32 device path
+    on the same files, within bf16 rounding"""
+    for name, m, p, feeds in _cases(tmp_path):
+        ref = NativePredictor(m, p, device=0).run(feeds)
+        pred = NativePredictor(m, p, device=0, bf16=True)
+        got = pred.run(feeds)
+        for g, r in zip(got, ref):
+            assert g.shape == r.shape
+            assert _relmax(g, r) < 3e-2, (name, _relmax(g, r))
+        again = pred.run(feeds)
+        for g, a in zip(got, again):
+            np.testing.assert_array_equal(g, a)
+
+
+@pytest.mark.gpu
+def test_native_bf16_latency_log(tmp_path):
+    """not a gate: ResNet-50 batch 8 and a BERT-base-sized encoder (4 layers, batch 8 x seq 128) on
+    the native GPU predictor, fp32 vs bf16 matrix products, for the log"""
+    import time
+    from paddle_hackathon_amd.vision.models import resnet50
+
+    class Enc(nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.enc = nn.TransformerEncoder(nn.TransformerEncoderLayer(768, 12, 3072, dropout=0.0,
+                                                                        activation="gelu"), 4)
+
+        def forward(self, x):
+            return self.enc(x)
+    paddle.seed(0)
+    rs = np.random.RandomState(0)
+    cases = [("ResNet-50 b8", _save(tmp_path, resnet50(), [InputSpec([None, 3, 224, 224], "float32", "x")], "r50"),
+              {"x": rs.randn(8, 3, 224, 224).astype("float32")}),
+             ("encoder-768x4 b8 s128", _save(tmp_path, Enc(), [InputSpec([None, 128, 768], "float32", "x")], "enc768"),
+              {"x": rs.randn(8, 128, 768).astype("float32")})]
+    for name, (m, p), feeds in cases:
+        res = {}
+        for bf in (False, True):
+            pred = NativePredictor(m, p, device=0, bf16=bf)
+            out = pred.run(feeds)
+            t0 = time.perf_counter()
+            for _ in range(5):
+                out = pred.run(feeds)
+            res[bf] = ((time.perf_counter() - t0) / 5, out)
+        err = _relmax(res[True][1][0], res[False][1][0])
+        print(f"\n[native-infer] {name}: fp32 {res[False][0] * 1e3:.2f} ms, bf16 {res[True][0] * 1e3:.2f} ms "
+              f"(max |bf16 - fp32| / max |fp32| = {err:.2e})")
+        assert err < 5e-2
