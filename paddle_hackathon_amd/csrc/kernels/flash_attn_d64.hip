@@ -2,7 +2,8 @@
 // in-kernel dropout of the probabilities and packed-QKV strides. Reference behaviour:
 // paddle/fluid/operators/fused/fmha_ref.h:87-172 (softmax(Q K^T / sqrt(d)) with dropout, then P V)
 // and its backward in fused_attention_op.cu; the dropout mask is the counter hash of fa_common.h
-// (seed, b*H + h, query, key), so these kernels and the generic 4-wave ones regenerate the same mask.
+// (seed, b*H + h, query, key) with a cheaper per-key draw (fa64_draw); the forward stores the keep bits
+// for the backward.
 //
 // Why separate kernels. The generic 4-wave kernels (flash_attn.hip fa_*_kernel<T, 64, ..>) stage
 // K / V through registers with a software transpose of V (u16 shuffles per element), take two
@@ -43,6 +44,37 @@ __device__ __forceinline__ void dma64(const T* base, long rs, int r0, int rmax, 
   glds64(voff, base + (long)r0 * rs, __builtin_amdgcn_readfirstlane(lds + p * 1024));
 }
 
+// the keep draw of these kernels: one 32-bit hash per key pair (16 bits per key against the
+// threshold) of (row seed + key / 2 * odd 24-bit constant) — one full-rate 24-bit and one 32-bit
+// multiply per draw instead of fa_keep's two 32-bit ones (the forward is the only place it runs when
+// the backward reads the stored keep bits; the re-hashing backward uses the same function)
+__device__ __forceinline__ unsigned fa64_draw(unsigned row, int key) {
+  unsigned x = row + __umul24((unsigned)(key >> 1), 0x9e3779u);
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  return x;
+}
+__device__ __forceinline__ bool fa64_keep(unsigned row, int key, unsigned thresh) {
+  const unsigned r = fa64_draw(row, key);
+  return ((key & 1) ? (r >> 16) : (r & 0xffffu)) >= thresh;
+}
+
+// additive score bias (natural-log units, key stride 1) of the lane's 16 keys of a 32-key block
+// (query on the lane: keys base + 8m + 4h + {0..3} are one float4), divided by the softmax scale so it
+// can start the unscaled S^T accumulator; keys past Sk read the last aligned quad (masked anyway)
+__device__ __forceinline__ void bias16(const float* brow, int base, int Sk, float inv_scale, f32x16& acc) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int k = min(base + 8 * m, Sk - 4);
+    const float4 v = *reinterpret_cast<const float4*>(brow + k);
+    acc[4 * m + 0] = v.x * inv_scale;
+    acc[4 * m + 1] = v.y * inv_scale;
+    acc[4 * m + 2] = v.z * inv_scale;
+    acc[4 * m + 3] = v.w * inv_scale;
+  }
+}
+
 __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(size_t)(__attribute__((address_space(3))) const unsigned char*)p;
 }
@@ -71,7 +103,7 @@ __device__ __forceinline__ u32x4 trA(const unsigned char* img, const int (&troff
 // per 64-key tile S^T = K Q^T (2 x 4 MFMAs), online softmax (deferred rescale), dropout on P for
 // the P V product only (the row sum is undropped), O^T += V^T P^T (4 x 2 MFMAs)
 // ============================================================================================
-template <typename T, bool CAUSAL, bool DROP>
+template <typename T, bool CAUSAL, bool DROP, bool BIAS = false>
 __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T* __restrict__ K,
                                                 const T* __restrict__ V, T* __restrict__ O, float* __restrict__ LSE,
                                                 int S, int Sk, int H, int Hk, float scale_log2, FaStrides fs, FaExt ex) {
@@ -97,6 +129,8 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
   }
   unsigned drow = 0;
   if constexpr (DROP) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
+  const float inv_scale = kLog2e / scale_log2;
+  const float* brow = BIAS ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)min(q, S - 1) * ex.sq : nullptr;
   f32x16 o[2];
   o[0] = zero16();
   o[1] = zero16();
@@ -129,8 +163,13 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
     const unsigned char* vl = kl + IMG64;
     if (!(CAUSAL && k0 > wq0 + 31)) {
       f32x16 s[2];
-      s[0] = zero16();
-      s[1] = zero16();
+      if constexpr (BIAS) {   // the bias / scale as the S^T chain's initial value
+        bias16(brow, k0 + 4 * h, Sk, inv_scale, s[0]);
+        bias16(brow, k0 + 32 + 4 * h, Sk, inv_scale, s[1]);
+      } else {
+        s[0] = zero16();
+        s[1] = zero16();
+      }
       if ((k0 + 64 > Sk) || (CAUSAL && k0 + 63 > wq0)) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
@@ -139,7 +178,7 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rb = (r & 3) + 8 * (r >> 2);
-            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : 0.f;
+            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : s[kb][r];
           }
         }
       }
@@ -187,7 +226,7 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kb * 32 + acc_row(r, h);
-            const bool kp = fa_keep(drow, key, ex.thresh);
+            const bool kp = fa64_keep(drow, key, ex.thresh);
             wb[kb] |= (unsigned)kp << acc_row(r, h);
             s[kb][r] = kp ? s[kb][r] * ex.keep_scale : 0.f;
           }
@@ -237,7 +276,7 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
 //   P^T = exp2(c S^T - lse), dS^T = P^T (Z dP^T / (1 - rate) - delta), dQ^T += K^T dS^T (transposed
 //   reads of the K image, dS^T packed as the B operand)
 // ============================================================================================
-template <typename T, bool CAUSAL, int DR>
+template <typename T, bool CAUSAL, int DR, bool BIAS = false>
 __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T* __restrict__ K,
                                                const T* __restrict__ V, const T* __restrict__ dO,
                                                const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -265,9 +304,11 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
   }
   const float c2 = scale * kLog2e;
   const float nl = -LSE[(long)bh * S + qc] * kLog2e, del = DELTA[(long)bh * S + qc];
+  const unsigned ksb = __float_as_uint(ex.keep_scale);
   unsigned drow = 0;
   if constexpr (DR == 1) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
   const unsigned* mrow = DR == 2 ? ex.dmask + ((long)bh * S + qc) * ex.dmask_w : nullptr;
+  const float* brow = BIAS ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)qc * ex.sq : nullptr;
   f32x16 dqt[2];
   dqt[0] = zero16();
   dqt[1] = zero16();
@@ -303,8 +344,12 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         dp[kb] = zero16();
+        if constexpr (BIAS) {
+          bias16(brow, k0 + kb * 32 + 4 * h, Sk, 1.f / scale, s[kb]);
+        } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+          for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+        }
       }
       if ((k0 + 64 > Sk) || (CAUSAL && k0 + 63 > wq0)) {
 #pragma unroll
@@ -314,7 +359,7 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rb = (r & 3) + 8 * (r >> 2);
-            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : 0.f;
+            s[kb][r] = ((rb > lim1) | (rb >= lim2)) ? -INFINITY : s[kb][r];
           }
         }
       }
@@ -332,14 +377,15 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = fexp2(fmaf(s[kb][r], c2, nl));
-          float g = dp[kb][r];
-          if constexpr (DR == 1) {
-            const int key = k0 + kb * 32 + acc_row(r, h);
-            g = fa_keep(drow, key, ex.thresh) ? g * ex.keep_scale : 0.f;
-          } else if constexpr (DR == 2) {
-            g = ((mw[kb] >> acc_row(r, h)) & 1u) ? g * ex.keep_scale : 0.f;
+          const float g = dp[kb][r];
+          if constexpr (DR != 0) {   // keep multiplier as in the dK/dV kernel
+            unsigned bit;
+            if constexpr (DR == 2) bit = __builtin_amdgcn_ubfe(mw[kb], (unsigned)acc_row(r, h), 1u);
+            else bit = fa64_keep(drow, k0 + kb * 32 + acc_row(r, h), ex.thresh) ? 1u : 0u;
+            s[kb][r] = p * fmaf(g, __uint_as_float((0u - bit) & ksb), -del);
+          } else {
+            s[kb][r] = p * (g - del);
           }
-          s[kb][r] = p * (g - del);
         }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -384,7 +430,7 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 // ============================================================================================
 constexpr int RC64 = 3 * 64 * 4 + 8 * 64 * 4;   // -lse/scale, -delta, row seeds, keep bits [8 words][64 rows]
 
-template <typename T, bool CAUSAL, int DR>
+template <typename T, bool CAUSAL, int DR, bool BIAS = false>
 __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const T* __restrict__ K,
                                                  const T* __restrict__ V, const T* __restrict__ dO,
                                                  const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -406,10 +452,15 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   const float* del_b = DELTA + (long)bh * S;
   const float c2 = scale * kLog2e, nis = -1.f / scale;
   constexpr bool DROP = DR != 0;
+  const unsigned ksb = __float_as_uint(ex.keep_scale);
   unsigned dstream = 0;
   if constexpr (DR == 1) dstream = fa_stream(fa_seed(ex), b * H + head);
 
   const int keyc = min(key, Sk - 1);
+  // additive bias column of this lane's key (key-padding masks: one value for every query)
+  const float inv_sc = 1.f / scale;
+  const float* bcol = BIAS ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + keyc : nullptr;
+  const float bkey = (BIAS && ex.sq == 0) ? bcol[0] * inv_sc : 0.f;
   frag kf[4], vf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
@@ -501,6 +552,15 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
           da[4 * m + 0] = d4.x; da[4 * m + 1] = d4.y; da[4 * m + 2] = d4.z; da[4 * m + 3] = d4.w;
         }
       }
+      if constexpr (BIAS) {   // + bias / scale of (query row, this lane's key)
+        if (ex.sq == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sa[r] += bkey;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sa[r] += bcol[(long)min(qh + acc_row(r, h), S - 1) * ex.sq] * inv_sc;
+        }
+      }
       if ((qh + 32 > S) || (wk0 + 32 > Sk) || (CAUSAL && wk0 + 31 > qh)) {
         const int lim = key >= Sk ? 32 : (CAUSAL ? key - qh - 4 * h : -1);
         const int lim2 = S - qh - 4 * h;
@@ -517,16 +577,15 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
         sa = MF<T>::mma(as_frag<frag>(qa), kf[kk], sa);
         da = MF<T>::mma(as_frag<frag>(ga), vf[kk], da);
       }
-      // dropout draws: lanes 2i, 2i+1 hold keys 2m, 2m+1, and fa_keep takes both keys' 16-bit
+      // dropout draws: lanes 2i, 2i+1 hold keys 2m, 2m+1, and fa64_keep takes both keys' 16-bit
       // halves from ONE 32-bit hash of (row seed ^ key / 2): each lane of the pair hashes 8 of the
       // 16 rows and the pair swaps results (DPP quad_perm 1,0,3,2) — half the multiply-heavy hashes
       unsigned rnd[16];
       if constexpr (DR == 1) {
         const bool odd = lane & 1;
-        const unsigned kx = (unsigned)(key >> 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const unsigned mine = fa_mix((odd ? sd[i + 8] : sd[i]) ^ kx);
+          const unsigned mine = fa64_draw(odd ? sd[i + 8] : sd[i], key);
           const unsigned other = (unsigned)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false);
           rnd[i] = odd ? other : mine;
           rnd[i + 8] = odd ? mine : other;
@@ -536,10 +595,14 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
       for (int r = 0; r < 16; ++r) {
         const float p = fexp2(sa[r] * c2);
         if constexpr (DROP) {
-          const bool kp = DR == 2 ? ((sd[r] >> lr) & 1u) != 0
-                                  : ((lane & 1) ? (rnd[r] >> 16) : (rnd[r] & 0xffffu)) >= ex.thresh;   // = fa_keep(sd[r], key, ..)
-          sa[r] = kp ? p * ex.keep_scale : 0.f;
-          da[r] = p * ((kp ? da[r] * ex.keep_scale : 0.f) + dl[r]);
+          // the keep decision as a multiplier m = keep ? 1 / (1 - rate) : 0, built from the bit with an
+          // AND on the scale's bits (no compare / select per element; both DR paths identical arithmetic)
+          unsigned bit;
+          if constexpr (DR == 2) bit = __builtin_amdgcn_ubfe(sd[r], (unsigned)lr, 1u);
+          else bit = ((lane & 1) ? (rnd[r] >> 16) : (rnd[r] & 0xffffu)) >= ex.thresh ? 1u : 0u;   // = fa64_keep
+          const float m = __uint_as_float((0u - bit) & ksb);
+          sa[r] = p * m;
+          da[r] = p * fmaf(da[r], m, dl[r]);
         } else {
           sa[r] = p;
           da[r] = p * da[r];
@@ -586,20 +649,28 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   }
 }
 
+template <typename T, bool C, int DR, bool BI>
+void launch64b(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
+               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
+               const FaStrides& fs, const FaExt& ex, hipStream_t st) {
+  const dim3 gq((S + 255) / 256, B * H), gk((Sk + 255) / 256, B * H), blk(512);
+  if (!bwd) {
+    hipLaunchKernelGGL((fa64_fwd<T, C, DR != 0, BI>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse,
+                       S, Sk, H, Hk, scale * kLog2e, fs, ex);
+    return;
+  }
+  hipLaunchKernelGGL((fa64_dkdv<T, C, DR, BI>), gk, blk, 0, st, (const T*)q, (const T*)k, (const T*)v,
+                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
+  hipLaunchKernelGGL((fa64_dq<T, C, DR, BI>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
+                     lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs, ex);
+}
+
 template <typename T, bool C, int DR>
 void launch64(bool bwd, const void* q, const void* k, const void* v, void* o, float* lse, const void* dout,
               const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk, float scale,
               const FaStrides& fs, const FaExt& ex, hipStream_t st) {
-  const dim3 gq((S + 255) / 256, B * H), gk((Sk + 255) / 256, B * H), blk(512);
-  if (!bwd) {
-    hipLaunchKernelGGL((fa64_fwd<T, C, DR != 0>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, S, Sk,
-                       H, Hk, scale * kLog2e, fs, ex);
-    return;
-  }
-  hipLaunchKernelGGL((fa64_dkdv<T, C, DR>), gk, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
-                     lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
-  hipLaunchKernelGGL((fa64_dq<T, C, DR>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
-                     lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs, ex);
+  if (ex.bias) launch64b<T, C, DR, true>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
+  else launch64b<T, C, DR, false>(bwd, q, k, v, o, lse, dout, delta, dq, dk, dv, B, S, Sk, H, Hk, scale, fs, ex, st);
 }
 
 template <typename T>
@@ -625,6 +696,13 @@ bool check64(const void* q, const void* k, const void* v, int S, int Sk, int H, 
   // the DMA's 32-bit offsets: 64 rows of the widest row stride
   return 64.0 * (double)(q_tok > kv_tok ? (q_tok > o_tok ? q_tok : o_tok) : (kv_tok > o_tok ? kv_tok : o_tok)) * 2 <
          4294967295.0;
+}
+
+// the bias rows are read as float4 quads of keys: 16-B aligned, key count and row strides in quads
+bool bias_ok(const float* bias, int Sk, long sb, long sh, long sq) {
+  if (!bias) return true;
+  return ((size_t)bias & 15) == 0 && Sk % 4 == 0 && sb % 4 == 0 && sh % 4 == 0 && sq % 4 == 0 && sb >= 0 && sh >= 0 &&
+         sq >= 0;
 }
 
 FaStrides strides64(long q_tok, int q_head, long kv_tok, int kv_head, long o_tok, int o_head) {
@@ -653,11 +731,11 @@ PHA_API int pha_fa64_mask_words(int Sk) { return 8 * ((Sk + 255) / 256); }
 PHA_API int pha_fa64_fwd(int dt, const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Sk,
                          int H, int Hk, float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head,
                          long o_tok, int o_head, float dropout, unsigned seed, const unsigned* seedp,
-                         hipStream_t stream, unsigned* dmask) {
+                         hipStream_t stream, unsigned* dmask, const float* bias, long sb, long sh, long sq) {
   if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
-      ((size_t)o & 7) || ((size_t)dmask & 15))
+      ((size_t)o & 7) || ((size_t)dmask & 15) || !bias_ok(bias, Sk, sb, sh, sq))
     return (int)hipErrorInvalidValue;
-  FaExt ex{nullptr, 0, 0, 0, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
   ex.seedp = seedp;
   ex.dmask = dropout > 0.f ? dmask : nullptr;
   ex.dmask_w = pha_fa64_mask_words(Sk);
@@ -679,12 +757,13 @@ PHA_API int pha_fa64_bwd(int dt, const void* q, const void* k, const void* v, co
                          const float* delta, void* dq, void* dk, void* dv, int B, int S, int Sk, int H, int Hk,
                          float scale, int causal, long q_tok, int q_head, long kv_tok, int kv_head, long o_tok,
                          int o_head, long gq_tok, int gq_head, long gkv_tok, int gkv_head, float dropout,
-                         unsigned seed, const unsigned* seedp, hipStream_t stream, const unsigned* dmask) {
+                         unsigned seed, const unsigned* seedp, hipStream_t stream, const unsigned* dmask,
+                         const float* bias, long sb, long sh, long sq) {
   if (B <= 0 || !check64(q, k, v, S, Sk, H, Hk, q_tok, q_head, kv_tok, kv_head, o_tok, o_head, dropout) ||
       ((size_t)dout & 15) || ((size_t)dq & 7) || ((size_t)dk & 7) || ((size_t)dv & 7) || (gq_tok | gkv_tok) % 4 ||
-      (gq_head | gkv_head) % 4)
+      (gq_head | gkv_head) % 4 || !bias_ok(bias, Sk, sb, sh, sq))
     return (int)hipErrorInvalidValue;
-  FaExt ex{nullptr, 0, 0, 0, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
+  FaExt ex{bias, sb, sh, sq, seed, (unsigned)(dropout * 65536.f + 0.5f), dropout > 0.f ? 1.f / (1.f - dropout) : 1.f};
   ex.seedp = seedp;
   ex.gq_tok = gq_tok;
   ex.gq_head = gq_head;

@@ -690,23 +690,35 @@ def _fa_bias(mask, B, H, S, Sk, device):
     return mask, (mask.stride(0), mask.stride(1), mask.stride(2))
 
 
-def _fa64_on(D, mask):
-    """head dim 64 without an additive mask: the 8-wave LDS-DMA kernels of flash_attn_d64.hip
-    (packed strides, in-kernel dropout with the generic kernels' mask stream); PHA_FA64=0 keeps the
-    generic 4-wave kernels"""
+def _fa64_on(D, mask, Sk=None):
+    """head dim 64: the 8-wave LDS-DMA kernels of flash_attn_d64.hip (packed strides, in-kernel
+    dropout whose keep bits the forward stores for the backward, an additive mask read as float4 key
+    quads: Sk % 4 == 0); PHA_FA64=0 keeps the generic 4-wave kernels"""
     import os
     L = _lib.lib
-    return (D == 64 and mask is None and L is not None and hasattr(L, "pha_fa64_fwd")
-            and os.environ.get("PHA_FA64", "1") != "0")
+    return (D == 64 and (mask is None or (Sk is not None and Sk % 4 == 0)) and L is not None
+            and hasattr(L, "pha_fa64_fwd") and os.environ.get("PHA_FA64", "1") != "0")
+
+
+def _fa64_bias(mask, B, H, S, Sk, device):
+    """(bias view, (sb, sh, sq)) for the D = 64 kernels, or (None, (0, 0, 0))"""
+    if mask is None:
+        return None, (0, 0, 0)
+    bias, st = _fa_bias(mask, B, H, S, Sk, device)
+    if bias.data_ptr() % 16 or any(x % 4 for x in st):
+        bias = bias.contiguous()
+        st = (bias.stride(0), bias.stride(1), bias.stride(2))
+    return bias, st
 
 
 def _fa64_sig(L):
     if not getattr(L, "_fa64_sig", False):
         P, I, LG, F, U = c_void_p, c_int, c_long, c_float, ctypes.c_uint
-        L.pha_fa64_fwd.argtypes = [I, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, F, U, P, P, P]
+        L.pha_fa64_fwd.argtypes = [I, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, F, U, P, P, P,
+                                   P, LG, LG, LG]
         L.pha_fa64_fwd.restype = c_int
         L.pha_fa64_bwd.argtypes = [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, LG, I, LG, I, LG, I, LG, I,
-                                   LG, I, F, U, P, P, P]
+                                   LG, I, F, U, P, P, P, P, LG, LG, LG]
         L.pha_fa64_mask_words.argtypes = [I]
         L.pha_fa64_mask_words.restype = c_int
         L.pha_fa64_bwd.restype = c_int
@@ -714,7 +726,8 @@ def _fa64_sig(L):
     return L
 
 
-def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_, dropout_p, seed, seed_dev, st):
+def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_, dropout_p, seed, seed_dev, st,
+              bias=None, bst=(0, 0, 0)):
     """qs / kvs / os_: (token, head) element strides of q, k / v and o. With dropout, returns the keep
     mask as bits (int32 [B * H * S * words]) for the backward — the reference fused attention keeps
     its dropout mask too (fmha_ref.h dropout_mask_out); PHA_FA64_MASKBITS=0 re-hashes instead"""
@@ -724,17 +737,19 @@ def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_,
     if dropout_p and os.environ.get("PHA_FA64_MASKBITS", "1") != "0":
         dmask = torch.empty(B * H * S * L.pha_fa64_mask_words(Sk), dtype=torch.int32, device=o.device)
     _check(L.pha_fa64_fwd(dt, qp, kp, vp, _ptr(o), _ptr(lse), B, S, Sk, H, Hk, sc, int(causal), qs[0], qs[1], kvs[0],
-                          kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask)),
+                          kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask),
+                          _ptr(bias), bst[0], bst[1], bst[2]),
            "fa64_fwd")
     return dmask
 
 
 def _fa64_bwd(dt, qp, kp, vp, do, lse, delta, dqp, dkp, dvp, B, S, Sk, H, Hk, sc, causal, qs, kvs, gqs, gkvs,
-              dropout_p, seed, seed_dev, st, dmask=None):
+              dropout_p, seed, seed_dev, st, dmask=None, bias=None, bst=(0, 0, 0)):
     L = _fa64_sig(_L())
     _check(L.pha_fa64_bwd(dt, qp, kp, vp, _ptr(do), _ptr(lse), _ptr(delta), dqp, dkp, dvp, B, S, Sk, H, Hk, sc,
                           int(causal), qs[0], qs[1], kvs[0], kvs[1], H * 64, 64, gqs[0], gqs[1], gkvs[0], gkvs[1],
-                          float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask)), "fa64_bwd")
+                          float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask), _ptr(bias), bst[0], bst[1],
+                          bst[2]), "fa64_bwd")
 
 
 class FlashAttentionExt(torch.autograd.Function):
@@ -752,12 +767,14 @@ class FlashAttentionExt(torch.autograd.Function):
         seed, seed_dev = dropout_seed(q.device) if dropout_p else (0, None)
         o = torch.empty_like(q)
         lse = torch.empty((B, H, S), dtype=torch.float32, device=q.device)
-        ctx.fa64 = _fa64_on(D, mask)
+        ctx.fa64 = _fa64_on(D, mask, Sk)
         if ctx.fa64:
+            b64, bst = _fa64_bias(mask, B, H, S, Sk, q.device)
             ctx.dmask = _fa64_fwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), o, lse, B, S, Sk, H, Hk, sc, causal,
-                                  (H * D, D), (Hk * D, D), (H * D, D), dropout_p, seed, seed_dev, _stream(q))
+                                  (H * D, D), (Hk * D, D), (H * D, D), dropout_p, seed, seed_dev, _stream(q),
+                                  b64, bst)
             ctx.save_for_backward(q, k, v, o, lse)
-            ctx.bias, ctx.strides, ctx.seed, ctx.seed_dev = None, (0, 0, 0), seed, seed_dev
+            ctx.bias, ctx.strides, ctx.seed, ctx.seed_dev = b64, bst, seed, seed_dev
             ctx.causal, ctx.scale, ctx.dropout_p = causal, sc, float(dropout_p)
             return o
         L = _L()
@@ -794,7 +811,7 @@ class FlashAttentionExt(torch.autograd.Function):
         if getattr(ctx, "fa64", False):
             _fa64_bwd(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), do, lse, delta, _ptr(dq), _ptr(dk), _ptr(dv), B, S, Sk,
                       H, Hk, ctx.scale, ctx.causal, (H * D, D), (Hk * D, D), (0, 0), (0, 0), ctx.dropout_p, ctx.seed,
-                      ctx.seed_dev, _stream(q), ctx.dmask)
+                      ctx.seed_dev, _stream(q), ctx.dmask, ctx.bias, ctx.strides)
         else:
             sb, sh, sq = ctx.strides
             _check(L.pha_flash_attn_bwd_ext(_DT[q.dtype], _ptr(q), _ptr(k), _ptr(v), _ptr(do), _ptr(lse), _ptr(delta),
@@ -819,16 +836,18 @@ class FlashAttentionExtPacked(torch.autograd.Function):
     def forward(ctx, qkv, causal, scale, mask, dropout_p):
         B, S, H, D3 = qkv.shape
         D = D3 // 3
-        ctx.fa64p = _fa64_on(D, mask) and qkv.is_contiguous()
+        ctx.fa64p = _fa64_on(D, mask, S) and qkv.is_contiguous()
         if ctx.fa64p:   # head dim 64: the kernels read q | k | v in place (no slice copies)
             sc = float(scale) if scale is not None else 1.0 / float(np.sqrt(D))
             seed, seed_dev = dropout_seed(qkv.device) if dropout_p else (0, None)
             o = torch.empty((B, S, H, D), dtype=qkv.dtype, device=qkv.device)
             lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
             es, base = qkv.element_size(), qkv.data_ptr()
+            b64, bst = _fa64_bias(mask, B, H, S, S, qkv.device)
             ctx.dmask = _fa64_fwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es),
                                   c_void_p(base + 2 * D * es), o, lse, B, S, S, H, H, sc, causal, (3 * H * D, 3 * D),
-                                  (3 * H * D, 3 * D), (H * D, D), dropout_p, seed, seed_dev, _stream(qkv))
+                                  (3 * H * D, 3 * D), (H * D, D), dropout_p, seed, seed_dev, _stream(qkv), b64, bst)
+            ctx.b64, ctx.bst = b64, bst
             ctx.save_for_backward(qkv, o, lse)
             ctx.seed, ctx.seed_dev, ctx.causal, ctx.scale, ctx.dropout_p = seed, seed_dev, causal, sc, float(dropout_p)
             return o
@@ -853,7 +872,8 @@ class FlashAttentionExtPacked(torch.autograd.Function):
             st = (3 * H * D, 3 * D)
             _fa64_bwd(_DT[qkv.dtype], c_void_p(base), c_void_p(base + D * es), c_void_p(base + 2 * D * es), do, lse,
                       delta, c_void_p(gb), c_void_p(gb + D * es), c_void_p(gb + 2 * D * es), B, S, S, H, H, ctx.scale,
-                      ctx.causal, st, st, st, st, ctx.dropout_p, ctx.seed, ctx.seed_dev, _stream(qkv), ctx.dmask)
+                      ctx.causal, st, st, st, st, ctx.dropout_p, ctx.seed, ctx.seed_dev, _stream(qkv), ctx.dmask,
+                      ctx.b64, ctx.bst)
             return g, None, None, None, None
         q, k, v, o, lse = ctx.saved_tensors
         do = do.contiguous()
