@@ -140,7 +140,7 @@ struct FaExt {
   // hipGraph replays: a device word xor-ed into seed (bumped by a captured kernel every replay, so
   // each replay draws a new mask; the backward reads the forward's copy). null: seed alone
   const unsigned* seedp = nullptr;
-  // head-dim-64 kernels: the forward's keep mask as bits [B*H][S][dmask_w] (word w of a row: keys
+  // head-dim-64 kernels: the forward's keep mask as bits [B*H][dmask_w][S up to 64] (word w: keys
   // 32w .. 32w + 31), read by the backward instead of re-hashing; null: the backward regenerates it
   unsigned* dmask = nullptr;
   int dmask_w = 0;

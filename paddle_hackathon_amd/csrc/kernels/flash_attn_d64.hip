@@ -21,6 +21,7 @@
 //    touch LDS); masks as -inf initial accumulators; row constants (-lse / scale, -delta) as the
 //    initial accumulators of the dK/dV kernel's S / dP chains (CDNA guide App. B).
 #include "fa_common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -220,20 +221,36 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
       psum += __shfl_xor(psum, 32, 64);
       l_run += psum;
       if constexpr (DROP) {
-        unsigned wb[2] = {0u, 0u};
+        // fa64_keep of the lane's 32 keys, one hash per (even, odd) key pair: registers r, r + 1 hold
+        // keys 2m, 2m + 1, whose draws are the low / high halves of fa64_draw(row, 2m); the odd key's
+        // test x >> 16 >= thresh is the full-word x >= thresh << 16. The keep scale 1 / (1 - rate) is
+        // applied once to the output instead of per element. Keep bits are shifted in (bit r: register
+        // r), then spread to key positions acc_row(r, h) = (r & 3) + 8 (r >> 2) + 4 h.
+        unsigned wb[2];
+        const unsigned t16 = ex.thresh << 16;
+        const unsigned rk = drow + (unsigned)((k0 + 4 * h) >> 1) * 0x9e3779u;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb) {
+          unsigned bits = 0;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kb * 32 + acc_row(r, h);
-            const bool kp = fa64_keep(drow, key, ex.thresh);
-            wb[kb] |= (unsigned)kp << acc_row(r, h);
-            s[kb][r] = kp ? s[kb][r] * ex.keep_scale : 0.f;
+          for (int pr = 7; pr >= 0; --pr) {
+            const int r = 2 * pr;
+            unsigned x = rk + (unsigned)(kb * 16 + (pr & 1) + 4 * (pr >> 1)) * 0x9e3779u;
+            x ^= x >> 16;
+            x *= 0x7feb352du;
+            x ^= x >> 15;
+            const bool klo = (x & 0xffffu) >= ex.thresh, khi = x >= t16;
+            bits = 4 * bits + 2 * (unsigned)khi + (unsigned)klo;
+            s[kb][r] = klo ? s[kb][r] : 0.f;
+            s[kb][r + 1] = khi ? s[kb][r + 1] : 0.f;
           }
-        if (ex.dmask) {   // the two 32-key words of this tile: lane half h stores word h
+          wb[kb] = ((bits & 0xfu) | (bits & 0xf0u) << 4 | (bits & 0xf00u) << 8 | (bits & 0xf000u) << 12) << (4 * h);
+        }
+        if (ex.dmask) {   // the two 32-key words of this tile: lane half h stores word h of its 32
+          // queries — [word][query] layout, so each half-wave writes 128 contiguous bytes
           const unsigned w0 = wb[0] | (unsigned)__shfl_xor((int)wb[0], 32, 64);
           const unsigned w1 = wb[1] | (unsigned)__shfl_xor((int)wb[1], 32, 64);
-          if (q < S) ex.dmask[((long)bh * S + q) * ex.dmask_w + 2 * t + h] = h ? w1 : w0;
+          if (q < S) ex.dmask[((long)bh * ex.dmask_w + 2 * t + h) * ((S + 63) & ~63) + q] = h ? w1 : w0;
         }
       }
 #pragma unroll
@@ -254,7 +271,7 @@ __global__ __launch_bounds__(512) void fa64_fwd(const T* __restrict__ Q, const T
     __syncthreads();
   }
   if (q < S) {
-    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    const float inv = l_run > 0.f ? (DROP ? ex.keep_scale : 1.f) / l_run : 0.f;
     T* orow = O + ((long)b * S + q) * fs.o_tok + (long)head * fs.o_head;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
@@ -307,7 +324,8 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
   const unsigned ksb = __float_as_uint(ex.keep_scale);
   unsigned drow = 0;
   if constexpr (DR == 1) drow = fa_row(fa_stream(fa_seed(ex), b * H + head), q);
-  const unsigned* mrow = DR == 2 ? ex.dmask + ((long)bh * S + qc) * ex.dmask_w : nullptr;
+  const long msp = (S + 63) & ~63;   // the keep words' row pitch ([B * H][words][msp])
+  const unsigned* mrow = DR == 2 ? ex.dmask + (long)bh * ex.dmask_w * msp + qc : nullptr;
   const float* brow = BIAS ? ex.bias + (long)b * ex.sb + (long)head * ex.sh + (long)qc * ex.sq : nullptr;
   f32x16 dqt[2];
   dqt[0] = zero16();
@@ -339,7 +357,10 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
     const unsigned char* vl = kl + IMG64;
     if (!(CAUSAL && k0 > wq0 + 31)) {
       u32x2 mw = {0u, 0u};
-      if constexpr (DR == 2) mw = *reinterpret_cast<const u32x2*>(mrow + 2 * t);
+      if constexpr (DR == 2) {
+        mw[0] = mrow[(2 * t) * msp];
+        mw[1] = mrow[(2 * t + 1) * msp];
+      }
       f32x16 s[2], dp[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -430,8 +451,8 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
 // ============================================================================================
 constexpr int RC64 = 3 * 64 * 4 + 8 * 64 * 4;   // -lse/scale, -delta, row seeds, keep bits [8 words][64 rows]
 
-template <typename T, bool CAUSAL, int DR, bool BIAS = false>
-__global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const T* __restrict__ K,
+template <typename T, bool CAUSAL, int DR, bool BIAS = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void fa64_dkdv(const T* __restrict__ Q, const T* __restrict__ K,
                                                  const T* __restrict__ V, const T* __restrict__ dO,
                                                  const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                  T* __restrict__ dK, T* __restrict__ dV, int S, int Sk, int H, int Hk,
@@ -443,7 +464,7 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   const int h = lane >> 5, lr = lane & 31;
   const int bh = blockIdx.y;
   const int head = bh % H, b = bh / H, hk = head / (H / Hk);
-  const int k0 = blockIdx.x * 256, wk0 = k0 + wid * 32, key = wk0 + lr;
+  const int k0 = blockIdx.x * (NW * 32), wk0 = k0 + wid * 32, key = wk0 + lr;
   const T* Qb = Q + (long)b * S * fs.q_tok + (long)head * fs.q_head;
   const T* dOb = dO + (long)b * S * fs.o_tok + (long)head * fs.o_head;
   const T* Kb = K + (long)b * Sk * fs.kv_tok + (long)hk * fs.kv_head;
@@ -476,21 +497,24 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
   float rcv = 0.f;
   unsigned rseed = 0;
   uint4 mreg = {0u, 0u, 0u, 0u};
+  // keep words: NW words x 64 rows per tile, one b128 (4 consecutive rows of one word) per thread
+  constexpr int MT0 = NW == 8 ? 256 : 128;
+  const long msp = (S + 63) & ~63;
+  const unsigned* mbase = DR == 2 ? ex.dmask + ((long)bh * ex.dmask_w + (k0 >> 5)) * msp : nullptr;
   auto load_tile = [&](int qt, int buf) {   // 16 pieces (Q 0-7, dO 8-15) + the row constants
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int gidx = wid * 2 + u, which = gidx >> 3;
+    for (int u = 0; u < 16 / NW; ++u) {
+      const int gidx = wid * (16 / NW) + u, which = gidx >> 3;
       if (which) dma64(dOb, fs.o_tok, qt, S - 1, gidx & 7, lane, lds0 + buf * BUF + IMG64);
       else dma64(Qb, fs.q_tok, qt, S - 1, gidx & 7, lane, lds0 + buf * BUF);
     }
     if (tid < 128) rcv = (tid < 64 ? lse_b : del_b)[min(qt + (tid & 63), S - 1)];
     if constexpr (DR == 1) {
       if (tid >= 128 && tid < 192) rseed = fa_row(dstream, qt + (tid & 63));
-    } else if constexpr (DR == 2) {   // the 8 keep words of the workgroup's 256 keys, 4 per thread
-      if (tid >= 256 && tid < 384) {
-        const int i = tid - 256;
-        mreg = *reinterpret_cast<const uint4*>(ex.dmask + ((long)bh * S + min(qt + (i >> 1), S - 1)) * ex.dmask_w +
-                                               (k0 >> 5) + 4 * (i & 1));
+    } else if constexpr (DR == 2) {   // rows past S (pitch padding) are masked out by the -inf row limit
+      if (tid >= MT0 && tid < MT0 + 16 * NW) {
+        const int i = tid - MT0;
+        mreg = *reinterpret_cast<const uint4*>(mbase + (i >> 4) * msp + qt + 4 * (i & 15));
       }
     }
   };
@@ -499,14 +523,10 @@ __global__ __launch_bounds__(512) void fa64_dkdv(const T* __restrict__ Q, const 
     if (tid < 128) rc[tid] = tid < 64 ? rcv * nis : -rcv;
     if constexpr (DR == 1) {
       if (tid >= 128 && tid < 192) reinterpret_cast<unsigned*>(rc)[tid] = rseed;
-    } else if constexpr (DR == 2) {   // transposed to [word][row]: a lane's 4 consecutive rows are one b128
-      if (tid >= 256 && tid < 384) {
-        const int i = tid - 256;
-        unsigned* mk = reinterpret_cast<unsigned*>(rc) + 192 + 4 * (i & 1) * 64 + (i >> 1);
-        mk[0] = mreg.x;
-        mk[64] = mreg.y;
-        mk[128] = mreg.z;
-        mk[192] = mreg.w;
+    } else if constexpr (DR == 2) {   // [word][row] in LDS, as in global memory: a lane's 4 rows are one b128
+      if (tid >= MT0 && tid < MT0 + 16 * NW) {
+        const int i = tid - MT0;
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned*>(rc) + 192 + 64 * (i >> 4) + 4 * (i & 15)) = mreg;
       }
     }
   };
@@ -659,8 +679,15 @@ void launch64b(bool bwd, const void* q, const void* k, const void* v, void* o, f
                        S, Sk, H, Hk, scale * kLog2e, fs, ex);
     return;
   }
-  hipLaunchKernelGGL((fa64_dkdv<T, C, DR, BI>), gk, blk, 0, st, (const T*)q, (const T*)k, (const T*)v,
-                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
+  // dK/dV workgroup size (PHA_FA64_DKDV_WAVES = 4: 128 keys per workgroup, two workgroups per CU
+  // with independent barriers; 8: 256 keys, one per CU)
+  const int nwk = getenv("PHA_FA64_DKDV_WAVES") && atoi(getenv("PHA_FA64_DKDV_WAVES")) == 4 ? 4 : 8;
+  if (nwk == 4)
+    hipLaunchKernelGGL((fa64_dkdv<T, C, DR, BI, 4>), dim3((Sk + 127) / 128, B * H), dim3(256), 0, st, (const T*)q,
+                       (const T*)k, (const T*)v, (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
+  else
+    hipLaunchKernelGGL((fa64_dkdv<T, C, DR, BI>), gk, blk, 0, st, (const T*)q, (const T*)k, (const T*)v,
+                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, S, Sk, H, Hk, scale, fs, ex);
   hipLaunchKernelGGL((fa64_dq<T, C, DR, BI>), gq, blk, 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout,
                      lse, delta, (T*)dq, S, Sk, H, Hk, scale, fs, ex);
 }
@@ -722,8 +749,12 @@ FaStrides strides64(long q_tok, int q_head, long kv_tok, int kv_head, long o_tok
 }  // namespace
 
 // keep-mask words per query row (keys rounded up to the dK/dV workgroup's 256): the forward's
-// dmask is [B * H * S * words] uint32
+// dmask is [B * H][words][S rounded up to 64] uint32 (word-major, so the forward's stores and the
+// backward's loads run along the queries)
 PHA_API int pha_fa64_mask_words(int Sk) { return 8 * ((Sk + 255) / 256); }
+PHA_API long pha_fa64_mask_size(int B, int H, int S, int Sk) {
+  return (long)B * H * pha_fa64_mask_words(Sk) * ((S + 63) & ~63);
+}
 
 // Head dim 64 forward: q [B, S, H, 64] / k, v [B, Sk, Hk, 64] with element strides (token, head)
 // q_tok / q_head, kv_tok / kv_head (a packed [B, S, H, 3 * 64] projection is read in place), o with

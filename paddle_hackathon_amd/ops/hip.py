@@ -721,6 +721,8 @@ def _fa64_sig(L):
                                    LG, I, F, U, P, P, P, P, LG, LG, LG]
         L.pha_fa64_mask_words.argtypes = [I]
         L.pha_fa64_mask_words.restype = c_int
+        L.pha_fa64_mask_size.argtypes = [I, I, I, I]
+        L.pha_fa64_mask_size.restype = c_long
         L.pha_fa64_bwd.restype = c_int
         L._fa64_sig = True
     return L
@@ -729,13 +731,13 @@ def _fa64_sig(L):
 def _fa64_fwd(dt, qp, kp, vp, o, lse, B, S, Sk, H, Hk, sc, causal, qs, kvs, os_, dropout_p, seed, seed_dev, st,
               bias=None, bst=(0, 0, 0)):
     """qs / kvs / os_: (token, head) element strides of q, k / v and o. With dropout, returns the keep
-    mask as bits (int32 [B * H * S * words]) for the backward — the reference fused attention keeps
+    mask as bits (int32 [B * H][words][S up to 64]) for the backward — the reference fused attention keeps
     its dropout mask too (fmha_ref.h dropout_mask_out); PHA_FA64_MASKBITS=0 re-hashes instead"""
     import os
     L = _fa64_sig(_L())
     dmask = None
     if dropout_p and os.environ.get("PHA_FA64_MASKBITS", "1") != "0":
-        dmask = torch.empty(B * H * S * L.pha_fa64_mask_words(Sk), dtype=torch.int32, device=o.device)
+        dmask = torch.empty(L.pha_fa64_mask_size(B, H, S, Sk), dtype=torch.int32, device=o.device)
     _check(L.pha_fa64_fwd(dt, qp, kp, vp, _ptr(o), _ptr(lse), B, S, Sk, H, Hk, sc, int(causal), qs[0], qs[1], kvs[0],
                           kvs[1], os_[0], os_[1], float(dropout_p), seed, _ptr(seed_dev), st, _ptr(dmask),
                           _ptr(bias), bst[0], bst[1], bst[2]),

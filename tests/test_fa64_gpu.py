@@ -201,3 +201,24 @@ def test_fa64_additive_masks_match_fp32(kind, causal):
     for a, b in zip(g1, g2):
         assert _rel(a, b) < 3e-2
     assert hip._fa64_on(64, mask, S)
+
+
+@pytest.mark.parametrize("waves", ["4", "8"])
+@pytest.mark.parametrize("causal,rate", [(False, 0.1), (True, 0.0), (False, 0.0)])
+def test_fa64_dkdv_workgroup_sizes_agree(waves, causal, rate, monkeypatch):
+    """the dK/dV kernel at 4 waves (128 keys per workgroup) and 8 waves (256 keys) computes the same
+    gradients (same per-key accumulation order: bitwise), ragged key count, stored keep bits"""
+    from paddle_hackathon_amd.ops import hip
+    torch.manual_seed(6)
+    B, S, H = 2, 456, 3
+    qkv = torch.randn(B, S, H, 192, device="cuda").bfloat16()
+    do = torch.randn(B, S, H, 64, device="cuda").bfloat16()
+    res = []
+    for w in (waves, "8"):
+        monkeypatch.setenv("PHA_FA64_DKDV_WAVES", w)
+        a = qkv.clone().requires_grad_()
+        torch.manual_seed(31)
+        o = hip.flash_attention_packed_ext(a, causal, None, None, rate)
+        (g,) = torch.autograd.grad(o, a, do)
+        res.append(g)
+    assert torch.equal(res[0], res[1])
