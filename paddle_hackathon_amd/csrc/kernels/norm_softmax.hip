@@ -9,6 +9,9 @@
 //
 // Reference behaviour: paddle/phi/kernels/gpu/layer_norm_kernel.cu,
 // layer_norm_grad_kernel.cu, softmax_kernel.cu / gpudnn/softmax_gpudnn.h.
+#include <stdlib.h>
+#include <type_traits>
+
 #include "common.h"
 
 using namespace pha;
@@ -20,17 +23,26 @@ constexpr int kWaves = 4;
 // counter-based dropout mask of the fused bias-dropout-residual-LN (fused_bias_dropout_residual_
 // layer_norm): element idx = row * H + col keeps iff a 16-bit hash of (seed, idx) >= thresh, so the
 // backward regenerates exactly the forward's mask and no mask tensor is stored.
-__device__ __forceinline__ unsigned bd_mix(unsigned x) {
-  x ^= x >> 16;
-  x *= 0x7feb352dU;
-  x ^= x >> 15;
-  x *= 0x846ca68bU;
-  x ^= x >> 16;
-  return x;
-}
-__device__ __forceinline__ bool bd_keep(unsigned seed, long idx, unsigned thresh) {
-  const unsigned h = bd_mix(seed ^ bd_mix((unsigned)idx ^ ((unsigned)(idx >> 32) * 0x9e3779b1U)));
-  return (h & 0xffffU) >= thresh;
+// keep bits (bit i: element idx0 + i) of the 8 elements idx0 .. idx0 + 7 (idx0 % 8 == 0) that one
+// lane's 16-B vector covers: ONE murmur finalizer per element pair, the low / high 16 bits are the
+// even / odd element's draw. Two 32-bit multiplies per pair instead of four per element (a
+// wave64 v_mul_lo_u32 is 16 cycles: the per-element double hash made the BDRLN passes VALU-bound)
+__device__ __forceinline__ unsigned bd_keep8(unsigned seed, long idx0, unsigned thresh) {
+  const unsigned s = seed ^ ((unsigned)(idx0 >> 33) * 0x85ebca6bU);
+  const unsigned p0 = (unsigned)(idx0 >> 1) * 0x9e3779b1U;
+  unsigned bits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned x = s ^ (p0 + (unsigned)j * 0x9e3779b1U);
+    x ^= x >> 16;
+    x *= 0x85ebca6bU;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35U;
+    x ^= x >> 16;
+    bits |= ((x & 0xffffU) >= thresh ? 1u : 0u) << (2 * j);
+    bits |= ((x >> 16) >= thresh ? 1u : 0u) << (2 * j + 1);
+  }
+  return bits;
 }
 
 struct BdArgs {            // x -> dropout(x + xb) before the residual add (thresh 0: no dropout)
@@ -71,10 +83,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
             if (bd.xb_f32) Vec8<float>::ld((const float*)bd.xb + col, bv);
             else Vec8<T>::ld((const T*)bd.xb + col, bv);
           }
+          const unsigned kb = bd.thresh ? bd_keep8(bd_seed(bd), (long)row * H + col, bd.thresh) : 0xffu;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             float z = round_to<T>(v[c][i] + (bd.xb ? bv[i] : 0.f));
-            if (bd.thresh) z = bd_keep(bd_seed(bd), (long)row * H + col + i, bd.thresh) ? round_to<T>(z * bd.kscale) : 0.f;
+            if (bd.thresh) z = ((kb >> i) & 1u) ? round_to<T>(z * bd.kscale) : 0.f;
             v[c][i] = z;
           }
         }
@@ -141,15 +154,29 @@ struct Raw8<float> {
 // XS: also per-block partial column sums of the final dx (part_x) — the bias gradient of a linear
 // layer whose output entered the residual sum (its bias folded into the add-LN forward), so that
 // layer's backward needs no separate column-sum pass over the same gradient
-template <typename T, typename W, int NCH, int BW, bool XS = false>
+// DRP: the fused bias-dropout-residual-LN backward in one pass — besides dx (= d residual) it writes
+// dxd = dropout'(dx): the regenerated keep mask (bd_keep) times kscale on dx rounded to T, exactly
+// what dropout_bias_bwd_kernel computes from the stored dx, without re-reading it
+template <typename T, typename W, int NCH, int BW, bool XS = false, bool DRP = false>
 __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 3 ? 4 : NCH <= 4 ? 2 : 1))) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const W* __restrict__ w, const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, T* __restrict__ dx,
                                                          float* __restrict__ part_w, float* __restrict__ part_b,
                                                          int rows, int H, const T* __restrict__ dres,
-                                                         float* __restrict__ part_x = nullptr) {
+                                                         float* __restrict__ part_x = nullptr,
+                                                         T* __restrict__ dxd = nullptr,
+                                                         BdArgs bd = BdArgs{nullptr, 0u, 0u, 1.f, 0}) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  const unsigned dseed = DRP ? bd_seed(bd) : 0u;
+  // dropout' of the finished dx of (row, col .. col + 7)
+  auto drop_store = [&](int row, int col, const float (&o)[8]) {
+    float g[8];
+    const unsigned kb = bd_keep8(dseed, (long)row * H + col, bd.thresh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = ((kb >> i) & 1u) ? round_to<T>(o[i]) * bd.kscale : 0.f;
+    Vec8<T>::st(dxd + (long)row * H + col, g);
+  };
   float aw[NCH][8], ab[NCH][8], ax[XS ? NCH : 1][8];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -225,6 +252,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
 #pragma unroll
           for (int i = 0; i < 8; ++i) ax[c][i] += round_to<T>(o[i]);   // the stored gradient's sum
         }
+        if constexpr (DRP) drop_store(row, col, o);
         Vec8<T>::st(dr + col, o);
       }
     }
@@ -280,6 +308,7 @@ __global__ __launch_bounds__(BW * 64) __attribute__((amdgpu_waves_per_eu(NCH <= 
 #pragma unroll
           for (int i = 0; i < 8; ++i) ax[c][i] += round_to<T>(o[i]);   // the stored gradient's sum
         }
+        if constexpr (DRP) drop_store(row, col, o);
         Vec8<T>::st(dr + col, o);
       }
     }
@@ -361,21 +390,37 @@ __global__ __launch_bounds__(BW * 64) void dropout_bias_bwd_kernel(const T* __re
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[c][i] = 0.f;
-  for (int row = blockIdx.x * BW + wid; row < rows; row += gridDim.x * BW) {
+  // rows strided over the grid, the next row's loads issued before this row's hash / store work
+  // (one HBM round trip per row in flight behind the VALU instead of a stall per row)
+  const int stride = gridDim.x * BW;
+  int row = blockIdx.x * BW + wid;
+  Raw8<T> cur[NCH];
+  auto load = [&](int r, Raw8<T>(&dst)[NCH]) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if (c * 512 + lane * 8 < H) dst[c].ld(dh + (long)r * H + c * 512 + lane * 8);
+  };
+  if (row < rows) load(row, cur);
+  for (; row < rows; row += stride) {
+    Raw8<T> nxt[NCH];
+    if (row + stride < rows) load(row + stride, nxt);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 512 + lane * 8;
       if (col < H) {
         float g[8];
-        Vec8<T>::ld(dh + (long)row * H + col, g);
+        cur[c].unpack(g);
+        const unsigned kb = thresh ? bd_keep8(seed, (long)row * H + col, thresh) : 0xffu;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          g[i] = (!thresh || bd_keep(seed, (long)row * H + col + i, thresh)) ? g[i] * kscale : 0.f;
+          g[i] = ((kb >> i) & 1u) ? g[i] * kscale : 0.f;
           acc[c][i] += round_to<T>(g[i]);
         }
         Vec8<T>::st(dx + (long)row * H + col, g);
       }
     }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) cur[c] = nxt[c];
   }
   __shared__ float red[BW][512];
 #pragma unroll
@@ -577,16 +622,90 @@ PHA_API int pha_layer_norm_fwd(int dt, int wdt, const void* x, const void* w, co
   return pha_layer_norm_fwd2(dt, wdt, x, nullptr, nullptr, w, b, y, mean, rstd, rows, H, eps, stream);
 }
 
-// column sums of the [P, H] partials into out: P > 4 * kColSplit rows go through the chip-wide first
-// stage into rows [P, P + kColSplit) of the same workspace
+// single-launch column sums of up to three [P, H] fp32 partial arrays (blockIdx.y picks the array):
+// 16 waves per 64-column stripe split the P rows, so each wave has at most P / 16 independent
+// loads in flight (one HBM / L2 round trip or two at P = 256) and a backward's weight, bias and
+// residual-bias gradients finish in ONE short launch instead of two per array (each tiny launch
+// costs ~4.5 us of the BERT-base step, 17 of them per layer)
+struct ColSumJob {
+  const float* part[3];
+  void* out[3];
+  int f32[3];   // output fp32 (else the activation type T)
+};
+constexpr int kColSum1MaxP = 1024;
+// PHA_COLSUM1=0: the two-launch-per-array path (A/B switch), read once
+inline bool colsum1_on() {
+  static const bool on = [] {
+    const char* e = getenv("PHA_COLSUM1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+template <typename T>
+__global__ __launch_bounds__(1024) void col_sum_n_kernel(ColSumJob job, int P, int H) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = blockIdx.y;
+  const float* part = j == 0 ? job.part[0] : j == 1 ? job.part[1] : job.part[2];
+  const int col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < H)
+#pragma unroll 8
+    for (int p = w; p < P; p += 16) s += part[(long)p * H + col];
+  __shared__ float red[16][64];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && col < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][lane];
+    void* out = j == 0 ? job.out[0] : j == 1 ? job.out[1] : job.out[2];
+    const int f32 = j == 0 ? job.f32[0] : j == 1 ? job.f32[1] : job.f32[2];
+    if (f32) static_cast<float*>(out)[col] = t;
+    else Cvt<T>::st(static_cast<T*>(out), col, t);
+  }
+}
+template <typename T>
+void col_sum_n(const ColSumJob& job, int n, int P, int H, hipStream_t stream) {
+  hipLaunchKernelGGL((col_sum_n_kernel<T>), dim3((H + 63) / 64, n), dim3(1024), 0, stream, job, P, H);
+}
+
+// column sums of the [P, H] partials into out: P <= kColSum1MaxP in one launch; larger P through
+// the chip-wide first stage into rows [P, P + kColSplit) of the same workspace
 template <typename W>
 void col_sum(float* part, W* out, int P, int H, hipStream_t stream) {
-  if (P > 4 * kColSplit) {
+  if (P <= kColSum1MaxP && colsum1_on()) {
+    ColSumJob job{{part, nullptr, nullptr}, {out, nullptr, nullptr}, {std::is_same<W, float>::value ? 1 : 0, 0, 0}};
+    col_sum_n<W>(job, 1, P, H, stream);
+  } else if (P > 4 * kColSplit) {
     float* stage = part + (long)P * H;
     hipLaunchKernelGGL(col_partial_kernel, dim3((H + 63) / 64, kColSplit), dim3(256), 0, stream, part, stage, P, H);
     hipLaunchKernelGGL((col_reduce_kernel<W>), dim3((H + 63) / 64), dim3(256), 0, stream, stage, out, kColSplit, H);
   } else {
     hipLaunchKernelGGL((col_reduce_kernel<W>), dim3((H + 63) / 64), dim3(256), 0, stream, part, out, P, H);
+  }
+}
+
+// the LN backward's dw (+ db, + dxs) column sums: one launch for all of them while P is small.
+// wf32 / xf32: dw, db / dxs are fp32 (else T)
+template <typename T>
+void col_sum_wbx(float* pw, void* dw, float* pb, void* db, float* px, void* dxs, bool wf32, bool xf32, int P, int H,
+                 hipStream_t stream) {
+  if (P <= kColSum1MaxP && colsum1_on()) {
+    ColSumJob job{{pw, nullptr, nullptr}, {dw, nullptr, nullptr}, {wf32, 0, 0}};
+    int n = 1;
+    if (db) { job.part[n] = pb; job.out[n] = db; job.f32[n] = wf32; ++n; }
+    if (dxs) { job.part[n] = px; job.out[n] = dxs; job.f32[n] = xf32; ++n; }
+    col_sum_n<T>(job, n, P, H, stream);
+    return;
+  }
+  if (wf32) col_sum<float>(pw, (float*)dw, P, H, stream);
+  else col_sum<T>(pw, (T*)dw, P, H, stream);
+  if (db) {
+    if (wf32) col_sum<float>(pb, (float*)db, P, H, stream);
+    else col_sum<T>(pb, (T*)db, P, H, stream);
+  }
+  if (dxs) {
+    if (xf32) col_sum<float>(px, (float*)dxs, P, H, stream);
+    else col_sum<T>(px, (T*)dxs, P, H, stream);
   }
 }
 
@@ -618,8 +737,7 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
                            (const T*)dres);
       });
       if (rc) return rc;
-      col_sum<float>(part_w, (float*)dw, nblocks, H, stream);
-      if (db) col_sum<float>(part_b, (float*)db, nblocks, H, stream);
+      col_sum_wbx<T>(part_w, dw, part_b, db, nullptr, nullptr, true, true, nblocks, H, stream);
     } else {
       rc = dispatch_nch_small(H, [&](auto nch) {
         hipLaunchKernelGGL((ln_bwd_kernel<T, T, decltype(nch)::value, bwd_waves(decltype(nch)::value)>), grid, dim3(bwd_waves(decltype(nch)::value) * 64), 0, stream,
@@ -627,8 +745,42 @@ PHA_API int pha_layer_norm_bwd2(int dt, int wdt, const void* dy, const void* x, 
                            (const T*)dres);
       });
       if (rc) return rc;
-      col_sum<T>(part_w, (T*)dw, nblocks, H, stream);
-      if (db) col_sum<T>(part_b, (T*)db, nblocks, H, stream);
+      col_sum_wbx<T>(part_w, dw, part_b, db, nullptr, nullptr, false, false, nblocks, H, stream);
+    }
+  });
+  return rc ? rc : (int)hipGetLastError();
+}
+
+// fused_bias_dropout_residual_layer_norm backward without the input bias: dx = LN'(dy) (the
+// residual's gradient) and dxd = dropout'(dx) with the forward's mask (seed / thresh / kscale / seedp
+// as pha_bdrln_fwd2) in one pass; dw / db as pha_layer_norm_bwd2
+PHA_API int pha_layer_norm_dropout_bwd(int dt, int wdt, const void* dy, const void* x, const void* w,
+                                       const float* mean, const float* rstd, void* dx, void* dxd, void* dw, void* db,
+                                       float* part_w, float* part_b, int nblocks, int rows, int H, unsigned seed,
+                                       unsigned thresh, float kscale, hipStream_t stream, const unsigned* seedp) {
+  if (H % 8 || rows <= 0 || nblocks <= 0 || !dxd || thresh == 0) return (int)hipErrorInvalidValue;
+  const dim3 grid(nblocks);
+  const BdArgs bd{nullptr, seed, thresh, kscale, 0, seedp};
+  int rc = 0;
+  PHA_DISPATCH_T(dt, T, {
+    if (wdt == kF32) {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        constexpr int nc = decltype(nch)::value;
+        hipLaunchKernelGGL((ln_bwd_kernel<T, float, nc, bwd_waves(nc), false, true>), grid, dim3(bwd_waves(nc) * 64),
+                           0, stream, (const T*)dy, (const T*)x, (const float*)w, mean, rstd, (T*)dx, part_w, part_b,
+                           rows, H, (const T*)nullptr, (float*)nullptr, (T*)dxd, bd);
+      });
+      if (rc) return rc;
+      col_sum_wbx<T>(part_w, dw, part_b, db, nullptr, nullptr, true, true, nblocks, H, stream);
+    } else {
+      rc = dispatch_nch_small(H, [&](auto nch) {
+        constexpr int nc = decltype(nch)::value;
+        hipLaunchKernelGGL((ln_bwd_kernel<T, T, nc, bwd_waves(nc), false, true>), grid, dim3(bwd_waves(nc) * 64), 0,
+                           stream, (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, part_w, part_b, rows,
+                           H, (const T*)nullptr, (float*)nullptr, (T*)dxd, bd);
+      });
+      if (rc) return rc;
+      col_sum_wbx<T>(part_w, dw, part_b, db, nullptr, nullptr, false, false, nblocks, H, stream);
     }
   });
   return rc ? rc : (int)hipGetLastError();
@@ -654,10 +806,7 @@ PHA_API int pha_layer_norm_bwd3(int dt, int wdt, int xsdt, const void* dy, const
                            (const T*)dres, part_x);
       });
       if (rc) return rc;
-      col_sum<float>(part_w, (float*)dw, nblocks, H, stream);
-      if (db) col_sum<float>(part_b, (float*)db, nblocks, H, stream);
-      if (xsdt == kF32) col_sum<float>(part_x, (float*)dxs, nblocks, H, stream);
-      else col_sum<T>(part_x, (T*)dxs, nblocks, H, stream);
+      col_sum_wbx<T>(part_w, dw, part_b, db, part_x, dxs, true, xsdt == kF32, nblocks, H, stream);
     } else {
       rc = dispatch_nch_small(H, [&](auto nch) {
         constexpr int N = decltype(nch)::value;
@@ -666,10 +815,7 @@ PHA_API int pha_layer_norm_bwd3(int dt, int wdt, int xsdt, const void* dy, const
                            (const T*)dres, part_x);
       });
       if (rc) return rc;
-      col_sum<T>(part_w, (T*)dw, nblocks, H, stream);
-      if (db) col_sum<T>(part_b, (T*)db, nblocks, H, stream);
-      if (xsdt == kF32) col_sum<float>(part_x, (float*)dxs, nblocks, H, stream);
-      else col_sum<T>(part_x, (T*)dxs, nblocks, H, stream);
+      col_sum_wbx<T>(part_w, dw, part_b, db, part_x, dxs, false, xsdt == kF32, nblocks, H, stream);
     }
   });
   return rc ? rc : (int)hipGetLastError();

@@ -14,6 +14,7 @@ Reference parity (what each op replaces in the reference):
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as TF
@@ -175,6 +176,10 @@ def rms_norm(x, weight, eps=1e-6):
     return y * weight if weight is not None else y
 
 
+# PHA_LN_DROP_FUSED=0: LN backward and the dropout backward as two passes (A/B switch)
+_LN_DROP_FUSED = os.environ.get("PHA_LN_DROP_FUSED", "1") != "0"
+
+
 class _BiasDropoutResidualLN(torch.autograd.Function):
     """y = LN(residual + dropout(x + bias)) in one HIP pass (hs stored for the backward); the dropout
     mask is a counter hash of (seed, element) regenerated in the backward, never stored.
@@ -196,6 +201,10 @@ class _BiasDropoutResidualLN(torch.autograd.Function):
     def backward(ctx, gy):
         hs, w, mean, rstd = ctx.saved_tensors
         seed, thresh, kscale, has_b, xb_dt = ctx.cfg
+        if thresh and xb_dt is None and _LN_DROP_FUSED:   # one pass: LN backward + dropout'
+            dh, dx, dw, db = _hip.layer_norm_dropout_bwd(gy.contiguous(), hs, w, mean, rstd, has_b, seed, thresh,
+                                                         kscale, ctx.seed_dev)
+            return dx, dh, None, dw, db, None, None
         dh, dw, db = _hip.layer_norm_bwd(gy.contiguous(), hs, w, mean, rstd, has_b)
         if thresh == 0 and xb_dt is None:
             dx, dxb = dh, None

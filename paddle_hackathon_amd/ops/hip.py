@@ -37,6 +37,7 @@ def _L():
             "pha_col_sum_rows": [I, P, P, I, I, P],
             "pha_bdrln_fwd": [I, I, P, P, P, P, P, P, P, P, P, I, I, F, c_uint, c_uint, F, P],
             "pha_dropout_bias_bwd": [I, I, P, P, P, P, I, I, I, c_uint, c_uint, F, P, P],
+            "pha_layer_norm_dropout_bwd": [I, I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, c_uint, c_uint, F, P, P],
             "pha_softmax_fwd": [I, P, P, I, I, P],
             "pha_softmax_bwd": [I, P, P, P, I, I, P],
             "pha_softmax_ce_fwd": [I, P, P, P, P, LG, I, I, P],
@@ -170,6 +171,25 @@ def bdrln_fwd(x, xbias, residual, w, b, eps, seed, thresh, kscale, seed_dev=None
                               _ptr(seed_dev)),
            "bdrln_fwd")
     return y, mean, rstd, hs
+
+
+def layer_norm_dropout_bwd(dy, x, w, mean, rstd, has_bias, seed, thresh, kscale, seed_dev=None):
+    """The bias-free fused_bias_dropout_residual_layer_norm backward in one pass: returns
+    (dh, dx, dw, db) with dh = LN'(dy) (the residual's gradient) and dx = dh * mask * kscale (the
+    forward's regenerated mask) — layer_norm_bwd + dropout_bias_bwd without re-reading dh."""
+    H = w.numel()
+    rows = x.numel() // H
+    nblocks = int(_L().pha_layer_norm_bwd_nblocks(rows, H))
+    dh, dx = torch.empty_like(x), torch.empty_like(x)
+    dw = torch.empty_like(w)
+    db = torch.empty_like(w) if has_bias else None
+    part = torch.empty((2, nblocks + 8, H), dtype=torch.float32, device=x.device)
+    _check(_L().pha_layer_norm_dropout_bwd(_DT[x.dtype], _DT[w.dtype], _ptr(dy), _ptr(x), _ptr(w), _ptr(mean),
+                                           _ptr(rstd), _ptr(dh), _ptr(dx), _ptr(dw), _ptr(db), _ptr(part[0]),
+                                           _ptr(part[1]), nblocks, rows, H, int(seed), int(thresh), float(kscale),
+                                           _stream(x), _ptr(seed_dev)),
+           "layer_norm_dropout_bwd")
+    return dh, dx, dw, db
 
 
 def dropout_bias_bwd(dh, seed, thresh, kscale, bias_dtype=None, seed_dev=None):

@@ -86,3 +86,52 @@ def test_graphed_bert_step_draws_new_masks_each_replay():
         assert len(set(round(v, 6) for v in losses[2:])) == 3, losses
     finally:
         paddle.set_device("cpu")
+
+
+@pytest.mark.parametrize("C,dtype,wdt", [(768, torch.bfloat16, torch.float32), (2048, torch.bfloat16, torch.float32),
+                                         (768, torch.float32, torch.float32), (1024, torch.float16, torch.float16)])
+def test_ln_dropout_fused_backward_equals_two_passes(C, dtype, wdt):
+    """the one-pass LN + dropout' backward (pha_layer_norm_dropout_bwd) is bitwise the LN backward
+    followed by dropout_bias_bwd on the stored residual gradient, incl. the device seed word"""
+    from paddle_hackathon_amd.ops import hip as H
+    g = torch.Generator(device="cuda").manual_seed(1)
+    rows = 1000
+    x = torch.randn(rows, C, device="cuda", generator=g).to(dtype)
+    r = torch.randn(rows, C, device="cuda", generator=g).to(dtype)
+    w = (torch.rand(C, device="cuda", generator=g) + 0.5).to(wdt)
+    b = (torch.randn(C, device="cuda", generator=g) * 0.1).to(wdt)
+    gy = torch.randn(rows, C, device="cuda", generator=g).to(dtype)
+    seed, thresh, ks = 777, int(0.1 * 65536), 1 / 0.9
+    dev = torch.tensor([0x1234567], dtype=torch.int32, device="cuda")
+    _, mean, rstd, hs = H.bdrln_fwd(x, None, r, w, b, 1e-5, seed, thresh, ks, dev)
+    dh0, dw0, db0 = H.layer_norm_bwd(gy, hs, w, mean, rstd, True)
+    dx0, _ = H.dropout_bias_bwd(dh0, seed, thresh, ks, None, dev)
+    dh1, dx1, dw1, db1 = H.layer_norm_dropout_bwd(gy, hs, w, mean, rstd, True, seed, thresh, ks, dev)
+    torch.cuda.synchronize()
+    assert torch.equal(dh0, dh1) and torch.equal(dx0, dx1)
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    keep = (dx1 != 0).float().mean().item()
+    assert 0.88 < keep < 0.92
+
+
+def test_bdrln_autograd_fused_backward_matches_unfused(monkeypatch):
+    """_BiasDropoutResidualLN backward with and without the one-pass kernel: same gradients"""
+    import paddle_hackathon_amd.ops.fused as FU
+    g = torch.Generator(device="cuda").manual_seed(2)
+    rows, C = 512, 768
+    x0 = torch.randn(rows, C, device="cuda", generator=g).bfloat16()
+    r0 = torch.randn(rows, C, device="cuda", generator=g).bfloat16()
+    w = torch.rand(C, device="cuda", generator=g) + 0.5
+    b = torch.randn(C, device="cuda", generator=g) * 0.1
+    gy = torch.randn(rows, C, device="cuda", generator=g).bfloat16()
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(FU, "_LN_DROP_FUSED", fused)
+        torch.manual_seed(5)   # same host dropout seed both times
+        x, r = x0.clone().requires_grad_(True), r0.clone().requires_grad_(True)
+        wl, bl = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        y = FU.bias_dropout_residual_layer_norm(x, r, None, wl, bl, 0.1, True, 1e-5)
+        y.backward(gy)
+        outs.append((y.detach(), x.grad, r.grad, wl.grad, bl.grad))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
