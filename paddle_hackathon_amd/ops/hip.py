@@ -144,6 +144,13 @@ def dropout_seed(device):
         buf = _SEED_BUFS[device] = torch.zeros(1, dtype=torch.int32, device=device)
     if not torch.cuda.is_current_stream_capturing():
         return seed, None
+    out = torch.empty(1, dtype=torch.int32, device=device)
+    L = _L()
+    if hasattr(L, "pha_seed_bump"):   # ++counter and the site's copy in one captured kernel
+        L.pha_seed_bump.argtypes = [c_void_p, c_void_p, c_void_p]
+        L.pha_seed_bump.restype = c_int
+        _check(L.pha_seed_bump(_ptr(buf), _ptr(out), _stream(buf)), "seed_bump")
+        return seed, out
     buf.add_(1)
     return seed, buf.clone()
 
