@@ -461,7 +461,25 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
     __syncthreads();
     const int c = tid * 4;
     if (c < dn) {
-      for (int k = 0; k < cnt; ++k) {
+      int k = 0;
+      // 8 gradient rows in flight per step (loads first, then the adds in list order: the same
+      // summation order as one row at a time — a serial load -> add chain cost ~1 HBM latency per row)
+      for (; k + 8 <= cnt; k += 8) {
+        float g[8][4];
+        int ee[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          ee[u] = list[k + u];
+          ld4<T>(gy + (long)(ee[u] >> 5) * D + d0 + c, g[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float* a = acc + (ee[u] & 31) * EB_DCH + c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[q] += g[u][q];
+        }
+      }
+      for (; k < cnt; ++k) {
         const int e = list[k];
         const long r = e >> 5;
         float g[4];
@@ -475,9 +493,11 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* __res
     cnt = 0;
   };
   const long t0 = (long)blockIdx.z * chunk, t1 = min(n, t0 + chunk);
+  long idn = t0 + tid < t1 ? ids[t0 + tid] : -1;   // the next 256 ids load during this batch's compaction
   for (long base = t0; base < t1; base += 256) {
     const long r = base + tid;
-    const long id = r < t1 ? ids[r] : -1;
+    const long id = idn;
+    idn = r + 256 < t1 ? ids[r + 256] : -1;
     const bool m = id >= v0 && id < v0 + EB_ROWS && id < V && id != pad;
     const unsigned long long bal = __ballot(m);
     const int pre = __popcll(bal & ((1ULL << lane) - 1ULL));
@@ -599,6 +619,75 @@ PHA_API int pha_col_sum_partial(int dt, const void* gy, float* part, int rows, i
   return (int)hipGetLastError();
 }
 
+// many weight transposes in ONE launch (the cached [out][in] copies of all linear weights an
+// optimizer step updated: 50 launches of ~5.5 us per BERT-base step before): block b takes global
+// tile b, its matrix found by a scan of the tile offsets (at most kTr16Batch, scalar loads)
+constexpr int kTr16Batch = 64;
+struct Tr16Batch {
+  const uint16_t* src[kTr16Batch];
+  uint16_t* dst[kTr16Batch];
+  int R[kTr16Batch], C[kTr16Batch];
+  int tile0[kTr16Batch + 1];   // first global tile of each matrix; tile0[n] = total
+  int n;
+};
+__global__ __launch_bounds__(256) void transpose16_batch_kernel(Tr16Batch bt) {
+  __shared__ uint16_t tile[64][66];
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < bt.n && bt.tile0[e + 1] <= b) ++e;
+  const int R = bt.R[e], C = bt.C[e];
+  const int t = b - bt.tile0[e], ct = (C + 63) / 64;
+  const int r0 = (t / ct) * 64, c0 = (t % ct) * 64;
+  const uint16_t* __restrict__ src = bt.src[e];
+  uint16_t* __restrict__ dst = bt.dst[e];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j;
+    const int rr = idx >> 3, cc = (idx & 7) * 8;
+    if (r0 + rr < R && c0 + cc < C) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src + (long)(r0 + rr) * C + c0 + cc);
+      const uint16_t* el = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tile[rr][cc + k] = el[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + 256 * j;
+    const int oc = idx >> 3, orr = (idx & 7) * 8;
+    if (c0 + oc < C && r0 + orr < R) {
+      uint4 v;
+      uint16_t* el = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) el[k] = tile[orr + k][oc];
+      *reinterpret_cast<uint4*>(dst + (long)(c0 + oc) * R + r0 + orr) = v;
+    }
+  }
+}
+
+// dst_i [C_i][R_i] = src_i [R_i][C_i]^T for n <= 64 matrices of 2-byte elements (R_i, C_i % 8 == 0)
+PHA_API int pha_transpose16_batch(int n, const void* const* src, void* const* dst, const int* R, const int* C,
+                                  hipStream_t stream) {
+  if (n <= 0 || n > kTr16Batch) return (int)hipErrorInvalidValue;
+  Tr16Batch bt{};
+  bt.n = n;
+  long tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    if (R[i] % 8 || C[i] % 8 || R[i] <= 0 || C[i] <= 0 || !src[i] || !dst[i]) return (int)hipErrorInvalidValue;
+    bt.src[i] = (const uint16_t*)src[i];
+    bt.dst[i] = (uint16_t*)dst[i];
+    bt.R[i] = R[i];
+    bt.C[i] = C[i];
+    bt.tile0[i] = (int)tiles;
+    tiles += (long)((R[i] + 63) / 64) * ((C[i] + 63) / 64);
+  }
+  if (tiles > 0x7fffffff) return (int)hipErrorInvalidValue;
+  bt.tile0[n] = (int)tiles;
+  hipLaunchKernelGGL(transpose16_batch_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, bt);
+  return (int)hipGetLastError();
+}
+
 // dst [C][R] = src [R][C]^T, 2-byte elements, R % 8 == C % 8 == 0
 PHA_API int pha_transpose16(const void* src, void* dst, int R, int C, hipStream_t stream) {
   if (R % 8 || C % 8 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
@@ -685,5 +774,24 @@ PHA_API int pha_embedding_bwd(int dt, const int64_t* ids, const void* gy, void* 
 PHA_API int pha_embedding_fwd(const int64_t* ids, const void* w, void* out, long rows, int row_bytes, long vocab, hipStream_t stream) {
   if (row_bytes % 16) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(embedding_fwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, ids, (const uint4*)w, (uint4*)out, rows, row_bytes / 16, vocab);
+  return (int)hipGetLastError();
+}
+
+// hipGraph-safe dropout seeds (ops/hip.dropout_seed): ++counter and a copy of the new value for one
+// dropout site in ONE launch (was an in-place add plus a clone: two tiny kernels per site and
+// replay, ~10 us of a BERT-base step each)
+namespace {
+__global__ void seed_bump_kernel(int* __restrict__ counter, int* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    const int v = counter[0] + 1;
+    counter[0] = v;
+    out[0] = v;
+  }
+}
+}  // namespace
+
+PHA_API int pha_seed_bump(int* counter, int* out, hipStream_t stream) {
+  if (!counter || !out) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(64), 0, stream, counter, out);
   return (int)hipGetLastError();
 }

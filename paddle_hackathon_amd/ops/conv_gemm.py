@@ -1220,8 +1220,65 @@ def matmul_kn(x, w):
 def weight_t(w):
     """[in, out] linear weight -> cached contiguous [out, in] copy (refreshed once per optimizer
     step via the parameter version): x @ W then runs as the NT-layout GEMM, which hipBLASLt runs
-    15-35 % faster than NN at the GPT shapes (tools/bench_gpt_gemms.py)."""
+    15-35 % faster than NN at the GPT shapes (tools/bench_gpt_gemms.py). The first stale copy met
+    after an optimizer step refreshes EVERY stale cached copy on that device in one batched
+    transpose launch, in place (pha_transpose16_batch; PHA_WT_BATCH=0: one launch per weight)."""
+    if _WT_BATCH and _tr16_ok(w) and hasattr(_L(), "pha_transpose16_batch"):
+        return _weight_t_batched(w)
     return _wlayout(w, "t", _transpose2d)
+
+
+_WT_BATCH = __import__("os").environ.get("PHA_WT_BATCH", "1") != "0"
+
+
+def _tr16_ok(t):
+    return (t.dim() == 2 and t.dtype in (torch.bfloat16, torch.float16) and t.shape[0] % 8 == 0
+            and t.shape[1] % 8 == 0 and t.is_contiguous() and t.is_cuda)
+
+
+def _weight_t_batched(w):
+    import weakref
+    key = (w.data_ptr(), tuple(w.shape), w.dtype, "t")
+    hit = _wlayouts.get(key)
+    if hit is not None and hit[0]() is w and hit[2] == w._version:
+        return hit[1]
+    todo = []   # (weight, cached [out][in] buffer, key): refreshed in place
+    for k, (ref, v, ver) in list(_wlayouts.items()):
+        if k[3] != "t":
+            continue
+        wi = ref()
+        if wi is None:
+            _wlayouts.pop(k, None)
+            continue
+        if (wi._version != ver and wi.device == w.device and _tr16_ok(wi) and k[0] == wi.data_ptr()
+                and tuple(v.shape) == (wi.shape[1], wi.shape[0])):
+            todo.append((wi, v, k))
+    if not any(k == key for _, _, k in todo):
+        _wlayouts.pop(key, None)
+        todo.append((w, torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device), key))
+    L = _L()
+    if not getattr(L, "_trb_sig", False):
+        L.pha_transpose16_batch.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        L.pha_transpose16_batch.restype = c_int
+        L._trb_sig = True
+    st = c_void_p(torch.cuda.current_stream(w.device).cuda_stream)
+    for i in range(0, len(todo), 64):
+        chunk = todo[i:i + 64]
+        n = len(chunk)
+        srcs = (c_void_p * n)(*[t.data_ptr() for t, _, _ in chunk])
+        dsts = (c_void_p * n)(*[v.data_ptr() for _, v, _ in chunk])
+        rs = (c_int * n)(*[t.shape[0] for t, _, _ in chunk])
+        cs = (c_int * n)(*[t.shape[1] for t, _, _ in chunk])
+        rc = L.pha_transpose16_batch(n, srcs, dsts, rs, cs, st)
+        if rc != 0:
+            raise RuntimeError(f"pha_transpose16_batch failed ({rc})")
+    res = next(v for _, v, k in todo if k == key)
+    if len(_wlayouts) + len(todo) > 4096:
+        _wlayouts.clear()
+        todo = [(w, res, key)]
+    for t, v, k in todo:
+        _wlayouts[k] = (weakref.ref(t), v, t._version)
+    return res
 
 
 def _transpose2d(t):
