@@ -400,10 +400,10 @@ __global__ __launch_bounds__(512) void fa64_dq(const T* __restrict__ Q, const T*
           const float p = fexp2(fmaf(s[kb][r], c2, nl));
           const float g = dp[kb][r];
           if constexpr (DR != 0) {   // keep multiplier as in the dK/dV kernel
-            unsigned bit;
-            if constexpr (DR == 2) bit = __builtin_amdgcn_ubfe(mw[kb], (unsigned)acc_row(r, h), 1u);
-            else bit = fa64_keep(drow, k0 + kb * 32 + acc_row(r, h), ex.thresh) ? 1u : 0u;
-            s[kb][r] = p * fmaf(g, __uint_as_float((0u - bit) & ksb), -del);
+            unsigned msk;   // all ones = keep (DR 2: one signed bitfield extract)
+            if constexpr (DR == 2) msk = (unsigned)__builtin_amdgcn_sbfe((int)mw[kb], (unsigned)acc_row(r, h), 1u);
+            else msk = fa64_keep(drow, k0 + kb * 32 + acc_row(r, h), ex.thresh) ? ~0u : 0u;
+            s[kb][r] = p * fmaf(g, __uint_as_float(msk & ksb), -del);
           } else {
             s[kb][r] = p * (g - del);
           }
@@ -617,10 +617,10 @@ __global__ __launch_bounds__(NW * 64) void fa64_dkdv(const T* __restrict__ Q, co
         if constexpr (DROP) {
           // the keep decision as a multiplier m = keep ? 1 / (1 - rate) : 0, built from the bit with an
           // AND on the scale's bits (no compare / select per element; both DR paths identical arithmetic)
-          unsigned bit;
-          if constexpr (DR == 2) bit = __builtin_amdgcn_ubfe(sd[r], (unsigned)lr, 1u);
-          else bit = ((lane & 1) ? (rnd[r] >> 16) : (rnd[r] & 0xffffu)) >= ex.thresh ? 1u : 0u;   // = fa64_keep
-          const float m = __uint_as_float((0u - bit) & ksb);
+          unsigned msk;   // all ones = keep (DR 2: one signed bitfield extract of the stored bit)
+          if constexpr (DR == 2) msk = (unsigned)__builtin_amdgcn_sbfe((int)sd[r], (unsigned)lr, 1u);
+          else msk = ((lane & 1) ? (rnd[r] >> 16) : (rnd[r] & 0xffffu)) >= ex.thresh ? ~0u : 0u;   // = fa64_keep
+          const float m = __uint_as_float(msk & ksb);
           sa[r] = p * m;
           da[r] = p * fmaf(da[r], m, dl[r]);
         } else {
